@@ -1,0 +1,431 @@
+"""Generate the golden fixtures in tests/golden/*.npz FROM THE REFERENCE ITSELF.
+
+Runs only in the build container (needs /root/reference); the committed .npz files
+are data (inputs + expected outputs). The reference is imported through
+ref_harness (stubs + device remap, nothing edited) and its torch RNG calls are
+replaced by draws from the keyed Philox stream (oracle/rng.py) so the oracle and
+the HIP kernels can consume identical randomness:
+  parallel_breakout.py torch.randint -> randbelow(env, STREAM_RESET, episode, kind)
+  mcts.py Dirichlet(...).sample()     -> injected noise rows (stored in fixture)
+  mcts.py torch.randint(len(best))    -> randbelow(env, STREAM_TIE, search_id, k)
+  train_torch.py Categorical.sample() -> inverse CDF of uniform(env, STREAM_SAMPLE, t, 0)
+
+Usage: python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+"""
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "muzero-breakout_amd"))
+
+import ref_harness  # noqa: E402
+
+ref_harness.install()
+import torch  # noqa: E402
+
+from oracle import rng as R  # noqa: E402
+from mzba.weights import init_state_dict  # noqa: E402
+
+SEED = 20251015
+torch.set_num_threads(8)
+
+
+class Proxy:
+    """Module proxy: attribute overrides, everything else forwarded to `base`."""
+
+    def __init__(self, base, **over):
+        self._base, self._over = base, over
+
+    def __getattr__(self, name):
+        if name in self._over:
+            return self._over[name]
+        return getattr(self._base, name)
+
+
+# --------------------------------------------------------------------------------------
+# env reset injection
+class ResetInjector:
+    def __init__(self, seed):
+        self.seed, self.episode, self.calls, self.batch = seed, 0, 0, None
+
+    def begin(self, batch):
+        self.calls, self.batch = 0, batch
+
+    def randint(self, *args, **kwargs):
+        if len(args) == 3:
+            low, high, size = args
+        elif len(args) == 2 and isinstance(args[1], tuple):
+            low, (high, size) = 0, args
+        else:
+            low, high, size = args[0], args[1], kwargs.get("size")
+        c = self.calls
+        self.calls += 1
+        if c < 3:
+            env = np.arange(self.batch)
+            kind = c
+        else:
+            env = np.array([c - 3])
+            kind = 3
+        v = low + R.randbelow(env, R.STREAM_RESET, self.episode, kind, self.seed, high - low)
+        return torch.from_numpy(v.astype(np.int64))
+
+
+def patched_env_class(inj):
+    import environment.parallel_breakout as pb
+
+    pb.torch = Proxy(torch, randint=inj.randint)
+    Base = pb.BreakoutEnvironment
+
+    class Env(Base):
+        def reset(self):
+            inj.begin(self.batch)
+            out = super().reset()
+            inj.episode += 1
+            return out
+
+    return Env
+
+
+def pack_state(s):
+    """(B,3,H,W) {0,1} f32 -> bit-packed uint8 (B,3,ceil(H*W/8))."""
+    a = np.asarray(s)
+    assert np.all((a == 0) | (a == 1))
+    B = a.shape[0]
+    return np.packbits(a.reshape(B, 3, -1).astype(np.uint8), axis=-1)
+
+
+# --------------------------------------------------------------------------------------
+def make_env(cfg):
+    out = {}
+    inj = ResetInjector(SEED)
+    Env = patched_env_class(inj)
+    for tag, (B, H, W, T) in {"16x20": (32, None, None, 261), "84x84": (8, 84, 84, 300)}.items():
+        e = Env({**cfg["environment"], "n_parallel": B})
+        if H:
+            e.height, e.width = H, W
+        inj.episode = 0
+        state, _ = e.reset()
+        done = torch.zeros(B, dtype=torch.bool)
+        states, rewards, dones, valids, dxs, dys, acts = [pack_state(state)], [], [], [], [], [], []
+        dxs.append(e.ball_dx.numpy().copy()); dys.append(e.ball_dy.numpy().copy())
+        for t in range(T):
+            a = R.randbelow(np.arange(B), 7, t, 0, SEED, 3)  # fixture-only action stream
+            act = torch.from_numpy(a)
+            state, r, done, v = e.step(state, act, done)
+            acts.append(a); states.append(pack_state(state)); rewards.append(r.numpy().copy())
+            dones.append(done.numpy().copy()); valids.append(v.numpy().copy())
+            dxs.append(e.ball_dx.numpy().copy()); dys.append(e.ball_dy.numpy().copy())
+        out[tag] = dict(B=B, H=H or 16, W=W or 20, actions=np.stack(acts), states=np.stack(states),
+                        rewards=np.stack(rewards), dones=np.stack(dones), valids=np.stack(valids),
+                        dx=np.stack(dxs), dy=np.stack(dys))
+    for tag, d in out.items():
+        np.savez_compressed(os.path.join(HERE, f"env_{tag}.npz"), seed=SEED, **d)
+        print("env", tag, {k: getattr(v, "shape", v) for k, v in d.items()},
+              "reward set", np.unique(d["rewards"]), "done frac", d["dones"][-1].mean())
+
+
+def make_env_fuzz(cfg):
+    """Random (one-ball) states incl. done envs and every dx/dy, one step each."""
+    from environment.parallel_breakout import BreakoutEnvironment
+    g = np.random.Generator(np.random.PCG64(SEED))
+    res = {}
+    for tag, (B, H, W) in {"16x20": (4096, 16, 20), "84x84": (512, 84, 84)}.items():
+        s = np.zeros((B, 3, H, W), np.float32)
+        # bricks: pairs-aligned most of the time, random bits sometimes, rows 0..H-3
+        rows = H - 2
+        pair = g.random((B, rows, W // 2)) < 0.5
+        s[:, 2, :rows, :] = np.repeat(pair, 2, axis=2)
+        rnd = g.random(B) < 0.25
+        s[rnd, 2, :rows, :] = (g.random((int(rnd.sum()), rows, W)) < 0.5)
+        empty = g.random(B) < 0.1
+        s[empty, 2] = 0
+        # paddle: contiguous 6 at a random column, sometimes absent, sometimes random bits
+        pc = g.integers(0, W - 6 + 1, B)
+        for b in range(B):
+            m = g.random()
+            if m < 0.8:
+                s[b, 0, H - 1, pc[b]:pc[b] + 6] = 1
+            elif m < 0.9:
+                s[b, 0, H - 1] = g.random(W) < 0.3
+        by = g.integers(0, H, B)
+        bx = g.integers(0, W, B)
+        # bias some balls to the interesting rows (0, 1, bricks, paddle row, edges)
+        sel = g.random(B)
+        by = np.where(sel < 0.15, 0, by)
+        by = np.where((sel >= 0.15) & (sel < 0.3), H - 1, by)
+        by = np.where((sel >= 0.3) & (sel < 0.45), g.integers(0, 4, B), by)
+        bx = np.where(g.random(B) < 0.2, g.choice([0, W - 1], B), bx)
+        s[np.arange(B), 1, by, bx] = 1
+        dx = g.choice([-1, 0, 1], B, p=[0.45, 0.1, 0.45]).astype(np.int64)
+        dy = g.choice([-1.0, 0.0, 1.0], B, p=[0.45, 0.1, 0.45]).astype(np.float32)
+        # near-win states: a single brick pair exactly where the ball moves next
+        win = np.nonzero(g.random(B) < 0.1)[0]
+        for b in win:
+            nx = bx[b] + dx[b]
+            if nx < 0 or nx >= W:
+                nx = bx[b] - dx[b]
+            ny = int(by[b] + dy[b])
+            if 0 <= ny < H - 2:
+                s[b, 2] = 0
+                s[b, 2, ny, nx - nx % 2: nx - nx % 2 + 2] = 1
+        done = g.random(B) < 0.15
+        action = g.integers(0, 3, B)
+        e = BreakoutEnvironment({**cfg["environment"], "n_parallel": B})
+        e.height, e.width = H, W
+        e.ball_dx = torch.from_numpy(dx.copy())
+        e.ball_dy = torch.from_numpy(dy.copy())
+        dm = torch.from_numpy(done.copy())
+        ns, r, d2, v = e.step(torch.from_numpy(s.copy()), torch.from_numpy(action), dm)
+        assert d2 is dm
+        res[tag] = dict(B=B, H=H, W=W, state=pack_state(s), dx=dx, dy=dy, done=done, action=action,
+                        next_state=pack_state(ns), reward=r.numpy(), next_done=d2.numpy(), valid=v.numpy(),
+                        next_dx=e.ball_dx.numpy(), next_dy=e.ball_dy.numpy())
+        np.savez_compressed(os.path.join(HERE, f"envfuzz_{tag}.npz"), **res[tag])
+        print("fuzz", tag, "rewards", np.unique(r.numpy(), return_counts=True))
+
+
+# --------------------------------------------------------------------------------------
+def small_model_cfg(cfg):
+    m = {**cfg["model"]}
+    m["latent_channels"] = [64, 64]
+    m["state_history_length"] = 4
+    m["representation_network"] = {"num_res_blocks": [1, 1, 1], "activation": "relu"}
+    m["dynamics_network"] = {"num_res_blocks": 2, "num_actions": 3, "activation": "relu"}
+    m["prediction_network"] = {"num_res_blocks": 2, "num_actions": 3, "activation": "relu"}
+    m["device"] = "cpu"
+    return m
+
+
+def load_agent(mcfg, seed):
+    from src.networks import MuZeroAgent
+    agent = MuZeroAgent(mcfg)
+    sd = init_state_dict(mcfg, seed)
+    agent.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    agent.eval_mode()
+    return agent
+
+
+def make_nets(cfg):
+    from utils import ScalarTransforms
+    g = np.random.Generator(np.random.PCG64(SEED + 1))
+    for tag, mcfg, B in (("full", {**cfg["model"], "device": "cpu"}, 3), ("small", small_model_cfg(cfg), 6)):
+        L = mcfg["state_history_length"]
+        agent = load_agent(mcfg, SEED)
+        st = ScalarTransforms(mcfg)
+        # realistic rep input: gray codes {0,.3,.6,1} frames + a/3 action planes
+        lut = np.array([0, 0.3, 0.6, 1.0], np.float32)
+        frames = lut[g.integers(0, 4, (B, L, 16, 20)) * (g.random((B, L, 16, 20)) < 0.3)]
+        acts = g.integers(0, 3, (B, L))
+        planes = np.broadcast_to((acts.astype(np.float32) / np.float32(3))[:, :, None, None], (B, L, 16, 20))
+        x = np.concatenate([frames, planes], axis=1).astype(np.float32)
+        act = g.integers(0, 3, B)
+        with torch.no_grad():
+            h = agent.create_hidden_state_root(torch.from_numpy(x))
+            raw = agent.rep_net(torch.from_numpy(x))
+            p0, v0 = agent.evaluate_state(h)
+            planes_a = torch.nn.functional.one_hot(torch.from_numpy(act), 3).float().view(B, 3, 1, 1).expand(-1, -1, 4, 5)
+            h1, r1 = agent.hidden_state_transition(h, planes_a)
+            p1, v1 = agent.evaluate_state(h1)
+            dv0 = st.inverted_softmax_expectation(v0)
+            dr1 = st.inverted_softmax_expectation(r1)
+            dv1 = st.inverted_softmax_expectation(v1)
+        np.savez_compressed(os.path.join(HERE, f"nets_{tag}.npz"), weight_seed=SEED, x=x, action=act,
+                            rep_raw=raw.numpy(), h=h.numpy(), p0=p0.numpy(), v0=v0.numpy(), h1=h1.numpy(),
+                            r1=r1.numpy(), p1=p1.numpy(), v1=v1.numpy(), dv0=dv0.numpy(), dr1=dr1.numpy(),
+                            dv1=dv1.numpy(), pi0=torch.softmax(p0, 1).numpy(), pi1=torch.softmax(p1, 1).numpy())
+        print("nets", tag, "h range", float(h.min()), float(h.max()), "v0", dv0.numpy()[:3])
+
+
+# --------------------------------------------------------------------------------------
+class SearchInjector:
+    """Patches src.mcts: Dirichlet -> noise rows, randint -> keyed tie-break stream,
+    and records decoded outputs in call order."""
+
+    def __init__(self, seed):
+        import src.mcts as mm
+        self.mm, self.seed = mm, seed
+        self.search_id = -1
+        self.cur_env = 0
+        self.calls = None
+        self.noise = None  # callable(search_id, B) -> (B,3)
+        self.dir_calls = 0
+        self.rec_softmax, self.rec_ise, self.rec_leaf = [], [], []
+        inj = self
+
+        class _Dir:
+            def __init__(self, conc):
+                pass
+
+            def sample(self):
+                b = inj.dir_calls
+                inj.dir_calls += 1
+                return torch.from_numpy(inj.cur_noise[b].astype(np.float32))
+
+        def randint(high, size, **kw):
+            env = inj.cur_env
+            k = inj.calls[env]
+            inj.calls[env] += 1
+            j = R.randbelow(env, R.STREAM_TIE, inj.search_id, k, inj.seed, high)
+            return torch.tensor([int(j)])
+
+        def softmax(x, dim):
+            out = torch.softmax(x, dim=dim)
+            inj.rec_softmax.append(out.detach().numpy().copy())
+            return out
+
+        mm.torch = Proxy(torch, randint=randint, softmax=softmax,
+                         distributions=Proxy(torch.distributions, Dirichlet=_Dir))
+        Base = mm.MCTSSearchVec
+
+        class Search(Base):
+            def search(self, hidden_state, action_mask, training_iteration):
+                B = hidden_state.shape[0]
+                inj.search_id += 1
+                inj.calls = [0] * B
+                inj.dir_calls = 0
+                inj.cur_noise = inj.noise(inj.search_id, B)
+                inj.rec_softmax, inj.rec_ise, inj.rec_leaf = [], [], []
+                ise = self.scalar_transforms.inverted_softmax_expectation
+
+                def rec_ise(x):
+                    out = ise(x)
+                    inj.rec_ise.append(out.detach().numpy().copy())
+                    return out
+
+                self.scalar_transforms.inverted_softmax_expectation = rec_ise
+                try:
+                    return super().search(hidden_state, action_mask, training_iteration)
+                finally:
+                    del self.scalar_transforms.inverted_softmax_expectation
+
+            def ucb_action(self, subtree, action_mask, idx):
+                inj.cur_env = idx
+                return super().ucb_action(subtree, action_mask, idx)
+
+            def _backup(self, trees, last_nodes, trajectories, *a, **k):
+                inj.rec_leaf.append((np.array([ln[1] for ln in last_nodes]),
+                                     np.array([len(t) + 1 for t in trajectories])))
+                return super()._backup(trees, last_nodes, trajectories, *a, **k)
+
+        self.Search = Search
+
+
+def dirichlet_noise(search_id, B):
+    g = np.random.Generator(np.random.PCG64([SEED, 99, search_id]))
+    return g.dirichlet([0.25, 0.25, 0.25], size=B).astype(np.float32)
+
+
+def make_mcts(cfg):
+    from utils import ScalarTransforms
+    g = np.random.Generator(np.random.PCG64(SEED + 2))
+    mcfg = small_model_cfg(cfg)
+    agent = load_agent(mcfg, SEED)
+    st = ScalarTransforms(mcfg)
+    inj = SearchInjector(SEED)
+    inj.noise = dirichlet_noise
+    for tag, (B, S) in {"b16_s50": (16, 50), "b4_s200": (4, 200)}.items():
+        c = {**cfg, "num_simulations": S}
+        search = inj.Search(c, agent, st)
+        x = g.random((B, 2 * mcfg["state_history_length"], 16, 20)).astype(np.float32)
+        with torch.no_grad():
+            h = agent.create_hidden_state_root(torch.from_numpy(x))
+            values, counts = search.search(h, torch.ones(B, 3), 0)
+        sm, ise = inj.rec_softmax, inj.rec_ise
+        assert len(sm) == S + 1 and len(ise) == 1 + 2 * S
+        d = dict(B=B, S=S, search_id=inj.search_id, seed=SEED, noise=inj.cur_noise,
+                 v_root=ise[0], pi_root=sm[0],
+                 r=np.stack(ise[1::2]), v=np.stack(ise[2::2]), pi=np.stack(sm[1:]),
+                 counts=counts.numpy(), values=values.numpy(),
+                 leaf_action=np.stack([a for a, _ in inj.rec_leaf]), depth=np.stack([d for _, d in inj.rec_leaf]),
+                 h=h.numpy())
+        np.savez_compressed(os.path.join(HERE, f"mcts_{tag}.npz"), **d)
+        print("mcts", tag, "counts[:4]", counts.numpy()[:4].tolist(), "max depth", d["depth"].max(),
+              "values[:4]", values.numpy()[:4])
+
+
+# --------------------------------------------------------------------------------------
+def make_acting(cfg):
+    """One reference `_acting_stage` episode (B=4, small nets) with injected RNG."""
+    import train_torch as tt
+    mcfg = small_model_cfg(cfg)
+    B = 4
+    c = {**cfg, "n_parallel": B, "model": mcfg, "num_episodes": 1,
+         "environment": {**cfg["environment"], "n_parallel": B}}
+    inj_reset = ResetInjector(SEED)
+    Env = patched_env_class(inj_reset)
+    sinj = SearchInjector(SEED)
+    sinj.noise = dirichlet_noise
+    ncat = [0]
+
+    class InjCategorical:
+        def __init__(self, probs):
+            self.p = probs.detach().numpy().astype(np.float32)
+
+        def sample(self):
+            k = ncat[0]
+            ncat[0] += 1
+            env, step = k % B, k // B
+            u = R.uniform(np.array([env]), R.STREAM_SAMPLE, step, 0, SEED)[0]
+            cdf, chosen, last = np.float32(0), -1, 0
+            for a in range(3):
+                if self.p[a] > 0:
+                    last = a
+                cdf = np.float32(cdf + self.p[a])
+                if chosen < 0 and u < cdf:
+                    chosen = a
+            return torch.tensor(chosen if chosen >= 0 else last)
+
+    tt.torch = Proxy(torch, distributions=Proxy(torch.distributions, Categorical=InjCategorical))
+    tt.get_class = lambda mod, name: {"MCTSSearchVec": sinj.Search, "BreakoutEnvironment": Env}.get(
+        name, getattr(__import__(mod, fromlist=[name]), name))
+    sys_ = tt.RLSystem(c)
+    sd = init_state_dict(mcfg, SEED)
+    sd_t = {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}
+    sys_.mu_zero_target.load_state_dict(sd_t)
+    sys_.mu_zero.load_state_dict(sd_t)
+    sys_.mu_zero_target.eval_mode()
+    state, _ = sys_.environment.reset()
+    sys_._pad_initial_state(sys_.convert_to_grayscale(state))
+    sys_._run_episode(state)
+    trajs = sys_.observation_trajectories
+    lens = [t.length for t in trajs]
+    L = mcfg["state_history_length"]
+    T = max(lens)
+    acts = np.full((B, T), -1, np.int64)
+    frames = np.zeros((B, T, 16, 20), np.float32)
+    rews = np.zeros((B, T), np.float32)
+    cnts = np.zeros((B, T, 3), np.int64)
+    vals = np.zeros((B, T), np.float32)
+    for b, t in enumerate(trajs):
+        n = t.length
+        acts[b, :n] = [int(a) for a in t.actions[L:]]
+        frames[b, :n] = np.stack([s.numpy().reshape(16, 20) for s in t.states[L - 1:]])
+        rews[b, :n] = [float(r) for r in t.rewards[L:]]
+        cnts[b, :n] = np.stack([v.numpy() for v in t.visit_counts[L:]])
+        vals[b, :n] = [float(v) for v in t.values[L:]]
+    np.savez_compressed(os.path.join(HERE, "acting_small_b4.npz"), seed=SEED, B=B, lengths=np.array(lens),
+                        actions=acts, frames=frames, rewards=rews, counts=cnts, values=vals,
+                        n_searches=sinj.search_id + 1,
+                        noise=np.stack([dirichlet_noise(i, B) for i in range(sinj.search_id + 1)]))
+    print("acting", "lengths", lens, "reward sums", [float(t.reward_sum) for t in trajs])
+
+
+if __name__ == "__main__":
+    cfg = ref_harness.load_config()
+    which = sys.argv[1:] or ["env", "fuzz", "nets", "mcts", "acting"]
+    if "env" in which:
+        make_env(cfg)
+    if "fuzz" in which:
+        make_env_fuzz(cfg)
+    if "nets" in which:
+        make_nets(cfg)
+    if "mcts" in which:
+        make_mcts(cfg)
+    if "acting" in which:
+        make_acting(cfg)
