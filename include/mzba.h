@@ -1,0 +1,137 @@
+/* mzba.h — C ABI of the MI355X (gfx950) MuZero-Breakout acting path (libmzba.so).
+ *
+ * Plain pointers (device memory unless noted) and sizes; `stream` is a hipStream_t
+ * (torch's current stream from Python). Every function returns 0 on success, a
+ * negative code for an invalid argument, or the positive hipError_t of a failed
+ * launch. Work is stream-ordered and never synchronises the host, so every call is
+ * HIP-graph capturable. Each entry point names the reference interface it replaces.
+ * Numerics and layouts: DESIGN.md.
+ */
+#ifndef MZBA_H
+#define MZBA_H
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- environment (environment/parallel_breakout.py) ---------------------------------- */
+
+/* BreakoutEnvironment.reset (parallel_breakout.py:107-139). state f32 (B,3,H,W), ball_dx i64[B],
+ * ball_dy f32[B]. Random draws from Philox(seed; env+env_offset, stream 0, episode, kind) or, when
+ * params != NULL, int32 params[4][B] = (paddle offset, ball col, ball row offset, dx). */
+int mzba_env_reset_planes(float* state, int64_t* ball_dx, float* ball_dy, int B, int H, int W, int paddle_width,
+                          int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
+                          hipStream_t stream);
+
+/* BreakoutEnvironment.step (parallel_breakout.py:158-254) + get_valid_actions (:141-155).
+ * done (u8[B], torch.bool storage) is updated in place. rewards4 (HOST) = {paddle_hit, brick_hit,
+ * game_lost, game_won}. *err |= 1 if an env does not hold exactly one ball (the reference raises). */
+int mzba_env_step_planes(const float* state, float* next_state, const int64_t* action, uint8_t* done,
+                         int64_t* ball_dx, float* ball_dy, float* reward, float* valid, int B, int H, int W,
+                         int paddle_width, const float* rewards4, int32_t* err, hipStream_t stream);
+
+/* RLSystem.convert_to_grayscale (train_torch.py:334-358): (B,3,H,W) -> (B,1,H,W) f32. */
+int mzba_grayscale_planes(const float* state, float* gray, int B, int H, int W, hipStream_t stream);
+
+/* Compact env for the fused acting loop: same rules as mzba_env_step_planes on SoA scalars
+ * (paddle col, ball x/y, dx, dy, done) + a brick bitmask (nw u64 words per env over the brick rows).
+ * Reset also does _pad_initial_state (train_torch.py:313-332): frame-history ring filled with
+ * g(s0) (L-1 frames of H*W u8 gray codes), action ring (L) zeroed, hist_len = 0. */
+int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
+                           uint64_t* bricks, int nw, uint8_t* cur_frame, uint8_t* hist_frames,
+                           uint8_t* hist_actions, int32_t* hist_len, int L, int B, int H, int W, int paddle_width,
+                           int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
+                           hipStream_t stream);
+
+/* One acting-loop env step (train_torch.py:201-209): step, render the u8 gray frame, push
+ * (action, frame) into the history ring when the env is recorded (not prev_done; at the first
+ * step prev_done aliases done, :179), and write the trajectory-sink row (rec_* may be NULL). */
+int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
+                          uint64_t* bricks, int nw, const int64_t* action, float* reward, float* valid,
+                          uint8_t* cur_frame, uint8_t* hist_frames, uint8_t* hist_actions, int32_t* hist_len, int L,
+                          uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
+                          int first_step, int B, int H, int W, int paddle_width, int brick_rows,
+                          const float* rewards4, hipStream_t stream);
+
+/* compact -> reference planes (B,3,H,W) f32. */
+int mzba_compact_to_planes(const int32_t* paddle, const int32_t* bx, const int32_t* by, const uint8_t* done,
+                           const uint64_t* bricks, int nw, float* planes, int B, int H, int W, int paddle_width,
+                           int brick_rows, hipStream_t stream);
+
+/* RLSystem._prepare_mcts_input + _encode_actions (train_torch.py:259-293) for all envs:
+ * NHWC out [B][HW][Cs] (f32 or bf16): L-1 ring frames oldest first, the current frame, L action
+ * planes a/3, zero padding to Cs. */
+int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* hist_frames, const uint8_t* hist_actions,
+                         const int32_t* hist_len, int L, void* out, int out_bf16, int B, int HW, int Cs,
+                         hipStream_t stream);
+
+/* ---- networks (src/networks.py) -------------------------------------------------------- */
+
+/* Conv2d(+BN folded)(+ReLU)(+residual) as one implicit-GEMM MFMA kernel: ConvBlock /
+ * ResidualBlock halves / plain Conv2d (networks.py:7-35, 48-72). dtype 0 = f32, 1 = bf16.
+ * in: NHWC, env b at in + b*in_env_stride (+ slot[b]*in_slot_stride when slot != NULL: gather of
+ * parent latents from the node pool). w: [Cout][ks*ks*Cin] (tap-major, K-contiguous). bias f32.
+ * act_bias f32 [HW][A][Cout] + act i32[B]: the dynamics net's one-hot action planes
+ * (mcts.py:252-268). res: residual [B*HW][Cout] (may alias out). Cin % (dtype ? 64 : 32) == 0. */
+int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
+                const void* w, const float* bias, const float* act_bias, const int32_t* act, int A, const void* res,
+                void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream);
+
+/* nn.AvgPool2d(2, 2) (networks.py:44), NHWC. */
+int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream);
+
+/* MuZeroAgent._scale_state (networks.py:314-328): per-env min-max over n values; writes out and,
+ * when pool != NULL, pool + b*pool_env_stride + (slot_arr ? slot_arr[b] : slot_const)*slot_stride. */
+int mzba_scale_state(int dtype, const void* h, void* out, void* pool, long long pool_env_stride,
+                     const int32_t* slot_arr, int slot_const, long long slot_stride, int B, int n,
+                     hipStream_t stream);
+
+/* Linear heads (networks.py:147-148, 207-208, 221-222) + decode: dec 0 = softmax (mcts.py:100,199),
+ * dec 1 = ScalarTransforms.inverted_softmax_expectation (utils.py:74-81). w: [O][K] f32 in NHWC
+ * flatten order; logits optional. */
+int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const float* b0, int K0, int O0, int dec0,
+               float* logits0, float* out0, const void* x1, const float* w1, const float* b1, int K1, int O1,
+               int dec1, float* logits1, float* out1, float smin, float smax, int B, hipStream_t stream);
+
+/* ---- latent MCTS (src/mcts.py:MCTSSearchVec) ------------------------------------------- */
+/* Tree buffers (device): nodes [B][S+1] x mzba_mcts_node_bytes(), root_sum f32[B], calls u32[B],
+ * leaf_parent/leaf_action/depth i32[B], path i32[B][S+1]; sqrt_tab/c_tab f32[S+1] =
+ * f32(sqrt(n)), f32(c1 + log((n+c2+1)/c2)) computed in double on the host (mcts.py:285-289). */
+int mzba_mcts_node_bytes(void);
+
+/* _initialize_trees + _expand_root_nodes (mcts.py:73-134): root P = f32(w_pol*pi) + f32(w_noise*noise),
+ * noise = noise_in or Dirichlet(alpha) from Philox stream 2 (written to noise_out), first ucb_action. */
+int mzba_mcts_root(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
+                   int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
+                   int env_offset, int search_id, uint64_t seed, const float* v_root, const float* pi_root,
+                   const float* noise_in, float* noise_out, float w_pol, float w_noise, float alpha,
+                   hipStream_t stream);
+
+/* _select_nodes (mcts.py:136-182) for simulation sim >= 1 (ucb_action :281-298). */
+int mzba_mcts_select(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
+                     int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
+                     int env_offset, int search_id, uint64_t seed, int sim, hipStream_t stream);
+
+/* _backup (mcts.py:203-234) with decoded r[B], v[B], pi[B][3] of the expanded leaves. */
+int mzba_mcts_backup(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
+                     int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
+                     int env_offset, int search_id, uint64_t seed, int sim, const float* r, const float* v,
+                     const float* pi, float gamma, hipStream_t stream);
+
+/* _compute_results (mcts.py:236-250): counts i64[B][3], values f32[B] = f32(double(root_sum)/S). */
+int mzba_mcts_results(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
+                      int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
+                      int env_offset, int search_id, uint64_t seed, int64_t* counts, float* values,
+                      hipStream_t stream);
+
+/* Temperature sampling (train_torch.py:191-198): p = counts^(1/T)/sum, inverse CDF of
+ * u = Philox uniform(env+env_offset, stream 3, step, 0). */
+int mzba_sample_actions(const int64_t* counts, int64_t* action, int B, float temperature, int env_offset, int step,
+                        uint64_t seed, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MZBA_H */

@@ -1,0 +1,304 @@
+// Implicit-GEMM convolution for the MuZero ResNets on gfx950 MFMA.
+//
+// out[m][n] = act( sum_k A[m][k] * Wp[n][k] + bias[n] (+ act_bias[p][a_b][n]) (+ res[m][n]) )
+//   m = (env b, pixel p = y*W + x)  — NHWC activations, channel stride Cin (multiple of BK)
+//   k = (tap (ky,kx), channel c)    — A[m][k] = in[b][y+ky-pad][x+kx-pad][c] or 0 (zero padding)
+//   Wp[n][k] = BN-folded weights packed K-contiguous per output channel
+// One kernel covers every conv of the reference nets (networks.py:7-35, 38-241): 3x3 and
+// 1x1, BN folded into (Wp, bias) on the host, ReLU and the residual add fused into the
+// epilogue, and the dynamics net's one-hot action planes folded into a per-(pixel, action)
+// bias table (mcts.py:252-268 planes are constant over the grid, so their conv
+// contribution only depends on the pixel's in-bounds taps).
+//
+// Tile 128x128, 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16 tiles. One K-step moves
+// one 128-byte row slice per tile row (BK = 64 bf16 or 32 f32) and lies inside a single
+// tap (Cin % BK == 0). Operands staged global -> VGPR -> LDS (double buffer, one barrier
+// per K-step), 16-B chunks XOR-swizzled by (row & 7) so the fragment reads are spread
+// over the LDS banks. bf16 uses v_mfma_f32_16x16x32_bf16; the f32 parity path uses
+// v_mfma_f32_16x16x4_f32 (exact f32 fma chain).
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int BM = 128, BN = 128, NT = 256;
+constexpr int ROWB = 128;  // bytes per tile row per K-step
+
+struct ConvArgs {
+  const void* in;
+  long long in_env_stride;   // elements between consecutive envs of the input
+  long long in_slot_stride;  // elements between node slots (latent pool); used when slot != null
+  const int32_t* slot;       // optional per-env slot index (gather of parent latents)
+  const void* w;             // [Cout][taps*Cin]
+  const float* bias;         // [Cout]
+  const float* act_bias;     // optional [HW][A][Cout]
+  const int32_t* act;        // optional per-env action
+  int A;
+  const void* res;           // optional residual, [B*HW][Cout]
+  void* out;                 // [B*HW][Cout]
+  int B, H, W, Cin, Cout, ks, relu;
+};
+
+template <typename T> struct Tr;
+template <> struct Tr<bf16_t> { static constexpr int BK = 64; };
+template <> struct Tr<float> { static constexpr int BK = 32; };
+
+MZ_DEV int swz(int row, int chunk) { return row * ROWB + ((chunk ^ (row & 7)) << 4); }
+
+template <typename T>
+__global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
+  constexpr int BK = Tr<T>::BK;
+  constexpr int EPC = 16 / sizeof(T);  // elements per 16-B chunk
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2][2][BM * ROWB];  // [buf][A/B]
+  const int HW = a.H * a.W;
+  const int M = a.B * HW;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int pad = a.ks / 2;
+  const int Ktot = a.ks * a.ks * a.Cin;
+  const int nK = Ktot / BK;
+
+  // per-thread staging geometry: chunk j of rows r + 32*i
+  const int j = tid & 7, r0 = tid >> 3;
+  const T* in = (const T*)a.in;
+  const T* wgt = (const T*)a.w;
+  const T* abase[4];
+  int ay[4], ax[4];
+  bool mval[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int m = m0 + r0 + 32 * i;
+    mval[i] = m < M;
+    int mm = mval[i] ? m : 0;
+    int b = mm / HW, p = mm - b * HW;
+    ay[i] = p / a.W; ax[i] = p - ay[i] * a.W;
+    long long off = (long long)b * a.in_env_stride;
+    if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
+    abase[i] = in + off;
+  }
+
+  uint4 ra[4], rb[4];
+  auto load_tile = [&](int ks) {
+    const int k0 = ks * BK;
+    const int tap = k0 / a.Cin, c0 = k0 - tap * a.Cin;
+    const int ky = tap / a.ks - pad, kx = tap % a.ks - pad;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int sy = ay[i] + ky, sx = ax[i] + kx;
+      bool ok = mval[i] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(abase[i] + ((long long)(sy * a.W + sx) * a.Cin + c0 + j * EPC))
+                 : make_uint4(0, 0, 0, 0);
+      int n = n0 + r0 + 32 * i;
+      rb[i] = n < a.Cout ? *reinterpret_cast<const uint4*>(wgt + ((long long)n * Ktot + k0 + j * EPC))
+                         : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int row = r0 + 32 * i;
+      *reinterpret_cast<uint4*>(&lds[buf][0][swz(row, j)]) = ra[i];
+      *reinterpret_cast<uint4*>(&lds[buf][1][swz(row, j)]) = rb[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int ks = 0; ks < nK; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nK) load_tile(ks + 1);
+    const uint8_t* la = lds[buf][0];
+    const uint8_t* lb = lds[buf][1];
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[4], bfv[4];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          int row = wm * 64 + mi * 16 + fr;
+          af[mi] = *reinterpret_cast<const bf16x8*>(la + swz(row, kk * 4 + fq));
+        }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          int row = wn * 64 + ni * 16 + fr;
+          bfv[ni] = *reinterpret_cast<const bf16x8*>(lb + swz(row, kk * 4 + fq));
+        }
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mi], bfv[ni], acc[mi][ni], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int kc = 0; kc < 8; ++kc) {
+        float af[4], bfv[4];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          int row = wm * 64 + mi * 16 + fr;
+          af[mi] = *reinterpret_cast<const float*>(la + swz(row, kc) + fq * 4);
+        }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          int row = wn * 64 + ni * 16 + fr;
+          bfv[ni] = *reinterpret_cast<const float*>(lb + swz(row, kc) + fq * 4);
+        }
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[mi], bfv[ni], acc[mi][ni], 0, 0, 0);
+      }
+    }
+    if (ks + 1 < nK) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: D[row = 4*fq + r][col = fr] of each 16x16 tile
+  T* out = (T*)a.out;
+  const T* res = (const T*)a.res;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = n0 + wn * 64 + ni * 16 + fr;
+    if (n >= a.Cout) continue;
+    const float bn = a.bias[n];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + mi * 16 + fq * 4 + r;
+        if (m >= M) continue;
+        float v = acc[mi][ni][r];
+        if (a.act_bias) {
+          int b = m / HW, p = m - b * HW;
+          v = v + a.act_bias[((long long)p * a.A + a.act[b]) * a.Cout + n];
+        }
+        v = v + bn;
+        if (res) v = v + ElemIO<T>::load(res + (long long)m * a.Cout + n);
+        if (a.relu) v = fmaxf(v, 0.f);
+        ElemIO<T>::store(out + (long long)m * a.Cout + n, v);
+      }
+    }
+  }
+}
+
+// 2x2 average pool, NHWC (networks.py:44 nn.AvgPool2d(2, 2))
+template <typename T>
+__global__ void avgpool2_kernel(const T* __restrict__ in, T* __restrict__ out, int B, int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2;
+  size_t n = (size_t)B * Ho * Wo * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    int c = (int)(i % C);
+    size_t q = i / C;
+    int xo = (int)(q % Wo);
+    size_t q2 = q / Wo;
+    int yo = (int)(q2 % Ho);
+    size_t b = q2 / Ho;
+    const T* base = in + ((b * H + 2 * yo) * W + 2 * xo) * C + c;
+    float s = ElemIO<T>::load(base) + ElemIO<T>::load(base + C);
+    s = s + ElemIO<T>::load(base + (size_t)W * C);
+    s = s + ElemIO<T>::load(base + (size_t)W * C + C);
+    ElemIO<T>::store(out + i, s / 4.0f);
+  }
+}
+
+// per-env min-max scaling (networks.py:314-328) over the HW*C real values; writes the
+// scaled latent to out (contiguous) and, when pool != null, to pool slot slot_idx.
+template <typename T>
+__global__ __launch_bounds__(256) void scale_state_kernel(const T* __restrict__ h, T* __restrict__ out,
+                                                          T* __restrict__ pool, long long pool_env_stride,
+                                                          const int32_t* __restrict__ slot_arr, int slot_const,
+                                                          long long slot_stride, int n) {
+  const int b = blockIdx.x;
+  const T* x = h + (size_t)b * n;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    float v = ElemIO<T>::load(x + i);
+    mn = fminf(mn, v); mx = fmaxf(mx, v);
+  }
+  for (int o = 32; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
+  __shared__ float smn[4], smx[4];
+  if ((threadIdx.x & 63) == 0) { smn[threadIdx.x >> 6] = mn; smx[threadIdx.x >> 6] = mx; }
+  __syncthreads();
+  mn = fminf(fminf(smn[0], smn[1]), fminf(smn[2], smn[3]));
+  mx = fmaxf(fmaxf(smx[0], smx[1]), fmaxf(smx[2], smx[3]));
+  const float den = (mx - mn) + 1e-8f;
+  T* o = out + (size_t)b * n;
+  T* po = nullptr;
+  if (pool) {
+    int s = slot_arr ? slot_arr[b] : slot_const;
+    po = pool + (size_t)b * pool_env_stride + (size_t)s * slot_stride;
+  }
+  for (int i = threadIdx.x; i < n; i += 256) {
+    float v = (ElemIO<T>::load(x + i) - mn) / den;
+    ElemIO<T>::store(o + i, v);
+    if (po) ElemIO<T>::store(po + i, v);
+  }
+}
+
+template <typename T>
+int launch_conv(const ConvArgs& a, hipStream_t s) {
+  const int M = a.B * a.H * a.W;
+  dim3 grid((M + BM - 1) / BM, (a.Cout + BN - 1) / BN);
+  hipLaunchKernelGGL(conv_igemm_kernel<T>, grid, dim3(NT), 0, s, a);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// dtype: 0 = f32 (parity), 1 = bf16
+int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
+                const void* w, const float* bias, const float* act_bias, const int32_t* act, int A, const void* res,
+                void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream) {
+  const int BK = dtype ? 64 : 32;
+  MZ_CHECK_ARG(B > 0 && H > 0 && W > 0 && (ks == 1 || ks == 3), -1);
+  MZ_CHECK_ARG(Cin % BK == 0 && Cout % 8 == 0, -2);
+  MZ_CHECK_ARG(!act_bias || (act && A > 0), -3);
+  ConvArgs a{in, in_env_stride, in_slot_stride, slot, w, bias, act_bias, act, A, res, out, B, H, W, Cin, Cout, ks, relu};
+  return dtype ? launch_conv<bf16_t>(a, stream) : launch_conv<float>(a, stream);
+}
+
+int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && H >= 2 && W >= 2, -1);
+  size_t n = (size_t)B * (H / 2) * (W / 2) * C;
+  unsigned grid = (unsigned)((n + 255) / 256);
+  if (grid > 8192) grid = 8192;
+  if (dtype)
+    hipLaunchKernelGGL(avgpool2_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, (const bf16_t*)in, (bf16_t*)out, B,
+                       H, W, C);
+  else
+    hipLaunchKernelGGL(avgpool2_kernel<float>, dim3(grid), dim3(256), 0, stream, (const float*)in, (float*)out, B, H,
+                       W, C);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_scale_state(int dtype, const void* h, void* out, void* pool, long long pool_env_stride,
+                     const int32_t* slot_arr, int slot_const, long long slot_stride, int B, int n,
+                     hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && n > 0, -1);
+  if (dtype)
+    hipLaunchKernelGGL(scale_state_kernel<bf16_t>, dim3(B), dim3(256), 0, stream, (const bf16_t*)h, (bf16_t*)out,
+                       (bf16_t*)pool, pool_env_stride, slot_arr, slot_const, slot_stride, n);
+  else
+    hipLaunchKernelGGL(scale_state_kernel<float>, dim3(B), dim3(256), 0, stream, (const float*)h, (float*)out,
+                       (float*)pool, pool_env_stride, slot_arr, slot_const, slot_stride, n);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,487 @@
+// Breakout environment kernels for gfx950.
+//
+// Two state representations, same rules (environment/parallel_breakout.py:107-254):
+//  * "planes": the reference's f32 (B,3,H,W) binary image + ball_dx i64 / ball_dy f32.
+//    Drop-in for BreakoutEnvironment.reset/step; one 64-lane wave per env.
+//  * "compact": SoA per-env scalars + a brick bitmask over the brick rows; used by the
+//    fused acting loop. Phase 1 = one thread per env (branchy scalar rules), phase 2 =
+//    the workgroup renders its envs' uint8 gray-code frames with 16-B coalesced stores
+//    and pushes them into the frame-history ring (train_torch.py:201-209, 259-293).
+#include "common.h"
+
+namespace {
+
+struct RewardCfg { float paddle_hit, brick_hit, lost, won; };
+
+// gray code of a pixel: bit0 paddle, bit1 ball, bit2 brick. The float value of a code is
+// clamp((0.3f*p + 1.0f*b) + 0.6f*br, 0, 1) (train_torch.py:334-358), see gray_lut().
+MZ_DEV uint8_t gray_code(bool paddle, bool ball, bool brick) {
+  return (uint8_t)((paddle ? 1 : 0) | (ball ? 2 : 0) | (brick ? 4 : 0));
+}
+
+// ---------------------------------------------------------------- reset (planes)
+__device__ void reset_params(int b, int B, int W, int pw, uint64_t seed, int episode, int env_offset,
+                             const int32_t* params, int& off, int& col, int& row, int& dx) {
+  if (params) {
+    off = params[0 * B + b]; col = params[1 * B + b]; row = params[2 * B + b]; dx = params[3 * B + b];
+    return;
+  }
+  uint32_t e = (uint32_t)(b + env_offset);
+  int low = -6;
+  int high = W - pw - (W / 2 - pw / 2 - 1);  // parallel_breakout.py:115
+  off = low + mz_randbelow(e, MZ_STREAM_RESET, episode, 0, seed, (uint32_t)(high - low));
+  col = 1 + mz_randbelow(e, MZ_STREAM_RESET, episode, 1, seed, (uint32_t)(W - 2));
+  row = -3 + mz_randbelow(e, MZ_STREAM_RESET, episode, 2, seed, 2u);
+  dx = mz_randbelow(e, MZ_STREAM_RESET, episode, 3, seed, 2u) == 0 ? -1 : 1;
+}
+
+__global__ void env_reset_planes_kernel(float* __restrict__ state, int64_t* __restrict__ ball_dx,
+                                        float* __restrict__ ball_dy, int B, int H, int W, int pw,
+                                        int brick_rows, uint64_t seed, int episode, int env_offset,
+                                        const int32_t* __restrict__ params) {
+  int b = blockIdx.x;
+  int off, col, row, dx;
+  reset_params(b, B, W, pw, seed, episode, env_offset, params, off, col, row, dx);
+  int ppos = W / 2 - pw / 2 + off;  // :120
+  int by = ((H + row) % H + H) % H;  // :128 negative index from the bottom
+  int HW = H * W;
+  float* s = state + (size_t)b * 3 * HW;
+  for (int i = threadIdx.x; i < 3 * HW; i += blockDim.x) {
+    int ch = i / HW, p = i - ch * HW, y = p / W, x = p - y * W;
+    float v = 0.f;
+    if (ch == 0) v = (y == H - 1 && x >= ppos && x < ppos + pw) ? 1.f : 0.f;
+    else if (ch == 1) v = (y == by && x == col) ? 1.f : 0.f;
+    else v = (y < brick_rows) ? 1.f : 0.f;
+    s[i] = v;
+  }
+  if (threadIdx.x == 0) { ball_dx[b] = dx; ball_dy[b] = -1.0f; }
+}
+
+// ---------------------------------------------------------------- step (planes)
+// One wave per env. Follows parallel_breakout.py:158-254 op for op.
+__global__ __launch_bounds__(64) void env_step_planes_kernel(
+    const float* __restrict__ state, float* __restrict__ next_state, const int64_t* __restrict__ action,
+    uint8_t* __restrict__ done, int64_t* __restrict__ ball_dx, float* __restrict__ ball_dy,
+    float* __restrict__ reward, float* __restrict__ valid, int B, int H, int W, int pw, RewardCfg rc,
+    int32_t* __restrict__ err) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int HW = H * W;
+  const float* sp = state + (size_t)b * 3 * HW;
+  const float* sball = sp + HW;
+  const float* sbrick = sp + 2 * HW;
+  // paddle position = first argmax of the paddle plane's last row (:177)
+  float best = -INFINITY; int bi = 0x7fffffff;
+  for (int x = lane; x < W; x += 64) {
+    float v = sp[(H - 1) * W + x];
+    if (v > best || (v == best && x < bi)) { best = v; bi = x; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    float ov = __shfl_xor(best, o); int oi = __shfl_xor(bi, o);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  // ball position (:189) — exactly one ball per env is required
+  int cnt = 0, bpos = -1;
+  for (int p = lane; p < HW; p += 64) {
+    if (sball[p] == 1.0f) { cnt++; bpos = p; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o);
+    int ob = __shfl_xor(bpos, o);
+    bpos = bpos > ob ? bpos : ob;
+  }
+  if (cnt != 1) {
+    if (lane == 0) atomicOr(err, 1);
+    return;
+  }
+  const int y = bpos / W, x = bpos - (bpos / W) * W;
+  const int64_t a = action[b];
+  int pnew = bi + (a == 0 ? -1 : (a == 2 ? 1 : 0));
+  pnew = pnew < 0 ? 0 : (pnew > W - pw ? W - pw : pnew);  // :178-179
+  const float ball_x = (float)x, ball_y = (float)y;
+  int64_t dx = ball_dx[b];
+  float dy = ball_dy[b];
+  const bool wall = (ball_x + (float)dx < 0.f) || (ball_x + (float)dx >= (float)W);  // :195
+  if (wall) dx = -dx;
+  float ny = ball_y + dy;        // :198
+  float nx = ball_x + (float)dx;  // :199
+  const bool missed = ny >= (float)H;  // :202
+  float r = 0.f;
+  if (missed) r = rc.lost;
+  bool dn = (done[b] != 0) || missed;  // :204
+  if (dn) { dx = 0; dy = 0.f; }       // :207-208
+  if (missed) ny = 0.f;                // :209
+  if (ny < 0.f) { dy = dy * -1.0f; ny = ball_y; }  // :213-214
+  const float old_dy = dy;                        // :217
+  const int ix = (int)nx;
+  const int bx = ix - (ix % 2);  // :218 (nx >= 0)
+  const int iy = (int)ny;        // in [0, H) here
+  const bool brick = !dn && sbrick[iy * W + bx] == 1.0f;  // :219 (bricks of done envs cleared)
+  if (brick) dy = -old_dy;                                // :220
+  if (brick) { ny = ball_y - old_dy; r = r + rc.brick_hit; }  // :224-226
+  const bool hit = (ny == (float)(H - 1)) && ix >= pnew && ix < pnew + pw;  // :229-234
+  if (hit) { dy = -dy; r = r + rc.paddle_hit; }                             // :235-239
+  const int fy = (((int)ny) % H + H) % H;  // :243 row -1 wraps to H-1
+  const int clr0 = iy * W + bx, clr1 = iy * W + ((bx + 1) % W);
+  // finished = no bricks left after the unconditional clear (:221-222, :246)
+  int any = 0;
+  if (!dn) {
+    for (int p = lane; p < HW; p += 64) any |= (sbrick[p] != 0.f && p != clr0 && p != clr1) ? 1 : 0;
+  }
+  for (int o = 32; o > 0; o >>= 1) any |= __shfl_xor(any, o);
+  const bool finished = any == 0;
+  const bool dfin = dn || finished;  // :247
+  if (finished != missed) r = r + rc.won;  // :250
+  float* np_ = next_state + (size_t)b * 3 * HW;
+  for (int p = lane; p < HW; p += 64) {
+    const int py = p / W, px = p - py * W;
+    float pv = dfin ? 0.f : (py == H - 1 ? ((px >= pnew && px < pnew + pw) ? 1.f : 0.f) : sp[p]);
+    float bv = (py == fy && px == ix) ? 1.f : 0.f;
+    float kv = dfin ? 0.f : ((p == clr0 || p == clr1) ? 0.f : sbrick[p]);
+    np_[p] = pv; np_[HW + p] = bv; np_[2 * HW + p] = kv;
+  }
+  if (lane == 0) {
+    done[b] = dfin ? 1 : 0;
+    ball_dx[b] = dx;
+    ball_dy[b] = dy;
+    reward[b] = r;
+    valid[b * 3 + 0] = pnew == 0 ? 0.f : 1.f;  // :153
+    valid[b * 3 + 1] = 1.f;
+    valid[b * 3 + 2] = (pnew + pw >= W) ? 0.f : 1.f;  // :154
+  }
+}
+
+// ---------------------------------------------------------------- compact state
+// SoA compact state (global env b):
+//   paddle[b] (i32, left column; plane empty <=> done), bx/by (i32), dx (i32), dy (f32),
+//   done (u8), bricks[b*nw .. b*nw+nw) (u64 bitmask, bit = row*W + col, rows < brick_rows)
+struct Compact {
+  int32_t* paddle; int32_t* bx; int32_t* by; int32_t* dx; float* dy; uint8_t* done; uint64_t* bricks; int nw;
+};
+
+// History ring (train_torch.py:313-332 pad, :204-209 record, :259-293 read):
+//   frames[b][L-1][HW] u8 gray codes, actions[b][L] u8, hlen[b] = records pushed so far.
+struct History { uint8_t* frames; uint8_t* actions; int32_t* hlen; int L; };
+
+// Trajectory sink (replay_buffer.py:17-35 ObservationTrajectory.add_observation),
+// per acting step t: rec_action[t][b] u8, rec_reward[t][b] f32, rec_mask[t][b] u8; the
+// recorded frame is cur_frame (written to rec_frame[t][b][HW] when non-null).
+struct Sink { uint8_t* action; float* reward; uint8_t* mask; uint8_t* frame; };
+
+__global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_frame, History hist, int B,
+                                         int H, int W, int pw, int brick_rows, uint64_t seed, int episode,
+                                         int env_offset, const int32_t* __restrict__ params) {
+  // one block per env: scalars by thread 0, frame + history pad by the block
+  const int b = blockIdx.x;
+  int off, col, row, dx;
+  reset_params(b, B, W, pw, seed, episode, env_offset, params, off, col, row, dx);
+  const int ppos = W / 2 - pw / 2 + off;
+  const int by = ((H + row) % H + H) % H;
+  const int HW = H * W;
+  if (threadIdx.x == 0) {
+    cs.paddle[b] = ppos; cs.bx[b] = col; cs.by[b] = by; cs.dx[b] = dx; cs.dy[b] = -1.0f; cs.done[b] = 0;
+    hist.hlen[b] = 0;
+  }
+  for (int w = threadIdx.x; w < cs.nw; w += blockDim.x) {
+    uint64_t m = 0;
+    for (int k = 0; k < 64; ++k) {
+      int bit = w * 64 + k;
+      if (bit < brick_rows * W) m |= (1ull << k);
+    }
+    cs.bricks[(size_t)b * cs.nw + w] = m;
+  }
+  uint8_t* cf = cur_frame + (size_t)b * HW;
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    int y = p / W, x = p - y * W;
+    uint8_t c = gray_code(y == H - 1 && x >= ppos && x < ppos + pw, y == by && x == col, y < brick_rows);
+    cf[p] = c;
+    for (int k = 0; k < hist.L - 1; ++k) hist.frames[((size_t)b * (hist.L - 1) + k) * HW + p] = c;
+  }
+  for (int k = threadIdx.x; k < hist.L; k += blockDim.x) hist.actions[(size_t)b * hist.L + k] = 0;
+}
+
+// Phase 1: one thread per env, all rules on the compact state (same op order as above).
+// Phase 2: the block renders its 256 envs' frames (16 B per lane per store) and pushes
+// them into the history ring when the env is recorded this step.
+template <int MAXW>
+__global__ __launch_bounds__(256) void env_step_compact_kernel(
+    Compact cs, const int64_t* __restrict__ action, float* __restrict__ reward, float* __restrict__ valid,
+    uint8_t* __restrict__ cur_frame, History hist, Sink sink, int first_step, int B, int H, int W, int pw,
+    int brick_rows, RewardCfg rc) {
+  __shared__ int s_paddle[256], s_bx[256], s_by[256];
+  __shared__ uint64_t s_br[256][MAXW];
+  __shared__ uint8_t s_done[256], s_rec[256];
+  const int t = threadIdx.x;
+  const int b = blockIdx.x * 256 + t;
+  const int nw = cs.nw;
+  if (b < B) {
+    const bool was_done = cs.done[b] != 0;
+    const int p0 = was_done ? 0 : cs.paddle[b];  // argmax of an empty row is 0 (:177)
+    const int64_t a = action[b];
+    int pnew = p0 + (a == 0 ? -1 : (a == 2 ? 1 : 0));
+    pnew = pnew < 0 ? 0 : (pnew > W - pw ? W - pw : pnew);
+    const int x = cs.bx[b], y = cs.by[b];
+    const float ball_x = (float)x, ball_y = (float)y;
+    int dx = cs.dx[b];
+    float dy = cs.dy[b];
+    uint64_t br[MAXW];
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w) br[w] = w < nw ? cs.bricks[(size_t)b * nw + w] : 0ull;
+    const bool wall = (ball_x + (float)dx < 0.f) || (ball_x + (float)dx >= (float)W);
+    if (wall) dx = -dx;
+    float ny = ball_y + dy;
+    float nx = ball_x + (float)dx;
+    const bool missed = ny >= (float)H;
+    float r = 0.f;
+    if (missed) r = rc.lost;
+    const bool dn = was_done || missed;
+    if (dn) { dx = 0; dy = 0.f; }
+    if (missed) ny = 0.f;
+    if (ny < 0.f) { dy = dy * -1.0f; ny = ball_y; }
+    const float old_dy = dy;
+    const int ix = (int)nx;
+    const int bxx = ix - (ix % 2);
+    const int iy = (int)ny;
+    bool brick = false;
+    if (!dn && iy < brick_rows) {
+      int bit = iy * W + bxx;
+      brick = (br[bit >> 6] >> (bit & 63)) & 1ull;
+    }
+    if (brick) dy = -old_dy;
+    if (iy < brick_rows) {  // unconditional clear of (iy,bxx),(iy,bxx+1)
+      int b0 = iy * W + bxx, b1 = iy * W + ((bxx + 1) % W);
+#pragma unroll
+      for (int w = 0; w < MAXW; ++w) {
+        if ((b0 >> 6) == w) br[w] &= ~(1ull << (b0 & 63));
+        if ((b1 >> 6) == w) br[w] &= ~(1ull << (b1 & 63));
+      }
+    }
+    if (brick) { ny = ball_y - old_dy; r = r + rc.brick_hit; }
+    const bool hit = (ny == (float)(H - 1)) && ix >= pnew && ix < pnew + pw;
+    if (hit) { dy = -dy; r = r + rc.paddle_hit; }
+    const int fy = (((int)ny) % H + H) % H;
+    uint64_t any = 0;
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w) any |= br[w];
+    const bool finished = dn || any == 0ull;
+    const bool dfin = dn || finished;
+    if (finished != missed) r = r + rc.won;
+    if (dfin) {
+#pragma unroll
+      for (int w = 0; w < MAXW; ++w) br[w] = 0ull;
+    }
+    cs.paddle[b] = pnew; cs.bx[b] = ix; cs.by[b] = fy; cs.dx[b] = dx; cs.dy[b] = dy;
+    cs.done[b] = dfin ? 1 : 0;
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w) if (w < nw) cs.bricks[(size_t)b * nw + w] = br[w];
+    reward[b] = r;
+    valid[b * 3 + 0] = pnew == 0 ? 0.f : 1.f;
+    valid[b * 3 + 1] = 1.f;
+    valid[b * 3 + 2] = (pnew + pw >= W) ? 0.f : 1.f;
+    // record iff not prev_done; at the first step prev_done aliases done (train_torch.py:179)
+    const bool rec = first_step ? !dfin : !was_done;
+    if (sink.action) {
+      sink.action[b] = (uint8_t)a; sink.reward[b] = r; sink.mask[b] = rec ? 1 : 0;
+    }
+    s_paddle[t] = dfin ? -1 : pnew; s_bx[t] = ix; s_by[t] = fy; s_done[t] = dfin; s_rec[t] = rec;
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w) s_br[t][w] = br[w];
+    if (rec) {
+      int hl = hist.hlen[b];
+      hist.actions[(size_t)b * hist.L + (hl % hist.L)] = (uint8_t)a;
+    }
+  }
+  __syncthreads();
+  // phase 2: render. Frame rows are HW bytes; lanes write 16 B (HW % 16 == 0 required).
+  const int HW = H * W;
+  const int chunks = HW / 16;
+  const int nenv = min(256, B - blockIdx.x * 256);
+  for (int i = t; i < nenv * chunks; i += 256) {
+    const int e = i / chunks, c = i - e * chunks;
+    const int gb = blockIdx.x * 256 + e;
+    uint32_t wv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        int p = c * 16 + q * 4 + k;
+        int py = p / W, px = p - py * W;
+        bool pad = s_paddle[e] >= 0 && py == H - 1 && px >= s_paddle[e] && px < s_paddle[e] + pw;
+        bool ball = py == s_by[e] && px == s_bx[e];
+        bool brk = false;
+        if (py < brick_rows) { int bit = py * W + px; brk = (s_br[e][bit >> 6] >> (bit & 63)) & 1ull; }
+        word |= (uint32_t)gray_code(pad, ball, brk) << (8 * k);
+      }
+      wv[q] = word;
+    }
+    uint4 v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+    *reinterpret_cast<uint4*>(cur_frame + (size_t)gb * HW + c * 16) = v;
+    if (sink.frame) *reinterpret_cast<uint4*>(sink.frame + (size_t)gb * HW + c * 16) = v;
+    if (s_rec[e]) {
+      int hl = hist.hlen[gb];
+      *reinterpret_cast<uint4*>(hist.frames + ((size_t)gb * (hist.L - 1) + (hl % (hist.L - 1))) * HW + c * 16) = v;
+    }
+  }
+  __syncthreads();
+  if (b < B && s_rec[t]) hist.hlen[b] = hist.hlen[b] + 1;
+}
+
+// compact -> planes (for parity checks and the drop-in API)
+__global__ void compact_to_planes_kernel(Compact cs, float* __restrict__ planes, int H, int W, int pw,
+                                         int brick_rows) {
+  const int b = blockIdx.x, HW = H * W;
+  const bool dn = cs.done[b] != 0;
+  const int pp = cs.paddle[b], bx = cs.bx[b], by = cs.by[b];
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    int y = p / W, x = p - y * W;
+    float* o = planes + (size_t)b * 3 * HW;
+    o[p] = (!dn && y == H - 1 && x >= pp && x < pp + pw) ? 1.f : 0.f;
+    o[HW + p] = (y == by && x == bx) ? 1.f : 0.f;
+    float k = 0.f;
+    if (y < brick_rows) { int bit = y * W + x; k = ((cs.bricks[(size_t)b * cs.nw + (bit >> 6)] >> (bit & 63)) & 1ull) ? 1.f : 0.f; }
+    o[2 * HW + p] = k;
+  }
+}
+
+// grayscale from planes (train_torch.py:334-358), f32 out (B,1,H,W)
+__global__ void grayscale_planes_kernel(const float* __restrict__ s, float* __restrict__ g, int B, int HW) {
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)B * HW) return;
+  size_t b = i / HW, p = i - b * HW;
+  const float* sp = s + b * 3 * HW;
+  float v = (sp[p] * 0.3f + sp[HW + p] * 1.0f) + sp[2 * HW + p] * 0.6f;
+  g[i] = fminf(fmaxf(v, 0.f), 1.f);
+}
+
+// Representation-net input (train_torch.py:259-293) from the history ring, NHWC with
+// channel stride Cs (>= 2L, zero padded): c < L-1: ring frames oldest first; c == L-1:
+// current frame; L <= c < 2L: action a/3 planes (oldest first).
+template <typename T>
+__global__ void build_rep_input_kernel(const uint8_t* __restrict__ cur_frame, History hist, T* __restrict__ out,
+                                       int B, int HW, int Cs) {
+  __shared__ float lut[8];
+  if (threadIdx.x < 8) {
+    int c = threadIdx.x;
+    float pv = (c & 1) ? 1.f : 0.f, bv = (c & 2) ? 1.f : 0.f, kv = (c & 4) ? 1.f : 0.f;
+    float v = (pv * 0.3f + bv * 1.0f) + kv * 0.6f;
+    lut[c] = fminf(fmaxf(v, 0.f), 1.f);
+  }
+  __syncthreads();
+  const int L = hist.L;
+  size_t n = (size_t)B * HW;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = i / HW, p = i - b * HW;
+    const int hl = hist.hlen[b];
+    T* o = out + i * Cs;
+    for (int c = 0; c < Cs; ++c) {
+      float v = 0.f;
+      if (c < L - 1) v = lut[hist.frames[(b * (L - 1) + ((hl + c) % (L - 1))) * HW + p] & 7];
+      else if (c == L - 1) v = lut[cur_frame[b * HW + p] & 7];
+      else if (c < 2 * L) v = (float)hist.actions[b * L + ((hl + c - L) % L)] / 3.0f;
+      ElemIO<T>::store(o + c, v);
+    }
+  }
+}
+
+}  // namespace
+
+// =============================================================================== C ABI
+extern "C" {
+
+int mzba_env_reset_planes(float* state, int64_t* ball_dx, float* ball_dy, int B, int H, int W, int paddle_width,
+                          int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
+                          hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && H > 3 && W > paddle_width && (W % 2) == 0, -1);
+  hipLaunchKernelGGL(env_reset_planes_kernel, dim3(B), dim3(256), 0, stream, state, ball_dx, ball_dy, B, H, W,
+                     paddle_width, brick_rows, seed, episode, env_offset, params);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_env_step_planes(const float* state, float* next_state, const int64_t* action, uint8_t* done,
+                         int64_t* ball_dx, float* ball_dy, float* reward, float* valid, int B, int H, int W,
+                         int paddle_width, const float* rewards4, int32_t* err, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && H > 3 && W > paddle_width && (W % 2) == 0 && rewards4 && err, -1);
+  RewardCfg rc{rewards4[0], rewards4[1], rewards4[2], rewards4[3]};
+  hipLaunchKernelGGL(env_step_planes_kernel, dim3(B), dim3(64), 0, stream, state, next_state, action, done, ball_dx,
+                     ball_dy, reward, valid, B, H, W, paddle_width, rc, err);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_grayscale_planes(const float* state, float* gray, int B, int H, int W, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0, -1);
+  size_t n = (size_t)B * H * W;
+  hipLaunchKernelGGL(grayscale_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, state, gray,
+                     B, H * W);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
+                           uint64_t* bricks, int nw, uint8_t* cur_frame, uint8_t* hist_frames,
+                           uint8_t* hist_actions, int32_t* hist_len, int L, int B, int H, int W, int paddle_width,
+                           int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
+                           hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && L >= 2 && nw * 64 >= brick_rows * W && nw <= 4 && (H * W) % 16 == 0, -1);
+  Compact cs{paddle, bx, by, dx, dy, done, bricks, nw};
+  History h{hist_frames, hist_actions, hist_len, L};
+  hipLaunchKernelGGL(env_reset_compact_kernel, dim3(B), dim3(256), 0, stream, cs, cur_frame, h, B, H, W,
+                     paddle_width, brick_rows, seed, episode, env_offset, params);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
+                          uint64_t* bricks, int nw, const int64_t* action, float* reward, float* valid,
+                          uint8_t* cur_frame, uint8_t* hist_frames, uint8_t* hist_actions, int32_t* hist_len, int L,
+                          uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
+                          int first_step, int B, int H, int W, int paddle_width, int brick_rows,
+                          const float* rewards4, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && L >= 2 && nw >= 1 && nw <= 4 && nw * 64 >= brick_rows * W && (H * W) % 16 == 0 && rewards4,
+               -1);
+  Compact cs{paddle, bx, by, dx, dy, done, bricks, nw};
+  History h{hist_frames, hist_actions, hist_len, L};
+  Sink sk{rec_action, rec_reward, rec_mask, rec_frame};
+  RewardCfg rc{rewards4[0], rewards4[1], rewards4[2], rewards4[3]};
+  dim3 grid((B + 255) / 256);
+  if (nw == 1)
+    hipLaunchKernelGGL(env_step_compact_kernel<1>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
+                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc);
+  else
+    hipLaunchKernelGGL(env_step_compact_kernel<4>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
+                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_compact_to_planes(const int32_t* paddle, const int32_t* bx, const int32_t* by, const uint8_t* done,
+                           const uint64_t* bricks, int nw, float* planes, int B, int H, int W, int paddle_width,
+                           int brick_rows, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0, -1);
+  Compact cs{(int32_t*)paddle, (int32_t*)bx, (int32_t*)by, nullptr, nullptr, (uint8_t*)done, (uint64_t*)bricks, nw};
+  hipLaunchKernelGGL(compact_to_planes_kernel, dim3(B), dim3(256), 0, stream, cs, planes, H, W, paddle_width,
+                     brick_rows);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* hist_frames, const uint8_t* hist_actions,
+                         const int32_t* hist_len, int L, void* out, int out_bf16, int B, int HW, int Cs,
+                         hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && Cs >= 2 * L, -1);
+  History h{(uint8_t*)hist_frames, (uint8_t*)hist_actions, (int32_t*)hist_len, L};
+  size_t n = (size_t)B * HW;
+  unsigned grid = (unsigned)((n + 255) / 256);
+  if (grid > 4096) grid = 4096;
+  if (out_bf16)
+    hipLaunchKernelGGL(build_rep_input_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, cur_frame, h,
+                       (bf16_t*)out, B, HW, Cs);
+  else
+    hipLaunchKernelGGL(build_rep_input_kernel<float>, dim3(grid), dim3(256), 0, stream, cur_frame, h, (float*)out,
+                       B, HW, Cs);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

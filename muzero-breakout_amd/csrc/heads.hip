@@ -1,0 +1,110 @@
+// Linear heads + decode (networks.py:138-149, 200-223; utils.py:74-81; mcts.py:97-100,
+// 197-199). Up to two heads per launch, one workgroup per env:
+//   logits_h = X_h[b] (flattened NHWC, K_h) . W_h^T + b_h   (W_h permuted on the host from
+//   torch's (c,h,w) flatten order to this (h,w,c) order), then
+//   decode_h = 0: softmax over the outputs (policy)            -> dec[b][o]
+//   decode_h = 1: support expectation + inverse transform       -> dec[b]
+#include "common.h"
+
+namespace {
+
+constexpr int MAXO = 16;
+
+struct HeadArgs {
+  const void* x[2];
+  const float* w[2];
+  const float* bias[2];
+  float* logits[2];  // optional [B][O]
+  float* dec[2];     // [B][O] (softmax) or [B] (value)
+  int K[2], O[2], decode[2];
+  int nheads;
+  float smin, smax;
+};
+
+MZ_DEV float decode_support(const float* l, int n, float smin, float smax) {
+  float m = l[0];
+  for (int i = 1; i < n; ++i) m = fmaxf(m, l[i]);
+  float e[MAXO];
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) { e[i] = expf(l[i] - m); s = s + e[i]; }
+  const float step = (smax - smin) / (float)(n - 1);
+  float x = 0.f;
+  for (int i = 0; i < n; ++i) {
+    float sup = smin + (float)i * step;  // torch.linspace(smin, smax, n)
+    x = x + (e[i] / s) * sup;
+  }
+  float t = fabsf(x) + 0.999f;  // utils.py:28, epsilon 0.001
+  float sg = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+  return sg * (t * t - 1.f);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ float red[4][2][MAXO];
+  __shared__ float outv[2][MAXO];
+  for (int h = 0; h < a.nheads; ++h) {
+    const T* x = (const T*)a.x[h] + (size_t)b * a.K[h];
+    const float* w = a.w[h];
+    const int K = a.K[h], O = a.O[h];
+    float acc[MAXO];
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o) acc[o] = 0.f;
+    for (int k = tid; k < K; k += 256) {
+      float xv = ElemIO<T>::load(x + k);
+#pragma unroll
+      for (int o = 0; o < MAXO; ++o)
+        if (o < O) acc[o] = acc[o] + xv * w[(size_t)o * K + k];
+    }
+#pragma unroll
+    for (int o = 0; o < MAXO; ++o) {
+      float v = acc[o];
+      for (int s = 32; s > 0; s >>= 1) v = v + __shfl_xor(v, s);
+      acc[o] = v;
+    }
+    if ((tid & 63) == 0)
+#pragma unroll
+      for (int o = 0; o < MAXO; ++o) red[tid >> 6][h][o] = acc[o];
+  }
+  __syncthreads();
+  if (tid < a.nheads) {
+    const int h = tid;
+    float l[MAXO];
+    for (int o = 0; o < a.O[h]; ++o) {
+      l[o] = ((red[0][h][o] + red[1][h][o]) + (red[2][h][o] + red[3][h][o])) + a.bias[h][o];
+      if (a.logits[h]) a.logits[h][(size_t)b * a.O[h] + o] = l[o];
+      outv[h][o] = l[o];
+    }
+    if (a.decode[h] == 0) {
+      float m = l[0];
+      for (int o = 1; o < a.O[h]; ++o) m = fmaxf(m, l[o]);
+      float e[MAXO], s = 0.f;
+      for (int o = 0; o < a.O[h]; ++o) { e[o] = expf(l[o] - m); s = s + e[o]; }
+      for (int o = 0; o < a.O[h]; ++o) a.dec[h][(size_t)b * a.O[h] + o] = e[o] / s;
+    } else {
+      a.dec[h][b] = decode_support(l, a.O[h], a.smin, a.smax);
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// x*: [B][K] activations (dtype 0 f32 / 1 bf16); w*: [O][K] f32; decode 0 softmax, 1 support
+int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const float* b0, int K0, int O0, int dec0,
+               float* logits0, float* out0, const void* x1, const float* w1, const float* b1, int K1, int O1,
+               int dec1, float* logits1, float* out1, float smin, float smax, int B, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && nheads >= 1 && nheads <= 2 && O0 <= MAXO && O0 > 0, -1);
+  MZ_CHECK_ARG(nheads == 1 || (O1 <= MAXO && O1 > 0), -1);
+  HeadArgs a{{x0, x1}, {w0, w1}, {b0, b1}, {logits0, logits1}, {out0, out1}, {K0, K1}, {O0, O1}, {dec0, dec1},
+             nheads, smin, smax};
+  if (dtype)
+    hipLaunchKernelGGL(heads_kernel<bf16_t>, dim3(B), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(heads_kernel<float>, dim3(B), dim3(256), 0, stream, a);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

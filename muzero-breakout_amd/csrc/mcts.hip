@@ -1,0 +1,294 @@
+// Latent MCTS tree kernels (src/mcts.py:24-298), one thread per env, trees in HBM.
+//
+// Tree: per env a node pool of S+1 slots (slot 0 = root, slot s+1 = node expanded at
+// simulation s), 64 B per node (one cache line): Q/P/R f32[3], N i32[3], child i32[3].
+// child < 0 = "not expanded". The root's first child (expanded by _expand_root_nodes at
+// sim 0) is deliberately NOT linked: the reference never sets its "expanded" flag
+// (mcts.py:121, 214-225), so the first later visit re-expands it (mcts.py:164-178).
+//
+// Every f32 expression is evaluated op by op in the reference's order (-ffp-contract=off):
+//   ucb_a = Q_a + ((P_a * f32(sqrt n)) / f32(1 + N_a)) * f32(c1 + log((n + c2 + 1)/c2))
+//   with f32(sqrt n) and f32(c1 + log(..)) taken from host tables computed in double
+//   exactly as Python does (mcts.py:285-289);
+//   G = f32(f32(G * f32(gamma)) + r); Q = f32(f32(f32(N) * Q) + G) / f32(N + 1) (mcts.py:231-233)
+// Tie-breaks draw best[randbelow(len(best))] from Philox (env, STREAM_TIE, search_id, k).
+#include "common.h"
+
+namespace {
+
+struct Node {
+  float Q[3];
+  float P[3];
+  float R[3];
+  int N[3];
+  int child[3];
+  int pad;
+};
+static_assert(sizeof(Node) == 64, "node = one 64-B line");
+
+struct TreeArgs {
+  Node* nodes;          // [B][S+1]
+  float* root_sum;      // [B]
+  uint32_t* calls;      // [B] ucb_action call counter (tie-break stream)
+  int32_t* leaf_parent; // [B]
+  int32_t* leaf_action; // [B]
+  int32_t* depth;       // [B]
+  int32_t* path;        // [B][S+1] packed (node << 2) | action
+  const float* sqrt_tab;  // [S+1]
+  const float* c_tab;     // [S+1]
+  int B, S, env_offset, search_id;
+  uint64_t seed;
+};
+
+MZ_DEV int ucb_select(const Node& nd, const TreeArgs& t, int b) {
+  const int n = nd.N[0] + nd.N[1] + nd.N[2];
+  const float sq = t.sqrt_tab[n], ct = t.c_tab[n];
+  float u[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float v = nd.P[a] * sq;
+    v = v / (float)(1 + nd.N[a]);
+    v = v * ct;
+    u[a] = nd.Q[a] + v;
+  }
+  float mx = fmaxf(fmaxf(u[0], u[1]), u[2]);
+  int best[3], cnt = 0;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+    if (u[a] == mx) best[cnt++] = a;
+  const uint32_t k = t.calls[b];
+  t.calls[b] = k + 1;
+  const int j = mz_randbelow((uint32_t)(b + t.env_offset), MZ_STREAM_TIE, (uint32_t)t.search_id, k, t.seed,
+                             (uint32_t)cnt);
+  return best[j];
+}
+
+// ---------------------------------------------------------------- Dirichlet noise
+struct NormalGen {
+  uint32_t env, step, k;
+  uint64_t seed;
+  float spare;
+  bool has;
+  MZ_DEV float uni() {  // (0,1]
+    uint32_t x = mz_u32(env, MZ_STREAM_NOISE, step, k++, seed);
+    return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  }
+  MZ_DEV float normal() {
+    if (has) { has = false; return spare; }
+    u32x4 r = philox4x32(env, MZ_STREAM_NOISE, step, k++, seed);
+    float u1 = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+    float u2 = (float)(r.y >> 8) * (1.0f / 16777216.0f);
+    float rad = sqrtf(-2.0f * logf(u1));
+    float ang = 6.283185307179586f * u2;
+    spare = rad * sinf(ang); has = true;
+    return rad * cosf(ang);
+  }
+  // Marsaglia–Tsang gamma(alpha), alpha < 1 via gamma(alpha + 1) * U^(1/alpha)
+  MZ_DEV float gamma(float alpha) {
+    const float a = alpha < 1.f ? alpha + 1.f : alpha;
+    const float d = a - 1.0f / 3.0f, c = 1.0f / sqrtf(9.0f * d);
+    float g = d;
+    for (int it = 0; it < 64; ++it) {
+      float x = normal();
+      float v = 1.0f + c * x;
+      if (v <= 0.f) continue;
+      v = v * v * v;
+      float u = uni();
+      if (logf(u) < 0.5f * x * x + d - d * v + d * logf(v)) { g = d * v; break; }
+    }
+    if (alpha < 1.f) g = g * powf(uni(), 1.0f / alpha);
+    return fmaxf(g, 1e-37f);
+  }
+};
+
+__global__ void root_init_kernel(TreeArgs t, const float* __restrict__ v_root, const float* __restrict__ pi_root,
+                                 const float* __restrict__ noise_in, float* __restrict__ noise_out, float w_pol,
+                                 float w_noise, float alpha) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= t.B) return;
+  float nz[3];
+  if (noise_in) {
+    nz[0] = noise_in[b * 3]; nz[1] = noise_in[b * 3 + 1]; nz[2] = noise_in[b * 3 + 2];
+  } else {  // mcts.py:114 Dirichlet(alpha * ones(3)).sample()
+    NormalGen g{(uint32_t)(b + t.env_offset), (uint32_t)t.search_id, 0u, t.seed, 0.f, false};
+    float g0 = g.gamma(alpha), g1 = g.gamma(alpha), g2 = g.gamma(alpha);
+    float s = (g0 + g1) + g2;
+    nz[0] = g0 / s; nz[1] = g1 / s; nz[2] = g2 / s;
+  }
+  if (noise_out) { noise_out[b * 3] = nz[0]; noise_out[b * 3 + 1] = nz[1]; noise_out[b * 3 + 2] = nz[2]; }
+  Node nd;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    nd.Q[a] = 0.f;
+    float p = w_pol * pi_root[b * 3 + a];  // mcts.py:119
+    float q = w_noise * nz[a];
+    nd.P[a] = p + q;
+    nd.R[a] = 0.f;
+    nd.N[a] = 0;
+    nd.child[a] = -1;
+  }
+  nd.pad = 0;
+  t.calls[b] = 0;
+  const int a0 = ucb_select(nd, t, b);  // mcts.py:124
+  t.nodes[(size_t)b * (t.S + 1)] = nd;
+  t.root_sum[b] = v_root[b];  // mcts.py:110
+  t.leaf_parent[b] = 0;
+  t.leaf_action[b] = a0;
+  t.depth[b] = 0;
+}
+
+// mcts.py:136-182 for sim >= 1: walk from the root through expanded children.
+__global__ void select_kernel(TreeArgs t, int sim) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= t.B) return;
+  Node* tree = t.nodes + (size_t)b * (t.S + 1);
+  int32_t* path = t.path + (size_t)b * (t.S + 1);
+  int node = 0, d = 0;
+  for (int it = 0;; ++it) {  // depth <= sim: every wave reaches the leaf branch
+    const Node nd = tree[node];
+    const int a = ucb_select(nd, t, b);
+    const int c = nd.child[a];
+    if (c >= 0 && c <= sim && it < sim) {
+      path[d++] = (node << 2) | a;
+      node = c;
+    } else {
+      tree[node].child[a] = sim + 1;  // the new node's slot (mcts.py:167-175 marks it expanded)
+      t.leaf_parent[b] = node;
+      t.leaf_action[b] = a;
+      t.depth[b] = d;
+      break;
+    }
+  }
+}
+
+// mcts.py:203-234: create the expanded node, set the parent edge's reward, back up.
+__global__ void backup_kernel(TreeArgs t, int sim, const float* __restrict__ r, const float* __restrict__ v,
+                              const float* __restrict__ pi, float gamma) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= t.B) return;
+  Node* tree = t.nodes + (size_t)b * (t.S + 1);
+  const int32_t* path = t.path + (size_t)b * (t.S + 1);
+  Node nd;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    nd.Q[a] = 0.f; nd.P[a] = pi[b * 3 + a]; nd.R[a] = 0.f; nd.N[a] = 0; nd.child[a] = -1;
+  }
+  nd.pad = 0;
+  tree[sim + 1] = nd;
+  const int lp = t.leaf_parent[b], la = t.leaf_action[b], d = t.depth[b];
+  const float rl = r[b];
+  tree[lp].R[la] = rl;
+  float G = v[b];
+  for (int i = d; i >= 0; --i) {
+    int node, a;
+    float rr;
+    if (i == d) { node = lp; a = la; rr = rl; }
+    else { node = path[i] >> 2; a = path[i] & 3; rr = tree[node].R[a]; }
+    float g1 = G * gamma;
+    G = g1 + rr;
+    if (node == 0) t.root_sum[b] = t.root_sum[b] + G;
+    Node* e = tree + node;
+    const int n = e->N[a];
+    float q = (float)n * e->Q[a];
+    q = q + G;
+    e->Q[a] = q / (float)(n + 1);
+    e->N[a] = n + 1;
+  }
+}
+
+// mcts.py:236-250 -> counts i64[B][3], values f32[B] = f32(double(root_sum) / S)
+__global__ void results_kernel(TreeArgs t, int64_t* __restrict__ counts, float* __restrict__ values) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= t.B) return;
+  const Node& nd = t.nodes[(size_t)b * (t.S + 1)];
+  counts[b * 3 + 0] = nd.N[0];
+  counts[b * 3 + 1] = nd.N[1];
+  counts[b * 3 + 2] = nd.N[2];
+  values[b] = (float)((double)t.root_sum[b] / (double)t.S);
+}
+
+// train_torch.py:191-198 with inverse-CDF sampling on u = uniform(env, STREAM_SAMPLE, step, 0)
+__global__ void sample_kernel(const int64_t* __restrict__ counts, int64_t* __restrict__ action, int B, float inv_t,
+                              int env_offset, int step, uint64_t seed) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float vt[3];
+  for (int a = 0; a < 3; ++a) {
+    float c = (float)counts[b * 3 + a];
+    vt[a] = inv_t == 1.0f ? c : powf(c, inv_t);
+  }
+  const float s = (vt[0] + vt[1]) + vt[2];
+  const float u = mz_uniform((uint32_t)(b + env_offset), MZ_STREAM_SAMPLE, (uint32_t)step, 0u, seed);
+  float cdf = 0.f;
+  int chosen = -1, last = 0;
+  for (int a = 0; a < 3; ++a) {
+    float p = vt[a] / s;
+    if (p > 0.f) last = a;
+    cdf = cdf + p;
+    if (chosen < 0 && u < cdf) chosen = a;
+  }
+  action[b] = chosen >= 0 ? chosen : last;
+}
+
+TreeArgs make_args(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
+                   int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
+                   int env_offset, int search_id, uint64_t seed) {
+  return TreeArgs{(Node*)nodes, root_sum, calls, leaf_parent, leaf_action, depth, path, sqrt_tab, c_tab,
+                  B,            S,        env_offset, search_id, seed};
+}
+
+}  // namespace
+
+#define MZ_TREE_PARAMS                                                                                       \
+  void *nodes, float *root_sum, uint32_t *calls, int32_t *leaf_parent, int32_t *leaf_action, int32_t *depth, \
+      int32_t *path, const float *sqrt_tab, const float *c_tab, int B, int S, int env_offset, int search_id, \
+      uint64_t seed
+#define MZ_TREE_ARGS \
+  make_args(nodes, root_sum, calls, leaf_parent, leaf_action, depth, path, sqrt_tab, c_tab, B, S, env_offset, search_id, seed)
+
+extern "C" {
+
+int mzba_mcts_node_bytes() { return (int)sizeof(Node); }
+
+int mzba_mcts_root(MZ_TREE_PARAMS, const float* v_root, const float* pi_root, const float* noise_in,
+                   float* noise_out, float w_pol, float w_noise, float alpha, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && S > 0, -1);
+  hipLaunchKernelGGL(root_init_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, MZ_TREE_ARGS, v_root, pi_root,
+                     noise_in, noise_out, w_pol, w_noise, alpha);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_mcts_select(MZ_TREE_PARAMS, int sim, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && sim >= 1 && sim < S, -1);
+  hipLaunchKernelGGL(select_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, MZ_TREE_ARGS, sim);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_mcts_backup(MZ_TREE_PARAMS, int sim, const float* r, const float* v, const float* pi, float gamma,
+                     hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && sim >= 0 && sim < S, -1);
+  hipLaunchKernelGGL(backup_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, MZ_TREE_ARGS, sim, r, v, pi, gamma);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_mcts_results(MZ_TREE_PARAMS, int64_t* counts, float* values, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0, -1);
+  hipLaunchKernelGGL(results_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, MZ_TREE_ARGS, counts, values);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_sample_actions(const int64_t* counts, int64_t* action, int B, float temperature, int env_offset, int step,
+                        uint64_t seed, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && temperature > 0.f, -1);
+  float inv_t = (float)(1.0 / (double)temperature);
+  hipLaunchKernelGGL(sample_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, counts, action, B, inv_t,
+                     env_offset, step, seed);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

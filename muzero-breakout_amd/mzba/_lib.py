@@ -1,0 +1,83 @@
+"""ctypes binding of the C-ABI library `libmzba.so` (include/mzba.h).
+
+The library is the only compute path: if it is missing or a GPU is absent, the
+product raises — there is no CPU fallback. torch is imported first so that the
+process's HIP runtime (torch's libamdhip64.so.7) is the one the library binds to;
+every launch goes to torch's current HIP stream (graph-capturable).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MZBA_LIB", os.path.join(_HERE, "libmzba.so"))
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+LL = ctypes.c_longlong
+U64 = ctypes.c_uint64
+F = ctypes.c_float
+
+# name -> argtypes (all return int: 0 ok, <0 bad argument, >0 hipError_t)
+SIGNATURES = {
+    "mzba_env_reset_planes": [P, P, P, I, I, I, I, I, U64, I, I, P, P],
+    "mzba_env_step_planes": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P],
+    "mzba_grayscale_planes": [P, P, I, I, I, P],
+    "mzba_env_reset_compact": [P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, U64, I, I, P, P],
+    "mzba_env_step_compact": [P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, P, P],
+    "mzba_compact_to_planes": [P, P, P, P, P, I, P, I, I, I, I, I, P],
+    "mzba_build_rep_input": [P, P, P, P, I, P, I, I, I, I, P],
+    "mzba_conv2d": [I, P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
+    "mzba_avgpool2": [I, P, P, I, I, I, I, P],
+    "mzba_scale_state": [I, P, P, P, LL, P, I, LL, I, I, P],
+    "mzba_heads": [I, I, P, P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, F, I, P],
+    "mzba_mcts_node_bytes": [],
+    "mzba_mcts_root": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P, F, F, F, P],
+    "mzba_mcts_select": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, I, P],
+    "mzba_mcts_backup": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, I, P, P, P, F, P],
+    "mzba_mcts_results": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P],
+    "mzba_sample_actions": [P, P, I, F, I, I, U64, P],
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"mzba: HIP library not built ({LIB_PATH}); run __graft_entry__.build() / make -C csrc")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, argt in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(SIGNATURES)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise RuntimeError("mzba: no HIP device visible; the MI355X path has no CPU fallback")
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t):
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with code {rc}")
+    return rc

@@ -1,0 +1,155 @@
+"""Fused on-device acting loop (mirror of train_torch.py:160-233 `_acting_stage` /
+`_run_episode` / `_sample_action`).
+
+One acting step = rep-input assembly from the frame-history ring (:259-293) ->
+representation + min-max scaling (:254) -> latent MCTS (:256) -> temperature
+sampling (:191-198) -> env step + gray render + history push + trajectory record
+(:201-209). Everything stays on the device; the per-step records land in a device
+trajectory sink (replay_buffer.py:ObservationTrajectory fields) that is copied to the
+host once per episode (or all-gathered over RCCL for multi-GPU runs).
+"""
+import numpy as np
+import torch
+
+from . import _lib as L
+from .env import CompactBreakout, gray_lut
+from .search import MCTSSearchVec, SearchWorkspace
+
+
+class ObservationTrajectory:
+    """Host record with the reference's fields (replay_buffer.py:4-35)."""
+
+    def __init__(self, actions, states, rewards, visit_counts, values, length, reward_sum):
+        self.actions, self.states, self.rewards = actions, states, rewards
+        self.visit_counts, self.values = visit_counts, values
+        self.length, self.reward_sum = length, reward_sum
+
+    def add_observation(self, action, state, reward, visit_counts, values):
+        self.actions.append(action); self.states.append(state); self.rewards.append(reward)
+        self.visit_counts.append(visit_counts); self.values.append(values)
+        self.reward_sum += reward
+        self.length += 1
+
+    def get_actions(self):
+        return torch.tensor(self.actions)
+
+    def get_states(self):
+        return torch.stack(self.states)
+
+    def get_rewards(self):
+        return torch.tensor(self.rewards)
+
+    def get_visit_counts(self):
+        return torch.stack(self.visit_counts)
+
+    def get_values(self):
+        return torch.tensor(self.values)
+
+    def get_reward_sum(self):
+        return self.reward_sum
+
+
+class ActingLoop:
+    """B envs acting with MCTS on one device. `env_offset` = global id of env 0 (sharding)."""
+
+    MAX_STEPS = 261  # train_torch.py:186 `length_counter > 260`
+
+    def __init__(self, cfg, agent, B, seed=0, env_offset=0, temperature=1.0, height=16, width=20,
+                 record_frames=True, max_steps=MAX_STEPS):
+        self.cfg, self.agent, self.B = cfg, agent, B
+        self.seed, self.env_offset = seed, env_offset
+        self.temperature = temperature
+        self.max_steps = max_steps
+        mcfg = cfg["model"]
+        self.Lh = mcfg["state_history_length"]
+        self.H, self.W = height, width
+        dev = agent.device
+        self.env = CompactBreakout(cfg["environment"], B, self.Lh, height, width, seed=seed, env_offset=env_offset,
+                                   device=dev)
+        self.search = MCTSSearchVec(cfg, agent, None, seed=seed, env_offset=env_offset)
+        self.ws = SearchWorkspace(self.search, B)
+        p = agent.packed
+        self.cs = (2 * self.Lh + 63) // 64 * 64
+        self.rep_in = torch.empty(B * height * width * self.cs, dtype=p.tdt, device=dev)
+        self.rep_runner = agent.runner(B, height, width)
+        self.action = torch.zeros(B, dtype=torch.int64, device=dev)
+        T = max_steps
+        self.rec = {
+            "action": torch.zeros(T, B, dtype=torch.uint8, device=dev),
+            "reward": torch.zeros(T, B, dtype=torch.float32, device=dev),
+            "mask": torch.zeros(T, B, dtype=torch.uint8, device=dev),
+            "frame": torch.zeros(T, B, height * width, dtype=torch.uint8, device=dev) if record_frames else None,
+            "counts": torch.zeros(T, B, 3, dtype=torch.int64, device=dev),
+            "values": torch.zeros(T, B, dtype=torch.float32, device=dev),
+        }
+        self.noise_log = None  # optional list: per-step Dirichlet noise used (parity tests)
+        self.search_id = 0
+        self.step_index = 0
+        self.episode = 0
+
+    def reset(self, episode=None, params=None):
+        """_acting_stage :166-167: env.reset + _pad_initial_state."""
+        if episode is not None:
+            self.episode = episode
+        self.env.reset(self.episode, params)
+        self.frame0 = self.env.cur_frame.clone()
+        self.episode += 1
+        self.t = 0
+
+    def act(self):
+        """One acting step t (no host synchronisation)."""
+        t = self.t
+        env, ws = self.env, self.ws
+        n = ws.n
+        # _prepare_mcts_input + create_hidden_state_root -> pool slot 0
+        env.build_rep_input(self.rep_in, self.cs, self.agent.dtype == "bf16")
+        self.rep_runner.representation(self.rep_in, ws.cur, pool=ws.pool, pool_env_stride=(ws.S + 1) * n)
+        values, counts = ws.run(self.search_id, None)
+        if self.noise_log is not None:
+            self.noise_log.append(ws.tree.noise.clone())
+        L.call("mzba_sample_actions", L.ptr(counts), L.ptr(self.action), self.B, float(self.temperature),
+               self.env_offset, self.step_index, self.seed, L.stream())
+        self.rec["counts"][t].copy_(counts)
+        self.rec["values"][t].copy_(values)
+        env.step(self.action, t == 0, self.rec, t)
+        self.search_id += 1
+        self.step_index += 1
+        self.t += 1
+
+    def all_done(self):
+        return bool(self.env.done.bool().all().item())
+
+    def run_episode(self, episode=None, params=None):
+        """_run_episode :171-233 -> list of ObservationTrajectory (host)."""
+        self.reset(episode, params)
+        while not self.all_done():
+            if self.t >= self.max_steps:
+                break
+            self.act()
+        return self.trajectories()
+
+    def trajectories(self):
+        """Per-env ObservationTrajectory exactly as _pad_initial_state + add_observation
+        build them (31 padding frames of g(s0), 32 padding actions 0, then the records)."""
+        T = self.t
+        B, L_ = self.B, self.Lh
+        H, W = self.H, self.W
+        rec = {k: (v[:T].cpu().numpy() if v is not None else None) for k, v in self.rec.items()}
+        lut = gray_lut()
+        f0 = self.frame0.view(B, H * W).cpu().numpy()
+        out = []
+        for b in range(B):
+            m = rec["mask"][:, b].astype(bool)
+            acts = [0] * L_ + [int(a) for a in rec["action"][m, b]]
+            pad = torch.from_numpy(lut[f0[b] & 7].reshape(1, H, W))
+            states = [pad] * (L_ - 1)
+            if rec["frame"] is not None:
+                states += [torch.from_numpy(lut[f & 7].reshape(1, H, W)) for f in rec["frame"][m, b]]
+            rews = [0] * L_ + [float(r) for r in rec["reward"][m, b]]
+            vc = [torch.zeros(3)] * L_ + [torch.from_numpy(c) for c in rec["counts"][m, b]]
+            vals = [0.0] * L_ + [float(v) for v in rec["values"][m, b]]
+            rs = np.float32(0)
+            for r in rec["reward"][m, b]:
+                rs = np.float32(rs + r)
+            out.append(ObservationTrajectory(acts, states, rews, vc, vals, int(m.sum()), float(rs)))
+        return out

@@ -1,0 +1,312 @@
+"""MuZero networks on the MI355X path (mirror of src/networks.py:MuZeroAgent, eval only).
+
+Weights are taken in the reference's `state_dict` format and packed once on the host:
+BatchNorm (eval, running stats) folded into the conv weights/bias, convs packed
+[Cout][tap][Cin_pad] (K-contiguous), the dynamics net's 3 action channels folded into a
+per-(pixel, action) bias table, and the Linear heads permuted from torch's (c,h,w)
+flatten order to the NHWC (h,w,c) order. Activations are NHWC on the device in bf16
+(throughput path) or f32 (parity path), computed by the HIP kernels in libmzba.so.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .weights import rep_layout, state_dict_spec
+
+BN_EPS = 1e-5
+DT_CODE = {"f32": 0, "bf16": 1}
+TORCH_DT = {"f32": torch.float32, "bf16": torch.bfloat16}
+
+
+def _np(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def _round64(c):
+    return (c + 63) // 64 * 64
+
+
+class PackedNets:
+    """Device-resident packed weights for one precision."""
+
+    def __init__(self, sd, mcfg, dtype, device):
+        self.mcfg, self.dtype, self.device = mcfg, dtype, device
+        self.tdt = TORCH_DT[dtype]
+        self.c0, self.c1 = mcfg["latent_channels"]
+        self.L = mcfg["state_history_length"]
+        self.lh, self.lw = mcfg["latent_resolution"]
+        self.ns = mcfg["num_supports"]
+        sd = {k: _np(v).astype(np.float64) for k, v in sd.items()}
+        self.rep = []
+        cin = 2 * self.L
+        nconv = 0
+        for kind, i in rep_layout(mcfg):
+            p = f"rep_net.blocks.{i}"
+            if kind == "conv":
+                cout = self.c0 if nconv == 0 else self.c1
+                self.rep.append(("conv", self._conv(sd[p + ".weight"], sd[p + ".bias"], None)))
+                nconv += 1
+                cin = cout
+            elif kind == "res":
+                self.rep.append(("res", self._res(sd, p)))
+            else:
+                self.rep.append(("pool", None))
+        # dynamics (networks.py:117-149)
+        w = sd["dyn_net.conv_block.conv.weight"]
+        cmain = self.c1
+        self.dyn0 = self._conv(w[:, :cmain], sd["dyn_net.conv_block.conv.bias"], self._bn(sd, "dyn_net.conv_block.bn"),
+                               act_w=w[:, cmain:])
+        self.dyn = [self._res(sd, f"dyn_net.res_blocks.{i}") for i in range(mcfg["dynamics_network"]["num_res_blocks"])]
+        self.rew_conv = self._conv(sd["dyn_net.reward_head.0.conv.weight"], sd["dyn_net.reward_head.0.conv.bias"],
+                                   self._bn(sd, "dyn_net.reward_head.0.bn"))
+        self.rew_lin = self._linear(sd["dyn_net.reward_head.2.weight"], sd["dyn_net.reward_head.2.bias"], self.c1)
+        # prediction (networks.py:190-223)
+        self.pred = [self._res(sd, f"pred_net.res_blocks.{i}") for i in range(mcfg["prediction_network"]["num_res_blocks"])]
+        self.pol_conv = self._conv(sd["pred_net.policy_head.0.conv.weight"], sd["pred_net.policy_head.0.conv.bias"],
+                                   self._bn(sd, "pred_net.policy_head.0.bn"))
+        self.pol_lin = self._linear(sd["pred_net.policy_head.2.weight"], sd["pred_net.policy_head.2.bias"], self.c1 // 2)
+        self.val_conv = self._conv(sd["pred_net.value_head.0.conv.weight"], sd["pred_net.value_head.0.conv.bias"],
+                                   self._bn(sd, "pred_net.value_head.0.bn"))
+        self.val_lin = self._linear(sd["pred_net.value_head.2.weight"], sd["pred_net.value_head.2.bias"], self.c1 // 2)
+
+    # -- packing helpers ---------------------------------------------------------------
+    @staticmethod
+    def _bn(sd, p):
+        g, b, m, v = sd[p + ".weight"], sd[p + ".bias"], sd[p + ".running_mean"], sd[p + ".running_var"]
+        alpha = g / np.sqrt(v + BN_EPS)
+        return alpha, b - m * alpha
+
+    def _conv(self, w, bias, bn, act_w=None):
+        cout, cin, k, _ = w.shape
+        if bn is not None:
+            alpha, beta = bn
+            w = w * alpha[:, None, None, None]
+            bias = bias * alpha + beta
+        cin_p = _round64(cin)
+        wp = np.zeros((cout, k, k, cin_p), dtype=np.float64)
+        wp[..., :cin] = w.transpose(0, 2, 3, 1)
+        layer = {
+            "w": torch.tensor(wp.reshape(cout, -1), dtype=torch.float32).to(self.tdt).to(self.device).contiguous(),
+            "b": torch.tensor(bias, dtype=torch.float32, device=self.device),
+            "cin": cin_p, "cout": cout, "ks": k, "act_bias": None,
+        }
+        if act_w is not None:  # (cout, A, k, k) scaled by alpha: per-(pixel, action) bias
+            if bn is not None:
+                act_w = act_w * bn[0][:, None, None, None]
+            A = act_w.shape[1]
+            H, W = self.lh, self.lw
+            tab = np.zeros((H * W, A, cout))
+            pad = k // 2
+            for y in range(H):
+                for x in range(W):
+                    for ky in range(k):
+                        for kx in range(k):
+                            sy, sx = y + ky - pad, x + kx - pad
+                            if 0 <= sy < H and 0 <= sx < W:
+                                tab[y * W + x] += act_w[:, :, ky, kx].T
+            layer["act_bias"] = torch.tensor(tab, dtype=torch.float32, device=self.device).contiguous()
+            layer["A"] = A
+        return layer
+
+    def _res(self, sd, p):
+        return (self._conv(sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], self._bn(sd, p + ".bn1")),
+                self._conv(sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], self._bn(sd, p + ".bn2")))
+
+    def _linear(self, w, b, c):
+        O, K = w.shape
+        hw = K // c
+        wp = w.reshape(O, c, hw).transpose(0, 2, 1).reshape(O, K)
+        return {"w": torch.tensor(wp, dtype=torch.float32, device=self.device).contiguous(),
+                "b": torch.tensor(b, dtype=torch.float32, device=self.device), "K": K, "O": O}
+
+
+class NetRunner:
+    """Launch sequences for the three nets on NHWC device buffers (workspace per B)."""
+
+    def __init__(self, packed, B, H, W):
+        self.p = packed
+        self.B, self.H, self.W = B, H, W
+        dev, tdt = packed.device, packed.tdt
+        c0, c1 = packed.c0, packed.c1
+        cmax = max(c0, c1, _round64(2 * packed.L))
+        HW = H * W
+        self.HW = HW
+        self.lhw = packed.lh * packed.lw
+        z = lambda *s: torch.empty(*s, dtype=tdt, device=dev)  # noqa: E731
+        self.r_a = z(B * HW * cmax)
+        self.r_t = z(B * HW * cmax)
+        self.r_b = z(B * HW * cmax)
+        self.x = z(B * self.lhw * c1)
+        self.t = z(B * self.lhw * c1)
+        self.rc = z(B * self.lhw * c1)
+        self.pc = z(B * self.lhw * (c1 // 2))
+        self.vc = z(B * self.lhw * (c1 // 2))
+        self.dt = DT_CODE[packed.dtype]
+
+    # -- primitives --------------------------------------------------------------------
+    def conv(self, x, layer, out, B, H, W, res=None, relu=True, slot=None, env_stride=None, slot_stride=0, act=None):
+        s = L.stream()
+        env_stride = H * W * layer["cin"] if env_stride is None else env_stride
+        ab = layer.get("act_bias")
+        L.call("mzba_conv2d", self.dt, L.ptr(x), env_stride, L.ptr(slot), slot_stride, L.ptr(layer["w"]),
+               L.ptr(layer["b"]), L.ptr(ab), L.ptr(act) if ab is not None else None, layer.get("A", 0),
+               L.ptr(res), L.ptr(out), B, H, W, layer["cin"], layer["cout"], layer["ks"], 1 if relu else 0, s)
+
+    def resblock(self, blk, x, t, out, B, H, W):
+        """networks.py:31-35; out may alias x (in-place residual)."""
+        self.conv(x, blk[0], t, B, H, W, relu=True)
+        self.conv(t, blk[1], out, B, H, W, res=x, relu=True)
+
+    # -- nets ----------------------------------------------------------------------------
+    def representation(self, x_in, out_latent, pool=None, pool_env_stride=0):
+        """RepresentationNetwork + _scale_state (networks.py:94-99, 271-280).
+        x_in: [B][H*W][Cin_pad] NHWC. Writes the scaled latent to out_latent (and pool slot 0)."""
+        B, H, W = self.B, self.H, self.W
+        cur, bufs = x_in, [self.r_a, self.r_b]
+        which = 0
+        for kind, layer in self.p.rep:
+            if kind == "conv":
+                dst = bufs[which]
+                self.conv(cur, layer, dst, B, H, W, relu=False)
+                cur = dst
+                which ^= 1
+            elif kind == "res":
+                self.resblock(layer, cur, self.r_t, cur, B, H, W)
+            else:
+                dst = bufs[which]
+                C = self.p.c1
+                L.call("mzba_avgpool2", self.dt, L.ptr(cur), L.ptr(dst), B, H, W, C, L.stream())
+                H, W = H // 2, W // 2
+                cur = dst
+                which ^= 1
+        n = H * W * self.p.c1
+        L.call("mzba_scale_state", self.dt, L.ptr(cur), L.ptr(out_latent), L.ptr(pool), pool_env_stride, None, 0,
+               0, B, n, L.stream())
+
+    def dynamics(self, parent_src, act, out_latent, r_dec, r_logits=None, slot=None, env_stride=None, slot_stride=0,
+                 pool=None, pool_env_stride=0, pool_slot=0):
+        """DynamicsNetwork + _scale_state (networks.py:151-167, 282-298) on NHWC latents.
+        parent_src (+ slot gather) -> out_latent (scaled), r_dec (decoded reward)."""
+        B, H, W = self.B, self.p.lh, self.p.lw
+        p = self.p
+        self.conv(parent_src, p.dyn0, self.x, B, H, W, relu=True, slot=slot, env_stride=env_stride,
+                  slot_stride=slot_stride, act=act)
+        for blk in p.dyn:
+            self.resblock(blk, self.x, self.t, self.x, B, H, W)
+        self.conv(self.x, p.rew_conv, self.rc, B, H, W, relu=True)
+        rl = p.rew_lin
+        L.call("mzba_heads", self.dt, 1, L.ptr(self.rc), L.ptr(rl["w"]), L.ptr(rl["b"]), rl["K"], rl["O"], 1,
+               L.ptr(r_logits), L.ptr(r_dec), None, None, None, 0, 0, 0, None, None,
+               float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B, L.stream())
+        n = H * W * p.c1
+        L.call("mzba_scale_state", self.dt, L.ptr(self.x), L.ptr(out_latent), L.ptr(pool), pool_env_stride, None,
+               pool_slot, n, B, n, L.stream())
+
+    def prediction(self, h, pi, v, p_logits=None, v_logits=None):
+        """PredictionNetwork (networks.py:225-241) + decode (mcts.py:97-100, 197-199)."""
+        B, H, W = self.B, self.p.lh, self.p.lw
+        p = self.p
+        cur = h
+        for i, blk in enumerate(p.pred):
+            self.resblock(blk, cur, self.t, self.x, B, H, W)
+            cur = self.x
+        self.conv(cur, p.pol_conv, self.pc, B, H, W, relu=True)
+        self.conv(cur, p.val_conv, self.vc, B, H, W, relu=True)
+        pl, vl = p.pol_lin, p.val_lin
+        L.call("mzba_heads", self.dt, 2, L.ptr(self.pc), L.ptr(pl["w"]), L.ptr(pl["b"]), pl["K"], pl["O"], 0,
+               L.ptr(p_logits), L.ptr(pi), L.ptr(self.vc), L.ptr(vl["w"]), L.ptr(vl["b"]), vl["K"], vl["O"], 1,
+               L.ptr(v_logits), L.ptr(v), float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B,
+               L.stream())
+
+
+class MuZeroAgent:
+    """Drop-in for src/networks.py:MuZeroAgent inference (eval mode).
+
+    cfg: the reference's `model` config dict. Extra key `dtype` ("bf16" | "f32",
+    default "bf16") selects the device precision; "f32" is the parity mode.
+    """
+
+    def __init__(self, cfg, dtype=None, device="cuda"):
+        L.require_gpu()
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype or cfg.get("dtype", "bf16")
+        self.packed = None
+        self._runners = {}
+        self._sd = None
+
+    # reference API ---------------------------------------------------------------------
+    def state_dict(self):
+        return self._sd
+
+    def load_state_dict(self, sd):
+        spec = state_dict_spec(self.cfg)
+        missing = [k for k, _ in spec if k not in sd]
+        if missing:
+            raise KeyError(f"missing keys in state_dict: {missing[:5]} ...")
+        for k, shape in spec:
+            if tuple(np.shape(_np(sd[k]))) != tuple(shape):
+                raise ValueError(f"shape mismatch for {k}: {np.shape(_np(sd[k]))} vs {shape}")
+        self._sd = {k: _np(sd[k]).copy() for k, _ in spec}
+        self.packed = PackedNets(self._sd, self.cfg, self.dtype, self.device)
+        self._runners = {}
+
+    def eval_mode(self):
+        pass  # BN always uses running stats on this path (networks.py:336-342)
+
+    def runner(self, B, H, W):
+        key = (B, H, W)
+        if key not in self._runners:
+            self._runners[key] = NetRunner(self.packed, B, H, W)
+        return self._runners[key]
+
+    # NCHW <-> NHWC glue (API surface only; the acting loop stays NHWC) ------------------
+    def _nhwc(self, x, cpad=None):
+        B, C, H, W = x.shape
+        cp = cpad or C
+        out = torch.zeros(B, H, W, cp, dtype=self.packed.tdt, device=self.device)
+        out[..., :C] = x.to(self.device).permute(0, 2, 3, 1).to(self.packed.tdt)
+        return out
+
+    def _nchw(self, x, B, C, H, W):
+        return x.view(B, H, W, C).permute(0, 3, 1, 2).float().contiguous()
+
+    def create_hidden_state_root(self, state):
+        """networks.py:271-280: (B, 2L, H, W) -> scaled latent (B, C, h, w)."""
+        B, C, H, W = state.shape
+        r = self.runner(B, H, W)
+        x = self._nhwc(state, _round64(C))
+        out = torch.empty(B * r.lhw * self.packed.c1, dtype=self.packed.tdt, device=self.device)
+        r.representation(x, out)
+        return self._nchw(out, B, self.packed.c1, self.packed.lh, self.packed.lw)
+
+    def hidden_state_transition(self, prev_hidden_state, action):
+        """networks.py:282-298: action = one-hot planes (B, A, h, w) -> (h', reward logits)."""
+        B = prev_hidden_state.shape[0]
+        r = self.runner(B, *self._rep_hw())
+        x = self._nhwc(prev_hidden_state)
+        act = action.to(self.device)[:, :, 0, 0].argmax(dim=1).to(torch.int32).contiguous()
+        out = torch.empty(B * r.lhw * self.packed.c1, dtype=self.packed.tdt, device=self.device)
+        rdec = torch.empty(B, dtype=torch.float32, device=self.device)
+        rlog = torch.empty(B, self.packed.ns, dtype=torch.float32, device=self.device)
+        r.dynamics(x, act, out, rdec, rlog)
+        return self._nchw(out, B, self.packed.c1, self.packed.lh, self.packed.lw), rlog
+
+    def evaluate_state(self, hidden_state):
+        """networks.py:300-312 -> (policy logits (B,3), value logits (B,11))."""
+        B = hidden_state.shape[0]
+        r = self.runner(B, *self._rep_hw())
+        x = self._nhwc(hidden_state)
+        pi = torch.empty(B, 3, dtype=torch.float32, device=self.device)
+        v = torch.empty(B, dtype=torch.float32, device=self.device)
+        pl = torch.empty(B, 3, dtype=torch.float32, device=self.device)
+        vl = torch.empty(B, self.packed.ns, dtype=torch.float32, device=self.device)
+        r.prediction(x, pi, v, pl, vl)
+        return pl, vl
+
+    def _rep_hw(self):
+        return (self.packed.lh * 4, self.packed.lw * 4)

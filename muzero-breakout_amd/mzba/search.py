@@ -1,0 +1,180 @@
+"""Latent MCTS on the MI355X path (mirror of src/mcts.py:MCTSSearchVec).
+
+The whole search runs on the device with no host synchronisation: per simulation
+one select kernel (all envs' tree walks), the dynamics net gathered from the latent
+node pool by the selected parent slots, the prediction net, and one backup kernel.
+The launch sequence is identical for every call of a given (B, S), so the acting loop
+can capture it in a HIP graph.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .agent import MuZeroAgent  # noqa: F401  (re-export for the drop-in module)
+
+
+def ucb_tables(S, c1, c2, device):
+    """f32(sqrt(n)) and f32(c1 + log((n + c2 + 1) / c2)) for n = 0..S, evaluated in
+    double exactly as mcts.py:285-289 does (math.sqrt / math.log on Python floats)."""
+    sq = np.array([math.sqrt(n) for n in range(S + 1)], dtype=np.float64).astype(np.float32)
+    ct = np.array([c1 + math.log((n + c2 + 1) / c2) for n in range(S + 1)], dtype=np.float64).astype(np.float32)
+    return torch.from_numpy(sq).to(device), torch.from_numpy(ct).to(device)
+
+
+class TreeState:
+    """Device buffers of B search trees with S simulations."""
+
+    def __init__(self, B, S, c1, c2, device):
+        self.B, self.S = B, S
+        nb = L.lib().mzba_mcts_node_bytes()
+        self.nodes = torch.empty(B * (S + 1) * nb, dtype=torch.uint8, device=device)
+        self.root_sum = torch.empty(B, dtype=torch.float32, device=device)
+        self.calls = torch.empty(B, dtype=torch.int32, device=device)
+        self.leaf_parent = torch.empty(B, dtype=torch.int32, device=device)
+        self.leaf_action = torch.empty(B, dtype=torch.int32, device=device)
+        self.depth = torch.empty(B, dtype=torch.int32, device=device)
+        self.path = torch.empty(B * (S + 1), dtype=torch.int32, device=device)
+        self.sqrt_tab, self.c_tab = ucb_tables(S, c1, c2, device)
+        self.counts = torch.empty(B, 3, dtype=torch.int64, device=device)
+        self.values = torch.empty(B, dtype=torch.float32, device=device)
+        self.noise = torch.empty(B, 3, dtype=torch.float32, device=device)
+
+    def args(self, env_offset, search_id, seed):
+        return (L.ptr(self.nodes), L.ptr(self.root_sum), L.ptr(self.calls), L.ptr(self.leaf_parent),
+                L.ptr(self.leaf_action), L.ptr(self.depth), L.ptr(self.path), L.ptr(self.sqrt_tab),
+                L.ptr(self.c_tab), self.B, self.S, env_offset, search_id, seed)
+
+    # individual kernels -----------------------------------------------------------------
+    def root(self, tree_args, v_root, pi_root, noise_in, w_pol, w_noise, alpha):
+        L.call("mzba_mcts_root", *tree_args, L.ptr(v_root), L.ptr(pi_root), L.ptr(noise_in), L.ptr(self.noise),
+               w_pol, w_noise, alpha, L.stream())
+
+    def select(self, tree_args, sim):
+        L.call("mzba_mcts_select", *tree_args, sim, L.stream())
+
+    def backup(self, tree_args, sim, r, v, pi, gamma):
+        L.call("mzba_mcts_backup", *tree_args, sim, L.ptr(r), L.ptr(v), L.ptr(pi), gamma, L.stream())
+
+    def results(self, tree_args):
+        L.call("mzba_mcts_results", *tree_args, L.ptr(self.counts), L.ptr(self.values), L.stream())
+
+
+class MCTSSearchVec:
+    """Drop-in for src/mcts.py:MCTSSearchVec (constructor and `search` signature).
+
+    search(hidden_state (B,C,h,w), action_mask (B,3), training_iteration)
+      -> (values f32[B] CPU, visit_counts i64[B,3] CPU), like mcts.py:71.
+    `action_mask` and `training_iteration` are accepted and ignored, as in the
+    reference (mcts.py:124,157 use ones_like(action_mask)).
+    Randomness: Dirichlet root noise and ucb tie-breaks come from the keyed Philox
+    stream (seed, global env, search id) — see DESIGN.md §RNG.
+    """
+
+    def __init__(self, cfg, mu_zero, scalar_transforms=None, seed=0, env_offset=0):
+        self.num_simulations = cfg["num_simulations"]  # mcts.py:13-22
+        self.actions = cfg["actions"]
+        self.c1 = cfg["search"]["c1"]
+        self.c2 = cfg["search"]["c2"]
+        self.discount = cfg["search"]["discount_factor"]
+        self.mu_zero = mu_zero
+        self.scalar_transforms = scalar_transforms
+        self.latent_resolution = cfg["latent_resolution"]
+        self.dirchlet_alpha = 0.25
+        self.noise_weight = 0.175
+        self.seed = seed
+        self.env_offset = env_offset
+        self.search_id = 0
+        self._ws = {}
+
+    # workspace per (B, agent) -------------------------------------------------------------
+    def workspace(self, B):
+        key = (B, id(self.mu_zero), self.mu_zero.dtype)
+        ws = self._ws.get(key)
+        if ws is None:
+            ws = SearchWorkspace(self, B)
+            self._ws = {key: ws}
+        return ws
+
+    def search(self, hidden_state, action_mask=None, training_iteration=0, noise=None):
+        B = hidden_state.shape[0]
+        ws = self.workspace(B)
+        ws.load_root(hidden_state)
+        values, counts = ws.run(self.search_id, noise)
+        self.search_id += 1
+        return values.cpu(), counts.cpu()
+
+
+class SearchWorkspace:
+    """Buffers + launch sequence of one search over B envs (NHWC latents)."""
+
+    def __init__(self, search, B):
+        agent = search.mu_zero
+        self.s = search
+        self.agent = agent
+        dev = agent.device
+        p = agent.packed
+        self.B, self.S = B, search.num_simulations
+        self.n = p.lh * p.lw * p.c1
+        self.tree = TreeState(B, self.S, search.c1, search.c2, dev)
+        self.pool = torch.empty(B * (self.S + 1) * self.n, dtype=p.tdt, device=dev)
+        self.cur = torch.empty(B * self.n, dtype=p.tdt, device=dev)
+        self.r = torch.empty(B, dtype=torch.float32, device=dev)
+        self.v = torch.empty(B, dtype=torch.float32, device=dev)
+        self.pi = torch.empty(B, 3, dtype=torch.float32, device=dev)
+        self.runner = agent.runner(B, p.lh * 4, p.lw * 4)
+
+    def load_root(self, hidden_state):
+        """NCHW (B,C,h,w) latent -> pool slot 0 (NHWC)."""
+        p = self.agent.packed
+        B = self.B
+        x = hidden_state.to(self.agent.device).permute(0, 2, 3, 1).reshape(B, self.n).to(p.tdt)
+        self.pool.view(B, self.S + 1, self.n)[:, 0].copy_(x)
+
+    def root_slot(self):
+        return self.pool.view(self.B, self.S + 1, self.n)[:, 0]
+
+    def run(self, search_id, noise=None):
+        """mcts.py:24-71 on the device. Root latent must be in pool slot 0."""
+        s = self.s
+        B, S, n = self.B, self.S, self.n
+        ta = self.tree.args(s.env_offset, search_id, s.seed)
+        rn = self.runner
+        root = self.pool.view(B, S + 1, n)[:, 0]
+        self.cur.view(B, n).copy_(root)
+        rn.prediction(self.cur, self.pi, self.v)  # _expand_root_nodes mcts.py:95-100
+        w_pol = float(np.float32(1 - s.noise_weight))
+        w_noise = float(np.float32(s.noise_weight))
+        self.tree.root(ta, self.v, self.pi, noise, w_pol, w_noise, s.dirchlet_alpha)
+        gamma = float(np.float32(s.discount))
+        env_stride = (S + 1) * n
+        for sim in range(S):
+            if sim > 0:
+                self.tree.select(ta, sim)
+            rn.dynamics(self.pool, self.tree.leaf_action, self.cur, self.r, slot=self.tree.leaf_parent,
+                        env_stride=env_stride, slot_stride=n, pool=self.pool, pool_env_stride=env_stride,
+                        pool_slot=sim + 1)
+            rn.prediction(self.cur, self.pi, self.v)
+            self.tree.backup(ta, sim, self.r, self.v, self.pi, gamma)
+        self.tree.results(ta)
+        return self.tree.values, self.tree.counts
+
+
+def replay_search(B, S, cfg, v_root, pi_root, noise, r, v, pi, seed, search_id, env_offset=0, device="cuda"):
+    """Tree kernels driven by recorded decoded network outputs (fixture replay mode):
+    the same select/backup/results launches as SearchWorkspace.run, without nets."""
+    L.require_gpu()
+    t = TreeState(B, S, cfg["search"]["c1"], cfg["search"]["c2"], device)
+    dv = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=device)  # noqa: E731
+    ta = t.args(env_offset, search_id, seed)
+    t.root(ta, dv(v_root), dv(pi_root), dv(noise), float(np.float32(1 - 0.175)), float(np.float32(0.175)), 0.25)
+    gamma = float(np.float32(cfg["search"]["discount_factor"]))
+    leaf = np.zeros((S, B), dtype=np.int64)
+    for sim in range(S):
+        if sim > 0:
+            t.select(ta, sim)
+        leaf[sim] = t.leaf_action.cpu().numpy()
+        t.backup(ta, sim, dv(r[sim]), dv(v[sim]), dv(pi[sim]), gamma)
+    t.results(ta)
+    return t.values.cpu().numpy(), t.counts.cpu().numpy(), leaf

@@ -1,0 +1,80 @@
+"""CPU-only checks of the host side: C-ABI library loads and exports every symbol
+declared in include/mzba.h (no compute without a GPU), weight packing/spec logic."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from mzba.config import default_config, small_model_cfg
+from mzba.weights import init_state_dict, state_dict_spec
+
+
+def _declared():
+    h = open(os.path.join(ROOT, "include", "mzba.h")).read()
+    return sorted(set(re.findall(r"\b(mzba_[a-z0-9_]+)\s*\(", h)))
+
+
+def test_library_exports_every_declared_symbol():
+    from mzba import _lib
+    L = _lib.lib()
+    decl = _declared()
+    assert decl, "no declarations parsed"
+    for name in decl:
+        assert hasattr(L, name), name
+    assert sorted(_lib.exported_symbols()) == decl
+
+
+def test_node_layout_is_one_line():
+    from mzba import _lib
+    assert _lib.lib().mzba_mcts_node_bytes() == 64
+
+
+def test_bad_arguments_rejected_without_gpu():
+    from mzba import _lib
+    import ctypes
+    rc = _lib.lib().mzba_conv2d(1, None, 0, None, 0, None, None, None, None, 0, None, None, 0, 4, 5, 256, 256, 3,
+                                1, None)
+    assert rc < 0
+    rc = _lib.lib().mzba_conv2d(1, None, 0, None, 0, None, None, None, None, 0, None, None, 2, 4, 5, 100, 256, 3,
+                                1, None)
+    assert rc == -2
+    del ctypes
+
+
+def test_product_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from mzba.agent import MuZeroAgent
+    with pytest.raises(RuntimeError):
+        MuZeroAgent(default_config()["model"])
+
+
+@pytest.mark.parametrize("small", [False, True])
+def test_state_dict_spec_matches_reference_layout(small):
+    cfg = default_config()
+    m = small_model_cfg(cfg) if small else cfg["model"]
+    spec = dict(state_dict_spec(m))
+    c1 = m["latent_channels"][1]
+    assert spec["dyn_net.conv_block.conv.weight"] == (c1, c1 + 3, 3, 3)
+    assert spec["pred_net.value_head.2.weight"] == (11, c1 // 2 * 20)
+    sd = init_state_dict(m, 0)
+    assert len(sd) == len(spec)
+    w = sd["rep_net.blocks.0.weight"]
+    assert np.abs(w).max() <= 1 / np.sqrt(np.prod(w.shape[1:]))
+    if not small:
+        n = sum(int(np.prod(s)) for k, s in spec.items() if not k.endswith("num_batches_tracked"))
+        assert n > 40_000_000  # rep 8.05M + dyn 17.26M + pred 16.90M
+
+
+def test_ucb_tables_double_precision():
+    import math
+    import torch
+    from mzba.search import ucb_tables
+    sq, ct = ucb_tables(50, 1.25, 19652.0, "cpu")
+    for n in (0, 1, 7, 50):
+        assert sq[n].item() == float(np.float32(math.sqrt(n)))
+        assert ct[n].item() == float(np.float32(1.25 + math.log((n + 19652.0 + 1) / 19652.0)))
+    del torch

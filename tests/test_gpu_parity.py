@@ -1,0 +1,332 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the oracle / golden fixtures.
+Run on the MI355X box: python -m pytest tests -m gpu -x -q"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import rng as R
+from oracle.env import BreakoutEnvOracle, convert_to_grayscale
+from oracle import nets as N
+from oracle.mcts import MCTSOracle, NetModel
+from oracle.acting import prepare_mcts_input, sample_actions, run_episode, Trajectory
+from mzba.config import default_config, small_model_cfg
+from mzba.weights import init_state_dict
+
+pytestmark = pytest.mark.gpu
+
+ENV_CFG = default_config()["environment"]
+
+
+def unpack(p, H, W):
+    B = p.shape[0]
+    return np.unpackbits(p, axis=-1)[..., : H * W].reshape(B, 3, H, W).astype(np.float32)
+
+
+def dev(x, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(x), device="cuda")
+    return t.to(dtype) if dtype is not None else t
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    from mzba import _lib
+    _lib.lib()
+
+
+# ------------------------------------------------------------------------------ env
+@pytest.mark.parametrize("tag", ["16x20", "84x84"])
+def test_env_planes_trajectory(tag):
+    from mzba.env import BreakoutEnvironment
+    d = np.load(os.path.join(GOLDEN, f"env_{tag}.npz"))
+    B, H, W, seed = int(d["B"]), int(d["H"]), int(d["W"]), int(d["seed"])
+    e = BreakoutEnvironment({**ENV_CFG, "n_parallel": B}, seed=seed)
+    e.height, e.width = H, W
+    s, _ = e.reset()  # device Philox draws == oracle reset_params == reference (fixture)
+    np.testing.assert_array_equal(s.cpu().numpy(), unpack(d["states"][0], H, W))
+    np.testing.assert_array_equal(e.ball_dx.cpu().numpy(), d["dx"][0])
+    done = torch.zeros(B, dtype=torch.bool, device="cuda")
+    for t in range(d["actions"].shape[0]):
+        s, r, done2, v = e.step(s, dev(d["actions"][t]), done)
+        assert done2 is done
+        np.testing.assert_array_equal(s.cpu().numpy(), unpack(d["states"][t + 1], H, W), err_msg=f"t={t}")
+        np.testing.assert_array_equal(r.cpu().numpy(), d["rewards"][t])
+        np.testing.assert_array_equal(done.cpu().numpy(), d["dones"][t])
+        np.testing.assert_array_equal(v.cpu().numpy(), d["valids"][t])
+        np.testing.assert_array_equal(e.ball_dx.cpu().numpy(), d["dx"][t + 1])
+        np.testing.assert_array_equal(e.ball_dy.cpu().numpy(), d["dy"][t + 1])
+
+
+@pytest.mark.parametrize("tag", ["16x20", "84x84"])
+def test_env_planes_fuzz(tag):
+    from mzba.env import BreakoutEnvironment
+    d = np.load(os.path.join(GOLDEN, f"envfuzz_{tag}.npz"))
+    B, H, W = int(d["B"]), int(d["H"]), int(d["W"])
+    e = BreakoutEnvironment({**ENV_CFG, "n_parallel": B})
+    e.height, e.width = H, W
+    e.ball_dx, e.ball_dy = dev(d["dx"]), dev(d["dy"])
+    done = dev(d["done"])
+    ns, r, dn, v = e.step(dev(unpack(d["state"], H, W)), dev(d["action"]), done)
+    np.testing.assert_array_equal(ns.cpu().numpy(), unpack(d["next_state"], H, W))
+    np.testing.assert_array_equal(r.cpu().numpy(), d["reward"])
+    np.testing.assert_array_equal(dn.cpu().numpy(), d["next_done"])
+    np.testing.assert_array_equal(v.cpu().numpy(), d["valid"])
+    np.testing.assert_array_equal(e.ball_dx.cpu().numpy(), d["next_dx"])
+    np.testing.assert_array_equal(e.ball_dy.cpu().numpy(), d["next_dy"])
+
+
+def test_env_planes_cpu_tensors_roundtrip():
+    """Drop-in: CPU state/done tensors in, CPU out, done mutated in place."""
+    from mzba.env import BreakoutEnvironment
+    e = BreakoutEnvironment({**ENV_CFG, "n_parallel": 8}, seed=3)
+    s, _ = e.reset()
+    s = s.cpu()
+    done = torch.zeros(8, dtype=torch.bool)
+    for t in range(40):
+        ns, r, d2, v = e.step(s, torch.full((8,), t % 3), done)
+        assert d2 is done and ns.device.type == "cpu"
+        s = ns
+
+
+def test_env_bad_state_raises():
+    from mzba.env import BreakoutEnvironment
+    e = BreakoutEnvironment({**ENV_CFG, "n_parallel": 2})
+    s, _ = e.reset()
+    s[:, 1] = 0  # no ball
+    with pytest.raises(IndexError):
+        e.step(s, torch.zeros(2, dtype=torch.int64, device="cuda"), torch.zeros(2, dtype=torch.bool, device="cuda"))
+
+
+@pytest.mark.parametrize("tag", ["16x20", "84x84"])
+def test_env_compact_matches_planes_and_reference(tag):
+    from mzba.env import CompactBreakout
+    d = np.load(os.path.join(GOLDEN, f"env_{tag}.npz"))
+    B, H, W, seed = int(d["B"]), int(d["H"]), int(d["W"]), int(d["seed"])
+    env = CompactBreakout(ENV_CFG, B, 4, H, W, seed=seed)
+    env.reset(0)
+    np.testing.assert_array_equal(env.to_planes().cpu().numpy(), unpack(d["states"][0], H, W))
+    from mzba.env import gray_lut
+    lut = gray_lut()
+    for t in range(d["actions"].shape[0]):
+        env.step(dev(d["actions"][t]), t == 0)
+        ref = unpack(d["states"][t + 1], H, W)
+        np.testing.assert_array_equal(env.to_planes().cpu().numpy(), ref, err_msg=f"t={t}")
+        np.testing.assert_array_equal(env.reward.cpu().numpy(), d["rewards"][t])
+        np.testing.assert_array_equal(env.done.cpu().numpy().astype(bool), d["dones"][t])
+        np.testing.assert_array_equal(env.valid.cpu().numpy(), d["valids"][t])
+        g = lut[env.cur_frame.view(B, H * W).cpu().numpy() & 7].reshape(B, 1, H, W)
+        np.testing.assert_array_equal(g, convert_to_grayscale(ref))
+
+
+def test_grayscale_kernel():
+    from mzba.env import grayscale
+    g = np.random.default_rng(0)
+    s = (g.random((64, 3, 16, 20)) < 0.3).astype(np.float32)
+    np.testing.assert_array_equal(grayscale(dev(s)).cpu().numpy(), convert_to_grayscale(s))
+
+
+def _oracle_history(B, L, H, W, steps, seed):
+    """Oracle env + trajectories for `steps` random actions (record rule of :204-209)."""
+    e = BreakoutEnvOracle({**ENV_CFG, "n_parallel": B})
+    e.height, e.width = H, W
+    s, _ = e.reset(e.reset_params(seed, 0))
+    g0 = convert_to_grayscale(s)
+    trajs = [Trajectory(L, g0[b]) for b in range(B)]
+    done = np.zeros(B, bool)
+    prev = done
+    acts = []
+    for t in range(steps):
+        a = R.randbelow(np.arange(B), 9, t, 0, seed, 3)
+        acts.append(a)
+        s, r, done, v = e.step(s, a, done)
+        w = convert_to_grayscale(s)
+        for b in range(B):
+            if not prev[b]:
+                trajs[b].add_observation(a[b], w[b], r[b], np.zeros(3, np.int64), 0.0)
+        prev = done.copy()
+    return trajs, convert_to_grayscale(s), acts
+
+
+@pytest.mark.parametrize("L,steps", [(32, 0), (32, 5), (32, 45), (4, 7), (4, 120)])
+def test_rep_input_builder(L, steps):
+    from mzba.env import CompactBreakout
+    B, H, W, seed = 16, 16, 20, 11
+    trajs, cur, acts = _oracle_history(B, L, H, W, steps, seed)
+    env = CompactBreakout(ENV_CFG, B, L, H, W, seed=seed)
+    env.reset(0)
+    for t in range(steps):
+        env.step(dev(acts[t]), t == 0)
+    cs = (2 * L + 63) // 64 * 64
+    out = torch.empty(B * H * W * cs, dtype=torch.float32, device="cuda")
+    env.build_rep_input(out, cs, False)
+    got = out.view(B, H, W, cs).permute(0, 3, 1, 2).cpu().numpy()
+    ref = np.stack([prepare_mcts_input(cur[b], trajs[b], L) for b in range(B)])
+    np.testing.assert_array_equal(got[:, : 2 * L], ref)
+    assert not got[:, 2 * L:].any()
+
+
+# ------------------------------------------------------------------------------ nets
+@pytest.mark.parametrize("tag", ["small", "full"])
+def test_nets_f32_match_reference(tag):
+    from mzba.agent import MuZeroAgent
+    d = np.load(os.path.join(GOLDEN, f"nets_{tag}.npz"))
+    cfg = default_config()
+    mcfg = cfg["model"] if tag == "full" else small_model_cfg(cfg)
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(init_state_dict(mcfg, int(d["weight_seed"])))
+    tol = dict(rtol=1e-5, atol=1e-5)  # north_star: within 1e-5 for network logits/values
+    h = ag.create_hidden_state_root(dev(d["x"])).cpu().numpy()
+    np.testing.assert_allclose(h, d["h"], **tol)
+    pl, vl = ag.evaluate_state(dev(d["h"]))
+    np.testing.assert_allclose(pl.cpu().numpy(), d["p0"], **tol)
+    np.testing.assert_allclose(vl.cpu().numpy(), d["v0"], **tol)
+    planes = N.encode_action_planes(d["action"], mcfg["latent_resolution"])
+    h1, rl = ag.hidden_state_transition(dev(d["h"]), dev(planes))
+    np.testing.assert_allclose(h1.cpu().numpy(), d["h1"], **tol)
+    np.testing.assert_allclose(rl.cpu().numpy(), d["r1"], **tol)
+
+
+def test_nets_bf16_close():
+    from mzba.agent import MuZeroAgent
+    d = np.load(os.path.join(GOLDEN, "nets_full.npz"))
+    mcfg = default_config()["model"]
+    ag = MuZeroAgent(mcfg, dtype="bf16")
+    ag.load_state_dict(init_state_dict(mcfg, int(d["weight_seed"])))
+    h = ag.create_hidden_state_root(dev(d["x"])).cpu().numpy()
+    assert np.abs(h - d["h"]).max() < 0.05
+    pl, vl = ag.evaluate_state(dev(d["h"]))
+    assert np.abs(pl.cpu().numpy() - d["p0"]).max() < 0.05
+    assert np.abs(vl.cpu().numpy() - d["v0"]).max() < 0.05
+
+
+def test_conv_kernel_vs_torch_fp32_random():
+    """Raw conv op vs a plain torch fp32 conv, ragged M (B*HW not a tile multiple), 1x1 and 3x3."""
+    from mzba import _lib as L
+    g = torch.Generator().manual_seed(0)
+    for (B, H, W, Cin, Cout, ks) in [(3, 4, 5, 64, 96, 3), (7, 16, 20, 64, 128, 3), (5, 4, 5, 256, 256, 1),
+                                     (2, 8, 10, 128, 32, 3)]:
+        x = torch.randn(B, Cin, H, W, generator=g)
+        w = torch.randn(Cout, Cin, ks, ks, generator=g) / (Cin * ks * ks) ** 0.5
+        b = torch.randn(Cout, generator=g)
+        res = torch.randn(B, Cout, H, W, generator=g)
+        ref = torch.relu(torch.nn.functional.conv2d(x, w, b, padding=ks // 2) + res)
+        for dt, tol in ((0, 2e-5), (1, 6e-2)):
+            tdt = torch.float32 if dt == 0 else torch.bfloat16
+            xd = x.permute(0, 2, 3, 1).contiguous().to(tdt).cuda()
+            wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().to(tdt).cuda()
+            rd = res.permute(0, 2, 3, 1).contiguous().to(tdt).cuda()
+            out = torch.empty(B, H, W, Cout, dtype=tdt, device="cuda")
+            L.call("mzba_conv2d", dt, L.ptr(xd), H * W * Cin, None, 0, L.ptr(wd), L.ptr(b.cuda()), None, None, 0,
+                   L.ptr(rd), L.ptr(out), B, H, W, Cin, Cout, ks, 1, L.stream())
+            got = out.float().permute(0, 3, 1, 2).cpu()
+            err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+            assert err < tol, (B, H, W, Cin, Cout, ks, dt, err)
+
+
+# ------------------------------------------------------------------------------ MCTS
+@pytest.mark.parametrize("tag", ["b16_s50", "b4_s200"])
+def test_mcts_replay_bit_exact(tag):
+    from mzba.search import replay_search
+    d = np.load(os.path.join(GOLDEN, f"mcts_{tag}.npz"))
+    cfg = default_config()
+    B, S = int(d["B"]), int(d["S"])
+    values, counts, leaf = replay_search(B, S, cfg, d["v_root"], d["pi_root"], d["noise"], d["r"], d["v"], d["pi"],
+                                         int(d["seed"]), int(d["search_id"]))
+    np.testing.assert_array_equal(leaf, d["leaf_action"])
+    np.testing.assert_array_equal(counts, d["counts"])
+    np.testing.assert_array_equal(values.view(np.uint32), d["values"].view(np.uint32))
+
+
+def test_dirichlet_noise_statistics():
+    from mzba.search import TreeState
+    from mzba import _lib as L
+    B = 65536
+    t = TreeState(B, 2, 1.25, 19652.0, "cuda")
+    ta = t.args(0, 5, 1234)
+    t.root(ta, torch.zeros(B, device="cuda"), torch.full((B, 3), 1 / 3, device="cuda"), None, 0.825, 0.175, 0.25)
+    n = t.noise.cpu().numpy().astype(np.float64)
+    assert np.all(n >= 0) and np.allclose(n.sum(1), 1, atol=1e-5)
+    # Dirichlet(0.25,0.25,0.25): mean 1/3, var = (1/3)(2/3)/(0.75+1) = 0.12698
+    assert abs(n.mean() - 1 / 3) < 5e-3
+    assert abs(n[:, 0].var() - (2 / 9) / 1.75) < 5e-3
+    # determinism: same (seed, search id) -> same noise
+    n2 = t.noise.clone()
+    t.root(ta, torch.zeros(B, device="cuda"), torch.full((B, 3), 1 / 3, device="cuda"), None, 0.825, 0.175, 0.25)
+    assert torch.equal(n2, t.noise)
+    del L
+
+
+def test_sample_kernel_matches_oracle():
+    from mzba import _lib as L
+    g = np.random.default_rng(1)
+    B = 4096
+    c = g.integers(0, 20, (B, 3)).astype(np.int64)
+    c[c.sum(1) == 0, 1] = 1
+    for T in (1.0, 0.5):
+        a = torch.empty(B, dtype=torch.int64, device="cuda")
+        L.call("mzba_sample_actions", L.ptr(dev(c)), L.ptr(a), B, T, 0, 17, 99, L.stream())
+        u = R.uniform(np.arange(B), R.STREAM_SAMPLE, 17, 0, 99)
+        ref = sample_actions(c, T, u)
+        got = a.cpu().numpy()
+        if T == 1.0:
+            np.testing.assert_array_equal(got, ref)
+        else:  # powf vs numpy power may differ in the last ulp at exact CDF edges
+            assert (got == ref).mean() > 0.999
+
+
+def _small_cfg(S):
+    cfg = default_config()
+    cfg["model"] = small_model_cfg(cfg)
+    cfg["num_simulations"] = S
+    return cfg
+
+
+def test_search_f32_matches_oracle():
+    from mzba.agent import MuZeroAgent
+    from mzba.search import MCTSSearchVec
+    cfg = _small_cfg(50)
+    mcfg = cfg["model"]
+    sd = init_state_dict(mcfg, 7)
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(sd)
+    B = 16
+    x = np.random.default_rng(3).random((B, 8, 16, 20)).astype(np.float32)
+    h = N.create_hidden_state_root(x, sd, mcfg)
+    s = MCTSSearchVec(cfg, ag, None, seed=42)
+    s.search_id = 3
+    values, counts = s.search(dev(h), torch.ones(B, 3), 0)
+    noise = s._ws[list(s._ws)[0]].tree.noise.cpu().numpy()
+    o = MCTSOracle(cfg, NetModel(sd, mcfg), 42)
+    ov, oc = o.search(h, noise, 3)
+    match = (counts.numpy() == oc).all(1).mean()
+    assert match >= 15 / 16, (match, counts.numpy(), oc)
+    np.testing.assert_allclose(values.numpy()[(counts.numpy() == oc).all(1)], ov[(counts.numpy() == oc).all(1)],
+                               rtol=1e-4, atol=1e-5)
+
+
+def test_acting_loop_f32_matches_oracle_episode():
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingLoop
+    cfg = _small_cfg(20)
+    mcfg = cfg["model"]
+    sd = init_state_dict(mcfg, 5)
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(sd)
+    B, seed = 8, 2024
+    loop = ActingLoop(cfg, ag, B, seed=seed, max_steps=30)
+    loop.noise_log = []
+    trajs = loop.run_episode(0)
+    noises = [n.cpu().numpy() for n in loop.noise_log]
+    otrajs, _ = run_episode(cfg, sd, seed, 0, lambda sid, n: noises[sid], B, max_steps=30)
+    L_ = mcfg["state_history_length"]
+    for b in range(B):
+        assert trajs[b].length == otrajs[b].length
+        np.testing.assert_array_equal(trajs[b].actions, otrajs[b].actions)
+        np.testing.assert_array_equal(np.stack([c.numpy() for c in trajs[b].visit_counts[L_:]]),
+                                      np.stack(otrajs[b].visit_counts[L_:]) if otrajs[b].length else np.zeros((0, 3)))
+        np.testing.assert_array_equal(np.array(trajs[b].rewards[L_:], np.float32), np.array(otrajs[b].rewards[L_:], np.float32))
+        np.testing.assert_array_equal(np.stack([s.numpy() for s in trajs[b].states]), np.stack(otrajs[b].states))
+        np.testing.assert_allclose(trajs[b].values[L_:], np.array(otrajs[b].values[L_:], np.float32), rtol=1e-4, atol=1e-5)
