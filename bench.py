@@ -1,0 +1,190 @@
+"""Headline benchmark: whole-node env-steps/s of the MuZero-Breakout acting loop.
+
+Workload (BASELINE.json configs[1]): 1024 parallel envs per GPU x 50 MCTS sims,
+random-init reference-architecture nets (state_dict format, seeded), bf16 on MFMA.
+One "step" = one acting step over all envs of a GPU: rep-input assembly ->
+representation -> 50 x (select, dynamics, prediction, backup) -> sampling -> env step
++ render + history + trajectory record; every RECORD_K steps the records are gathered
+(RCCL all-gather for N>1) into rank 0's pinned host buffer (the replay-buffer sink).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "muzero-breakout_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+RECORD_K = 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
+    ap.add_argument("--sims", type=int, default=50)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-envs", type=int, default=16, help="bounded oracle sample (cpu_baseline + match rate)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def conv_flops(B, hw, C):
+    return 2.0 * B * hw * C * 9 * C
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from mzba.config import default_config
+    from mzba.weights import init_state_dict
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingLoop
+    from mzba.shard import TrajectoryGather
+    from mzba import _lib as L
+
+    cfg = default_config()
+    cfg["num_simulations"] = args.sims
+    mcfg = cfg["model"]
+    B = args.envs
+    sd = init_state_dict(mcfg, args.seed)
+    agent = MuZeroAgent(mcfg, dtype=args.dtype, device=f"cuda:{local}")
+    agent.load_state_dict(sd)
+    loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B)
+    gather = TrajectoryGather(world, rank, RECORD_K, B, 16 * 20, f"cuda:{local}")
+    loop.reset(0)
+    last_flush = [0]
+
+    def one_step():
+        if loop.t >= loop.max_steps or (loop.t > 0 and loop.all_done()):
+            flush()
+            loop.reset()
+            last_flush[0] = 0
+        loop.act()
+        if loop.t - last_flush[0] >= RECORD_K:
+            flush()
+
+    def flush():
+        if loop.t > last_flush[0]:
+            gather.exchange(loop.rec, last_flush[0], loop.t)
+            last_flush[0] = loop.t
+
+    for _ in range(args.warmup):
+        one_step()
+
+    # ---- visit-count match + CPU baseline on a bounded sample (rank 0, N=1 only) -------
+    cpu_info, match = None, None
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu
+    if want_cpu:
+        nb = min(args.cpu_envs, B)
+        cs = loop.cs
+        x32 = torch.empty(B * 320 * cs, dtype=torch.float32, device=agent.device)
+        L.call("mzba_build_rep_input", L.ptr(loop.env.cur_frame), L.ptr(loop.env.hist_frames),
+               L.ptr(loop.env.hist_actions), L.ptr(loop.env.hist_len), loop.Lh, L.ptr(x32), 0, B, 320, cs, L.stream())
+        sid = loop.search_id
+        t_before = loop.t
+        one_step()
+        torch.cuda.synchronize()
+        gpu_counts = loop.rec["counts"][t_before].cpu().numpy()[:nb] if loop.t == t_before + 1 else None
+        noise = loop.ws.tree.noise.cpu().numpy()[:nb]
+        x = x32.view(B, 16, 20, cs)[:nb, :, :, : 2 * loop.Lh].permute(0, 3, 1, 2).cpu().numpy()
+        from oracle import nets as N
+        from oracle.mcts import MCTSOracle, NetModel
+        nthreads = torch.get_num_threads()
+        t0 = time.perf_counter()
+        h = N.create_hidden_state_root(x, sd, mcfg)
+        _, oc = MCTSOracle(cfg, NetModel(sd, mcfg), args.seed).search(h, noise, sid)
+        cpu_s = time.perf_counter() - t0
+        if gpu_counts is not None:
+            match = float((gpu_counts == oc).all(1).mean())
+        cpu_info = {"value": nb / cpu_s, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
+                    "sample": f"oracle (numpy f32) representation + {args.sims}-sim search for {nb} envs of the "
+                              f"bench's own state, 1 acting step ({cpu_s:.1f} s)"}
+
+    # ---- timed region ---------------------------------------------------------------------
+    probe = []
+    runner = loop.ws.runner
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        runner.probe = probe if i == args.steps // 2 else None
+        one_step()
+    flush()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    runner.probe = None
+    if world > 1:
+        tt = torch.tensor([dt], device=agent.device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    value = world * B * args.steps / dt
+    conv_ms = float(np.mean([a.elapsed_time(b) for a, b in probe])) if probe else None
+    p = agent.packed
+    fl = conv_flops(B, p.lh * p.lw, p.c1)
+    achieved = fl / (conv_ms * 1e-3) / 1e12 if conv_ms else None
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "conv_hbm_traffic.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get("envs") == B:
+                traffic = tj.get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic: seeded random-init reference-architecture nets, seeded Breakout episodes",
+            "config": {"workload": f"config 2: {B} envs/GPU x {args.sims} MCTS sims, 16x20 Breakout, 32-frame stack",
+                       "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
+                       "parallelism": f"env-sharded x{world}, RCCL all-gather of trajectory records"},
+            "roofline": {"bound": "mfma", "kernel": "conv_igemm_kernel<bf16> 3x3 256->256 (M=B*20,N=256,K=2304)",
+                         "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": traffic,
+                         "avg_launch_ms": conv_ms, "launches_timed": len(probe)},
+            "cpu_baseline": cpu_info,
+            "visit_count_match": match,
+            "whole_step_mfma_frac": (B * world * (3.4446e9 + 0.6738e9 + args.sims * 1.3610e9) * args.steps / dt / 1e12)
+                                    / (PEAK_BF16_TFLOPS * world),
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

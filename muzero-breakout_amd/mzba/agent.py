@@ -146,6 +146,9 @@ class NetRunner:
         self.pc = z(B * self.lhw * (c1 // 2))
         self.vc = z(B * self.lhw * (c1 // 2))
         self.dt = DT_CODE[packed.dtype]
+        # optional live probe: list that receives (start, end) HIP events around every
+        # latent-resolution residual conv (the dominant kernel shape M=B*h*w, N=C, K=9C)
+        self.probe = None
 
     # -- primitives --------------------------------------------------------------------
     def conv(self, x, layer, out, B, H, W, res=None, relu=True, slot=None, env_stride=None, slot_stride=0, act=None):
@@ -158,7 +161,14 @@ class NetRunner:
 
     def resblock(self, blk, x, t, out, B, H, W):
         """networks.py:31-35; out may alias x (in-place residual)."""
+        pr = self.probe if (H, W) == (self.p.lh, self.p.lw) else None
+        if pr is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         self.conv(x, blk[0], t, B, H, W, relu=True)
+        if pr is not None:
+            e1.record()
+            pr.append((e0, e1))
         self.conv(t, blk[1], out, B, H, W, res=x, relu=True)
 
     # -- nets ----------------------------------------------------------------------------
