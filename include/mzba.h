@@ -79,6 +79,16 @@ int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_
                 const void* w, const float* bias, const float* act_bias, const int32_t* act, int A, const void* res,
                 void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream);
 
+/* Latent-resolution conv (bf16): same contract as mzba_conv2d for H*W <= 160, Cin in {64,128,256},
+ * Cout % 32 == 0, but the weights are in fragment-major order wf[Cout/32][2][ks*ks][Cin/32][64][8]
+ * followed by 8*64*8 padding elements (the weight ring prefetches 8 k steps past the end; see
+ * DESIGN.md §conv_lat); a workgroup keeps E = 160/(H*W) envs' activations in LDS. */
+int mzba_conv_lat_supported(int H, int W, int Cin, int Cout, int ks);
+int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
+                  const void* wf, const float* bias, const float* act_bias, const int32_t* act, int A,
+                  const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
+                  hipStream_t stream);
+
 /* nn.AvgPool2d(2, 2) (networks.py:44), NHWC. */
 int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream);
 

@@ -18,12 +18,22 @@ from .weights import rep_layout, state_dict_spec
 BN_EPS = 1e-5
 DT_CODE = {"f32": 0, "bf16": 1}
 TORCH_DT = {"f32": torch.float32, "bf16": torch.bfloat16}
+LAT_PAD_ELEMS = 8 * 64 * 8  # conv_lat weight-ring overrun: 8 k steps x 64 lanes x 8 bf16
 
 
 def _np(x):
     if isinstance(x, torch.Tensor):
         return x.detach().cpu().numpy()
     return np.asarray(x)
+
+
+def pack_lat(wp, cout, ks, cin):
+    """Fragment-major weights for conv_lat: wf[ct][kh][tap][c][lane][8] =
+    Wp[32ct + lane%32][tap*cin + kh*cin/2 + 16c + 8(lane//32) + j] (each wave's stream of
+    one 32-column tile x one channel half is contiguous), + 8 padding k steps."""
+    nh = cin // 32
+    wf = wp.reshape(cout // 32, 32, ks * ks, 2, nh, 2, 8).transpose(0, 3, 2, 4, 5, 1, 6).reshape(-1)
+    return np.concatenate([wf, np.zeros(LAT_PAD_ELEMS, wf.dtype)])  # ring prefetch overrun
 
 
 def _round64(c):
@@ -110,6 +120,9 @@ class PackedNets:
                                 tab[y * W + x] += act_w[:, :, ky, kx].T
             layer["act_bias"] = torch.tensor(tab, dtype=torch.float32, device=self.device).contiguous()
             layer["A"] = A
+        if self.dtype == "bf16" and cout % 32 == 0 and cin_p in (64, 128, 256):
+            layer["wf"] = torch.tensor(pack_lat(wp.reshape(cout, -1), cout, k, cin_p),
+                                       dtype=torch.float32).to(self.tdt).to(self.device)
         return layer
 
     def _res(self, sd, p):
@@ -149,12 +162,19 @@ class NetRunner:
         # optional live probe: list that receives (start, end) HIP events around every
         # latent-resolution residual conv (the dominant kernel shape M=B*h*w, N=C, K=9C)
         self.probe = None
+        self.use_lat = True  # latent-resolution bf16 convs on conv_lat (False: generic implicit GEMM)
 
     # -- primitives --------------------------------------------------------------------
     def conv(self, x, layer, out, B, H, W, res=None, relu=True, slot=None, env_stride=None, slot_stride=0, act=None):
         s = L.stream()
         env_stride = H * W * layer["cin"] if env_stride is None else env_stride
         ab = layer.get("act_bias")
+        if "wf" in layer and self.use_lat and L.lib().mzba_conv_lat_supported(H, W, layer["cin"], layer["cout"],
+                                                                             layer["ks"]):
+            L.call("mzba_conv_lat", L.ptr(x), env_stride, L.ptr(slot), slot_stride, L.ptr(layer["wf"]),
+                   L.ptr(layer["b"]), L.ptr(ab), L.ptr(act) if ab is not None else None, layer.get("A", 0),
+                   L.ptr(res), L.ptr(out), B, H, W, layer["cin"], layer["cout"], layer["ks"], 1 if relu else 0, s)
+            return
         L.call("mzba_conv2d", self.dt, L.ptr(x), env_stride, L.ptr(slot), slot_stride, L.ptr(layer["w"]),
                L.ptr(layer["b"]), L.ptr(ab), L.ptr(act) if ab is not None else None, layer.get("A", 0),
                L.ptr(res), L.ptr(out), B, H, W, layer["cin"], layer["cout"], layer["ks"], 1 if relu else 0, s)

@@ -219,7 +219,8 @@ def test_conv_kernel_vs_torch_fp32_random():
             wd = w.permute(0, 2, 3, 1).reshape(Cout, -1).contiguous().to(tdt).cuda()
             rd = res.permute(0, 2, 3, 1).contiguous().to(tdt).cuda()
             out = torch.empty(B, H, W, Cout, dtype=tdt, device="cuda")
-            L.call("mzba_conv2d", dt, L.ptr(xd), H * W * Cin, None, 0, L.ptr(wd), L.ptr(b.cuda()), None, None, 0,
+            bd = b.cuda()
+            L.call("mzba_conv2d", dt, L.ptr(xd), H * W * Cin, None, 0, L.ptr(wd), L.ptr(bd), None, None, 0,
                    L.ptr(rd), L.ptr(out), B, H, W, Cin, Cout, ks, 1, L.stream())
             got = out.float().permute(0, 3, 1, 2).cpu()
             err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
@@ -267,7 +268,8 @@ def test_sample_kernel_matches_oracle():
     c[c.sum(1) == 0, 1] = 1
     for T in (1.0, 0.5):
         a = torch.empty(B, dtype=torch.int64, device="cuda")
-        L.call("mzba_sample_actions", L.ptr(dev(c)), L.ptr(a), B, T, 0, 17, 99, L.stream())
+        cd = dev(c)
+        L.call("mzba_sample_actions", L.ptr(cd), L.ptr(a), B, T, 0, 17, 99, L.stream())
         u = R.uniform(np.arange(B), R.STREAM_SAMPLE, 17, 0, 99)
         ref = sample_actions(c, T, u)
         got = a.cpu().numpy()
@@ -330,3 +332,43 @@ def test_acting_loop_f32_matches_oracle_episode():
         np.testing.assert_array_equal(np.array(trajs[b].rewards[L_:], np.float32), np.array(otrajs[b].rewards[L_:], np.float32))
         np.testing.assert_array_equal(np.stack([s.numpy() for s in trajs[b].states]), np.stack(otrajs[b].states))
         np.testing.assert_allclose(trajs[b].values[L_:], np.array(otrajs[b].values[L_:], np.float32), rtol=1e-4, atol=1e-5)
+
+
+def _pack_wf(wp, cout):
+    K = wp.shape[1]
+    wf = wp.reshape(cout // 32, 32, K // 16, 2, 8).transpose(0, 2, 3, 1, 4).reshape(-1)
+    return np.concatenate([wf, np.zeros(8 * 64 * 8, wf.dtype)])
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,ks", [(7, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 3), (9, 4, 5, 256, 128, 3),
+                                                (13, 4, 5, 256, 256, 1), (5, 8, 10, 256, 256, 3), (3, 4, 5, 64, 64, 3),
+                                                (17, 4, 5, 64, 32, 1), (4, 8, 10, 128, 128, 3)])
+def test_conv_lat_vs_torch(B, H, W, Cin, Cout, ks):
+    """conv_lat (LDS-resident activations, fragment-major weights) vs torch fp32 conv, with
+    the slot gather, the per-(pixel, action) bias and the residual all exercised."""
+    from mzba import _lib as L
+    g = torch.Generator().manual_seed(B * 7 + Cout)
+    S1 = 3
+    pool = torch.randn(B, S1, H, W, Cin, generator=g).to(torch.bfloat16)
+    slot = torch.randint(0, S1, (B,), generator=g, dtype=torch.int32)
+    w = torch.randn(Cout, Cin, ks, ks, generator=g) / (Cin * ks * ks) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    A = 3
+    act = torch.randint(0, A, (B,), generator=g, dtype=torch.int32)
+    ab = torch.randn(H * W, A, Cout, generator=g)
+    res = torch.randn(B, H, W, Cout, generator=g).to(torch.bfloat16)
+    x = pool[torch.arange(B), slot.long()].float()  # (B,H,W,Cin)
+    wq = w.to(torch.bfloat16).float()
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), wq, b, padding=ks // 2).permute(0, 2, 3, 1)
+    ref = torch.relu(ref + ab.view(H, W, A, Cout)[:, :, act.long()].permute(2, 0, 1, 3) + res.float())
+    wp = w.permute(0, 2, 3, 1).reshape(Cout, -1).numpy()
+    from mzba.agent import pack_lat
+    wf = torch.from_numpy(pack_lat(wp, Cout, ks, Cin)).to(torch.bfloat16).cuda()
+    out = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+    assert L.lib().mzba_conv_lat_supported(H, W, Cin, Cout, ks) == 1
+    d = {k: v.cuda() for k, v in dict(pool=pool, slot=slot, b=b, ab=ab, act=act, res=res).items()}  # keep alive
+    L.call("mzba_conv_lat", L.ptr(d["pool"]), S1 * H * W * Cin, L.ptr(d["slot"]), H * W * Cin, L.ptr(wf),
+           L.ptr(d["b"]), L.ptr(d["ab"]), L.ptr(d["act"]), A, L.ptr(d["res"]), L.ptr(out), B, H, W, Cin,
+           Cout, ks, 1, L.stream())
+    err = (out.float().cpu() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+    assert err < 1e-2, err

@@ -1,0 +1,45 @@
+"""Micro-benchmark of the conv kernels on the MI355X (isolated launches, HIP events)."""
+import os
+import sys
+import json
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "muzero-breakout_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from mzba import _lib as L  # noqa: E402
+
+
+def run(B, H, W, Cin, Cout, ks, kind, iters=50):
+    x = torch.randn(B * H * W * Cin, device="cuda").to(torch.bfloat16)
+    out = torch.empty(B * H * W * Cout, device="cuda", dtype=torch.bfloat16)
+    K = ks * ks * Cin
+    w = (torch.randn(Cout * K + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
+    b = torch.zeros(Cout, device="cuda")
+
+    def launch():
+        if kind == "lat":
+            L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(w), L.ptr(b), None, None, 0, L.ptr(x)
+                   if Cin == Cout else None, L.ptr(out), B, H, W, Cin, Cout, ks, 1, L.stream())
+        else:
+            L.call("mzba_conv2d", 1, L.ptr(x), H * W * Cin, None, 0, L.ptr(w), L.ptr(b), None, None, 0, L.ptr(x)
+                   if Cin == Cout else None, L.ptr(out), B, H, W, Cin, Cout, ks, 1, L.stream())
+    for _ in range(5):
+        launch()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for e0, e1 in ev:
+        e0.record(); launch(); e1.record()
+    torch.cuda.synchronize()
+    ms = np.median([a.elapsed_time(c) for a, c in ev])
+    fl = 2.0 * B * H * W * Cout * K
+    return {"kind": kind, "B": B, "HW": (H, W), "Cin": Cin, "Cout": Cout, "ks": ks, "us": ms * 1e3,
+            "tflops": fl / (ms * 1e-3) / 1e12}
+
+
+if __name__ == "__main__":
+    shapes = [(1024, 4, 5, 256, 256, 3), (4096, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 1),
+              (1024, 4, 5, 256, 128, 3), (1024, 8, 10, 256, 256, 3)]
+    for s in shapes:
+        for kind in ("gen", "lat"):
+            print(json.dumps(run(*s, kind)))
