@@ -172,7 +172,7 @@ def main():
             "config": {"workload": f"config 2: {B} envs/GPU x {args.sims} MCTS sims, 16x20 Breakout, 32-frame stack",
                        "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
                        "parallelism": f"env-sharded x{world}, RCCL all-gather of trajectory records"},
-            "roofline": {"bound": "mfma", "kernel": "conv_igemm_kernel<bf16> 3x3 256->256 (M=B*20,N=256,K=2304)",
+            "roofline": {"bound": "mfma", "kernel": "conv_lat_kernel<3,256> bf16 3x3 256->256 (M=B*20,N=256,K=2304)",
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": traffic,
                          "avg_launch_ms": conv_ms, "launches_timed": len(probe)},

@@ -105,6 +105,12 @@ int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const flo
                float* logits0, float* out0, const void* x1, const float* w1, const float* b1, int K1, int O1,
                int dec1, float* logits1, float* out1, float smin, float smax, int B, hipStream_t stream);
 
+/* bf16 path of mzba_heads as a small MFMA GEMM (16 envs per workgroup): x* [B][K] bf16, w* [16][K]
+ * bf16 with zero rows >= O, K % 32 == 0. */
+int mzba_heads_bf16(int nheads, const void* x0, const void* w0, const float* b0, int K0, int O0, int dec0,
+                    float* logits0, float* out0, const void* x1, const void* w1, const float* b1, int K1, int O1,
+                    int dec1, float* logits1, float* out1, float smin, float smax, int B, hipStream_t stream);
+
 /* ---- latent MCTS (src/mcts.py:MCTSSearchVec) ------------------------------------------- */
 /* Tree buffers (device): nodes [B][S+1] x mzba_mcts_node_bytes(), root_sum f32[B], calls u32[B],
  * leaf_parent/leaf_action/depth i32[B], path i32[B][S+1]; sqrt_tab/c_tab f32[S+1] =

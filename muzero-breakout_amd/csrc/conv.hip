@@ -213,18 +213,65 @@ __global__ void avgpool2_kernel(const T* __restrict__ in, T* __restrict__ out, i
   }
 }
 
-// per-env min-max scaling (networks.py:314-328) over the HW*C real values; writes the
-// scaled latent to out (contiguous) and, when pool != null, to pool slot slot_idx.
-template <typename T>
+// per-env min-max scaling (networks.py:314-328) over the HW*C values: one wave per env, a
+// single pass (the env's values stay in registers between the min/max and the write), 16-B
+// accesses. Writes the scaled latent to out and, when pool != null, to its node-pool slot.
+template <typename T, int CPL>
 __global__ __launch_bounds__(256) void scale_state_kernel(const T* __restrict__ h, T* __restrict__ out,
                                                           T* __restrict__ pool, long long pool_env_stride,
                                                           const int32_t* __restrict__ slot_arr, int slot_const,
-                                                          long long slot_stride, int n) {
+                                                          long long slot_stride, int B, int n) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int nch = n / EPC;
+  const uint4* x = reinterpret_cast<const uint4*>(h + (size_t)b * n);
+  uint4 v[CPL];
+  float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < CPL; ++u) {
+    const int c = u * 64 + lane;
+    v[u] = c < nch ? x[c] : x[0];
+    const T* e = reinterpret_cast<const T*>(&v[u]);
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) {
+      const float f = ElemIO<T>::load(e + j);
+      mn = fminf(mn, f); mx = fmaxf(mx, f);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
+  const float den = (mx - mn) + 1e-8f;
+  uint4* o1 = reinterpret_cast<uint4*>(out + (size_t)b * n);
+  uint4* o2 = nullptr;
+  if (pool) {
+    const int s = slot_arr ? slot_arr[b] : slot_const;
+    o2 = reinterpret_cast<uint4*>(pool + (size_t)b * pool_env_stride + (size_t)s * slot_stride);
+  }
+#pragma unroll
+  for (int u = 0; u < CPL; ++u) {
+    const int c = u * 64 + lane;
+    if (c >= nch) break;
+    uint4 r = v[u];
+    T* e = reinterpret_cast<T*>(&r);
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) ElemIO<T>::store(e + j, (ElemIO<T>::load(e + j) - mn) / den);
+    o1[c] = r;
+    if (o2) o2[c] = r;
+  }
+}
+
+// generic two-pass fallback for large latents (e.g. 21x21x256 at 84x84): one workgroup per env
+template <typename T>
+__global__ __launch_bounds__(256) void scale_state_big_kernel(const T* __restrict__ h, T* __restrict__ out,
+                                                              T* __restrict__ pool, long long pool_env_stride,
+                                                              const int32_t* __restrict__ slot_arr, int slot_const,
+                                                              long long slot_stride, int n) {
   const int b = blockIdx.x;
   const T* x = h + (size_t)b * n;
   float mn = INFINITY, mx = -INFINITY;
   for (int i = threadIdx.x; i < n; i += 256) {
-    float v = ElemIO<T>::load(x + i);
+    const float v = ElemIO<T>::load(x + i);
     mn = fminf(mn, v); mx = fmaxf(mx, v);
   }
   for (int o = 32; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
@@ -236,12 +283,9 @@ __global__ __launch_bounds__(256) void scale_state_kernel(const T* __restrict__ 
   const float den = (mx - mn) + 1e-8f;
   T* o = out + (size_t)b * n;
   T* po = nullptr;
-  if (pool) {
-    int s = slot_arr ? slot_arr[b] : slot_const;
-    po = pool + (size_t)b * pool_env_stride + (size_t)s * slot_stride;
-  }
+  if (pool) po = pool + (size_t)b * pool_env_stride + (size_t)(slot_arr ? slot_arr[b] : slot_const) * slot_stride;
   for (int i = threadIdx.x; i < n; i += 256) {
-    float v = (ElemIO<T>::load(x + i) - mn) / den;
+    const float v = (ElemIO<T>::load(x + i) - mn) / den;
     ElemIO<T>::store(o + i, v);
     if (po) ElemIO<T>::store(po + i, v);
   }
@@ -290,13 +334,25 @@ int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int
 int mzba_scale_state(int dtype, const void* h, void* out, void* pool, long long pool_env_stride,
                      const int32_t* slot_arr, int slot_const, long long slot_stride, int B, int n,
                      hipStream_t stream) {
+  const int epc = dtype ? 8 : 4;
   MZ_CHECK_ARG(B > 0 && n > 0, -1);
+  if (n % epc != 0 || n / epc > 64 * (dtype ? 10 : 20)) {
+    if (dtype)
+      hipLaunchKernelGGL(scale_state_big_kernel<bf16_t>, dim3(B), dim3(256), 0, stream, (const bf16_t*)h,
+                         (bf16_t*)out, (bf16_t*)pool, pool_env_stride, slot_arr, slot_const, slot_stride, n);
+    else
+      hipLaunchKernelGGL(scale_state_big_kernel<float>, dim3(B), dim3(256), 0, stream, (const float*)h, (float*)out,
+                         (float*)pool, pool_env_stride, slot_arr, slot_const, slot_stride, n);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  }
+  dim3 grid((B + 3) / 4);
   if (dtype)
-    hipLaunchKernelGGL(scale_state_kernel<bf16_t>, dim3(B), dim3(256), 0, stream, (const bf16_t*)h, (bf16_t*)out,
-                       (bf16_t*)pool, pool_env_stride, slot_arr, slot_const, slot_stride, n);
+    hipLaunchKernelGGL((scale_state_kernel<bf16_t, 10>), grid, dim3(256), 0, stream, (const bf16_t*)h, (bf16_t*)out,
+                       (bf16_t*)pool, pool_env_stride, slot_arr, slot_const, slot_stride, B, n);
   else
-    hipLaunchKernelGGL(scale_state_kernel<float>, dim3(B), dim3(256), 0, stream, (const float*)h, (float*)out,
-                       (float*)pool, pool_env_stride, slot_arr, slot_const, slot_stride, n);
+    hipLaunchKernelGGL((scale_state_kernel<float, 20>), grid, dim3(256), 0, stream, (const float*)h, (float*)out,
+                       (float*)pool, pool_env_stride, slot_arr, slot_const, slot_stride, B, n);
   MZ_LAUNCH_CHECK();
   return 0;
 }

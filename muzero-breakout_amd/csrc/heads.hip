@@ -87,9 +87,94 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
   }
 }
 
+// bf16 path: the heads as a small MFMA GEMM. A workgroup = 16 envs x 16 (padded) outputs;
+// 8 waves split K; v_mfma_f32_16x16x32_bf16 with A = activations (lane: env l&15, 8 k),
+// B = bf16 weights Wb[16][K] (lane: output l&15, 8 k); partial sums reduced through LDS.
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+struct HeadArgsB {
+  const bf16_t* x[2];
+  const bf16_t* w[2];  // [16][K] (rows >= O are zero)
+  const float* bias[2];
+  float* logits[2];
+  float* dec[2];
+  int K[2], O[2], decode[2];
+  int nheads, B;
+  float smin, smax;
+};
+
+__global__ __launch_bounds__(512) void heads_mfma_kernel(HeadArgsB a) {
+  __shared__ float part[8][16][17];
+  __shared__ float lg[2][16][MAXO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int e0 = blockIdx.x * 16;
+  const int el = lane & 15, q = lane >> 4;
+  for (int hd = 0; hd < a.nheads; ++hd) {
+    const int K = a.K[hd];
+    const int env = min(e0 + el, a.B - 1);
+    const bf16_t* xr = a.x[hd] + (size_t)env * K;
+    const bf16_t* wr = a.w[hd] + (size_t)el * K;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int nk = K / 32;
+    for (int s = wave; s < nk; s += 8) {
+      const int k = s * 32 + q * 8;
+      const bf16x8 av = *reinterpret_cast<const bf16x8*>(xr + k);
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + k);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+    }
+    // D[row = env 4q + i][col = output el]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[wave][4 * q + i][el] = acc[i];
+    __syncthreads();
+    if (tid < 256) {
+      const int e = tid >> 4, o = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v = v + part[w][e][o];
+      if (o < a.O[hd]) lg[hd][e][o] = v + a.bias[hd][o];
+    }
+    __syncthreads();
+  }
+  if (tid < 16 * a.nheads) {
+    const int hd = tid >> 4, e = tid & 15, b = e0 + e;
+    if (b < a.B) {
+      const int O = a.O[hd];
+      float l[MAXO];
+      for (int o = 0; o < O; ++o) {
+        l[o] = lg[hd][e][o];
+        if (a.logits[hd]) a.logits[hd][(size_t)b * O + o] = l[o];
+      }
+      if (a.decode[hd] == 0) {
+        float m = l[0];
+        for (int o = 1; o < O; ++o) m = fmaxf(m, l[o]);
+        float ex[MAXO], s = 0.f;
+        for (int o = 0; o < O; ++o) { ex[o] = expf(l[o] - m); s = s + ex[o]; }
+        for (int o = 0; o < O; ++o) a.dec[hd][(size_t)b * O + o] = ex[o] / s;
+      } else {
+        a.dec[hd][b] = decode_support(l, O, a.smin, a.smax);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// bf16 MFMA heads: x*: [B][K] bf16, w*: [16][K] bf16 (zero rows >= O), K % 32 == 0.
+int mzba_heads_bf16(int nheads, const void* x0, const void* w0, const float* b0, int K0, int O0, int dec0,
+                    float* logits0, float* out0, const void* x1, const void* w1, const float* b1, int K1, int O1,
+                    int dec1, float* logits1, float* out1, float smin, float smax, int B, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && nheads >= 1 && nheads <= 2 && O0 > 0 && O0 <= MAXO && K0 % 32 == 0, -1);
+  MZ_CHECK_ARG(nheads == 1 || (O1 > 0 && O1 <= MAXO && K1 % 32 == 0), -1);
+  HeadArgsB a{{(const bf16_t*)x0, (const bf16_t*)x1}, {(const bf16_t*)w0, (const bf16_t*)w1}, {b0, b1},
+              {logits0, logits1}, {out0, out1}, {K0, K1}, {O0, O1}, {dec0, dec1}, nheads, B, smin, smax};
+  hipLaunchKernelGGL(heads_mfma_kernel, dim3((B + 15) / 16), dim3(512), 0, stream, a);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
 
 // x*: [B][K] activations (dtype 0 f32 / 1 bf16); w*: [O][K] f32; decode 0 softmax, 1 support
 int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const float* b0, int K0, int O0, int dec0,

@@ -133,8 +133,13 @@ class PackedNets:
         O, K = w.shape
         hw = K // c
         wp = w.reshape(O, c, hw).transpose(0, 2, 1).reshape(O, K)
-        return {"w": torch.tensor(wp, dtype=torch.float32, device=self.device).contiguous(),
-                "b": torch.tensor(b, dtype=torch.float32, device=self.device), "K": K, "O": O}
+        lin = {"w": torch.tensor(wp, dtype=torch.float32, device=self.device).contiguous(),
+               "b": torch.tensor(b, dtype=torch.float32, device=self.device), "K": K, "O": O}
+        if self.dtype == "bf16" and K % 32 == 0 and O <= 16:
+            wb = np.zeros((16, K))
+            wb[:O] = wp
+            lin["wb"] = torch.tensor(wb, dtype=torch.float32).to(torch.bfloat16).to(self.device).contiguous()
+        return lin
 
 
 class NetRunner:
@@ -229,9 +234,14 @@ class NetRunner:
             self.resblock(blk, self.x, self.t, self.x, B, H, W)
         self.conv(self.x, p.rew_conv, self.rc, B, H, W, relu=True)
         rl = p.rew_lin
-        L.call("mzba_heads", self.dt, 1, L.ptr(self.rc), L.ptr(rl["w"]), L.ptr(rl["b"]), rl["K"], rl["O"], 1,
-               L.ptr(r_logits), L.ptr(r_dec), None, None, None, 0, 0, 0, None, None,
-               float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B, L.stream())
+        if "wb" in rl:
+            L.call("mzba_heads_bf16", 1, L.ptr(self.rc), L.ptr(rl["wb"]), L.ptr(rl["b"]), rl["K"], rl["O"], 1,
+                   L.ptr(r_logits), L.ptr(r_dec), None, None, None, 0, 0, 0, None, None,
+                   float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B, L.stream())
+        else:
+            L.call("mzba_heads", self.dt, 1, L.ptr(self.rc), L.ptr(rl["w"]), L.ptr(rl["b"]), rl["K"], rl["O"], 1,
+                   L.ptr(r_logits), L.ptr(r_dec), None, None, None, 0, 0, 0, None, None,
+                   float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B, L.stream())
         n = H * W * p.c1
         L.call("mzba_scale_state", self.dt, L.ptr(self.x), L.ptr(out_latent), L.ptr(pool), pool_env_stride, None,
                pool_slot, n, B, n, L.stream())
@@ -247,6 +257,12 @@ class NetRunner:
         self.conv(cur, p.pol_conv, self.pc, B, H, W, relu=True)
         self.conv(cur, p.val_conv, self.vc, B, H, W, relu=True)
         pl, vl = p.pol_lin, p.val_lin
+        if "wb" in pl and "wb" in vl:
+            L.call("mzba_heads_bf16", 2, L.ptr(self.pc), L.ptr(pl["wb"]), L.ptr(pl["b"]), pl["K"], pl["O"], 0,
+                   L.ptr(p_logits), L.ptr(pi), L.ptr(self.vc), L.ptr(vl["wb"]), L.ptr(vl["b"]), vl["K"], vl["O"], 1,
+                   L.ptr(v_logits), L.ptr(v), float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B,
+                   L.stream())
+            return
         L.call("mzba_heads", self.dt, 2, L.ptr(self.pc), L.ptr(pl["w"]), L.ptr(pl["b"]), pl["K"], pl["O"], 0,
                L.ptr(p_logits), L.ptr(pi), L.ptr(self.vc), L.ptr(vl["w"]), L.ptr(vl["b"]), vl["K"], vl["O"], 1,
                L.ptr(v_logits), L.ptr(v), float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B,
