@@ -84,6 +84,8 @@ int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_
  * followed by 8*64*8 padding elements (the weight ring prefetches 8 k steps past the end; see
  * DESIGN.md §conv_lat); a workgroup keeps E = 160/(H*W) envs' activations in LDS. */
 int mzba_conv_lat_supported(int H, int W, int Cin, int Cout, int ks);
+/* Kernel shape selection for A/B experiments (0 = default 8-wave kernel, 1 = 4-wave 2-tile kernel). */
+int mzba_conv_lat_set_variant(int v);
 int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                   const void* wf, const float* bias, const float* act_bias, const int32_t* act, int A,
                   const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,

@@ -24,6 +24,22 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 constexpr int R = 5;          // 32-row tiles per workgroup (E*HW <= 160)
+
+#ifdef MZ_LAT_STAMPS
+// diagnostic build only (libmzba_diag.so, tools/stamp_conv.py): per-workgroup phase stamps
+__device__ unsigned long long mz_lat_stamps[4096][8];
+#define MZ_STAMP(k)                                                                        \
+  do {                                                                                     \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x + gridDim.x * blockIdx.y < 4096) {           \
+      const int w_ = threadIdx.x >> 6;                                                     \
+      if (w_ == 0 || (k == 3 && w_ == 4))                                                  \
+        mz_lat_stamps[blockIdx.x + gridDim.x * blockIdx.y][(k == 3 && w_ == 4) ? 7 : k] =  \
+            __builtin_amdgcn_s_memtime();                                                  \
+    }                                                                                      \
+  } while (0)
+#else
+#define MZ_STAMP(k) do {} while (0)
+#endif
 constexpr int MAXROWS = 32 * R;
 
 struct LatArgs {
@@ -41,17 +57,89 @@ struct LatArgs {
   int B, H, W, Cin, Cout, ks, relu, E;
 };
 
-template <int KS, int CIN>
-__global__ __launch_bounds__(512, 2) void conv_lat_kernel(LatArgs a) {
+// epilogue: (1) issue the residual loads (16 B per lane) so they land while the f32 tile is
+// reduced through LDS; (2) finish 16-B output chunks: + residual, ReLU, bf16, 16-B stores.
+// Bias and the per-(pixel, action) bias were folded into the accumulator init.
+constexpr int EPT_MAX = 10;
+template <int NT>
+__device__ __forceinline__ void lat_res_prefetch(const LatArgs& a, uint4 (&rv)[EPT_MAX], int rows, int env0, int HW,
+                                                 int tid) {
+  constexpr int EPT = (MAXROWS * 16 + NT - 1) / NT;
+  const int ncols = min(128, a.Cout - blockIdx.y * 128);
+  const int ncb = ncols / 8;
+  const int nchunks = rows * ncb;
+  if (a.res) {
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      int i = u * NT + tid;
+      i = i < nchunks ? i : 0;
+      const int row = i / ncb, cc = i - (i / ncb) * ncb;
+      const long long m = (long long)env0 * HW + row;
+      rv[u] = *reinterpret_cast<const uint4*>(a.res + m * a.Cout + blockIdx.y * 128 + cc * 8);
+    }
+  }
+}
+template <int NT>
+__device__ __forceinline__ void lat_epilogue(const LatArgs& a, const float* ot, const uint4 (&rv)[EPT_MAX], int rows,
+                                             int env0, int HW, int tid) {
+  constexpr int EPT = (MAXROWS * 16 + NT - 1) / NT;
+  const int ncols = min(128, a.Cout - blockIdx.y * 128);
+  const int ncb = ncols / 8;
+  const int nchunks = rows * ncb;
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int i = u * NT + tid;
+    if (i >= nchunks) break;
+    const int row = i / ncb, cc = i - (i / ncb) * ncb;
+    const long long m = (long long)env0 * HW + row;
+    const int n0 = blockIdx.y * 128 + cc * 8;
+    float v[8];
+    const float4 x0 = *reinterpret_cast<const float4*>(ot + row * 128 + cc * 8);
+    const float4 x1 = *reinterpret_cast<const float4*>(ot + row * 128 + cc * 8 + 4);
+    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+    if (a.res) {
+      const uint32_t w[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = v[j] + bf16_to_f32((bf16_t)(w[j >> 1] >> (16 * (j & 1))));
+    }
+    if (a.relu) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    uint4 o;
+    o.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+    o.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+    o.z = (uint32_t)f32_to_bf16(v[4]) | ((uint32_t)f32_to_bf16(v[5]) << 16);
+    o.w = (uint32_t)f32_to_bf16(v[6]) | ((uint32_t)f32_to_bf16(v[7]) << 16);
+    *reinterpret_cast<uint4*>(a.out + m * a.Cout + n0) = o;
+  }
+}
+
+// accumulator init for the first channel group: bias (+ per-(pixel, action) bias) of this
+// lane's (row, col) elements, so the epilogue only adds the residual.
+__device__ __forceinline__ float lat_acc_init(const LatArgs& a, float bias_n, int row, int rows, int n, int env0,
+                                              int HW) {
+  float v = bias_n;
+  if (a.act_bias) {
+    const int rr = row < rows ? row : 0;
+    const int e = rr / HW, p = rr - e * HW;
+    v = a.act_bias[((long long)p * a.A + a.act[env0 + e]) * a.Cout + n] + v;
+  }
+  return v;
+}
+
+template <int KS, int CIN, int WAVES, int DMAX>
+__global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs a) {
+  constexpr int KSPLIT = WAVES / 4;      // channel groups per tap (1: 4 waves, 2: 8 waves)
   constexpr int NC = CIN / 16;           // k steps per tap
-  constexpr int NH = NC / 2;             // k steps per tap per wave (channel half)
+  constexpr int NH = NC / KSPLIT;        // k steps per tap per wave
   constexpr int NSW = KS * KS * NH;      // k steps per wave
-  constexpr int D = NH >= 8 ? 8 : NH;    // weight ring depth (k steps in flight)
+  constexpr int D = NH >= DMAX ? DMAX : NH;  // weight ring depth (k steps in flight)
   constexpr int ROWB = CIN * 2;          // bytes per LDS row
   constexpr int NCHUNK = CIN / 8;        // 16-B chunks per row
   constexpr int SMASK = NCHUNK >= 16 ? 15 : NCHUNK - 1;
   constexpr int PAD = KS / 2;
-  constexpr int NT = 512;
+  constexpr int NT = 64 * WAVES;
   static_assert(NH % D == 0, "ring / tap alignment");
   constexpr int LDS_A = (MAXROWS + 1) * ROWB, LDS_C = MAXROWS * 128 * 4;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_A > LDS_C ? LDS_A : LDS_C];
@@ -61,15 +149,17 @@ __global__ __launch_bounds__(512, 2) void conv_lat_kernel(LatArgs a) {
   const int nenv = min(a.E, a.B - env0);
   const int rows = nenv * HW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wq = wave & 3, kh = wave >> 2;  // 32-column slot, channel half
+  const int wq = wave & 3, kh = wave >> 2;  // 32-column slot, channel group
   const int ct = blockIdx.y * 4 + wq;        // this wave's 32-column tile
   const bool active = ct * 32 < a.Cout;
   // weight stream first (latency hides under the staging); wf[ct][kh][step][lane][8] is
   // contiguous per wave and padded by 8 steps, so every ring load is unconditional.
-  const uint4* wp = reinterpret_cast<const uint4*>(a.wf) + ((size_t)(active ? ct : 0) * 2 + kh) * NSW * 64 + lane;
+  MZ_STAMP(0);
+  const uint4* wp = reinterpret_cast<const uint4*>(a.wf) + ((size_t)(active ? ct : 0) * KSPLIT + kh) * NSW * 64 + lane;
   uint4 bq[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) bq[i] = wp[(size_t)i * 64];
+  const float bias_n = a.bias[active ? ct * 32 + (lane & 31) : 0];  // lands during the staging
 
   // per-env source base (slot gather resolved once, so the staging loads are branch-free)
   if (tid < a.E) {
@@ -104,13 +194,17 @@ __global__ __launch_bounds__(512, 2) void conv_lat_kernel(LatArgs a) {
     }
   }
   __syncthreads();
+  MZ_STAMP(1);
 
   const int l32 = lane & 31, h = lane >> 5;
   f32x16 acc[R];
 #pragma unroll
   for (int rt = 0; rt < R; ++rt)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[rt][i] = 0.f;
+    for (int i = 0; i < 16; ++i)
+      acc[rt][i] = (active && kh == 0) ? lat_acc_init(a, bias_n, rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h, rows,
+                                                     ct * 32 + l32, env0, HW)
+                                       : 0.f;
   if (active) {
     int ry[R], rx[R], rbase[R];
     bool rval[R];
@@ -135,7 +229,7 @@ __global__ __launch_bounds__(512, 2) void conv_lat_kernel(LatArgs a) {
         sw[rt] = (r & SMASK) << 4;
       }
     };
-    const int cbase = kh * NC + h;  // 16-B chunk of this lane's 8 channels at step 0 of a tap
+    const int cbase = kh * (2 * NH) + h;  // 16-B chunk of this lane's 8 channels at step 0 of a tap
     int offc[R], swc[R], offn[R], swn[R];
     tap_rows(0, offc, swc);
     bf16x8 afc[R], afn[R];
@@ -143,28 +237,43 @@ __global__ __launch_bounds__(512, 2) void conv_lat_kernel(LatArgs a) {
     for (int rt = 0; rt < R; ++rt)
       afc[rt] = *reinterpret_cast<const bf16x8*>(lds + offc[rt] + ((cbase << 4) ^ swc[rt]));
     for (int tap = 0; tap < KS * KS; ++tap) {
-      if (tap + 1 < KS * KS) tap_rows(tap + 1, offn, swn);
+      // next tap's source rows (the last tap re-reads its own rows: harmless, branch-free)
+      tap_rows(tap + 1 < KS * KS ? tap + 1 : tap, offn, swn);
 #pragma unroll
       for (int c = 0; c < NH; ++c) {
         const int s = tap * NH + c;
         const uint4 bcur = bq[c % D];
+#if defined(MZ_LAT_ABLATE) && MZ_LAT_ABLATE == 1
+        bq[c % D] = wp[(size_t)((s + D) & 7) * 64];  // ablation: weights from an 8-step (8 KB) hot window
+#else
         bq[c % D] = wp[(size_t)(s + D) * 64];
-        // prefetch the next k step's A fragments (the next tap's rows after the last step)
-        if (c + 1 < NH) {
-          const int cb = (cbase + 2 * (c + 1)) << 4;
-#pragma unroll
-          for (int rt = 0; rt < R; ++rt) afn[rt] = *reinterpret_cast<const bf16x8*>(lds + offc[rt] + (cb ^ swc[rt]));
-        } else if (tap + 1 < KS * KS) {
-#pragma unroll
-          for (int rt = 0; rt < R; ++rt)
-            afn[rt] = *reinterpret_cast<const bf16x8*>(lds + offn[rt] + ((cbase << 4) ^ swn[rt]));
-        }
-        // pin the order: next-step reads + weight load in flight while this step's MFMAs run
-        __builtin_amdgcn_sched_barrier(0);
+#endif
         const bf16x8 bfr = __builtin_bit_cast(bf16x8, bcur);
+        // MFMA on this step's fragment, then issue the next step's read of the same row tile:
+        // it has the 4 following MFMAs (~128 cycles) to land.
 #pragma unroll
-        for (int rt = 0; rt < R; ++rt)
+        for (int rt = 0; rt < R; ++rt) {
+#if defined(MZ_LAT_ABLATE) && MZ_LAT_ABLATE == 3
+          asm volatile("" ::"v"(afc[rt]), "v"(bfr));  // ablation: no MFMA
+#else
           acc[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[rt], bfr, acc[rt], 0, 0, 0);
+#endif
+#if !(defined(MZ_LAT_ABLATE) && MZ_LAT_ABLATE == 2)
+          if (c + 1 < NH)
+            afn[rt] = *reinterpret_cast<const bf16x8*>(lds + offc[rt] + (((cbase + 2 * (c + 1)) << 4) ^ swc[rt]));
+          else
+            afn[rt] = *reinterpret_cast<const bf16x8*>(lds + offn[rt] + ((cbase << 4) ^ swn[rt]));
+#endif
+        }
+        // interleave {MFMA, DS read, VALU} x R, then the weight load; the reads' consumers are
+        // behind the step barrier, so no MFMA waits on a read issued in its own step
+#pragma unroll
+        for (int rt = 0; rt < R; ++rt) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int rt = 0; rt < R; ++rt) afc[rt] = afn[rt];
@@ -177,7 +286,11 @@ __global__ __launch_bounds__(512, 2) void conv_lat_kernel(LatArgs a) {
   // ---- epilogue, staged through LDS: channel-half 0 writes its f32 partial tile, half 1
   // adds its own (each element owned by one lane), then every lane finishes 16-B chunks:
   // + bias (+ act bias) (+ residual, 16-B loads), ReLU, bf16, 16-B stores.
+  MZ_STAMP(3);
+  uint4 rv[EPT_MAX];
+  lat_res_prefetch<NT>(a, rv, rows, env0, HW, tid);
   __syncthreads();  // every wave is done reading the A tile
+  MZ_STAMP(4);
   float* ot = reinterpret_cast<float*>(lds);
   if (active && kh == 0) {
 #pragma unroll
@@ -186,7 +299,7 @@ __global__ __launch_bounds__(512, 2) void conv_lat_kernel(LatArgs a) {
       for (int r = 0; r < 16; ++r) ot[(rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 128 + wq * 32 + l32] = acc[rt][r];
   }
   __syncthreads();
-  if (active && kh == 1) {
+  if (active && kh == 1 && KSPLIT == 2) {
 #pragma unroll
     for (int rt = 0; rt < R; ++rt)
 #pragma unroll
@@ -196,61 +309,207 @@ __global__ __launch_bounds__(512, 2) void conv_lat_kernel(LatArgs a) {
       }
   }
   __syncthreads();
-  const int ncols = min(128, a.Cout - blockIdx.y * 128);
-  const int ncb = ncols / 8;  // 16-B chunks per output row
-  const int nchunks = rows * ncb;
-  constexpr int EPT = (MAXROWS * 16 + NT - 1) / NT;  // chunks per thread (upper bound)
-  uint4 rv[EPT];
-  if (a.res) {
+  lat_epilogue<NT>(a, ot, rv, rows, env0, HW, tid);
+  MZ_STAMP(5);
+}
+
+// Variant with 2 column tiles per wave: 4 waves = 2 column halves (64 channels each) x 2
+// channel halves of every tap, one wave per SIMD (512-register budget). Each A fragment read
+// from LDS feeds 2 MFMAs (half the LDS traffic per FLOP of conv_lat_kernel). Same weight
+// packing as the 8-wave kernel (pack_lat ksplit=2).
+template <int KS, int CIN>
+__global__ __launch_bounds__(256, 1) void conv_lat2_kernel(LatArgs a) {
+  constexpr int NC = CIN / 16;
+  constexpr int NH = NC / 2;             // k steps per tap per wave
+  constexpr int NSW = KS * KS * NH;      // k steps per wave
+  constexpr int D = NH >= 8 ? 8 : NH;    // ring depth per column tile
+  constexpr int ROWB = CIN * 2;
+  constexpr int NCHUNK = CIN / 8;
+  constexpr int SMASK = NCHUNK >= 16 ? 15 : NCHUNK - 1;
+  constexpr int PAD = KS / 2;
+  constexpr int NT = 256;
+  static_assert(NH % D == 0, "ring / tap alignment");
+  constexpr int LDS_A = (MAXROWS + 1) * ROWB, LDS_C = MAXROWS * 128 * 4;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_A > LDS_C ? LDS_A : LDS_C];
+  __shared__ long long envoff[32 * R];
+  const int HW = a.H * a.W;
+  const int env0 = blockIdx.x * a.E;
+  const int nenv = min(a.E, a.B - env0);
+  const int rows = nenv * HW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cw = wave & 1, kh = wave >> 1;          // column half (2 tiles), channel half
+  const int ct0 = blockIdx.y * 4 + 2 * cw;           // first of this wave's two 32-column tiles
+  const bool act0 = ct0 * 32 < a.Cout, act1 = (ct0 + 1) * 32 < a.Cout;
+  MZ_STAMP(0);
+  const uint4* wp0 = reinterpret_cast<const uint4*>(a.wf) + ((size_t)(act0 ? ct0 : 0) * 2 + kh) * NSW * 64 + lane;
+  const uint4* wp1 = reinterpret_cast<const uint4*>(a.wf) + ((size_t)(act1 ? ct0 + 1 : 0) * 2 + kh) * NSW * 64 + lane;
+  uint4 bq0[D], bq1[D];
 #pragma unroll
-    for (int u = 0; u < EPT; ++u) {
-      int i = u * NT + tid;
-      i = i < nchunks ? i : 0;
-      const int row = i / ncb, cc = i - (i / ncb) * ncb;
-      const long long m = (long long)env0 * HW + row;
-      rv[u] = *reinterpret_cast<const uint4*>(a.res + m * a.Cout + blockIdx.y * 128 + cc * 8);
+  for (int i = 0; i < D; ++i) { bq0[i] = wp0[(size_t)i * 64]; bq1[i] = wp1[(size_t)i * 64]; }
+  const float bias0 = a.bias[act0 ? ct0 * 32 + (lane & 31) : 0], bias1 = a.bias[act1 ? ct0 * 32 + 32 + (lane & 31) : 0];
+
+  if (tid < a.E) {
+    const int b = env0 + (tid < nenv ? tid : 0);
+    long long off = (long long)b * a.in_env_stride;
+    if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
+    envoff[tid] = off;
+  }
+  __syncthreads();
+  constexpr int TOTAL = (MAXROWS + 1) * NCHUNK;
+  constexpr int PER = (TOTAL + NT - 1) / NT;
+  constexpr int BATCH = PER < 11 ? PER : 11;
+#pragma unroll
+  for (int base = 0; base < PER; base += BATCH) {
+    uint4 v[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int i = (base + u) * NT + tid;
+      const int r = i / NCHUNK, c = i % NCHUNK;
+      const bool ok = base + u < PER && i < TOTAL && r < rows;
+      const int rr = ok ? r : 0;
+      const int e = rr / HW, p = rr - (rr / HW) * HW;
+      v[u] = *reinterpret_cast<const uint4*>(a.in + envoff[e] + (long long)p * CIN + c * 8);
+      if (!ok) v[u] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int i = (base + u) * NT + tid;
+      if (base + u < PER && i < TOTAL) {
+        const int r = i / NCHUNK, c = i % NCHUNK;
+        *reinterpret_cast<uint4*>(lds + r * ROWB + ((c ^ (r & SMASK)) << 4)) = v[u];
+      }
     }
   }
+  __syncthreads();
+  MZ_STAMP(1);
+
+  const int l32 = lane & 31, h = lane >> 5;
+  f32x16 acc0[R], acc1[R];
 #pragma unroll
-  for (int u = 0; u < EPT; ++u) {
-    const int i = u * NT + tid;
-    if (i >= nchunks) break;
-    const int row = i / ncb, cc = i - (i / ncb) * ncb;
-    const long long m = (long long)env0 * HW + row;
-    const int n0 = blockIdx.y * 128 + cc * 8;
-    float v[8];
-    const float4 x0 = *reinterpret_cast<const float4*>(ot + row * 128 + cc * 8);
-    const float4 x1 = *reinterpret_cast<const float4*>(ot + row * 128 + cc * 8 + 4);
-    v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-    if (a.act_bias) {
-      const int e = row / HW, p = row - e * HW;
-      const float* ab = a.act_bias + ((long long)p * a.A + a.act[env0 + e]) * a.Cout + n0;
+  for (int rt = 0; rt < R; ++rt)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = v[j] + ab[j];
+    for (int i = 0; i < 16; ++i) {
+      const int row = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
+      acc0[rt][i] = (act0 && kh == 0) ? lat_acc_init(a, bias0, row, rows, ct0 * 32 + (lane & 31), env0, HW) : 0.f;
+      acc1[rt][i] = (act1 && kh == 0) ? lat_acc_init(a, bias1, row, rows, ct0 * 32 + 32 + (lane & 31), env0, HW) : 0.f;
     }
+  {
+    int ry[R], rx[R], rbase[R];
+    bool rval[R];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = v[j] + a.bias[n0 + j];
-    if (a.res) {
-      const uint32_t w[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = v[j] + bf16_to_f32((bf16_t)(w[j >> 1] >> (16 * (j & 1))));
+    for (int rt = 0; rt < R; ++rt) {
+      const int m = rt * 32 + l32;
+      rval[rt] = m < rows;
+      const int e = m / HW, p = m - (m / HW) * HW;
+      ry[rt] = p / a.W;
+      rx[rt] = p - ry[rt] * a.W;
+      rbase[rt] = e * HW;
     }
-    if (a.relu) {
+    auto tap_rows = [&](int tap, int (&off)[R], int (&sw)[R]) {
+      const int ky = tap / KS - PAD, kx = tap % KS - PAD;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+      for (int rt = 0; rt < R; ++rt) {
+        const int sy = ry[rt] + ky, sx = rx[rt] + kx;
+        const bool ok = rval[rt] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
+        const int r = ok ? rbase[rt] + sy * a.W + sx : MAXROWS;
+        off[rt] = r * ROWB;
+        sw[rt] = (r & SMASK) << 4;
+      }
+    };
+    const int cbase = kh * (2 * NH) + h;
+    int offc[R], swc[R], offn[R], swn[R];
+    tap_rows(0, offc, swc);
+    bf16x8 afc[R], afn[R];
+#pragma unroll
+    for (int rt = 0; rt < R; ++rt)
+      afc[rt] = *reinterpret_cast<const bf16x8*>(lds + offc[rt] + ((cbase << 4) ^ swc[rt]));
+    for (int tap = 0; tap < KS * KS; ++tap) {
+      tap_rows(tap + 1 < KS * KS ? tap + 1 : tap, offn, swn);
+#pragma unroll
+      for (int c = 0; c < NH; ++c) {
+        const int s = tap * NH + c;
+        const bf16x8 b0 = __builtin_bit_cast(bf16x8, bq0[c % D]);
+        const bf16x8 b1 = __builtin_bit_cast(bf16x8, bq1[c % D]);
+        bq0[c % D] = wp0[(size_t)(s + D) * 64];
+        bq1[c % D] = wp1[(size_t)(s + D) * 64];
+#pragma unroll
+        for (int rt = 0; rt < R; ++rt) {
+          acc0[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[rt], b0, acc0[rt], 0, 0, 0);
+          acc1[rt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afc[rt], b1, acc1[rt], 0, 0, 0);
+          if (c + 1 < NH)
+            afn[rt] = *reinterpret_cast<const bf16x8*>(lds + offc[rt] + (((cbase + 2 * (c + 1)) << 4) ^ swc[rt]));
+          else
+            afn[rt] = *reinterpret_cast<const bf16x8*>(lds + offn[rt] + ((cbase << 4) ^ swn[rt]));
+        }
+#pragma unroll
+        for (int rt = 0; rt < R; ++rt) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int rt = 0; rt < R; ++rt) afc[rt] = afn[rt];
+      }
+#pragma unroll
+      for (int rt = 0; rt < R; ++rt) { offc[rt] = offn[rt]; swc[rt] = swn[rt]; }
     }
-    uint4 o;
-    o.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
-    o.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
-    o.z = (uint32_t)f32_to_bf16(v[4]) | ((uint32_t)f32_to_bf16(v[5]) << 16);
-    o.w = (uint32_t)f32_to_bf16(v[6]) | ((uint32_t)f32_to_bf16(v[7]) << 16);
-    *reinterpret_cast<uint4*>(a.out + m * a.Cout + n0) = o;
   }
+
+  MZ_STAMP(3);
+  uint4 rv[EPT_MAX];
+  lat_res_prefetch<NT>(a, rv, rows, env0, HW, tid);
+  __syncthreads();
+  MZ_STAMP(4);
+  float* ot = reinterpret_cast<float*>(lds);
+  const int col0 = cw * 64 + l32;
+  if (kh == 0) {
+#pragma unroll
+    for (int rt = 0; rt < R; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        ot[row * 128 + col0] = acc0[rt][r];
+        ot[row * 128 + col0 + 32] = acc1[rt][r];
+      }
+  }
+  __syncthreads();
+  if (kh == 1) {
+#pragma unroll
+    for (int rt = 0; rt < R; ++rt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        ot[row * 128 + col0] += acc0[rt][r];
+        ot[row * 128 + col0 + 32] += acc1[rt][r];
+      }
+  }
+  __syncthreads();
+  lat_epilogue<NT>(a, ot, rv, rows, env0, HW, tid);
+  MZ_STAMP(5);
 }
 
 }  // namespace
 
+static int g_lat_variant = 0;  // kernel shape (experiments): see mzba_conv_lat_set_variant
+
 extern "C" {
+
+// 0: 8 waves (2 per SIMD: 4 column tiles x 2 channel halves), the default;
+// 1: 4 waves with 2 column tiles each (conv_lat2_kernel, experiment). Same weight packing.
+int mzba_conv_lat_set_variant(int v) {
+  if (v < 0 || v > 1) return -1;
+  g_lat_variant = v;
+  return 0;
+}
+
+#ifdef MZ_LAT_STAMPS
+int mzba_lat_stamps_read(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mz_lat_stamps), sizeof(unsigned long long) * 8 * n);
+}
+#endif
 
 int mzba_conv_lat_supported(int H, int W, int Cin, int Cout, int ks) {
   const int HW = H * W;
@@ -271,9 +530,17 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
   LatArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (const bf16_t*)wf, bias, act_bias, act, A,
             (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, relu, E};
   dim3 grid((B + E - 1) / E, (Cout + 127) / 128);
-#define MZ_LAT(KS_, CIN_) \
-  if (ks == KS_ && Cin == CIN_) { hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_>), grid, dim3(512), 0, stream, a); }
-  MZ_LAT(3, 256) else MZ_LAT(1, 256) else MZ_LAT(3, 128) else MZ_LAT(1, 128) else MZ_LAT(3, 64) else MZ_LAT(1, 64)
+  const int v = g_lat_variant;
+#define MZ_LAT(KS_, CIN_, W_, D_) \
+  if (ks == KS_ && Cin == CIN_) { hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, W_, D_>), grid, dim3(64 * W_), 0, stream, a); }
+  if (v == 1) {
+    if (ks == 3 && Cin == 256) hipLaunchKernelGGL((conv_lat2_kernel<3, 256>), grid, dim3(256), 0, stream, a);
+    else if (ks == 1 && Cin == 256) hipLaunchKernelGGL((conv_lat2_kernel<1, 256>), grid, dim3(256), 0, stream, a);
+    else return -4;
+  } else {
+    MZ_LAT(3, 256, 8, 8) else MZ_LAT(1, 256, 8, 8) else MZ_LAT(3, 128, 8, 8) else MZ_LAT(1, 128, 8, 8)
+    else MZ_LAT(3, 64, 8, 8) else MZ_LAT(1, 64, 8, 8)
+  }
 #undef MZ_LAT
   MZ_LAUNCH_CHECK();
   return 0;

@@ -30,6 +30,7 @@ SIGNATURES = {
     "mzba_build_rep_input": [P, P, P, P, I, P, I, I, I, I, P],
     "mzba_conv2d": [I, P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
     "mzba_conv_lat_supported": [I, I, I, I, I],
+    "mzba_conv_lat_set_variant": [I],
     "mzba_conv_lat": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
     "mzba_avgpool2": [I, P, P, I, I, I, I, P],
     "mzba_scale_state": [I, P, P, P, LL, P, I, LL, I, I, P],
