@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-envs", type=int, default=16, help="bounded oracle sample (cpu_baseline + match rate)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
     return ap.parse_args()
 
 
@@ -75,12 +76,12 @@ def main():
     loop.reset(0)
     last_flush = [0]
 
-    def one_step():
+    def one_step(eager=False):
         if loop.t >= loop.max_steps or (loop.t > 0 and loop.all_done()):
             flush()
             loop.reset()
             last_flush[0] = 0
-        loop.act()
+        loop.act(eager=eager)
         if loop.t - last_flush[0] >= RECORD_K:
             flush()
 
@@ -90,7 +91,9 @@ def main():
             last_flush[0] = loop.t
 
     for _ in range(args.warmup):
-        one_step()
+        one_step(eager=True)
+    if not args.no_graph:
+        loop.capture()  # one acting step (~S x 65 launches) as a HIP graph, replayed per step
 
     # ---- visit-count match + CPU baseline on a bounded sample (rank 0, N=1 only) -------
     cpu_info, match = None, None
@@ -129,8 +132,11 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        runner.probe = probe if i == args.steps // 2 else None
-        one_step()
+        # the middle step runs eagerly with HIP events around every latent residual conv
+        # (the dominant kernel) to measure its launch duration live inside the timed region
+        probe_step = i == args.steps // 2
+        runner.probe = probe if probe_step else None
+        one_step(eager=probe_step)
     flush()
     if world > 1:
         dist.barrier()
@@ -178,6 +184,7 @@ def main():
                          "avg_launch_ms": conv_ms, "launches_timed": len(probe)},
             "cpu_baseline": cpu_info,
             "visit_count_match": match,
+            "launch": "eager" if args.no_graph else "hip-graph replay (probe step eager)",
             "whole_step_mfma_frac": (B * world * (3.4446e9 + 0.6738e9 + args.sims * 1.3610e9) * args.steps / dt / 1e12)
                                     / (PEAK_BF16_TFLOPS * world),
         }

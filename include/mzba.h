@@ -47,13 +47,15 @@ int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* d
 
 /* One acting-loop env step (train_torch.py:201-209): step, render the u8 gray frame, push
  * (action, frame) into the history ring when the env is recorded (not prev_done; at the first
- * step prev_done aliases done, :179), and write the trajectory-sink row (rec_* may be NULL). */
+ * step prev_done aliases done, :179), and write the trajectory-sink row (rec_* may be NULL).
+ * ctx (optional, graph replay): device int32[3] step context; when given, the sink row is
+ * ctx[2] (rec_* are the (T,B,..) bases) and first_step = (ctx[2] == 0). */
 int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
                           uint64_t* bricks, int nw, const int64_t* action, float* reward, float* valid,
                           uint8_t* cur_frame, uint8_t* hist_frames, uint8_t* hist_actions, int32_t* hist_len, int L,
                           uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
                           int first_step, int B, int H, int W, int paddle_width, int brick_rows,
-                          const float* rewards4, hipStream_t stream);
+                          const float* rewards4, const int32_t* ctx, hipStream_t stream);
 
 /* compact -> reference planes (B,3,H,W) f32. */
 int mzba_compact_to_planes(const int32_t* paddle, const int32_t* bx, const int32_t* by, const uint8_t* done,
@@ -114,7 +116,9 @@ int mzba_heads_bf16(int nheads, const void* x0, const void* w0, const float* b0,
                     int dec1, float* logits1, float* out1, float smin, float smax, int B, hipStream_t stream);
 
 /* ---- latent MCTS (src/mcts.py:MCTSSearchVec) ------------------------------------------- */
-/* Tree buffers (device): nodes [B][S+1] x mzba_mcts_node_bytes(), root_sum f32[B], calls u32[B],
+/* Every tree entry point takes an optional device step context ctx (int32[3]: search id, step
+ * index, episode row); when non-NULL its ctx[0] replaces search_id, so one captured HIP graph
+ * replays every search. Tree buffers (device): nodes [B][S+1] x mzba_mcts_node_bytes(), root_sum f32[B], calls u32[B],
  * leaf_parent/leaf_action/depth i32[B], path i32[B][S+1]; sqrt_tab/c_tab f32[S+1] =
  * f32(sqrt(n)), f32(c1 + log((n+c2+1)/c2)) computed in double on the host (mcts.py:285-289). */
 int mzba_mcts_node_bytes(void);
@@ -123,31 +127,39 @@ int mzba_mcts_node_bytes(void);
  * noise = noise_in or Dirichlet(alpha) from Philox stream 2 (written to noise_out), first ucb_action. */
 int mzba_mcts_root(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
                    int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
-                   int env_offset, int search_id, uint64_t seed, const float* v_root, const float* pi_root,
+                   int env_offset, int search_id, uint64_t seed, const int32_t* ctx, const float* v_root, const float* pi_root,
                    const float* noise_in, float* noise_out, float w_pol, float w_noise, float alpha,
                    hipStream_t stream);
 
 /* _select_nodes (mcts.py:136-182) for simulation sim >= 1 (ucb_action :281-298). */
 int mzba_mcts_select(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
                      int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
-                     int env_offset, int search_id, uint64_t seed, int sim, hipStream_t stream);
+                     int env_offset, int search_id, uint64_t seed, const int32_t* ctx, int sim, hipStream_t stream);
 
 /* _backup (mcts.py:203-234) with decoded r[B], v[B], pi[B][3] of the expanded leaves. */
 int mzba_mcts_backup(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
                      int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
-                     int env_offset, int search_id, uint64_t seed, int sim, const float* r, const float* v,
+                     int env_offset, int search_id, uint64_t seed, const int32_t* ctx, int sim, const float* r, const float* v,
                      const float* pi, float gamma, hipStream_t stream);
 
 /* _compute_results (mcts.py:236-250): counts i64[B][3], values f32[B] = f32(double(root_sum)/S). */
 int mzba_mcts_results(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
                       int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
-                      int env_offset, int search_id, uint64_t seed, int64_t* counts, float* values,
+                      int env_offset, int search_id, uint64_t seed, const int32_t* ctx, int64_t* counts, float* values,
                       hipStream_t stream);
 
 /* Temperature sampling (train_torch.py:191-198): p = counts^(1/T)/sum, inverse CDF of
  * u = Philox uniform(env+env_offset, stream 3, step, 0). */
 int mzba_sample_actions(const int64_t* counts, int64_t* action, int B, float temperature, int env_offset, int step,
-                        uint64_t seed, hipStream_t stream);
+                        uint64_t seed, const int32_t* ctx, hipStream_t stream);
+
+/* Trajectory-sink row of the search results: rec_counts[t][b] = counts[b], rec_values[t][b] = values[b],
+ * t = ctx ? ctx[2] : t (replay_buffer.py:17-35 visit_counts / values). */
+int mzba_record_results(const int64_t* counts, const float* values, int64_t* rec_counts, float* rec_values, int B,
+                        int t, const int32_t* ctx, hipStream_t stream);
+
+/* ctx[0..2] += 1 (end of one captured acting step). */
+int mzba_ctx_advance(int32_t* ctx, hipStream_t stream);
 
 #ifdef __cplusplus
 }

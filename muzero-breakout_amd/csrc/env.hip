@@ -205,8 +205,16 @@ __global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_f
 template <int MAXW>
 __global__ __launch_bounds__(256) void env_step_compact_kernel(
     Compact cs, const int64_t* __restrict__ action, float* __restrict__ reward, float* __restrict__ valid,
-    uint8_t* __restrict__ cur_frame, History hist, Sink sink, int first_step, int B, int H, int W, int pw,
-    int brick_rows, RewardCfg rc) {
+    uint8_t* __restrict__ cur_frame, History hist, Sink sink, int first_step_arg, int B, int H, int W, int pw,
+    int brick_rows, RewardCfg rc, const int32_t* __restrict__ ctx) {
+  // graph replay: the episode row t comes from the device context; the sink pointers are the
+  // (T, B, ...) bases and row t is selected here; t == 0 is the first step
+  const int first_step = ctx ? (ctx[2] == 0) : first_step_arg;
+  if (ctx) {
+    const long long t = ctx[2];
+    if (sink.action) { sink.action += t * B; sink.reward += t * B; sink.mask += t * B; }
+    if (sink.frame) sink.frame += t * B * H * W;
+  }
   __shared__ int s_paddle[256], s_bx[256], s_by[256];
   __shared__ uint64_t s_br[256][MAXW];
   __shared__ uint8_t s_done[256], s_rec[256];
@@ -437,7 +445,7 @@ int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx
                           uint8_t* cur_frame, uint8_t* hist_frames, uint8_t* hist_actions, int32_t* hist_len, int L,
                           uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
                           int first_step, int B, int H, int W, int paddle_width, int brick_rows,
-                          const float* rewards4, hipStream_t stream) {
+                          const float* rewards4, const int32_t* ctx, hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && L >= 2 && nw >= 1 && nw <= 4 && nw * 64 >= brick_rows * W && (H * W) % 16 == 0 && rewards4,
                -1);
   Compact cs{paddle, bx, by, dx, dy, done, bricks, nw};
@@ -447,10 +455,10 @@ int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx
   dim3 grid((B + 255) / 256);
   if (nw == 1)
     hipLaunchKernelGGL(env_step_compact_kernel<1>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
-                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc);
+                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx);
   else
     hipLaunchKernelGGL(env_step_compact_kernel<4>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
-                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc);
+                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx);
   MZ_LAUNCH_CHECK();
   return 0;
 }

@@ -38,7 +38,10 @@ struct TreeArgs {
   const float* c_tab;     // [S+1]
   int B, S, env_offset, search_id;
   uint64_t seed;
+  const int32_t* ctx;   // optional device step context (graph replay): ctx[0] = search id
 };
+
+MZ_DEV int tree_search_id(const TreeArgs& t) { return t.ctx ? t.ctx[0] : t.search_id; }
 
 MZ_DEV int ucb_select(const Node& nd, const TreeArgs& t, int b) {
   const int n = nd.N[0] + nd.N[1] + nd.N[2];
@@ -58,7 +61,7 @@ MZ_DEV int ucb_select(const Node& nd, const TreeArgs& t, int b) {
     if (u[a] == mx) best[cnt++] = a;
   const uint32_t k = t.calls[b];
   t.calls[b] = k + 1;
-  const int j = mz_randbelow((uint32_t)(b + t.env_offset), MZ_STREAM_TIE, (uint32_t)t.search_id, k, t.seed,
+  const int j = mz_randbelow((uint32_t)(b + t.env_offset), MZ_STREAM_TIE, (uint32_t)tree_search_id(t), k, t.seed,
                              (uint32_t)cnt);
   return best[j];
 }
@@ -110,7 +113,7 @@ __global__ void root_init_kernel(TreeArgs t, const float* __restrict__ v_root, c
   if (noise_in) {
     nz[0] = noise_in[b * 3]; nz[1] = noise_in[b * 3 + 1]; nz[2] = noise_in[b * 3 + 2];
   } else {  // mcts.py:114 Dirichlet(alpha * ones(3)).sample()
-    NormalGen g{(uint32_t)(b + t.env_offset), (uint32_t)t.search_id, 0u, t.seed, 0.f, false};
+    NormalGen g{(uint32_t)(b + t.env_offset), (uint32_t)tree_search_id(t), 0u, t.seed, 0.f, false};
     float g0 = g.gamma(alpha), g1 = g.gamma(alpha), g2 = g.gamma(alpha);
     float s = (g0 + g1) + g2;
     nz[0] = g0 / s; nz[1] = g1 / s; nz[2] = g2 / s;
@@ -209,9 +212,10 @@ __global__ void results_kernel(TreeArgs t, int64_t* __restrict__ counts, float* 
 
 // train_torch.py:191-198 with inverse-CDF sampling on u = uniform(env, STREAM_SAMPLE, step, 0)
 __global__ void sample_kernel(const int64_t* __restrict__ counts, int64_t* __restrict__ action, int B, float inv_t,
-                              int env_offset, int step, uint64_t seed) {
+                              int env_offset, int step_arg, uint64_t seed, const int32_t* __restrict__ ctx) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
+  const int step = ctx ? ctx[1] : step_arg;
   float vt[3];
   for (int a = 0; a < 3; ++a) {
     float c = (float)counts[b * 3 + a];
@@ -230,11 +234,28 @@ __global__ void sample_kernel(const int64_t* __restrict__ counts, int64_t* __res
   action[b] = chosen >= 0 ? chosen : last;
 }
 
+// acting-loop records of the search results at row ctx[2] (train_torch.py:204-208 sink)
+__global__ void record_results_kernel(const int64_t* __restrict__ counts, const float* __restrict__ values,
+                                      int64_t* __restrict__ rec_counts, float* __restrict__ rec_values, int B,
+                                      int t_arg, const int32_t* __restrict__ ctx) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const long long t = ctx ? ctx[2] : t_arg;
+  rec_counts[(t * B + b) * 3 + 0] = counts[b * 3 + 0];
+  rec_counts[(t * B + b) * 3 + 1] = counts[b * 3 + 1];
+  rec_counts[(t * B + b) * 3 + 2] = counts[b * 3 + 2];
+  rec_values[t * B + b] = values[b];
+}
+
+__global__ void ctx_advance_kernel(int32_t* ctx) {
+  if (threadIdx.x < 3) ctx[threadIdx.x] += 1;  // search id, step index, episode row
+}
+
 TreeArgs make_args(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
                    int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
-                   int env_offset, int search_id, uint64_t seed) {
+                   int env_offset, int search_id, uint64_t seed, const int32_t* ctx) {
   return TreeArgs{(Node*)nodes, root_sum, calls, leaf_parent, leaf_action, depth, path, sqrt_tab, c_tab,
-                  B,            S,        env_offset, search_id, seed};
+                  B,            S,        env_offset, search_id, seed, ctx};
 }
 
 }  // namespace
@@ -242,9 +263,10 @@ TreeArgs make_args(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_
 #define MZ_TREE_PARAMS                                                                                       \
   void *nodes, float *root_sum, uint32_t *calls, int32_t *leaf_parent, int32_t *leaf_action, int32_t *depth, \
       int32_t *path, const float *sqrt_tab, const float *c_tab, int B, int S, int env_offset, int search_id, \
-      uint64_t seed
+      uint64_t seed, const int32_t *ctx
 #define MZ_TREE_ARGS \
-  make_args(nodes, root_sum, calls, leaf_parent, leaf_action, depth, path, sqrt_tab, c_tab, B, S, env_offset, search_id, seed)
+  make_args(nodes, root_sum, calls, leaf_parent, leaf_action, depth, path, sqrt_tab, c_tab, B, S, env_offset, search_id, \
+            seed, ctx)
 
 extern "C" {
 
@@ -282,11 +304,27 @@ int mzba_mcts_results(MZ_TREE_PARAMS, int64_t* counts, float* values, hipStream_
 }
 
 int mzba_sample_actions(const int64_t* counts, int64_t* action, int B, float temperature, int env_offset, int step,
-                        uint64_t seed, hipStream_t stream) {
+                        uint64_t seed, const int32_t* ctx, hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && temperature > 0.f, -1);
   float inv_t = (float)(1.0 / (double)temperature);
   hipLaunchKernelGGL(sample_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, counts, action, B, inv_t,
-                     env_offset, step, seed);
+                     env_offset, step, seed, ctx);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_record_results(const int64_t* counts, const float* values, int64_t* rec_counts, float* rec_values, int B,
+                        int t, const int32_t* ctx, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0, -1);
+  hipLaunchKernelGGL(record_results_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, counts, values, rec_counts,
+                     rec_values, B, t, ctx);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_ctx_advance(int32_t* ctx, hipStream_t stream) {
+  MZ_CHECK_ARG(ctx != nullptr, -1);
+  hipLaunchKernelGGL(ctx_advance_kernel, dim3(1), dim3(64), 0, stream, ctx);
   MZ_LAUNCH_CHECK();
   return 0;
 }

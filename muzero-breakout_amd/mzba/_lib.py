@@ -25,7 +25,7 @@ SIGNATURES = {
     "mzba_env_step_planes": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "mzba_grayscale_planes": [P, P, I, I, I, P],
     "mzba_env_reset_compact": [P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, U64, I, I, P, P],
-    "mzba_env_step_compact": [P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, P, P],
+    "mzba_env_step_compact": [P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, P, P, P],
     "mzba_compact_to_planes": [P, P, P, P, P, I, P, I, I, I, I, I, P],
     "mzba_build_rep_input": [P, P, P, P, I, P, I, I, I, I, P],
     "mzba_conv2d": [I, P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
@@ -37,11 +37,13 @@ SIGNATURES = {
     "mzba_heads": [I, I, P, P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, F, I, P],
     "mzba_heads_bf16": [I, P, P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, F, I, P],
     "mzba_mcts_node_bytes": [],
-    "mzba_mcts_root": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P, F, F, F, P],
-    "mzba_mcts_select": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, I, P],
-    "mzba_mcts_backup": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, I, P, P, P, F, P],
-    "mzba_mcts_results": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P],
-    "mzba_sample_actions": [P, P, I, F, I, I, U64, P],
+    "mzba_mcts_root": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P, P, F, F, F, P],
+    "mzba_mcts_select": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, I, P],
+    "mzba_mcts_backup": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, I, P, P, P, F, P],
+    "mzba_mcts_results": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P],
+    "mzba_sample_actions": [P, P, I, F, I, I, U64, P, P],
+    "mzba_record_results": [P, P, P, P, I, I, P, P],
+    "mzba_ctx_advance": [P, P],
 }
 
 _lib = None

@@ -86,6 +86,10 @@ class ActingLoop:
         self.search_id = 0
         self.step_index = 0
         self.episode = 0
+        # device step context [search id, step index, episode row t]: every per-step varying
+        # value is read from here, so one captured HIP graph replays every acting step
+        self.ctx = torch.zeros(3, dtype=torch.int32, device=dev)
+        self.graph = None
 
     def reset(self, episode=None, params=None):
         """_acting_stage :166-167: env.reset + _pad_initial_state."""
@@ -95,23 +99,41 @@ class ActingLoop:
         self.frame0 = self.env.cur_frame.clone()
         self.episode += 1
         self.t = 0
+        self.ctx.copy_(torch.tensor([self.search_id, self.step_index, 0], dtype=torch.int32))
 
-    def act(self):
-        """One acting step t (no host synchronisation)."""
-        t = self.t
+    def _act_body(self):
+        """One acting step, every launch stream-ordered and parameterised by self.ctx."""
         env, ws = self.env, self.ws
         n = ws.n
         # _prepare_mcts_input + create_hidden_state_root -> pool slot 0
         env.build_rep_input(self.rep_in, self.cs, self.agent.dtype == "bf16")
         self.rep_runner.representation(self.rep_in, ws.cur, pool=ws.pool, pool_env_stride=(ws.S + 1) * n)
-        values, counts = ws.run(self.search_id, None)
-        if self.noise_log is not None:
-            self.noise_log.append(ws.tree.noise.clone())
+        values, counts = ws.run(self.search_id, None, ctx=self.ctx)
         L.call("mzba_sample_actions", L.ptr(counts), L.ptr(self.action), self.B, float(self.temperature),
-               self.env_offset, self.step_index, self.seed, L.stream())
-        self.rec["counts"][t].copy_(counts)
-        self.rec["values"][t].copy_(values)
-        env.step(self.action, t == 0, self.rec, t)
+               self.env_offset, self.step_index, self.seed, L.ptr(self.ctx), L.stream())
+        L.call("mzba_record_results", L.ptr(counts), L.ptr(values), L.ptr(self.rec["counts"]),
+               L.ptr(self.rec["values"]), self.B, 0, L.ptr(self.ctx), L.stream())
+        env.step(self.action, False, self.rec, 0, ctx=self.ctx)
+        L.call("mzba_ctx_advance", L.ptr(self.ctx), L.stream())
+
+    def capture(self):
+        """Capture one acting step (~S x 65 launches) into a HIP graph; act() then replays it."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self._act_body()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = g
+
+    def act(self, eager=False):
+        """One acting step t (no host synchronisation)."""
+        if self.graph is not None and not eager and self.noise_log is None:
+            self.graph.replay()
+        else:
+            self._act_body()
+            if self.noise_log is not None:
+                self.noise_log.append(self.ws.tree.noise.clone())
         self.search_id += 1
         self.step_index += 1
         self.t += 1

@@ -162,16 +162,20 @@ class CompactBreakout:
                self.brick_rows, self.seed, episode, self.env_offset, L.ptr(pr), L.stream())
         self.valid.fill_(1.0)
 
-    def step(self, action, first_step, rec=None, t=0):
-        """action: int64 (B,) device. rec: optional sink dict of (T,B,...) buffers."""
+    def step(self, action, first_step, rec=None, t=0, ctx=None):
+        """action: int64 (B,) device. rec: optional sink dict of (T,B,...) buffers, row t; with a
+        device step context `ctx` the row (and first_step) are read on the device instead."""
         ra = rr = rm = rf = None
         if rec is not None:
-            ra, rr, rm = rec["action"][t], rec["reward"][t], rec["mask"][t]
-            rf = rec["frame"][t] if rec.get("frame") is not None else None
+            if ctx is not None:
+                ra, rr, rm, rf = rec["action"], rec["reward"], rec["mask"], rec.get("frame")
+            else:
+                ra, rr, rm = rec["action"][t], rec["reward"][t], rec["mask"][t]
+                rf = rec["frame"][t] if rec.get("frame") is not None else None
         L.call("mzba_env_step_compact", *self._state_ptrs(), L.ptr(action), L.ptr(self.reward), L.ptr(self.valid),
                L.ptr(self.cur_frame), L.ptr(self.hist_frames), L.ptr(self.hist_actions), L.ptr(self.hist_len), self.Lh,
                L.ptr(ra), L.ptr(rr), L.ptr(rm), L.ptr(rf), 1 if first_step else 0, self.B, self.H, self.W, self.pw,
-               self.brick_rows, self.rewards4, L.stream())
+               self.brick_rows, self.rewards4, L.ptr(ctx), L.stream())
 
     def to_planes(self):
         planes = torch.empty(self.B, 3, self.H, self.W, dtype=torch.float32, device=self.device)

@@ -41,10 +41,11 @@ class TreeState:
         self.values = torch.empty(B, dtype=torch.float32, device=device)
         self.noise = torch.empty(B, 3, dtype=torch.float32, device=device)
 
-    def args(self, env_offset, search_id, seed):
+    def args(self, env_offset, search_id, seed, ctx=None):
+        """ctx: optional device int32[3] step context (its [0] overrides search_id; graph replay)."""
         return (L.ptr(self.nodes), L.ptr(self.root_sum), L.ptr(self.calls), L.ptr(self.leaf_parent),
                 L.ptr(self.leaf_action), L.ptr(self.depth), L.ptr(self.path), L.ptr(self.sqrt_tab),
-                L.ptr(self.c_tab), self.B, self.S, env_offset, search_id, seed)
+                L.ptr(self.c_tab), self.B, self.S, env_offset, search_id, seed, L.ptr(ctx))
 
     # individual kernels -----------------------------------------------------------------
     def root(self, tree_args, v_root, pi_root, noise_in, w_pol, w_noise, alpha):
@@ -135,11 +136,12 @@ class SearchWorkspace:
     def root_slot(self):
         return self.pool.view(self.B, self.S + 1, self.n)[:, 0]
 
-    def run(self, search_id, noise=None):
-        """mcts.py:24-71 on the device. Root latent must be in pool slot 0."""
+    def run(self, search_id, noise=None, ctx=None):
+        """mcts.py:24-71 on the device. Root latent must be in pool slot 0. With `ctx` the
+        search id is read on the device (HIP-graph replayable launch sequence)."""
         s = self.s
         B, S, n = self.B, self.S, self.n
-        ta = self.tree.args(s.env_offset, search_id, s.seed)
+        ta = self.tree.args(s.env_offset, search_id, s.seed, ctx)
         rn = self.runner
         root = self.pool.view(B, S + 1, n)[:, 0]
         self.cur.view(B, n).copy_(root)

@@ -269,7 +269,7 @@ def test_sample_kernel_matches_oracle():
     for T in (1.0, 0.5):
         a = torch.empty(B, dtype=torch.int64, device="cuda")
         cd = dev(c)
-        L.call("mzba_sample_actions", L.ptr(cd), L.ptr(a), B, T, 0, 17, 99, L.stream())
+        L.call("mzba_sample_actions", L.ptr(cd), L.ptr(a), B, T, 0, 17, 99, None, L.stream())
         u = R.uniform(np.arange(B), R.STREAM_SAMPLE, 17, 0, 99)
         ref = sample_actions(c, T, u)
         got = a.cpu().numpy()
@@ -372,3 +372,27 @@ def test_conv_lat_vs_torch(B, H, W, Cin, Cout, ks):
            Cout, ks, 1, L.stream())
     err = (out.float().cpu() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
     assert err < 1e-2, err
+
+
+def test_acting_graph_replay_matches_eager():
+    """One captured HIP graph per acting step, replayed: identical records to eager launches."""
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingLoop
+    cfg = _small_cfg(8)
+    mcfg = cfg["model"]
+    sd = init_state_dict(mcfg, 9)
+    ag = MuZeroAgent(mcfg, dtype="bf16")
+    ag.load_state_dict(sd)
+    out = []
+    for graph in (False, True):
+        loop = ActingLoop(cfg, ag, 64, seed=77, max_steps=12)
+        loop.reset(0)
+        loop.act(eager=True)
+        if graph:
+            loop.capture()
+        for _ in range(11):
+            loop.act()
+        torch.cuda.synchronize()
+        out.append({k: v.cpu().numpy() for k, v in loop.rec.items() if v is not None})
+    for k in out[0]:
+        np.testing.assert_array_equal(out[0][k], out[1][k], err_msg=k)
