@@ -109,6 +109,9 @@ int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const flo
                float* logits0, float* out0, const void* x1, const float* w1, const float* b1, int K1, int O1,
                int dec1, float* logits1, float* out1, float smin, float smax, int B, hipStream_t stream);
 
+/* ScalarTransforms.inverted_softmax_expectation (utils.py:74-81) on rows x n f32 logits. */
+int mzba_support_decode(const float* logits, float* out, int rows, int n, float smin, float smax, hipStream_t stream);
+
 /* bf16 path of mzba_heads as a small MFMA GEMM (16 envs per workgroup): x* [B][K] bf16, w* [16][K]
  * bf16 with zero rows >= O, K % 32 == 0. */
 int mzba_heads_bf16(int nheads, const void* x0, const void* w0, const float* b0, int K0, int O0, int dec0,

@@ -158,9 +158,29 @@ __global__ __launch_bounds__(512) void heads_mfma_kernel(HeadArgsB a) {
   }
 }
 
+// ScalarTransforms.inverted_softmax_expectation over rows of n logits (utils.py:74-81)
+__global__ void support_decode_kernel(const float* __restrict__ logits, float* __restrict__ out, int rows, int n,
+                                      float smin, float smax) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  float l[MAXO];
+  for (int i = 0; i < n; ++i) l[i] = logits[(size_t)r * n + i];
+  out[r] = decode_support(l, n, smin, smax);
+}
+
 }  // namespace
 
 extern "C" {
+
+int mzba_support_decode(const float* logits, float* out, int rows, int n, float smin, float smax,
+                        hipStream_t stream) {
+  MZ_CHECK_ARG(rows > 0 && n > 1 && n <= MAXO, -1);
+  hipLaunchKernelGGL(support_decode_kernel, dim3((rows + 255) / 256), dim3(256), 0, stream, logits, out, rows, n, smin,
+                     smax);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
 
 // bf16 MFMA heads: x*: [B][K] bf16, w*: [16][K] bf16 (zero rows >= O), K % 32 == 0.
 int mzba_heads_bf16(int nheads, const void* x0, const void* w0, const float* b0, int K0, int O0, int dec0,

@@ -175,3 +175,43 @@ class ActingLoop:
                 rs = np.float32(rs + r)
             out.append(ObservationTrajectory(acts, states, rews, vc, vals, int(m.sum()), float(rs)))
         return out
+
+
+class ActingStage:
+    """Mirror of RLSystem._acting_stage (train_torch.py:160-169): `num_episodes` episodes of
+    `n_parallel` envs with the target agent, returning the per-env ObservationTrajectory
+    lists (what the reference hands to ReplayBuffer.save_observation_trajectory).
+    `temperature` / `noise_weight` follow the caller's schedule (train_torch.py:129-135)."""
+
+    def __init__(self, cfg, agent, seed=0, env_offset=0, use_graph=True):
+        self.cfg = cfg
+        self.loop = ActingLoop(cfg, agent, cfg["n_parallel"], seed=seed, env_offset=env_offset)
+        self.use_graph = use_graph
+        self.num_episodes = cfg["num_episodes"]
+
+    @property
+    def temperature(self):
+        return self.loop.temperature
+
+    @temperature.setter
+    def temperature(self, t):
+        if t != self.loop.temperature:
+            self.loop.graph = None  # the sampling kernel's 1/T is a launch argument
+        self.loop.temperature = t
+
+    def set_noise_weight(self, w):
+        if w != self.loop.search.noise_weight:
+            self.loop.graph = None
+        self.loop.search.noise_weight = w
+
+    def run(self):
+        out = []
+        for _ in range(self.num_episodes):
+            loop = self.loop
+            loop.reset()
+            while not loop.all_done() and loop.t < loop.max_steps:
+                loop.act()
+                if self.use_graph and loop.graph is None:
+                    loop.capture()
+            out.append(loop.trajectories())
+        return out

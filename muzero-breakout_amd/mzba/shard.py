@@ -70,7 +70,10 @@ class TrajectoryGather:
         n = t1 - t0
         pack_records(rec, t0, t1, self.slab[:n])
         if self.ws > 1:
-            dist.all_gather_into_tensor(self.gathered.view(-1), self.slab.view(-1))
+            if dist.get_backend() == "nccl":  # RCCL over xGMI: one flat all-gather
+                dist.all_gather_into_tensor(self.gathered.view(-1), self.slab.view(-1))
+            else:  # gloo (CPU tests)
+                dist.all_gather(list(self.gathered.unbind(0)), self.slab)
         else:
             self.gathered[0].copy_(self.slab)
         if self.rank == 0:
