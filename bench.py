@@ -148,7 +148,10 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     value = world * B * args.steps / dt
-    conv_ms = float(np.mean([a.elapsed_time(b) for a, b in probe])) if probe else None
+    # probe entries: (start, end, convs in the launch); per-conv average over the latent residual convs
+    conv_ms = (float(sum(a.elapsed_time(b) for a, b, _ in probe) / sum(n for _, _, n in probe))) if probe else None
+    tower_launch_ms = (float(np.mean([a.elapsed_time(b) for a, b, n in probe if n > 1]))
+                       if any(n > 1 for _, _, n in probe) else None)
     p = agent.packed
     fl = conv_flops(B, p.lh * p.lw, p.c1)
     achieved = fl / (conv_ms * 1e-3) / 1e12 if conv_ms else None
@@ -157,7 +160,8 @@ def main():
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            if tj.get("envs") == B:
+            want = "tower_kernel" if any(n > 1 for _, _, n in probe) else "conv_lat_kernel"
+            if tj.get("envs") == B and tj.get("kernel", "").startswith(want):
                 traffic = tj.get("bytes_per_launch")
         except Exception:
             traffic = None
@@ -178,10 +182,14 @@ def main():
             "config": {"workload": f"config 2: {B} envs/GPU x {args.sims} MCTS sims, 16x20 Breakout, 32-frame stack",
                        "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
                        "parallelism": f"env-sharded x{world}, RCCL all-gather of trajectory records"},
-            "roofline": {"bound": "mfma", "kernel": "conv_lat_kernel<3,256> bf16 3x3 256->256 (M=B*20,N=256,K=2304)",
+            "roofline": {"bound": "mfma",
+                         "kernel": "tower_kernel (fused 14-block residual tower, bf16 3x3 256->256 convs, M=B*20,"
+                                   " N=256, K=2304 each)" if tower_launch_ms else
+                                   "conv_lat_kernel<3,256> bf16 3x3 256->256 (M=B*20,N=256,K=2304)",
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": traffic,
-                         "avg_launch_ms": conv_ms, "launches_timed": len(probe)},
+                         "flop_per_conv": fl, "avg_ms_per_conv": conv_ms, "avg_launch_ms": tower_launch_ms or conv_ms,
+                         "launches_timed": len(probe)},
             "cpu_baseline": cpu_info,
             "visit_count_match": match,
             "launch": "eager" if args.no_graph else "hip-graph replay (probe step eager)",

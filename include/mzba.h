@@ -93,6 +93,14 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
                   const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
                   hipStream_t stream);
 
+/* Fused residual tower: nblocks ResidualBlock(256) on the 4x5 latent in ONE launch (networks.py:19-35,
+ * 124-131, 190-197); a workgroup keeps 4 envs' activations in LDS for the whole tower. wf16: per conv
+ * [16 col tiles][72 k steps][64 lanes][8] bf16 (pack_lat16), convs back to back, + 8*64*8 padding
+ * elements; bias: per conv [256] f32 (BN folded). in: env b at in + b*in_env_stride
+ * (+ slot[b]*in_slot_stride); out: [B][20][256] bf16. */
+int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride, void* out,
+               const void* wf16, const float* bias, int nblocks, int B, hipStream_t stream);
+
 /* nn.AvgPool2d(2, 2) (networks.py:44), NHWC. */
 int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream);
 

@@ -32,6 +32,7 @@ SIGNATURES = {
     "mzba_conv_lat_supported": [I, I, I, I, I],
     "mzba_conv_lat_set_variant": [I],
     "mzba_conv_lat": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
+    "mzba_tower": [P, LL, P, LL, P, P, P, I, I, P],
     "mzba_avgpool2": [I, P, P, I, I, I, I, P],
     "mzba_scale_state": [I, P, P, P, LL, P, I, LL, I, I, P],
     "mzba_heads": [I, I, P, P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, F, I, P],

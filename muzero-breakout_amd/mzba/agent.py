@@ -36,6 +36,13 @@ def pack_lat(wp, cout, ks, cin):
     return np.concatenate([wf, np.zeros(LAT_PAD_ELEMS, wf.dtype)])  # ring prefetch overrun
 
 
+def pack_lat16(wp, cout, ks, cin):
+    """16-column fragment-major weights for the fused tower (v_mfma_f32_16x16x32_bf16 B operand):
+    wf16[ct][s][lane][8] = Wp[16ct + lane%16][32s + 8(lane//16) + j]."""
+    K = ks * ks * cin
+    return wp.reshape(cout // 16, 16, K // 32, 4, 8).transpose(0, 2, 3, 1, 4).reshape(-1)
+
+
 def _round64(c):
     return (c + 63) // 64 * 64
 
@@ -76,6 +83,11 @@ class PackedNets:
         self.rew_lin = self._linear(sd["dyn_net.reward_head.2.weight"], sd["dyn_net.reward_head.2.bias"], self.c1)
         # prediction (networks.py:190-223)
         self.pred = [self._res(sd, f"pred_net.res_blocks.{i}") for i in range(mcfg["prediction_network"]["num_res_blocks"])]
+        # fused-tower packing (bf16, 256 channels, 4x5 latent): every residual conv of a tower
+        # back to back in the 16-column fragment-major order + 8 padding k steps
+        self.tower_ok = (self.dtype == "bf16" and self.c1 == 256 and (self.lh, self.lw) == (4, 5))
+        self.dyn_tower = self._tower(sd, "dyn_net.res_blocks", mcfg["dynamics_network"]["num_res_blocks"])
+        self.pred_tower = self._tower(sd, "pred_net.res_blocks", mcfg["prediction_network"]["num_res_blocks"])
         self.pol_conv = self._conv(sd["pred_net.policy_head.0.conv.weight"], sd["pred_net.policy_head.0.conv.bias"],
                                    self._bn(sd, "pred_net.policy_head.0.bn"))
         self.pol_lin = self._linear(sd["pred_net.policy_head.2.weight"], sd["pred_net.policy_head.2.bias"], self.c1 // 2)
@@ -129,6 +141,22 @@ class PackedNets:
         return (self._conv(sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], self._bn(sd, p + ".bn1")),
                 self._conv(sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], self._bn(sd, p + ".bn2")))
 
+    def _tower(self, sd, prefix, n):
+        if not self.tower_ok or n == 0:
+            return None
+        wfs, bs = [], []
+        for i in range(n):
+            for k in (1, 2):
+                p = f"{prefix}.{i}"
+                alpha, beta = self._bn(sd, f"{p}.bn{k}")
+                w = sd[f"{p}.conv{k}.weight"] * alpha[:, None, None, None]
+                b = sd[f"{p}.conv{k}.bias"] * alpha + beta
+                wfs.append(pack_lat16(w.transpose(0, 2, 3, 1).reshape(256, -1), 256, 3, 256))
+                bs.append(b)
+        wf = np.concatenate(wfs + [np.zeros(LAT_PAD_ELEMS)])
+        return {"wf": torch.tensor(wf, dtype=torch.float32).to(self.tdt).to(self.device),
+                "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device), "n": n}
+
     def _linear(self, w, b, c):
         O, K = w.shape
         hw = K // c
@@ -168,6 +196,7 @@ class NetRunner:
         # latent-resolution residual conv (the dominant kernel shape M=B*h*w, N=C, K=9C)
         self.probe = None
         self.use_lat = True  # latent-resolution bf16 convs on conv_lat (False: generic implicit GEMM)
+        self.use_tower = True  # dyn/pred residual towers as one fused launch each (bf16, C=256, 4x5)
 
     # -- primitives --------------------------------------------------------------------
     def conv(self, x, layer, out, B, H, W, res=None, relu=True, slot=None, env_stride=None, slot_stride=0, act=None):
@@ -184,6 +213,19 @@ class NetRunner:
                L.ptr(layer["b"]), L.ptr(ab), L.ptr(act) if ab is not None else None, layer.get("A", 0),
                L.ptr(res), L.ptr(out), B, H, W, layer["cin"], layer["cout"], layer["ks"], 1 if relu else 0, s)
 
+    def tower(self, tw, x, out):
+        """All residual blocks of a dyn/pred tower in one launch (activations stay in LDS).
+        `out` may alias `x` (each workgroup reads its 4 envs before writing them)."""
+        pr = self.probe
+        if pr is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        L.call("mzba_tower", L.ptr(x), 20 * 256, None, 0, L.ptr(out), L.ptr(tw["wf"]), L.ptr(tw["b"]), tw["n"],
+               self.B, L.stream())
+        if pr is not None:
+            e1.record()
+            pr.append((e0, e1, 2 * tw["n"]))
+
     def resblock(self, blk, x, t, out, B, H, W):
         """networks.py:31-35; out may alias x (in-place residual)."""
         pr = self.probe if (H, W) == (self.p.lh, self.p.lw) else None
@@ -193,7 +235,7 @@ class NetRunner:
         self.conv(x, blk[0], t, B, H, W, relu=True)
         if pr is not None:
             e1.record()
-            pr.append((e0, e1))
+            pr.append((e0, e1, 1))
         self.conv(t, blk[1], out, B, H, W, res=x, relu=True)
 
     # -- nets ----------------------------------------------------------------------------
@@ -230,8 +272,11 @@ class NetRunner:
         p = self.p
         self.conv(parent_src, p.dyn0, self.x, B, H, W, relu=True, slot=slot, env_stride=env_stride,
                   slot_stride=slot_stride, act=act)
-        for blk in p.dyn:
-            self.resblock(blk, self.x, self.t, self.x, B, H, W)
+        if p.dyn_tower is not None and self.use_tower:
+            self.tower(p.dyn_tower, self.x, self.x)
+        else:
+            for blk in p.dyn:
+                self.resblock(blk, self.x, self.t, self.x, B, H, W)
         self.conv(self.x, p.rew_conv, self.rc, B, H, W, relu=True)
         rl = p.rew_lin
         if "wb" in rl:
@@ -251,9 +296,13 @@ class NetRunner:
         B, H, W = self.B, self.p.lh, self.p.lw
         p = self.p
         cur = h
-        for i, blk in enumerate(p.pred):
-            self.resblock(blk, cur, self.t, self.x, B, H, W)
+        if p.pred_tower is not None and self.use_tower:
+            self.tower(p.pred_tower, cur, self.x)
             cur = self.x
+        else:
+            for i, blk in enumerate(p.pred):
+                self.resblock(blk, cur, self.t, self.x, B, H, W)
+                cur = self.x
         self.conv(cur, p.pol_conv, self.pc, B, H, W, relu=True)
         self.conv(cur, p.val_conv, self.vc, B, H, W, relu=True)
         pl, vl = p.pol_lin, p.val_lin

@@ -37,7 +37,35 @@ def run(B, H, W, Cin, Cout, ks, kind, iters=50):
             "tflops": fl / (ms * 1e-3) / 1e12}
 
 
+def run_tower(B, nblocks, iters=20):
+    from mzba.agent import pack_lat16  # noqa: F401
+    C = 256
+    x = torch.randn(B * 20 * C, device="cuda").to(torch.bfloat16)
+    out = torch.empty_like(x)
+    wf = (torch.randn(2 * nblocks * C * 2304 + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
+    b = torch.zeros(2 * nblocks * C, device="cuda")
+
+    def launch():
+        L.call("mzba_tower", L.ptr(x), 20 * C, None, 0, L.ptr(out), L.ptr(wf), L.ptr(b), nblocks, B, L.stream())
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(iters)]
+    for e0, e1 in ev:
+        e0.record(); launch(); e1.record()
+    torch.cuda.synchronize()
+    ms = np.median([a.elapsed_time(c) for a, c in ev])
+    fl = 2.0 * B * 20 * C * 2304 * 2 * nblocks
+    return {"kind": "tower", "B": B, "nblocks": nblocks, "us": ms * 1e3, "us_per_conv": ms * 1e3 / (2 * nblocks),
+            "tflops": fl / (ms * 1e-3) / 1e12}
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "tower":
+        for s in [(1024, 1), (1024, 14), (4096, 14)]:
+            print(json.dumps(run_tower(*s)))
+        print(json.dumps(run(1024, 4, 5, 256, 256, 3, "lat")))
+        sys.exit(0)
     shapes = [(1024, 4, 5, 256, 256, 3), (4096, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 1),
               (1024, 4, 5, 256, 128, 3), (1024, 8, 10, 256, 256, 3)]
     for s in shapes:
