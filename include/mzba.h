@@ -94,12 +94,20 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
                   hipStream_t stream);
 
 /* Fused residual tower: nblocks ResidualBlock(256) on the 4x5 latent in ONE launch (networks.py:19-35,
- * 124-131, 190-197); a workgroup keeps 4 envs' activations in LDS for the whole tower. wf16: per conv
- * [16 col tiles][72 k steps][64 lanes][8] bf16 (pack_lat16), convs back to back, + 8*64*8 padding
- * elements; bias: per conv [256] f32 (BN folded). in: env b at in + b*in_env_stride
+ * 124-131, 190-197); a workgroup keeps 4 (or, for B >= 8 x CUs, 8) envs' activations in LDS for the
+ * whole tower. wf16: per conv [16 col tiles][72 k steps][64 lanes][8] bf16 with taps ordered (dx, dy)
+ * (agent.pack_tower_conv), convs back to back, + 8*64*8 padding elements; bias: per conv [256] f32 (BN folded). in: env b at in + b*in_env_stride
  * (+ slot[b]*in_slot_stride); out: [B][20][256] bf16. */
+/* kernel choice for experiments/tests: 0 by batch (default), 1 four-env kernel, 2 eight-env kernel */
+int mzba_tower_set_variant(int v);
+/* kernel mzba_tower runs for batch B: 1 four-env (workgroup = 4 envs, 8 waves), 2 eight-env (B >= 8 x CUs;
+ * workgroup = 8 envs, 4 waves: half the weight stream per env). Both take agent.pack_tower_conv weights. */
+int mzba_tower_plan(int B);
+/* device scratch bytes mzba_tower needs for batch B (0 for both kernels; the ws argument may be null) */
+long long mzba_tower_ws_bytes(int B);
 int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride, void* out,
-               const void* wf16, const float* bias, int nblocks, int B, hipStream_t stream);
+               const void* wf16, const float* bias, int nblocks, int B, void* ws, long long ws_bytes,
+               hipStream_t stream);
 
 /* nn.AvgPool2d(2, 2) (networks.py:44), NHWC. */
 int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream);

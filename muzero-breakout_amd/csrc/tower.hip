@@ -4,13 +4,19 @@
 // 124-131, 190-197). Launching every conv separately re-stages the activations into LDS
 // and writes them back to HBM 28 times per tower. Here ONE workgroup owns E = 4 whole envs
 // (80 rows) x all 256 channels for the whole tower:
-//   * X (block input / output) and T (conv1 output) stay resident in LDS (2 x 40 KB,
-//     16-B chunks XOR-swizzled by row) across every block; one zero row serves the padding;
+//   * X (block input / output) and T (conv1 output) stay resident in LDS (2 x 40 KB) across
+//     every block. LDS row of (env e, latent y, x) = 16x + 4y + e: a 16-row MFMA tile is one
+//     latent COLUMN x of all 4 envs, so a 3x3 tap (dy, dx) maps tile x to tile x + dx whole
+//     (tiles with x + dx outside 0..4 are skipped: 39 of 45 tile-taps run) and shifts rows
+//     by 4 dy inside the tile. 16-B chunks are XOR-swizzled by (row & 15) = 4y + e; rows that
+//     fall outside y = 0..3 read a 16-row zero block at the row key ((y + dy) & 3) * 4 + e,
+//     so every ds_read_b128 lane group hits 16 distinct bank slots for every tap;
 //   * weights stream into VGPRs from a 16-column fragment-major packing
-//     wf16[col tile][k step][lane][8] (one coalesced 1 KB wave load per 32-deep k step and
-//     column tile, 8 steps in flight); each of the 8 waves owns 32 output channels;
-//   * v_mfma_f32_16x16x32_bf16: 5 row tiles x 2 column tiles per wave = 10 independent
-//     accumulators; MFMA / next-step ds_read_b128 / VALU interleaved by sched_group_barrier;
+//     wf16[col tile][k step][lane][8] with taps ordered (dx, dy) (agent.pack_tower_conv),
+//     one coalesced 1 KB wave load per 32-deep k step and column tile, 4 steps in flight;
+//     each of the 8 waves owns 32 output channels;
+//   * v_mfma_f32_16x16x32_bf16: up to 5 row tiles x 2 column tiles per wave; MFMA /
+//     next-step ds_read_b128 / VALU interleaved by sched_group_barrier;
 //   * conv1 epilogue: + bias, ReLU -> T (LDS); conv2: accumulator initialised with
 //     bias + residual X, ReLU -> X in place (each element is owned by one lane).
 // Input is read from HBM once (optional per-env slot gather from the latent node pool) and
@@ -26,10 +32,20 @@ constexpr int TE = 4;              // envs per workgroup
 constexpr int TROWS = 80;          // TE * 20 (4x5 latent)
 constexpr int TC = 256;            // channels
 constexpr int TROWB = TC * 2;      // 512 B per LDS row
-constexpr int TR = 5;              // 16-row tiles
+constexpr int TR = 5;              // 16-row tiles = latent columns x
 constexpr int TNS = 9 * TC / 32;   // 72 k steps per 3x3 conv
-constexpr int TD = 4;              // weight ring depth (k steps)
+#ifndef TOWER_TD
+#define TOWER_TD 4
+#endif
+constexpr int TD = TOWER_TD;       // weight ring depth (k steps); must divide the 8 steps of a tap
+static_assert(8 % TD == 0, "ring index restarts at every tap");
+#ifndef TOWER_ABLATE
+#define TOWER_ABLATE 0  // diagnostic builds only (make tower-variants): 1 hot weights, 2 no LDS A reads,
+                        // 3 duplicate weight streams
+#endif
 constexpr int TNT = 512;
+constexpr int IMG = TROWS * TROWB;         // one activation image (40 KB)
+constexpr int LDS_X = 0, LDS_T = IMG, LDS_Z = 2 * IMG, LDS_BYTES = 2 * IMG + 16 * TROWB;
 
 struct TowerArgs {
   const bf16_t* in;
@@ -43,22 +59,96 @@ struct TowerArgs {
   int B;
 };
 
-// LDS byte offset of (row, 16-B chunk) in a swizzled activation image
+// LDS row of (env e, latent position p = 5y + x) and the byte offset of (row, 16-B chunk)
+MZ_DEV int trow(int e, int p) { return (p % 5) * 16 + (p / 5) * 4 + e; }
 MZ_DEV int toff(int row, int chunk) { return row * TROWB + ((chunk ^ (row & 15)) << 4); }
 
+// A-row addressing of this lane for latent row shift dy: byte offset of its row in source
+// tile 0 (or of its zero-block row), the per-tile stride (0 for zero rows) and the swizzle key
+MZ_DEV void tap_rows(int srcimg, int y, int e, int dy, int& base, int& tstride, int& sw) {
+  const int yy = y + dy;
+  const bool ok = (unsigned)yy < 4u;
+  const int key = ((yy & 3) << 2) | e;
+  base = ok ? srcimg + key * TROWB : LDS_Z + key * TROWB;
+  tstride = ok ? 16 * TROWB : 0;
+  sw = key << 4;
+}
+
+// the 24 k steps (3 dy x 8 channel chunks) of the taps with column shift DX
+template <int DX>
+__device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int srcimg, const uint4* __restrict__ wp0,
+                                         const uint4* __restrict__ wp1, uint4 (&b0q)[TD], uint4 (&b1q)[TD],
+                                         f32x4 (&acc0)[TR], f32x4 (&acc1)[TR], int lane) {
+  constexpr int NT = DX == 0 ? 5 : 4;   // active tiles
+  constexpr int A0 = DX < 0 ? 1 : 0;    // first accumulator tile (output column x)
+  constexpr int S0 = DX > 0 ? 1 : 0;    // first source tile (x + dx)
+  constexpr int SB = (DX + 1) * 24;     // first k step of this column shift
+  const int q = lane >> 4, y = (lane & 15) >> 2, e = lane & 3;
+  int base, tst, sw;
+  tap_rows(srcimg + S0 * 16 * TROWB, y, e, -1, base, tst, sw);
+  bf16x8 afc[NT], afn[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * tst + ((q << 4) ^ sw));
+  constexpr int NC = TC / 32;  // 8 k steps per tap
+#pragma unroll 1
+  for (int dyi = 0; dyi < 3; ++dyi) {
+    int nbase, ntst, nsw;
+    tap_rows(srcimg + S0 * 16 * TROWB, y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int s = SB + dyi * NC + c;
+      const bf16x8 w0 = __builtin_bit_cast(bf16x8, b0q[c % TD]);
+      const bf16x8 w1 = __builtin_bit_cast(bf16x8, b1q[c % TD]);
+#if TOWER_ABLATE == 1  // diagnostic only: weights from one L1-resident k step
+      b0q[c % TD] = wp0[(size_t)((s + TD) & 1) * 64];
+      b1q[c % TD] = wp1[(size_t)((s + TD) & 1) * 64];
+#else
+      b0q[c % TD] = wp0[(size_t)(s + TD) * 64];
+      b1q[c % TD] = wp1[(size_t)(s + TD) * 64];
+#endif
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        acc0[A0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[j], w0, acc0[A0 + j], 0, 0, 0);
+        acc1[A0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[j], w1, acc1[A0 + j], 0, 0, 0);
+        if (TOWER_ABLATE == 2)  // diagnostic only: no LDS A reads inside the loop
+          afn[j] = afc[j];
+        else if (c + 1 < NC)
+          afn[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
+        else
+          afn[j] = *reinterpret_cast<const bf16x8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) afc[j] = afn[j];
+    }
+    base = nbase; tst = ntst; sw = nsw;
+  }
+}
+
 template <bool RESID>
-__device__ __forceinline__ void tower_conv(const TowerArgs& a, const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+__device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg, int dstimg,
                                            const uint4* __restrict__ wconv, const float* __restrict__ bconv,
-                                           const int (&ry)[TR], const int (&rx)[TR], const int (&rb)[TR],
-                                           const bool (&rv)[TR], int lane, int wave) {
+                                           int lane, int wave) {
   const int q = lane >> 4, l16 = lane & 15;
+#if TOWER_ABLATE == 3  // diagnostic only: waves w and w+4 stream the same weights (half the L2 bytes)
+  const int ct0 = 2 * (wave & 3), ct1 = 2 * (wave & 3) + 1;
+#else
   const int ct0 = 2 * wave, ct1 = 2 * wave + 1;  // 16-column tiles of this wave
+#endif
   const uint4* wp0 = wconv + (size_t)ct0 * TNS * 64 + lane;
   const uint4* wp1 = wconv + (size_t)ct1 * TNS * 64 + lane;
   uint4 b0q[TD], b1q[TD];
 #pragma unroll
   for (int i = 0; i < TD; ++i) { b0q[i] = wp0[(size_t)i * 64]; b1q[i] = wp1[(size_t)i * 64]; }
-  // accumulator init: bias (+ residual X for conv2); D[row = 4q + i][col = l16]
+  // accumulator init: bias (+ residual X for conv2); D[row = 4q + i][col = l16] of tile rt
   const int n0 = ct0 * 16 + l16, n1 = ct1 * 16 + l16;
   const float bb0 = bconv[n0], bb1 = bconv[n1];
   f32x4 acc0[TR], acc1[TR];
@@ -69,78 +159,28 @@ __device__ __forceinline__ void tower_conv(const TowerArgs& a, const uint8_t* __
       float r0 = bb0, r1 = bb1;
       if (RESID) {
         const int row = rt * 16 + 4 * q + i;
-        const bf16_t* xr = reinterpret_cast<const bf16_t*>(dst + toff(row, n0 >> 3)) + (n0 & 7);
-        const bf16_t* xr1 = reinterpret_cast<const bf16_t*>(dst + toff(row, n1 >> 3)) + (n1 & 7);
-        r0 = r0 + bf16_to_f32(*xr);
-        r1 = r1 + bf16_to_f32(*xr1);
+        r0 = r0 + bf16_to_f32(*(reinterpret_cast<const bf16_t*>(lds + dstimg + toff(row, n0 >> 3)) + (n0 & 7)));
+        r1 = r1 + bf16_to_f32(*(reinterpret_cast<const bf16_t*>(lds + dstimg + toff(row, n1 >> 3)) + (n1 & 7)));
       }
       acc0[rt][i] = r0;
       acc1[rt][i] = r1;
     }
-  auto tap_rows = [&](int tap, int (&off)[TR], int (&sw)[TR]) {
-    const int ky = tap / 3 - 1, kx = tap % 3 - 1;
-#pragma unroll
-    for (int rt = 0; rt < TR; ++rt) {
-      const int sy = ry[rt] + ky, sx = rx[rt] + kx;
-      const bool ok = rv[rt] && sy >= 0 && sy < 4 && sx >= 0 && sx < 5;
-      const int r = ok ? rb[rt] + sy * 5 + sx : TROWS;
-      off[rt] = r * TROWB;
-      sw[rt] = (r & 15) << 4;
-    }
-  };
-  int offc[TR], swc[TR], offn[TR], swn[TR];
-  tap_rows(0, offc, swc);
-  bf16x8 afc[TR], afn[TR];
-#pragma unroll
-  for (int rt = 0; rt < TR; ++rt) afc[rt] = *reinterpret_cast<const bf16x8*>(src + offc[rt] + ((q << 4) ^ swc[rt]));
-  constexpr int NC = TC / 32;  // 8 k steps per tap
-  for (int tap = 0; tap < 9; ++tap) {
-    tap_rows(tap < 8 ? tap + 1 : tap, offn, swn);
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int s = tap * NC + c;
-      const bf16x8 w0 = __builtin_bit_cast(bf16x8, b0q[c % TD]);
-      const bf16x8 w1 = __builtin_bit_cast(bf16x8, b1q[c % TD]);
-      b0q[c % TD] = wp0[(size_t)(s + TD) * 64];
-      b1q[c % TD] = wp1[(size_t)(s + TD) * 64];
-#pragma unroll
-      for (int rt = 0; rt < TR; ++rt) {
-        acc0[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[rt], w0, acc0[rt], 0, 0, 0);
-        acc1[rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[rt], w1, acc1[rt], 0, 0, 0);
-        if (c + 1 < NC)
-          afn[rt] = *reinterpret_cast<const bf16x8*>(src + offc[rt] + (((4 * (c + 1) + q) << 4) ^ swc[rt]));
-        else
-          afn[rt] = *reinterpret_cast<const bf16x8*>(src + offn[rt] + ((q << 4) ^ swn[rt]));
-      }
-#pragma unroll
-      for (int rt = 0; rt < TR; ++rt) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int rt = 0; rt < TR; ++rt) afc[rt] = afn[rt];
-    }
-#pragma unroll
-    for (int rt = 0; rt < TR; ++rt) { offc[rt] = offn[rt]; swc[rt] = swn[rt]; }
-  }
+  tower_dx<-1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+  tower_dx<0>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+  tower_dx<1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
   // epilogue: ReLU -> bf16 -> dst (T for conv1, X in place for conv2)
 #pragma unroll
   for (int rt = 0; rt < TR; ++rt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = rt * 16 + 4 * q + i;
-      *(reinterpret_cast<bf16_t*>(dst + toff(row, n0 >> 3)) + (n0 & 7)) = f32_to_bf16(fmaxf(acc0[rt][i], 0.f));
-      *(reinterpret_cast<bf16_t*>(dst + toff(row, n1 >> 3)) + (n1 & 7)) = f32_to_bf16(fmaxf(acc1[rt][i], 0.f));
+      *(reinterpret_cast<bf16_t*>(lds + dstimg + toff(row, n0 >> 3)) + (n0 & 7)) = f32_to_bf16(fmaxf(acc0[rt][i], 0.f));
+      *(reinterpret_cast<bf16_t*>(lds + dstimg + toff(row, n1 >> 3)) + (n1 & 7)) = f32_to_bf16(fmaxf(acc1[rt][i], 0.f));
     }
 }
 
 __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t xs[(TROWS + 1) * TROWB];  // X + zero row
-  __shared__ __attribute__((aligned(16))) uint8_t ts[(TROWS + 1) * TROWB];  // T + zero row
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];  // X | T | 16 zero rows
   __shared__ long long envoff[TE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int env0 = blockIdx.x * TE;
@@ -153,7 +193,7 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
     envoff[tid] = off;
   }
   __syncthreads();
-  // stage X (80 rows x 32 chunks = 2560 chunks, 5 per thread) and zero both pad rows
+  // stage X: global row r = 20 e + p (80 rows x 32 chunks = 2560 chunks, 5 per thread); zero block
   {
     uint4 v[5];
 #pragma unroll
@@ -168,30 +208,18 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
 #pragma unroll
     for (int u = 0; u < 5; ++u) {
       const int i = u * TNT + tid;
-      *reinterpret_cast<uint4*>(xs + toff(i >> 5, i & 31)) = v[u];
+      const int r = i >> 5;
+      *reinterpret_cast<uint4*>(lds + LDS_X + toff(trow(r / 20, r % 20), i & 31)) = v[u];
     }
-    if (tid < 32) {
-      *reinterpret_cast<uint4*>(xs + TROWS * TROWB + tid * 16) = make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(ts + TROWS * TROWB + tid * 16) = make_uint4(0, 0, 0, 0);
-    }
+    *reinterpret_cast<uint4*>(lds + LDS_Z + tid * 16) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
-  // per row tile: this lane's A row geometry (row = rt*16 + (lane & 15))
-  int ry[TR], rx[TR], rb[TR];
-  bool rv[TR];
-#pragma unroll
-  for (int rt = 0; rt < TR; ++rt) {
-    const int m = rt * 16 + (lane & 15);
-    rv[rt] = m < rows;
-    const int e = m / 20, p = m - e * 20;
-    ry[rt] = p / 5; rx[rt] = p - (p / 5) * 5; rb[rt] = e * 20;
-  }
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;  // uint4 per conv
   for (int blk = 0; blk < a.nblocks; ++blk) {
-    tower_conv<false>(a, xs, ts, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, ry, rx, rb, rv, lane, wave);
+    tower_conv<false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, lane, wave);
     __syncthreads();
-    tower_conv<true>(a, ts, xs, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, ry, rx, rb, rv, lane, wave);
+    tower_conv<true>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, lane, wave);
     __syncthreads();
   }
   // write the tower output (16-B chunks, rows < rows)
@@ -201,23 +229,240 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
     const int r = i >> 5, c = i & 31;
     if (r < rows)
       *reinterpret_cast<uint4*>(a.out + (long long)(env0 + r / 20) * 20 * TC + (r % 20) * TC + c * 8) =
-          *reinterpret_cast<const uint4*>(xs + toff(r, c));
+          *reinterpret_cast<const uint4*>(lds + LDS_X + toff(trow(r / 20, r % 20), c));
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 8-env variant (tower8_kernel): ONE workgroup = 8 envs (160 rows) x 256 channels, 4 waves (one per
+// SIMD, up to 512 registers each), every wave all 10 row tiles x 4 column tiles (64 channels).
+// Each weight fragment loaded from L2 now feeds 10 MFMAs instead of 5, halving the per-CU weight
+// stream per env (the bound of the 4-env kernel). Weights are the MFMA A operand, so a
+// lane's accumulator holds 4 consecutive channels of one row: 8-byte LDS epilogue stores/loads.
+// One activation image: a conv reads it whole, then (after a barrier) its output overwrites it in
+// place; conv1 first lifts the block input at its own output positions into registers (the residual).
+namespace t8 {
+constexpr int E = 8, ROWS = 160, NRT = 10, NT = 256, CT = 4;  // 4 waves
+constexpr int IMG = ROWS * TROWB;                       // 80 KB
+constexpr int LZ = IMG, BYTES = IMG + 16 * TROWB;       // + 16 zero rows
+// LDS row of (env e, latent position p = 5y + x): env quad (e >> 2) owns tiles 5 (e >> 2) .. +4
+MZ_DEV int row8(int e, int p) { return (e >> 2) * 80 + (p % 5) * 16 + (p / 5) * 4 + (e & 3); }
+}  // namespace t8
+
+template <int DX>
+__device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
+                                          uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[t8::NRT][t8::CT], int lane) {
+  constexpr int NX = DX == 0 ? 5 : 4;   // active x tiles per env quad
+  constexpr int NA = 2 * NX;            // active tiles
+  constexpr int A0 = DX < 0 ? 1 : 0;    // first accumulator x tile
+  constexpr int S0 = DX > 0 ? 1 : 0;    // first source x tile
+  constexpr int SB = (DX + 1) * 24;     // first k step of this column shift
+  const int q = lane >> 4, y = (lane & 15) >> 2, e = lane & 3;
+  int base, tst, sw;
+  tap_rows(S0 * 16 * TROWB, y, e, -1, base, tst, sw);
+  // active tile j: quad j / NX, x tile j % NX -> source tile index (in 16-row tiles from S0)
+  auto soff = [&](int j, int b, int ts) { return b + ((j / NX) * 5 + (j % NX)) * ts; };
+  bf16x8 afc[NA], afn[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + soff(j, base, tst) + ((q << 4) ^ sw));
+  constexpr int NC = TC / 32;
+#pragma unroll 1
+  for (int dyi = 0; dyi < 3; ++dyi) {
+    int nbase, ntst, nsw;
+    tap_rows(S0 * 16 * TROWB, y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int s = SB + dyi * NC + c;
+      bf16x8 w[t8::CT];
+#pragma unroll
+      for (int ct = 0; ct < t8::CT; ++ct) {
+        w[ct] = __builtin_bit_cast(bf16x8, bq[ct][c % TD]);
+        bq[ct][c % TD] = wp[ct][(size_t)(s + TD) * 64];
+      }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int at = (j / NX) * 5 + A0 + (j % NX);
+#pragma unroll
+        for (int ct = 0; ct < t8::CT; ++ct)
+          acc[at][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[ct], afc[j], acc[at][ct], 0, 0, 0);
+        if (c + 1 < NC)
+          afn[j] = *reinterpret_cast<const bf16x8*>(lds + soff(j, base, tst) + (((4 * (c + 1) + q) << 4) ^ sw));
+        else
+          afn[j] = *reinterpret_cast<const bf16x8*>(lds + soff(j, nbase, ntst) + ((q << 4) ^ nsw));
+      }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        if (j < t8::CT) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) afc[j] = afn[j];
+    }
+    base = nbase; tst = ntst; sw = nsw;
+  }
+}
+
+// one 3x3 conv of the tower over the 8-env image (in place). RESID: acc starts at bias + res.
+template <bool RESID>
+__device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const uint4* __restrict__ wconv,
+                                            const float* __restrict__ bconv, uint2 (&res)[t8::NRT][t8::CT],
+                                            int lane, int wave) {
+  const int q = lane >> 4, l16 = lane & 15;
+  const uint4* wp[t8::CT];
+  uint4 bq[t8::CT][TD];
+#pragma unroll
+  for (int ct = 0; ct < t8::CT; ++ct) {
+    wp[ct] = wconv + (size_t)(wave * t8::CT + ct) * TNS * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < TD; ++i) bq[ct][i] = wp[ct][(size_t)i * 64];
+  }
+  // D[channel 16 ct' + 4q + i][row 16 rt + l16], ct' = 4 wave + ct
+  f32x4 acc[t8::NRT][t8::CT];
+#pragma unroll
+  for (int ct = 0; ct < t8::CT; ++ct) {
+    const float4 b4 = *reinterpret_cast<const float4*>(bconv + (wave * t8::CT + ct) * 16 + 4 * q);
+#pragma unroll
+    for (int rt = 0; rt < t8::NRT; ++rt) {
+      f32x4 v = {b4.x, b4.y, b4.z, b4.w};
+      if (RESID) {
+        const uint2 r = res[rt][ct];
+        v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
+        v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
+      }
+      acc[rt][ct] = v;
+    }
+  }
+  tower8_dx<-1>(lds, wp, bq, acc, lane);
+  tower8_dx<0>(lds, wp, bq, acc, lane);
+  tower8_dx<1>(lds, wp, bq, acc, lane);
+  __syncthreads();  // every wave has read the whole image
+#pragma unroll
+  for (int rt = 0; rt < t8::NRT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < t8::CT; ++ct) {
+      const int n = (wave * t8::CT + ct) * 16 + 4 * q;
+      uint2* p = reinterpret_cast<uint2*>(lds + toff(rt * 16 + l16, n >> 3) + ((n & 7) << 1));
+      if (!RESID) res[rt][ct] = *p;  // block input at this position: conv2's residual
+      uint2 o;
+      o.x = (uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][0], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][1], 0.f)) << 16);
+      o.y = (uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][2], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][3], 0.f)) << 16);
+      *p = o;
+    }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[t8::BYTES];
+  __shared__ long long envoff[t8::E];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int env0 = blockIdx.x * t8::E;
+  const int nenv = min(t8::E, a.B - env0);
+  const int rows = nenv * 20;
+  if (tid < t8::E) {
+    const int b = env0 + (tid < nenv ? tid : 0);
+    long long off = (long long)b * a.in_env_stride;
+    if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
+    envoff[tid] = off;
+  }
+  __syncthreads();
+  {  // stage X: 160 rows x 32 chunks = 5120 chunks, 20 per thread (two batches of 10)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint4 v[10];
+#pragma unroll
+      for (int u = 0; u < 10; ++u) {
+        const int i = (h * 10 + u) * t8::NT + tid;
+        const int r = i >> 5, c = i & 31;
+        const bool ok = r < rows;
+        const int rr = ok ? r : 0;
+        v[u] = *reinterpret_cast<const uint4*>(a.in + envoff[rr / 20] + (long long)(rr % 20) * TC + c * 8);
+        if (!ok) v[u] = make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 10; ++u) {
+        const int i = (h * 10 + u) * t8::NT + tid;
+        const int r = i >> 5;
+        *reinterpret_cast<uint4*>(lds + toff(t8::row8(r / 20, r % 20), i & 31)) = v[u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) *reinterpret_cast<uint4*>(lds + t8::LZ + (u * t8::NT + tid) * 16) = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
+  constexpr size_t WCONV = (size_t)16 * TNS * 64;
+  uint2 res[t8::NRT][t8::CT];
+  for (int blk = 0; blk < a.nblocks; ++blk) {
+    tower8_conv<false>(lds, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, res, lane, wave);
+    tower8_conv<true>(lds, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, res, lane, wave);
+  }
+#pragma unroll 4
+  for (int u = 0; u < 20; ++u) {
+    const int i = u * t8::NT + tid;
+    const int r = i >> 5, c = i & 31;
+    if (r < rows)
+      *reinterpret_cast<uint4*>(a.out + (long long)(env0 + r / 20) * 20 * TC + (r % 20) * TC + c * 8) =
+          *reinterpret_cast<const uint4*>(lds + toff(t8::row8(r / 20, r % 20), c));
+  }
+}
+
+static int g_tower_variant = 0;  // 0 auto, 1 four-env kernel, 2 eight-env kernel
+
+static int tower_ncu() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  return ncu;
 }
 
 }  // namespace
 
 extern "C" {
 
-// nblocks residual blocks (256 ch, 4x5) fused; wf16: per conv [16][72][64][8] bf16 (+8 KB pad after
-// the last conv), bias: per conv [256] f32 (BN folded). in: env b at in + b*in_env_stride
-// (+ slot[b]*in_slot_stride); out: [B][20][256].
+// 0: pick by batch (default), 1: force the 4-env kernel, 2: force the 8-env kernel
+int mzba_tower_set_variant(int v) {
+  if (v < 0 || v > 2) return -1;
+  g_tower_variant = v;
+  return 0;
+}
+
+// kernel used for batch B: 1 four-env, 2 eight-env (B >= 8 x CUs: it halves the per-env weight stream
+// but needs that many envs to fill the chip). Both take agent.pack_tower_conv weights.
+int mzba_tower_plan(int B) {
+  if (B <= 0) return -1;
+  if (g_tower_variant) return g_tower_variant;
+  return B >= 8 * tower_ncu() ? 2 : 1;
+}
+
+// device workspace bytes mzba_tower needs for batch B (0 for both current kernels)
+long long mzba_tower_ws_bytes(int B) { return B > 0 ? 0 : -1; }
+
+// nblocks residual blocks (256 ch, 4x5) fused; wf16: per conv [16][72][64][8] bf16, k steps in the
+// (dx, dy) tap order of agent.pack_tower_conv (+8 KB pad after the last conv),
+// bias: per conv [256] f32 (BN folded). in: env b at in + b*in_env_stride (+ slot[b]*in_slot_stride);
+// out: [B][20][256]. ws: mzba_tower_ws_bytes(B) bytes of device scratch (may be null when 0).
 int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride, void* out,
-               const void* wf16, const float* bias, int nblocks, int B, hipStream_t stream) {
+               const void* wf16, const float* bias, int nblocks, int B, void* ws, long long ws_bytes,
+               hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && out && wf16 && bias, -1);
+  const int plan = mzba_tower_plan(B);
+  MZ_CHECK_ARG(plan > 0, -2);
   TowerArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (bf16_t*)out, (const bf16_t*)wf16, bias,
               nblocks, B};
-  hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
+  (void)ws;
+  (void)ws_bytes;
+  if (plan == 2) {
+    hipLaunchKernelGGL(tower8_kernel, dim3((B + t8::E - 1) / t8::E), dim3(t8::NT), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
+  }
   MZ_LAUNCH_CHECK();
   return 0;
 }

@@ -32,7 +32,10 @@ SIGNATURES = {
     "mzba_conv_lat_supported": [I, I, I, I, I],
     "mzba_conv_lat_set_variant": [I],
     "mzba_conv_lat": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
-    "mzba_tower": [P, LL, P, LL, P, P, P, I, I, P],
+    "mzba_tower": [P, LL, P, LL, P, P, P, I, I, P, LL, P],
+    "mzba_tower_plan": [I],
+    "mzba_tower_ws_bytes": [I],
+    "mzba_tower_set_variant": [I],
     "mzba_avgpool2": [I, P, P, I, I, I, I, P],
     "mzba_scale_state": [I, P, P, P, LL, P, I, LL, I, I, P],
     "mzba_heads": [I, I, P, P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, F, I, P],
@@ -51,6 +54,10 @@ SIGNATURES = {
 _lib = None
 
 
+# entry points that return something other than a status code
+RESTYPES = {"mzba_tower_ws_bytes": LL, "mzba_tower_plan": I}
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -60,7 +67,7 @@ def lib():
         for name, argt in SIGNATURES.items():
             fn = getattr(L, name)
             fn.argtypes = argt
-            fn.restype = ctypes.c_int
+            fn.restype = RESTYPES.get(name, ctypes.c_int)
         _lib = L
     return _lib
 

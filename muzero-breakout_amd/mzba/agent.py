@@ -43,6 +43,13 @@ def pack_lat16(wp, cout, ks, cin):
     return wp.reshape(cout // 16, 16, K // 32, 4, 8).transpose(0, 2, 3, 1, 4).reshape(-1)
 
 
+def pack_tower_conv(w):
+    """3x3 conv weight (OIHW, BN folded) -> the fused tower's packing: pack_lat16 with the taps
+    ordered (dx, dy) (tower.hip walks column shifts outermost)."""
+    cout, cin = w.shape[0], w.shape[1]
+    return pack_lat16(np.ascontiguousarray(w.transpose(0, 3, 2, 1)).reshape(cout, -1), cout, 3, cin)
+
+
 def _round64(c):
     return (c + 63) // 64 * 64
 
@@ -144,18 +151,22 @@ class PackedNets:
     def _tower(self, sd, prefix, n):
         if not self.tower_ok or n == 0:
             return None
-        wfs, bs = [], []
+        ws, bs = [], []
         for i in range(n):
             for k in (1, 2):
                 p = f"{prefix}.{i}"
                 alpha, beta = self._bn(sd, f"{p}.bn{k}")
-                w = sd[f"{p}.conv{k}.weight"] * alpha[:, None, None, None]
-                b = sd[f"{p}.conv{k}.bias"] * alpha + beta
-                wfs.append(pack_lat16(w.transpose(0, 2, 3, 1).reshape(256, -1), 256, 3, 256))
-                bs.append(b)
-        wf = np.concatenate(wfs + [np.zeros(LAT_PAD_ELEMS)])
-        return {"wf": torch.tensor(wf, dtype=torch.float32).to(self.tdt).to(self.device),
-                "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device), "n": n}
+                ws.append(sd[f"{p}.conv{k}.weight"] * alpha[:, None, None, None])
+                bs.append(sd[f"{p}.conv{k}.bias"] * alpha + beta)
+        return {"w": ws, "wf": {}, "n": n,
+                "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device)}
+
+    def tower_weights(self, tw, plan):
+        """Device weights of a tower in the packing of mzba_tower's plan (cached per plan)."""
+        if plan not in tw["wf"]:
+            wf = np.concatenate([pack_tower_conv(w) for w in tw["w"]] + [np.zeros(LAT_PAD_ELEMS)])
+            tw["wf"][plan] = torch.tensor(wf, dtype=torch.float32).to(self.tdt).to(self.device)
+        return tw["wf"][plan]
 
     def _linear(self, w, b, c):
         O, K = w.shape
@@ -197,6 +208,12 @@ class NetRunner:
         self.probe = None
         self.use_lat = True  # latent-resolution bf16 convs on conv_lat (False: generic implicit GEMM)
         self.use_tower = True  # dyn/pred residual towers as one fused launch each (bf16, C=256, 4x5)
+        self.tower_plan = self.tower_ws = None
+        if packed.tower_ok:
+            self.tower_plan = L.lib().mzba_tower_plan(B)
+            nb = L.lib().mzba_tower_ws_bytes(B)
+            self.tower_ws = torch.zeros(max(nb, 16), dtype=torch.uint8, device=dev)
+            self.tower_ws_bytes = nb
 
     # -- primitives --------------------------------------------------------------------
     def conv(self, x, layer, out, B, H, W, res=None, relu=True, slot=None, env_stride=None, slot_stride=0, act=None):
@@ -215,13 +232,14 @@ class NetRunner:
 
     def tower(self, tw, x, out):
         """All residual blocks of a dyn/pred tower in one launch (activations stay in LDS).
-        `out` may alias `x` (each workgroup reads its 4 envs before writing them)."""
+        `out` may alias `x` (every workgroup stages its envs before any of them is written)."""
         pr = self.probe
         if pr is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        L.call("mzba_tower", L.ptr(x), 20 * 256, None, 0, L.ptr(out), L.ptr(tw["wf"]), L.ptr(tw["b"]), tw["n"],
-               self.B, L.stream())
+        wf = self.p.tower_weights(tw, self.tower_plan)
+        L.call("mzba_tower", L.ptr(x), 20 * 256, None, 0, L.ptr(out), L.ptr(wf), L.ptr(tw["b"]), tw["n"],
+               self.B, L.ptr(self.tower_ws), self.tower_ws_bytes, L.stream())
         if pr is not None:
             e1.record()
             pr.append((e0, e1, 2 * tw["n"]))

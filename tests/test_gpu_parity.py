@@ -446,12 +446,13 @@ def test_dropin_modules_resolve_via_get_class():
     assert tuple(s.shape) == e.state_shape
 
 
+@pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("B,nblocks,gather", [(4, 1, False), (13, 3, True), (1024, 2, False)])
-def test_tower_matches_conv_chain(B, nblocks, gather):
+def test_tower_matches_conv_chain(B, nblocks, gather, variant):
     """Fused tower (activations LDS-resident across blocks) vs torch fp32 residual blocks with
     bf16-rounded weights and bf16 intermediates."""
     from mzba import _lib as L
-    from mzba.agent import pack_lat16
+    from mzba.agent import pack_tower_conv
     g = torch.Generator().manual_seed(B + nblocks)
     C, H, W = 256, 4, 5
     S1 = 3 if gather else 1
@@ -465,12 +466,23 @@ def test_tower_matches_conv_chain(B, nblocks, gather):
         t1 = bf(torch.relu(torch.nn.functional.conv2d(x, bf(ws[2 * k]), bs[2 * k], padding=1)))
         x = bf(torch.relu(torch.nn.functional.conv2d(t1, bf(ws[2 * k + 1]), bs[2 * k + 1], padding=1) + x))
     ref = x.permute(0, 2, 3, 1)
-    wf = np.concatenate([pack_lat16(w.permute(0, 2, 3, 1).reshape(C, -1).numpy(), C, 3, C) for w in ws]
+    L.call("mzba_tower_set_variant", variant)
+    plan = L.lib().mzba_tower_plan(B)
+    nb = L.lib().mzba_tower_ws_bytes(B)
+    L.call("mzba_tower_set_variant", 0)
+    assert plan == variant and nb == 0
+    wsb = torch.zeros(max(nb, 16), dtype=torch.uint8, device="cuda")
+    wf = np.concatenate([pack_tower_conv(w.numpy()) for w in ws]
                         + [np.zeros(8 * 64 * 8, np.float32)])
     d = dict(pool=pool.cuda(), slot=slot.cuda(), wf=torch.from_numpy(wf).to(torch.bfloat16).cuda(),
              b=torch.cat(bs).cuda())
     out = torch.empty(B, H, W, C, dtype=torch.bfloat16, device="cuda")
-    L.call("mzba_tower", L.ptr(d["pool"]), S1 * H * W * C, L.ptr(d["slot"]) if gather else None, H * W * C,
-           L.ptr(out), L.ptr(d["wf"]), L.ptr(d["b"]), nblocks, B, L.stream())
+    L.call("mzba_tower_set_variant", variant)
+    try:
+        L.call("mzba_tower", L.ptr(d["pool"]), S1 * H * W * C, L.ptr(d["slot"]) if gather else None, H * W * C,
+               L.ptr(out), L.ptr(d["wf"]), L.ptr(d["b"]), nblocks, B, L.ptr(wsb), nb, L.stream())
+        torch.cuda.synchronize()
+    finally:
+        L.call("mzba_tower_set_variant", 0)
     err = (out.float().cpu() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
     assert err < 3e-2, err

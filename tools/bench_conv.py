@@ -37,16 +37,20 @@ def run(B, H, W, Cin, Cout, ks, kind, iters=50):
             "tflops": fl / (ms * 1e-3) / 1e12}
 
 
-def run_tower(B, nblocks, iters=20):
-    from mzba.agent import pack_lat16  # noqa: F401
+def run_tower(B, nblocks, iters=20, variant=0):
     C = 256
+    L.call("mzba_tower_set_variant", variant)
+    nb = L.lib().mzba_tower_ws_bytes(B)
+    ws = torch.zeros(max(nb, 16), dtype=torch.uint8, device="cuda")
     x = torch.randn(B * 20 * C, device="cuda").to(torch.bfloat16)
     out = torch.empty_like(x)
     wf = (torch.randn(2 * nblocks * C * 2304 + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
     b = torch.zeros(2 * nblocks * C, device="cuda")
 
+
     def launch():
-        L.call("mzba_tower", L.ptr(x), 20 * C, None, 0, L.ptr(out), L.ptr(wf), L.ptr(b), nblocks, B, L.stream())
+        L.call("mzba_tower", L.ptr(x), 20 * C, None, 0, L.ptr(out), L.ptr(wf), L.ptr(b), nblocks, B, L.ptr(ws), nb,
+               L.stream())
     for _ in range(3):
         launch()
     torch.cuda.synchronize()
@@ -56,14 +60,16 @@ def run_tower(B, nblocks, iters=20):
     torch.cuda.synchronize()
     ms = np.median([a.elapsed_time(c) for a, c in ev])
     fl = 2.0 * B * 20 * C * 2304 * 2 * nblocks
-    return {"kind": "tower", "B": B, "nblocks": nblocks, "us": ms * 1e3, "us_per_conv": ms * 1e3 / (2 * nblocks),
+    L.call("mzba_tower_set_variant", 0)
+    return {"kind": "tower", "variant": variant, "B": B, "nblocks": nblocks, "us": ms * 1e3, "us_per_conv": ms * 1e3 / (2 * nblocks),
             "tflops": fl / (ms * 1e-3) / 1e12}
 
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "tower":
-        for s in [(1024, 1), (1024, 14), (4096, 14)]:
-            print(json.dumps(run_tower(*s)))
+        for s in [(1024, 1), (1024, 14), (2048, 14), (4096, 14)]:
+            for v in (1, 2):
+                print(json.dumps(run_tower(*s, variant=v)))
         print(json.dumps(run(1024, 4, 5, 256, 256, 3, "lat")))
         sys.exit(0)
     shapes = [(1024, 4, 5, 256, 256, 3), (4096, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 1),

@@ -18,8 +18,11 @@ if len(sys.argv) > 2 and sys.argv[2] == "tower":
     out = torch.empty_like(x)
     wf = (torch.randn(2 * nb * C * 9 * C + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
     b = torch.zeros(2 * nb * C, device="cuda")
+    nws = L.lib().mzba_tower_ws_bytes(B)
+    ws = torch.zeros(max(nws, 16), dtype=torch.uint8, device="cuda")
     for _ in range(20):
-        L.call("mzba_tower", L.ptr(x), H * W * C, None, 0, L.ptr(out), L.ptr(wf), L.ptr(b), nb, B, L.stream())
+        L.call("mzba_tower", L.ptr(x), H * W * C, None, 0, L.ptr(out), L.ptr(wf), L.ptr(b), nb, B, L.ptr(ws), nws,
+               L.stream())
     torch.cuda.synchronize()
     print("done tower", B, nb)
     sys.exit(0)

@@ -9,8 +9,13 @@ import sys
 
 import numpy as np
 
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+
 
 def counter(dirpath, name, kname):
+    if glob.glob(f"{dirpath}/**/*.db", recursive=True):  # rocpd SQLite output (rocprofv3 default here)
+        from rocpd_report import counter_values
+        return counter_values(dirpath, name, kname)
     vals = []
     for f in glob.glob(f"{dirpath}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
