@@ -96,7 +96,7 @@ def main():
         loop.capture()  # one acting step (~S x 65 launches) as a HIP graph, replayed per step
 
     # ---- visit-count match + CPU baseline on a bounded sample (rank 0, N=1 only) -------
-    cpu_info, match = None, None
+    cpu_info, match, match_f32 = None, None, None
     want_cpu = rank == 0 and world == 1 and not args.no_cpu
     if want_cpu:
         nb = min(args.cpu_envs, B)
@@ -120,6 +120,15 @@ def main():
         cpu_s = time.perf_counter() - t0
         if gpu_counts is not None:
             match = float((gpu_counts == oc).all(1).mean())
+        # the same envs through the f32 parity path of this build (same keyed noise / tie-breaks)
+        from mzba.search import MCTSSearchVec
+        agent32 = MuZeroAgent(mcfg, dtype="f32", device=agent.device)
+        agent32.load_state_dict(sd)
+        h32 = agent32.create_hidden_state_root(torch.from_numpy(np.ascontiguousarray(x)).to(agent.device))
+        s32 = MCTSSearchVec(cfg, agent32, None, seed=args.seed, env_offset=0)
+        s32.search_id = sid
+        _, c32 = s32.search(h32)
+        match_f32 = float((c32.numpy() == oc).all(1).mean())
         cpu_info = {"value": nb / cpu_s, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
                     "sample": f"oracle (numpy f32) representation + {args.sims}-sim search for {nb} envs of the "
                               f"bench's own state, 1 acting step ({cpu_s:.1f} s)"}
@@ -192,6 +201,7 @@ def main():
                          "launches_timed": len(probe)},
             "cpu_baseline": cpu_info,
             "visit_count_match": match,
+            "visit_count_match_f32_path": match_f32,
             "launch": "eager" if args.no_graph else "hip-graph replay (probe step eager)",
             "whole_step_mfma_frac": (B * world * (3.4446e9 + 0.6738e9 + args.sims * 1.3610e9) * args.steps / dt / 1e12)
                                     / (PEAK_BF16_TFLOPS * world),

@@ -108,6 +108,41 @@ long long mzba_tower_ws_bytes(int B);
 int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride, void* out,
                const void* wf16, const float* bias, int nblocks, int B, void* ws, long long ws_bytes,
                hipStream_t stream);
+/* Fused per-simulation nets around the tower (4-env kernel, plan 1): the dynamics ConvBlock
+ * before it and the reward / policy / value heads after it run in the same launch, so one
+ * dynamics step and one prediction step are one kernel each (networks.py:151-167, 200-241,
+ * 314-328; utils.py:74-81). */
+typedef struct mzba_tower_ext {
+  /* prologue: dynamics ConvBlock 259->256 = 3x3 conv (tower packing) + bias + per-(position,
+   * action) bias table [20][A][256] f32 (the action planes folded in), ReLU; w0 = NULL: none */
+  const void* w0;
+  const float* b0;
+  const float* act_bias;
+  const int32_t* act;
+  int A;
+  /* epilogue: 0 none (out = tower output); 1 dynamics: reward ConvBlock1x1 256->256 (we1/be1) +
+   * Linear lw[0] -> lO[0] logits -> decode to dec[0][B], then the per-env min-max scaled latent
+   * to out and to pool slot pool_slot; 2 prediction: policy ConvBlock3x3 256->128 (we3/be3) and
+   * value ConvBlock1x1 256->128 (we1/be1), Linear lw[0] -> softmax dec[0][B][lO[0]],
+   * Linear lw[1] -> decode dec[1][B] */
+  int epilogue;
+  const void* we3;
+  const float* be3;
+  const void* we1;
+  const float* be1;
+  const void* lw[2];      /* bf16 [16][20*C], (position, channel) order, rows >= lO zero */
+  const float* lb[2];
+  int lO[2];
+  float* logits[2];       /* optional [B][lO] */
+  float* dec[2];
+  void* pool;             /* bf16 latent node pool (epilogue 1), may be NULL */
+  long long pool_env_stride;
+  int pool_slot;
+  float smin, smax;       /* support range */
+} mzba_tower_ext;
+int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
+                     void* out, const void* wf16, const float* bias, int nblocks, int B,
+                     const mzba_tower_ext* ext, hipStream_t stream);
 
 /* nn.AvgPool2d(2, 2) (networks.py:44), NHWC. */
 int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream);

@@ -70,3 +70,22 @@ MZ_DEV int mz_randbelow(uint32_t env, uint32_t stream, uint32_t step, uint32_t c
   uint64_t x = mz_u32(env, stream, step, call, seed) >> 8;
   return (int)((x * (uint64_t)n) >> 24);
 }
+
+// ScalarTransforms.inverted_softmax_expectation (utils.py:74-81) for n <= 16 logits: softmax,
+// expectation over torch.linspace(smin, smax, n), then the reference's inverse transform.
+MZ_DEV float decode_support(const float* l, int n, float smin, float smax) {
+  float m = l[0];
+  for (int i = 1; i < n; ++i) m = fmaxf(m, l[i]);
+  float e[16];
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) { e[i] = expf(l[i] - m); s = s + e[i]; }
+  const float step = (smax - smin) / (float)(n - 1);
+  float x = 0.f;
+  for (int i = 0; i < n; ++i) {
+    float sup = smin + (float)i * step;  // torch.linspace(smin, smax, n)
+    x = x + (e[i] / s) * sup;
+  }
+  float t = fabsf(x) + 0.999f;  // utils.py:28, epsilon 0.001
+  float sg = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+  return sg * (t * t - 1.f);
+}

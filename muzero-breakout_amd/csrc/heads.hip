@@ -21,23 +21,6 @@ struct HeadArgs {
   float smin, smax;
 };
 
-MZ_DEV float decode_support(const float* l, int n, float smin, float smax) {
-  float m = l[0];
-  for (int i = 1; i < n; ++i) m = fmaxf(m, l[i]);
-  float e[MAXO];
-  float s = 0.f;
-  for (int i = 0; i < n; ++i) { e[i] = expf(l[i] - m); s = s + e[i]; }
-  const float step = (smax - smin) / (float)(n - 1);
-  float x = 0.f;
-  for (int i = 0; i < n; ++i) {
-    float sup = smin + (float)i * step;  // torch.linspace(smin, smax, n)
-    x = x + (e[i] / s) * sup;
-  }
-  float t = fabsf(x) + 0.999f;  // utils.py:28, epsilon 0.001
-  float sg = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
-  return sg * (t * t - 1.f);
-}
-
 template <typename T>
 __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a) {
   const int b = blockIdx.x, tid = threadIdx.x;

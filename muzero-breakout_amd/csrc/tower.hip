@@ -57,6 +57,7 @@ struct TowerArgs {
   const float* bias;         // per conv: [256]
   int nblocks;               // residual blocks (2 convs each)
   int B;
+  mzba_tower_ext x;          // fused prologue / epilogue (4-env kernel); all zero = plain tower
 };
 
 // LDS row of (env e, latent position p = 5y + x) and the byte offset of (row, 16-B chunk)
@@ -133,23 +134,54 @@ __device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int sr
   }
 }
 
-template <bool RESID>
+// the 8 k steps of a 1x1 conv (centre tap only: every row valid, all 5 tiles)
+__device__ __forceinline__ void tower_center(const uint8_t* __restrict__ lds, int srcimg, const uint4* __restrict__ wp0,
+                                             const uint4* __restrict__ wp1, uint4 (&b0q)[TD], uint4 (&b1q)[TD],
+                                             f32x4 (&acc0)[TR], f32x4 (&acc1)[TR], int lane) {
+  const int q = lane >> 4, key = lane & 15;
+  const int base = srcimg + key * TROWB, sw = key << 4;
+  bf16x8 afc[TR], afn[TR];
+#pragma unroll
+  for (int j = 0; j < TR; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const bf16x8 w0 = __builtin_bit_cast(bf16x8, b0q[c % TD]);
+    const bf16x8 w1 = __builtin_bit_cast(bf16x8, b1q[c % TD]);
+    if (c + TD < 8) {
+      b0q[c % TD] = wp0[(size_t)(c + TD) * 64];
+      b1q[c % TD] = wp1[(size_t)(c + TD) * 64];
+    }
+#pragma unroll
+    for (int j = 0; j < TR; ++j) {
+      acc0[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[j], w0, acc0[j], 0, 0, 0);
+      acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[j], w1, acc1[j], 0, 0, 0);
+      if (c + 1 < 8)
+        afn[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
+    }
+#pragma unroll
+    for (int j = 0; j < TR; ++j) afc[j] = afn[j];
+  }
+}
+
+// One conv of the 4-env kernel, this wave's two 16-channel column tiles ct0, ct0 + 1 of a weight pack
+// with `tns` k steps per tile (72: 3x3, 8: 1x1); pack column n lands on image channel nout + n.
+// MODE 0: bias; 1: bias + residual (the destination image); 2: bias + act_bias[pos][act[e]][n].
+// Epilogue: ReLU -> bf16 -> dst.
+template <int MODE, bool CENTER>
 __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg, int dstimg,
-                                           const uint4* __restrict__ wconv, const float* __restrict__ bconv,
-                                           int lane, int wave) {
+                                           const uint4* __restrict__ wconv, int tns, int ct0,
+                                           const float* __restrict__ bconv, int nout,
+                                           const float* __restrict__ actb, const int* acts, int A, int lane) {
   const int q = lane >> 4, l16 = lane & 15;
-#if TOWER_ABLATE == 3  // diagnostic only: waves w and w+4 stream the same weights (half the L2 bytes)
-  const int ct0 = 2 * (wave & 3), ct1 = 2 * (wave & 3) + 1;
-#else
-  const int ct0 = 2 * wave, ct1 = 2 * wave + 1;  // 16-column tiles of this wave
-#endif
-  const uint4* wp0 = wconv + (size_t)ct0 * TNS * 64 + lane;
-  const uint4* wp1 = wconv + (size_t)ct1 * TNS * 64 + lane;
+  const int ct1 = ct0 + 1;
+  const uint4* wp0 = wconv + (size_t)ct0 * tns * 64 + lane;
+  const uint4* wp1 = wconv + (size_t)ct1 * tns * 64 + lane;
   uint4 b0q[TD], b1q[TD];
 #pragma unroll
   for (int i = 0; i < TD; ++i) { b0q[i] = wp0[(size_t)i * 64]; b1q[i] = wp1[(size_t)i * 64]; }
-  // accumulator init: bias (+ residual X for conv2); D[row = 4q + i][col = l16] of tile rt
+  // accumulator init; D[row = 4q + i][col = l16] of tile rt: latent (y = q, x = rt), env i
   const int n0 = ct0 * 16 + l16, n1 = ct1 * 16 + l16;
+  const int c0 = nout + n0, c1 = nout + n1;  // image channels
   const float bb0 = bconv[n0], bb1 = bconv[n1];
   f32x4 acc0[TR], acc1[TR];
 #pragma unroll
@@ -157,44 +189,155 @@ __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       float r0 = bb0, r1 = bb1;
-      if (RESID) {
+      if (MODE == 1) {
         const int row = rt * 16 + 4 * q + i;
-        r0 = r0 + bf16_to_f32(*(reinterpret_cast<const bf16_t*>(lds + dstimg + toff(row, n0 >> 3)) + (n0 & 7)));
-        r1 = r1 + bf16_to_f32(*(reinterpret_cast<const bf16_t*>(lds + dstimg + toff(row, n1 >> 3)) + (n1 & 7)));
+        r0 = r0 + bf16_to_f32(*(reinterpret_cast<const bf16_t*>(lds + dstimg + toff(row, c0 >> 3)) + (c0 & 7)));
+        r1 = r1 + bf16_to_f32(*(reinterpret_cast<const bf16_t*>(lds + dstimg + toff(row, c1 >> 3)) + (c1 & 7)));
+      } else if (MODE == 2) {
+        const float* t = actb + ((size_t)(q * 5 + rt) * A + acts[i]) * TC;
+        r0 = r0 + t[n0];
+        r1 = r1 + t[n1];
       }
       acc0[rt][i] = r0;
       acc1[rt][i] = r1;
     }
-  tower_dx<-1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
-  tower_dx<0>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
-  tower_dx<1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
-  // epilogue: ReLU -> bf16 -> dst (T for conv1, X in place for conv2)
+  if (CENTER) {
+    tower_center(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+  } else {
+    tower_dx<-1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+    tower_dx<0>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+    tower_dx<1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+  }
 #pragma unroll
   for (int rt = 0; rt < TR; ++rt)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = rt * 16 + 4 * q + i;
-      *(reinterpret_cast<bf16_t*>(lds + dstimg + toff(row, n0 >> 3)) + (n0 & 7)) = f32_to_bf16(fmaxf(acc0[rt][i], 0.f));
-      *(reinterpret_cast<bf16_t*>(lds + dstimg + toff(row, n1 >> 3)) + (n1 & 7)) = f32_to_bf16(fmaxf(acc1[rt][i], 0.f));
+      *(reinterpret_cast<bf16_t*>(lds + dstimg + toff(row, c0 >> 3)) + (c0 & 7)) = f32_to_bf16(fmaxf(acc0[rt][i], 0.f));
+      *(reinterpret_cast<bf16_t*>(lds + dstimg + toff(row, c1 >> 3)) + (c1 & 7)) = f32_to_bf16(fmaxf(acc1[rt][i], 0.f));
     }
+}
+
+// Linear heads on an LDS image (networks.py:147, 207, 221): head h reads image channels
+// [hc0[h], hc0[h] + hC[h]) of the 20 positions of each env, K = 20 hC[h] in (position, channel)
+// order against bf16 weights lw[h][16][K]. One v_mfma_f32_16x16x32_bf16 per 32-deep k step
+// (A rows = the 4 envs, zero-padded to 16; B cols = outputs), k steps split over the 8 waves,
+// partial sums added through LDS in wave order; then softmax (dec_kind 0) or support decode (1).
+__device__ __forceinline__ void tower_heads(const TowerArgs& a, const uint8_t* __restrict__ lds, int img,
+                                            int nh, const int (&hc0)[2], const int (&hC)[2], const int (&kind)[2],
+                                            float (*part)[4][16], float (*lg)[4][16], int env0, int nenv,
+                                            int tid) {
+  const int lane = tid & 63, wave = tid >> 6, q = lane >> 4, el = lane & 15;
+  for (int hd = 0; hd < nh; ++hd) {
+    const int C = hC[hd], K = 20 * C, nk = K / 32;
+    const bf16_t* wr = reinterpret_cast<const bf16_t*>(a.x.lw[hd]) + (size_t)el * K;
+    const int er = el < nenv ? el : 0;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int s = wave; s < nk; s += 8) {
+      const int k = s * 32 + q * 8;
+      const int pos = k / C, c = hc0[hd] + (k - pos * C);
+      bf16x8 av = *reinterpret_cast<const bf16x8*>(lds + img + toff(trow(er, pos), c >> 3));
+      if (el >= 4) av = bf16x8{};
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + k);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+    }
+    if (q == 0)  // D[row = env i][col = output el]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part[wave * 4 + i][0][el] = acc[i];
+    __syncthreads();
+    if (tid < 64) {
+      const int e = tid >> 4, o = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v = v + part[w * 4 + e][0][o];
+      if (o < a.x.lO[hd]) lg[hd * 4 + e][0][o] = v + a.x.lb[hd][o];
+    }
+    __syncthreads();
+  }
+  if (tid < 4 * nh) {
+    const int hd = tid >> 2, e = tid & 3, b = env0 + e;
+    if (e < nenv) {
+      const int O = a.x.lO[hd];
+      float l[16];
+      for (int o = 0; o < O; ++o) {
+        l[o] = lg[hd * 4 + e][0][o];
+        if (a.x.logits[hd]) a.x.logits[hd][(size_t)b * O + o] = l[o];
+      }
+      if (kind[hd] == 0) {
+        float m = l[0];
+        for (int o = 1; o < O; ++o) m = fmaxf(m, l[o]);
+        float ex[16], sum = 0.f;
+        for (int o = 0; o < O; ++o) { ex[o] = expf(l[o] - m); sum = sum + ex[o]; }
+        for (int o = 0; o < O; ++o) a.x.dec[hd][(size_t)b * O + o] = ex[o] / sum;
+      } else {
+        a.x.dec[hd][b] = decode_support(l, O, a.x.smin, a.x.smax);
+      }
+    }
+  }
+}
+
+// _scale_state (networks.py:314-328) of the tower output X: per env (h - min) / (max - min + 1e-8)
+// in f32, bf16 result to out (and to the pool slot). 128 threads per env, 5 chunks each.
+__device__ __forceinline__ void tower_scale(const TowerArgs& a, const uint8_t* __restrict__ lds, float (*mm)[2][2],
+                                            int env0, int nenv, int tid) {
+  const int e = tid >> 7, t = tid & 127;
+  uint4 v[5];
+  float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int i = u * 128 + t, p = i >> 5, c = i & 31;
+    v[u] = *reinterpret_cast<const uint4*>(lds + LDS_X + toff(trow(e, p), c));
+    const bf16_t* h = reinterpret_cast<const bf16_t*>(&v[u]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const float f = bf16_to_f32(h[j]); mn = fminf(mn, f); mx = fmaxf(mx, f); }
+  }
+  for (int o = 32; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
+  if ((t & 63) == 0) { mm[e][t >> 6][0] = mn; mm[e][t >> 6][1] = mx; }
+  __syncthreads();
+  mn = fminf(mm[e][0][0], mm[e][1][0]);
+  mx = fmaxf(mm[e][0][1], mm[e][1][1]);
+  if (e >= nenv) return;
+  const float den = (mx - mn) + 1e-8f;
+  const int b = env0 + e;
+  bf16_t* o1 = a.out + (size_t)b * 20 * TC;
+  bf16_t* o2 = a.x.pool ? reinterpret_cast<bf16_t*>(a.x.pool) + (size_t)b * a.x.pool_env_stride +
+                              (size_t)a.x.pool_slot * 20 * TC
+                        : nullptr;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int i = u * 128 + t, p = i >> 5, c = i & 31;
+    uint4 r = v[u];
+    bf16_t* h = reinterpret_cast<bf16_t*>(&r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = f32_to_bf16((bf16_to_f32(h[j]) - mn) / den);
+    *reinterpret_cast<uint4*>(o1 + p * TC + c * 8) = r;
+    if (o2) *reinterpret_cast<uint4*>(o2 + p * TC + c * 8) = r;
+  }
 }
 
 __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];  // X | T | 16 zero rows
   __shared__ long long envoff[TE];
+  __shared__ int acts[TE];
+  __shared__ float part[32][4][16];  // head partial sums [wave * 4 + env][.][output]; min/max scratch
+  __shared__ float lg[8][4][16];     // head logits [head * 4 + env][.][output]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int env0 = blockIdx.x * TE;
   const int nenv = min(TE, a.B - env0);
   const int rows = nenv * 20;
+  const bool pro = a.x.w0 != nullptr;
   if (tid < TE) {
     const int b = env0 + (tid < nenv ? tid : 0);
     long long off = (long long)b * a.in_env_stride;
     if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
     envoff[tid] = off;
+    acts[tid] = pro ? a.x.act[b] : 0;
   }
   __syncthreads();
-  // stage X: global row r = 20 e + p (80 rows x 32 chunks = 2560 chunks, 5 per thread); zero block
+  // stage X (80 rows x 32 chunks = 2560 chunks, 5 per thread; into T when a prologue conv follows)
+  // and zero the zero block
   {
+    const int stg = pro ? LDS_T : LDS_X;
     uint4 v[5];
 #pragma unroll
     for (int u = 0; u < 5; ++u) {
@@ -209,18 +352,46 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
     for (int u = 0; u < 5; ++u) {
       const int i = u * TNT + tid;
       const int r = i >> 5;
-      *reinterpret_cast<uint4*>(lds + LDS_X + toff(trow(r / 20, r % 20), i & 31)) = v[u];
+      *reinterpret_cast<uint4*>(lds + stg + toff(trow(r / 20, r % 20), i & 31)) = v[u];
     }
     *reinterpret_cast<uint4*>(lds + LDS_Z + tid * 16) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
+  if (pro) {  // dynamics ConvBlock: T -> X
+    tower_conv<2, false>(lds, LDS_T, LDS_X, reinterpret_cast<const uint4*>(a.x.w0), TNS, 2 * wave, a.x.b0, 0,
+                         a.x.act_bias, acts, a.x.A, lane);
+    __syncthreads();
+  }
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;  // uint4 per conv
   for (int blk = 0; blk < a.nblocks; ++blk) {
-    tower_conv<false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, lane, wave);
+    tower_conv<0, false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, TNS, 2 * wave, a.bias + (2 * blk) * TC, 0,
+                         nullptr, nullptr, 0, lane);
     __syncthreads();
-    tower_conv<true>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, lane, wave);
+    tower_conv<1, false>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, TNS, 2 * wave, a.bias + (2 * blk + 1) * TC,
+                         0, nullptr, nullptr, 0, lane);
     __syncthreads();
+  }
+  if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1 (X -> T), Linear + decode, scaled latent
+    tower_conv<0, true>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we1), 8, 2 * wave, a.x.be1, 0,
+                        nullptr, nullptr, 0, lane);
+    __syncthreads();
+    const int hc0[2] = {0, 0}, hC[2] = {TC, 0}, kind[2] = {1, 0};
+    tower_heads(a, lds, LDS_T, 1, hc0, hC, kind, part, lg, env0, nenv, tid);
+    tower_scale(a, lds, reinterpret_cast<float(*)[2][2]>(&part[0][0][0]), env0, nenv, tid);
+    return;
+  }
+  if (a.x.epilogue == 2) {  // prediction: policy 3x3 -> T[0,128), value 1x1 -> T[128,256); Linears
+    if (wave < 4)
+      tower_conv<0, false>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we3), TNS, 2 * wave, a.x.be3, 0,
+                           nullptr, nullptr, 0, lane);
+    else
+      tower_conv<0, true>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we1), 8, 2 * (wave - 4), a.x.be1,
+                          128, nullptr, nullptr, 0, lane);
+    __syncthreads();
+    const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
+    tower_heads(a, lds, LDS_T, 2, hc0, hC, kind, part, lg, env0, nenv, tid);
+    return;
   }
   // write the tower output (16-B chunks, rows < rows)
 #pragma unroll
@@ -455,7 +626,7 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
   const int plan = mzba_tower_plan(B);
   MZ_CHECK_ARG(plan > 0, -2);
   TowerArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (bf16_t*)out, (const bf16_t*)wf16, bias,
-              nblocks, B};
+              nblocks, B, mzba_tower_ext{}};
   (void)ws;
   (void)ws_bytes;
   if (plan == 2) {
@@ -463,6 +634,29 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
   } else {
     hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
   }
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+// Dynamics / prediction step as one launch of the 4-env kernel (see include/mzba.h). Returns -4 when the
+// batch is planned on the 8-env kernel (the caller then runs the unfused sequence).
+int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
+                     void* out, const void* wf16, const float* bias, int nblocks, int B, const mzba_tower_ext* ext,
+                     hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && wf16 && bias && ext, -1);
+  MZ_CHECK_ARG(mzba_tower_plan(B) == 1, -4);
+  const mzba_tower_ext& x = *ext;
+  MZ_CHECK_ARG(x.epilogue >= 0 && x.epilogue <= 2, -2);
+  MZ_CHECK_ARG(!x.w0 || (x.b0 && x.act_bias && x.act && x.A > 0), -3);
+  MZ_CHECK_ARG(x.epilogue != 0 || out, -3);
+  MZ_CHECK_ARG(x.epilogue != 1 || (out && x.we1 && x.be1 && x.lw[0] && x.lb[0] && x.dec[0] && x.lO[0] > 1 &&
+                                   x.lO[0] <= 16), -3);
+  MZ_CHECK_ARG(x.epilogue != 2 || (x.we3 && x.be3 && x.we1 && x.be1 && x.lw[0] && x.lw[1] && x.lb[0] && x.lb[1] &&
+                                   x.dec[0] && x.dec[1] && x.lO[0] >= 1 && x.lO[0] <= 16 && x.lO[1] > 1 &&
+                                   x.lO[1] <= 16), -3);
+  TowerArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (bf16_t*)out, (const bf16_t*)wf16, bias,
+              nblocks, B, x};
+  hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
   MZ_LAUNCH_CHECK();
   return 0;
 }

@@ -35,6 +35,7 @@ SIGNATURES = {
     "mzba_tower": [P, LL, P, LL, P, P, P, I, I, P, LL, P],
     "mzba_tower_plan": [I],
     "mzba_tower_ws_bytes": [I],
+    "mzba_tower_fused": [P, LL, P, LL, P, P, P, I, I, P, P],
     "mzba_tower_set_variant": [I],
     "mzba_avgpool2": [I, P, P, I, I, I, I, P],
     "mzba_scale_state": [I, P, P, P, LL, P, I, LL, I, I, P],
@@ -52,6 +53,17 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+class TowerExt(ctypes.Structure):
+    """include/mzba.h mzba_tower_ext (fused dynamics / prediction step around the tower)."""
+    _fields_ = [("w0", P), ("b0", P), ("act_bias", P), ("act", P), ("A", I),
+                ("epilogue", I),
+                ("we3", P), ("be3", P), ("we1", P), ("be1", P),
+                ("lw", P * 2), ("lb", P * 2), ("lO", I * 2),
+                ("logits", P * 2), ("dec", P * 2),
+                ("pool", P), ("pool_env_stride", LL), ("pool_slot", I),
+                ("smin", F), ("smax", F)]
 
 
 # entry points that return something other than a status code

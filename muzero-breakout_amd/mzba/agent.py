@@ -7,6 +7,7 @@ per-(pixel, action) bias table, and the Linear heads permuted from torch's (c,h,
 flatten order to the NHWC (h,w,c) order. Activations are NHWC on the device in bf16
 (throughput path) or f32 (parity path), computed by the HIP kernels in libmzba.so.
 """
+import ctypes
 import math
 
 import numpy as np
@@ -101,6 +102,39 @@ class PackedNets:
         self.val_conv = self._conv(sd["pred_net.value_head.0.conv.weight"], sd["pred_net.value_head.0.conv.bias"],
                                    self._bn(sd, "pred_net.value_head.0.bn"))
         self.val_lin = self._linear(sd["pred_net.value_head.2.weight"], sd["pred_net.value_head.2.bias"], self.c1 // 2)
+        self.fused = self._fused(sd, w[:, :cmain])
+
+    def _fused(self, sd, w0):
+        """Weights of the fused dynamics / prediction steps (mzba_tower_fused): the dynamics
+        ConvBlock and the head convs in the tower packings, next to the existing linear heads."""
+        if not (self.dyn_tower and self.pred_tower and "wb" in self.rew_lin and "wb" in self.pol_lin
+                and "wb" in self.val_lin and self.c1 // 2 == 128 and self.ns <= 16):
+            return None
+
+        def fold(cw, cb, bn):
+            alpha, beta = self._bn(sd, bn)
+            return cw * alpha[:, None, None, None], cb * alpha + beta
+
+        def dev(x, dt=None):
+            return torch.tensor(np.asarray(x), dtype=torch.float32).to(dt or torch.float32).to(self.device)
+
+        def pack3(cw):
+            return dev(np.concatenate([pack_tower_conv(cw), np.zeros(LAT_PAD_ELEMS)]), self.tdt)
+
+        def pack1(cw):
+            co, ci = cw.shape[:2]
+            return dev(np.concatenate([pack_lat16(cw.reshape(co, ci), co, 1, ci), np.zeros(LAT_PAD_ELEMS)]), self.tdt)
+
+        a0, b0 = self._bn(sd, "dyn_net.conv_block.bn")
+        rw, rb = fold(sd["dyn_net.reward_head.0.conv.weight"], sd["dyn_net.reward_head.0.conv.bias"],
+                      "dyn_net.reward_head.0.bn")
+        pw, pb = fold(sd["pred_net.policy_head.0.conv.weight"], sd["pred_net.policy_head.0.conv.bias"],
+                      "pred_net.policy_head.0.bn")
+        vw, vb = fold(sd["pred_net.value_head.0.conv.weight"], sd["pred_net.value_head.0.conv.bias"],
+                      "pred_net.value_head.0.bn")
+        return {"w0": pack3(w0 * a0[:, None, None, None]), "b0": self.dyn0["b"], "act_bias": self.dyn0["act_bias"],
+                "A": self.dyn0["A"], "rw": pack1(rw), "rb": dev(rb), "pw": pack3(pw), "pb": dev(pb),
+                "vw": pack1(vw), "vb": dev(vb)}
 
     # -- packing helpers ---------------------------------------------------------------
     @staticmethod
@@ -208,6 +242,7 @@ class NetRunner:
         self.probe = None
         self.use_lat = True  # latent-resolution bf16 convs on conv_lat (False: generic implicit GEMM)
         self.use_tower = True  # dyn/pred residual towers as one fused launch each (bf16, C=256, 4x5)
+        self.use_fused = True  # ... with the dynamics ConvBlock and the heads inside (4-env kernel)
         self.tower_plan = self.tower_ws = None
         if packed.tower_ok:
             self.tower_plan = L.lib().mzba_tower_plan(B)
@@ -282,12 +317,50 @@ class NetRunner:
         L.call("mzba_scale_state", self.dt, L.ptr(cur), L.ptr(out_latent), L.ptr(pool), pool_env_stride, None, 0,
                0, B, n, L.stream())
 
+    def fused_ok(self):
+        return self.use_fused and self.use_tower and self.p.fused is not None and self.tower_plan == 1
+
+    def _ext(self, epilogue):
+        p, f = self.p, self.p.fused
+        x = L.TowerExt()
+        x.epilogue = epilogue
+        x.smin, x.smax = float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"])
+        if epilogue == 1:
+            x.w0, x.b0, x.act_bias, x.A = L.ptr(f["w0"]), L.ptr(f["b0"]), L.ptr(f["act_bias"]), f["A"]
+            x.we1, x.be1 = L.ptr(f["rw"]), L.ptr(f["rb"])
+            x.lw[0], x.lb[0], x.lO[0] = L.ptr(p.rew_lin["wb"]), L.ptr(p.rew_lin["b"]), p.rew_lin["O"]
+        else:
+            x.we3, x.be3, x.we1, x.be1 = L.ptr(f["pw"]), L.ptr(f["pb"]), L.ptr(f["vw"]), L.ptr(f["vb"])
+            x.lw[0], x.lb[0], x.lO[0] = L.ptr(p.pol_lin["wb"]), L.ptr(p.pol_lin["b"]), p.pol_lin["O"]
+            x.lw[1], x.lb[1], x.lO[1] = L.ptr(p.val_lin["wb"]), L.ptr(p.val_lin["b"]), p.val_lin["O"]
+        return x
+
+    def _fused_call(self, tw, src, env_stride, slot, slot_stride, out, x):
+        pr = self.probe
+        if pr is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        wf = self.p.tower_weights(tw, self.tower_plan)
+        L.call("mzba_tower_fused", L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(out), L.ptr(wf),
+               L.ptr(tw["b"]), tw["n"], self.B, ctypes.byref(x), L.stream())
+        if pr is not None:
+            e1.record()
+            pr.append((e0, e1, 2 * tw["n"] + (1 if x.w0 else 0)))
+
     def dynamics(self, parent_src, act, out_latent, r_dec, r_logits=None, slot=None, env_stride=None, slot_stride=0,
                  pool=None, pool_env_stride=0, pool_slot=0):
         """DynamicsNetwork + _scale_state (networks.py:151-167, 282-298) on NHWC latents.
         parent_src (+ slot gather) -> out_latent (scaled), r_dec (decoded reward)."""
         B, H, W = self.B, self.p.lh, self.p.lw
         p = self.p
+        if self.fused_ok():  # one launch: ConvBlock + 14 blocks + reward head + scale
+            x = self._ext(1)
+            x.act = L.ptr(act)
+            x.logits[0], x.dec[0] = L.ptr(r_logits), L.ptr(r_dec)
+            x.pool, x.pool_env_stride, x.pool_slot = L.ptr(pool), pool_env_stride, pool_slot
+            self._fused_call(p.dyn_tower, parent_src, H * W * p.c1 if env_stride is None else env_stride, slot,
+                             slot_stride, out_latent, x)
+            return
         self.conv(parent_src, p.dyn0, self.x, B, H, W, relu=True, slot=slot, env_stride=env_stride,
                   slot_stride=slot_stride, act=act)
         if p.dyn_tower is not None and self.use_tower:
@@ -313,6 +386,12 @@ class NetRunner:
         """PredictionNetwork (networks.py:225-241) + decode (mcts.py:97-100, 197-199)."""
         B, H, W = self.B, self.p.lh, self.p.lw
         p = self.p
+        if self.fused_ok():  # one launch: 14 blocks + policy / value heads
+            x = self._ext(2)
+            x.logits[0], x.dec[0] = L.ptr(p_logits), L.ptr(pi)
+            x.logits[1], x.dec[1] = L.ptr(v_logits), L.ptr(v)
+            self._fused_call(p.pred_tower, h, H * W * p.c1, None, 0, None, x)
+            return
         cur = h
         if p.pred_tower is not None and self.use_tower:
             self.tower(p.pred_tower, cur, self.x)

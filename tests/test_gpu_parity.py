@@ -200,6 +200,48 @@ def test_nets_bf16_close():
     pl, vl = ag.evaluate_state(dev(d["h"]))
     assert np.abs(pl.cpu().numpy() - d["p0"]).max() < 0.05
     assert np.abs(vl.cpu().numpy() - d["v0"]).max() < 0.05
+    planes = N.encode_action_planes(d["action"], mcfg["latent_resolution"])
+    h1, rl = ag.hidden_state_transition(dev(d["h"]), dev(planes))
+    assert np.abs(h1.cpu().numpy() - d["h1"]).max() < 0.05
+    assert np.abs(rl.cpu().numpy() - d["r1"]).max() < 0.05
+
+
+@pytest.mark.parametrize("B", [13, 1024])
+def test_fused_steps_match_unfused(B):
+    """mzba_tower_fused (dynamics ConvBlock + tower + reward head + scale in one launch; tower +
+    policy/value heads in one launch) vs the per-layer launch sequence, both bf16, same inputs."""
+    from mzba.agent import MuZeroAgent
+    mcfg = default_config()["model"]
+    ag = MuZeroAgent(mcfg, dtype="bf16")
+    ag.load_state_dict(init_state_dict(mcfg, 7))
+    rn = ag.runner(B, 16, 20)
+    assert rn.fused_ok()
+    S1, n = 3, 20 * 256
+    g = torch.Generator().manual_seed(B)
+    pool0 = torch.rand(B, S1 + 1, n, generator=g).to(torch.bfloat16).cuda()
+    slot = torch.randint(0, S1, (B,), generator=g, dtype=torch.int32).cuda()
+    act = torch.randint(0, 3, (B,), generator=g, dtype=torch.int32).cuda()
+    res = {}
+    try:
+        for fused in (False, True):
+            rn.use_fused = fused
+            pool = pool0.clone()
+            out = torch.empty(B, n, dtype=torch.bfloat16, device="cuda")
+            f = lambda *s: torch.full(s, float("nan"), device="cuda")  # noqa: E731
+            r, rl, pi, v, plg, vlg = f(B), f(B, 11), f(B, 3), f(B), f(B, 3), f(B, 11)
+            rn.dynamics(pool, act, out, r, rl, slot=slot, env_stride=(S1 + 1) * n, slot_stride=n, pool=pool,
+                        pool_env_stride=(S1 + 1) * n, pool_slot=S1)
+            rn.prediction(out, pi, v, plg, vlg)
+            torch.cuda.synchronize()
+            res[fused] = [t.float().cpu() for t in (out, pool[:, S1], r, rl, pi, v, plg, vlg)]
+    finally:
+        rn.use_fused = True
+    names = ["latent", "pool", "r", "r_logits", "pi", "v", "p_logits", "v_logits"]
+    for nm, a, b in zip(names, res[False], res[True]):
+        assert torch.isfinite(b).all(), nm
+        err = (a - b).abs().max().item()
+        assert err < 0.05, (nm, err)
+    assert torch.equal(res[True][0], res[True][1])  # scaled latent also written to the pool slot
 
 
 def test_conv_kernel_vs_torch_fp32_random():

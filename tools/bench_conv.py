@@ -72,8 +72,16 @@ if __name__ == "__main__":
                 print(json.dumps(run_tower(*s, variant=v)))
         print(json.dumps(run(1024, 4, 5, 256, 256, 3, "lat")))
         sys.exit(0)
-    shapes = [(1024, 4, 5, 256, 256, 3), (4096, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 1),
-              (1024, 4, 5, 256, 128, 3), (1024, 8, 10, 256, 256, 3)]
+    shapes = [(1024, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 1), (1024, 8, 10, 256, 256, 3),
+              (1024, 16, 20, 256, 256, 3), (1024, 16, 20, 128, 128, 3), (1024, 16, 20, 64, 128, 3),
+              (1024, 16, 20, 128, 256, 3)]
+    if len(sys.argv) > 1 and sys.argv[1] == "rep":
+        for s in shapes[2:]:
+            for kind in ("gen", "lat"):
+                if kind == "lat" and not L.lib().mzba_conv_lat_supported(*s[1:]):
+                    continue
+                print(json.dumps(run(*s, kind)))
+        sys.exit(0)
     for s in shapes:
         for kind in ("gen", "lat"):
             print(json.dumps(run(*s, kind)))
