@@ -98,6 +98,13 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
  * whole tower. wf16: per conv [16 col tiles][72 k steps][64 lanes][8] bf16 with taps ordered (dx, dy)
  * (agent.pack_tower_conv), convs back to back, + 8*64*8 padding elements; bias: per conv [256] f32 (BN folded). in: env b at in + b*in_env_stride
  * (+ slot[b]*in_slot_stride); out: [B][20][256] bf16. */
+/* Representation-net 3x3 convs at 16x20 (networks.py:38-99, 7-35): one workgroup per (env, 10-column
+ * band), 160 rows x Cout, weights in the tower packing (agent.pack_tower_conv, + 8 KB pad).
+ * out = [relu](conv(in) + bias [+ res]); NHWC bf16, env strides 320*Cin / 320*Cout; out may alias res. */
+int mzba_conv_band_supported(int H, int W, int Cin, int Cout, int ks);
+int mzba_conv_band(const void* in, const void* wf16, const float* bias, const void* res, void* out, int B, int H,
+                   int W, int Cin, int Cout, int relu, hipStream_t stream);
+
 /* kernel choice for experiments/tests: 0 by batch (default), 1 four-env kernel, 2 eight-env kernel */
 int mzba_tower_set_variant(int v);
 /* kernel mzba_tower runs for batch B: 1 four-env (workgroup = 4 envs, 8 waves), 2 eight-env (B >= 8 x CUs;

@@ -1,0 +1,236 @@
+// Representation-net convs at the full 16x20 resolution (bf16, gfx950 MFMA): "band" kernel.
+//
+// RepresentationNetwork runs 3x3 convs 128->128, 128->256 and 256->256 at 16x20 (networks.py:38-99;
+// ConvBlock / ResidualBlock :7-35), M = B*320 rows. A workgroup owns one env and 10 output columns
+// x0..x0+9 (160 rows) x all Cout channels:
+//   * the input band (12 columns x0-1..x0+10, zero outside the image, x all 16 rows x Cin) is staged
+//     once into LDS; LDS row = 16 j + y for source column j. A 16-row MFMA tile is one image COLUMN,
+//     so a tap (dy, dx) maps output column t to source column t + 1 + dx whole and shifts rows by dy
+//     inside it; rows leaving 0..15 read a 16-row zero block;
+//   * weights are the MFMA A operand (pack: agent.pack_tower_conv, taps (dx, dy)), activations the
+//     B operand: B column j of every tile carries image row SIG[j], and LDS row y has its 16-B
+//     chunks XOR-swizzled by KEY[y]. (SIG, KEY) is a pair for which every ds_read_b128 lane group
+//     hits 16 distinct bank slots for all three row shifts (found by search; 16x20's 1-row shifts
+//     defeat the plain row-XOR swizzle);
+//   * 4 waves (one per SIMD), each all 10 column tiles x Cout/64 channel tiles: every weight fragment
+//     fetched from L2 feeds 10 MFMAs;
+//   * epilogue through LDS: + bias (+ residual staged coalesced), optional ReLU, bf16, then coalesced
+//     16-B stores.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int BH = 16, BW = 20;      // image
+constexpr int XT = 10;               // output columns per workgroup
+constexpr int NSRC = XT + 2;         // staged source columns (with the halo)
+constexpr int BNT = 256;             // 4 waves
+constexpr int TDB = 4;               // weight ring depth (k steps)
+constexpr unsigned long long SIG = 0x93f5a4260ce8b7d1ull;  // nibble j: image row of B column j
+constexpr unsigned long long KEY = 0x35a0e1879df426bcull;  // nibble y: swizzle key of image row y
+
+MZ_DEV int nib(unsigned long long t, int i) { return (int)((t >> (4 * i)) & 15); }
+
+struct BandArgs {
+  const bf16_t* in;   // [B][320][Cin]
+  const bf16_t* wf;   // tower packing [Cout/16][9*Cin/32][64][8] (+ pad)
+  const float* bias;  // [Cout]
+  const bf16_t* res;  // optional [B][320][Cout]
+  bf16_t* out;        // [B][320][Cout]
+  int B, relu;
+};
+
+template <int CIN, int COUT>
+struct BandGeo {
+  static constexpr int RB = CIN * 2;               // LDS bytes per source row
+  static constexpr int NCH = CIN / 8;              // 16-B chunks per source row
+  static constexpr int NC = CIN / 32;              // k steps per tap
+  static constexpr int TNS = 9 * NC;               // k steps per channel tile
+  static constexpr int CTW = COUT / 64;            // 16-channel tiles per wave
+  static constexpr int OB = COUT * 2;              // LDS bytes per output row
+  static constexpr int LZ = NSRC * 16 * RB;        // zero block offset
+  static constexpr int IN_BYTES = LZ + 16 * RB;
+  static constexpr int OUT_BYTES = XT * 16 * OB;
+  static constexpr int BYTES = IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES;
+};
+
+// the 3 dy x NC k steps of column shift DX
+template <int CIN, int COUT, int DX>
+__device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, const uint4* const (&wp)[COUT / 64],
+                                        uint4 (&bq)[COUT / 64][TDB], f32x4 (&acc)[XT][COUT / 64], int lane) {
+  using G = BandGeo<CIN, COUT>;
+  constexpr int CTW = G::CTW, NC = G::NC;
+  constexpr int SB = (DX + 1) * 3 * NC;
+  const int q = lane >> 4, ys = nib(SIG, lane & 15);
+  auto rows = [&](int dy, int& base, int& tst, int& sw) {
+    const int yy = ys + dy;
+    const bool ok = (unsigned)yy < (unsigned)BH;
+    base = ok ? ((1 + DX) * 16 + yy) * G::RB : G::LZ + (yy & 15) * G::RB;
+    tst = ok ? 16 * G::RB : 0;
+    sw = nib(KEY, yy & 15) << 4;
+  };
+  int base, tst, sw;
+  rows(-1, base, tst, sw);
+  bf16x8 afc[XT], afn[XT];
+#pragma unroll
+  for (int t = 0; t < XT; ++t) afc[t] = *reinterpret_cast<const bf16x8*>(lds + base + t * tst + ((q << 4) ^ sw));
+#pragma unroll 1
+  for (int dyi = 0; dyi < 3; ++dyi) {
+    int nbase, ntst, nsw;
+    rows(dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int s = SB + dyi * NC + c;
+      bf16x8 w[CTW];
+#pragma unroll
+      for (int ct = 0; ct < CTW; ++ct) {
+        w[ct] = __builtin_bit_cast(bf16x8, bq[ct][c % TDB]);
+        bq[ct][c % TDB] = wp[ct][(size_t)(s + TDB) * 64];
+      }
+#pragma unroll
+      for (int t = 0; t < XT; ++t) {
+#pragma unroll
+        for (int ct = 0; ct < CTW; ++ct)
+          acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[ct], afc[t], acc[t][ct], 0, 0, 0);
+        if (c + 1 < NC)
+          afn[t] = *reinterpret_cast<const bf16x8*>(lds + base + t * tst + (((4 * (c + 1) + q) << 4) ^ sw));
+        else
+          afn[t] = *reinterpret_cast<const bf16x8*>(lds + nbase + t * ntst + ((q << 4) ^ nsw));
+      }
+#pragma unroll
+      for (int t = 0; t < XT; ++t) {
+        __builtin_amdgcn_sched_group_barrier(0x008, CTW / 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, CTW - CTW / 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        if (t < CTW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < XT; ++t) afc[t] = afn[t];
+    }
+    base = nbase; tst = ntst; sw = nsw;
+  }
+}
+
+template <int CIN, int COUT>
+__global__ __launch_bounds__(BNT, 1) void band_conv_kernel(BandArgs a) {
+  using G = BandGeo<CIN, COUT>;
+  constexpr int CTW = G::CTW;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x >> 1, x0 = (blockIdx.x & 1) * XT;
+  // stage the band: NSRC*16 rows x NCH chunks (UB loads in flight per thread), then the zero block
+  {
+    constexpr int N = NSRC * 16 * G::NCH;
+    constexpr int UB = N % (8 * BNT) == 0 ? 8 : 4;
+    static_assert(N % (UB * BNT) == 0, "staging batches");
+    const bf16_t* src = a.in + (size_t)b * BH * BW * CIN;
+#pragma unroll 1
+    for (int i0 = 0; i0 < N; i0 += UB * BNT) {
+      uint4 v[UB];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int i = i0 + u * BNT + tid;
+        const int row = i / G::NCH, ch = i % G::NCH;
+        const int x = x0 - 1 + (row >> 4), y = row & 15;
+        const bool ok = (unsigned)x < (unsigned)BW;
+        v[u] = *reinterpret_cast<const uint4*>(src + ((size_t)(y * BW + (ok ? x : 0)) * CIN + ch * 8));
+        if (!ok) v[u] = make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int i = i0 + u * BNT + tid;
+        const int row = i / G::NCH, ch = i % G::NCH;
+        *reinterpret_cast<uint4*>(lds + row * G::RB + ((ch ^ nib(KEY, row & 15)) << 4)) = v[u];
+      }
+    }
+    for (int i = tid; i < 16 * G::NCH; i += BNT) *reinterpret_cast<uint4*>(lds + G::LZ + i * 16) = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+  const uint4* wp[CTW];
+  uint4 bq[CTW][TDB];
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) {
+    wp[ct] = reinterpret_cast<const uint4*>(a.wf) + (size_t)(wave * CTW + ct) * G::TNS * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < TDB; ++i) bq[ct][i] = wp[ct][(size_t)i * 64];
+  }
+  f32x4 acc[XT][CTW];
+#pragma unroll
+  for (int t = 0; t < XT; ++t)
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  band_dx<CIN, COUT, -1>(lds, wp, bq, acc, lane);
+  band_dx<CIN, COUT, 0>(lds, wp, bq, acc, lane);
+  band_dx<CIN, COUT, 1>(lds, wp, bq, acc, lane);
+  __syncthreads();  // the band is no longer read
+  // output tile in LDS: row 16 t + y, 16-B chunks swizzled by KEY[y]
+  constexpr int ONCH = COUT / 8;
+  bf16_t* gout = a.out + (size_t)b * BH * BW * COUT;
+  if (a.res) {  // stage the residual tile (coalesced)
+    const bf16_t* gres = a.res + (size_t)b * BH * BW * COUT;
+    for (int i = tid; i < XT * 16 * ONCH; i += BNT) {
+      const int row = i / ONCH, ch = i % ONCH, t = row >> 4, y = row & 15;
+      *reinterpret_cast<uint4*>(lds + row * G::OB + ((ch ^ nib(KEY, y)) << 4)) =
+          *reinterpret_cast<const uint4*>(gres + (size_t)(y * BW + x0 + t) * COUT + ch * 8);
+    }
+    __syncthreads();
+  }
+  {
+    const int q = lane >> 4, ys = nib(SIG, lane & 15), ky = nib(KEY, ys);
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) {
+      const int n = (wave * CTW + ct) * 16 + 4 * q;  // D[channel n + i][column j = lane & 15]
+      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + n);
+#pragma unroll
+      for (int t = 0; t < XT; ++t) {
+        uint2* p = reinterpret_cast<uint2*>(lds + (t * 16 + ys) * G::OB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1));
+        float v0 = acc[t][ct][0] + b4.x, v1 = acc[t][ct][1] + b4.y, v2 = acc[t][ct][2] + b4.z, v3 = acc[t][ct][3] + b4.w;
+        if (a.res) {
+          const uint2 r = *p;
+          v0 += __uint_as_float(r.x << 16); v1 += __uint_as_float(r.x & 0xffff0000u);
+          v2 += __uint_as_float(r.y << 16); v3 += __uint_as_float(r.y & 0xffff0000u);
+        }
+        if (a.relu) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
+        uint2 o;
+        o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+        o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
+        *p = o;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < XT * 16 * ONCH; i += BNT) {
+    const int row = i / ONCH, ch = i % ONCH, t = row >> 4, y = row & 15;
+    *reinterpret_cast<uint4*>(gout + (size_t)(y * BW + x0 + t) * COUT + ch * 8) =
+        *reinterpret_cast<const uint4*>(lds + row * G::OB + ((ch ^ nib(KEY, y)) << 4));
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mzba_conv_band_supported(int H, int W, int Cin, int Cout, int ks) {
+  return H == BH && W == BW && ks == 3 && (Cin == 128 || Cin == 256) && (Cout == 128 || Cout == 256);
+}
+
+// 3x3 conv, stride 1, pad 1, on B images of 16x20 (NHWC bf16, env stride 320*Cin / 320*Cout):
+// out = [relu](conv(in, W) + bias [+ res]); weights in the tower packing (+8 KB pad). out may not alias in.
+int mzba_conv_band(const void* in, const void* wf16, const float* bias, const void* res, void* out, int B, int H,
+                   int W, int Cin, int Cout, int relu, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && in && wf16 && bias && out && in != out && mzba_conv_band_supported(H, W, Cin, Cout, 3), -1);
+  BandArgs a{(const bf16_t*)in, (const bf16_t*)wf16, bias, (const bf16_t*)res, (bf16_t*)out, B, relu};
+  dim3 grid(2 * B);
+  if (Cin == 256 && Cout == 256) hipLaunchKernelGGL((band_conv_kernel<256, 256>), grid, dim3(BNT), 0, stream, a);
+  else if (Cin == 128 && Cout == 256) hipLaunchKernelGGL((band_conv_kernel<128, 256>), grid, dim3(BNT), 0, stream, a);
+  else if (Cin == 128 && Cout == 128) hipLaunchKernelGGL((band_conv_kernel<128, 128>), grid, dim3(BNT), 0, stream, a);
+  else hipLaunchKernelGGL((band_conv_kernel<256, 128>), grid, dim3(BNT), 0, stream, a);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

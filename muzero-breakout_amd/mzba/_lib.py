@@ -36,6 +36,8 @@ SIGNATURES = {
     "mzba_tower_plan": [I],
     "mzba_tower_ws_bytes": [I],
     "mzba_tower_fused": [P, LL, P, LL, P, P, P, I, I, P, P],
+    "mzba_conv_band_supported": [I, I, I, I, I],
+    "mzba_conv_band": [P, P, P, P, P, I, I, I, I, I, I, P],
     "mzba_tower_set_variant": [I],
     "mzba_avgpool2": [I, P, P, I, I, I, I, P],
     "mzba_scale_state": [I, P, P, P, LL, P, I, LL, I, I, P],

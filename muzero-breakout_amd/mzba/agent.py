@@ -73,11 +73,11 @@ class PackedNets:
             p = f"rep_net.blocks.{i}"
             if kind == "conv":
                 cout = self.c0 if nconv == 0 else self.c1
-                self.rep.append(("conv", self._conv(sd[p + ".weight"], sd[p + ".bias"], None)))
+                self.rep.append(("conv", self._conv(sd[p + ".weight"], sd[p + ".bias"], None, band=True)))
                 nconv += 1
                 cin = cout
             elif kind == "res":
-                self.rep.append(("res", self._res(sd, p)))
+                self.rep.append(("res", self._res(sd, p, band=True)))
             else:
                 self.rep.append(("pool", None))
         # dynamics (networks.py:117-149)
@@ -143,7 +143,7 @@ class PackedNets:
         alpha = g / np.sqrt(v + BN_EPS)
         return alpha, b - m * alpha
 
-    def _conv(self, w, bias, bn, act_w=None):
+    def _conv(self, w, bias, bn, act_w=None, band=False):
         cout, cin, k, _ = w.shape
         if bn is not None:
             alpha, beta = bn
@@ -176,11 +176,15 @@ class PackedNets:
         if self.dtype == "bf16" and cout % 32 == 0 and cin_p in (64, 128, 256):
             layer["wf"] = torch.tensor(pack_lat(wp.reshape(cout, -1), cout, k, cin_p),
                                        dtype=torch.float32).to(self.tdt).to(self.device)
+        if band and self.dtype == "bf16" and k == 3 and cin in (128, 256) and cout in (128, 256):
+            # representation convs at full resolution: the band kernel's packing (tower order)
+            layer["wt"] = torch.tensor(np.concatenate([pack_tower_conv(w), np.zeros(LAT_PAD_ELEMS)]),
+                                       dtype=torch.float32).to(self.tdt).to(self.device)
         return layer
 
-    def _res(self, sd, p):
-        return (self._conv(sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], self._bn(sd, p + ".bn1")),
-                self._conv(sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], self._bn(sd, p + ".bn2")))
+    def _res(self, sd, p, band=False):
+        return (self._conv(sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], self._bn(sd, p + ".bn1"), band=band),
+                self._conv(sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], self._bn(sd, p + ".bn2"), band=band))
 
     def _tower(self, sd, prefix, n):
         if not self.tower_ok or n == 0:
@@ -243,6 +247,7 @@ class NetRunner:
         self.use_lat = True  # latent-resolution bf16 convs on conv_lat (False: generic implicit GEMM)
         self.use_tower = True  # dyn/pred residual towers as one fused launch each (bf16, C=256, 4x5)
         self.use_fused = True  # ... with the dynamics ConvBlock and the heads inside (4-env kernel)
+        self.use_band = True  # 16x20 representation convs on the band kernel
         self.tower_plan = self.tower_ws = None
         if packed.tower_ok:
             self.tower_plan = L.lib().mzba_tower_plan(B)
@@ -255,6 +260,11 @@ class NetRunner:
         s = L.stream()
         env_stride = H * W * layer["cin"] if env_stride is None else env_stride
         ab = layer.get("act_bias")
+        if ("wt" in layer and self.use_band and slot is None and env_stride == H * W * layer["cin"] and ab is None
+                and L.lib().mzba_conv_band_supported(H, W, layer["cin"], layer["cout"], layer["ks"])):
+            L.call("mzba_conv_band", L.ptr(x), L.ptr(layer["wt"]), L.ptr(layer["b"]), L.ptr(res), L.ptr(out), B, H, W,
+                   layer["cin"], layer["cout"], 1 if relu else 0, s)
+            return
         if "wf" in layer and self.use_lat and L.lib().mzba_conv_lat_supported(H, W, layer["cin"], layer["cout"],
                                                                              layer["ks"]):
             L.call("mzba_conv_lat", L.ptr(x), env_stride, L.ptr(slot), slot_stride, L.ptr(layer["wf"]),

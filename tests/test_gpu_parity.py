@@ -244,6 +244,33 @@ def test_fused_steps_match_unfused(B):
     assert torch.equal(res[True][0], res[True][1])  # scaled latent also written to the pool slot
 
 
+@pytest.mark.parametrize("Cin,Cout,resid,relu", [(128, 128, False, True), (128, 256, False, False),
+                                                   (256, 256, True, True), (256, 128, False, True)])
+def test_band_conv_vs_torch_fp32(Cin, Cout, resid, relu):
+    """16x20 band kernel vs a plain torch fp32 conv (bf16-rounded operands), incl. residual + ReLU."""
+    from mzba import _lib as L
+    from mzba.agent import pack_tower_conv, LAT_PAD_ELEMS
+    B, H, W = 5, 16, 20
+    g = torch.Generator().manual_seed(Cin + Cout)
+    bf = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    x = bf(torch.randn(B, Cin, H, W, generator=g))
+    w = bf(torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5)
+    b = torch.randn(Cout, generator=g)
+    res = bf(torch.randn(B, Cout, H, W, generator=g))
+    ref = torch.nn.functional.conv2d(x, w, b, padding=1) + (res if resid else 0)
+    ref = torch.relu(ref) if relu else ref
+    d = dict(x=x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda(),
+             w=torch.from_numpy(np.concatenate([pack_tower_conv(w.numpy()), np.zeros(LAT_PAD_ELEMS, np.float32)]))
+             .to(torch.bfloat16).cuda(), b=b.cuda(), r=res.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda())
+    out = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+    assert L.lib().mzba_conv_band_supported(H, W, Cin, Cout, 3)
+    L.call("mzba_conv_band", L.ptr(d["x"]), L.ptr(d["w"]), L.ptr(d["b"]), L.ptr(d["r"]) if resid else None,
+           L.ptr(out), B, H, W, Cin, Cout, 1 if relu else 0, L.stream())
+    got = out.float().cpu().permute(0, 3, 1, 2)
+    err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+    assert err < 1e-2, err
+
+
 def test_conv_kernel_vs_torch_fp32_random():
     """Raw conv op vs a plain torch fp32 conv, ragged M (B*HW not a tile multiple), 1x1 and 3x3."""
     from mzba import _lib as L

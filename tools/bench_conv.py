@@ -17,8 +17,14 @@ def run(B, H, W, Cin, Cout, ks, kind, iters=50):
     w = (torch.randn(Cout * K + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
     b = torch.zeros(Cout, device="cuda")
 
+    wt = None
+    if kind == "band":
+        wt = (torch.randn(Cout * K + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
+
     def launch():
-        if kind == "lat":
+        if kind == "band":
+            L.call("mzba_conv_band", L.ptr(x), L.ptr(wt), L.ptr(b), None, L.ptr(out), B, H, W, Cin, Cout, 1, L.stream())
+        elif kind == "lat":
             L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(w), L.ptr(b), None, None, 0, L.ptr(x)
                    if Cin == Cout else None, L.ptr(out), B, H, W, Cin, Cout, ks, 1, L.stream())
         else:
@@ -77,8 +83,10 @@ if __name__ == "__main__":
               (1024, 16, 20, 128, 256, 3)]
     if len(sys.argv) > 1 and sys.argv[1] == "rep":
         for s in shapes[2:]:
-            for kind in ("gen", "lat"):
+            for kind in ("gen", "lat", "band"):
                 if kind == "lat" and not L.lib().mzba_conv_lat_supported(*s[1:]):
+                    continue
+                if kind == "band" and not L.lib().mzba_conv_band_supported(*s[1:]):
                     continue
                 print(json.dumps(run(*s, kind)))
         sys.exit(0)
