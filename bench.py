@@ -42,7 +42,97 @@ def parse():
     ap.add_argument("--cpu-envs", type=int, default=16, help="bounded oracle sample (cpu_baseline + match rate)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
+    ap.add_argument("--workload", default="acting", choices=["acting", "env"],
+                    help="acting: the whole acting loop (headline); env: env step + render + frame stack only "
+                         "(configs 1/3, HBM roofline)")
+    ap.add_argument("--height", type=int, default=None, help="env workload frame height (default 84)")
+    ap.add_argument("--width", type=int, default=None, help="env workload frame width (default 84)")
+    ap.add_argument("--hist", type=int, default=4, help="env workload frame-stack length")
     return ap.parse_args()
+
+
+def env_bytes(H, W):
+    """SURVEY §8(d) algorithmic HBM bytes per env-step: the H*W uint8 frame write, the compact
+    state read + write (2 x 16 B), the action (8 B) and reward/done/valid (8 B)."""
+    return H * W + 2 * 16 + 8 + 8
+
+
+def run_env(args, world, rank, local):
+    """Configs 1/3: B envs x (step + render + frame-stack push) per step, no search.
+    `value` = env-steps/s over all ranks; roofline = algorithmic bytes / kernel time vs HBM."""
+    sys.path.insert(0, os.path.join(ROOT, "muzero-breakout_amd"))
+    from mzba.config import default_config
+    from mzba.env import CompactBreakout
+    from mzba import _lib as L
+    H, W = args.height or 84, args.width or 84
+    B = args.envs
+    cfg = default_config()
+    dev = torch.device(f"cuda:{local}")
+    env = CompactBreakout(cfg["environment"], B, args.hist, H, W, seed=args.seed, env_offset=rank * B, device=dev)
+    env.reset(0)
+    g = torch.Generator(device=dev).manual_seed(args.seed + rank)
+    acts = torch.randint(0, 3, (args.warmup + args.steps, B), device=dev, generator=g)
+    for i in range(args.warmup):
+        env.step(acts[i], i == 0)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(torch.cuda.current_stream())
+        env.step(acts[args.warmup + i], False)
+        ev[i][1].record(torch.cuda.current_stream())
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    kms = float(np.median([a.elapsed_time(c) for a, c in ev]))
+    achieved = B * env_bytes(H, W) / (kms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle.env import BreakoutEnvOracle, convert_to_grayscale
+        nb = min(B, 256)
+        e = BreakoutEnvOracle({**cfg["environment"], "n_parallel": nb})
+        e.height, e.width = H, W
+        s, _ = e.reset(e.reset_params(args.seed, 0))
+        done = np.zeros(nb, dtype=bool)
+        rng = np.random.default_rng(args.seed)
+        n, c0 = 0, time.perf_counter()
+        while time.perf_counter() - c0 < 10.0 and n < 2000:
+            s, r, done, v = e.step(s, rng.integers(0, 3, nb), done)
+            convert_to_grayscale(s)
+            n += 1
+        cs = time.perf_counter() - c0
+        cpu = {"value": nb * n / cs, "unit": "env-steps/s", "cores": 1, "kind": "port",
+               "sample": f"oracle numpy env (batched like parallel_breakout.py) + grayscale, {nb} envs x {n} steps "
+                         f"at {H}x{W} ({cs:.1f} s)"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "env-steps/sec, env step + render + frame stack only (SURVEY configs 1/3)",
+            "value": world * B * args.steps / dt, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic: seeded resets, uniform random actions",
+            "config": {"workload": f"{B} envs/GPU x {H}x{W} Breakout, {args.hist}-frame stack, no search",
+                       "envs_per_gpu": B},
+            "roofline": {"bound": "hbm", "kernel": "env_step_compact_kernel (step + render + history push)",
+                         "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
+                         "traffic": None, "bytes_per_env_step": env_bytes(H, W), "avg_launch_ms": kms},
+            "cpu_baseline": cpu,
+        }))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cfg_name(B, S):
+    """Which BASELINE config an acting-loop run is (per-GPU batch and sims)."""
+    return {(1024, 50): "config 2", (4096, 50): "config 4 (per-GPU share)", (4096, 200): "config 5 (bf16)"}.get(
+        (B, S), "custom")
 
 
 def conv_flops(B, hw, C):
@@ -57,6 +147,8 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.workload == "env":
+        return run_env(args, world, rank, local)
     from mzba.config import default_config
     from mzba.weights import init_state_dict
     from mzba.agent import MuZeroAgent
@@ -188,7 +280,8 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic: seeded random-init reference-architecture nets, seeded Breakout episodes",
-            "config": {"workload": f"config 2: {B} envs/GPU x {args.sims} MCTS sims, 16x20 Breakout, 32-frame stack",
+            "config": {"workload": f"{cfg_name(B, args.sims)}: {B} envs/GPU x {args.sims} MCTS sims, 16x20 Breakout, "
+                                   "32-frame stack",
                        "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
                        "parallelism": f"env-sharded x{world}, RCCL all-gather of trajectory records"},
             "roofline": {"bound": "mfma",

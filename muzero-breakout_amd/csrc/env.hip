@@ -200,13 +200,14 @@ __global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_f
 }
 
 // Phase 1: one thread per env, all rules on the compact state (same op order as above).
-// Phase 2: the block renders its 256 envs' frames (16 B per lane per store) and pushes
-// them into the history ring when the env is recorded this step.
+// Phase 2: the block renders its E envs' frames (16 B per lane per store) and pushes
+// them into the history ring when the env is recorded this step. E (<= 256) is chosen by the
+// launcher so that the grid fills the chip and a block has ~1-4 stores per lane.
 template <int MAXW>
 __global__ __launch_bounds__(256) void env_step_compact_kernel(
     Compact cs, const int64_t* __restrict__ action, float* __restrict__ reward, float* __restrict__ valid,
     uint8_t* __restrict__ cur_frame, History hist, Sink sink, int first_step_arg, int B, int H, int W, int pw,
-    int brick_rows, RewardCfg rc, const int32_t* __restrict__ ctx) {
+    int brick_rows, RewardCfg rc, const int32_t* __restrict__ ctx, int E) {
   // graph replay: the episode row t comes from the device context; the sink pointers are the
   // (T, B, ...) bases and row t is selected here; t == 0 is the first step
   const int first_step = ctx ? (ctx[2] == 0) : first_step_arg;
@@ -219,9 +220,9 @@ __global__ __launch_bounds__(256) void env_step_compact_kernel(
   __shared__ uint64_t s_br[256][MAXW];
   __shared__ uint8_t s_done[256], s_rec[256];
   const int t = threadIdx.x;
-  const int b = blockIdx.x * 256 + t;
+  const int b = blockIdx.x * E + t;
   const int nw = cs.nw;
-  if (b < B) {
+  if (t < E && b < B) {
     const bool was_done = cs.done[b] != 0;
     const int p0 = was_done ? 0 : cs.paddle[b];  // argmax of an empty row is 0 (:177)
     const int64_t a = action[b];
@@ -302,25 +303,34 @@ __global__ __launch_bounds__(256) void env_step_compact_kernel(
   // phase 2: render. Frame rows are HW bytes; lanes write 16 B (HW % 16 == 0 required).
   const int HW = H * W;
   const int chunks = HW / 16;
-  const int nenv = min(256, B - blockIdx.x * 256);
+  const int nenv = min(E, B - blockIdx.x * E);
   for (int i = t; i < nenv * chunks; i += 256) {
     const int e = i / chunks, c = i - e * chunks;
-    const int gb = blockIdx.x * 256 + e;
-    uint32_t wv[4];
+    const int gb = blockIdx.x * E + e;
+    uint32_t wv[4] = {0u, 0u, 0u, 0u};
+    // most chunks lie between the brick rows and the paddle row: all zero unless the ball is there
+    const int p0 = c * 16;
+    const int ballp = s_by[e] * W + s_bx[e];
+    const bool plain = p0 >= brick_rows * W && p0 + 16 <= (H - 1) * W;
+    if (plain) {
+      const int o = ballp - p0;
+      if (o >= 0 && o < 16) wv[o >> 2] = (uint32_t)gray_code(false, true, false) << (8 * (o & 3));
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      uint32_t word = 0;
+      for (int q = 0; q < 4; ++q) {
+        uint32_t word = 0;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        int p = c * 16 + q * 4 + k;
-        int py = p / W, px = p - py * W;
-        bool pad = s_paddle[e] >= 0 && py == H - 1 && px >= s_paddle[e] && px < s_paddle[e] + pw;
-        bool ball = py == s_by[e] && px == s_bx[e];
-        bool brk = false;
-        if (py < brick_rows) { int bit = py * W + px; brk = (s_br[e][bit >> 6] >> (bit & 63)) & 1ull; }
-        word |= (uint32_t)gray_code(pad, ball, brk) << (8 * k);
+        for (int k = 0; k < 4; ++k) {
+          int p = p0 + q * 4 + k;
+          int py = p / W, px = p - py * W;
+          bool pad = s_paddle[e] >= 0 && py == H - 1 && px >= s_paddle[e] && px < s_paddle[e] + pw;
+          bool ball = p == ballp;
+          bool brk = false;
+          if (py < brick_rows) { int bit = py * W + px; brk = (s_br[e][bit >> 6] >> (bit & 63)) & 1ull; }
+          word |= (uint32_t)gray_code(pad, ball, brk) << (8 * k);
+        }
+        wv[q] = word;
       }
-      wv[q] = word;
     }
     uint4 v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     *reinterpret_cast<uint4*>(cur_frame + (size_t)gb * HW + c * 16) = v;
@@ -331,7 +341,7 @@ __global__ __launch_bounds__(256) void env_step_compact_kernel(
     }
   }
   __syncthreads();
-  if (b < B && s_rec[t]) hist.hlen[b] = hist.hlen[b] + 1;
+  if (t < E && b < B && s_rec[t]) hist.hlen[b] = hist.hlen[b] + 1;
 }
 
 // compact -> planes (for parity checks and the drop-in API)
@@ -452,13 +462,17 @@ int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx
   History h{hist_frames, hist_actions, hist_len, L};
   Sink sk{rec_action, rec_reward, rec_mask, rec_frame};
   RewardCfg rc{rewards4[0], rewards4[1], rewards4[2], rewards4[3]};
-  dim3 grid((B + 255) / 256);
+  // envs per block: ~<= 4 16-B render stores per lane, and >= ~512 blocks when B allows
+  const int chunks = H * W / 16;
+  int E = 1;
+  while (E < 256 && 2 * E * chunks <= 1024 && 2 * E * 512 <= B) E *= 2;
+  dim3 grid((B + E - 1) / E);
   if (nw == 1)
     hipLaunchKernelGGL(env_step_compact_kernel<1>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
-                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx);
+                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx, E);
   else
     hipLaunchKernelGGL(env_step_compact_kernel<4>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
-                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx);
+                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx, E);
   MZ_LAUNCH_CHECK();
   return 0;
 }
