@@ -105,6 +105,29 @@ int mzba_conv_band_supported(int H, int W, int Cin, int Cout, int ks);
 int mzba_conv_band(const void* in, const void* wf16, const float* bias, const void* res, void* out, int B, int H,
                    int W, int Cin, int Cout, int relu, hipStream_t stream);
 
+/* Replay ingest on the device (replay_buffer.py:96-165, train_torch.py:223-225). Records of one episode
+ * batch as the acting loop's sink holds them: action u8 [T][B], reward f32 [T][B], mask u8 [T][B]
+ * (recorded = not prev_done, a prefix), counts i64 [T][B][3], value f32 [T][B], frame u8 [T][B][HW]
+ * gray codes, frame0 u8 [B][HW] = g(s0).
+ * plan: lens i32[B], rsum f32[B] (reward sums), offsets i32[B+1] = exclusive scan of the window counts
+ *       (L - K + 1 for trajectories with L > min_len, else 0).
+ * write: windows [j0, n) with j0 = max(0, n - cap) into ring slots (head + j) % cap: past actions
+ *       i64 [cap][hist], future actions i64 [cap][K], frames u8 [cap][hist][HW], rewards / values /
+ *       n-step targets f32 [cap][K], counts f32 [cap][K][3], reward sum f32 [cap]; dpow f32[T + 2]:
+ *       dpow[k] = f32(discount**k) for k <= T, dpow[T + 1] = f32(discount**K) (python double pow).
+ * states: out f32 [n][hist][HW] = lut8[code & 7] for ring slots slots[n] (the learner's input). */
+int mzba_replay_plan(const uint8_t* action, const float* reward, const uint8_t* mask, const int64_t* counts,
+                     const float* value, const uint8_t* frame, const uint8_t* frame0, int T, int B, int HW, int K,
+                     int min_len, int32_t* lens, float* rsum, int32_t* offsets, hipStream_t stream);
+int mzba_replay_write(const uint8_t* action, const float* reward, const uint8_t* mask, const int64_t* counts,
+                      const float* value, const uint8_t* frame, const uint8_t* frame0, int T, int B, int HW,
+                      const int32_t* lens, const float* rsum, const int32_t* offsets, int n_windows,
+                      int64_t* past_actions, int64_t* future_actions, uint8_t* states, float* rewards,
+                      float* counts_out, float* values_out, float* targets, float* reward_sum, int cap, int head,
+                      int K, int hist, const float* dpow, hipStream_t stream);
+int mzba_replay_states(const uint8_t* states, const int32_t* slots, int n, const float* lut8, float* out, int hist,
+                       int HW, hipStream_t stream);
+
 /* kernel choice for experiments/tests: 0 by batch (default), 1 four-env kernel, 2 eight-env kernel */
 int mzba_tower_set_variant(int v);
 /* kernel mzba_tower runs for batch B: 1 four-env (workgroup = 4 envs, 8 waves), 2 eight-env (B >= 8 x CUs;

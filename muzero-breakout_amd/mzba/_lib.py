@@ -37,6 +37,9 @@ SIGNATURES = {
     "mzba_tower_ws_bytes": [I],
     "mzba_tower_fused": [P, LL, P, LL, P, P, P, I, I, P, P],
     "mzba_conv_band_supported": [I, I, I, I, I],
+    "mzba_replay_plan": [P, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P],
+    "mzba_replay_write": [P, P, P, P, P, P, P, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, I, I, I, I, P, P],
+    "mzba_replay_states": [P, P, I, P, P, I, I, P],
     "mzba_conv_band": [P, P, P, P, P, I, I, I, I, I, I, P],
     "mzba_tower_set_variant": [I],
     "mzba_avgpool2": [I, P, P, I, I, I, I, P],

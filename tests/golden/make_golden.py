@@ -416,9 +416,64 @@ def make_acting(cfg):
     print("acting", "lengths", lens, "reward sums", [float(t.reward_sum) for t in trajs])
 
 
+def make_replay(cfg):
+    """ReplayBuffer.save_observation_trajectory on seeded synthetic trajectories (reference
+    ObservationTrajectory objects padded like _pad_initial_state), small max_length so the
+    FIFO eviction runs; every window's getters are stored."""
+    import replay_buffer as rb
+    K, hist = cfg["num_unroll_steps"], cfg["model"]["state_history_length"]
+    H, W = 16, 20
+    rng = np.random.default_rng(SEED)
+    # the grayscale value set of convert_to_grayscale (train_torch.py:334-358) over the 3 planes
+    gray = np.unique(np.array([min(max(np.float32(np.float32(0.3) * p + np.float32(1.0) * b) + np.float32(0.6) * k, 0),
+                                   1) for p in (0, 1) for b in (0, 1) for k in (0, 1)], np.float32))
+    lengths = [3, 12, 6, 40, 7, 25, 8]  # 3 <= K: no windows; the rest overflow max_length=60
+    max_length, nsum = 60, 24
+    buf = rb.ReplayBuffer(hist, K, max_length, cfg["discount_factor"], nsum)
+    n = len(lengths)
+    T = max(lengths)
+    acts = np.zeros((n, T), np.int64)
+    frames = np.zeros((n, T, H, W), np.float32)
+    frame0 = np.zeros((n, H, W), np.float32)
+    rews = np.zeros((n, T), np.float32)
+    cnts = np.zeros((n, T, 3), np.int64)
+    vals = np.zeros((n, T), np.float32)
+    for i, L in enumerate(lengths):
+        frame0[i] = gray[rng.integers(0, 5, (H, W))]
+        t = rb.ObservationTrajectory(actions=[0 for _ in range(hist)],
+                                     states=[torch.from_numpy(frame0[i].reshape(1, H, W)) for _ in range(hist - 1)],
+                                     rewards=[0 for _ in range(hist)], visit_counts=[torch.zeros(3) for _ in range(hist)],
+                                     values=[0.0 for _ in range(hist)], length=0, reward_sum=0)
+        for s in range(L):
+            a = int(rng.integers(0, 3))
+            f = gray[rng.integers(0, 5, (H, W))]
+            r = np.float32(rng.choice([-1.0, 0.0, 0.0, 1.0, 5.0, 6.0]))
+            c = rng.multinomial(50, [0.3, 0.3, 0.4]).astype(np.int64)
+            v = np.float32(rng.normal() * 2)
+            acts[i, s], frames[i, s], rews[i, s], cnts[i, s], vals[i, s] = a, f, r, c, v
+            t.add_observation(torch.tensor(a), torch.from_numpy(f.reshape(1, H, W)), torch.tensor(r),
+                              torch.from_numpy(c), torch.tensor(v))
+        buf.save_observation_trajectory(t)
+    idx = torch.arange(buf.length)
+    out = dict(seed=SEED, K=K, hist=hist, max_length=max_length, num_rewards_to_sum=nsum,
+               discount=cfg["discount_factor"], lengths=np.array(lengths), actions=acts, frames=frames,
+               frame0=frame0, rewards=rews, counts=cnts, values=vals, n=buf.length,
+               past_actions=buf.get_batched_past_actions(idx).numpy(),
+               future_actions=buf.get_batched_future_actions(idx).numpy(),
+               states=buf.get_batched_states(idx).numpy(),
+               b_rewards=buf.get_batched_rewards(idx).numpy(),
+               b_counts=buf.get_batched_visit_counts(idx).numpy(),
+               b_values=np.stack([v.numpy() for v in buf.value_buffer]),
+               targets=buf.get_batched_values(idx).numpy(),
+               reward_sums=np.array([float(x) for x in buf.get_reward_sums()], np.float32))
+    for k in ("past_actions", "future_actions", "states", "b_rewards", "b_counts", "targets"):
+        print("replay", k, out[k].dtype, out[k].shape)
+    np.savez_compressed(os.path.join(HERE, "replay.npz"), **out)
+
+
 if __name__ == "__main__":
     cfg = ref_harness.load_config()
-    which = sys.argv[1:] or ["env", "fuzz", "nets", "mcts", "acting"]
+    which = sys.argv[1:] or ["env", "fuzz", "nets", "mcts", "acting", "replay"]
     if "env" in which:
         make_env(cfg)
     if "fuzz" in which:
@@ -429,3 +484,5 @@ if __name__ == "__main__":
         make_mcts(cfg)
     if "acting" in which:
         make_acting(cfg)
+    if "replay" in which:
+        make_replay(cfg)

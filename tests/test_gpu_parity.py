@@ -555,3 +555,77 @@ def test_tower_matches_conv_chain(B, nblocks, gather, variant):
         L.call("mzba_tower_set_variant", 0)
     err = (out.float().cpu() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
     assert err < 3e-2, err
+
+
+# ------------------------------------------------------------------------------ replay ingest
+def _replay_oracle_from(trajs, cfg, max_length, nsum):
+    from oracle.replay import ReplayOracle
+    K, h = cfg["num_unroll_steps"], cfg["model"]["state_history_length"]
+    o = ReplayOracle(h, K, max_length, cfg["discount_factor"], nsum)
+    for t in trajs:
+        if t.length > K + 1:  # train_torch.py:224
+            o.save([int(a) for a in t.actions[h:]], np.stack([np.asarray(s).reshape(16, 20) for s in t.states[h - 1:]]),
+                   np.asarray(t.states[0]).reshape(16, 20), np.array([float(r) for r in t.rewards[h:]], np.float32),
+                   np.stack([np.asarray(c) for c in t.visit_counts[h:]]), np.array(t.values[h:], np.float32))
+    return o
+
+
+def _check_replay(buf, o):
+    idx = torch.arange(len(o))
+    assert len(buf) == len(o)
+    np.testing.assert_array_equal(buf.get_batched_past_actions(idx).cpu().numpy(), o.batched("past_actions", idx))
+    np.testing.assert_array_equal(buf.get_batched_future_actions(idx).cpu().numpy(), o.batched("future_actions", idx))
+    np.testing.assert_array_equal(buf.get_batched_states(idx).cpu().numpy()[:, :, 0], o.batched("states", idx))
+    np.testing.assert_array_equal(buf.get_batched_rewards(idx).cpu().numpy(), o.batched("rewards", idx))
+    np.testing.assert_array_equal(buf.get_batched_visit_counts(idx).cpu().numpy(), o.batched("visit_counts", idx))
+    np.testing.assert_array_equal(buf.get_values(idx).cpu().numpy(), o.batched("values", idx))
+    np.testing.assert_array_equal(buf.get_batched_values(idx).cpu().numpy(), o.batched("targets", idx))
+    np.testing.assert_array_equal(np.array(buf.get_reward_sums(), np.float32), o.reward_sums())
+
+
+def test_replay_buffer_matches_reference_fixture():
+    """Drop-in ReplayBuffer (device windows + n-step targets) vs the reference run on the same
+    trajectories (tests/golden/replay.npz), including FIFO eviction: bit-exact."""
+    from replay_buffer import ReplayBuffer, ObservationTrajectory
+    d = np.load(os.path.join(GOLDEN, "replay.npz"))
+    h, K = int(d["hist"]), int(d["K"])
+    buf = ReplayBuffer(h, K, int(d["max_length"]), float(d["discount"]), int(d["num_rewards_to_sum"]))
+    for i, L in enumerate(d["lengths"]):
+        f0 = torch.from_numpy(d["frame0"][i].reshape(1, 16, 20))
+        t = ObservationTrajectory([0] * h, [f0] * (h - 1), [0] * h, [torch.zeros(3)] * h, [0.0] * h, 0, 0)
+        for s in range(L):
+            t.add_observation(int(d["actions"][i, s]), torch.from_numpy(d["frames"][i, s].reshape(1, 16, 20)),
+                              float(d["rewards"][i, s]), torch.from_numpy(d["counts"][i, s]), float(d["values"][i, s]))
+        buf.save_observation_trajectory(t)
+    idx = torch.arange(int(d["n"]))
+    assert len(buf) == int(d["n"])
+    np.testing.assert_array_equal(buf.get_batched_past_actions(idx).cpu().numpy(), d["past_actions"])
+    np.testing.assert_array_equal(buf.get_batched_future_actions(idx).cpu().numpy(), d["future_actions"])
+    np.testing.assert_array_equal(buf.get_batched_states(idx).cpu().numpy(), d["states"])
+    np.testing.assert_array_equal(buf.get_batched_rewards(idx).cpu().numpy(), d["b_rewards"])
+    np.testing.assert_array_equal(buf.get_batched_visit_counts(idx).cpu().numpy(), d["b_counts"])
+    np.testing.assert_array_equal(buf.get_batched_values(idx).cpu().numpy(), d["targets"])
+    np.testing.assert_array_equal(np.array(buf.get_reward_sums(), np.float32), d["reward_sums"])
+
+
+@pytest.mark.parametrize("max_length", [100000, 97])
+def test_replay_ingest_from_acting_records(max_length):
+    """Device ingest straight from the acting loop's sink (no host trajectories) vs the oracle
+    ReplayBuffer fed the same episode's ObservationTrajectory lists; small ring = eviction."""
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingLoop
+    from mzba.replay import DeviceReplayBuffer
+    cfg = _small_cfg(8)
+    mcfg = cfg["model"]
+    ag = MuZeroAgent(mcfg, dtype="bf16")
+    ag.load_state_dict(init_state_dict(mcfg, 31))
+    B = 48
+    loop = ActingLoop(cfg, ag, B, seed=99, max_steps=40)
+    trajs = loop.run_episode(0)
+    K, h = cfg["num_unroll_steps"], mcfg["state_history_length"]
+    buf = DeviceReplayBuffer(h, K, max_length, cfg["discount_factor"], 64)
+    buf.ingest_records(loop.rec, loop.frame0.view(B, -1), loop.t)
+    buf.ingest_records(loop.rec, loop.frame0.view(B, -1), loop.t)  # a second episode batch: FIFO order
+    o = _replay_oracle_from(list(trajs) + list(trajs), cfg, max_length, 64)
+    assert len(o) > 0
+    _check_replay(buf, o)

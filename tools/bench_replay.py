@@ -1,0 +1,68 @@
+"""Replay ingest timing: one episode batch of B envs x T steps of acting
+records -> ReplayBuffer windows on the device, vs the oracle's restatement of the reference's
+Python loop on a sample of the same trajectories (numpy, one core).
+
+usage: python tools/bench_replay.py [B] [T]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "muzero-breakout_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+from mzba.replay import DeviceReplayBuffer  # noqa: E402
+from mzba.env import gray_lut  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 261
+K, h, HW = 5, 32, 320
+g = torch.Generator(device="cuda").manual_seed(0)
+lens = torch.randint(1, T + 1, (B,), device="cuda", generator=g)
+t = torch.arange(T, device="cuda")[:, None]
+rec = {
+    "action": torch.randint(0, 3, (T, B), device="cuda", generator=g).to(torch.uint8),
+    "reward": torch.randint(-1, 2, (T, B), device="cuda", generator=g).to(torch.float32),
+    "mask": (t < lens[None]).to(torch.uint8),
+    "counts": torch.randint(0, 51, (T, B, 3), device="cuda", generator=g),
+    "values": torch.randn(T, B, device="cuda", generator=g),
+    "frame": torch.randint(0, 8, (T, B, HW), device="cuda", generator=g).to(torch.uint8),
+}
+frame0 = torch.randint(0, 8, (B, HW), device="cuda", generator=g).to(torch.uint8)
+buf = DeviceReplayBuffer(h, K, 600000, 0.985, 512)
+buf.ingest_records(rec, frame0, T)  # warm-up
+buf.empty_buffer()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+n = buf.ingest_records(rec, frame0, T)
+torch.cuda.synchronize()
+dt = time.perf_counter() - t0
+idx = torch.randint(0, len(buf), (512,), device="cuda", generator=g)
+buf.get_batched_states(idx)  # warm-up (code object load)
+torch.cuda.synchronize()
+t1 = time.perf_counter()
+st = buf.get_batched_states(idx)
+torch.cuda.synchronize()
+dts = time.perf_counter() - t1
+
+# CPU: the oracle's restatement of save_observation_trajectory on 16 of the trajectories
+from oracle.replay import ReplayOracle  # noqa: E402
+lut = gray_lut()
+cpu = {k: v.cpu().numpy() for k, v in rec.items()}
+f0 = frame0.cpu().numpy()
+o = ReplayOracle(h, K, 600000, 0.985, 512)
+ln = lens.cpu().numpy()
+sample = [b for b in range(B) if ln[b] > K + 1][:16]
+c0 = time.perf_counter()
+for b in sample:
+    L = ln[b]
+    o.save(cpu["action"][:L, b], lut[cpu["frame"][:L, b] & 7].reshape(L, 16, 20), lut[f0[b] & 7].reshape(16, 20),
+           cpu["reward"][:L, b], cpu["counts"][:L, b], cpu["values"][:L, b])
+cs = time.perf_counter() - c0
+print(json.dumps({"B": B, "T": T, "windows": n, "ingest_ms": dt * 1e3, "windows_per_s": n / dt,
+                  "bytes_written": n * (h * HW + 8 * (h + K) + 4 * K * 6 + 4),
+                  "state_batch_512_ms": dts * 1e3,
+                  "cpu_oracle_windows_per_s": len(o) / cs, "cpu_sample_trajectories": len(sample)}))
