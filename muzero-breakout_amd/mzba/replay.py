@@ -159,3 +159,48 @@ class DeviceReplayBuffer:
 
     def empty_buffer(self):
         self.start = self.length = 0
+
+    # -- the reference's list layout (checkpoint replay_buffer, train_torch.py:624-635) ----
+    def to_reference_lists(self):
+        idx = torch.arange(self.length, device=self.device)
+        cpu = lambda t: list(t.cpu().unbind(0)) if self.length else []  # noqa: E731
+        sl = self._slots(idx) if self.length else idx
+        return {
+            "past_actions_buffer": cpu(self._ring["past_actions"][sl]),
+            "future_actions_buffer": cpu(self._ring["future_actions"][sl]),
+            "state_buffer": cpu(self.get_batched_states(idx)) if self.length else [],
+            "reward_buffer": cpu(self._ring["rewards"][sl]),
+            "visit_counts_buffer": cpu(self._ring["counts"][sl]),
+            "value_buffer": cpu(self._ring["values"][sl]),
+            "reward_sums": [float(x) for x in self._ring["reward_sum"][sl].cpu()],
+            "length": self.length,
+            "max_length": self.max_length,
+            "bootstrapped_values": cpu(self._ring["targets"][sl]),
+        }
+
+    def load_reference_lists(self, d):
+        """Replace the contents with a reference replay_buffer dict (oldest first)."""
+        n = int(d["length"])
+        if n > self.max_length:
+            raise ValueError(f"checkpoint holds {n} windows, buffer max_length is {self.max_length}")
+        self.empty_buffer()
+        if n == 0:
+            return
+        lut = gray_lut()
+        vals, first = np.unique(lut, return_index=True)
+        st = np.stack([np.asarray(s, np.float32) for s in d["state_buffer"][:n]]).reshape(n, self.hist_seq_len, -1)
+        pos = np.searchsorted(vals, st).clip(0, len(vals) - 1)
+        if not np.array_equal(vals[pos], st):
+            raise ValueError("state_buffer holds values that are not convert_to_grayscale outputs")
+        g, dev = self._ring, self.device
+        put = lambda key, rows, dt: g[key][:n].copy_(torch.as_tensor(np.stack([np.asarray(x) for x in rows]),  # noqa: E731
+                                                                  dtype=dt).to(dev))
+        g["states"][:n].copy_(torch.from_numpy(first[pos].astype(np.uint8)).to(dev))
+        put("past_actions", d["past_actions_buffer"][:n], torch.int64)
+        put("future_actions", d["future_actions_buffer"][:n], torch.int64)
+        put("rewards", d["reward_buffer"][:n], torch.float32)
+        put("counts", d["visit_counts_buffer"][:n], torch.float32)
+        put("values", d["value_buffer"][:n], torch.float32)
+        put("targets", d["bootstrapped_values"][:n], torch.float32)
+        g["reward_sum"][:n].copy_(torch.tensor(np.asarray(d["reward_sums"][:n], np.float32)).to(dev))
+        self.start, self.length = 0, n

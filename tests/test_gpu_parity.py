@@ -629,3 +629,44 @@ def test_replay_ingest_from_acting_records(max_length):
     o = _replay_oracle_from(list(trajs) + list(trajs), cfg, max_length, 64)
     assert len(o) > 0
     _check_replay(buf, o)
+
+
+def test_checkpoint_reference_format_roundtrip(tmp_path):
+    """save_checkpoint writes RLSystem._save_weights' dict (train_torch.py:612-637); load_checkpoint
+    (weights_only) restores the agent and the device replay buffer exactly."""
+    from mzba.agent import MuZeroAgent
+    from mzba.checkpoint import save_checkpoint, load_checkpoint, REPLAY_KEYS
+    from replay_buffer import ReplayBuffer, ObservationTrajectory
+    cfg = _small_cfg(8)
+    mcfg = cfg["model"]
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(init_state_dict(mcfg, 3))
+    d = np.load(os.path.join(GOLDEN, "replay.npz"))
+    h, K = int(d["hist"]), int(d["K"])
+    buf = ReplayBuffer(h, K, int(d["max_length"]), float(d["discount"]), int(d["num_rewards_to_sum"]))
+    for i, L in enumerate(d["lengths"]):
+        f0 = torch.from_numpy(d["frame0"][i].reshape(1, 16, 20))
+        t = ObservationTrajectory([0] * h, [f0] * (h - 1), [0] * h, [torch.zeros(3)] * h, [0.0] * h, 0, 0)
+        for s in range(L):
+            t.add_observation(int(d["actions"][i, s]), torch.from_numpy(d["frames"][i, s].reshape(1, 16, 20)),
+                              float(d["rewards"][i, s]), torch.from_numpy(d["counts"][i, s]), float(d["values"][i, s]))
+        buf.save_observation_trajectory(t)
+    p = str(tmp_path / "checkpt.pth")
+    save_checkpoint(p, ag, buf, training_iteration=7, acting_step=3, iteration=11)
+    raw = torch.load(p, weights_only=True)
+    assert set(raw) == {"model_state_dict", "optimizer_state_dict", "training_iteration", "acting_step", "iteration",
+                        "replay_buffer"}
+    assert set(raw["replay_buffer"]) == set(REPLAY_KEYS)
+    np.testing.assert_array_equal(torch.stack(raw["replay_buffer"]["state_buffer"]).numpy(), d["states"])
+    np.testing.assert_array_equal(torch.stack(raw["replay_buffer"]["bootstrapped_values"]).numpy(), d["targets"])
+    ag2 = MuZeroAgent(mcfg, dtype="f32")
+    buf2 = ReplayBuffer(h, K, int(d["max_length"]), float(d["discount"]), int(d["num_rewards_to_sum"]))
+    ck = load_checkpoint(p, ag2, buf2)
+    assert ck["training_iteration"] == 7 and ck["iteration"] == 11
+    for k, v in ag.state_dict().items():
+        np.testing.assert_array_equal(ag2.state_dict()[k], v)
+    idx = torch.arange(len(buf))
+    for get in ("get_batched_past_actions", "get_batched_future_actions", "get_batched_states", "get_batched_rewards",
+                "get_batched_visit_counts", "get_batched_values"):
+        assert torch.equal(getattr(buf, get)(idx), getattr(buf2, get)(idx)), get
+    assert buf.get_reward_sums() == buf2.get_reward_sums()
