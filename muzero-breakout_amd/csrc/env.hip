@@ -386,17 +386,34 @@ __global__ void build_rep_input_kernel(const uint8_t* __restrict__ cur_frame, Hi
   }
   __syncthreads();
   const int L = hist.L;
-  size_t n = (size_t)B * HW;
+  const int CH = Cs / 8;  // 8-channel chunks per pixel: one 16-B (bf16) / 32-B (f32) store per thread
+  const size_t n = (size_t)B * HW * CH;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const size_t b = i / HW, p = i - b * HW;
+    const size_t pix = i / CH;
+    const int ch = (int)(i - pix * CH);
+    const size_t b = pix / HW, p = pix - b * HW;
     const int hl = hist.hlen[b];
-    T* o = out + i * Cs;
-    for (int c = 0; c < Cs; ++c) {
-      float v = 0.f;
-      if (c < L - 1) v = lut[hist.frames[(b * (L - 1) + ((hl + c) % (L - 1))) * HW + p] & 7];
-      else if (c == L - 1) v = lut[cur_frame[b * HW + p] & 7];
-      else if (c < 2 * L) v = (float)hist.actions[b * L + ((hl + c - L) % L)] / 3.0f;
-      ElemIO<T>::store(o + c, v);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = ch * 8 + j;
+      float x = 0.f;
+      if (c < L - 1) x = lut[hist.frames[(b * (L - 1) + ((hl + c) % (L - 1))) * HW + p] & 7];
+      else if (c == L - 1) x = lut[cur_frame[b * HW + p] & 7];
+      else if (c < 2 * L) x = (float)hist.actions[b * L + ((hl + c - L) % L)] / 3.0f;
+      v[j] = x;
+    }
+    T* o = out + pix * Cs + ch * 8;
+    if constexpr (sizeof(T) == 2) {
+      uint4 w;
+      w.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+      w.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+      w.z = (uint32_t)f32_to_bf16(v[4]) | ((uint32_t)f32_to_bf16(v[5]) << 16);
+      w.w = (uint32_t)f32_to_bf16(v[6]) | ((uint32_t)f32_to_bf16(v[7]) << 16);
+      *reinterpret_cast<uint4*>(o) = w;
+    } else {
+      reinterpret_cast<float4*>(o)[0] = make_float4(v[0], v[1], v[2], v[3]);
+      reinterpret_cast<float4*>(o)[1] = make_float4(v[4], v[5], v[6], v[7]);
     }
   }
 }
@@ -491,11 +508,11 @@ int mzba_compact_to_planes(const int32_t* paddle, const int32_t* bx, const int32
 int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* hist_frames, const uint8_t* hist_actions,
                          const int32_t* hist_len, int L, void* out, int out_bf16, int B, int HW, int Cs,
                          hipStream_t stream) {
-  MZ_CHECK_ARG(B > 0 && Cs >= 2 * L, -1);
+  MZ_CHECK_ARG(B > 0 && Cs >= 2 * L && Cs % 8 == 0, -1);
   History h{(uint8_t*)hist_frames, (uint8_t*)hist_actions, (int32_t*)hist_len, L};
-  size_t n = (size_t)B * HW;
+  size_t n = (size_t)B * HW * (Cs / 8);
   unsigned grid = (unsigned)((n + 255) / 256);
-  if (grid > 4096) grid = 4096;
+  if (grid > 16384) grid = 16384;
   if (out_bf16)
     hipLaunchKernelGGL(build_rep_input_kernel<bf16_t>, dim3(grid), dim3(256), 0, stream, cur_frame, h,
                        (bf16_t*)out, B, HW, Cs);
