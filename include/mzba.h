@@ -142,6 +142,27 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
  * before it and the reward / policy / value heads after it run in the same launch, so one
  * dynamics step and one prediction step are one kernel each (networks.py:151-167, 200-241,
  * 314-328; utils.py:74-81). */
+/* One simulation's tree update folded into the fused prediction step: after the heads, each env's
+ * thread backs up this simulation's leaf (mcts.py:203-234) and, when sim + 1 < S, selects the next
+ * leaf (mcts.py:136-182). Fields as the mzba_mcts_* tree arguments. */
+typedef struct mzba_tree_step {
+  void* nodes;
+  float* root_sum;
+  uint32_t* calls;
+  int32_t* leaf_parent;
+  int32_t* leaf_action;
+  int32_t* depth;
+  int32_t* path;
+  const float* sqrt_tab;
+  const float* c_tab;
+  int B, S, env_offset, search_id;
+  uint64_t seed;
+  const int32_t* ctx;
+  int sim;
+  float gamma;
+  const float* r;         /* decoded rewards of this simulation's dynamics step [B] */
+} mzba_tree_step;
+
 typedef struct mzba_tower_ext {
   /* prologue: dynamics ConvBlock 259->256 = 3x3 conv (tower packing) + bias + per-(position,
    * action) bias table [20][A][256] f32 (the action planes folded in), ReLU; w0 = NULL: none */
@@ -169,6 +190,7 @@ typedef struct mzba_tower_ext {
   long long pool_env_stride;
   int pool_slot;
   float smin, smax;       /* support range */
+  const mzba_tree_step* tree;  /* epilogue 2 only, may be NULL */
 } mzba_tower_ext;
 int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                      void* out, const void* wf16, const float* bias, int nblocks, int B,

@@ -13,58 +13,9 @@
 //   G = f32(f32(G * f32(gamma)) + r); Q = f32(f32(f32(N) * Q) + G) / f32(N + 1) (mcts.py:231-233)
 // Tie-breaks draw best[randbelow(len(best))] from Philox (env, STREAM_TIE, search_id, k).
 #include "common.h"
+#include "tree_dev.h"
 
 namespace {
-
-struct Node {
-  float Q[3];
-  float P[3];
-  float R[3];
-  int N[3];
-  int child[3];
-  int pad;
-};
-static_assert(sizeof(Node) == 64, "node = one 64-B line");
-
-struct TreeArgs {
-  Node* nodes;          // [B][S+1]
-  float* root_sum;      // [B]
-  uint32_t* calls;      // [B] ucb_action call counter (tie-break stream)
-  int32_t* leaf_parent; // [B]
-  int32_t* leaf_action; // [B]
-  int32_t* depth;       // [B]
-  int32_t* path;        // [B][S+1] packed (node << 2) | action
-  const float* sqrt_tab;  // [S+1]
-  const float* c_tab;     // [S+1]
-  int B, S, env_offset, search_id;
-  uint64_t seed;
-  const int32_t* ctx;   // optional device step context (graph replay): ctx[0] = search id
-};
-
-MZ_DEV int tree_search_id(const TreeArgs& t) { return t.ctx ? t.ctx[0] : t.search_id; }
-
-MZ_DEV int ucb_select(const Node& nd, const TreeArgs& t, int b) {
-  const int n = nd.N[0] + nd.N[1] + nd.N[2];
-  const float sq = t.sqrt_tab[n], ct = t.c_tab[n];
-  float u[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    float v = nd.P[a] * sq;
-    v = v / (float)(1 + nd.N[a]);
-    v = v * ct;
-    u[a] = nd.Q[a] + v;
-  }
-  float mx = fmaxf(fmaxf(u[0], u[1]), u[2]);
-  int best[3], cnt = 0;
-#pragma unroll
-  for (int a = 0; a < 3; ++a)
-    if (u[a] == mx) best[cnt++] = a;
-  const uint32_t k = t.calls[b];
-  t.calls[b] = k + 1;
-  const int j = mz_randbelow((uint32_t)(b + t.env_offset), MZ_STREAM_TIE, (uint32_t)tree_search_id(t), k, t.seed,
-                             (uint32_t)cnt);
-  return best[j];
-}
 
 // ---------------------------------------------------------------- Dirichlet noise
 struct NormalGen {
@@ -144,24 +95,7 @@ __global__ void root_init_kernel(TreeArgs t, const float* __restrict__ v_root, c
 __global__ void select_kernel(TreeArgs t, int sim) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= t.B) return;
-  Node* tree = t.nodes + (size_t)b * (t.S + 1);
-  int32_t* path = t.path + (size_t)b * (t.S + 1);
-  int node = 0, d = 0;
-  for (int it = 0;; ++it) {  // depth <= sim: every wave reaches the leaf branch
-    const Node nd = tree[node];
-    const int a = ucb_select(nd, t, b);
-    const int c = nd.child[a];
-    if (c >= 0 && c <= sim && it < sim) {
-      path[d++] = (node << 2) | a;
-      node = c;
-    } else {
-      tree[node].child[a] = sim + 1;  // the new node's slot (mcts.py:167-175 marks it expanded)
-      t.leaf_parent[b] = node;
-      t.leaf_action[b] = a;
-      t.depth[b] = d;
-      break;
-    }
-  }
+  tree_select_env(t, sim, b);
 }
 
 // mcts.py:203-234: create the expanded node, set the parent edge's reward, back up.
@@ -169,34 +103,7 @@ __global__ void backup_kernel(TreeArgs t, int sim, const float* __restrict__ r, 
                               const float* __restrict__ pi, float gamma) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= t.B) return;
-  Node* tree = t.nodes + (size_t)b * (t.S + 1);
-  const int32_t* path = t.path + (size_t)b * (t.S + 1);
-  Node nd;
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    nd.Q[a] = 0.f; nd.P[a] = pi[b * 3 + a]; nd.R[a] = 0.f; nd.N[a] = 0; nd.child[a] = -1;
-  }
-  nd.pad = 0;
-  tree[sim + 1] = nd;
-  const int lp = t.leaf_parent[b], la = t.leaf_action[b], d = t.depth[b];
-  const float rl = r[b];
-  tree[lp].R[la] = rl;
-  float G = v[b];
-  for (int i = d; i >= 0; --i) {
-    int node, a;
-    float rr;
-    if (i == d) { node = lp; a = la; rr = rl; }
-    else { node = path[i] >> 2; a = path[i] & 3; rr = tree[node].R[a]; }
-    float g1 = G * gamma;
-    G = g1 + rr;
-    if (node == 0) t.root_sum[b] = t.root_sum[b] + G;
-    Node* e = tree + node;
-    const int n = e->N[a];
-    float q = (float)n * e->Q[a];
-    q = q + G;
-    e->Q[a] = q / (float)(n + 1);
-    e->N[a] = n + 1;
-  }
+  tree_backup_env(t, sim, b, r[b], v[b], pi + b * 3, gamma);
 }
 
 // mcts.py:236-250 -> counts i64[B][3], values f32[B] = f32(double(root_sum) / S)

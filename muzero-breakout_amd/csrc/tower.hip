@@ -22,6 +22,7 @@
 // Input is read from HBM once (optional per-env slot gather from the latent node pool) and
 // the tower output written once. Grid: ceil(B / 4) workgroups of 512 threads.
 #include "common.h"
+#include "tree_dev.h"
 
 namespace {
 
@@ -58,6 +59,10 @@ struct TowerArgs {
   int nblocks;               // residual blocks (2 convs each)
   int B;
   mzba_tower_ext x;          // fused prologue / epilogue (4-env kernel); all zero = plain tower
+  TreeArgs tree;             // prediction epilogue: backup(tree_sim) + select(tree_sim + 1) per env
+  int tree_on, tree_sim;
+  float tree_gamma;
+  const float* tree_r;
 };
 
 // LDS row of (env e, latent position p = 5y + x) and the byte offset of (row, 16-B chunk)
@@ -225,8 +230,8 @@ __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg
 // partial sums added through LDS in wave order; then softmax (dec_kind 0) or support decode (1).
 __device__ __forceinline__ void tower_heads(const TowerArgs& a, const uint8_t* __restrict__ lds, int img,
                                             int nh, const int (&hc0)[2], const int (&hC)[2], const int (&kind)[2],
-                                            float (*part)[4][16], float (*lg)[4][16], int env0, int nenv,
-                                            int tid) {
+                                            float (*part)[4][16], float (*lg)[4][16], float (*dec)[4][4],
+                                            int env0, int nenv, int tid) {
   const int lane = tid & 63, wave = tid >> 6, q = lane >> 4, el = lane & 15;
   for (int hd = 0; hd < nh; ++hd) {
     const int C = hC[hd], K = 20 * C, nk = K / 32;
@@ -268,9 +273,15 @@ __device__ __forceinline__ void tower_heads(const TowerArgs& a, const uint8_t* _
         for (int o = 1; o < O; ++o) m = fmaxf(m, l[o]);
         float ex[16], sum = 0.f;
         for (int o = 0; o < O; ++o) { ex[o] = expf(l[o] - m); sum = sum + ex[o]; }
-        for (int o = 0; o < O; ++o) a.x.dec[hd][(size_t)b * O + o] = ex[o] / sum;
+        for (int o = 0; o < O; ++o) {
+          const float p = ex[o] / sum;
+          a.x.dec[hd][(size_t)b * O + o] = p;
+          if (o < 4) dec[hd][e][o] = p;
+        }
       } else {
-        a.x.dec[hd][b] = decode_support(l, O, a.x.smin, a.x.smax);
+        const float d = decode_support(l, O, a.x.smin, a.x.smax);
+        a.x.dec[hd][b] = d;
+        dec[hd][e][0] = d;
       }
     }
   }
@@ -321,6 +332,7 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
   __shared__ int acts[TE];
   __shared__ float part[32][4][16];  // head partial sums [wave * 4 + env][.][output]; min/max scratch
   __shared__ float lg[8][4][16];     // head logits [head * 4 + env][.][output]
+  __shared__ float dec[2][4][4];     // decoded head outputs [head][env][output]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int env0 = blockIdx.x * TE;
   const int nenv = min(TE, a.B - env0);
@@ -377,7 +389,7 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
                         nullptr, nullptr, 0, lane);
     __syncthreads();
     const int hc0[2] = {0, 0}, hC[2] = {TC, 0}, kind[2] = {1, 0};
-    tower_heads(a, lds, LDS_T, 1, hc0, hC, kind, part, lg, env0, nenv, tid);
+    tower_heads(a, lds, LDS_T, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     tower_scale(a, lds, reinterpret_cast<float(*)[2][2]>(&part[0][0][0]), env0, nenv, tid);
     return;
   }
@@ -390,7 +402,15 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
                           128, nullptr, nullptr, 0, lane);
     __syncthreads();
     const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
-    tower_heads(a, lds, LDS_T, 2, hc0, hC, kind, part, lg, env0, nenv, tid);
+    tower_heads(a, lds, LDS_T, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
+      __syncthreads();
+      if (tid < nenv) {
+        const int b = env0 + tid;
+        tree_backup_env(a.tree, a.tree_sim, b, a.tree_r[b], dec[1][tid][0], &dec[0][tid][0], a.tree_gamma);
+        if (a.tree_sim + 1 < a.tree.S) tree_select_env(a.tree, a.tree_sim + 1, b);
+      }
+    }
     return;
   }
   // write the tower output (16-B chunks, rows < rows)
@@ -626,7 +646,7 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
   const int plan = mzba_tower_plan(B);
   MZ_CHECK_ARG(plan > 0, -2);
   TowerArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (bf16_t*)out, (const bf16_t*)wf16, bias,
-              nblocks, B, mzba_tower_ext{}};
+              nblocks, B, mzba_tower_ext{}, TreeArgs{}, 0, 0, 0.f, nullptr};
   (void)ws;
   (void)ws_bytes;
   if (plan == 2) {
@@ -655,7 +675,17 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
                                    x.dec[0] && x.dec[1] && x.lO[0] >= 1 && x.lO[0] <= 16 && x.lO[1] > 1 &&
                                    x.lO[1] <= 16), -3);
   TowerArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (bf16_t*)out, (const bf16_t*)wf16, bias,
-              nblocks, B, x};
+              nblocks, B, x, TreeArgs{}, 0, 0, 0.f, nullptr};
+  if (x.tree) {
+    const mzba_tree_step& t = *x.tree;
+    MZ_CHECK_ARG(x.epilogue == 2 && t.B == B && t.sim >= 0 && t.sim < t.S && t.r && t.nodes, -3);
+    a.tree = TreeArgs{(Node*)t.nodes, t.root_sum, t.calls, t.leaf_parent, t.leaf_action, t.depth, t.path,
+                      t.sqrt_tab, t.c_tab, t.B, t.S, t.env_offset, t.search_id, t.seed, t.ctx};
+    a.tree_on = 1;
+    a.tree_sim = t.sim;
+    a.tree_gamma = t.gamma;
+    a.tree_r = t.r;
+  }
   hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
   MZ_LAUNCH_CHECK();
   return 0;

@@ -60,6 +60,13 @@ SIGNATURES = {
 _lib = None
 
 
+class TreeStep(ctypes.Structure):
+    """include/mzba.h mzba_tree_step (backup + next select inside the fused prediction step)."""
+    _fields_ = [("nodes", P), ("root_sum", P), ("calls", P), ("leaf_parent", P), ("leaf_action", P), ("depth", P),
+                ("path", P), ("sqrt_tab", P), ("c_tab", P), ("B", I), ("S", I), ("env_offset", I),
+                ("search_id", I), ("seed", U64), ("ctx", P), ("sim", I), ("gamma", F), ("r", P)]
+
+
 class TowerExt(ctypes.Structure):
     """include/mzba.h mzba_tower_ext (fused dynamics / prediction step around the tower)."""
     _fields_ = [("w0", P), ("b0", P), ("act_bias", P), ("act", P), ("A", I),
@@ -68,7 +75,7 @@ class TowerExt(ctypes.Structure):
                 ("lw", P * 2), ("lb", P * 2), ("lO", I * 2),
                 ("logits", P * 2), ("dec", P * 2),
                 ("pool", P), ("pool_env_stride", LL), ("pool_slot", I),
-                ("smin", F), ("smax", F)]
+                ("smin", F), ("smax", F), ("tree", ctypes.POINTER(TreeStep))]
 
 
 # entry points that return something other than a status code

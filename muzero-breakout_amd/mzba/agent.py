@@ -392,16 +392,22 @@ class NetRunner:
         L.call("mzba_scale_state", self.dt, L.ptr(self.x), L.ptr(out_latent), L.ptr(pool), pool_env_stride, None,
                pool_slot, n, B, n, L.stream())
 
-    def prediction(self, h, pi, v, p_logits=None, v_logits=None):
-        """PredictionNetwork (networks.py:225-241) + decode (mcts.py:97-100, 197-199)."""
+    def prediction(self, h, pi, v, p_logits=None, v_logits=None, tree=None):
+        """PredictionNetwork (networks.py:225-241) + decode (mcts.py:97-100, 197-199).
+        tree: optional L.TreeStep — on the fused path the same launch then runs this simulation's
+        backup and the next selection (mcts.py:136-234); the caller checks fused_ok() first."""
         B, H, W = self.B, self.p.lh, self.p.lw
         p = self.p
-        if self.fused_ok():  # one launch: 14 blocks + policy / value heads
+        if self.fused_ok():  # one launch: 14 blocks + policy / value heads (+ tree step)
             x = self._ext(2)
             x.logits[0], x.dec[0] = L.ptr(p_logits), L.ptr(pi)
             x.logits[1], x.dec[1] = L.ptr(v_logits), L.ptr(v)
+            if tree is not None:
+                x.tree = ctypes.pointer(tree)
             self._fused_call(p.pred_tower, h, H * W * p.c1, None, 0, None, x)
             return
+        if tree is not None:
+            raise RuntimeError("the tree step rides on the fused prediction launch only")
         cur = h
         if p.pred_tower is not None and self.use_tower:
             self.tower(p.pred_tower, cur, self.x)

@@ -7,6 +7,7 @@ The launch sequence is identical for every call of a given (B, S), so the acting
 can capture it in a HIP graph.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -40,6 +41,13 @@ class TreeState:
         self.counts = torch.empty(B, 3, dtype=torch.int64, device=device)
         self.values = torch.empty(B, dtype=torch.float32, device=device)
         self.noise = torch.empty(B, 3, dtype=torch.float32, device=device)
+
+    def step(self, env_offset, search_id, seed, ctx, sim, gamma, r):
+        """The same tree arguments as mzba_tree_step (fused prediction + backup + next select)."""
+        return L.TreeStep(L.ptr(self.nodes), L.ptr(self.root_sum), L.ptr(self.calls), L.ptr(self.leaf_parent),
+                          L.ptr(self.leaf_action), L.ptr(self.depth), L.ptr(self.path), L.ptr(self.sqrt_tab),
+                          L.ptr(self.c_tab), self.B, self.S, env_offset, search_id, seed, L.ptr(ctx), sim, gamma,
+                          L.ptr(r))
 
     def args(self, env_offset, search_id, seed, ctx=None):
         """ctx: optional device int32[3] step context (its [0] overrides search_id; graph replay)."""
@@ -125,6 +133,8 @@ class SearchWorkspace:
         self.v = torch.empty(B, dtype=torch.float32, device=dev)
         self.pi = torch.empty(B, 3, dtype=torch.float32, device=dev)
         self.runner = agent.runner(B, p.lh * 4, p.lw * 4)
+        # backup + next select ride on the fused prediction launch (MZBA_TREE_FUSION=0: separate kernels)
+        self.use_tree_fusion = os.environ.get("MZBA_TREE_FUSION", "1") != "0"
 
     def load_root(self, hidden_state):
         """NCHW (B,C,h,w) latent -> pool slot 0 (NHWC)."""
@@ -151,14 +161,19 @@ class SearchWorkspace:
         self.tree.root(ta, self.v, self.pi, noise, w_pol, w_noise, s.dirchlet_alpha)
         gamma = float(np.float32(s.discount))
         env_stride = (S + 1) * n
+        fused = rn.fused_ok() and self.use_tree_fusion
         for sim in range(S):
-            if sim > 0:
+            if sim > 0 and not fused:
                 self.tree.select(ta, sim)
             rn.dynamics(self.pool, self.tree.leaf_action, self.cur, self.r, slot=self.tree.leaf_parent,
                         env_stride=env_stride, slot_stride=n, pool=self.pool, pool_env_stride=env_stride,
                         pool_slot=sim + 1)
-            rn.prediction(self.cur, self.pi, self.v)
-            self.tree.backup(ta, sim, self.r, self.v, self.pi, gamma)
+            if fused:  # prediction + backup(sim) + select(sim + 1) in one launch
+                rn.prediction(self.cur, self.pi, self.v,
+                              tree=self.tree.step(s.env_offset, search_id, s.seed, ctx, sim, gamma, self.r))
+            else:
+                rn.prediction(self.cur, self.pi, self.v)
+                self.tree.backup(ta, sim, self.r, self.v, self.pi, gamma)
         self.tree.results(ta)
         return self.tree.values, self.tree.counts
 

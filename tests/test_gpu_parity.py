@@ -670,3 +670,28 @@ def test_checkpoint_reference_format_roundtrip(tmp_path):
                 "get_batched_visit_counts", "get_batched_values"):
         assert torch.equal(getattr(buf, get)(idx), getattr(buf2, get)(idx)), get
     assert buf.get_reward_sums() == buf2.get_reward_sums()
+
+
+def test_tree_step_fused_into_prediction_is_identical():
+    """backup(sim) + select(sim + 1) inside the fused prediction launch == the separate tree
+    kernels: same visit counts, values and tie-break draws, bit for bit (bf16 nets)."""
+    from mzba.agent import MuZeroAgent
+    from mzba.search import MCTSSearchVec
+    cfg = default_config()
+    cfg["num_simulations"] = 12
+    mcfg = cfg["model"]
+    ag = MuZeroAgent(mcfg, dtype="bf16")
+    ag.load_state_dict(init_state_dict(mcfg, 4))
+    B = 13
+    g = torch.Generator().manual_seed(5)
+    h = torch.rand(B, 256, 4, 5, generator=g).cuda()
+    out = []
+    for fuse in (False, True):
+        s = MCTSSearchVec(cfg, ag, None, seed=17)
+        ws = s.workspace(B)
+        ws.use_tree_fusion = fuse
+        assert ws.runner.fused_ok()
+        v, c = s.search(h)
+        out.append((v.numpy(), c.numpy()))
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    np.testing.assert_array_equal(out[0][0], out[1][0])
