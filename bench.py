@@ -93,6 +93,12 @@ def run_env(args, world, rank, local):
         dt = float(tt.item())
     kms = float(np.median([a.elapsed_time(c) for a, c in ev]))
     achieved = B * env_bytes(H, W) / (kms * 1e-3) / 1e9
+    traffic = None  # PMC bytes per launch (tools/gpu_round.sh), when measured for this geometry
+    tpath = os.path.join(ROOT, "profiles", "env_hbm_traffic.json")
+    if os.path.exists(tpath):
+        tj = json.load(open(tpath))
+        if (tj.get("envs"), tj.get("H"), tj.get("W")) == (B, H, W) and tj.get("write_bytes") is not None:
+            traffic = tj["write_bytes"] + (tj.get("fetch_bytes") or 0)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle.env import BreakoutEnvOracle, convert_to_grayscale
@@ -122,7 +128,7 @@ def run_env(args, world, rank, local):
                        "envs_per_gpu": B},
             "roofline": {"bound": "hbm", "kernel": "env_step_compact_kernel (step + render + history push)",
                          "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
-                         "traffic": None, "bytes_per_env_step": env_bytes(H, W), "avg_launch_ms": kms},
+                         "traffic": traffic, "bytes_per_env_step": env_bytes(H, W), "avg_launch_ms": kms},
             "cpu_baseline": cpu,
         }))
     if world > 1:
