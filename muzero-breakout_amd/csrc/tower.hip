@@ -69,6 +69,14 @@ struct TowerArgs {
 MZ_DEV int trow(int e, int p) { return (p % 5) * 16 + (p / 5) * 4 + e; }
 MZ_DEV int toff(int row, int chunk) { return row * TROWB + ((chunk ^ (row & 15)) << 4); }
 
+namespace t8 {
+constexpr int E = 8, ROWS = 160, NRT = 10, NT = 256, CT = 4;  // 4 waves
+constexpr int IMG = ROWS * TROWB;                       // 80 KB
+constexpr int LZ = IMG, BYTES = IMG + 16 * TROWB;       // + 16 zero rows
+// LDS row of (env e, latent position p = 5y + x): env quad (e >> 2) owns tiles 5 (e >> 2) .. +4
+MZ_DEV int row8(int e, int p) { return (e >> 2) * 80 + (p % 5) * 16 + (p / 5) * 4 + (e & 3); }
+}  // namespace t8
+
 // A-row addressing of this lane for latent row shift dy: byte offset of its row in source
 // tile 0 (or of its zero-block row), the per-tile stride (0 for zero rows) and the swizzle key
 MZ_DEV void tap_rows(int srcimg, int y, int e, int dy, int& base, int& tstride, int& sw) {
@@ -228,44 +236,47 @@ __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg
 // order against bf16 weights lw[h][16][K]. One v_mfma_f32_16x16x32_bf16 per 32-deep k step
 // (A rows = the 4 envs, zero-padded to 16; B cols = outputs), k steps split over the 8 waves,
 // partial sums added through LDS in wave order; then softmax (dec_kind 0) or support decode (1).
+template <int NE, int NW, bool R8>
 __device__ __forceinline__ void tower_heads(const TowerArgs& a, const uint8_t* __restrict__ lds, int img,
                                             int nh, const int (&hc0)[2], const int (&hC)[2], const int (&kind)[2],
-                                            float (*part)[4][16], float (*lg)[4][16], float (*dec)[4][4],
-                                            int env0, int nenv, int tid) {
+                                            float* part, float* lg, float (*dec)[8][4], int env0, int nenv,
+                                            int tid) {
+  // NE envs per workgroup, NW waves; part: [NW][8][16] partial sums, lg: [2][8][16] logits
   const int lane = tid & 63, wave = tid >> 6, q = lane >> 4, el = lane & 15;
   for (int hd = 0; hd < nh; ++hd) {
     const int C = hC[hd], K = 20 * C, nk = K / 32;
     const bf16_t* wr = reinterpret_cast<const bf16_t*>(a.x.lw[hd]) + (size_t)el * K;
     const int er = el < nenv ? el : 0;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int s = wave; s < nk; s += 8) {
+    for (int s = wave; s < nk; s += NW) {
       const int k = s * 32 + q * 8;
       const int pos = k / C, c = hc0[hd] + (k - pos * C);
-      bf16x8 av = *reinterpret_cast<const bf16x8*>(lds + img + toff(trow(er, pos), c >> 3));
-      if (el >= 4) av = bf16x8{};
+      const int row = R8 ? t8::row8(er, pos) : trow(er, pos);
+      bf16x8 av = *reinterpret_cast<const bf16x8*>(lds + img + toff(row, c >> 3));
+      if (el >= NE) av = bf16x8{};
       const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + k);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
     }
-    if (q == 0)  // D[row = env i][col = output el]
+    if (4 * q < NE)  // D[row = env 4q + i][col = output el]
 #pragma unroll
-      for (int i = 0; i < 4; ++i) part[wave * 4 + i][0][el] = acc[i];
+      for (int i = 0; i < 4; ++i) part[(wave * 8 + 4 * q + i) * 16 + el] = acc[i];
     __syncthreads();
-    if (tid < 64) {
+    if (tid < NE * 16) {
       const int e = tid >> 4, o = tid & 15;
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) v = v + part[w * 4 + e][0][o];
-      if (o < a.x.lO[hd]) lg[hd * 4 + e][0][o] = v + a.x.lb[hd][o];
+      for (int w = 0; w < NW; ++w) v = v + part[(w * 8 + e) * 16 + o];
+      if (o < a.x.lO[hd]) lg[(hd * 8 + e) * 16 + o] = v + a.x.lb[hd][o];
     }
     __syncthreads();
   }
-  if (tid < 4 * nh) {
-    const int hd = tid >> 2, e = tid & 3, b = env0 + e;
+  if (tid < NE * nh) {
+    const int hd = tid / NE, e = tid % NE, b = env0 + e;
     if (e < nenv) {
       const int O = a.x.lO[hd];
       float l[16];
       for (int o = 0; o < O; ++o) {
-        l[o] = lg[hd * 4 + e][0][o];
+        l[o] = lg[(hd * 8 + e) * 16 + o];
         if (a.x.logits[hd]) a.x.logits[hd][(size_t)b * O + o] = l[o];
       }
       if (kind[hd] == 0) {
@@ -330,9 +341,9 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];  // X | T | 16 zero rows
   __shared__ long long envoff[TE];
   __shared__ int acts[TE];
-  __shared__ float part[32][4][16];  // head partial sums [wave * 4 + env][.][output]; min/max scratch
-  __shared__ float lg[8][4][16];     // head logits [head * 4 + env][.][output]
-  __shared__ float dec[2][4][4];     // decoded head outputs [head][env][output]
+  __shared__ float part[8 * 8 * 16];  // head partial sums [wave][env][output]; min/max scratch
+  __shared__ float lg[2 * 8 * 16];    // head logits [head][env][output]
+  __shared__ float dec[2][8][4];      // decoded head outputs [head][env][output]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int env0 = blockIdx.x * TE;
   const int nenv = min(TE, a.B - env0);
@@ -389,8 +400,8 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
                         nullptr, nullptr, 0, lane);
     __syncthreads();
     const int hc0[2] = {0, 0}, hC[2] = {TC, 0}, kind[2] = {1, 0};
-    tower_heads(a, lds, LDS_T, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
-    tower_scale(a, lds, reinterpret_cast<float(*)[2][2]>(&part[0][0][0]), env0, nenv, tid);
+    tower_heads<TE, 8, false>(a, lds, LDS_T, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    tower_scale(a, lds, reinterpret_cast<float(*)[2][2]>(part), env0, nenv, tid);
     return;
   }
   if (a.x.epilogue == 2) {  // prediction: policy 3x3 -> T[0,128), value 1x1 -> T[128,256); Linears
@@ -402,7 +413,7 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
                           128, nullptr, nullptr, 0, lane);
     __syncthreads();
     const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
-    tower_heads(a, lds, LDS_T, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    tower_heads<TE, 8, false>(a, lds, LDS_T, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
       __syncthreads();
       if (tid < nenv) {
@@ -432,13 +443,6 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
 // lane's accumulator holds 4 consecutive channels of one row: 8-byte LDS epilogue stores/loads.
 // One activation image: a conv reads it whole, then (after a barrier) its output overwrites it in
 // place; conv1 first lifts the block input at its own output positions into registers (the residual).
-namespace t8 {
-constexpr int E = 8, ROWS = 160, NRT = 10, NT = 256, CT = 4;  // 4 waves
-constexpr int IMG = ROWS * TROWB;                       // 80 KB
-constexpr int LZ = IMG, BYTES = IMG + 16 * TROWB;       // + 16 zero rows
-// LDS row of (env e, latent position p = 5y + x): env quad (e >> 2) owns tiles 5 (e >> 2) .. +4
-MZ_DEV int row8(int e, int p) { return (e >> 2) * 80 + (p % 5) * 16 + (p / 5) * 4 + (e & 3); }
-}  // namespace t8
 
 template <int DX>
 __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
@@ -497,67 +501,161 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
   }
 }
 
-// one 3x3 conv of the tower over the 8-env image (in place). RESID: acc starts at bias + res.
-template <bool RESID>
-__device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const uint4* __restrict__ wconv,
-                                            const float* __restrict__ bconv, uint2 (&res)[t8::NRT][t8::CT],
-                                            int lane, int wave) {
+// the 8 k steps of a 1x1 conv on the 8-env image (centre tap: all 10 tiles, every row valid)
+__device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
+                                              uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[t8::NRT][t8::CT], int lane) {
+  const int q = lane >> 4, key = lane & 15;
+  const int base = key * TROWB, sw = key << 4;
+  bf16x8 afc[t8::NRT], afn[t8::NRT];
+#pragma unroll
+  for (int j = 0; j < t8::NRT; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    bf16x8 w[t8::CT];
+#pragma unroll
+    for (int ct = 0; ct < t8::CT; ++ct) {
+      w[ct] = __builtin_bit_cast(bf16x8, bq[ct][c % TD]);
+      if (c + TD < 8) bq[ct][c % TD] = wp[ct][(size_t)(c + TD) * 64];
+    }
+#pragma unroll
+    for (int j = 0; j < t8::NRT; ++j) {
+#pragma unroll
+      for (int ct = 0; ct < t8::CT; ++ct)
+        acc[j][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[ct], afc[j], acc[j][ct], 0, 0, 0);
+      if (c + 1 < 8)
+        afn[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
+    }
+#pragma unroll
+    for (int j = 0; j < t8::NRT; ++j) afc[j] = afn[j];
+  }
+}
+
+// k loop of one conv over the 8-env image: this wave's 4 channel tiles ct0..ct0+3 of a weight pack
+// with `tns` k steps per tile (72: 3x3, 8: 1x1). D[pack channel 16 ct + 4q + i][row 16 rt + l16].
+// MODE 0: acc starts at bias; 1: bias + res (registers); 2: bias + act_bias[pos][act[env]].
+template <int MODE, bool CENTER>
+__device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const uint4* __restrict__ wconv, int tns,
+                                           int ct0, const float* __restrict__ bconv, const float* __restrict__ actb,
+                                           const int* acts, int A, const uint2 (&res)[t8::NRT][t8::CT],
+                                           f32x4 (&acc)[t8::NRT][t8::CT], int lane) {
   const int q = lane >> 4, l16 = lane & 15;
   const uint4* wp[t8::CT];
   uint4 bq[t8::CT][TD];
 #pragma unroll
   for (int ct = 0; ct < t8::CT; ++ct) {
-    wp[ct] = wconv + (size_t)(wave * t8::CT + ct) * TNS * 64 + lane;
+    wp[ct] = wconv + (size_t)(ct0 + ct) * tns * 64 + lane;
 #pragma unroll
     for (int i = 0; i < TD; ++i) bq[ct][i] = wp[ct][(size_t)i * 64];
   }
-  // D[channel 16 ct' + 4q + i][row 16 rt + l16], ct' = 4 wave + ct
-  f32x4 acc[t8::NRT][t8::CT];
 #pragma unroll
   for (int ct = 0; ct < t8::CT; ++ct) {
-    const float4 b4 = *reinterpret_cast<const float4*>(bconv + (wave * t8::CT + ct) * 16 + 4 * q);
+    const int n = (ct0 + ct) * 16 + 4 * q;
+    const float4 b4 = *reinterpret_cast<const float4*>(bconv + n);
 #pragma unroll
     for (int rt = 0; rt < t8::NRT; ++rt) {
       f32x4 v = {b4.x, b4.y, b4.z, b4.w};
-      if (RESID) {
+      if (MODE == 1) {
         const uint2 r = res[rt][ct];
         v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
         v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
+      } else if (MODE == 2) {  // row -> env quad rt / 5, latent x = rt % 5, y = l16 >> 2, env l16 & 3
+        const int env = (rt / 5) * 4 + (l16 & 3), pos = (l16 >> 2) * 5 + rt % 5;
+        const float4 t = *reinterpret_cast<const float4*>(actb + ((size_t)pos * A + acts[env]) * TC + n);
+        v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
       }
       acc[rt][ct] = v;
     }
   }
-  tower8_dx<-1>(lds, wp, bq, acc, lane);
-  tower8_dx<0>(lds, wp, bq, acc, lane);
-  tower8_dx<1>(lds, wp, bq, acc, lane);
-  __syncthreads();  // every wave has read the whole image
+  if (CENTER) {
+    tower8_center(lds, wp, bq, acc, lane);
+  } else {
+    tower8_dx<-1>(lds, wp, bq, acc, lane);
+    tower8_dx<0>(lds, wp, bq, acc, lane);
+    tower8_dx<1>(lds, wp, bq, acc, lane);
+  }
+}
+
+// ReLU -> bf16 -> the image at channel nout + 16 (ct0 + ct) + 4q (8-byte stores, in place after a
+// barrier); SAVE: first lift the image's values there into res (the block input = conv2's residual)
+template <bool SAVE>
+__device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, const f32x4 (&acc)[t8::NRT][t8::CT],
+                                                 uint2 (&res)[t8::NRT][t8::CT], int nout, int ct0, int lane) {
+  const int q = lane >> 4, l16 = lane & 15;
 #pragma unroll
   for (int rt = 0; rt < t8::NRT; ++rt)
 #pragma unroll
     for (int ct = 0; ct < t8::CT; ++ct) {
-      const int n = (wave * t8::CT + ct) * 16 + 4 * q;
+      const int n = nout + (ct0 + ct) * 16 + 4 * q;
       uint2* p = reinterpret_cast<uint2*>(lds + toff(rt * 16 + l16, n >> 3) + ((n & 7) << 1));
-      if (!RESID) res[rt][ct] = *p;  // block input at this position: conv2's residual
+      if (SAVE) res[rt][ct] = *p;
       uint2 o;
       o.x = (uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][0], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][1], 0.f)) << 16);
       o.y = (uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][2], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][3], 0.f)) << 16);
       *p = o;
     }
+}
+
+// _scale_state over the 8-env image: 32 threads per env, 20 chunks each; bf16 to out (+ pool slot)
+__device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* __restrict__ lds, int env0, int nenv,
+                                             int tid) {
+  const int e = tid >> 5, t = tid & 31;
+  float mn = INFINITY, mx = -INFINITY;
+  for (int u = 0; u < 20; ++u) {
+    const int i = u * 32 + t, p = i >> 5, c = i & 31;
+    const uint4 v = *reinterpret_cast<const uint4*>(lds + toff(t8::row8(e, p), c));
+    const bf16_t* h = reinterpret_cast<const bf16_t*>(&v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const float f = bf16_to_f32(h[j]); mn = fminf(mn, f); mx = fmaxf(mx, f); }
+  }
+  for (int o = 16; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
+  if (e >= nenv) return;
+  const float den = (mx - mn) + 1e-8f;
+  const int b = env0 + e;
+  bf16_t* o1 = a.out + (size_t)b * 20 * TC;
+  bf16_t* o2 = a.x.pool ? reinterpret_cast<bf16_t*>(a.x.pool) + (size_t)b * a.x.pool_env_stride +
+                              (size_t)a.x.pool_slot * 20 * TC
+                        : nullptr;
+  for (int u = 0; u < 20; ++u) {
+    const int i = u * 32 + t, p = i >> 5, c = i & 31;
+    uint4 r = *reinterpret_cast<const uint4*>(lds + toff(t8::row8(e, p), c));
+    bf16_t* h = reinterpret_cast<bf16_t*>(&r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = f32_to_bf16((bf16_to_f32(h[j]) - mn) / den);
+    *reinterpret_cast<uint4*>(o1 + p * TC + c * 8) = r;
+    if (o2) *reinterpret_cast<uint4*>(o2 + p * TC + c * 8) = r;
+  }
+}
+
+// one residual-tower conv (in place): k loop, barrier, write back, barrier
+template <bool RESID>
+__device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const uint4* __restrict__ wconv,
+                                            const float* __restrict__ bconv, uint2 (&res)[t8::NRT][t8::CT],
+                                            int lane, int wave) {
+  f32x4 acc[t8::NRT][t8::CT];
+  tower8_acc<RESID ? 1 : 0, false>(lds, wconv, TNS, wave * t8::CT, bconv, nullptr, nullptr, 0, res, acc, lane);
+  __syncthreads();  // every wave has read the whole image
+  tower8_writeback<!RESID>(lds, acc, res, 0, wave * t8::CT, lane);
   __syncthreads();
 }
 
 __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[t8::BYTES];
   __shared__ long long envoff[t8::E];
+  __shared__ int acts[t8::E];
+  __shared__ float part[4 * 8 * 16];  // head partial sums [wave][env][output]
+  __shared__ float lg[2 * 8 * 16];    // head logits [head][env][output]
+  __shared__ float dec[2][8][4];      // decoded head outputs [head][env][output]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int env0 = blockIdx.x * t8::E;
   const int nenv = min(t8::E, a.B - env0);
   const int rows = nenv * 20;
+  const bool pro = a.x.w0 != nullptr;
   if (tid < t8::E) {
     const int b = env0 + (tid < nenv ? tid : 0);
     long long off = (long long)b * a.in_env_stride;
     if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
     envoff[tid] = off;
+    acts[tid] = pro ? a.x.act[b] : 0;
   }
   __syncthreads();
   {  // stage X: 160 rows x 32 chunks = 5120 chunks, 20 per thread (two batches of 10)
@@ -584,12 +682,57 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     for (int u = 0; u < 2; ++u) *reinterpret_cast<uint4*>(lds + t8::LZ + (u * t8::NT + tid) * 16) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
+  uint2 res[t8::NRT][t8::CT];
+  if (pro) {  // dynamics ConvBlock (in place)
+    f32x4 acc[t8::NRT][t8::CT];
+    tower8_acc<2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), TNS, wave * t8::CT, a.x.b0, a.x.act_bias, acts,
+                         a.x.A, res, acc, lane);
+    __syncthreads();
+    tower8_writeback<false>(lds, acc, res, 0, wave * t8::CT, lane);
+    __syncthreads();
+  }
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;
-  uint2 res[t8::NRT][t8::CT];
   for (int blk = 0; blk < a.nblocks; ++blk) {
     tower8_conv<false>(lds, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, res, lane, wave);
     tower8_conv<true>(lds, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, res, lane, wave);
+  }
+  if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1, the scaled latent from X, then Linear + decode
+    f32x4 acc[t8::NRT][t8::CT];
+    tower8_acc<0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, wave * t8::CT, a.x.be1, nullptr, nullptr, 0,
+                        res, acc, lane);
+    __syncthreads();
+    tower8_scale(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
+    __syncthreads();
+    tower8_writeback<false>(lds, acc, res, 0, wave * t8::CT, lane);
+    __syncthreads();
+    const int hc0[2] = {0, 0}, hC[2] = {TC, 0}, kind[2] = {1, 0};
+    tower_heads<t8::E, 4, true>(a, lds, 0, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    return;
+  }
+  if (a.x.epilogue == 2) {  // prediction: policy 3x3 (waves 0-1) -> [0,128), value 1x1 (waves 2-3) -> [128,256)
+    f32x4 acc[t8::NRT][t8::CT];
+    const int ct0 = (wave & 1) * t8::CT;
+    if (wave < 2)
+      tower8_acc<0, false>(lds, reinterpret_cast<const uint4*>(a.x.we3), TNS, ct0, a.x.be3, nullptr, nullptr, 0, res,
+                           acc, lane);
+    else
+      tower8_acc<0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, ct0, a.x.be1, nullptr, nullptr, 0, res, acc,
+                          lane);
+    __syncthreads();
+    tower8_writeback<false>(lds, acc, res, wave < 2 ? 0 : 128, ct0, lane);
+    __syncthreads();
+    const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
+    tower_heads<t8::E, 4, true>(a, lds, 0, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
+      __syncthreads();
+      if (tid < nenv) {
+        const int b = env0 + tid;
+        tree_backup_env(a.tree, a.tree_sim, b, a.tree_r[b], dec[1][tid][0], &dec[0][tid][0], a.tree_gamma);
+        if (a.tree_sim + 1 < a.tree.S) tree_select_env(a.tree, a.tree_sim + 1, b);
+      }
+    }
+    return;
   }
 #pragma unroll 4
   for (int u = 0; u < 20; ++u) {
@@ -658,13 +801,13 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
   return 0;
 }
 
-// Dynamics / prediction step as one launch of the 4-env kernel (see include/mzba.h). Returns -4 when the
-// batch is planned on the 8-env kernel (the caller then runs the unfused sequence).
+// Dynamics / prediction step as one launch of the planned tower kernel (see include/mzba.h).
 int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                      void* out, const void* wf16, const float* bias, int nblocks, int B, const mzba_tower_ext* ext,
                      hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && wf16 && bias && ext, -1);
-  MZ_CHECK_ARG(mzba_tower_plan(B) == 1, -4);
+  const int plan = mzba_tower_plan(B);
+  MZ_CHECK_ARG(plan == 1 || plan == 2, -4);
   const mzba_tower_ext& x = *ext;
   MZ_CHECK_ARG(x.epilogue >= 0 && x.epilogue <= 2, -2);
   MZ_CHECK_ARG(!x.w0 || (x.b0 && x.act_bias && x.act && x.A > 0), -3);
@@ -686,7 +829,10 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
     a.tree_gamma = t.gamma;
     a.tree_r = t.r;
   }
-  hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
+  if (plan == 2)
+    hipLaunchKernelGGL(tower8_kernel, dim3((B + t8::E - 1) / t8::E), dim3(t8::NT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
   MZ_LAUNCH_CHECK();
   return 0;
 }

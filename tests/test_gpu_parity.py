@@ -206,16 +206,22 @@ def test_nets_bf16_close():
     assert np.abs(rl.cpu().numpy() - d["r1"]).max() < 0.05
 
 
-@pytest.mark.parametrize("B", [13, 1024])
-def test_fused_steps_match_unfused(B):
+@pytest.mark.parametrize("B,variant", [(13, 1), (1024, 1), (13, 2), (2048, 0)])
+def test_fused_steps_match_unfused(B, variant):
     """mzba_tower_fused (dynamics ConvBlock + tower + reward head + scale in one launch; tower +
-    policy/value heads in one launch) vs the per-layer launch sequence, both bf16, same inputs."""
+    policy/value heads in one launch) vs the per-layer launch sequence, both bf16, same inputs;
+    on the 4-env (variant 1) and the 8-env kernel (2; 0 = by batch: 2048 plans the 8-env one)."""
+    from mzba import _lib as L
     from mzba.agent import MuZeroAgent
     mcfg = default_config()["model"]
     ag = MuZeroAgent(mcfg, dtype="bf16")
     ag.load_state_dict(init_state_dict(mcfg, 7))
-    rn = ag.runner(B, 16, 20)
-    assert rn.fused_ok()
+    L.call("mzba_tower_set_variant", variant)
+    try:
+        rn = ag.runner(B, 16, 20)
+    finally:
+        L.call("mzba_tower_set_variant", 0)
+    assert rn.fused_ok() and rn.tower_plan == (variant or 2)
     S1, n = 3, 20 * 256
     g = torch.Generator().manual_seed(B)
     pool0 = torch.rand(B, S1 + 1, n, generator=g).to(torch.bfloat16).cuda()
@@ -672,9 +678,11 @@ def test_checkpoint_reference_format_roundtrip(tmp_path):
     assert buf.get_reward_sums() == buf2.get_reward_sums()
 
 
-def test_tree_step_fused_into_prediction_is_identical():
+@pytest.mark.parametrize("variant", [1, 2])
+def test_tree_step_fused_into_prediction_is_identical(variant):
     """backup(sim) + select(sim + 1) inside the fused prediction launch == the separate tree
     kernels: same visit counts, values and tie-break draws, bit for bit (bf16 nets)."""
+    from mzba import _lib as L
     from mzba.agent import MuZeroAgent
     from mzba.search import MCTSSearchVec
     cfg = default_config()
@@ -686,12 +694,17 @@ def test_tree_step_fused_into_prediction_is_identical():
     g = torch.Generator().manual_seed(5)
     h = torch.rand(B, 256, 4, 5, generator=g).cuda()
     out = []
-    for fuse in (False, True):
-        s = MCTSSearchVec(cfg, ag, None, seed=17)
-        ws = s.workspace(B)
-        ws.use_tree_fusion = fuse
-        assert ws.runner.fused_ok()
-        v, c = s.search(h)
-        out.append((v.numpy(), c.numpy()))
+    L.call("mzba_tower_set_variant", variant)
+    try:
+        for fuse in (False, True):
+            ag._runners = {}
+            s = MCTSSearchVec(cfg, ag, None, seed=17)
+            ws = s.workspace(B)
+            ws.use_tree_fusion = fuse
+            assert ws.runner.fused_ok() and ws.runner.tower_plan == variant
+            v, c = s.search(h)
+            out.append((v.numpy(), c.numpy()))
+    finally:
+        L.call("mzba_tower_set_variant", 0)
     np.testing.assert_array_equal(out[0][1], out[1][1])
     np.testing.assert_array_equal(out[0][0], out[1][0])
