@@ -38,24 +38,27 @@ int mzba_grayscale_planes(const float* state, float* gray, int B, int H, int W, 
 /* Compact env for the fused acting loop: same rules as mzba_env_step_planes on SoA scalars
  * (paddle col, ball x/y, dx, dy, done) + a brick bitmask (nw u64 words per env over the brick rows).
  * Reset also does _pad_initial_state (train_torch.py:313-332): frame-history ring filled with
- * g(s0) (L-1 frames of H*W u8 gray codes), action ring (L) zeroed, hist_len = 0. */
+ * g(s0) (L-1 frames of H*W u8 gray codes), action ring (L) filled with pad_action (0 for the acting
+ * loop, 1 for run_test_simulation, train_torch.py:545), hist_len = 0. */
 int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
                            uint64_t* bricks, int nw, uint8_t* cur_frame, uint8_t* hist_frames,
                            uint8_t* hist_actions, int32_t* hist_len, int L, int B, int H, int W, int paddle_width,
                            int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
-                           hipStream_t stream);
+                           int pad_action, hipStream_t stream);
 
 /* One acting-loop env step (train_torch.py:201-209): step, render the u8 gray frame, push
  * (action, frame) into the history ring when the env is recorded (not prev_done; at the first
  * step prev_done aliases done, :179), and write the trajectory-sink row (rec_* may be NULL).
  * ctx (optional, graph replay): device int32[3] step context; when given, the sink row is
  * ctx[2] (rec_* are the (T,B,..) bases) and first_step = (ctx[2] == 0). */
+/* rec_flags: 0 = record envs that were live before the step (the acting loop); bit 0 = record every
+ * env, bit 1 = record env 0's action for every env (run_test_simulation, train_torch.py:594-598). */
 int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
                           uint64_t* bricks, int nw, const int64_t* action, float* reward, float* valid,
                           uint8_t* cur_frame, uint8_t* hist_frames, uint8_t* hist_actions, int32_t* hist_len, int L,
                           uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
                           int first_step, int B, int H, int W, int paddle_width, int brick_rows,
-                          const float* rewards4, const int32_t* ctx, hipStream_t stream);
+                          const float* rewards4, const int32_t* ctx, int rec_flags, hipStream_t stream);
 
 /* compact -> reference planes (B,3,H,W) f32. */
 int mzba_compact_to_planes(const int32_t* paddle, const int32_t* bx, const int32_t* by, const uint8_t* done,

@@ -167,7 +167,7 @@ struct History { uint8_t* frames; uint8_t* actions; int32_t* hlen; int L; };
 // recorded frame is cur_frame (written to rec_frame[t][b][HW] when non-null).
 struct Sink { uint8_t* action; float* reward; uint8_t* mask; uint8_t* frame; };
 
-__global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_frame, History hist, int B,
+__global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_frame, History hist, int pad_action, int B,
                                          int H, int W, int pw, int brick_rows, uint64_t seed, int episode,
                                          int env_offset, const int32_t* __restrict__ params) {
   // one block per env: scalars by thread 0, frame + history pad by the block
@@ -196,7 +196,7 @@ __global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_f
     cf[p] = c;
     for (int k = 0; k < hist.L - 1; ++k) hist.frames[((size_t)b * (hist.L - 1) + k) * HW + p] = c;
   }
-  for (int k = threadIdx.x; k < hist.L; k += blockDim.x) hist.actions[(size_t)b * hist.L + k] = 0;
+  for (int k = threadIdx.x; k < hist.L; k += blockDim.x) hist.actions[(size_t)b * hist.L + k] = (uint8_t)pad_action;
 }
 
 // Phase 1: one thread per env, all rules on the compact state (same op order as above).
@@ -207,7 +207,7 @@ template <int MAXW>
 __global__ __launch_bounds__(256) void env_step_compact_kernel(
     Compact cs, const int64_t* __restrict__ action, float* __restrict__ reward, float* __restrict__ valid,
     uint8_t* __restrict__ cur_frame, History hist, Sink sink, int first_step_arg, int B, int H, int W, int pw,
-    int brick_rows, RewardCfg rc, const int32_t* __restrict__ ctx, int E) {
+    int brick_rows, RewardCfg rc, const int32_t* __restrict__ ctx, int E, int rec_flags) {
   // graph replay: the episode row t comes from the device context; the sink pointers are the
   // (T, B, ...) bases and row t is selected here; t == 0 is the first step
   const int first_step = ctx ? (ctx[2] == 0) : first_step_arg;
@@ -286,17 +286,20 @@ __global__ __launch_bounds__(256) void env_step_compact_kernel(
     valid[b * 3 + 0] = pnew == 0 ? 0.f : 1.f;
     valid[b * 3 + 1] = 1.f;
     valid[b * 3 + 2] = (pnew + pw >= W) ? 0.f : 1.f;
-    // record iff not prev_done; at the first step prev_done aliases done (train_torch.py:179)
-    const bool rec = first_step ? !dfin : !was_done;
+    // record iff not prev_done; at the first step prev_done aliases done (train_torch.py:179).
+    // rec_flags (run_test_simulation, train_torch.py:594-598): bit 0 records every env, bit 1
+    // records env 0's action for every env (the reference's action[0] there)
+    const bool rec = (rec_flags & 1) ? true : (first_step ? !dfin : !was_done);
+    const int64_t ra = (rec_flags & 2) ? action[0] : a;
     if (sink.action) {
-      sink.action[b] = (uint8_t)a; sink.reward[b] = r; sink.mask[b] = rec ? 1 : 0;
+      sink.action[b] = (uint8_t)ra; sink.reward[b] = r; sink.mask[b] = rec ? 1 : 0;
     }
     s_paddle[t] = dfin ? -1 : pnew; s_bx[t] = ix; s_by[t] = fy; s_done[t] = dfin; s_rec[t] = rec;
 #pragma unroll
     for (int w = 0; w < MAXW; ++w) s_br[t][w] = br[w];
     if (rec) {
       int hl = hist.hlen[b];
-      hist.actions[(size_t)b * hist.L + (hl % hist.L)] = (uint8_t)a;
+      hist.actions[(size_t)b * hist.L + (hl % hist.L)] = (uint8_t)ra;
     }
   }
   __syncthreads();
@@ -457,11 +460,12 @@ int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* d
                            uint64_t* bricks, int nw, uint8_t* cur_frame, uint8_t* hist_frames,
                            uint8_t* hist_actions, int32_t* hist_len, int L, int B, int H, int W, int paddle_width,
                            int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
-                           hipStream_t stream) {
-  MZ_CHECK_ARG(B > 0 && L >= 2 && nw * 64 >= brick_rows * W && nw <= 4 && (H * W) % 16 == 0, -1);
+                           int pad_action, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && L >= 2 && nw * 64 >= brick_rows * W && nw <= 4 && (H * W) % 16 == 0 && pad_action >= 0 &&
+               pad_action < 3, -1);
   Compact cs{paddle, bx, by, dx, dy, done, bricks, nw};
   History h{hist_frames, hist_actions, hist_len, L};
-  hipLaunchKernelGGL(env_reset_compact_kernel, dim3(B), dim3(256), 0, stream, cs, cur_frame, h, B, H, W,
+  hipLaunchKernelGGL(env_reset_compact_kernel, dim3(B), dim3(256), 0, stream, cs, cur_frame, h, pad_action, B, H, W,
                      paddle_width, brick_rows, seed, episode, env_offset, params);
   MZ_LAUNCH_CHECK();
   return 0;
@@ -472,7 +476,7 @@ int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx
                           uint8_t* cur_frame, uint8_t* hist_frames, uint8_t* hist_actions, int32_t* hist_len, int L,
                           uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
                           int first_step, int B, int H, int W, int paddle_width, int brick_rows,
-                          const float* rewards4, const int32_t* ctx, hipStream_t stream) {
+                          const float* rewards4, const int32_t* ctx, int rec_flags, hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && L >= 2 && nw >= 1 && nw <= 4 && nw * 64 >= brick_rows * W && (H * W) % 16 == 0 && rewards4,
                -1);
   Compact cs{paddle, bx, by, dx, dy, done, bricks, nw};
@@ -486,10 +490,10 @@ int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx
   dim3 grid((B + E - 1) / E);
   if (nw == 1)
     hipLaunchKernelGGL(env_step_compact_kernel<1>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
-                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx, E);
+                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx, E, rec_flags);
   else
     hipLaunchKernelGGL(env_step_compact_kernel<4>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
-                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx, E);
+                       h, sk, first_step, B, H, W, paddle_width, brick_rows, rc, ctx, E, rec_flags);
   MZ_LAUNCH_CHECK();
   return 0;
 }

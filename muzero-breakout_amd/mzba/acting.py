@@ -55,7 +55,7 @@ class ActingLoop:
     MAX_STEPS = 261  # train_torch.py:186 `length_counter > 260`
 
     def __init__(self, cfg, agent, B, seed=0, env_offset=0, temperature=1.0, height=16, width=20,
-                 record_frames=True, max_steps=MAX_STEPS):
+                 record_frames=True, max_steps=MAX_STEPS, pad_action=0, rec_flags=0):
         self.cfg, self.agent, self.B = cfg, agent, B
         self.seed, self.env_offset = seed, env_offset
         self.temperature = temperature
@@ -65,7 +65,7 @@ class ActingLoop:
         self.H, self.W = height, width
         dev = agent.device
         self.env = CompactBreakout(cfg["environment"], B, self.Lh, height, width, seed=seed, env_offset=env_offset,
-                                   device=dev)
+                                   device=dev, pad_action=pad_action, rec_flags=rec_flags)
         self.search = MCTSSearchVec(cfg, agent, None, seed=seed, env_offset=env_offset)
         self.ws = SearchWorkspace(self.search, B)
         p = agent.packed
@@ -162,7 +162,7 @@ class ActingLoop:
         out = []
         for b in range(B):
             m = rec["mask"][:, b].astype(bool)
-            acts = [0] * L_ + [int(a) for a in rec["action"][m, b]]
+            acts = [self.env.pad_action] * L_ + [int(a) for a in rec["action"][m, b]]
             pad = torch.from_numpy(lut[f0[b] & 7].reshape(1, H, W))
             states = [pad] * (L_ - 1)
             if rec["frame"] is not None:
@@ -175,6 +175,35 @@ class ActingLoop:
                 rs = np.float32(rs + r)
             out.append(ObservationTrajectory(acts, states, rews, vc, vals, int(m.sum()), float(rs)))
         return out
+
+
+def run_test_simulation(cfg, agent, batch=2, seed=0, episode=0, max_steps_test=200, temperature=0.1,
+                        log_noise=False):
+    """RLSystem.run_test_simulation (train_torch.py:530-610) on the device: `batch` envs played
+    with the given agent at temperature 0.1 until all are done or after max_steps_test + 1 steps,
+    with the reference's quirks (padding action 1, every env recorded every step with env 0's
+    action). Returns (ObservationTrajectory per env, frames per env: the grayscale (1, H, W)
+    frames of the steps after which the env was still live — what the reference logs — and the
+    loop). The reference writes the frames of env 0 to tensorboard; logging is left to the caller."""
+    loop = ActingLoop(cfg, agent, batch, seed=seed, temperature=temperature, max_steps=max_steps_test + 1,
+                      pad_action=1, rec_flags=3)
+    loop.noise_log = [] if log_noise else None
+    loop.reset(episode)
+    H, W = loop.H, loop.W
+    lut = gray_lut()
+    frames = [[] for _ in range(batch)]
+    step_i = 0
+    while not loop.all_done():  # :559
+        if step_i > max_steps_test:  # :562
+            break
+        loop.act(eager=True)
+        done = loop.env.done.cpu().numpy().astype(bool)
+        cur = loop.env.cur_frame.view(batch, -1).cpu().numpy()
+        for b in range(batch):  # :583-585
+            if not done[b]:
+                frames[b].append(torch.from_numpy(lut[cur[b] & 7].reshape(1, H, W)))
+        step_i += 1
+    return loop.trajectories(), frames, loop
 
 
 class ActingStage:

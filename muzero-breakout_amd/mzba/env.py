@@ -125,12 +125,14 @@ class CompactBreakout:
     """Device-resident compact env state for B envs + frame-history ring of length L."""
 
     def __init__(self, cfg_env, B, L_hist, height=16, width=20, paddle_width=6, brick_rows=3, seed=0, env_offset=0,
-                 device="cuda"):
+                 device="cuda", pad_action=0, rec_flags=0):
         L.require_gpu()
         self.B, self.H, self.W = B, height, width
         self.pw, self.brick_rows = paddle_width, brick_rows
         self.Lh = L_hist
         self.seed, self.env_offset = seed, env_offset
+        # run_test_simulation (train_torch.py:530-610): pad action 1, every env recorded with action[0]
+        self.pad_action, self.rec_flags = pad_action, rec_flags
         self.rewards4 = (ctypes.c_float * 4)(cfg_env["paddle_hit_reward"], cfg_env["brick_hit_reward"],
                                              cfg_env["game_lost_reward"], cfg_env["game_won_reward"])
         dev = torch.device(device)
@@ -159,7 +161,7 @@ class CompactBreakout:
             pr = torch.as_tensor(np.asarray(params, dtype=np.int32), device=self.device).contiguous()
         L.call("mzba_env_reset_compact", *self._state_ptrs(), L.ptr(self.cur_frame), L.ptr(self.hist_frames),
                L.ptr(self.hist_actions), L.ptr(self.hist_len), self.Lh, self.B, self.H, self.W, self.pw,
-               self.brick_rows, self.seed, episode, self.env_offset, L.ptr(pr), L.stream())
+               self.brick_rows, self.seed, episode, self.env_offset, L.ptr(pr), self.pad_action, L.stream())
         self.valid.fill_(1.0)
 
     def step(self, action, first_step, rec=None, t=0, ctx=None):
@@ -175,7 +177,7 @@ class CompactBreakout:
         L.call("mzba_env_step_compact", *self._state_ptrs(), L.ptr(action), L.ptr(self.reward), L.ptr(self.valid),
                L.ptr(self.cur_frame), L.ptr(self.hist_frames), L.ptr(self.hist_actions), L.ptr(self.hist_len), self.Lh,
                L.ptr(ra), L.ptr(rr), L.ptr(rm), L.ptr(rf), 1 if first_step else 0, self.B, self.H, self.W, self.pw,
-               self.brick_rows, self.rewards4, L.ptr(ctx), L.stream())
+               self.brick_rows, self.rewards4, L.ptr(ctx), self.rec_flags, L.stream())
 
     def to_planes(self):
         planes = torch.empty(self.B, 3, self.H, self.W, dtype=torch.float32, device=self.device)

@@ -118,3 +118,38 @@ def run_episode(cfg, sd, seed, episode, noise_fn, n_parallel, max_steps=261, tem
             on_step(t, log[-1])
         t += 1
     return trajs, log
+
+
+def run_test_simulation(cfg, sd, seed, episode, noise_fn, batch=2, max_steps_test=200, temperature=0.1,
+                        search_id0=0, step0=0):
+    """RLSystem.run_test_simulation (train_torch.py:530-610) with injected randomness: padding
+    action 1 (:545), temperature 0.1 sampling (:571-579), frames kept while the env is live
+    (:583-585), and every env's trajectory extended every step with env 0's action (:594-598)."""
+    mcfg = cfg["model"]
+    L = mcfg["state_history_length"]
+    env = BreakoutEnvOracle({**cfg["environment"], "n_parallel": batch})
+    state, _ = env.reset(env.reset_params(seed, episode))
+    warp = convert_to_grayscale(state)
+    trajs = [Trajectory(L, warp[b], pad_action=1) for b in range(batch)]
+    search = MCTSOracle(cfg, NetModel(sd, mcfg), seed)
+    done = np.zeros(batch, dtype=bool)
+    frames = [[] for _ in range(batch)]
+    step_i = 0
+    while not np.all(done):
+        if step_i > max_steps_test:
+            break
+        x = np.stack([prepare_mcts_input(warp[b], trajs[b], L) for b in range(batch)])
+        h = N.create_hidden_state_root(x, sd, mcfg)
+        sid = search_id0 + step_i
+        values, counts = search.search(h, noise_fn(sid, batch), sid, 0)
+        u = R.uniform(np.arange(batch), R.STREAM_SAMPLE, step0 + step_i, 0, seed)
+        action = sample_actions(counts, temperature, u)
+        state, reward, done, valid = env.step(state, action, done)
+        warp = convert_to_grayscale(state)
+        for b in range(batch):
+            if not done[b]:
+                frames[b].append(warp[b].copy())
+        step_i += 1
+        for b in range(batch):
+            trajs[b].add_observation(action[0], warp[b], reward[b], counts[b], values[b])
+    return trajs, frames

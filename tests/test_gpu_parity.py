@@ -708,3 +708,31 @@ def test_tree_step_fused_into_prediction_is_identical(variant):
         L.call("mzba_tower_set_variant", 0)
     np.testing.assert_array_equal(out[0][1], out[1][1])
     np.testing.assert_array_equal(out[0][0], out[1][0])
+
+
+def test_test_simulation_matches_oracle():
+    """run_test_simulation (train_torch.py:530-610) on the device vs the oracle restatement: padding
+    action 1, T = 0.1 sampling, action[0] recorded for every env, frames while live (f32 nets)."""
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import run_test_simulation
+    from oracle.acting import run_test_simulation as oracle_test
+    cfg = _small_cfg(12)
+    mcfg = cfg["model"]
+    sd = init_state_dict(mcfg, 8)
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(sd)
+    trajs, frames, loop = run_test_simulation(cfg, ag, batch=2, seed=55, max_steps_test=40, log_noise=True)
+    noises = [n.cpu().numpy() for n in loop.noise_log]
+    otrajs, oframes = oracle_test(cfg, sd, 55, 0, lambda sid, n: noises[sid], batch=2, max_steps_test=40)
+    L_ = mcfg["state_history_length"]
+    for b in range(2):
+        assert trajs[b].length == otrajs[b].length
+        np.testing.assert_array_equal(trajs[b].actions, otrajs[b].actions)
+        np.testing.assert_array_equal(np.stack([s.numpy() for s in trajs[b].states]), np.stack(otrajs[b].states))
+        np.testing.assert_array_equal(np.array(trajs[b].rewards[L_:], np.float32),
+                                      np.array(otrajs[b].rewards[L_:], np.float32))
+        np.testing.assert_array_equal(np.stack([c.numpy() for c in trajs[b].visit_counts[L_:]]),
+                                      np.stack(otrajs[b].visit_counts[L_:]))
+        assert len(frames[b]) == len(oframes[b])
+        if frames[b]:
+            np.testing.assert_array_equal(np.stack([f.numpy() for f in frames[b]]), np.stack(oframes[b]))
