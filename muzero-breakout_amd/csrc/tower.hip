@@ -42,7 +42,12 @@ constexpr int TD = TOWER_TD;       // weight ring depth (k steps); must divide t
 static_assert(8 % TD == 0, "ring index restarts at every tap");
 #ifndef TOWER_ABLATE
 #define TOWER_ABLATE 0  // diagnostic builds only (make tower-variants): 1 hot weights, 2 no LDS A reads,
-                        // 3 duplicate weight streams
+                        // 3 duplicate weight streams (waves w, w+4), 4 = 3 with waves 4-7 started late
+#endif
+#if TOWER_ABLATE == 3 || TOWER_ABLATE == 4
+#define TOWER_CT0(wave) (2 * ((wave) & 3))
+#else
+#define TOWER_CT0(wave) (2 * (wave))
 #endif
 constexpr int TNT = 512;
 constexpr int IMG = TROWS * TROWB;         // one activation image (40 KB)
@@ -388,11 +393,17 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;  // uint4 per conv
   for (int blk = 0; blk < a.nblocks; ++blk) {
-    tower_conv<0, false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, TNS, 2 * wave, a.bias + (2 * blk) * TC, 0,
+#if TOWER_ABLATE == 4  // diagnostic: the duplicate-stream waves trail by ~1 k step so their loads hit L1
+    if (wave >= 4) __builtin_amdgcn_s_sleep(6);
+#endif
+    tower_conv<0, false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, TNS, TOWER_CT0(wave), a.bias + (2 * blk) * TC, 0,
                          nullptr, nullptr, 0, lane);
     __syncthreads();
-    tower_conv<1, false>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, TNS, 2 * wave, a.bias + (2 * blk + 1) * TC,
-                         0, nullptr, nullptr, 0, lane);
+#if TOWER_ABLATE == 4
+    if (wave >= 4) __builtin_amdgcn_s_sleep(6);
+#endif
+    tower_conv<1, false>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, TNS, TOWER_CT0(wave),
+                         a.bias + (2 * blk + 1) * TC, 0, nullptr, nullptr, 0, lane);
     __syncthreads();
   }
   if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1 (X -> T), Linear + decode, scaled latent

@@ -5,7 +5,7 @@ set -e
 export TMPDIR=/tmp
 O=gpurun_out/$1
 mkdir -p $O
-for v in def ab1 ab3; do
+for v in def ab3 ab4; do
   if [ $v = def ]; then unset MZBA_LIB; else export MZBA_LIB=muzero-breakout_amd/mzba/libmzba_$v.so; fi
   timeout -k 10 200 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCR_TCP_STALL_CYCLES_sum TA_BUSY_avr GRBM_GUI_ACTIVE --kernel-trace -d $O/$v -o run -- python3 tools/pmc_conv.py 1024 tower 14 > $O/$v.log 2>&1 && echo $v ok
   timeout -k 10 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum TCC_BUSY_avr TD_TD_BUSY_avr --kernel-trace -d $O/${v}_b -o run -- python3 tools/pmc_conv.py 1024 tower 14 > $O/${v}_b.log 2>&1 && echo $v b ok
@@ -13,7 +13,7 @@ done
 python3 - "$O" <<'PY'
 import sys, glob, sqlite3, statistics
 o = sys.argv[1]
-for p in ("def", "ab1", "ab3", "def_b", "ab1_b", "ab3_b"):
+for p in ("def", "ab3", "ab4", "def_b", "ab3_b", "ab4_b"):
     dbs = glob.glob(f"{o}/{p}/**/*.db", recursive=True)
     if not dbs:
         print(p, "no db"); continue
