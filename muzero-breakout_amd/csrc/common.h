@@ -24,10 +24,12 @@
 // ------------------------------------------------------------------ bf16
 typedef uint16_t bf16_t;
 MZ_DEV float bf16_to_f32(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
-MZ_DEV bf16_t f32_to_bf16(float f) {  // round-to-nearest-even (finite inputs)
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
+typedef __attribute__((ext_vector_type(2))) __bf16 mz_bf16x2;
+// round-to-nearest-even; gfx950 converts in hardware (v_cvt_pk_bf16_f32)
+MZ_DEV bf16_t f32_to_bf16(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+MZ_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  const mz_bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 template <typename T> struct ElemIO;

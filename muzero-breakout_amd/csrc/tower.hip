@@ -127,8 +127,8 @@ __device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int sr
 #endif
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        acc0[A0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[j], w0, acc0[A0 + j], 0, 0, 0);
-        acc1[A0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[j], w1, acc1[A0 + j], 0, 0, 0);
+        acc0[A0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, afc[j], acc0[A0 + j], 0, 0, 0);
+        acc1[A0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, afc[j], acc1[A0 + j], 0, 0, 0);
         if (TOWER_ABLATE == 2)  // diagnostic only: no LDS A reads inside the loop
           afn[j] = afc[j];
         else if (c + 1 < NC)
@@ -171,8 +171,8 @@ __device__ __forceinline__ void tower_center(const uint8_t* __restrict__ lds, in
     }
 #pragma unroll
     for (int j = 0; j < TR; ++j) {
-      acc0[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[j], w0, acc0[j], 0, 0, 0);
-      acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afc[j], w1, acc1[j], 0, 0, 0);
+      acc0[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, afc[j], acc0[j], 0, 0, 0);
+      acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, afc[j], acc1[j], 0, 0, 0);
       if (c + 1 < 8)
         afn[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
     }
@@ -197,28 +197,34 @@ __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg
   uint4 b0q[TD], b1q[TD];
 #pragma unroll
   for (int i = 0; i < TD; ++i) { b0q[i] = wp0[(size_t)i * 64]; b1q[i] = wp1[(size_t)i * 64]; }
-  // accumulator init; D[row = 4q + i][col = l16] of tile rt: latent (y = q, x = rt), env i
-  const int n0 = ct0 * 16 + l16, n1 = ct1 * 16 + l16;
-  const int c0 = nout + n0, c1 = nout + n1;  // image channels
-  const float bb0 = bconv[n0], bb1 = bconv[n1];
+  // weights are the MFMA A operand: D[pack channel 16 ct + 4q + i][row 16 rt + l16], so a lane
+  // holds 4 consecutive channels of one row (8-byte LDS reads / writes); row l16 of tile rt =
+  // latent (y = l16 >> 2, x = rt) of env l16 & 3
+  const int n0 = ct0 * 16 + 4 * q, n1 = ct1 * 16 + 4 * q;  // pack channels
+  const int c0 = nout + n0, c1 = nout + n1;                // image channels
+  const float4 bb0 = *reinterpret_cast<const float4*>(bconv + n0);
+  const float4 bb1 = *reinterpret_cast<const float4*>(bconv + n1);
   f32x4 acc0[TR], acc1[TR];
 #pragma unroll
-  for (int rt = 0; rt < TR; ++rt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float r0 = bb0, r1 = bb1;
-      if (MODE == 1) {
-        const int row = rt * 16 + 4 * q + i;
-        r0 = r0 + bf16_to_f32(*(reinterpret_cast<const bf16_t*>(lds + dstimg + toff(row, c0 >> 3)) + (c0 & 7)));
-        r1 = r1 + bf16_to_f32(*(reinterpret_cast<const bf16_t*>(lds + dstimg + toff(row, c1 >> 3)) + (c1 & 7)));
-      } else if (MODE == 2) {
-        const float* t = actb + ((size_t)(q * 5 + rt) * A + acts[i]) * TC;
-        r0 = r0 + t[n0];
-        r1 = r1 + t[n1];
-      }
-      acc0[rt][i] = r0;
-      acc1[rt][i] = r1;
+  for (int rt = 0; rt < TR; ++rt) {
+    f32x4 r0 = {bb0.x, bb0.y, bb0.z, bb0.w}, r1 = {bb1.x, bb1.y, bb1.z, bb1.w};
+    const int row = rt * 16 + l16;
+    if (MODE == 1) {
+      const uint2 x0 = *reinterpret_cast<const uint2*>(lds + dstimg + toff(row, c0 >> 3) + ((c0 & 7) << 1));
+      const uint2 x1 = *reinterpret_cast<const uint2*>(lds + dstimg + toff(row, c1 >> 3) + ((c1 & 7) << 1));
+      r0[0] += __uint_as_float(x0.x << 16); r0[1] += __uint_as_float(x0.x & 0xffff0000u);
+      r0[2] += __uint_as_float(x0.y << 16); r0[3] += __uint_as_float(x0.y & 0xffff0000u);
+      r1[0] += __uint_as_float(x1.x << 16); r1[1] += __uint_as_float(x1.x & 0xffff0000u);
+      r1[2] += __uint_as_float(x1.y << 16); r1[3] += __uint_as_float(x1.y & 0xffff0000u);
+    } else if (MODE == 2) {
+      const float* t = actb + ((size_t)((l16 >> 2) * 5 + rt) * A + acts[l16 & 3]) * TC;
+      const float4 t0 = *reinterpret_cast<const float4*>(t + n0), t1 = *reinterpret_cast<const float4*>(t + n1);
+      r0[0] += t0.x; r0[1] += t0.y; r0[2] += t0.z; r0[3] += t0.w;
+      r1[0] += t1.x; r1[1] += t1.y; r1[2] += t1.z; r1[3] += t1.w;
     }
+    acc0[rt] = r0;
+    acc1[rt] = r1;
+  }
   if (CENTER) {
     tower_center(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
   } else {
@@ -227,13 +233,16 @@ __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg
     tower_dx<1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
   }
 #pragma unroll
-  for (int rt = 0; rt < TR; ++rt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = rt * 16 + 4 * q + i;
-      *(reinterpret_cast<bf16_t*>(lds + dstimg + toff(row, c0 >> 3)) + (c0 & 7)) = f32_to_bf16(fmaxf(acc0[rt][i], 0.f));
-      *(reinterpret_cast<bf16_t*>(lds + dstimg + toff(row, c1 >> 3)) + (c1 & 7)) = f32_to_bf16(fmaxf(acc1[rt][i], 0.f));
-    }
+  for (int rt = 0; rt < TR; ++rt) {
+    const int row = rt * 16 + l16;
+    uint2 o0, o1;
+    o0.x = pack_bf16x2(fmaxf(acc0[rt][0], 0.f), fmaxf(acc0[rt][1], 0.f));
+    o0.y = pack_bf16x2(fmaxf(acc0[rt][2], 0.f), fmaxf(acc0[rt][3], 0.f));
+    o1.x = pack_bf16x2(fmaxf(acc1[rt][0], 0.f), fmaxf(acc1[rt][1], 0.f));
+    o1.y = pack_bf16x2(fmaxf(acc1[rt][2], 0.f), fmaxf(acc1[rt][3], 0.f));
+    *reinterpret_cast<uint2*>(lds + dstimg + toff(row, c0 >> 3) + ((c0 & 7) << 1)) = o0;
+    *reinterpret_cast<uint2*>(lds + dstimg + toff(row, c1 >> 3) + ((c1 & 7) << 1)) = o1;
+  }
 }
 
 // Linear heads on an LDS image (networks.py:147, 207, 221): head h reads image channels
@@ -600,8 +609,8 @@ __device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, cons
       uint2* p = reinterpret_cast<uint2*>(lds + toff(rt * 16 + l16, n >> 3) + ((n & 7) << 1));
       if (SAVE) res[rt][ct] = *p;
       uint2 o;
-      o.x = (uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][0], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][1], 0.f)) << 16);
-      o.y = (uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][2], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[rt][ct][3], 0.f)) << 16);
+      o.x = pack_bf16x2(fmaxf(acc[rt][ct][0], 0.f), fmaxf(acc[rt][ct][1], 0.f));
+      o.y = pack_bf16x2(fmaxf(acc[rt][ct][2], 0.f), fmaxf(acc[rt][ct][3], 0.f));
       *p = o;
     }
 }
