@@ -68,3 +68,10 @@ def small_model_cfg(cfg=None):
     m["prediction_network"] = {"num_res_blocks": 2, "num_actions": 3, "activation": "relu"}
     m["device"] = "cpu"
     return m
+
+
+def learner_model_cfg(cfg=None):
+    """The narrow learner fixture config (tests/golden/learner_small.npz): 32 channels, L = 4."""
+    m = small_model_cfg(cfg)
+    m["latent_channels"] = [32, 32]
+    return m
