@@ -79,7 +79,7 @@ int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* hist_frames, c
  * in: NHWC, env b at in + b*in_env_stride (+ slot[b]*in_slot_stride when slot != NULL: gather of
  * parent latents from the node pool). w: [Cout][ks*ks*Cin] (tap-major, K-contiguous). bias f32.
  * act_bias f32 [HW][A][Cout] + act i32[B]: the dynamics net's one-hot action planes
- * (mcts.py:252-268). res: residual [B*HW][Cout] (may alias out). Cin % (dtype ? 64 : 32) == 0. */
+ * (mcts.py:252-268). res: residual [B*HW][Cout] (may alias out). Cin % (dtype ? 8 : 4) == 0, Cout % 4 == 0. */
 int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                 const void* w, const float* bias, const float* act_bias, const int32_t* act, int A, const void* res,
                 void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream);
@@ -269,6 +269,77 @@ int mzba_record_results(const int64_t* counts, const float* values, int64_t* rec
 
 /* ctx[0..2] += 1 (end of one captured acting step). */
 int mzba_ctx_advance(int32_t* ctx, hipStream_t stream);
+
+/* ===================== learner: one minibatch of RLSystem._training_stage
+ * (train_torch.py:380-407) — _k_step_rollout (:487-528) with train-mode BN, loss_fn (:33-66),
+ * backward, torch.optim.Adam(lr, weight_decay=1e-4) (networks.py:268). NHWC activations, dtype
+ * 0 = f32, 1 = bf16 storage; statistics, gradients and parameters f32. ws = caller scratch. */
+
+/* BatchNorm2d forward statistics in train mode (nn.BatchNorm2d in ConvBlock / ResidualBlock,
+ * networks.py:7-35): stats[4][C] = (mean, invstd, gamma*invstd, beta - mean*gamma*invstd) over the
+ * M rows of x [M][C]; running_mean / running_var (may be NULL) updated with momentum and the
+ * unbiased variance. ws >= ceil(M/256)*C*8 bytes. */
+int mzba_bn_stats(int dtype, const void* x, int M, int C, float eps, float momentum, const float* gamma,
+                  const float* beta, float* stats, float* run_mean, float* run_var, void* ws, long long ws_bytes,
+                  hipStream_t stream);
+/* out = x*stats[2] + stats[3] (+ res) (ReLU if relu); out may alias x or res. C % 4 == 0. */
+int mzba_bn_apply(int dtype, const void* x, const float* stats, const void* res, int relu, void* out, int M, int C,
+                  hipStream_t stream);
+/* BN (+ReLU) backward: if y != NULL, dy *= [y > 0] in place (the ReLU after the BN / residual
+ * add); dgamma += sum(dy*xhat), dbeta += sum(dy); dx = (dy - (x-mean)*k - mean(dy))*gamma*invstd.
+ * ws >= ceil(M/256)*C*8 + 12*C bytes. */
+int mzba_bn_backward(int dtype, void* dy, const void* y, const void* x, const float* stats, int M, int C,
+                     float* dgamma, float* dbeta, void* dx, void* ws, long long ws_bytes, hipStream_t stream);
+/* Weight packs from the f32 master weights w [Cout][taps][Cin]: flip = 0: cast copy (forward);
+ * flip = 1: wt [cin_used][taps][Cout] = w[co][taps-1-tap][ci] (the input-gradient convolution). */
+int mzba_conv_wpack(int dtype, const float* w, void* wt, int Cout, int taps, int Cin, int cin_used, int flip,
+                    hipStream_t stream);
+/* Conv2d weight / bias gradient: dw [Cout][ks*ks][Cin] += sum_m dy[m][co] * x_tap[m][ci],
+ * db [Cout] += sum_m dy[m][co] (db may be NULL). x NHWC [B][H][W][Cin], dy [B][H][W][Cout]. */
+long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks);
+int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
+                    float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream);
+/* nn.AvgPool2d(2, 2) backward: dx [B][H][W][C] = dy[y/2][x/2] / 4. */
+int mzba_avgpool2_backward(int dtype, const void* dy, void* dx, int B, int H, int W, int C, hipStream_t stream);
+/* y += x (n elements). */
+int mzba_axpy(int dtype, void* y, const void* x, long long n, hipStream_t stream);
+/* _scale_state forward (networks.py:314-328) recording minmax[B][2] and the NHWC index of the first
+ * min / max in NCHW flatten order (torch.min/max(dim=1) index semantics) in argminmax[B][2]. */
+int mzba_scale_forward(int dtype, const void* h, void* out, float* minmax, int32_t* argminmax, int B, int HW, int C,
+                       hipStream_t stream);
+/* _scale_state backward: dh (= or +=) autograd of (h - min)/(max - min + 1e-8), min / max gradients
+ * routed to the recorded indices. */
+int mzba_scale_backward(int dtype, const void* dy, const void* h, const float* minmax, const int32_t* argminmax,
+                        void* dh, int B, int n, int accumulate, hipStream_t stream);
+/* nn.Linear heads (networks.py:147, 207, 221) on an NHWC image: out[b][o] = bias[o] + sum_k w[o][k] x[b][k],
+ * k = pixel*C + channel (the reference's (c, y, x) flatten order is permuted into the weight layout). */
+int mzba_linear_forward(int dtype, const void* x, const float* w, const float* bias, float* out, int B, int K, int O,
+                        hipStream_t stream);
+long long mzba_linear_ws_bytes(int B, int K, int O);
+/* dx (= or += when accumulate; NULL = skip) = dy w; dw += dy^T x; db += sum_b dy. */
+int mzba_linear_backward(int dtype, const void* x, const float* w, const float* dy, void* dx, int accumulate,
+                         float* dw, float* db, int B, int K, int O, void* ws, long long ws_bytes, hipStream_t stream);
+/* loss_fn (train_torch.py:33-66) over logits [K][B][ns|na] with targets from replay rows slots[b]
+ * (slots NULL: row b) of rewards [.][K], targets [.][K], counts [.][K][na]: supports_representation
+ * (utils.py:30-64) two-hot targets, KL(batchmean) x3, loss[4] = (total, reward, value, policy) and the
+ * logit gradients of the total. */
+int mzba_learner_loss(const float* logit_r, const float* logit_v, const float* logit_p, const float* rewards,
+                      const float* targets, const float* counts, const int32_t* slots, int B, int K, int ns, int na,
+                      float smin, float smax, float* dlogit_r, float* dlogit_v, float* dlogit_p, float* loss,
+                      hipStream_t stream);
+/* Adam with L2 weight decay, torch single-tensor order: g = grad + wd*p; m += (1-b1)(g - m);
+ * v = v*b2 + (1-b2)*g*g; p += (-step_size*m) / (sqrt(v)/bc2_sqrt + eps). Host computes
+ * neg_step = -lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t) in double (python float semantics). */
+int mzba_adam(float* p, const float* grad, float* m, float* v, long long n, float neg_step, float one_m_b1, float b2,
+              float one_m_b2, float bc2_sqrt, float eps, float weight_decay, hipStream_t stream);
+/* Representation input of a minibatch (_prepare_minibatch + _encode_actions, train_torch.py:437-470,
+ * 279-293) straight from the replay ring: out [B][HW][Cp] = (lut[frame code] x L, a/3 x L, 0...). */
+int mzba_learner_input(int dtype, const uint8_t* states, const int64_t* past_actions, const int32_t* slots,
+                       const float* lut8, void* out, int B, int L, int HW, int Cp, hipStream_t stream);
+/* Dynamics input (_encode_action_dynamics, train_torch.py:295-311): out [B][HW][Cp] =
+ * (h [B][HW][C], one-hot(future_actions[slots[b]][k]) x A, 0...). */
+int mzba_dyn_input(int dtype, const void* h, const int64_t* future_actions, const int32_t* slots, int K, int k,
+                   void* out, int B, int HW, int C, int A, int Cp, hipStream_t stream);
 
 #ifdef __cplusplus
 }

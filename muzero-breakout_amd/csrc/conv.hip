@@ -1,7 +1,7 @@
 // Implicit-GEMM convolution for the MuZero ResNets on gfx950 MFMA.
 //
 // out[m][n] = act( sum_k A[m][k] * Wp[n][k] + bias[n] (+ act_bias[p][a_b][n]) (+ res[m][n]) )
-//   m = (env b, pixel p = y*W + x)  — NHWC activations, channel stride Cin (multiple of BK)
+//   m = (env b, pixel p = y*W + x)  — NHWC activations, channel stride Cin (multiple of 4 f32 / 8 bf16)
 //   k = (tap (ky,kx), channel c)    — A[m][k] = in[b][y+ky-pad][x+kx-pad][c] or 0 (zero padding)
 //   Wp[n][k] = BN-folded weights packed K-contiguous per output channel
 // One kernel covers every conv of the reference nets (networks.py:7-35, 38-241): 3x3 and
@@ -11,8 +11,8 @@
 // contribution only depends on the pixel's in-bounds taps).
 //
 // Tile 128x128, 4 waves (2x2), each wave 64x64 = 4x4 MFMA 16x16 tiles. One K-step moves
-// one 128-byte row slice per tile row (BK = 64 bf16 or 32 f32) and lies inside a single
-// tap (Cin % BK == 0). Operands staged global -> VGPR -> LDS (double buffer, one barrier
+// one 128-byte row slice per tile row (BK = 64 bf16 or 32 f32), split into
+// tap-resolved 16-B chunks (Cin % 4 f32 / % 8 bf16). Operands staged global -> VGPR -> LDS (double buffer, one barrier
 // per K-step), 16-B chunks XOR-swizzled by (row & 7) so the fragment reads are spread
 // over the LDS banks. bf16 uses v_mfma_f32_16x16x32_bf16; the f32 parity path uses
 // v_mfma_f32_16x16x4_f32 (exact f32 fma chain).
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
   const int wm = wave >> 1, wn = wave & 1;
   const int pad = a.ks / 2;
   const int Ktot = a.ks * a.ks * a.Cin;
-  const int nK = Ktot / BK;
+  const int nK = (Ktot + BK - 1) / BK;  // the last K-step may be ragged (zero-filled)
 
   // per-thread staging geometry: chunk j of rows r + 32*i
   const int j = tid & 7, r0 = tid >> 3;
@@ -81,19 +81,22 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
   }
 
   uint4 ra[4], rb[4];
+  // each 16-B chunk j of a K-step resolves its own tap (Cin % EPC == 0: a chunk never
+  // straddles two taps), so Cin need not be a multiple of BK
   auto load_tile = [&](int ks) {
-    const int k0 = ks * BK;
-    const int tap = k0 / a.Cin, c0 = k0 - tap * a.Cin;
+    const int k = ks * BK + j * EPC;
+    const bool kok = k < Ktot;
+    const int tap = k / a.Cin, c = k - tap * a.Cin;
     const int ky = tap / a.ks - pad, kx = tap % a.ks - pad;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int sy = ay[i] + ky, sx = ax[i] + kx;
-      bool ok = mval[i] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(abase[i] + ((long long)(sy * a.W + sx) * a.Cin + c0 + j * EPC))
+      bool ok = kok && mval[i] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(abase[i] + ((long long)(sy * a.W + sx) * a.Cin + c))
                  : make_uint4(0, 0, 0, 0);
       int n = n0 + r0 + 32 * i;
-      rb[i] = n < a.Cout ? *reinterpret_cast<const uint4*>(wgt + ((long long)n * Ktot + k0 + j * EPC))
-                         : make_uint4(0, 0, 0, 0);
+      rb[i] = kok && n < a.Cout ? *reinterpret_cast<const uint4*>(wgt + ((long long)n * Ktot + k))
+                                : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_tile = [&](int buf) {
@@ -308,9 +311,9 @@ extern "C" {
 int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                 const void* w, const float* bias, const float* act_bias, const int32_t* act, int A, const void* res,
                 void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream) {
-  const int BK = dtype ? 64 : 32;
+  const int EPC = dtype ? 8 : 4;  // elements per 16-B chunk
   MZ_CHECK_ARG(B > 0 && H > 0 && W > 0 && (ks == 1 || ks == 3), -1);
-  MZ_CHECK_ARG(Cin % BK == 0 && Cout % 8 == 0, -2);
+  MZ_CHECK_ARG(Cin % EPC == 0 && Cout % 4 == 0, -2);
   MZ_CHECK_ARG(!act_bias || (act && A > 0), -3);
   ConvArgs a{in, in_env_stride, in_slot_stride, slot, w, bias, act_bias, act, A, res, out, B, H, W, Cin, Cout, ks, relu};
   return dtype ? launch_conv<bf16_t>(a, stream) : launch_conv<float>(a, stream);

@@ -1,0 +1,873 @@
+// Learner kernels: one minibatch of RLSystem._training_stage
+// (train_torch.py:380-407) = _k_step_rollout forward with train-mode BatchNorm, loss_fn, the
+// backward pass and the Adam step, on NHWC activations (T = f32 for parity, bf16 for
+// throughput; statistics, gradients and parameters are f32 throughout).
+//
+// The convolutions themselves run on conv_igemm_kernel (conv.hip): forward with the f32 master
+// weights (or their bf16 cast), input gradients as a convolution of the output gradient with
+// the flipped, transposed weights (conv_wt_kernel packs them every step). This file holds what
+// is specific to training:
+//   bn_stats_*        batch mean / biased variance per channel (chunk-wise mean + M2, combined
+//                     with Chan's formula in double), running-stat update (networks.py BN layers
+//                     in train mode, momentum 0.1, unbiased running variance);
+//   bn_apply          y = x * (gamma * invstd) + (beta - mean * gamma * invstd) (+ residual) (ReLU);
+//   bn_bwd_*          g = dy * [y > 0] (in place), dgamma / dbeta, dx = (g - (x - mean) k - mean_g)
+//                     * gamma * invstd with k = sum(g (x - mean)) invstd^2 / N (torch's CPU order);
+//   conv_wgrad        dW[co][tap][ci] = sum_m dY[m][co] X_tap[m][ci] (+ conv bias grad), split
+//                     over m into deterministic partials, then reduced into the gradient buffer;
+//   scale_fwd / bwd   MuZeroAgent._scale_state (networks.py:314-328) with the first min / max
+//                     index in NCHW flatten order (torch.min/max(dim) semantics) for the backward;
+//   linear_*          the heads' nn.Linear on an NHWC image (weights kept in [o][pixel][channel]);
+//   loss              supports_representation (utils.py:30-64) + log_softmax + KL(batchmean)
+//                     for reward / value / policy and their logit gradients (loss_fn :33-66);
+//   adam              torch.optim.Adam(lr, weight_decay = 1e-4) single-tensor update (networks.py:268).
+#include "common.h"
+
+namespace {
+
+template <typename T> MZ_DEV float ld(const T* p) { return ElemIO<T>::load(p); }
+template <typename T> MZ_DEV void st(T* p, float v) { ElemIO<T>::store(p, v); }
+
+// ------------------------------------------------------------------ BatchNorm statistics
+// part[chunk][c] = (chunk mean, chunk M2) over rows [chunk*rpc, min(M, (chunk+1)*rpc)).
+// 256 threads = 64 channels x 4 row lanes.
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restrict__ x, int M, int C, int rpc,
+                                                               float2* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
+  const int n = r1 - r0;
+  float s = 0.f;
+  if (c < C)
+    for (int r = r0 + ty; r < r1; r += 4) s += ld(x + (size_t)r * C + c);
+  red[ty][tx] = s;
+  __syncthreads();
+  const float mean = ((red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx])) / (float)n;
+  __syncthreads();
+  float q = 0.f;
+  if (c < C)
+    for (int r = r0 + ty; r < r1; r += 4) {
+      const float d = ld(x + (size_t)r * C + c) - mean;
+      q += d * d;
+    }
+  red[ty][tx] = q;
+  __syncthreads();
+  if (ty == 0 && c < C)
+    part[(size_t)blockIdx.y * C + c] = make_float2(mean, (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]));
+}
+
+// combine the chunks (Chan et al., in double, chunk order) -> mean, invstd, alpha = gamma*invstd,
+// beta' = beta - mean*alpha; running stats: r = momentum*stat + (1 - momentum)*r (unbiased var)
+__global__ void bn_stats_final_kernel(const float2* __restrict__ part, int nchunk, int rpc, int M, int C, float eps,
+                                      float momentum, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                      float* __restrict__ stats, float* __restrict__ run_mean,
+                                      float* __restrict__ run_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double n = 0, mean = 0, m2 = 0;
+  for (int k = 0; k < nchunk; ++k) {
+    const double nb = (double)min(rpc, M - k * rpc);
+    const float2 p = part[(size_t)k * C + c];
+    const double d = (double)p.x - mean, tot = n + nb;
+    mean += d * nb / tot;
+    m2 += (double)p.y + d * d * n * nb / tot;
+    n = tot;
+  }
+  const float var = (float)(m2 / M);
+  const float invstd = (float)(1.0 / sqrt((double)var + (double)eps));
+  const float alpha = invstd * gamma[c];
+  const float fm = (float)mean;
+  stats[c] = fm;                 // mean
+  stats[C + c] = invstd;         // invstd
+  stats[2 * C + c] = alpha;      // gamma * invstd
+  stats[3 * C + c] = beta[c] - fm * alpha;
+  if (run_mean) {
+    run_mean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)run_mean[c]);
+    const double unbiased = M > 1 ? m2 / (double)(M - 1) : m2;
+    run_var[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)run_var[c]);
+  }
+}
+
+// y = x*alpha + beta' (+ res) (ReLU); 4 channels per thread (C % 4 == 0)
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, const float* __restrict__ stats,
+                                                       const T* res, int relu, T* out, int M, int C) {
+  const size_t n4 = (size_t)M * C / 4;
+  const float* alpha = stats + 2 * C;
+  const float* beta = stats + 3 * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = i * 4;
+    const int c = (int)(e % C);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float v = ld(x + e + j) * alpha[c + j] + beta[c + j];
+      if (res) v = v + ld(res + e + j);
+      if (relu) v = fmaxf(v, 0.f);
+      st(out + e + j, v);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ BatchNorm backward
+// g = dy * [y > 0] (written back to dy when y != null); part[chunk][c] = (sum g, sum g (x - mean))
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_partial_kernel(T* __restrict__ dy, const T* __restrict__ y,
+                                                             const T* __restrict__ x, const float* __restrict__ stats,
+                                                             int M, int C, int rpc, float2* __restrict__ part) {
+  __shared__ float red[2][4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
+  float sg = 0.f, sd = 0.f;
+  if (c < C) {
+    const float mean = stats[c];
+    for (int r = r0 + ty; r < r1; r += 4) {
+      const size_t i = (size_t)r * C + c;
+      float g = ld(dy + i);
+      if (y) {
+        if (!(ld(y + i) > 0.f)) g = 0.f;
+        st(dy + i, g);
+      }
+      sg += g;
+      sd += g * (ld(x + i) - mean);
+    }
+  }
+  red[0][ty][tx] = sg;
+  red[1][ty][tx] = sd;
+  __syncthreads();
+  if (ty == 0 && c < C)
+    part[(size_t)blockIdx.y * C + c] = make_float2((red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]),
+                                                   (red[1][0][tx] + red[1][1][tx]) + (red[1][2][tx] + red[1][3][tx]));
+}
+
+// dgamma += dot*invstd, dbeta += sum g; coef = (mean_g, k = dot*invstd^2/N, gamma*invstd)
+__global__ void bn_bwd_final_kernel(const float2* __restrict__ part, int nchunk, int M, int C,
+                                    const float* __restrict__ stats, float* __restrict__ dgamma,
+                                    float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double sg = 0, dot = 0;
+  for (int k = 0; k < nchunk; ++k) {
+    const float2 p = part[(size_t)k * C + c];
+    sg += p.x;
+    dot += p.y;
+  }
+  const float invstd = stats[C + c];
+  dgamma[c] += (float)dot * invstd;
+  dbeta[c] += (float)sg;
+  coef[c] = (float)(sg / M);
+  coef[C + c] = (float)dot * invstd * invstd / (float)M;
+  coef[2 * C + c] = stats[2 * C + c];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ g, const T* __restrict__ x,
+                                                           const float* __restrict__ stats,
+                                                           const float* __restrict__ coef, T* __restrict__ dx, int M,
+                                                           int C) {
+  const size_t n = (size_t)M * C;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float proj = (ld(x + i) - stats[c]) * coef[C + c];
+    st(dx + i, ((ld(g + i) - proj) - coef[c]) * coef[2 * C + c]);
+  }
+}
+
+// ------------------------------------------------------------------ conv weight packs
+// wt[ci][tap][co] = w[co][taps-1-tap][ci] for ci < cin_used (input-gradient conv), or a plain
+// cast wt = w (mode 0). w: f32 master [Cout][taps][Cin].
+template <typename T>
+__global__ void conv_wt_kernel(const float* __restrict__ w, T* __restrict__ wt, int Cout, int taps, int Cin,
+                               int cin_used, int flip) {
+  const size_t n = flip ? (size_t)cin_used * taps * Cout : (size_t)Cout * taps * Cin;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    if (!flip) {
+      st(wt + i, w[i]);
+    } else {
+      const int co = (int)(i % Cout);
+      const size_t q = i / Cout;
+      const int tap = (int)(q % taps), ci = (int)(q / taps);
+      st(wt + i, w[((size_t)co * taps + (taps - 1 - tap)) * Cin + ci]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ conv weight gradient
+// One workgroup: a 64 (co) x 64 (ci) tile of one tap over a chunk of m rows, 4 waves as 2x2 of
+// 32x32 (2x2 MFMA 16x16 tiles). K = m in steps of 16 rows staged through LDS.
+// f32: v_mfma_f32_16x16x4_f32 (lane: row l&15, k = l>>4). bf16: rows are widened to f32 in LDS.
+constexpr int WG_ROWS = 16, WG_LD = 80;  // LDS row stride (floats): 16-bank shift per k row
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy, int B,
+                                                         int H, int W, int Cin, int Cout, int ks, int rows_per_split,
+                                                         float* __restrict__ part, float* __restrict__ bpart) {
+  __shared__ float la[2][WG_ROWS][WG_LD];  // dY tile [m][co]
+  __shared__ float lb[2][WG_ROWS][WG_LD];  // X tile  [m][ci]
+  const int taps = ks * ks, pad = ks / 2;
+  const int nci = (Cin + 63) / 64;
+  int t = blockIdx.x;
+  const int cit = t % nci; t /= nci;
+  const int tap = t % taps; t /= taps;
+  const int cot = t;
+  const int split = blockIdx.y;
+  const int HW = H * W, M = B * HW;
+  const int m0 = split * rows_per_split, m1 = min(M, m0 + rows_per_split);
+  const int ky = tap / ks - pad, kx = tap % ks - pad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  // staging: thread -> (row lr = tid >> 4, 4 channels at 4*(tid & 15))
+  const int lr = tid >> 4, lc = (tid & 15) * 4;
+  const int co_s = cot * 64 + lc, ci_s = cit * 64 + lc;
+  float4 va, vb;
+  auto load = [&](int mb) {
+    const int m = mb + lr;
+    va = make_float4(0.f, 0.f, 0.f, 0.f);
+    vb = va;
+    if (m < m1) {
+      const int b = m / HW, p = m - b * HW, yy = p / W, xx = p - yy * W;
+      const T* d = dy + (size_t)m * Cout + co_s;
+      if (co_s < Cout) va = make_float4(ld(d), ld(d + 1), ld(d + 2), ld(d + 3));
+      const int sy = yy + ky, sx = xx + kx;
+      if (ci_s < Cin && sy >= 0 && sy < H && sx >= 0 && sx < W) {
+        const T* s = x + ((size_t)b * HW + sy * W + sx) * Cin + ci_s;
+        vb = make_float4(ld(s), ld(s + 1), ld(s + 2), ld(s + 3));
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    *reinterpret_cast<float4*>(&la[buf][lr][lc]) = va;
+    *reinterpret_cast<float4*>(&lb[buf][lr][lc]) = vb;
+  };
+  const bool do_bias = bpart && tap == 0 && cit == 0;
+  typedef __attribute__((ext_vector_type(4))) float f4;
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (m1 - m0 + WG_ROWS - 1) / WG_ROWS;
+  if (nsteps > 0) {
+    load(m0);
+    store(0);
+  }
+  __syncthreads();
+  const int fr = lane & 15, fk = lane >> 4;
+  float4 bacc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (do_bias) { bacc.x += va.x; bacc.y += va.y; bacc.z += va.z; bacc.w += va.w; }
+    if (s + 1 < nsteps) load(m0 + (s + 1) * WG_ROWS);
+#pragma unroll
+    for (int kk = 0; kk < WG_ROWS / 4; ++kk) {
+      const int r = kk * 4 + fk;
+      float a[2], bb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = la[buf][r][wr * 32 + i * 16 + fr];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bb[j] = lb[buf][r][wc * 32 + j * 16 + fr];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], bb[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+  // D[row = co 4*fk + r][col = ci fr] of each 16x16 tile
+  const size_t K = (size_t)taps * Cin;
+  float* outp = part + (size_t)split * Cout * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = cit * 64 + wc * 32 + j * 16 + fr;
+      if (ci >= Cin) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = cot * 64 + wr * 32 + i * 16 + 4 * fk + r;
+        if (co < Cout) outp[(size_t)co * K + (size_t)tap * Cin + ci] = acc[i][j][r];
+      }
+    }
+  if (do_bias) {  // reduce the 16 row lanes of each channel group through LDS
+    __shared__ float4 bred[16][16];
+    bred[lr][tid & 15] = bacc;
+    __syncthreads();
+    if (tid < 16) {
+      float4 s = bred[0][tid];
+      for (int r = 1; r < 16; ++r) { s.x += bred[r][tid].x; s.y += bred[r][tid].y; s.z += bred[r][tid].z; s.w += bred[r][tid].w; }
+      const int co = cot * 64 + tid * 4;
+      float* bp = bpart + (size_t)split * Cout;
+      if (co < Cout) { bp[co] = s.x; bp[co + 1] = s.y; bp[co + 2] = s.z; bp[co + 3] = s.w; }
+    }
+  }
+}
+
+// acc[i] += sum_s part[s][i] (split order)
+__global__ void sum_partials_kernel(const float* __restrict__ part, int nsplit, size_t n, float* __restrict__ acc) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float s = part[i];
+    for (int k = 1; k < nsplit; ++k) s += part[(size_t)k * n + i];
+    acc[i] += s;
+  }
+}
+
+// ------------------------------------------------------------------ avg-pool backward, axpy
+template <typename T>
+__global__ void avgpool2_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int H, int W, int C) {
+  const size_t n = (size_t)B * H * W * C;
+  const int Ho = H / 2, Wo = W / 2;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    size_t q = i / C;
+    const int xx = (int)(q % W); q /= W;
+    const int yy = (int)(q % H);
+    const size_t b = q / H;
+    st(dx + i, ld(dy + ((b * Ho + yy / 2) * Wo + xx / 2) * C + c) / 4.0f);
+  }
+}
+
+template <typename T>
+__global__ void axpy_kernel(T* __restrict__ y, const T* __restrict__ x, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    st(y + i, ld(y + i) + ld(x + i));
+}
+
+// ------------------------------------------------------------------ min-max scale
+// one workgroup per env over n = HW*C values (NHWC); the first min / max in NCHW order
+// (index c*HW + p) is recorded for the backward. mm[b] = (min, max), idx[b] = NHWC indices.
+template <typename T>
+__global__ __launch_bounds__(256) void scale_fwd_kernel(const T* __restrict__ h, T* __restrict__ out,
+                                                        float2* __restrict__ mm, int2* __restrict__ idx, int HW,
+                                                        int C) {
+  const int b = blockIdx.x, n = HW * C;
+  const T* x = h + (size_t)b * n;
+  float mn = INFINITY, mx = -INFINITY;
+  int kmn = 0x7fffffff, kmx = 0x7fffffff;  // NCHW keys
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float v = ld(x + i);
+    const int c = i % C, key = c * HW + i / C;
+    if (v < mn || (v == mn && key < kmn)) { mn = v; kmn = key; }
+    if (v > mx || (v == mx && key < kmx)) { mx = v; kmx = key; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float m2 = __shfl_xor(mn, o), x2 = __shfl_xor(mx, o);
+    const int k2 = __shfl_xor(kmn, o), kx2 = __shfl_xor(kmx, o);
+    if (m2 < mn || (m2 == mn && k2 < kmn)) { mn = m2; kmn = k2; }
+    if (x2 > mx || (x2 == mx && kx2 < kmx)) { mx = x2; kmx = kx2; }
+  }
+  __shared__ float smn[4], smx[4];
+  __shared__ int skn[4], skx[4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { smn[w] = mn; smx[w] = mx; skn[w] = kmn; skx[w] = kmx; }
+  __syncthreads();
+  mn = smn[0]; mx = smx[0]; kmn = skn[0]; kmx = skx[0];
+  for (int k = 1; k < 4; ++k) {
+    if (smn[k] < mn || (smn[k] == mn && skn[k] < kmn)) { mn = smn[k]; kmn = skn[k]; }
+    if (smx[k] > mx || (smx[k] == mx && skx[k] < kmx)) { mx = smx[k]; kmx = skx[k]; }
+  }
+  const float den = (mx - mn) + 1e-8f;
+  T* o = out + (size_t)b * n;
+  for (int i = threadIdx.x; i < n; i += 256) st(o + i, (ld(x + i) - mn) / den);
+  if (threadIdx.x == 0) {
+    mm[b] = make_float2(mn, mx);
+    idx[b] = make_int2((kmn % HW) * C + kmn / HW, (kmx % HW) * C + kmx / HW);
+  }
+}
+
+// dh (=|+=) dy/den, then dh[argmin] += -sum(dy)/den - d_den, dh[argmax] += d_den with
+// d_den = -sum(dy * (h - min)) / den^2 (autograd of (h - min) / (max - min + 1e-8))
+template <typename T>
+__global__ __launch_bounds__(256) void scale_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ h,
+                                                        const float2* __restrict__ mm, const int2* __restrict__ idx,
+                                                        T* dh, int n, int accumulate) {
+  const int b = blockIdx.x;
+  const float mn = mm[b].x, mx = mm[b].y;
+  const float den = (mx - mn) + 1e-8f;
+  const T* g = dy + (size_t)b * n;
+  const T* x = h + (size_t)b * n;
+  T* o = dh + (size_t)b * n;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float gv = ld(g + i);
+    const float d = gv / den;
+    s1 += d;
+    s2 += gv * (ld(x + i) - mn);
+    st(o + i, accumulate ? ld(o + i) + d : d);
+  }
+  for (int off = 32; off > 0; off >>= 1) { s1 += __shfl_xor(s1, off); s2 += __shfl_xor(s2, off); }
+  __shared__ float r1[4], r2[4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { r1[w] = s1; r2[w] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float S1 = (r1[0] + r1[1]) + (r1[2] + r1[3]);
+    const float S2 = (r2[0] + r2[1]) + (r2[2] + r2[3]);
+    const float dden = -(S2 / den) / den;
+    const int2 k = idx[b];
+    st(o + k.x, ld(o + k.x) + (-S1 - dden));
+    st(o + k.y, ld(o + k.y) + dden);
+  }
+}
+
+// ------------------------------------------------------------------ heads: nn.Linear on NHWC
+// out[b][o] = bias[o] + sum_k w[o][k] x[b][k], k = p*C + c (weights kept in that order)
+template <typename T>
+__global__ __launch_bounds__(256) void linear_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, float* __restrict__ out,
+                                                         int K, int O) {
+  const int b = blockIdx.x;
+  const T* xb = x + (size_t)b * K;
+  float acc[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) acc[o] = 0.f;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    const float v = ld(xb + k);
+#pragma unroll
+    for (int o = 0; o < 16; ++o)
+      if (o < O) acc[o] += v * w[(size_t)o * K + k];
+  }
+  __shared__ float red[4][16];
+  const int w_ = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 0; o < 16; ++o) {
+    float v = acc[o];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if ((threadIdx.x & 63) == 0) red[w_][o] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < O) {
+    const int o = threadIdx.x;
+    out[(size_t)b * O + o] = ((red[0][o] + red[1][o]) + (red[2][o] + red[3][o])) + bias[o];
+  }
+}
+
+// dx[b][k] (=|+=) sum_o dy[b][o] w[o][k]
+template <typename T>
+__global__ void linear_bwd_x_kernel(const float* __restrict__ dy, const float* __restrict__ w, T* dx, int B, int K,
+                                    int O, int accumulate) {
+  const size_t n = (size_t)B * K;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % K);
+    const size_t b = i / K;
+    float s = 0.f;
+    for (int o = 0; o < O; ++o) s += dy[b * O + o] * w[(size_t)o * K + k];
+    st(dx + i, accumulate ? ld(dx + i) + s : s);
+  }
+}
+
+// part[split][o][k] = sum_{b in split} dy[b][o] x[b][k]; bpart[split][o] = sum dy[b][o]
+template <typename T>
+__global__ void linear_bwd_w_kernel(const float* __restrict__ dy, const T* __restrict__ x, int B, int K, int O,
+                                    int rows_per_split, float* __restrict__ part, float* __restrict__ bpart) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int split = blockIdx.y;
+  const int b0 = split * rows_per_split, b1 = min(B, b0 + rows_per_split);
+  float acc[16];
+#pragma unroll
+  for (int o = 0; o < 16; ++o) acc[o] = 0.f;
+  if (k < K)
+    for (int b = b0; b < b1; ++b) {
+      const float v = ld(x + (size_t)b * K + k);
+#pragma unroll
+      for (int o = 0; o < 16; ++o)
+        if (o < O) acc[o] += dy[(size_t)b * O + o] * v;
+    }
+  if (k < K)
+    for (int o = 0; o < O; ++o) part[((size_t)split * O + o) * K + k] = acc[o];
+  if (blockIdx.x == 0 && threadIdx.x < O) {
+    float s = 0.f;
+    for (int b = b0; b < b1; ++b) s += dy[(size_t)b * O + threadIdx.x];
+    bpart[(size_t)split * O + threadIdx.x] = s;
+  }
+}
+
+// ------------------------------------------------------------------ loss (loss_fn, train_torch.py:33-66)
+// One workgroup. Row r = (b, k) of the (B, K) targets; logits[k][b][n]. Per row: compact
+// transform + two-hot over the integer supports (utils.py:30-64), log_softmax, KL terms
+// t*(log t - logp) (0 where t == 0), and the logit gradient (softmax*sum(t) - t)/(B*K)/K.
+// loss[0..3] = total, reward, value, policy.
+constexpr int LOSS_T = 256;
+
+MZ_DEV void two_hot(float x, float smin, float smax, int ns, float* t) {
+  const float sg = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+  const float c = sg * ((sqrtf(fabsf(x) + 1.f) - 1.f) + 0.001f * x);
+  const float step = (smax - smin) / (float)(ns - 1);
+  int lo = -1;  // searchsorted(right=True) - 1
+  for (int i = 0; i < ns; ++i)
+    if (smin + (float)i * step <= c) lo = i;
+  lo = lo < 0 ? 0 : (lo > ns - 2 ? ns - 2 : lo);
+  const float sl = smin + (float)lo * step, su = smin + (float)(lo + 1) * step;
+  const float pl = (su - c) / ((su - sl) + 1e-10f);
+  for (int i = 0; i < ns; ++i) t[i] = 0.f;
+  t[lo] = pl;
+  t[lo + 1] = 1.f - pl;
+}
+
+MZ_DEV double kl_row(const float* z, const float* t, int n, float scale, float* dz) {
+  float m = z[0];
+  for (int i = 1; i < n; ++i) m = fmaxf(m, z[i]);
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += expf(z[i] - m);
+  const float ls = logf(s);
+  float tsum = 0.f;
+  double kl = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const float lp = (z[i] - m) - ls;  // torch log_softmax: (x - max) - log(sum exp(x - max))
+    if (t[i] > 0.f) kl += (double)(t[i] * (logf(t[i]) - lp));
+    tsum += t[i];
+  }
+  for (int i = 0; i < n; ++i) dz[i] = (expf((z[i] - m) - ls) * tsum - t[i]) * scale;
+  return kl;
+}
+
+__global__ __launch_bounds__(LOSS_T) void loss_kernel(const float* __restrict__ lr, const float* __restrict__ lv,
+                                                      const float* __restrict__ lp, const float* __restrict__ rewards,
+                                                      const float* __restrict__ targets,
+                                                      const float* __restrict__ counts, const int32_t* slots, int B,
+                                                      int K, int ns, int na, float smin, float smax,
+                                                      float* __restrict__ dlr, float* __restrict__ dlv,
+                                                      float* __restrict__ dlp, float* __restrict__ loss) {
+  __shared__ double red[3][LOSS_T];
+  const float scale = (1.f / (float)K) / (float)(B * K);
+  double acc[3] = {0.0, 0.0, 0.0};
+  for (int r = threadIdx.x; r < B * K; r += LOSS_T) {
+    const int b = r / K, k = r - b * K;
+    const size_t src = slots ? (size_t)slots[b] : (size_t)b;  // ring row of window b
+    float t[16], z[16], dz[16];
+    const size_t o1 = ((size_t)k * B + b) * ns, o3 = ((size_t)k * B + b) * na;
+    two_hot(rewards[src * K + k], smin, smax, ns, t);
+    for (int i = 0; i < ns; ++i) z[i] = lr[o1 + i];
+    acc[0] += kl_row(z, t, ns, scale, dz);
+    for (int i = 0; i < ns; ++i) dlr[o1 + i] = dz[i];
+    two_hot(targets[src * K + k], smin, smax, ns, t);
+    for (int i = 0; i < ns; ++i) z[i] = lv[o1 + i];
+    acc[1] += kl_row(z, t, ns, scale, dz);
+    for (int i = 0; i < ns; ++i) dlv[o1 + i] = dz[i];
+    float cs = 0.f;
+    for (int i = 0; i < na; ++i) cs += counts[(src * K + k) * na + i];
+    for (int i = 0; i < na; ++i) { t[i] = counts[(src * K + k) * na + i] / cs; z[i] = lp[o3 + i]; }
+    acc[2] += kl_row(z, t, na, scale, dz);
+    for (int i = 0; i < na; ++i) dlp[o3 + i] = dz[i];
+  }
+  for (int j = 0; j < 3; ++j) red[j][threadIdx.x] = acc[j];
+  __syncthreads();
+  for (int s = LOSS_T / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+      for (int j = 0; j < 3; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float rl = (float)(red[0][0] / (B * K)), vl = (float)(red[1][0] / (B * K)), pl = (float)(red[2][0] / (B * K));
+    loss[0] = (1.f / (float)K) * ((rl + vl) + pl);
+    loss[1] = rl; loss[2] = vl; loss[3] = pl;
+  }
+}
+
+// ------------------------------------------------------------------ Adam (networks.py:268)
+// g = grad + wd*p; m += (1-b1)(g - m); v = v*b2 + (1-b2)*g*g; p += (-step_size*m) / (sqrt(v)/bc2s + eps)
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ grad, float* __restrict__ m,
+                            float* __restrict__ v, size_t n, float neg_step, float one_m_b1, float b2, float one_m_b2,
+                            float bc2s, float eps, float wd) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float pv = p[i];
+    const float g = grad[i] + wd * pv;
+    const float mv = m[i] + one_m_b1 * (g - m[i]);
+    const float vv = v[i] * b2 + (one_m_b2 * g) * g;
+    m[i] = mv;
+    v[i] = vv;
+    p[i] = pv + (neg_step * mv) / (sqrtf(vv) / bc2s + eps);
+  }
+}
+
+// ------------------------------------------------------------------ learner inputs
+// rep input [B][HW][Cp]: channel c < L = lut[frame code], L <= c < 2L = a/3 (train_torch.py:279-293,
+// 437-470), zero beyond 2L. states u8 ring [cap][L][HW], past_actions i64 ring [cap][L].
+template <typename T>
+__global__ void learner_input_kernel(const uint8_t* __restrict__ states, const int64_t* __restrict__ past,
+                                     const int32_t* __restrict__ slots, const float* __restrict__ lut, T* __restrict__ out,
+                                     int B, int L, int HW, int Cp) {
+  const size_t n = (size_t)B * HW * Cp;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    const size_t q = i / Cp;
+    const int p = (int)(q % HW);
+    const size_t b = q / HW, s = (size_t)slots[b];
+    float v = 0.f;
+    if (c < L) v = lut[states[(s * L + c) * HW + p] & 7];
+    else if (c < 2 * L) v = (float)past[s * L + (c - L)] / 3.0f;
+    st(out + i, v);
+  }
+}
+
+// dynamics input [B][HW][Cp] = [h (C channels), one-hot(a) (3), 0...] (train_torch.py:295-311)
+template <typename T>
+__global__ void dyn_input_kernel(const T* __restrict__ h, const int64_t* __restrict__ fut,
+                                 const int32_t* __restrict__ slots, int K, int k, T* __restrict__ out, int B, int HW,
+                                 int C, int A, int Cp) {
+  const size_t n = (size_t)B * HW * Cp;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    const size_t q = i / Cp;  // b*HW + p
+    const size_t b = q / HW;
+    float v = 0.f;
+    if (c < C) v = ld(h + q * C + c);
+    else if (c < C + A) v = (fut[(size_t)slots[b] * K + k] == (int64_t)(c - C)) ? 1.f : 0.f;
+    st(out + i, v);
+  }
+}
+
+unsigned grid_for(size_t n, int block = 256, unsigned cap = 16384) {
+  size_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  return (unsigned)(g > cap ? cap : g);
+}
+
+template <typename F>
+int dispatch(int dtype, F&& f) {
+  if (dtype == 0) return f(float{});
+  if (dtype == 1) return f(bf16_t{});
+  return -9;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mzba_bn_stats(int dtype, const void* x, int M, int C, float eps, float momentum, const float* gamma,
+                  const float* beta, float* stats, float* run_mean, float* run_var, void* ws, long long ws_bytes,
+                  hipStream_t stream) {
+  MZ_CHECK_ARG(x && stats && gamma && beta && ws && M > 0 && C > 0, -1);
+  const int rpc = 256;
+  const int nchunk = (M + rpc - 1) / rpc;
+  MZ_CHECK_ARG((long long)nchunk * C * (long long)sizeof(float2) <= ws_bytes, -2);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(bn_stats_partial_kernel<T>, dim3((C + 63) / 64, nchunk), dim3(256), 0, stream, (const T*)x, M,
+                       C, rpc, (float2*)ws);
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((C + 127) / 128), dim3(128), 0, stream, (const float2*)ws, nchunk,
+                       rpc, M, C, eps, momentum, gamma, beta, stats, run_mean, run_var);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_bn_apply(int dtype, const void* x, const float* stats, const void* res, int relu, void* out, int M, int C,
+                  hipStream_t stream) {
+  MZ_CHECK_ARG(x && stats && out && M > 0 && C > 0 && C % 4 == 0, -1);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for((size_t)M * C / 4)), dim3(256), 0, stream, (const T*)x, stats,
+                       (const T*)res, relu, (T*)out, M, C);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_bn_backward(int dtype, void* dy, const void* y, const void* x, const float* stats, int M, int C,
+                     float* dgamma, float* dbeta, void* dx, void* ws, long long ws_bytes, hipStream_t stream) {
+  MZ_CHECK_ARG(dy && x && stats && dgamma && dbeta && dx && ws && M > 0 && C > 0, -1);
+  const int rpc = 256;
+  const int nchunk = (M + rpc - 1) / rpc;
+  MZ_CHECK_ARG((long long)nchunk * C * (long long)sizeof(float2) + 3LL * C * 4 <= ws_bytes, -2);
+  float2* part = (float2*)ws;
+  float* coef = (float*)((char*)ws + (size_t)nchunk * C * sizeof(float2));
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(bn_bwd_partial_kernel<T>, dim3((C + 63) / 64, nchunk), dim3(256), 0, stream, (T*)dy,
+                       (const T*)y, (const T*)x, stats, M, C, rpc, part);
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 127) / 128), dim3(128), 0, stream, (const float2*)part, nchunk,
+                       M, C, stats, dgamma, dbeta, coef);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for((size_t)M * C)), dim3(256), 0, stream, (const T*)dy,
+                       (const T*)x, stats, (const float*)coef, (T*)dx, M, C);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_conv_wpack(int dtype, const float* w, void* wt, int Cout, int taps, int Cin, int cin_used, int flip,
+                    hipStream_t stream) {
+  MZ_CHECK_ARG(w && wt && Cout > 0 && taps > 0 && Cin > 0 && cin_used > 0 && cin_used <= Cin, -1);
+  const size_t n = flip ? (size_t)cin_used * taps * Cout : (size_t)Cout * taps * Cin;
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(conv_wt_kernel<T>, dim3(grid_for(n)), dim3(256), 0, stream, w, (T*)wt, Cout, taps, Cin,
+                       cin_used, flip);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks) {
+  const long long M = (long long)B * H * W;
+  const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64) * ks * ks;
+  long long nsplit = (512 + tiles - 1) / tiles;
+  const long long maxs = (M + 255) / 256;
+  if (nsplit > maxs) nsplit = maxs;
+  if (nsplit < 1) nsplit = 1;
+  return nsplit * ((long long)Cout * ks * ks * Cin + Cout) * 4;
+}
+
+int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
+                    float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream) {
+  MZ_CHECK_ARG(x && dy && dw && ws && B > 0 && (ks == 1 || ks == 3) && Cin % 4 == 0 && Cout % 4 == 0, -1);
+  const long long M = (long long)B * H * W;
+  const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64) * ks * ks;
+  long long nsplit = (512 + tiles - 1) / tiles;
+  const long long maxs = (M + 255) / 256;
+  if (nsplit > maxs) nsplit = maxs;
+  if (nsplit < 1) nsplit = 1;
+  const int rps = (int)(((M + nsplit - 1) / nsplit + WG_ROWS - 1) / WG_ROWS * WG_ROWS);
+  const size_t nw = (size_t)Cout * ks * ks * Cin;
+  MZ_CHECK_ARG(mzba_conv_wgrad_ws_bytes(B, H, W, Cin, Cout, ks) <= ws_bytes, -2);
+  float* part = (float*)ws;
+  float* bpart = db ? part + nsplit * nw : nullptr;
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(conv_wgrad_kernel<T>, dim3((unsigned)tiles, (unsigned)nsplit), dim3(256), 0, stream,
+                       (const T*)x, (const T*)dy, B, H, W, Cin, Cout, ks, rps, part, bpart);
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(nw)), dim3(256), 0, stream, (const float*)part,
+                       (int)nsplit, nw, dw);
+    if (db)
+      hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(Cout)), dim3(256), 0, stream, (const float*)bpart,
+                         (int)nsplit, (size_t)Cout, db);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_avgpool2_backward(int dtype, const void* dy, void* dx, int B, int H, int W, int C, hipStream_t stream) {
+  MZ_CHECK_ARG(dy && dx && B > 0 && H % 2 == 0 && W % 2 == 0, -1);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(avgpool2_bwd_kernel<T>, dim3(grid_for((size_t)B * H * W * C)), dim3(256), 0, stream,
+                       (const T*)dy, (T*)dx, B, H, W, C);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_axpy(int dtype, void* y, const void* x, long long n, hipStream_t stream) {
+  MZ_CHECK_ARG(y && x && n >= 0, -1);
+  if (n == 0) return 0;
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(axpy_kernel<T>, dim3(grid_for((size_t)n)), dim3(256), 0, stream, (T*)y, (const T*)x, (size_t)n);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_scale_forward(int dtype, const void* h, void* out, float* minmax, int32_t* argminmax, int B, int HW, int C,
+                       hipStream_t stream) {
+  MZ_CHECK_ARG(h && out && minmax && argminmax && B > 0 && HW > 0 && C > 0, -1);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(scale_fwd_kernel<T>, dim3(B), dim3(256), 0, stream, (const T*)h, (T*)out, (float2*)minmax,
+                       (int2*)argminmax, HW, C);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_scale_backward(int dtype, const void* dy, const void* h, const float* minmax, const int32_t* argminmax,
+                        void* dh, int B, int n, int accumulate, hipStream_t stream) {
+  MZ_CHECK_ARG(dy && h && minmax && argminmax && dh && B > 0 && n > 0, -1);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(scale_bwd_kernel<T>, dim3(B), dim3(256), 0, stream, (const T*)dy, (const T*)h,
+                       (const float2*)minmax, (const int2*)argminmax, (T*)dh, n, accumulate);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_linear_forward(int dtype, const void* x, const float* w, const float* bias, float* out, int B, int K, int O,
+                        hipStream_t stream) {
+  MZ_CHECK_ARG(x && w && bias && out && B > 0 && K > 0 && O > 0 && O <= 16, -1);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(linear_fwd_kernel<T>, dim3(B), dim3(256), 0, stream, (const T*)x, w, bias, out, K, O);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+long long mzba_linear_ws_bytes(int B, int K, int O) {
+  const int nsplit = B >= 64 ? 16 : 1;
+  return (long long)nsplit * ((long long)O * K + O) * 4;
+}
+
+int mzba_linear_backward(int dtype, const void* x, const float* w, const float* dy, void* dx, int accumulate,
+                         float* dw, float* db, int B, int K, int O, void* ws, long long ws_bytes, hipStream_t stream) {
+  MZ_CHECK_ARG(x && w && dy && dw && db && ws && B > 0 && K > 0 && O > 0 && O <= 16, -1);
+  MZ_CHECK_ARG(mzba_linear_ws_bytes(B, K, O) <= ws_bytes, -2);
+  const int nsplit = B >= 64 ? 16 : 1;
+  const int rps = (B + nsplit - 1) / nsplit;
+  float* part = (float*)ws;
+  float* bpart = part + (size_t)nsplit * O * K;
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    if (dx)
+      hipLaunchKernelGGL(linear_bwd_x_kernel<T>, dim3(grid_for((size_t)B * K)), dim3(256), 0, stream, dy, w, (T*)dx, B,
+                         K, O, accumulate);
+    hipLaunchKernelGGL(linear_bwd_w_kernel<T>, dim3((K + 255) / 256, nsplit), dim3(256), 0, stream, dy, (const T*)x,
+                       B, K, O, rps, part, bpart);
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for((size_t)O * K)), dim3(256), 0, stream, (const float*)part,
+                       nsplit, (size_t)O * K, dw);
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, stream, (const float*)bpart, nsplit, (size_t)O, db);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_learner_loss(const float* logit_r, const float* logit_v, const float* logit_p, const float* rewards,
+                      const float* targets, const float* counts, const int32_t* slots, int B, int K, int ns, int na,
+                      float smin, float smax, float* dlogit_r, float* dlogit_v, float* dlogit_p, float* loss,
+                      hipStream_t stream) {
+  MZ_CHECK_ARG(logit_r && logit_v && logit_p && rewards && targets && counts && dlogit_r && dlogit_v && dlogit_p &&
+                   loss && B > 0 && K > 0 && ns >= 2 && ns <= 16 && na > 0 && na <= 16,
+               -1);
+  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(LOSS_T), 0, stream, logit_r, logit_v, logit_p, rewards, targets, counts,
+                     slots, B, K, ns, na, smin, smax, dlogit_r, dlogit_v, dlogit_p, loss);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_adam(float* p, const float* grad, float* m, float* v, long long n, float neg_step, float one_m_b1, float b2,
+              float one_m_b2, float bc2_sqrt, float eps, float weight_decay, hipStream_t stream) {
+  MZ_CHECK_ARG(p && grad && m && v && n >= 0, -1);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, stream, p, grad, m, v, (size_t)n, neg_step,
+                     one_m_b1, b2, one_m_b2, bc2_sqrt, eps, weight_decay);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_learner_input(int dtype, const uint8_t* states, const int64_t* past_actions, const int32_t* slots,
+                       const float* lut8, void* out, int B, int L, int HW, int Cp, hipStream_t stream) {
+  MZ_CHECK_ARG(states && past_actions && slots && lut8 && out && B > 0 && L > 0 && Cp >= 2 * L, -1);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(learner_input_kernel<T>, dim3(grid_for((size_t)B * HW * Cp)), dim3(256), 0, stream, states,
+                       past_actions, slots, lut8, (T*)out, B, L, HW, Cp);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_dyn_input(int dtype, const void* h, const int64_t* future_actions, const int32_t* slots, int K, int k,
+                   void* out, int B, int HW, int C, int A, int Cp, hipStream_t stream) {
+  MZ_CHECK_ARG(h && future_actions && slots && out && B > 0 && k >= 0 && k < K && Cp >= C + A, -1);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(dyn_input_kernel<T>, dim3(grid_for((size_t)B * HW * Cp)), dim3(256), 0, stream, (const T*)h,
+                       future_actions, slots, K, k, (T*)out, B, HW, C, A, Cp);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+}  // extern "C"

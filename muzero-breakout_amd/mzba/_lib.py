@@ -55,6 +55,24 @@ SIGNATURES = {
     "mzba_sample_actions": [P, P, I, F, I, I, U64, P, P],
     "mzba_record_results": [P, P, P, P, I, I, P, P],
     "mzba_ctx_advance": [P, P],
+    # learner (learn.hip)
+    "mzba_bn_stats": [I, P, I, I, F, F, P, P, P, P, P, P, LL, P],
+    "mzba_bn_apply": [I, P, P, P, I, P, I, I, P],
+    "mzba_bn_backward": [I, P, P, P, P, I, I, P, P, P, P, LL, P],
+    "mzba_conv_wpack": [I, P, P, I, I, I, I, I, P],
+    "mzba_conv_wgrad_ws_bytes": [I, I, I, I, I, I],
+    "mzba_conv_wgrad": [I, P, P, I, I, I, I, I, I, P, P, P, LL, P],
+    "mzba_avgpool2_backward": [I, P, P, I, I, I, I, P],
+    "mzba_axpy": [I, P, P, LL, P],
+    "mzba_scale_forward": [I, P, P, P, P, I, I, I, P],
+    "mzba_scale_backward": [I, P, P, P, P, P, I, I, I, P],
+    "mzba_linear_forward": [I, P, P, P, P, I, I, I, P],
+    "mzba_linear_ws_bytes": [I, I, I],
+    "mzba_linear_backward": [I, P, P, P, P, I, P, P, I, I, I, P, LL, P],
+    "mzba_learner_loss": [P, P, P, P, P, P, P, I, I, I, I, F, F, P, P, P, P, P],
+    "mzba_adam": [P, P, P, P, LL, F, F, F, F, F, F, F, P],
+    "mzba_learner_input": [I, P, P, P, P, P, I, I, I, I, P],
+    "mzba_dyn_input": [I, P, P, P, I, I, P, I, I, I, I, I, P],
 }
 
 _lib = None
@@ -79,7 +97,8 @@ class TowerExt(ctypes.Structure):
 
 
 # entry points that return something other than a status code
-RESTYPES = {"mzba_tower_ws_bytes": LL, "mzba_tower_plan": I}
+RESTYPES = {"mzba_tower_ws_bytes": LL, "mzba_tower_plan": I, "mzba_conv_wgrad_ws_bytes": LL,
+            "mzba_linear_ws_bytes": LL}
 
 
 def lib():

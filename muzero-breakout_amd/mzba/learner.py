@@ -1,0 +1,570 @@
+"""Device learner: the training side of the reference's RLSystem.
+
+One minibatch of `RLSystem._training_stage` (train_torch.py:380-407) runs as a sequence of
+HIP launches over NHWC device buffers (csrc/learn.hip + the implicit-GEMM conv of conv.hip):
+
+  _prepare_minibatch + _encode_actions   mzba_learner_input (frames + a/3 planes straight from the
+                                          replay ring, no host gather)
+  _k_step_rollout (:487-528)             representation -> min-max scale -> K x (prediction,
+                                          dynamics), every BatchNorm in train mode
+  loss_fn (:33-66)                        mzba_learner_loss (two-hot targets, KL batchmean x3)
+  loss.backward()                         the reverse sweep below (BN / conv / linear / scale /
+                                          pool backward kernels), gradients accumulated over the
+                                          K unrolled uses of each weight
+  mu_zero.optimizer.step()                one mzba_adam launch over the flat parameter buffer
+
+Parameters live in one flat f32 buffer in kernel layouts (conv [Cout][tap][Cin_pad], linear
+[O][pixel][C]); `state_dict()` / `load_state_dict()` convert to and from the reference's
+`MuZeroAgent.state_dict()` keys and layouts, so a reference checkpoint trains here and the
+trained weights load into the acting agent (`load_latest_weights`, train_torch.py:361-367).
+dtype "f32" is the parity path; "bf16" stores activations and conv weights in bf16 (MFMA
+bf16) with f32 statistics, gradients, Adam state and master weights.
+"""
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .env import gray_lut
+from .weights import init_state_dict, rep_layout, state_dict_spec
+
+BN_EPS, BN_MOMENTUM = 1e-5, 0.1
+BETAS, ADAM_EPS, WEIGHT_DECAY = (0.9, 0.999), 1e-8, 1e-4
+
+
+def _pad8(c):
+    return (c + 7) // 8 * 8
+
+
+class _Param:
+    """One reference parameter in the flat buffer: kernel-layout view + layout converters."""
+
+    def __init__(self, key, shape, kind, off, kshape, cin=None, hw=None):
+        self.key, self.shape, self.kind, self.off, self.kshape = key, tuple(shape), kind, off, tuple(kshape)
+        self.cin, self.hw = cin, hw
+        self.n = int(np.prod(kshape))
+
+    def to_kernel(self, a):
+        a = torch.as_tensor(np.asarray(a, dtype=np.float32))
+        if self.kind == "conv_w":  # (co, ci, k, k) -> [co][k*k][ci_pad]
+            co, ci, k, _ = self.shape
+            out = torch.zeros(self.kshape)
+            out[:, :, :ci] = a.permute(0, 2, 3, 1).reshape(co, k * k, ci)
+            return out
+        if self.kind == "lin_w":  # (o, c*hw) -> [o][hw][c]
+            o = self.shape[0]
+            return a.reshape(o, self.cin, self.hw).permute(0, 2, 1).contiguous()
+        return a.reshape(self.kshape)
+
+    def to_ref(self, t):
+        t = t.detach().float().cpu()
+        if self.kind == "conv_w":
+            co, ci, k, _ = self.shape
+            return t[:, :, :ci].reshape(co, k, k, ci).permute(0, 3, 1, 2).contiguous()
+        if self.kind == "lin_w":
+            o = self.shape[0]
+            return t.reshape(o, self.hw, self.cin).permute(0, 2, 1).reshape(self.shape).contiguous()
+        return t.reshape(self.shape).clone()
+
+
+class _Conv:
+    def __init__(self, learner, prefix, cin, cout, ks, bn, w_key, b_key):
+        self.L, self.cin, self.cout, self.ks, self.bn = learner, cin, cout, ks, bn
+        self.cin_p = _pad8(cin)
+        self.w, self.b = learner._view(w_key), learner._view(b_key)
+        self.dw, self.db = learner._gview(w_key), learner._gview(b_key)
+        if bn:
+            self.gamma, self.beta = learner._view(prefix + ".weight"), learner._view(prefix + ".bias")
+            self.dgamma, self.dbeta = learner._gview(prefix + ".weight"), learner._gview(prefix + ".bias")
+            self.bn_key = prefix
+        self.wt = None  # input-gradient pack
+        self.wf = None  # bf16 forward pack
+
+
+class Learner:
+    """Device learner for one `MuZeroAgent` (mu_zero) + its Adam optimizer.
+
+    `train_minibatch(replay, slots)` = one iteration of the `_training_stage` loop body;
+    `training_stage(replay, num_batches, minibatch_size)` = the whole loop.
+    """
+
+    def __init__(self, mcfg, state_dict=None, K=5, dtype="f32", lr=None, seed=0, device="cuda"):
+        L.require_gpu()
+        if dtype not in ("f32", "bf16"):
+            raise ValueError("dtype must be 'f32' or 'bf16'")
+        self.m, self.K, self.device = mcfg, K, torch.device(device)
+        self.dt = 0 if dtype == "f32" else 1
+        self.tdtype = torch.float32 if dtype == "f32" else torch.bfloat16
+        self.lr = float(mcfg["learning_rate"] if lr is None else lr)
+        self.hist = mcfg["state_history_length"]
+        self.c0, self.c1 = mcfg["latent_channels"]
+        self.lat = tuple(mcfg["latent_resolution"])
+        self.ns, self.na = mcfg["num_supports"], mcfg["prediction_network"]["num_actions"]
+        self.A = mcfg["dynamics_network"]["num_actions"]
+        self.smin, self.smax = float(mcfg["supports_min"]), float(mcfg["supports_max"])
+        self._build_params()
+        self.step_count = 0
+        self.nbt = {k: 0 for k in self.bn_keys}
+        self._zero = torch.zeros(max(self.c0, self.c1, 2 * self.hist, 64), device=self.device)
+        self._lut = torch.from_numpy(gray_lut()).to(self.device)
+        self._ws = {}
+        self._build_modules()
+        self.load_state_dict(state_dict if state_dict is not None else init_state_dict(mcfg, seed))
+
+    # -- parameters --------------------------------------------------------------------------
+    def _build_params(self):
+        m = self.m
+        hw_lat = self.lat[0] * self.lat[1]
+        self.params, self.bn_keys = OrderedDict(), []
+        off = 0
+        for key, shape in state_dict_spec(m):
+            if key.endswith(("running_mean", "running_var", "num_batches_tracked")):
+                if key.endswith("running_mean"):
+                    self.bn_keys.append(key[: -len(".running_mean")])
+                continue
+            if len(shape) == 4:
+                co, ci, k, _ = shape
+                p = _Param(key, shape, "conv_w", off, (co, k * k, _pad8(ci)))
+            elif len(shape) == 2:
+                o, kk = shape
+                c = kk // hw_lat
+                p = _Param(key, shape, "lin_w", off, (o, hw_lat, c), cin=c, hw=hw_lat)
+            else:
+                p = _Param(key, shape, "vec", off, shape)
+            self.params[key] = p
+            off += (p.n + 15) // 16 * 16
+        self.n_flat = off
+        z = lambda: torch.zeros(off, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.P, self.G, self.M1, self.M2 = z(), z(), z(), z()
+        self.run = {}
+
+    def _view(self, key):
+        p = self.params[key]
+        return self.P[p.off:p.off + p.n].view(p.kshape)
+
+    def _gview(self, key):
+        p = self.params[key]
+        return self.G[p.off:p.off + p.n].view(p.kshape)
+
+    def load_state_dict(self, sd):
+        """Reference `MuZeroAgent.state_dict()` keys / shapes (also resets the Adam state)."""
+        with torch.no_grad():
+            self.P.zero_()
+            for key, p in self.params.items():
+                self._view(key).copy_(p.to_kernel(sd[key]).to(self.device))
+            self.run = {}
+            for k in self.bn_keys:
+                rm = torch.as_tensor(np.asarray(sd[k + ".running_mean"], np.float32)).to(self.device).clone()
+                rv = torch.as_tensor(np.asarray(sd[k + ".running_var"], np.float32)).to(self.device).clone()
+                self.run[k] = (rm, rv)
+                self.nbt[k] = int(np.asarray(sd[k + ".num_batches_tracked"]))
+            self.M1.zero_()
+            self.M2.zero_()
+            self.step_count = 0
+
+    def state_dict(self):
+        out = OrderedDict()
+        for key, shape in state_dict_spec(self.m):
+            if key in self.params:
+                out[key] = self.params[key].to_ref(self._view(key))
+            else:
+                bn = key.rsplit(".", 1)[0]
+                if key.endswith("running_mean"):
+                    out[key] = self.run[bn][0].detach().cpu().clone()
+                elif key.endswith("running_var"):
+                    out[key] = self.run[bn][1].detach().cpu().clone()
+                else:
+                    out[key] = torch.tensor(self.nbt[bn], dtype=torch.int64)
+        return out
+
+    def optimizer_state_dict(self):
+        """`mu_zero.optimizer.state_dict()` format (torch.optim.Adam, params in
+        `MuZeroAgent.parameters()` order) — the checkpoint's optimizer_state_dict."""
+        group = dict(torch.optim.Adam([torch.zeros(1)], lr=self.lr, weight_decay=WEIGHT_DECAY).state_dict()
+                     ["param_groups"][0])
+        group["params"] = list(range(len(self.params)))
+        state = {}
+        if self.step_count:
+            for i, (key, p) in enumerate(self.params.items()):
+                state[i] = {"step": torch.tensor(float(self.step_count)),
+                            "exp_avg": p.to_ref(self.M1[p.off:p.off + p.n].view(p.kshape)),
+                            "exp_avg_sq": p.to_ref(self.M2[p.off:p.off + p.n].view(p.kshape))}
+        return {"state": state, "param_groups": [group]}
+
+    def load_optimizer_state_dict(self, d):
+        """Inverse of optimizer_state_dict (a reference checkpoint's optimizer_state_dict)."""
+        st = d.get("state", {})
+        with torch.no_grad():
+            self.M1.zero_()
+            self.M2.zero_()
+            steps = set()
+            for i, (key, p) in enumerate(self.params.items()):
+                if i not in st:
+                    continue
+                self.M1[p.off:p.off + p.n].view(p.kshape).copy_(p.to_kernel(st[i]["exp_avg"]).to(self.device))
+                self.M2[p.off:p.off + p.n].view(p.kshape).copy_(p.to_kernel(st[i]["exp_avg_sq"]).to(self.device))
+                steps.add(int(float(st[i]["step"])))
+            if len(steps) > 1:
+                raise ValueError("optimizer state holds different step counts per parameter")
+            self.step_count = steps.pop() if steps else 0
+            if d.get("param_groups"):
+                self.lr = float(d["param_groups"][0]["lr"])
+
+    def gradients(self):
+        """Reference-layout gradients of the last minibatch (param.grad after loss.backward())."""
+        return OrderedDict((k, p.to_ref(self.G[p.off:p.off + p.n].view(p.kshape))) for k, p in self.params.items())
+
+    # -- modules ------------------------------------------------------------------------------
+    def _build_modules(self):
+        m = self.m
+        c0, c1 = self.c0, self.c1
+        self.rep = []
+        cin, nconv = 2 * self.hist, 0
+        for kind, i in rep_layout(m):
+            pre = f"rep_net.blocks.{i}"
+            if kind == "conv":
+                cout = c0 if nconv == 0 else c1
+                self.rep.append(("conv", _Conv(self, pre, cin, cout, 3, False, pre + ".weight", pre + ".bias")))
+                cin, nconv = cout, nconv + 1
+            elif kind == "res":
+                self.rep.append(("res", self._res(pre, cin)))
+            else:
+                self.rep.append(("pool", None))
+        self.dyn_block = _Conv(self, "dyn_net.conv_block.bn", c1 + self.A, c1, 3, True,
+                               "dyn_net.conv_block.conv.weight", "dyn_net.conv_block.conv.bias")
+        self.dyn_res = [self._res(f"dyn_net.res_blocks.{i}", c1) for i in range(m["dynamics_network"]["num_res_blocks"])]
+        self.dyn_rconv = _Conv(self, "dyn_net.reward_head.0.bn", c1, c1, 1, True, "dyn_net.reward_head.0.conv.weight",
+                               "dyn_net.reward_head.0.conv.bias")
+        self.dyn_rlin = ("dyn_net.reward_head.2", c1, self.ns)
+        self.pred_res = [self._res(f"pred_net.res_blocks.{i}", c1)
+                         for i in range(m["prediction_network"]["num_res_blocks"])]
+        self.pred_pconv = _Conv(self, "pred_net.policy_head.0.bn", c1, c1 // 2, 3, True,
+                                "pred_net.policy_head.0.conv.weight", "pred_net.policy_head.0.conv.bias")
+        self.pred_plin = ("pred_net.policy_head.2", c1 // 2, self.na)
+        self.pred_vconv = _Conv(self, "pred_net.value_head.0.bn", c1, c1 // 2, 1, True,
+                                "pred_net.value_head.0.conv.weight", "pred_net.value_head.0.conv.bias")
+        self.pred_vlin = ("pred_net.value_head.2", c1 // 2, self.ns)
+        self.convs = [c for k, c in self.rep if k == "conv"] + [c for k, r in self.rep if k == "res" for c in r]
+        self.convs += [self.dyn_block, self.dyn_rconv, self.pred_pconv, self.pred_vconv]
+        self.convs += [c for r in self.dyn_res + self.pred_res for c in r]
+
+    def _res(self, pre, c):
+        return (_Conv(self, pre + ".bn1", c, c, 3, True, pre + ".conv1.weight", pre + ".conv1.bias"),
+                _Conv(self, pre + ".bn2", c, c, 3, True, pre + ".conv2.weight", pre + ".conv2.bias"))
+
+    # -- scratch -------------------------------------------------------------------------------
+    def _scratch(self, name, nbytes):
+        t = self._ws.get(name)
+        if t is None or t.numel() < nbytes:
+            t = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
+            self._ws[name] = t
+        return t
+
+    def _act(self, rows, c):
+        return torch.empty(rows, c, dtype=self.tdtype, device=self.device)
+
+    # -- primitive ops ----------------------------------------------------------------------------
+    def _prepare_packs(self):
+        """Per-step weight packs: bf16 casts for the forward, flipped transposes for dgrad."""
+        s = L.stream()
+        for c in self.convs:
+            taps = c.ks * c.ks
+            cin_used = min(c.cin, self.c1) if c is self.dyn_block else c.cin_p
+            if c is self.rep[0][1]:  # the input planes need no gradient
+                if self.dt == 1 and c.wf is None:
+                    c.wf = torch.empty(c.cout, taps, c.cin_p, dtype=self.tdtype, device=self.device)
+                if self.dt == 1:
+                    L.call("mzba_conv_wpack", 1, L.ptr(c.w), L.ptr(c.wf), c.cout, taps, c.cin_p, c.cin_p, 0, s)
+                continue
+            if c.wt is None:
+                c.wt = torch.empty(cin_used, taps, c.cout, dtype=self.tdtype, device=self.device)
+                if self.dt == 1:
+                    c.wf = torch.empty(c.cout, taps, c.cin_p, dtype=self.tdtype, device=self.device)
+            L.call("mzba_conv_wpack", self.dt, L.ptr(c.w), L.ptr(c.wt), c.cout, taps, c.cin_p, cin_used, 1, s)
+            if self.dt == 1:
+                L.call("mzba_conv_wpack", 1, L.ptr(c.w), L.ptr(c.wf), c.cout, taps, c.cin_p, c.cin_p, 0, s)
+
+    def _conv(self, c, x, B, H, W):
+        t = self._act(B * H * W, c.cout)
+        w = c.w if self.dt == 0 else c.wf
+        L.call("mzba_conv2d", self.dt, L.ptr(x), H * W * c.cin_p, None, 0, L.ptr(w), L.ptr(c.b), None, None, 0,
+               None, L.ptr(t), B, H, W, c.cin_p, c.cout, c.ks, 0, L.stream())
+        return t
+
+    def _bn(self, c, t, res=None, relu=True):
+        M = t.shape[0]
+        stats = torch.empty(4, c.cout, dtype=torch.float32, device=self.device)
+        rm, rv = self.run[c.bn_key]
+        ws = self._scratch("bn", ((M + 255) // 256) * c.cout * 8 + 12 * c.cout)
+        L.call("mzba_bn_stats", self.dt, L.ptr(t), M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma), L.ptr(c.beta),
+               L.ptr(stats), L.ptr(rm), L.ptr(rv), L.ptr(ws), ws.numel(), L.stream())
+        self.nbt[c.bn_key] += 1
+        y = self._act(M, c.cout)
+        L.call("mzba_bn_apply", self.dt, L.ptr(t), L.ptr(stats), L.ptr(res), int(relu), L.ptr(y), M, c.cout,
+               L.stream())
+        return y, stats
+
+    def _bn_bwd(self, c, dy, y, t, stats):
+        M = t.shape[0]
+        dt = self._act(M, c.cout)
+        ws = self._scratch("bn", ((M + 255) // 256) * c.cout * 8 + 12 * c.cout)
+        L.call("mzba_bn_backward", self.dt, L.ptr(dy), L.ptr(y), L.ptr(t), L.ptr(stats), M, c.cout, L.ptr(c.dgamma),
+               L.ptr(c.dbeta), L.ptr(dt), L.ptr(ws), ws.numel(), L.stream())
+        return dt
+
+    def _wgrad(self, c, x, dy, B, H, W):
+        nb = L.lib().mzba_conv_wgrad_ws_bytes(B, H, W, c.cin_p, c.cout, c.ks)
+        ws = self._scratch("wg", nb)
+        L.call("mzba_conv_wgrad", self.dt, L.ptr(x), L.ptr(dy), B, H, W, c.cin_p, c.cout, c.ks, L.ptr(c.dw),
+               L.ptr(c.db), L.ptr(ws), ws.numel(), L.stream())
+
+    def _dgrad(self, c, dy, B, H, W, acc=None):
+        """Input gradient of conv c (first cin_used channels); added into `acc` when given."""
+        cu = c.wt.shape[0]
+        out = acc if acc is not None else self._act(B * H * W, cu)
+        L.call("mzba_conv2d", self.dt, L.ptr(dy), H * W * c.cout, None, 0, L.ptr(c.wt), L.ptr(self._zero), None,
+               None, 0, L.ptr(acc), L.ptr(out), B, H, W, c.cout, cu, c.ks, 0, L.stream())
+        return out
+
+    def _linear(self, key, x, B, cin, O, out):
+        K = self.lat[0] * self.lat[1] * cin
+        L.call("mzba_linear_forward", self.dt, L.ptr(x), L.ptr(self._view(key + ".weight")),
+               L.ptr(self._view(key + ".bias")), L.ptr(out), B, K, O, L.stream())
+
+    def _linear_bwd(self, key, x, dy, B, cin, O):
+        K = self.lat[0] * self.lat[1] * cin
+        dx = self._act(B * self.lat[0] * self.lat[1], cin)
+        ws = self._scratch("lin", L.lib().mzba_linear_ws_bytes(B, K, O))
+        L.call("mzba_linear_backward", self.dt, L.ptr(x), L.ptr(self._view(key + ".weight")), L.ptr(dy), L.ptr(dx), 0,
+               L.ptr(self._gview(key + ".weight")), L.ptr(self._gview(key + ".bias")), B, K, O, L.ptr(ws), ws.numel(),
+               L.stream())
+        return dx
+
+    # -- blocks: forward returns (out, saved); backward takes the output gradient ------------------------
+    def _res_fwd(self, r, x, B, H, W):
+        c1, c2 = r
+        t1 = self._conv(c1, x, B, H, W)
+        a1, s1 = self._bn(c1, t1)
+        t2 = self._conv(c2, a1, B, H, W)
+        out, s2 = self._bn(c2, t2, res=x)
+        return out, (x, t1, a1, s1, t2, s2, out)
+
+    def _res_bwd(self, r, sv, g, gx, B, H, W):
+        """g: gradient of the block output (overwritten with the ReLU-masked gradient);
+        gx: existing gradient of the block input or None. Returns the input gradient."""
+        c1, c2 = r
+        x, t1, a1, s1, t2, s2, out = sv
+        dt2 = self._bn_bwd(c2, g, out, t2, s2)           # g <- g * [out > 0]
+        self._wgrad(c2, a1, dt2, B, H, W)
+        da1 = self._dgrad(c2, dt2, B, H, W)
+        del dt2
+        dt1 = self._bn_bwd(c1, da1, a1, t1, s1)
+        del da1
+        self._wgrad(c1, x, dt1, B, H, W)
+        if gx is None:                                     # skip path: the masked g itself
+            return self._dgrad(c1, dt1, B, H, W, acc=g)
+        self._dgrad(c1, dt1, B, H, W, acc=gx)
+        L.call("mzba_axpy", self.dt, L.ptr(gx), L.ptr(g), gx.numel(), L.stream())
+        return gx
+
+    def _block_fwd(self, c, x, B, H, W):  # ConvBlock: conv -> BN -> ReLU
+        t = self._conv(c, x, B, H, W)
+        y, s = self._bn(c, t)
+        return y, (x, t, s, y)
+
+    def _block_bwd(self, c, sv, g, B, H, W, acc=None):
+        x, t, s, y = sv
+        dt = self._bn_bwd(c, g, y, t, s)
+        self._wgrad(c, x, dt, B, H, W)
+        return self._dgrad(c, dt, B, H, W, acc=acc)
+
+    def _scale_fwd(self, h, B):
+        hw, C = h.shape[0] // B, h.shape[1]
+        out = self._act(h.shape[0], C)
+        mm = torch.empty(B, 2, dtype=torch.float32, device=self.device)
+        idx = torch.empty(B, 2, dtype=torch.int32, device=self.device)
+        L.call("mzba_scale_forward", self.dt, L.ptr(h), L.ptr(out), L.ptr(mm), L.ptr(idx), B, hw, C, L.stream())
+        self._scale_idx.append((idx, hw, C))
+        return out, (h, mm, idx)
+
+    def scale_indices(self):
+        """(argmin, argmax) of every _scale_state of the last minibatch (representation, then
+        dynamics k = 0..K-1) as NCHW flatten indices [B][2] (torch.min/max(dim=1) semantics)."""
+        out = []
+        for idx, hw, C in self._scale_idx:
+            i = idx.long().cpu().numpy()
+            out.append((i % C) * hw + i // C)
+        return out
+
+    def _scale_bwd(self, sv, dy, B, acc=None):
+        h, mm, idx = sv
+        out = acc if acc is not None else self._act(*h.shape)
+        L.call("mzba_scale_backward", self.dt, L.ptr(dy), L.ptr(h), L.ptr(mm), L.ptr(idx), L.ptr(out), B,
+               h.shape[0] // B * h.shape[1], int(acc is not None), L.stream())
+        return out
+
+    # -- one minibatch ------------------------------------------------------------------------------
+    def train_minibatch(self, ring, slots):
+        """One `_training_stage` iteration on replay windows `slots` (i32 ring rows) of `ring`
+        (a DeviceReplayBuffer, or any object with the same `_ring` dict). Returns the device
+        loss vector (total, reward, value, policy)."""
+        g = ring._ring
+        slots = slots.to(device=self.device, dtype=torch.int32).contiguous()
+        B, K, Lh = slots.numel(), self.K, self.hist
+        H, W = 16, 20
+        hl, wl = self.lat
+        HWl = hl * wl
+        s = L.stream()
+        self.G.zero_()
+        self._scale_idx = []
+        self._prepare_packs()
+        # ---- forward (_k_step_rollout)
+        cin_p = self.rep[0][1].cin_p
+        x = self._act(B * H * W, cin_p)
+        L.call("mzba_learner_input", self.dt, L.ptr(g["states"]), L.ptr(g["past_actions"]), L.ptr(slots),
+               L.ptr(self._lut), L.ptr(x), B, Lh, H * W, cin_p, s)
+        tape, h, hh, ww = [], x, H, W
+        for kind, mod in self.rep:
+            if kind == "conv":
+                y = self._conv(mod, h, B, hh, ww)
+                tape.append(("conv", mod, (h, hh, ww)))
+                h = y
+            elif kind == "res":
+                h, sv = self._res_fwd(mod, h, B, hh, ww)
+                tape.append(("res", mod, (sv, hh, ww)))
+            else:
+                y = self._act(B * (hh // 2) * (ww // 2), h.shape[1])
+                L.call("mzba_avgpool2", self.dt, L.ptr(h), L.ptr(y), B, hh, ww, h.shape[1], s)
+                tape.append(("pool", None, (hh, ww, h.shape[1])))
+                h, hh, ww = y, hh // 2, ww // 2
+        h, rep_scale = self._scale_fwd(h, B)
+        lr_all = torch.empty(K, B, self.ns, device=self.device)
+        lv_all = torch.empty(K, B, self.ns, device=self.device)
+        lp_all = torch.empty(K, B, self.na, device=self.device)
+        unroll = []
+        cdyn = self.dyn_block.cin_p
+        for k in range(K):
+            # prediction(h_k)
+            p_in, psv = h, []
+            xp = h
+            for r in self.pred_res:
+                xp, sv = self._res_fwd(r, xp, B, hl, wl)
+                psv.append(sv)
+            yp, spol = self._block_fwd(self.pred_pconv, xp, B, hl, wl)
+            self._linear(self.pred_plin[0], yp, B, self.pred_plin[1], self.na, lp_all[k])
+            yv, sval = self._block_fwd(self.pred_vconv, xp, B, hl, wl)
+            self._linear(self.pred_vlin[0], yv, B, self.pred_vlin[1], self.ns, lv_all[k])
+            # dynamics(h_k, a_k)
+            xin = self._act(B * HWl, cdyn)
+            L.call("mzba_dyn_input", self.dt, L.ptr(h), L.ptr(g["future_actions"]), L.ptr(slots), K, k, L.ptr(xin),
+                   B, HWl, self.c1, self.A, cdyn, s)
+            xd, sblk = self._block_fwd(self.dyn_block, xin, B, hl, wl)
+            dsv = []
+            for r in self.dyn_res:
+                xd, sv = self._res_fwd(r, xd, B, hl, wl)
+                dsv.append(sv)
+            yr, srew = self._block_fwd(self.dyn_rconv, xd, B, hl, wl)
+            self._linear(self.dyn_rlin[0], yr, B, self.dyn_rlin[1], self.ns, lr_all[k])
+            h_next, ssc = self._scale_fwd(xd, B)
+            unroll.append(dict(p_in=p_in, psv=psv, xp=xp, spol=spol, sval=sval, yp=yp, yv=yv, sblk=sblk, dsv=dsv,
+                               xd=xd, yr=yr, srew=srew, ssc=ssc))
+            h = h_next
+        # ---- loss_fn
+        dlr, dlv, dlp = torch.empty_like(lr_all), torch.empty_like(lv_all), torch.empty_like(lp_all)
+        loss = torch.empty(4, device=self.device)
+        L.call("mzba_learner_loss", L.ptr(lr_all), L.ptr(lv_all), L.ptr(lp_all), L.ptr(g["rewards"]),
+               L.ptr(g["targets"]), L.ptr(g["counts"]), L.ptr(slots), B, K, self.ns, self.na, self.smin, self.smax,
+               L.ptr(dlr), L.ptr(dlv), L.ptr(dlp), L.ptr(loss), s)
+        self.last_logits = (lr_all, lv_all, lp_all)
+        # ---- backward
+        gh = None  # gradient of h_{k+1} (scaled latent)
+        for k in reversed(range(K)):
+            u = unroll[k]
+            # dynamics k: scale -> reward head -> res blocks -> conv block
+            gx = self._scale_bwd(u["ssc"], gh, B) if gh is not None else None
+            dyr = self._linear_bwd(self.dyn_rlin[0], u["yr"], dlr[k], B, self.dyn_rlin[1], self.ns)
+            gx = self._block_bwd(self.dyn_rconv, u["srew"], dyr, B, hl, wl, acc=gx)
+            del dyr
+            for r, sv in zip(reversed(self.dyn_res), reversed(u["dsv"])):
+                gx = self._res_bwd(r, sv, gx, None, B, hl, wl)
+            gh = self._block_bwd(self.dyn_block, u["sblk"], gx, B, hl, wl)  # d h_k (first c1 channels)
+            del gx
+            # prediction k: heads -> res blocks, accumulating into d h_k
+            dyv = self._linear_bwd(self.pred_vlin[0], u["yv"], dlv[k], B, self.pred_vlin[1], self.ns)
+            gp = self._block_bwd(self.pred_vconv, u["sval"], dyv, B, hl, wl)
+            dyp = self._linear_bwd(self.pred_plin[0], u["yp"], dlp[k], B, self.pred_plin[1], self.na)
+            self._block_bwd(self.pred_pconv, u["spol"], dyp, B, hl, wl, acc=gp)
+            del dyv, dyp
+            for i in reversed(range(len(self.pred_res))):
+                gp = self._res_bwd(self.pred_res[i], u["psv"][i], gp, gh if i == 0 else None, B, hl, wl)
+            if not self.pred_res:
+                L.call("mzba_axpy", self.dt, L.ptr(gh), L.ptr(gp), gh.numel(), s)
+            unroll[k] = None
+        # representation: scale -> [pool | res | conv] reversed
+        gx = self._scale_bwd(rep_scale, gh, B)
+        for kind, mod, sv in reversed(tape):
+            if kind == "pool":
+                hh2, ww2, C = sv
+                dx = self._act(B * hh2 * ww2, C)
+                L.call("mzba_avgpool2_backward", self.dt, L.ptr(gx), L.ptr(dx), B, hh2, ww2, C, s)
+                gx = dx
+            elif kind == "res":
+                svr, hh2, ww2 = sv
+                gx = self._res_bwd(mod, svr, gx, None, B, hh2, ww2)
+            else:
+                xin, hh2, ww2 = sv
+                self._wgrad(mod, xin, gx, B, hh2, ww2)
+                gx = self._dgrad(mod, gx, B, hh2, ww2) if mod is not self.rep[0][1] else None
+        # ---- Adam (networks.py:268)
+        self.step_count += 1
+        t = self.step_count
+        b1, b2 = BETAS
+        L.call("mzba_adam", L.ptr(self.P), L.ptr(self.G), L.ptr(self.M1), L.ptr(self.M2), self.n_flat,
+               -(self.lr / (1 - b1 ** t)), 1 - b1, b2, 1 - b2, (1 - b2 ** t) ** 0.5, ADAM_EPS, WEIGHT_DECAY, s)
+        return loss
+
+    def training_stage(self, ring, num_batches, minibatch_size, generator=None):
+        """`_training_stage` loop (train_torch.py:373-407): randperm over the buffer, num_batches
+        minibatches; returns the per-minibatch losses (host floats)."""
+        n = len(ring)
+        perm = torch.randperm(n, generator=generator)
+        losses = []
+        for i in range(num_batches):
+            idx = perm[i * minibatch_size:(i + 1) * minibatch_size]
+            if idx.numel() < minibatch_size:
+                break
+            slots = (idx.to(self.device) + ring.start) % ring.max_length
+            losses.append(self.train_minibatch(ring, slots))
+        return [float(x[0]) for x in losses]
+
+
+class MinibatchRing:
+    """A replay-ring-shaped holder for explicit minibatch arrays (tests, tools): the windows
+    of `mb` become ring rows 0..B-1. Frames must be convert_to_grayscale values."""
+
+    def __init__(self, mb, device="cuda"):
+        lut = gray_lut()
+        vals, first = np.unique(lut, return_index=True)
+        st = np.asarray(mb["states"], np.float32)
+        B = st.shape[0]
+        st = st.reshape(B, st.shape[1], -1)
+        pos = np.searchsorted(vals, st).clip(0, len(vals) - 1)
+        if not np.array_equal(vals[pos], st):
+            raise ValueError("states hold values that are not convert_to_grayscale outputs")
+        dev = torch.device(device)
+        self._ring = {
+            "states": torch.from_numpy(first[pos].astype(np.uint8)).to(dev),
+            "past_actions": torch.as_tensor(np.asarray(mb["past_actions"], np.int64)).to(dev),
+            "future_actions": torch.as_tensor(np.asarray(mb["future_actions"], np.int64)).to(dev),
+            "rewards": torch.as_tensor(np.asarray(mb["rewards"], np.float32)).to(dev),
+            "targets": torch.as_tensor(np.asarray(mb["targets"], np.float32)).to(dev),
+            "counts": torch.as_tensor(np.asarray(mb["counts"], np.float32)).to(dev),
+        }
+        self.start, self.max_length, self.length = 0, B, B
+
+    def __len__(self):
+        return self.length
+
+    def slots(self):
+        return torch.arange(self.length, dtype=torch.int32, device=self._ring["states"].device)

@@ -40,12 +40,12 @@ def rep_layout(mcfg):
 
 def supports_representation(x, smin, smax, n, eps=0.001):
     """utils.py:30-64: compact transform, two-hot over linspace(smin, smax, n)."""
-    sup = torch.linspace(smin, smax, n)
+    sup = torch.linspace(smin, smax, n, dtype=x.dtype)
     t = torch.sign(x) * (torch.sqrt(torch.abs(x) + 1) - 1 + eps * x)
     lo = (torch.searchsorted(sup, t, right=True) - 1).clamp(0, n - 2)
     hi = lo + 1
     pl = (sup[hi] - t) / (sup[hi] - sup[lo] + 1e-10)
-    out = torch.zeros(*x.shape, n)
+    out = torch.zeros(*x.shape, n, dtype=x.dtype)
     out.scatter_(-1, lo.unsqueeze(-1), pl.unsqueeze(-1))
     out.scatter_(-1, hi.unsqueeze(-1), (1 - pl).unsqueeze(-1))
     return out
@@ -60,16 +60,18 @@ def kl_batchmean(logits, target):
 class LearnerOracle:
     """Parameters, BN running stats and Adam state of the three nets; `step(minibatch)`."""
 
-    def __init__(self, mcfg, state_dict, K=5, lr=None):
-        self.m, self.K = mcfg, K
+    def __init__(self, mcfg, state_dict, K=5, lr=None, dtype=torch.float32):
+        self.m, self.K, self.dtype = mcfg, K, dtype
         self.lr = mcfg["learning_rate"] if lr is None else lr
         self.p, self.buf = OrderedDict(), OrderedDict()
         for k, v in state_dict.items():
             t = torch.tensor(np.asarray(v))
-            if k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+            if k.endswith(("running_mean", "running_var")):
+                self.buf[k] = t.clone().to(dtype)
+            elif k.endswith("num_batches_tracked"):
                 self.buf[k] = t.clone()
             else:
-                self.p[k] = t.clone().float().requires_grad_(True)
+                self.p[k] = t.clone().to(dtype).requires_grad_(True)
         self.adam = {k: [0, torch.zeros_like(v), torch.zeros_like(v)] for k, v in self.p.items()}
 
     # -- modules -----------------------------------------------------------------------------
@@ -91,11 +93,20 @@ class LearnerOracle:
     def _linear(self, x, pre):
         return F.linear(x.flatten(1), self.p[pre + ".weight"], self.p[pre + ".bias"])
 
-    @staticmethod
-    def _scale(h):
+    force_index = None  # optional list of (B, 2) NCHW-flat (argmin, argmax) per _scale call
+
+    def _scale(self, h):
         f = h.view(h.shape[0], -1)
-        mn = f.min(dim=1, keepdim=True)[0].view(-1, 1, 1, 1)
-        mx = f.max(dim=1, keepdim=True)[0].view(-1, 1, 1, 1)
+        if self.force_index is not None:
+            # the min / max taken at given positions: the same values up to rounding near-ties, and
+            # the gradient routed to those positions (torch.min/max(dim) route to their index)
+            idx = torch.as_tensor(np.asarray(self.force_index[self._nscale]), dtype=torch.int64)
+            self._nscale += 1
+            mn = f.gather(1, idx[:, :1]).view(-1, 1, 1, 1)
+            mx = f.gather(1, idx[:, 1:2]).view(-1, 1, 1, 1)
+        else:
+            mn = f.min(dim=1, keepdim=True)[0].view(-1, 1, 1, 1)
+            mx = f.max(dim=1, keepdim=True)[0].view(-1, 1, 1, 1)
         return (h - mn) / (mx - mn + 1e-8)
 
     def representation(self, x):
@@ -118,7 +129,7 @@ class LearnerOracle:
 
     def dynamics(self, h, a):
         B, _, H, W = h.shape
-        planes = F.one_hot(a, 3).float().view(B, 3, 1, 1).expand(-1, -1, H, W)
+        planes = F.one_hot(a, 3).to(self.dtype).view(B, 3, 1, 1).expand(-1, -1, H, W)
         x = self._block(torch.cat([h, planes], 1), "dyn_net.conv_block", 1)
         for i in range(self.m["dynamics_network"]["num_res_blocks"]):
             x = self._res(x, f"dyn_net.res_blocks.{i}")
@@ -127,11 +138,13 @@ class LearnerOracle:
 
     # -- one minibatch --------------------------------------------------------------------------
     def forward_loss(self, mb):
+        self._nscale = 0
         L = self.m["state_history_length"]
-        states = torch.from_numpy(np.asarray(mb["states"], np.float32))
+        dt = self.dtype
+        states = torch.from_numpy(np.asarray(mb["states"], np.float32)).to(dt)
         B = states.shape[0]
         acts = torch.from_numpy(np.asarray(mb["past_actions"], np.int64))
-        planes = (acts / 3)[:, :, None, None].expand(-1, -1, 16, 20)
+        planes = (acts.to(dt) / 3)[:, :, None, None].expand(-1, -1, 16, 20)
         x = torch.cat([states.view(B, L, 16, 20), planes], 1)
         h = self.representation(x)
         fut = torch.from_numpy(np.asarray(mb["future_actions"], np.int64))
@@ -143,12 +156,20 @@ class LearnerOracle:
             rews.append(r)
         pr, pv, pp = torch.stack(rews, 1), torch.stack(vals, 1), torch.stack(pols, 1)
         s = (self.m["supports_min"], self.m["supports_max"], self.m["num_supports"])
-        rl = kl_batchmean(pr, supports_representation(torch.from_numpy(np.asarray(mb["rewards"], np.float32)), *s))
-        vl = kl_batchmean(pv, supports_representation(torch.from_numpy(np.asarray(mb["targets"], np.float32)), *s))
-        c = torch.from_numpy(np.asarray(mb["counts"], np.float32))
+        rl = kl_batchmean(pr, supports_representation(torch.from_numpy(np.asarray(mb["rewards"], np.float32)).to(dt), *s))
+        vl = kl_batchmean(pv, supports_representation(torch.from_numpy(np.asarray(mb["targets"], np.float32)).to(dt), *s))
+        c = torch.from_numpy(np.asarray(mb["counts"], np.float32)).to(dt)
         pl = kl_batchmean(pp, c / c.sum(dim=-1, keepdim=True))
         loss = (1 / self.K) * (rl + vl + pl)
         return loss, (rl, vl, pl), (pr, pv, pp)
+
+    def gradients(self, mb):
+        """loss.backward() only (no update): (loss parts, logits, grads)."""
+        for v in self.p.values():
+            v.grad = None
+        loss, parts, logits = self.forward_loss(mb)
+        loss.backward()
+        return parts, [x.detach() for x in logits], {k: v.grad.detach().clone() for k, v in self.p.items()}
 
     def step(self, mb):
         for v in self.p.values():

@@ -548,6 +548,12 @@ def make_learner(cfg):
             for k in ("loss", "rl", "vl", "pl"):
                 out[f"s{step}/{k}"] = res[k]
             if full:
+                if step == 1:  # Adam moments after step 1 (reference optimizer state, param order)
+                    names = [k for k, _ in agent.named_parameters()]
+                    ost = agent.optimizer.state_dict()["state"]
+                    for i, k in enumerate(names):
+                        out[f"s1/opt/exp_avg/{k}"] = ost[i]["exp_avg"].numpy()
+                        out[f"s1/opt/exp_avg_sq/{k}"] = ost[i]["exp_avg_sq"].numpy()
                 for k in ("pr", "pv", "pp"):
                     out[f"s{step}/{k}"] = res[k]
                 for k, v in grads.items():
@@ -570,6 +576,16 @@ def make_learner(cfg):
                         out[f"s{step}/delta_sum/{k}"] = np.array([d.sum(), np.abs(d).sum()])
                     else:
                         out[f"s{step}/buf_sum/{k}"] = np.array([flat.sum(), np.abs(flat).sum()])
+            if full:  # the reference's own f32 error: its logits / gradients against an f64
+                # evaluation of the same algorithm (oracle/learner.py, pinned to the reference in f32)
+                from oracle.learner import LearnerOracle
+                start = sd0 if step == 1 else {k[len("s1/param/"):]: out[k] for k in out if k.startswith("s1/param/")}
+                o64 = LearnerOracle(mcfg, start, K=K, dtype=torch.float64)
+                _, lg64, g64 = o64.gradients(mb)
+                for k, a in zip(("pr", "pv", "pp"), lg64):
+                    out[f"s{step}/err_ref/{k}"] = np.float64(np.abs(res[k].astype(np.float64) - a.numpy()).max())
+                for k, gr in grads.items():
+                    out[f"s{step}/err_ref/grad/{k}"] = np.float64(np.abs(gr.astype(np.float64) - g64[k].numpy()).max())
             print("learner", tag, "step", step, "loss", float(res["loss"]), float(res["rl"]), float(res["vl"]),
                   float(res["pl"]))
         np.savez_compressed(os.path.join(HERE, f"learner_{tag}.npz"), **out)
