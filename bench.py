@@ -42,12 +42,13 @@ def parse():
     ap.add_argument("--cpu-envs", type=int, default=16, help="bounded oracle sample (cpu_baseline + match rate)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
-    ap.add_argument("--workload", default="acting", choices=["acting", "env"],
+    ap.add_argument("--workload", default="acting", choices=["acting", "env", "learner"],
                     help="acting: the whole acting loop (headline); env: env step + render + frame stack only "
                          "(configs 1/3, HBM roofline)")
     ap.add_argument("--height", type=int, default=None, help="env workload frame height (default 84)")
     ap.add_argument("--width", type=int, default=None, help="env workload frame width (default 84)")
     ap.add_argument("--hist", type=int, default=4, help="env workload frame-stack length")
+    ap.add_argument("--minibatch", type=int, default=512, help="learner workload minibatch (config.yaml:7)")
     return ap.parse_args()
 
 
@@ -135,6 +136,103 @@ def run_env(args, world, rank, local):
         dist.destroy_process_group()
 
 
+def run_learner(args, world, rank, local):
+    """RLSystem._training_stage minibatches (B windows, K = 5 unroll, train-mode
+    BN, backward, Adam) on the device learner over a synthetic device replay ring. `value` =
+    windows/s (all ranks; N > 1 = independent replicas, the reference's learner is single-device).
+    roofline = the minibatch's algorithmic conv/linear FLOPs / its time vs the dense MFMA peak
+    of the arithmetic type (f32 157.3 TF, bf16 2500 TF)."""
+    from mzba.config import default_config
+    from mzba.learner import Learner
+    from mzba.weights import init_state_dict
+    dt = args.dtype if args.dtype in ("f32", "bf16") else "f32"
+    mcfg = default_config()["model"]
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    B, K, Lh, cap = args.minibatch, 5, mcfg["state_history_length"], 4096
+    g = torch.Generator(device=dev).manual_seed(args.seed + rank)
+
+    class Ring:
+        pass
+    ring = Ring()
+    ring.start, ring.max_length, ring.length = 0, cap, cap
+    ring._ring = {
+        "states": (torch.randint(0, 8, (cap, Lh, 320), device=dev, generator=g) *
+                   (torch.rand(cap, Lh, 320, device=dev, generator=g) < 0.3)).to(torch.uint8),
+        "past_actions": torch.randint(0, 3, (cap, Lh), device=dev, generator=g),
+        "future_actions": torch.randint(0, 3, (cap, K), device=dev, generator=g),
+        "rewards": torch.randint(-1, 2, (cap, K), device=dev, generator=g).float(),
+        "targets": torch.randn(cap, K, device=dev, generator=g) * 2,
+        "counts": torch.randint(0, 51, (cap, K, 3), device=dev, generator=g).float() + 1,
+    }
+    ln = Learner(mcfg, init_state_dict(mcfg, args.seed), K=K, dtype=dt, device=dev)
+    slots = [torch.randperm(cap, device=dev, generator=g)[:B].to(torch.int32) for _ in range(args.warmup + args.steps)]
+    for i in range(args.warmup):
+        ln.train_minibatch(ring, slots[i])
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(torch.cuda.current_stream())
+        loss = ln.train_minibatch(ring, slots[args.warmup + i])
+        ev[i][1].record(torch.cuda.current_stream())
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dtt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dtt], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dtt = float(tt.item())
+    kms = float(np.median([a.elapsed_time(c) for a, c in ev]))
+    fl = ln.flops_per_minibatch(B)
+    peak = 157.3 if dt == "f32" else PEAK_BF16_TFLOPS
+    achieved = fl / (kms * 1e-3) / 1e12
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        from oracle.learner import LearnerOracle
+        from mzba.learner import MinibatchRing  # noqa: F401
+        nb = 8
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        gen = np.random.default_rng(args.seed)
+        lut = np.array([0, 0.3, 0.6, 1.0], np.float32)
+        mb = dict(states=lut[gen.integers(0, 4, (nb, Lh, 16, 20)) * (gen.random((nb, Lh, 16, 20)) < 0.3)],
+                  past_actions=gen.integers(0, 3, (nb, Lh)), future_actions=gen.integers(0, 3, (nb, K)),
+                  rewards=gen.choice(np.array([-1, 0, 1], np.float32), (nb, K)),
+                  targets=(gen.normal(size=(nb, K)) * 2).astype(np.float32),
+                  counts=gen.multinomial(50, [0.3, 0.3, 0.4], (nb, K)).astype(np.float32) + 1)
+        o = LearnerOracle(mcfg, init_state_dict(mcfg, args.seed), K=K)
+        o.step(mb)
+        c0, n = time.perf_counter(), 0
+        while n < 3 and time.perf_counter() - c0 < 20.0:
+            o.step(mb)
+            n += 1
+        cs = time.perf_counter() - c0
+        cpu = {"value": nb * n / cs, "unit": "windows/s", "cores": torch.get_num_threads(), "kind": "port",
+               "sample": f"oracle/learner.py (torch-CPU f32, the reference's ops) on {n} minibatches of {nb} "
+                         f"windows ({cs:.1f} s)"}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "learner windows/sec (RLSystem._training_stage minibatch: K=5 rollout, train-mode BN, "
+                      "backward, Adam)",
+            "value": world * B * args.steps / dtt, "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": dtt / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": dt,
+            "data": "synthetic replay ring (4096 windows), seeded random-init reference-architecture nets",
+            "config": {"workload": f"learner minibatch {B} windows x K=5, full-width nets (config.yaml)",
+                       "minibatch": B, "parallelism": "replicas" if world > 1 else "single device"},
+            "roofline": {"bound": "mfma", "kernel": "whole minibatch (conv fwd / dgrad / wgrad + BN + heads + Adam)",
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
+                         "traffic": None, "flop_per_minibatch": fl, "avg_launch_ms": kms},
+            "loss": float(loss[0]),
+            "cpu_baseline": cpu,
+        }))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def cfg_name(B, S):
     """Which BASELINE config an acting-loop run is (per-GPU batch and sims)."""
     return {(1024, 50): "config 2", (4096, 50): "config 4 (per-GPU share)", (4096, 200): "config 5 (bf16)"}.get(
@@ -155,6 +253,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.workload == "env":
         return run_env(args, world, rank, local)
+    if args.workload == "learner":
+        return run_learner(args, world, rank, local)
     from mzba.config import default_config
     from mzba.weights import init_state_dict
     from mzba.agent import MuZeroAgent

@@ -524,6 +524,31 @@ class Learner:
                -(self.lr / (1 - b1 ** t)), 1 - b1, b2, 1 - b2, (1 - b2 ** t) ** 0.5, ADAM_EPS, WEIGHT_DECAY, s)
         return loss
 
+    def flops_per_minibatch(self, B):
+        """Algorithmic conv + linear FLOPs of one minibatch: forward, input gradients (all convs
+        but the first) and weight gradients, 2 * M * Cout * Cin * taps each (Cin unpadded)."""
+        H, W = 16, 20
+        hw = self.lat[0] * self.lat[1]
+        fl, hh, ww = 0.0, H, W
+        first = True
+        for kind, mod in self.rep:
+            if kind == "pool":
+                hh, ww = hh // 2, ww // 2
+                continue
+            convs = [mod] if kind == "conv" else list(mod)
+            for c in convs:
+                f = 2.0 * B * hh * ww * c.cout * c.cin * c.ks * c.ks
+                fl += f * (2 if first else 3)
+                first = False
+        per = [self.dyn_block, self.dyn_rconv, self.pred_pconv, self.pred_vconv]
+        per += [c for r in self.dyn_res + self.pred_res for c in r]
+        for c in per:
+            cin = self.c1 if c is self.dyn_block else c.cin  # action planes: no input gradient needed
+            fl += self.K * 2.0 * B * hw * c.cout * (2 * c.cin + cin) * c.ks * c.ks
+        lin = [(self.dyn_rlin[1], self.ns), (self.pred_plin[1], self.na), (self.pred_vlin[1], self.ns)]
+        fl += self.K * sum(3 * 2.0 * B * hw * cin * o for cin, o in lin)
+        return fl
+
     def training_stage(self, ring, num_batches, minibatch_size, generator=None):
         """`_training_stage` loop (train_torch.py:373-407): randperm over the buffer, num_batches
         minibatches; returns the per-minibatch losses (host floats)."""
