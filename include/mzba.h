@@ -278,7 +278,7 @@ int mzba_ctx_advance(int32_t* ctx, hipStream_t stream);
 /* BatchNorm2d forward statistics in train mode (nn.BatchNorm2d in ConvBlock / ResidualBlock,
  * networks.py:7-35): stats[4][C] = (mean, invstd, gamma*invstd, beta - mean*gamma*invstd) over the
  * M rows of x [M][C]; running_mean / running_var (may be NULL) updated with momentum and the
- * unbiased variance. ws >= ceil(M/256)*C*8 bytes. */
+ * unbiased variance. C % 4 == 0; ws >= ceil(M/64)*C*8 bytes. */
 int mzba_bn_stats(int dtype, const void* x, int M, int C, float eps, float momentum, const float* gamma,
                   const float* beta, float* stats, float* run_mean, float* run_var, void* ws, long long ws_bytes,
                   hipStream_t stream);
@@ -287,7 +287,7 @@ int mzba_bn_apply(int dtype, const void* x, const float* stats, const void* res,
                   hipStream_t stream);
 /* BN (+ReLU) backward: if y != NULL, dy *= [y > 0] in place (the ReLU after the BN / residual
  * add); dgamma += sum(dy*xhat), dbeta += sum(dy); dx = (dy - (x-mean)*k - mean(dy))*gamma*invstd.
- * ws >= ceil(M/256)*C*8 + 12*C bytes. */
+ * C % 4 == 0; ws >= ceil(M/64)*C*8 + 12*C bytes. */
 int mzba_bn_backward(int dtype, void* dy, const void* y, const void* x, const float* stats, int M, int C,
                      float* dgamma, float* dbeta, void* dx, void* ws, long long ws_bytes, hipStream_t stream);
 /* Weight packs from the f32 master weights w [Cout][taps][Cin]: flip = 0: cast copy (forward);

@@ -25,37 +25,69 @@
 
 namespace {
 
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
 template <typename T> MZ_DEV float ld(const T* p) { return ElemIO<T>::load(p); }
 template <typename T> MZ_DEV void st(T* p, float v) { ElemIO<T>::store(p, v); }
 
 // ------------------------------------------------------------------ BatchNorm statistics
+// 4 consecutive channels per thread (C % 4 == 0): f32 float4 / bf16 8-byte loads.
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  static MZ_DEV float4 load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  static MZ_DEV void store(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+};
+template <> struct Vec4<bf16_t> {
+  static MZ_DEV float4 load(const bf16_t* p) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+  }
+  static MZ_DEV void store(bf16_t* p, float4 v) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
+  }
+};
+MZ_DEV float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
+
 // part[chunk][c] = (chunk mean, chunk M2) over rows [chunk*rpc, min(M, (chunk+1)*rpc)).
-// 256 threads = 64 channels x 4 row lanes.
+// 256 threads = (channel quads of a 64-channel group = 16) x 16 row lanes.
+constexpr int BN_RPC = 64;
 template <typename T>
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restrict__ x, int M, int C, int rpc,
                                                                float2* __restrict__ part) {
-  __shared__ float red[4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+  __shared__ float4 red[16][16];
+  const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + tq * 4;
   const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
   const int n = r1 - r0;
-  float s = 0.f;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < C)
-    for (int r = r0 + ty; r < r1; r += 4) s += ld(x + (size_t)r * C + c);
-  red[ty][tx] = s;
+    for (int r = r0 + ty; r < r1; r += 16) s = f4add(s, Vec4<T>::load(x + (size_t)r * C + c));
+  red[ty][tq] = s;
   __syncthreads();
-  const float mean = ((red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx])) / (float)n;
+  float4 t = red[0][tq];
+  for (int k = 1; k < 16; ++k) t = f4add(t, red[k][tq]);
+  const float4 mean = make_float4(t.x / n, t.y / n, t.z / n, t.w / n);
   __syncthreads();
-  float q = 0.f;
+  float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < C)
-    for (int r = r0 + ty; r < r1; r += 4) {
-      const float d = ld(x + (size_t)r * C + c) - mean;
-      q += d * d;
+    for (int r = r0 + ty; r < r1; r += 16) {
+      const float4 v = Vec4<T>::load(x + (size_t)r * C + c);
+      const float4 d = make_float4(v.x - mean.x, v.y - mean.y, v.z - mean.z, v.w - mean.w);
+      q = make_float4(q.x + d.x * d.x, q.y + d.y * d.y, q.z + d.z * d.z, q.w + d.w * d.w);
     }
-  red[ty][tx] = q;
+  red[ty][tq] = q;
   __syncthreads();
-  if (ty == 0 && c < C)
-    part[(size_t)blockIdx.y * C + c] = make_float2(mean, (red[0][tx] + red[1][tx]) + (red[2][tx] + red[3][tx]));
+  if (ty == 0 && c < C) {
+    float4 m2 = red[0][tq];
+    for (int k = 1; k < 16; ++k) m2 = f4add(m2, red[k][tq]);
+    float2* o = part + (size_t)blockIdx.y * C + c;
+    o[0] = make_float2(mean.x, m2.x);
+    o[1] = make_float2(mean.y, m2.y);
+    o[2] = make_float2(mean.z, m2.z);
+    o[3] = make_float2(mean.w, m2.w);
+  }
 }
 
 // combine the chunks (Chan et al., in double, chunk order) -> mean, invstd, alpha = gamma*invstd,
@@ -100,13 +132,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     const size_t e = i * 4;
     const int c = (int)(e % C);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float v = ld(x + e + j) * alpha[c + j] + beta[c + j];
-      if (res) v = v + ld(res + e + j);
-      if (relu) v = fmaxf(v, 0.f);
-      st(out + e + j, v);
-    }
+    const float4 v = Vec4<T>::load(x + e);
+    const float4 a = *reinterpret_cast<const float4*>(alpha + c), b = *reinterpret_cast<const float4*>(beta + c);
+    float4 y = make_float4(v.x * a.x + b.x, v.y * a.y + b.y, v.z * a.z + b.z, v.w * a.w + b.w);
+    if (res) y = f4add(y, Vec4<T>::load(res + e));
+    if (relu) y = make_float4(fmaxf(y.x, 0.f), fmaxf(y.y, 0.f), fmaxf(y.z, 0.f), fmaxf(y.w, 0.f));
+    Vec4<T>::store(out + e, y);
   }
 }
 
@@ -116,30 +147,42 @@ template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(T* __restrict__ dy, const T* __restrict__ y,
                                                              const T* __restrict__ x, const float* __restrict__ stats,
                                                              int M, int C, int rpc, float2* __restrict__ part) {
-  __shared__ float red[2][4][64];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+  __shared__ float4 red[2][16][16];
+  const int tq = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = blockIdx.x * 64 + tq * 4;
   const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
-  float sg = 0.f, sd = 0.f;
+  float4 sg = make_float4(0.f, 0.f, 0.f, 0.f), sd = sg;
   if (c < C) {
-    const float mean = stats[c];
-    for (int r = r0 + ty; r < r1; r += 4) {
+    const float4 mean = *reinterpret_cast<const float4*>(stats + c);
+    for (int r = r0 + ty; r < r1; r += 16) {
       const size_t i = (size_t)r * C + c;
-      float g = ld(dy + i);
+      float4 g = Vec4<T>::load(dy + i);
       if (y) {
-        if (!(ld(y + i) > 0.f)) g = 0.f;
-        st(dy + i, g);
+        const float4 yv = Vec4<T>::load(y + i);
+        if (!(yv.x > 0.f)) g.x = 0.f;
+        if (!(yv.y > 0.f)) g.y = 0.f;
+        if (!(yv.z > 0.f)) g.z = 0.f;
+        if (!(yv.w > 0.f)) g.w = 0.f;
+        Vec4<T>::store(dy + i, g);
       }
-      sg += g;
-      sd += g * (ld(x + i) - mean);
+      const float4 xv = Vec4<T>::load(x + i);
+      sg = f4add(sg, g);
+      sd = make_float4(sd.x + g.x * (xv.x - mean.x), sd.y + g.y * (xv.y - mean.y), sd.z + g.z * (xv.z - mean.z),
+                       sd.w + g.w * (xv.w - mean.w));
     }
   }
-  red[0][ty][tx] = sg;
-  red[1][ty][tx] = sd;
+  red[0][ty][tq] = sg;
+  red[1][ty][tq] = sd;
   __syncthreads();
-  if (ty == 0 && c < C)
-    part[(size_t)blockIdx.y * C + c] = make_float2((red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]),
-                                                   (red[1][0][tx] + red[1][1][tx]) + (red[1][2][tx] + red[1][3][tx]));
+  if (ty == 0 && c < C) {
+    float4 a = red[0][0][tq], b = red[1][0][tq];
+    for (int k = 1; k < 16; ++k) { a = f4add(a, red[0][k][tq]); b = f4add(b, red[1][k][tq]); }
+    float2* o = part + (size_t)blockIdx.y * C + c;
+    o[0] = make_float2(a.x, b.x);
+    o[1] = make_float2(a.y, b.y);
+    o[2] = make_float2(a.z, b.z);
+    o[3] = make_float2(a.w, b.w);
+  }
 }
 
 // dgamma += dot*invstd, dbeta += sum g; coef = (mean_g, k = dot*invstd^2/N, gamma*invstd)
@@ -167,11 +210,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ stats,
                                                            const float* __restrict__ coef, T* __restrict__ dx, int M,
                                                            int C) {
-  const size_t n = (size_t)M * C;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const float proj = (ld(x + i) - stats[c]) * coef[C + c];
-    st(dx + i, ((ld(g + i) - proj) - coef[c]) * coef[2 * C + c]);
+  const size_t n4 = (size_t)M * C / 4;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t e = i * 4;
+    const int c = (int)(e % C);
+    const float4 gv = Vec4<T>::load(g + e), xv = Vec4<T>::load(x + e);
+    const float4 mu = *reinterpret_cast<const float4*>(stats + c);
+    const float4 mg = *reinterpret_cast<const float4*>(coef + c);
+    const float4 k = *reinterpret_cast<const float4*>(coef + C + c);
+    const float4 s = *reinterpret_cast<const float4*>(coef + 2 * C + c);
+    Vec4<T>::store(dx + e, make_float4(((gv.x - (xv.x - mu.x) * k.x) - mg.x) * s.x, ((gv.y - (xv.y - mu.y) * k.y) - mg.y) * s.y,
+                                       ((gv.z - (xv.z - mu.z) * k.z) - mg.z) * s.z, ((gv.w - (xv.w - mu.w) * k.w) - mg.w) * s.w));
   }
 }
 
@@ -301,6 +350,139 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(const T* __restrict__ x
       const int co = cot * 64 + tid * 4;
       float* bp = bpart + (size_t)split * Cout;
       if (co < Cout) { bp[co] = s.x; bp[co + 1] = s.y; bp[co + 2] = s.z; bp[co + 3] = s.w; }
+    }
+  }
+}
+
+// bf16: v_mfma_f32_16x16x32_bf16 with both operands read by ds_read_b64_tr_b16 from row-major
+// [m][channel] LDS tiles (rows staged straight from HBM, 16-B chunks). A = dY^T (co x m), B = X_tap
+// (m x ci). Lane group g (lanes 16g..16g+15) takes k rows {4g..4g+3} and {16+4g..16+4g+3} of each
+// 32-row k step (the same permutation for A and B); a 160-B row stride makes each 32-lane half's
+// eight rows hit disjoint banks.
+constexpr int WB_M = 64, WB_LD = 80;  // rows per stage, bf16 per LDS row
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+MZ_DEV bf16x8_t tr_frag(const bf16_t* base) {  // base: this lane's address for the first 4 rows
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + 16 * WB_LD));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, r);  // bit pattern, not a numeric short -> bf16 conversion
+}
+
+__global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(const bf16_t* __restrict__ x,
+                                                              const bf16_t* __restrict__ dy, int B, int H, int W,
+                                                              int Cin, int Cout, int ks, int rows_per_split,
+                                                              float* __restrict__ part, float* __restrict__ bpart) {
+  __shared__ __attribute__((aligned(16))) bf16_t la[2][WB_M][WB_LD];
+  __shared__ __attribute__((aligned(16))) bf16_t lb[2][WB_M][WB_LD];
+  __shared__ float bred[32][64];
+  const int taps = ks * ks, pad = ks / 2;
+  const int nci = (Cin + 63) / 64;
+  int t = blockIdx.x;
+  const int cit = t % nci; t /= nci;
+  const int tap = t % taps; t /= taps;
+  const int cot = t;
+  const int split = blockIdx.y;
+  const int HW = H * W, M = B * HW;
+  const int m0 = split * rows_per_split, m1 = min(M, m0 + rows_per_split);
+  const int ky = tap / ks - pad, kx = tap % ks - pad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  // staging: chunk c = tid + 256u (u = 0, 1): row c >> 3, 8 channels at 8*(c & 7)
+  const int ch = tid & 7;
+  const int co_s = cot * 64 + ch * 8, ci_s = cit * 64 + ch * 8;
+  uint4 va[2], vb[2];
+  auto load = [&](int mb) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int m = mb + ((tid + 256 * u) >> 3);
+      va[u] = make_uint4(0, 0, 0, 0);
+      vb[u] = va[u];
+      if (m < m1) {
+        const int b = m / HW, p = m - b * HW, yy = p / W, xx = p - yy * W;
+        if (co_s < Cout) va[u] = *reinterpret_cast<const uint4*>(dy + (size_t)m * Cout + co_s);
+        const int sy = yy + ky, sx = xx + kx;
+        if (ci_s < Cin && sy >= 0 && sy < H && sx >= 0 && sx < W)
+          vb[u] = *reinterpret_cast<const uint4*>(x + ((size_t)b * HW + sy * W + sx) * Cin + ci_s);
+      }
+    }
+  };
+  const bool do_bias = bpart && tap == 0 && cit == 0;
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = (tid + 256 * u) >> 3;
+      *reinterpret_cast<uint4*>(&la[buf][r][ch * 8]) = va[u];
+      *reinterpret_cast<uint4*>(&lb[buf][r][ch * 8]) = vb[u];
+      if (do_bias) {
+        const bf16_t* e = reinterpret_cast<const bf16_t*>(&va[u]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bacc[j] += bf16_to_f32(e[j]);
+      }
+    }
+  };
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (m1 - m0 + WB_M - 1) / WB_M;
+  if (nsteps > 0) {
+    load(m0);
+    store(0);
+  }
+  __syncthreads();
+  // transposed-read lane address: group g = lane >> 4 takes rows 4g + q, q = (lane & 15) >> 2,
+  // columns 4p.. (p = lane & 3) of its 16-column block
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) load(m0 + (s + 1) * WB_M);
+#pragma unroll
+    for (int kk = 0; kk < WB_M / 32; ++kk) {
+      const int row = kk * 32 + 4 * g + q;
+      bf16x8_t a[2], bfr[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = tr_frag(&la[buf][row][wr * 32 + i * 16 + 4 * pp]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bfr[j] = tr_frag(&lb[buf][row][wc * 32 + j * 16 + 4 * pp]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+  const size_t K = (size_t)taps * Cin;
+  float* outp = part + (size_t)split * Cout * K;
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ci = cit * 64 + wc * 32 + j * 16 + fr;
+      if (ci >= Cin) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = cot * 64 + wr * 32 + i * 16 + 4 * fk + r;
+        if (co < Cout) outp[(size_t)co * K + (size_t)tap * Cin + ci] = acc[i][j][r];
+      }
+    }
+  if (do_bias) {  // 32 row lanes per channel group -> column sums
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bred[tid >> 3][ch * 8 + j] = bacc[j];
+    __syncthreads();
+    if (tid < 64) {
+      float sum = 0.f;
+      for (int r = 0; r < 32; ++r) sum += bred[r][tid];
+      const int co = cot * 64 + tid;
+      if (co < Cout) bpart[(size_t)split * Cout + co] = sum;
     }
   }
 }
@@ -639,8 +821,8 @@ extern "C" {
 int mzba_bn_stats(int dtype, const void* x, int M, int C, float eps, float momentum, const float* gamma,
                   const float* beta, float* stats, float* run_mean, float* run_var, void* ws, long long ws_bytes,
                   hipStream_t stream) {
-  MZ_CHECK_ARG(x && stats && gamma && beta && ws && M > 0 && C > 0, -1);
-  const int rpc = 256;
+  MZ_CHECK_ARG(x && stats && gamma && beta && ws && M > 0 && C > 0 && C % 4 == 0, -1);
+  const int rpc = BN_RPC;
   const int nchunk = (M + rpc - 1) / rpc;
   MZ_CHECK_ARG((long long)nchunk * C * (long long)sizeof(float2) <= ws_bytes, -2);
   return dispatch(dtype, [&](auto t) {
@@ -668,8 +850,8 @@ int mzba_bn_apply(int dtype, const void* x, const float* stats, const void* res,
 
 int mzba_bn_backward(int dtype, void* dy, const void* y, const void* x, const float* stats, int M, int C,
                      float* dgamma, float* dbeta, void* dx, void* ws, long long ws_bytes, hipStream_t stream) {
-  MZ_CHECK_ARG(dy && x && stats && dgamma && dbeta && dx && ws && M > 0 && C > 0, -1);
-  const int rpc = 256;
+  MZ_CHECK_ARG(dy && x && stats && dgamma && dbeta && dx && ws && M > 0 && C > 0 && C % 4 == 0, -1);
+  const int rpc = BN_RPC;
   const int nchunk = (M + rpc - 1) / rpc;
   MZ_CHECK_ARG((long long)nchunk * C * (long long)sizeof(float2) + 3LL * C * 4 <= ws_bytes, -2);
   float2* part = (float2*)ws;
@@ -680,7 +862,7 @@ int mzba_bn_backward(int dtype, void* dy, const void* y, const void* x, const fl
                        (const T*)y, (const T*)x, stats, M, C, rpc, part);
     hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 127) / 128), dim3(128), 0, stream, (const float2*)part, nchunk,
                        M, C, stats, dgamma, dbeta, coef);
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for((size_t)M * C)), dim3(256), 0, stream, (const T*)dy,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for((size_t)M * C / 4)), dim3(256), 0, stream, (const T*)dy,
                        (const T*)x, stats, (const float*)coef, (T*)dx, M, C);
     MZ_LAUNCH_CHECK();
     return 0;
@@ -700,34 +882,40 @@ int mzba_conv_wpack(int dtype, const float* w, void* wt, int Cout, int taps, int
   });
 }
 
+static long long wgrad_splits(long long M, long long tiles) {
+  long long nsplit = (512 + tiles - 1) / tiles;  // >= 2 workgroups per CU
+  const long long maxs = (M + 255) / 256;        // >= 256 rows per split
+  if (nsplit > maxs) nsplit = maxs;
+  return nsplit < 1 ? 1 : nsplit;
+}
+
 long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks) {
   const long long M = (long long)B * H * W;
   const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64) * ks * ks;
-  long long nsplit = (512 + tiles - 1) / tiles;
-  const long long maxs = (M + 255) / 256;
-  if (nsplit > maxs) nsplit = maxs;
-  if (nsplit < 1) nsplit = 1;
-  return nsplit * ((long long)Cout * ks * ks * Cin + Cout) * 4;
+  return wgrad_splits(M, tiles) * ((long long)Cout * ks * ks * Cin + Cout) * 4;
 }
 
 int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
                     float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream) {
   MZ_CHECK_ARG(x && dy && dw && ws && B > 0 && (ks == 1 || ks == 3) && Cin % 4 == 0 && Cout % 4 == 0, -1);
+  MZ_CHECK_ARG(dtype == 0 || (Cin % 8 == 0 && Cout % 8 == 0), -1);
   const long long M = (long long)B * H * W;
   const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64) * ks * ks;
-  long long nsplit = (512 + tiles - 1) / tiles;
-  const long long maxs = (M + 255) / 256;
-  if (nsplit > maxs) nsplit = maxs;
-  if (nsplit < 1) nsplit = 1;
-  const int rps = (int)(((M + nsplit - 1) / nsplit + WG_ROWS - 1) / WG_ROWS * WG_ROWS);
+  const long long nsplit = wgrad_splits(M, tiles);
+  const int step = dtype ? WB_M : WG_ROWS;
+  const int rps = (int)(((M + nsplit - 1) / nsplit + step - 1) / step * step);
   const size_t nw = (size_t)Cout * ks * ks * Cin;
   MZ_CHECK_ARG(mzba_conv_wgrad_ws_bytes(B, H, W, Cin, Cout, ks) <= ws_bytes, -2);
   float* part = (float*)ws;
   float* bpart = db ? part + nsplit * nw : nullptr;
-  return dispatch(dtype, [&](auto t) {
-    using T = decltype(t);
-    hipLaunchKernelGGL(conv_wgrad_kernel<T>, dim3((unsigned)tiles, (unsigned)nsplit), dim3(256), 0, stream,
-                       (const T*)x, (const T*)dy, B, H, W, Cin, Cout, ks, rps, part, bpart);
+  MZ_CHECK_ARG(dtype == 0 || dtype == 1, -9);
+  {
+    if (dtype == 1)
+      hipLaunchKernelGGL(conv_wgrad_bf16_kernel, dim3((unsigned)tiles, (unsigned)nsplit), dim3(256), 0, stream,
+                         (const bf16_t*)x, (const bf16_t*)dy, B, H, W, Cin, Cout, ks, rps, part, bpart);
+    else
+      hipLaunchKernelGGL(conv_wgrad_kernel<float>, dim3((unsigned)tiles, (unsigned)nsplit), dim3(256), 0, stream,
+                         (const float*)x, (const float*)dy, B, H, W, Cin, Cout, ks, rps, part, bpart);
     hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(nw)), dim3(256), 0, stream, (const float*)part,
                        (int)nsplit, nw, dw);
     if (db)
@@ -735,7 +923,7 @@ int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int 
                          (int)nsplit, (size_t)Cout, db);
     MZ_LAUNCH_CHECK();
     return 0;
-  });
+  }
 }
 
 int mzba_avgpool2_backward(int dtype, const void* dy, void* dx, int B, int H, int W, int C, hipStream_t stream) {

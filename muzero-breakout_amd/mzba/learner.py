@@ -296,7 +296,7 @@ class Learner:
         M = t.shape[0]
         stats = torch.empty(4, c.cout, dtype=torch.float32, device=self.device)
         rm, rv = self.run[c.bn_key]
-        ws = self._scratch("bn", ((M + 255) // 256) * c.cout * 8 + 12 * c.cout)
+        ws = self._scratch("bn", ((M + 63) // 64) * c.cout * 8 + 12 * c.cout)
         L.call("mzba_bn_stats", self.dt, L.ptr(t), M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma), L.ptr(c.beta),
                L.ptr(stats), L.ptr(rm), L.ptr(rv), L.ptr(ws), ws.numel(), L.stream())
         self.nbt[c.bn_key] += 1
@@ -308,7 +308,7 @@ class Learner:
     def _bn_bwd(self, c, dy, y, t, stats):
         M = t.shape[0]
         dt = self._act(M, c.cout)
-        ws = self._scratch("bn", ((M + 255) // 256) * c.cout * 8 + 12 * c.cout)
+        ws = self._scratch("bn", ((M + 63) // 64) * c.cout * 8 + 12 * c.cout)
         L.call("mzba_bn_backward", self.dt, L.ptr(dy), L.ptr(y), L.ptr(t), L.ptr(stats), M, c.cout, L.ptr(c.dgamma),
                L.ptr(c.dbeta), L.ptr(dt), L.ptr(ws), ws.numel(), L.stream())
         return dt

@@ -234,3 +234,35 @@ def test_learner_bf16_tracks_f32():
     vals = np.array(list(cos.values()))
     print("bf16 gradient cosines: min", vals.min(), "median", np.median(vals))
     assert vals.min() >= 0.5 and np.median(vals) >= 0.9, sorted(cos.items(), key=lambda kv: kv[1])[:5]
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("shape", [(8, 16, 20, 64, 128, 3), (16, 4, 5, 264, 256, 3), (16, 4, 5, 256, 128, 1),
+                                   (3, 8, 10, 256, 256, 3), (5, 4, 5, 40, 24, 3)])
+def test_conv_wgrad_matches_torch(dt, shape):
+    """mzba_conv_wgrad (weight + bias gradient, accumulated into the gradient buffers) against
+    torch.nn.grad.conv2d_weight in f64 on the same (bf16-rounded for bf16) operands."""
+    from mzba import _lib as L
+    B, H, W, Cin, Cout, ks = shape
+    if dt == "bf16" and (Cin % 8 or Cout % 8):
+        pytest.skip("bf16 path needs Cin, Cout % 8")
+    g = torch.Generator().manual_seed(sum(shape))
+    tdt = torch.float32 if dt == "f32" else torch.bfloat16
+    x = torch.randn(B, H, W, Cin, generator=g).to(tdt)
+    dy = torch.randn(B, H, W, Cout, generator=g).to(tdt)
+    dw0 = torch.randn(Cout, ks * ks, Cin, generator=g)
+    db0 = torch.randn(Cout, generator=g)
+    dev = torch.device("cuda")
+    xd, dyd, dw, db = x.to(dev), dy.to(dev), dw0.clone().to(dev), db0.clone().to(dev)
+    nb = L.lib().mzba_conv_wgrad_ws_bytes(B, H, W, Cin, Cout, ks)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    L.call("mzba_conv_wgrad", 0 if dt == "f32" else 1, L.ptr(xd), L.ptr(dyd), B, H, W, Cin, Cout, ks, L.ptr(dw),
+           L.ptr(db), L.ptr(ws), nb, L.stream())
+    ref = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (Cout, Cin, ks, ks),
+                                      dy.double().permute(0, 3, 1, 2), padding=ks // 2)
+    ref = ref.permute(0, 2, 3, 1).reshape(Cout, ks * ks, Cin) + dw0.double()
+    refb = dy.double().sum(dim=(0, 1, 2)) + db0.double()
+    tol = 1e-5 if dt == "f32" else 2e-3
+    scale = ref.abs().max().item()
+    assert (dw.cpu().double() - ref).abs().max().item() <= tol * scale
+    assert (db.cpu().double() - refb).abs().max().item() <= tol * refb.abs().max().item() + 1e-4
