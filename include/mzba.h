@@ -294,6 +294,11 @@ int mzba_bn_backward(int dtype, void* dy, const void* y, const void* x, const fl
  * flip = 1: wt [cin_used][taps][Cout] = w[co][taps-1-tap][ci] (the input-gradient convolution). */
 int mzba_conv_wpack(int dtype, const float* w, void* wt, int Cout, int taps, int Cin, int cin_used, int flip,
                     hipStream_t stream);
+/* bf16 packs for mzba_conv_lat (layout 1) / mzba_conv_band (layout 2, 3x3) from the f32 master
+ * weights w [Cout][taps][Cin]: logical W'[n][tap][c] = flip ? w[c][taps-1-tap][n] : w[n][tap][c]
+ * (N x Cc; flip: N <= Cin, Cc = Cout), + pad zero elements. */
+int mzba_conv_pack_bf16(const float* w, void* out, int Cout, int taps, int Cin, int N, int Cc, int flip, int layout,
+                        long long pad, hipStream_t stream);
 /* Conv2d weight / bias gradient: dw [Cout][ks*ks][Cin] += sum_m dy[m][co] * x_tap[m][ci],
  * db [Cout] += sum_m dy[m][co] (db may be NULL). x NHWC [B][H][W][Cin], dy [B][H][W][Cout]. */
 long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks);

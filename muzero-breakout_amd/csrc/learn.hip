@@ -90,23 +90,33 @@ __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restri
   }
 }
 
-// combine the chunks (Chan et al., in double, chunk order) -> mean, invstd, alpha = gamma*invstd,
-// beta' = beta - mean*alpha; running stats: r = momentum*stat + (1 - momentum)*r (unbiased var)
-__global__ void bn_stats_final_kernel(const float2* __restrict__ part, int nchunk, int rpc, int M, int C, float eps,
-                                      float momentum, const float* __restrict__ gamma, const float* __restrict__ beta,
-                                      float* __restrict__ stats, float* __restrict__ run_mean,
-                                      float* __restrict__ run_var) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// combine the chunks (Chan et al., in double) -> mean, invstd, alpha = gamma*invstd,
+// beta' = beta - mean*alpha; running stats: r = momentum*stat + (1 - momentum)*r (unbiased var).
+// One wave per channel: lane l folds chunks l, l+64, ...; then a fixed butterfly over the lanes.
+MZ_DEV void chan_combine(double& n, double& mean, double& m2, double nb, double mb, double m2b) {
+  if (nb == 0) return;
+  const double tot = n + nb, d = mb - mean;
+  mean += d * nb / tot;
+  m2 += m2b + d * d * n * nb / tot;
+  n = tot;
+}
+
+__global__ __launch_bounds__(64) void bn_stats_final_kernel(const float2* __restrict__ part, int nchunk, int rpc, int M,
+                                                            int C, float eps, float momentum,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float* __restrict__ stats,
+                                                            float* __restrict__ run_mean, float* __restrict__ run_var) {
+  const int c = blockIdx.x, lane = threadIdx.x;
   double n = 0, mean = 0, m2 = 0;
-  for (int k = 0; k < nchunk; ++k) {
-    const double nb = (double)min(rpc, M - k * rpc);
+  for (int k = lane; k < nchunk; k += 64) {
     const float2 p = part[(size_t)k * C + c];
-    const double d = (double)p.x - mean, tot = n + nb;
-    mean += d * nb / tot;
-    m2 += (double)p.y + d * d * n * nb / tot;
-    n = tot;
+    chan_combine(n, mean, m2, (double)min(rpc, M - k * rpc), (double)p.x, (double)p.y);
   }
+  for (int o = 1; o < 64; o <<= 1) {
+    const double n2 = __shfl_xor(n, o), mean2 = __shfl_xor(mean, o), m22 = __shfl_xor(m2, o);
+    chan_combine(n, mean, m2, n2, mean2, m22);
+  }
+  if (lane) return;
   const float var = (float)(m2 / M);
   const float invstd = (float)(1.0 / sqrt((double)var + (double)eps));
   const float alpha = invstd * gamma[c];
@@ -185,18 +195,23 @@ __global__ __launch_bounds__(256) void bn_bwd_partial_kernel(T* __restrict__ dy,
   }
 }
 
-// dgamma += dot*invstd, dbeta += sum g; coef = (mean_g, k = dot*invstd^2/N, gamma*invstd)
-__global__ void bn_bwd_final_kernel(const float2* __restrict__ part, int nchunk, int M, int C,
-                                    const float* __restrict__ stats, float* __restrict__ dgamma,
-                                    float* __restrict__ dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// dgamma += dot*invstd, dbeta += sum g; coef = (mean_g, k = dot*invstd^2/N, gamma*invstd).
+// One wave per channel, double sums, fixed butterfly order.
+__global__ __launch_bounds__(64) void bn_bwd_final_kernel(const float2* __restrict__ part, int nchunk, int M, int C,
+                                                          const float* __restrict__ stats, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x, lane = threadIdx.x;
   double sg = 0, dot = 0;
-  for (int k = 0; k < nchunk; ++k) {
+  for (int k = lane; k < nchunk; k += 64) {
     const float2 p = part[(size_t)k * C + c];
     sg += p.x;
     dot += p.y;
   }
+  for (int o = 1; o < 64; o <<= 1) {
+    sg += __shfl_xor(sg, o);
+    dot += __shfl_xor(dot, o);
+  }
+  if (lane) return;
   const float invstd = stats[C + c];
   dgamma[c] += (float)dot * invstd;
   dbeta[c] += (float)sg;
@@ -240,6 +255,47 @@ __global__ void conv_wt_kernel(const float* __restrict__ w, T* __restrict__ wt, 
       const int tap = (int)(q % taps), ci = (int)(q / taps);
       st(wt + i, w[((size_t)co * taps + (taps - 1 - tap)) * Cin + ci]);
     }
+  }
+}
+
+// bf16 weight packs for the latent / band conv kernels, straight from the f32 master weights:
+// logical W'[n][tap][c] = flip ? w[c][taps-1-tap][n] : w[n][tap][c] (n < N rows, c < Cc).
+// layout 1 (conv_lat, agent.pack_lat): out[ct][kh][tap][cc][h][r][j] = W'[32ct + r][tap][kh Cc/2 + 16cc + 8h + j];
+// layout 2 (tower / band, agent.pack_tower_conv, 3x3): out[ct][s][g][r][j] = W'[16ct + r] at
+// k' = 32s + 8g + j with taps in (dx, dy) order: q = k' / Cc, tap = (q % 3) * 3 + q / 3.
+// `pad` zero elements follow (the kernels' weight-ring overrun).
+__global__ void conv_pack_kernel(const float* __restrict__ w, bf16_t* __restrict__ out, int Cout, int taps, int Cin,
+                                 int N, int Cc, int flip, int layout, size_t pad) {
+  const size_t n_el = (size_t)N * taps * Cc;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_el + pad; i += (size_t)gridDim.x * blockDim.x) {
+    if (i >= n_el) { out[i] = 0; continue; }
+    int n, tap, c;
+    size_t q = i;
+    if (layout == 1) {
+      const int j = (int)(q % 8); q /= 8;
+      const int r = (int)(q % 32); q /= 32;
+      const int h = (int)(q % 2); q /= 2;
+      const int cc = (int)(q % (Cc / 32)); q /= (Cc / 32);
+      tap = (int)(q % taps); q /= taps;
+      const int kh = (int)(q % 2);
+      const int ct = (int)(q / 2);
+      n = 32 * ct + r;
+      c = kh * (Cc / 2) + 16 * cc + 8 * h + j;
+    } else {
+      const int j = (int)(q % 8); q /= 8;
+      const int r = (int)(q % 16); q /= 16;
+      const int g = (int)(q % 4); q /= 4;
+      const size_t nk = (size_t)taps * Cc / 32;
+      const int s_ = (int)(q % nk);
+      const int ct = (int)(q / nk);
+      n = 16 * ct + r;
+      const int k = 32 * s_ + 8 * g + j;
+      const int qq = k / Cc;
+      c = k - qq * Cc;
+      tap = (qq % 3) * 3 + qq / 3;
+    }
+    const float v = flip ? w[((size_t)c * taps + (taps - 1 - tap)) * Cin + n] : w[((size_t)n * taps + tap) * Cin + c];
+    out[i] = f32_to_bf16(v);
   }
 }
 
@@ -829,7 +885,7 @@ int mzba_bn_stats(int dtype, const void* x, int M, int C, float eps, float momen
     using T = decltype(t);
     hipLaunchKernelGGL(bn_stats_partial_kernel<T>, dim3((C + 63) / 64, nchunk), dim3(256), 0, stream, (const T*)x, M,
                        C, rpc, (float2*)ws);
-    hipLaunchKernelGGL(bn_stats_final_kernel, dim3((C + 127) / 128), dim3(128), 0, stream, (const float2*)ws, nchunk,
+    hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(64), 0, stream, (const float2*)ws, nchunk,
                        rpc, M, C, eps, momentum, gamma, beta, stats, run_mean, run_var);
     MZ_LAUNCH_CHECK();
     return 0;
@@ -860,7 +916,7 @@ int mzba_bn_backward(int dtype, void* dy, const void* y, const void* x, const fl
     using T = decltype(t);
     hipLaunchKernelGGL(bn_bwd_partial_kernel<T>, dim3((C + 63) / 64, nchunk), dim3(256), 0, stream, (T*)dy,
                        (const T*)y, (const T*)x, stats, M, C, rpc, part);
-    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3((C + 127) / 128), dim3(128), 0, stream, (const float2*)part, nchunk,
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(64), 0, stream, (const float2*)part, nchunk,
                        M, C, stats, dgamma, dbeta, coef);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for((size_t)M * C / 4)), dim3(256), 0, stream, (const T*)dy,
                        (const T*)x, stats, (const float*)coef, (T*)dx, M, C);
@@ -887,6 +943,19 @@ static long long wgrad_splits(long long M, long long tiles) {
   const long long maxs = (M + 255) / 256;        // >= 256 rows per split
   if (nsplit > maxs) nsplit = maxs;
   return nsplit < 1 ? 1 : nsplit;
+}
+
+int mzba_conv_pack_bf16(const float* w, void* out, int Cout, int taps, int Cin, int N, int Cc, int flip, int layout,
+                        long long pad, hipStream_t stream) {
+  MZ_CHECK_ARG(w && out && Cout > 0 && Cin > 0 && N > 0 && Cc > 0 && pad >= 0 && (layout == 1 || layout == 2), -1);
+  MZ_CHECK_ARG(layout != 1 || (N % 32 == 0 && Cc % 32 == 0), -2);
+  MZ_CHECK_ARG(layout != 2 || (taps == 9 && N % 16 == 0 && Cc % 32 == 0), -3);
+  MZ_CHECK_ARG(flip ? (N <= Cin && Cc == Cout) : (N == Cout && Cc <= Cin), -4);
+  const size_t n = (size_t)N * taps * Cc + (size_t)pad;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(grid_for(n)), dim3(256), 0, stream, w, (bf16_t*)out, Cout, taps, Cin, N, Cc,
+                     flip, layout, (size_t)pad);
+  MZ_LAUNCH_CHECK();
+  return 0;
 }
 
 long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks) {

@@ -29,6 +29,8 @@ from . import _lib as L
 from .env import gray_lut
 from .weights import init_state_dict, rep_layout, state_dict_spec
 
+LAT_PAD_ELEMS = 8 * 64 * 8  # conv_lat / band weight-ring overrun (agent.LAT_PAD_ELEMS)
+
 BN_EPS, BN_MOMENTUM = 1e-5, 0.1
 BETAS, ADAM_EPS, WEIGHT_DECAY = (0.9, 0.999), 1e-8, 1e-4
 
@@ -80,6 +82,8 @@ class _Conv:
             self.bn_key = prefix
         self.wt = None  # input-gradient pack
         self.wf = None  # bf16 forward pack
+        self.H = self.W = None  # spatial size the conv runs at (set by the learner)
+        self.fkind = self.dkind = "gen"  # kernels: "gen" (conv_igemm), "lat" (conv_lat), "band" (conv_band)
 
 
 class Learner:
@@ -248,10 +252,30 @@ class Learner:
         self.convs = [c for k, c in self.rep if k == "conv"] + [c for k, r in self.rep if k == "res" for c in r]
         self.convs += [self.dyn_block, self.dyn_rconv, self.pred_pconv, self.pred_vconv]
         self.convs += [c for r in self.dyn_res + self.pred_res for c in r]
+        # spatial size of every conv (representation at 16x20, then 8x10 after the first pool)
+        hh, ww = 16, 20
+        for kind, mod in self.rep:
+            if kind == "pool":
+                hh, ww = hh // 2, ww // 2
+            else:
+                for c in ([mod] if kind == "conv" else mod):
+                    c.H, c.W = hh, ww
+        for c in self.convs:
+            if c.H is None:
+                c.H, c.W = self.lat
 
     def _res(self, pre, c):
         return (_Conv(self, pre + ".bn1", c, c, 3, True, pre + ".conv1.weight", pre + ".conv1.bias"),
                 _Conv(self, pre + ".bn2", c, c, 3, True, pre + ".conv2.weight", pre + ".conv2.bias"))
+
+    def _kernel_for(self, H, W, cin, cout, ks):
+        """bf16 conv kernel for an (input channels, output channels) pair at H x W."""
+        lib = L.lib()
+        if self.dt == 1 and lib.mzba_conv_lat_supported(H, W, cin, cout, ks):
+            return "lat"
+        if self.dt == 1 and lib.mzba_conv_band_supported(H, W, cin, cout, ks):
+            return "band"
+        return "gen"
 
     # -- scratch -------------------------------------------------------------------------------
     def _scratch(self, name, nbytes):
@@ -266,30 +290,53 @@ class Learner:
 
     # -- primitive ops ----------------------------------------------------------------------------
     def _prepare_packs(self):
-        """Per-step weight packs: bf16 casts for the forward, flipped transposes for dgrad."""
+        """Per-step weight packs from the f32 master weights: bf16 forward packs (plain / conv_lat /
+        band layouts), and flipped-transposed packs for the input-gradient convs."""
         s = L.stream()
+        pad = LAT_PAD_ELEMS
         for c in self.convs:
             taps = c.ks * c.ks
+            first = c is self.rep[0][1]  # the input planes need no gradient
             cin_used = min(c.cin, self.c1) if c is self.dyn_block else c.cin_p
-            if c is self.rep[0][1]:  # the input planes need no gradient
-                if self.dt == 1 and c.wf is None:
-                    c.wf = torch.empty(c.cout, taps, c.cin_p, dtype=self.tdtype, device=self.device)
-                if self.dt == 1:
-                    L.call("mzba_conv_wpack", 1, L.ptr(c.w), L.ptr(c.wf), c.cout, taps, c.cin_p, c.cin_p, 0, s)
-                continue
             if c.wt is None:
-                c.wt = torch.empty(cin_used, taps, c.cout, dtype=self.tdtype, device=self.device)
                 if self.dt == 1:
-                    c.wf = torch.empty(c.cout, taps, c.cin_p, dtype=self.tdtype, device=self.device)
-            L.call("mzba_conv_wpack", self.dt, L.ptr(c.w), L.ptr(c.wt), c.cout, taps, c.cin_p, cin_used, 1, s)
+                    c.fkind = self._kernel_for(c.H, c.W, c.cin_p, c.cout, c.ks)
+                    n = c.cout * taps * c.cin_p + (pad if c.fkind != "gen" else 0)
+                    c.wf = torch.empty(n, dtype=self.tdtype, device=self.device)
+                if not first:
+                    c.dkind = self._kernel_for(c.H, c.W, c.cout, cin_used, c.ks)
+                    n = cin_used * taps * c.cout + (pad if c.dkind != "gen" else 0)
+                    c.wt = torch.empty(n, dtype=self.tdtype, device=self.device)
+                else:
+                    c.wt = torch.empty(0, device=self.device)
             if self.dt == 1:
-                L.call("mzba_conv_wpack", 1, L.ptr(c.w), L.ptr(c.wf), c.cout, taps, c.cin_p, c.cin_p, 0, s)
+                if c.fkind == "gen":
+                    L.call("mzba_conv_wpack", 1, L.ptr(c.w), L.ptr(c.wf), c.cout, taps, c.cin_p, c.cin_p, 0, s)
+                else:
+                    L.call("mzba_conv_pack_bf16", L.ptr(c.w), L.ptr(c.wf), c.cout, taps, c.cin_p, c.cout, c.cin_p, 0,
+                           1 if c.fkind == "lat" else 2, pad, s)
+            if first:
+                continue
+            if c.dkind == "gen":
+                L.call("mzba_conv_wpack", self.dt, L.ptr(c.w), L.ptr(c.wt), c.cout, taps, c.cin_p, cin_used, 1, s)
+            else:
+                L.call("mzba_conv_pack_bf16", L.ptr(c.w), L.ptr(c.wt), c.cout, taps, c.cin_p, cin_used, c.cout, 1,
+                       1 if c.dkind == "lat" else 2, pad, s)
+
+    def _run_conv(self, kind, x, cin, w, bias, res, out, B, H, W, cout, ks):
+        s = L.stream()
+        if kind == "lat":
+            L.call("mzba_conv_lat", L.ptr(x), H * W * cin, None, 0, L.ptr(w), L.ptr(bias), None, None, 0, L.ptr(res),
+                   L.ptr(out), B, H, W, cin, cout, ks, 0, s)
+        elif kind == "band":
+            L.call("mzba_conv_band", L.ptr(x), L.ptr(w), L.ptr(bias), L.ptr(res), L.ptr(out), B, H, W, cin, cout, 0, s)
+        else:
+            L.call("mzba_conv2d", self.dt, L.ptr(x), H * W * cin, None, 0, L.ptr(w), L.ptr(bias), None, None, 0,
+                   L.ptr(res), L.ptr(out), B, H, W, cin, cout, ks, 0, s)
 
     def _conv(self, c, x, B, H, W):
         t = self._act(B * H * W, c.cout)
-        w = c.w if self.dt == 0 else c.wf
-        L.call("mzba_conv2d", self.dt, L.ptr(x), H * W * c.cin_p, None, 0, L.ptr(w), L.ptr(c.b), None, None, 0,
-               None, L.ptr(t), B, H, W, c.cin_p, c.cout, c.ks, 0, L.stream())
+        self._run_conv(c.fkind, x, c.cin_p, c.w if self.dt == 0 else c.wf, c.b, None, t, B, H, W, c.cout, c.ks)
         return t
 
     def _bn(self, c, t, res=None, relu=True):
@@ -321,10 +368,9 @@ class Learner:
 
     def _dgrad(self, c, dy, B, H, W, acc=None):
         """Input gradient of conv c (first cin_used channels); added into `acc` when given."""
-        cu = c.wt.shape[0]
+        cu = min(c.cin, self.c1) if c is self.dyn_block else c.cin_p
         out = acc if acc is not None else self._act(B * H * W, cu)
-        L.call("mzba_conv2d", self.dt, L.ptr(dy), H * W * c.cout, None, 0, L.ptr(c.wt), L.ptr(self._zero), None,
-               None, 0, L.ptr(acc), L.ptr(out), B, H, W, c.cout, cu, c.ks, 0, L.stream())
+        self._run_conv(c.dkind, dy, c.cout, c.wt, self._zero, acc, out, B, H, W, cu, c.ks)
         return out
 
     def _linear(self, key, x, B, cin, O, out):

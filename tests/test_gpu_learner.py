@@ -266,3 +266,45 @@ def test_conv_wgrad_matches_torch(dt, shape):
     scale = ref.abs().max().item()
     assert (dw.cpu().double() - ref).abs().max().item() <= tol * scale
     assert (db.cpu().double() - refb).abs().max().item() <= tol * refb.abs().max().item() + 1e-4
+
+
+@pytest.mark.parametrize("case", [("lat", 4, 5, 256, 256, 3), ("lat", 4, 5, 256, 128, 1), ("lat", 4, 5, 128, 256, 3),
+                                  ("lat", 8, 10, 256, 256, 3), ("band", 16, 20, 128, 256, 3),
+                                  ("band", 16, 20, 256, 128, 3)])
+@pytest.mark.parametrize("flip", [0, 1])
+def test_learner_bf16_conv_packs(case, flip):
+    """mzba_conv_pack_bf16 (conv_lat / band layouts, plain and flipped-transposed) driving the
+    latent / band conv kernels: forward conv (flip 0) and input-gradient conv (flip 1) of a random
+    f32 master weight against torch in f64 on the same bf16-rounded operands."""
+    from mzba import _lib as L
+    from mzba.learner import LAT_PAD_ELEMS
+    kind, H, W, Cin, Cout, ks = case
+    B, taps = 3, ks * ks
+    g = torch.Generator().manual_seed(Cin + Cout + H + flip)
+    w = torch.randn(Cout, taps, Cin, generator=g) * 0.05            # master layout [Cout][tap][Cin]
+    N, Cc = (Cin, Cout) if flip else (Cout, Cin)                     # the pack's rows / columns
+    if not getattr(L.lib(), f"mzba_conv_{kind}_supported")(H, W, Cc, N, ks):
+        pytest.skip("shape not supported by this kernel")
+    x = torch.randn(B, H, W, Cc, generator=g).bfloat16()
+    dev = torch.device("cuda")
+    wd = w.to(dev)
+    pack = torch.empty(N * taps * Cc + LAT_PAD_ELEMS, dtype=torch.bfloat16, device=dev)
+    L.call("mzba_conv_pack_bf16", L.ptr(wd), L.ptr(pack), Cout, taps, Cin, N, Cc, flip, 1 if kind == "lat" else 2,
+           LAT_PAD_ELEMS, L.stream())
+    xd = x.to(dev)
+    out = torch.empty(B, H, W, N, dtype=torch.bfloat16, device=dev)
+    bias = torch.zeros(N, device=dev)
+    if kind == "lat":
+        L.call("mzba_conv_lat", L.ptr(xd), H * W * Cc, None, 0, L.ptr(pack), L.ptr(bias), None, None, 0, None,
+               L.ptr(out), B, H, W, Cc, N, ks, 0, L.stream())
+    else:
+        L.call("mzba_conv_band", L.ptr(xd), L.ptr(pack), L.ptr(bias), None, L.ptr(out), B, H, W, Cc, N, 0, L.stream())
+    wb = w.bfloat16().double().reshape(Cout, ks, ks, Cin).permute(0, 3, 1, 2)   # OIHW
+    xin = x.double().permute(0, 3, 1, 2)
+    if flip:
+        ref = torch.nn.grad.conv2d_input((B, Cin, H, W), wb, xin, padding=ks // 2)
+    else:
+        ref = torch.nn.functional.conv2d(xin, wb, padding=ks // 2)
+    ref = ref.permute(0, 2, 3, 1)
+    err = (out.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), (err, ref.abs().max().item())
