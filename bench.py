@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dyn-dtype", default=None, choices=[None, "fp16"], help="fp16 dynamics net (config 5)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-envs", type=int, default=16, help="bounded oracle sample (cpu_baseline + match rate)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -233,10 +234,11 @@ def run_learner(args, world, rank, local):
         dist.destroy_process_group()
 
 
-def cfg_name(B, S):
-    """Which BASELINE config an acting-loop run is (per-GPU batch and sims)."""
-    return {(1024, 50): "config 2", (4096, 50): "config 4 (per-GPU share)", (4096, 200): "config 5 (bf16)"}.get(
-        (B, S), "custom")
+def cfg_name(B, S, dyn=None):
+    """Which BASELINE config an acting-loop run is (per-GPU batch, sims, dynamics precision)."""
+    if (B, S) == (4096, 200):
+        return "config 5" if dyn == "fp16" else "config 5 geometry (bf16 dynamics)"
+    return {(1024, 50): "config 2", (4096, 50): "config 4 (per-GPU share)"}.get((B, S), "custom")
 
 
 def conv_flops(B, hw, C):
@@ -267,7 +269,7 @@ def main():
     mcfg = cfg["model"]
     B = args.envs
     sd = init_state_dict(mcfg, args.seed)
-    agent = MuZeroAgent(mcfg, dtype=args.dtype, device=f"cuda:{local}")
+    agent = MuZeroAgent(mcfg, dtype=args.dtype, device=f"cuda:{local}", dyn_dtype=args.dyn_dtype)
     agent.load_state_dict(sd)
     loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B)
     gather = TrajectoryGather(world, rank, RECORD_K, B, 16 * 20, f"cuda:{local}")
@@ -384,9 +386,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": args.dtype,
+            "dtype": args.dtype + ("; dynamics fp16" if args.dyn_dtype == "fp16" else ""),
             "data": "synthetic: seeded random-init reference-architecture nets, seeded Breakout episodes",
-            "config": {"workload": f"{cfg_name(B, args.sims)}: {B} envs/GPU x {args.sims} MCTS sims, 16x20 Breakout, "
+            "config": {"workload": f"{cfg_name(B, args.sims, args.dyn_dtype)}: {B} envs/GPU x {args.sims} MCTS sims, 16x20 Breakout, "
                                    "32-frame stack",
                        "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
                        "parallelism": f"env-sharded x{world}, RCCL all-gather of trajectory records"},

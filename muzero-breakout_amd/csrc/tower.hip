@@ -1,4 +1,4 @@
-// Fused residual tower for the dynamics / prediction nets (bf16, gfx950 MFMA).
+// Fused residual tower for the dynamics / prediction nets (bf16 or fp16, gfx950 MFMA).
 //
 // The towers are nblocks x ResidualBlock(256) on a 4x5 latent (src/networks.py:19-35,
 // 124-131, 190-197). Launching every conv separately re-stages the activations into LDS
@@ -27,7 +27,46 @@
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(8))) _Float16 f16x8;
+typedef __attribute__((ext_vector_type(2))) _Float16 f16x2;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// Element type of the LDS images and weights: EL 0 = bf16, 1 = fp16 (the fp16 dynamics net of
+// BASELINE config 5). Latents in HBM (tower input, node pool, output) stay bf16: fp16 towers
+// convert on staging and write the scaled latent back as bf16.
+template <int EL> struct Elt;
+template <> struct Elt<0> {
+  typedef bf16x8 v8;
+  static MZ_DEV f32x4 mfma(v8 a, v8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+  static MZ_DEV uint32_t pack2(float a, float b) { return pack_bf16x2(a, b); }
+  static MZ_DEV float lo(uint32_t u) { return __uint_as_float(u << 16); }
+  static MZ_DEV float hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+  static MZ_DEV uint4 from_bf16(uint4 v) { return v; }
+  static MZ_DEV uint4 to_bf16(uint4 v) { return v; }
+};
+template <> struct Elt<1> {
+  typedef f16x8 v8;
+  static MZ_DEV f32x4 mfma(v8 a, v8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+  static MZ_DEV uint32_t pack2(float a, float b) {
+    const f16x2 v = {(_Float16)a, (_Float16)b};  // round to nearest even
+    return __builtin_bit_cast(uint32_t, v);
+  }
+  static MZ_DEV float lo(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu)); }
+  static MZ_DEV float hi(uint32_t u) { return (float)__builtin_bit_cast(_Float16, (uint16_t)(u >> 16)); }
+  static MZ_DEV uint4 from_bf16(uint4 v) {
+    return make_uint4(pack2(Elt<0>::lo(v.x), Elt<0>::hi(v.x)), pack2(Elt<0>::lo(v.y), Elt<0>::hi(v.y)),
+                      pack2(Elt<0>::lo(v.z), Elt<0>::hi(v.z)), pack2(Elt<0>::lo(v.w), Elt<0>::hi(v.w)));
+  }
+  static MZ_DEV uint4 to_bf16(uint4 v) {
+    return make_uint4(pack_bf16x2(lo(v.x), hi(v.x)), pack_bf16x2(lo(v.y), hi(v.y)), pack_bf16x2(lo(v.z), hi(v.z)),
+                      pack_bf16x2(lo(v.w), hi(v.w)));
+  }
+};
+// the 8 values of a 16-B chunk of element type EL as f32
+template <int EL> MZ_DEV void unpack8(uint4 v, float (&f)[8]) {
+  f[0] = Elt<EL>::lo(v.x); f[1] = Elt<EL>::hi(v.x); f[2] = Elt<EL>::lo(v.y); f[3] = Elt<EL>::hi(v.y);
+  f[4] = Elt<EL>::lo(v.z); f[5] = Elt<EL>::hi(v.z); f[6] = Elt<EL>::lo(v.w); f[7] = Elt<EL>::hi(v.w);
+}
 
 constexpr int TE = 4;              // envs per workgroup
 constexpr int TROWS = 80;          // TE * 20 (4x5 latent)
@@ -94,7 +133,7 @@ MZ_DEV void tap_rows(int srcimg, int y, int e, int dy, int& base, int& tstride, 
 }
 
 // the 24 k steps (3 dy x 8 channel chunks) of the taps with column shift DX
-template <int DX>
+template <int EL, int DX>
 __device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int srcimg, const uint4* __restrict__ wp0,
                                          const uint4* __restrict__ wp1, uint4 (&b0q)[TD], uint4 (&b1q)[TD],
                                          f32x4 (&acc0)[TR], f32x4 (&acc1)[TR], int lane) {
@@ -105,9 +144,9 @@ __device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int sr
   const int q = lane >> 4, y = (lane & 15) >> 2, e = lane & 3;
   int base, tst, sw;
   tap_rows(srcimg + S0 * 16 * TROWB, y, e, -1, base, tst, sw);
-  bf16x8 afc[NT], afn[NT];
+  typename Elt<EL>::v8 afc[NT], afn[NT];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * tst + ((q << 4) ^ sw));
+  for (int j = 0; j < NT; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + ((q << 4) ^ sw));
   constexpr int NC = TC / 32;  // 8 k steps per tap
 #pragma unroll 1
   for (int dyi = 0; dyi < 3; ++dyi) {
@@ -116,8 +155,8 @@ __device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int sr
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int s = SB + dyi * NC + c;
-      const bf16x8 w0 = __builtin_bit_cast(bf16x8, b0q[c % TD]);
-      const bf16x8 w1 = __builtin_bit_cast(bf16x8, b1q[c % TD]);
+      const typename Elt<EL>::v8 w0 = __builtin_bit_cast(typename Elt<EL>::v8, b0q[c % TD]);
+      const typename Elt<EL>::v8 w1 = __builtin_bit_cast(typename Elt<EL>::v8, b1q[c % TD]);
 #if TOWER_ABLATE == 1  // diagnostic only: weights from one L1-resident k step
       b0q[c % TD] = wp0[(size_t)((s + TD) & 1) * 64];
       b1q[c % TD] = wp1[(size_t)((s + TD) & 1) * 64];
@@ -127,14 +166,14 @@ __device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int sr
 #endif
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        acc0[A0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, afc[j], acc0[A0 + j], 0, 0, 0);
-        acc1[A0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, afc[j], acc1[A0 + j], 0, 0, 0);
+        acc0[A0 + j] = Elt<EL>::mfma(w0, afc[j], acc0[A0 + j]);
+        acc1[A0 + j] = Elt<EL>::mfma(w1, afc[j], acc1[A0 + j]);
         if (TOWER_ABLATE == 2)  // diagnostic only: no LDS A reads inside the loop
           afn[j] = afc[j];
         else if (c + 1 < NC)
-          afn[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
         else
-          afn[j] = *reinterpret_cast<const bf16x8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
       }
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
@@ -153,28 +192,29 @@ __device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int sr
 }
 
 // the 8 k steps of a 1x1 conv (centre tap only: every row valid, all 5 tiles)
+template <int EL>
 __device__ __forceinline__ void tower_center(const uint8_t* __restrict__ lds, int srcimg, const uint4* __restrict__ wp0,
                                              const uint4* __restrict__ wp1, uint4 (&b0q)[TD], uint4 (&b1q)[TD],
                                              f32x4 (&acc0)[TR], f32x4 (&acc1)[TR], int lane) {
   const int q = lane >> 4, key = lane & 15;
   const int base = srcimg + key * TROWB, sw = key << 4;
-  bf16x8 afc[TR], afn[TR];
+  typename Elt<EL>::v8 afc[TR], afn[TR];
 #pragma unroll
-  for (int j = 0; j < TR; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
+  for (int j = 0; j < TR; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    const bf16x8 w0 = __builtin_bit_cast(bf16x8, b0q[c % TD]);
-    const bf16x8 w1 = __builtin_bit_cast(bf16x8, b1q[c % TD]);
+    const typename Elt<EL>::v8 w0 = __builtin_bit_cast(typename Elt<EL>::v8, b0q[c % TD]);
+    const typename Elt<EL>::v8 w1 = __builtin_bit_cast(typename Elt<EL>::v8, b1q[c % TD]);
     if (c + TD < 8) {
       b0q[c % TD] = wp0[(size_t)(c + TD) * 64];
       b1q[c % TD] = wp1[(size_t)(c + TD) * 64];
     }
 #pragma unroll
     for (int j = 0; j < TR; ++j) {
-      acc0[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, afc[j], acc0[j], 0, 0, 0);
-      acc1[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, afc[j], acc1[j], 0, 0, 0);
+      acc0[j] = Elt<EL>::mfma(w0, afc[j], acc0[j]);
+      acc1[j] = Elt<EL>::mfma(w1, afc[j], acc1[j]);
       if (c + 1 < 8)
-        afn[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
+        afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
     }
 #pragma unroll
     for (int j = 0; j < TR; ++j) afc[j] = afn[j];
@@ -185,7 +225,7 @@ __device__ __forceinline__ void tower_center(const uint8_t* __restrict__ lds, in
 // with `tns` k steps per tile (72: 3x3, 8: 1x1); pack column n lands on image channel nout + n.
 // MODE 0: bias; 1: bias + residual (the destination image); 2: bias + act_bias[pos][act[e]][n].
 // Epilogue: ReLU -> bf16 -> dst.
-template <int MODE, bool CENTER>
+template <int EL, int MODE, bool CENTER>
 __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg, int dstimg,
                                            const uint4* __restrict__ wconv, int tns, int ct0,
                                            const float* __restrict__ bconv, int nout,
@@ -212,10 +252,10 @@ __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg
     if (MODE == 1) {
       const uint2 x0 = *reinterpret_cast<const uint2*>(lds + dstimg + toff(row, c0 >> 3) + ((c0 & 7) << 1));
       const uint2 x1 = *reinterpret_cast<const uint2*>(lds + dstimg + toff(row, c1 >> 3) + ((c1 & 7) << 1));
-      r0[0] += __uint_as_float(x0.x << 16); r0[1] += __uint_as_float(x0.x & 0xffff0000u);
-      r0[2] += __uint_as_float(x0.y << 16); r0[3] += __uint_as_float(x0.y & 0xffff0000u);
-      r1[0] += __uint_as_float(x1.x << 16); r1[1] += __uint_as_float(x1.x & 0xffff0000u);
-      r1[2] += __uint_as_float(x1.y << 16); r1[3] += __uint_as_float(x1.y & 0xffff0000u);
+      r0[0] += Elt<EL>::lo(x0.x); r0[1] += Elt<EL>::hi(x0.x);
+      r0[2] += Elt<EL>::lo(x0.y); r0[3] += Elt<EL>::hi(x0.y);
+      r1[0] += Elt<EL>::lo(x1.x); r1[1] += Elt<EL>::hi(x1.x);
+      r1[2] += Elt<EL>::lo(x1.y); r1[3] += Elt<EL>::hi(x1.y);
     } else if (MODE == 2) {
       const float* t = actb + ((size_t)((l16 >> 2) * 5 + rt) * A + acts[l16 & 3]) * TC;
       const float4 t0 = *reinterpret_cast<const float4*>(t + n0), t1 = *reinterpret_cast<const float4*>(t + n1);
@@ -226,20 +266,20 @@ __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg
     acc1[rt] = r1;
   }
   if (CENTER) {
-    tower_center(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+    tower_center<EL>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
   } else {
-    tower_dx<-1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
-    tower_dx<0>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
-    tower_dx<1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+    tower_dx<EL, -1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+    tower_dx<EL, 0>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
+    tower_dx<EL, 1>(lds, srcimg, wp0, wp1, b0q, b1q, acc0, acc1, lane);
   }
 #pragma unroll
   for (int rt = 0; rt < TR; ++rt) {
     const int row = rt * 16 + l16;
     uint2 o0, o1;
-    o0.x = pack_bf16x2(fmaxf(acc0[rt][0], 0.f), fmaxf(acc0[rt][1], 0.f));
-    o0.y = pack_bf16x2(fmaxf(acc0[rt][2], 0.f), fmaxf(acc0[rt][3], 0.f));
-    o1.x = pack_bf16x2(fmaxf(acc1[rt][0], 0.f), fmaxf(acc1[rt][1], 0.f));
-    o1.y = pack_bf16x2(fmaxf(acc1[rt][2], 0.f), fmaxf(acc1[rt][3], 0.f));
+    o0.x = Elt<EL>::pack2(fmaxf(acc0[rt][0], 0.f), fmaxf(acc0[rt][1], 0.f));
+    o0.y = Elt<EL>::pack2(fmaxf(acc0[rt][2], 0.f), fmaxf(acc0[rt][3], 0.f));
+    o1.x = Elt<EL>::pack2(fmaxf(acc1[rt][0], 0.f), fmaxf(acc1[rt][1], 0.f));
+    o1.y = Elt<EL>::pack2(fmaxf(acc1[rt][2], 0.f), fmaxf(acc1[rt][3], 0.f));
     *reinterpret_cast<uint2*>(lds + dstimg + toff(row, c0 >> 3) + ((c0 & 7) << 1)) = o0;
     *reinterpret_cast<uint2*>(lds + dstimg + toff(row, c1 >> 3) + ((c1 & 7) << 1)) = o1;
   }
@@ -250,7 +290,7 @@ __device__ __forceinline__ void tower_conv(uint8_t* __restrict__ lds, int srcimg
 // order against bf16 weights lw[h][16][K]. One v_mfma_f32_16x16x32_bf16 per 32-deep k step
 // (A rows = the 4 envs, zero-padded to 16; B cols = outputs), k steps split over the 8 waves,
 // partial sums added through LDS in wave order; then softmax (dec_kind 0) or support decode (1).
-template <int NE, int NW, bool R8>
+template <int EL, int NE, int NW, bool R8>
 __device__ __forceinline__ void tower_heads(const TowerArgs& a, const uint8_t* __restrict__ lds, int img,
                                             int nh, const int (&hc0)[2], const int (&hC)[2], const int (&kind)[2],
                                             float* part, float* lg, float (*dec)[8][4], int env0, int nenv,
@@ -266,10 +306,10 @@ __device__ __forceinline__ void tower_heads(const TowerArgs& a, const uint8_t* _
       const int k = s * 32 + q * 8;
       const int pos = k / C, c = hc0[hd] + (k - pos * C);
       const int row = R8 ? t8::row8(er, pos) : trow(er, pos);
-      bf16x8 av = *reinterpret_cast<const bf16x8*>(lds + img + toff(row, c >> 3));
-      if (el >= NE) av = bf16x8{};
-      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(wr + k);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+      typename Elt<EL>::v8 av = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + img + toff(row, c >> 3));
+      if (el >= NE) av = typename Elt<EL>::v8{};
+      const typename Elt<EL>::v8 bv = *reinterpret_cast<const typename Elt<EL>::v8*>(wr + k);
+      acc = Elt<EL>::mfma(av, bv, acc);
     }
     if (4 * q < NE)  // D[row = env 4q + i][col = output el]
 #pragma unroll
@@ -314,6 +354,7 @@ __device__ __forceinline__ void tower_heads(const TowerArgs& a, const uint8_t* _
 
 // _scale_state (networks.py:314-328) of the tower output X: per env (h - min) / (max - min + 1e-8)
 // in f32, bf16 result to out (and to the pool slot). 128 threads per env, 5 chunks each.
+template <int EL>
 __device__ __forceinline__ void tower_scale(const TowerArgs& a, const uint8_t* __restrict__ lds, float (*mm)[2][2],
                                             int env0, int nenv, int tid) {
   const int e = tid >> 7, t = tid & 127;
@@ -323,9 +364,10 @@ __device__ __forceinline__ void tower_scale(const TowerArgs& a, const uint8_t* _
   for (int u = 0; u < 5; ++u) {
     const int i = u * 128 + t, p = i >> 5, c = i & 31;
     v[u] = *reinterpret_cast<const uint4*>(lds + LDS_X + toff(trow(e, p), c));
-    const bf16_t* h = reinterpret_cast<const bf16_t*>(&v[u]);
+    float f[8];
+    unpack8<EL>(v[u], f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { const float f = bf16_to_f32(h[j]); mn = fminf(mn, f); mx = fmaxf(mx, f); }
+    for (int j = 0; j < 8; ++j) { mn = fminf(mn, f[j]); mx = fmaxf(mx, f[j]); }
   }
   for (int o = 32; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
   if ((t & 63) == 0) { mm[e][t >> 6][0] = mn; mm[e][t >> 6][1] = mx; }
@@ -342,15 +384,16 @@ __device__ __forceinline__ void tower_scale(const TowerArgs& a, const uint8_t* _
 #pragma unroll
   for (int u = 0; u < 5; ++u) {
     const int i = u * 128 + t, p = i >> 5, c = i & 31;
-    uint4 r = v[u];
-    bf16_t* h = reinterpret_cast<bf16_t*>(&r);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) h[j] = f32_to_bf16((bf16_to_f32(h[j]) - mn) / den);
+    float f[8];
+    unpack8<EL>(v[u], f);
+    const uint4 r = make_uint4(pack_bf16x2((f[0] - mn) / den, (f[1] - mn) / den), pack_bf16x2((f[2] - mn) / den, (f[3] - mn) / den),
+                               pack_bf16x2((f[4] - mn) / den, (f[5] - mn) / den), pack_bf16x2((f[6] - mn) / den, (f[7] - mn) / den));
     *reinterpret_cast<uint4*>(o1 + p * TC + c * 8) = r;
     if (o2) *reinterpret_cast<uint4*>(o2 + p * TC + c * 8) = r;
   }
 }
 
+template <int EL>
 __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];  // X | T | 16 zero rows
   __shared__ long long envoff[TE];
@@ -382,7 +425,7 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
       const int r = i >> 5, c = i & 31;
       const bool ok = r < rows;
       const int rr = ok ? r : 0;
-      v[u] = *reinterpret_cast<const uint4*>(a.in + envoff[rr / 20] + (long long)(rr % 20) * TC + c * 8);
+      v[u] = Elt<EL>::from_bf16(*reinterpret_cast<const uint4*>(a.in + envoff[rr / 20] + (long long)(rr % 20) * TC + c * 8));
       if (!ok) v[u] = make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -395,7 +438,7 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
   }
   __syncthreads();
   if (pro) {  // dynamics ConvBlock: T -> X
-    tower_conv<2, false>(lds, LDS_T, LDS_X, reinterpret_cast<const uint4*>(a.x.w0), TNS, 2 * wave, a.x.b0, 0,
+    tower_conv<EL, 2, false>(lds, LDS_T, LDS_X, reinterpret_cast<const uint4*>(a.x.w0), TNS, 2 * wave, a.x.b0, 0,
                          a.x.act_bias, acts, a.x.A, lane);
     __syncthreads();
   }
@@ -405,35 +448,35 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
 #if TOWER_ABLATE == 4  // diagnostic: the duplicate-stream waves trail by ~1 k step so their loads hit L1
     if (wave >= 4) __builtin_amdgcn_s_sleep(6);
 #endif
-    tower_conv<0, false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, TNS, TOWER_CT0(wave), a.bias + (2 * blk) * TC, 0,
+    tower_conv<EL, 0, false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, TNS, TOWER_CT0(wave), a.bias + (2 * blk) * TC, 0,
                          nullptr, nullptr, 0, lane);
     __syncthreads();
 #if TOWER_ABLATE == 4
     if (wave >= 4) __builtin_amdgcn_s_sleep(6);
 #endif
-    tower_conv<1, false>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, TNS, TOWER_CT0(wave),
+    tower_conv<EL, 1, false>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, TNS, TOWER_CT0(wave),
                          a.bias + (2 * blk + 1) * TC, 0, nullptr, nullptr, 0, lane);
     __syncthreads();
   }
   if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1 (X -> T), Linear + decode, scaled latent
-    tower_conv<0, true>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we1), 8, 2 * wave, a.x.be1, 0,
+    tower_conv<EL, 0, true>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we1), 8, 2 * wave, a.x.be1, 0,
                         nullptr, nullptr, 0, lane);
     __syncthreads();
     const int hc0[2] = {0, 0}, hC[2] = {TC, 0}, kind[2] = {1, 0};
-    tower_heads<TE, 8, false>(a, lds, LDS_T, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
-    tower_scale(a, lds, reinterpret_cast<float(*)[2][2]>(part), env0, nenv, tid);
+    tower_heads<EL, TE, 8, false>(a, lds, LDS_T, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    tower_scale<EL>(a, lds, reinterpret_cast<float(*)[2][2]>(part), env0, nenv, tid);
     return;
   }
   if (a.x.epilogue == 2) {  // prediction: policy 3x3 -> T[0,128), value 1x1 -> T[128,256); Linears
     if (wave < 4)
-      tower_conv<0, false>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we3), TNS, 2 * wave, a.x.be3, 0,
+      tower_conv<EL, 0, false>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we3), TNS, 2 * wave, a.x.be3, 0,
                            nullptr, nullptr, 0, lane);
     else
-      tower_conv<0, true>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we1), 8, 2 * (wave - 4), a.x.be1,
+      tower_conv<EL, 0, true>(lds, LDS_X, LDS_T, reinterpret_cast<const uint4*>(a.x.we1), 8, 2 * (wave - 4), a.x.be1,
                           128, nullptr, nullptr, 0, lane);
     __syncthreads();
     const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
-    tower_heads<TE, 8, false>(a, lds, LDS_T, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    tower_heads<EL, TE, 8, false>(a, lds, LDS_T, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
       __syncthreads();
       if (tid < nenv) {
@@ -451,7 +494,7 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
     const int r = i >> 5, c = i & 31;
     if (r < rows)
       *reinterpret_cast<uint4*>(a.out + (long long)(env0 + r / 20) * 20 * TC + (r % 20) * TC + c * 8) =
-          *reinterpret_cast<const uint4*>(lds + LDS_X + toff(trow(r / 20, r % 20), c));
+          Elt<EL>::to_bf16(*reinterpret_cast<const uint4*>(lds + LDS_X + toff(trow(r / 20, r % 20), c)));
   }
 }
 
@@ -464,7 +507,7 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
 // One activation image: a conv reads it whole, then (after a barrier) its output overwrites it in
 // place; conv1 first lifts the block input at its own output positions into registers (the residual).
 
-template <int DX>
+template <int EL, int DX>
 __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
                                           uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[t8::NRT][t8::CT], int lane) {
   constexpr int NX = DX == 0 ? 5 : 4;   // active x tiles per env quad
@@ -477,9 +520,9 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
   tap_rows(S0 * 16 * TROWB, y, e, -1, base, tst, sw);
   // active tile j: quad j / NX, x tile j % NX -> source tile index (in 16-row tiles from S0)
   auto soff = [&](int j, int b, int ts) { return b + ((j / NX) * 5 + (j % NX)) * ts; };
-  bf16x8 afc[NA], afn[NA];
+  typename Elt<EL>::v8 afc[NA], afn[NA];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + soff(j, base, tst) + ((q << 4) ^ sw));
+  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, base, tst) + ((q << 4) ^ sw));
   constexpr int NC = TC / 32;
 #pragma unroll 1
   for (int dyi = 0; dyi < 3; ++dyi) {
@@ -488,10 +531,10 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int s = SB + dyi * NC + c;
-      bf16x8 w[t8::CT];
+      typename Elt<EL>::v8 w[t8::CT];
 #pragma unroll
       for (int ct = 0; ct < t8::CT; ++ct) {
-        w[ct] = __builtin_bit_cast(bf16x8, bq[ct][c % TD]);
+        w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
         bq[ct][c % TD] = wp[ct][(size_t)(s + TD) * 64];
       }
 #pragma unroll
@@ -499,11 +542,11 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
         const int at = (j / NX) * 5 + A0 + (j % NX);
 #pragma unroll
         for (int ct = 0; ct < t8::CT; ++ct)
-          acc[at][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[ct], afc[j], acc[at][ct], 0, 0, 0);
+          acc[at][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[at][ct]);
         if (c + 1 < NC)
-          afn[j] = *reinterpret_cast<const bf16x8*>(lds + soff(j, base, tst) + (((4 * (c + 1) + q) << 4) ^ sw));
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, base, tst) + (((4 * (c + 1) + q) << 4) ^ sw));
         else
-          afn[j] = *reinterpret_cast<const bf16x8*>(lds + soff(j, nbase, ntst) + ((q << 4) ^ nsw));
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, nbase, ntst) + ((q << 4) ^ nsw));
       }
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
@@ -522,28 +565,29 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 }
 
 // the 8 k steps of a 1x1 conv on the 8-env image (centre tap: all 10 tiles, every row valid)
+template <int EL>
 __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
                                               uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[t8::NRT][t8::CT], int lane) {
   const int q = lane >> 4, key = lane & 15;
   const int base = key * TROWB, sw = key << 4;
-  bf16x8 afc[t8::NRT], afn[t8::NRT];
+  typename Elt<EL>::v8 afc[t8::NRT], afn[t8::NRT];
 #pragma unroll
-  for (int j = 0; j < t8::NRT; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
+  for (int j = 0; j < t8::NRT; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    bf16x8 w[t8::CT];
+    typename Elt<EL>::v8 w[t8::CT];
 #pragma unroll
     for (int ct = 0; ct < t8::CT; ++ct) {
-      w[ct] = __builtin_bit_cast(bf16x8, bq[ct][c % TD]);
+      w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
       if (c + TD < 8) bq[ct][c % TD] = wp[ct][(size_t)(c + TD) * 64];
     }
 #pragma unroll
     for (int j = 0; j < t8::NRT; ++j) {
 #pragma unroll
       for (int ct = 0; ct < t8::CT; ++ct)
-        acc[j][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[ct], afc[j], acc[j][ct], 0, 0, 0);
+        acc[j][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[j][ct]);
       if (c + 1 < 8)
-        afn[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
+        afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
     }
 #pragma unroll
     for (int j = 0; j < t8::NRT; ++j) afc[j] = afn[j];
@@ -553,7 +597,7 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
 // k loop of one conv over the 8-env image: this wave's 4 channel tiles ct0..ct0+3 of a weight pack
 // with `tns` k steps per tile (72: 3x3, 8: 1x1). D[pack channel 16 ct + 4q + i][row 16 rt + l16].
 // MODE 0: acc starts at bias; 1: bias + res (registers); 2: bias + act_bias[pos][act[env]].
-template <int MODE, bool CENTER>
+template <int EL, int MODE, bool CENTER>
 __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const uint4* __restrict__ wconv, int tns,
                                            int ct0, const float* __restrict__ bconv, const float* __restrict__ actb,
                                            const int* acts, int A, const uint2 (&res)[t8::NRT][t8::CT],
@@ -576,8 +620,8 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
       f32x4 v = {b4.x, b4.y, b4.z, b4.w};
       if (MODE == 1) {
         const uint2 r = res[rt][ct];
-        v[0] += __uint_as_float(r.x << 16); v[1] += __uint_as_float(r.x & 0xffff0000u);
-        v[2] += __uint_as_float(r.y << 16); v[3] += __uint_as_float(r.y & 0xffff0000u);
+        v[0] += Elt<EL>::lo(r.x); v[1] += Elt<EL>::hi(r.x);
+        v[2] += Elt<EL>::lo(r.y); v[3] += Elt<EL>::hi(r.y);
       } else if (MODE == 2) {  // row -> env quad rt / 5, latent x = rt % 5, y = l16 >> 2, env l16 & 3
         const int env = (rt / 5) * 4 + (l16 & 3), pos = (l16 >> 2) * 5 + rt % 5;
         const float4 t = *reinterpret_cast<const float4*>(actb + ((size_t)pos * A + acts[env]) * TC + n);
@@ -587,17 +631,17 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
     }
   }
   if (CENTER) {
-    tower8_center(lds, wp, bq, acc, lane);
+    tower8_center<EL>(lds, wp, bq, acc, lane);
   } else {
-    tower8_dx<-1>(lds, wp, bq, acc, lane);
-    tower8_dx<0>(lds, wp, bq, acc, lane);
-    tower8_dx<1>(lds, wp, bq, acc, lane);
+    tower8_dx<EL, -1>(lds, wp, bq, acc, lane);
+    tower8_dx<EL, 0>(lds, wp, bq, acc, lane);
+    tower8_dx<EL, 1>(lds, wp, bq, acc, lane);
   }
 }
 
 // ReLU -> bf16 -> the image at channel nout + 16 (ct0 + ct) + 4q (8-byte stores, in place after a
 // barrier); SAVE: first lift the image's values there into res (the block input = conv2's residual)
-template <bool SAVE>
+template <int EL, bool SAVE>
 __device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, const f32x4 (&acc)[t8::NRT][t8::CT],
                                                  uint2 (&res)[t8::NRT][t8::CT], int nout, int ct0, int lane) {
   const int q = lane >> 4, l16 = lane & 15;
@@ -609,13 +653,14 @@ __device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, cons
       uint2* p = reinterpret_cast<uint2*>(lds + toff(rt * 16 + l16, n >> 3) + ((n & 7) << 1));
       if (SAVE) res[rt][ct] = *p;
       uint2 o;
-      o.x = pack_bf16x2(fmaxf(acc[rt][ct][0], 0.f), fmaxf(acc[rt][ct][1], 0.f));
-      o.y = pack_bf16x2(fmaxf(acc[rt][ct][2], 0.f), fmaxf(acc[rt][ct][3], 0.f));
+      o.x = Elt<EL>::pack2(fmaxf(acc[rt][ct][0], 0.f), fmaxf(acc[rt][ct][1], 0.f));
+      o.y = Elt<EL>::pack2(fmaxf(acc[rt][ct][2], 0.f), fmaxf(acc[rt][ct][3], 0.f));
       *p = o;
     }
 }
 
 // _scale_state over the 8-env image: 32 threads per env, 20 chunks each; bf16 to out (+ pool slot)
+template <int EL>
 __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* __restrict__ lds, int env0, int nenv,
                                              int tid) {
   const int e = tid >> 5, t = tid & 31;
@@ -623,9 +668,10 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
   for (int u = 0; u < 20; ++u) {
     const int i = u * 32 + t, p = i >> 5, c = i & 31;
     const uint4 v = *reinterpret_cast<const uint4*>(lds + toff(t8::row8(e, p), c));
-    const bf16_t* h = reinterpret_cast<const bf16_t*>(&v);
+    float f[8];
+    unpack8<EL>(v, f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { const float f = bf16_to_f32(h[j]); mn = fminf(mn, f); mx = fmaxf(mx, f); }
+    for (int j = 0; j < 8; ++j) { mn = fminf(mn, f[j]); mx = fmaxf(mx, f[j]); }
   }
   for (int o = 16; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
   if (e >= nenv) return;
@@ -637,27 +683,28 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
                         : nullptr;
   for (int u = 0; u < 20; ++u) {
     const int i = u * 32 + t, p = i >> 5, c = i & 31;
-    uint4 r = *reinterpret_cast<const uint4*>(lds + toff(t8::row8(e, p), c));
-    bf16_t* h = reinterpret_cast<bf16_t*>(&r);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) h[j] = f32_to_bf16((bf16_to_f32(h[j]) - mn) / den);
+    float f[8];
+    unpack8<EL>(*reinterpret_cast<const uint4*>(lds + toff(t8::row8(e, p), c)), f);
+    const uint4 r = make_uint4(pack_bf16x2((f[0] - mn) / den, (f[1] - mn) / den), pack_bf16x2((f[2] - mn) / den, (f[3] - mn) / den),
+                               pack_bf16x2((f[4] - mn) / den, (f[5] - mn) / den), pack_bf16x2((f[6] - mn) / den, (f[7] - mn) / den));
     *reinterpret_cast<uint4*>(o1 + p * TC + c * 8) = r;
     if (o2) *reinterpret_cast<uint4*>(o2 + p * TC + c * 8) = r;
   }
 }
 
 // one residual-tower conv (in place): k loop, barrier, write back, barrier
-template <bool RESID>
+template <int EL, bool RESID>
 __device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const uint4* __restrict__ wconv,
                                             const float* __restrict__ bconv, uint2 (&res)[t8::NRT][t8::CT],
                                             int lane, int wave) {
   f32x4 acc[t8::NRT][t8::CT];
-  tower8_acc<RESID ? 1 : 0, false>(lds, wconv, TNS, wave * t8::CT, bconv, nullptr, nullptr, 0, res, acc, lane);
+  tower8_acc<EL, RESID ? 1 : 0, false>(lds, wconv, TNS, wave * t8::CT, bconv, nullptr, nullptr, 0, res, acc, lane);
   __syncthreads();  // every wave has read the whole image
-  tower8_writeback<!RESID>(lds, acc, res, 0, wave * t8::CT, lane);
+  tower8_writeback<EL, !RESID>(lds, acc, res, 0, wave * t8::CT, lane);
   __syncthreads();
 }
 
+template <int EL>
 __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[t8::BYTES];
   __shared__ long long envoff[t8::E];
@@ -688,7 +735,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
         const int r = i >> 5, c = i & 31;
         const bool ok = r < rows;
         const int rr = ok ? r : 0;
-        v[u] = *reinterpret_cast<const uint4*>(a.in + envoff[rr / 20] + (long long)(rr % 20) * TC + c * 8);
+        v[u] = Elt<EL>::from_bf16(*reinterpret_cast<const uint4*>(a.in + envoff[rr / 20] + (long long)(rr % 20) * TC + c * 8));
         if (!ok) v[u] = make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
@@ -705,45 +752,45 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   uint2 res[t8::NRT][t8::CT];
   if (pro) {  // dynamics ConvBlock (in place)
     f32x4 acc[t8::NRT][t8::CT];
-    tower8_acc<2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), TNS, wave * t8::CT, a.x.b0, a.x.act_bias, acts,
+    tower8_acc<EL, 2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), TNS, wave * t8::CT, a.x.b0, a.x.act_bias, acts,
                          a.x.A, res, acc, lane);
     __syncthreads();
-    tower8_writeback<false>(lds, acc, res, 0, wave * t8::CT, lane);
+    tower8_writeback<EL, false>(lds, acc, res, 0, wave * t8::CT, lane);
     __syncthreads();
   }
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;
   for (int blk = 0; blk < a.nblocks; ++blk) {
-    tower8_conv<false>(lds, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, res, lane, wave);
-    tower8_conv<true>(lds, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, res, lane, wave);
+    tower8_conv<EL, false>(lds, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, res, lane, wave);
+    tower8_conv<EL, true>(lds, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, res, lane, wave);
   }
   if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1, the scaled latent from X, then Linear + decode
     f32x4 acc[t8::NRT][t8::CT];
-    tower8_acc<0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, wave * t8::CT, a.x.be1, nullptr, nullptr, 0,
+    tower8_acc<EL, 0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, wave * t8::CT, a.x.be1, nullptr, nullptr, 0,
                         res, acc, lane);
     __syncthreads();
-    tower8_scale(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
+    tower8_scale<EL>(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
     __syncthreads();
-    tower8_writeback<false>(lds, acc, res, 0, wave * t8::CT, lane);
+    tower8_writeback<EL, false>(lds, acc, res, 0, wave * t8::CT, lane);
     __syncthreads();
     const int hc0[2] = {0, 0}, hC[2] = {TC, 0}, kind[2] = {1, 0};
-    tower_heads<t8::E, 4, true>(a, lds, 0, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    tower_heads<EL, t8::E, 4, true>(a, lds, 0, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     return;
   }
   if (a.x.epilogue == 2) {  // prediction: policy 3x3 (waves 0-1) -> [0,128), value 1x1 (waves 2-3) -> [128,256)
     f32x4 acc[t8::NRT][t8::CT];
     const int ct0 = (wave & 1) * t8::CT;
     if (wave < 2)
-      tower8_acc<0, false>(lds, reinterpret_cast<const uint4*>(a.x.we3), TNS, ct0, a.x.be3, nullptr, nullptr, 0, res,
+      tower8_acc<EL, 0, false>(lds, reinterpret_cast<const uint4*>(a.x.we3), TNS, ct0, a.x.be3, nullptr, nullptr, 0, res,
                            acc, lane);
     else
-      tower8_acc<0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, ct0, a.x.be1, nullptr, nullptr, 0, res, acc,
+      tower8_acc<EL, 0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, ct0, a.x.be1, nullptr, nullptr, 0, res, acc,
                           lane);
     __syncthreads();
-    tower8_writeback<false>(lds, acc, res, wave < 2 ? 0 : 128, ct0, lane);
+    tower8_writeback<EL, false>(lds, acc, res, wave < 2 ? 0 : 128, ct0, lane);
     __syncthreads();
     const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
-    tower_heads<t8::E, 4, true>(a, lds, 0, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    tower_heads<EL, t8::E, 4, true>(a, lds, 0, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
       __syncthreads();
       if (tid < nenv) {
@@ -760,7 +807,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     const int r = i >> 5, c = i & 31;
     if (r < rows)
       *reinterpret_cast<uint4*>(a.out + (long long)(env0 + r / 20) * 20 * TC + (r % 20) * TC + c * 8) =
-          *reinterpret_cast<const uint4*>(lds + toff(t8::row8(r / 20, r % 20), c));
+          Elt<EL>::to_bf16(*reinterpret_cast<const uint4*>(lds + toff(t8::row8(r / 20, r % 20), c)));
   }
 }
 
@@ -813,9 +860,9 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
   (void)ws;
   (void)ws_bytes;
   if (plan == 2) {
-    hipLaunchKernelGGL(tower8_kernel, dim3((B + t8::E - 1) / t8::E), dim3(t8::NT), 0, stream, a);
+    hipLaunchKernelGGL(tower8_kernel<0>, dim3((B + t8::E - 1) / t8::E), dim3(t8::NT), 0, stream, a);
   } else {
-    hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
+    hipLaunchKernelGGL(tower_kernel<0>, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
   }
   MZ_LAUNCH_CHECK();
   return 0;
@@ -829,7 +876,7 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
   const int plan = mzba_tower_plan(B);
   MZ_CHECK_ARG(plan == 1 || plan == 2, -4);
   const mzba_tower_ext& x = *ext;
-  MZ_CHECK_ARG(x.epilogue >= 0 && x.epilogue <= 2, -2);
+  MZ_CHECK_ARG(x.epilogue >= 0 && x.epilogue <= 2 && (x.elem == 0 || x.elem == 1), -2);
   MZ_CHECK_ARG(!x.w0 || (x.b0 && x.act_bias && x.act && x.A > 0), -3);
   MZ_CHECK_ARG(x.epilogue != 0 || out, -3);
   MZ_CHECK_ARG(x.epilogue != 1 || (out && x.we1 && x.be1 && x.lw[0] && x.lb[0] && x.dec[0] && x.lO[0] > 1 &&
@@ -849,10 +896,14 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
     a.tree_gamma = t.gamma;
     a.tree_r = t.r;
   }
-  if (plan == 2)
-    hipLaunchKernelGGL(tower8_kernel, dim3((B + t8::E - 1) / t8::E), dim3(t8::NT), 0, stream, a);
-  else
-    hipLaunchKernelGGL(tower_kernel, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
+  const dim3 g8((B + t8::E - 1) / t8::E), g4((B + TE - 1) / TE);
+  if (x.elem == 1) {
+    if (plan == 2) hipLaunchKernelGGL(tower8_kernel<1>, g8, dim3(t8::NT), 0, stream, a);
+    else hipLaunchKernelGGL(tower_kernel<1>, g4, dim3(TNT), 0, stream, a);
+  } else {
+    if (plan == 2) hipLaunchKernelGGL(tower8_kernel<0>, g8, dim3(t8::NT), 0, stream, a);
+    else hipLaunchKernelGGL(tower_kernel<0>, g4, dim3(TNT), 0, stream, a);
+  }
   MZ_LAUNCH_CHECK();
   return 0;
 }

@@ -58,8 +58,11 @@ def _round64(c):
 class PackedNets:
     """Device-resident packed weights for one precision."""
 
-    def __init__(self, sd, mcfg, dtype, device):
+    def __init__(self, sd, mcfg, dtype, device, dyn_dtype=None):
         self.mcfg, self.dtype, self.device = mcfg, dtype, device
+        if dyn_dtype not in (None, dtype, "fp16") or (dyn_dtype == "fp16" and dtype != "bf16"):
+            raise ValueError("dyn_dtype: None / the net dtype, or 'fp16' with dtype 'bf16'")
+        self.dyn_fp16 = dyn_dtype == "fp16"  # BASELINE config 5: fp16 dynamics net (fused step only)
         self.tdt = TORCH_DT[dtype]
         self.c0, self.c1 = mcfg["latent_channels"]
         self.L = mcfg["state_history_length"]
@@ -118,12 +121,13 @@ class PackedNets:
         def dev(x, dt=None):
             return torch.tensor(np.asarray(x), dtype=torch.float32).to(dt or torch.float32).to(self.device)
 
-        def pack3(cw):
-            return dev(np.concatenate([pack_tower_conv(cw), np.zeros(LAT_PAD_ELEMS)]), self.tdt)
+        def pack3(cw, dt=None):
+            return dev(np.concatenate([pack_tower_conv(cw), np.zeros(LAT_PAD_ELEMS)]), dt or self.tdt)
 
-        def pack1(cw):
+        def pack1(cw, dt=None):
             co, ci = cw.shape[:2]
-            return dev(np.concatenate([pack_lat16(cw.reshape(co, ci), co, 1, ci), np.zeros(LAT_PAD_ELEMS)]), self.tdt)
+            return dev(np.concatenate([pack_lat16(cw.reshape(co, ci), co, 1, ci), np.zeros(LAT_PAD_ELEMS)]),
+                       dt or self.tdt)
 
         a0, b0 = self._bn(sd, "dyn_net.conv_block.bn")
         rw, rb = fold(sd["dyn_net.reward_head.0.conv.weight"], sd["dyn_net.reward_head.0.conv.bias"],
@@ -132,9 +136,18 @@ class PackedNets:
                       "pred_net.policy_head.0.bn")
         vw, vb = fold(sd["pred_net.value_head.0.conv.weight"], sd["pred_net.value_head.0.conv.bias"],
                       "pred_net.value_head.0.bn")
-        return {"w0": pack3(w0 * a0[:, None, None, None]), "b0": self.dyn0["b"], "act_bias": self.dyn0["act_bias"],
-                "A": self.dyn0["A"], "rw": pack1(rw), "rb": dev(rb), "pw": pack3(pw), "pb": dev(pb),
-                "vw": pack1(vw), "vb": dev(vb)}
+        out = {"w0": pack3(w0 * a0[:, None, None, None]), "b0": self.dyn0["b"], "act_bias": self.dyn0["act_bias"],
+               "A": self.dyn0["A"], "rw": pack1(rw), "rb": dev(rb), "pw": pack3(pw), "pb": dev(pb),
+               "vw": pack1(vw), "vb": dev(vb)}
+        if self.dyn_fp16:  # the dynamics step's fp16 weights (tower packs: tower_weights(..., fp16=True))
+            w = sd["dyn_net.reward_head.2.weight"]  # the reward Linear in the heads' (position, channel) order
+            O, K = w.shape
+            lw = np.zeros((16, K))
+            lw[:O] = w.reshape(O, self.c1, K // self.c1).transpose(0, 2, 1).reshape(O, K)
+            lw = dev(lw, torch.float16)
+            out["dyn16"] = {"w0": pack3(w0 * a0[:, None, None, None], torch.float16), "rw": pack1(rw, torch.float16),
+                            "lw": lw}
+        return out
 
     # -- packing helpers ---------------------------------------------------------------
     @staticmethod
@@ -199,12 +212,13 @@ class PackedNets:
         return {"w": ws, "wf": {}, "n": n,
                 "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device)}
 
-    def tower_weights(self, tw, plan):
-        """Device weights of a tower in the packing of mzba_tower's plan (cached per plan)."""
-        if plan not in tw["wf"]:
+    def tower_weights(self, tw, plan, fp16=False):
+        """Device weights of a tower in the packing of mzba_tower's plan (cached per plan and dtype)."""
+        key = (plan, fp16)
+        if key not in tw["wf"]:
             wf = np.concatenate([pack_tower_conv(w) for w in tw["w"]] + [np.zeros(LAT_PAD_ELEMS)])
-            tw["wf"][plan] = torch.tensor(wf, dtype=torch.float32).to(self.tdt).to(self.device)
-        return tw["wf"][plan]
+            tw["wf"][key] = torch.tensor(wf, dtype=torch.float32).to(torch.float16 if fp16 else self.tdt).to(self.device)
+        return tw["wf"][key]
 
     def _linear(self, w, b, c):
         O, K = w.shape
@@ -336,9 +350,11 @@ class NetRunner:
         x.epilogue = epilogue
         x.smin, x.smax = float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"])
         if epilogue == 1:
-            x.w0, x.b0, x.act_bias, x.A = L.ptr(f["w0"]), L.ptr(f["b0"]), L.ptr(f["act_bias"]), f["A"]
-            x.we1, x.be1 = L.ptr(f["rw"]), L.ptr(f["rb"])
-            x.lw[0], x.lb[0], x.lO[0] = L.ptr(p.rew_lin["wb"]), L.ptr(p.rew_lin["b"]), p.rew_lin["O"]
+            d16 = f.get("dyn16")
+            x.w0, x.b0, x.act_bias, x.A = L.ptr(d16["w0"] if d16 else f["w0"]), L.ptr(f["b0"]), L.ptr(f["act_bias"]), f["A"]
+            x.we1, x.be1 = L.ptr(d16["rw"] if d16 else f["rw"]), L.ptr(f["rb"])
+            x.lw[0], x.lb[0], x.lO[0] = L.ptr(d16["lw"] if d16 else p.rew_lin["wb"]), L.ptr(p.rew_lin["b"]), p.rew_lin["O"]
+            x.elem = 1 if d16 else 0
         else:
             x.we3, x.be3, x.we1, x.be1 = L.ptr(f["pw"]), L.ptr(f["pb"]), L.ptr(f["vw"]), L.ptr(f["vb"])
             x.lw[0], x.lb[0], x.lO[0] = L.ptr(p.pol_lin["wb"]), L.ptr(p.pol_lin["b"]), p.pol_lin["O"]
@@ -350,7 +366,7 @@ class NetRunner:
         if pr is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        wf = self.p.tower_weights(tw, self.tower_plan)
+        wf = self.p.tower_weights(tw, self.tower_plan, fp16=bool(x.elem))
         L.call("mzba_tower_fused", L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(out), L.ptr(wf),
                L.ptr(tw["b"]), tw["n"], self.B, ctypes.byref(x), L.stream())
         if pr is not None:
@@ -371,6 +387,8 @@ class NetRunner:
             self._fused_call(p.dyn_tower, parent_src, H * W * p.c1 if env_stride is None else env_stride, slot,
                              slot_stride, out_latent, x)
             return
+        if p.dyn_fp16:
+            raise RuntimeError("the fp16 dynamics net runs on the fused dynamics step only (fused_ok() is False)")
         self.conv(parent_src, p.dyn0, self.x, B, H, W, relu=True, slot=slot, env_stride=env_stride,
                   slot_stride=slot_stride, act=act)
         if p.dyn_tower is not None and self.use_tower:
@@ -438,11 +456,12 @@ class MuZeroAgent:
     default "bf16") selects the device precision; "f32" is the parity mode.
     """
 
-    def __init__(self, cfg, dtype=None, device="cuda"):
+    def __init__(self, cfg, dtype=None, device="cuda", dyn_dtype=None):
         L.require_gpu()
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype or cfg.get("dtype", "bf16")
+        self.dyn_dtype = dyn_dtype or cfg.get("dyn_dtype")  # "fp16": fp16 dynamics net (BASELINE config 5)
         self.packed = None
         self._runners = {}
         self._sd = None
@@ -460,7 +479,7 @@ class MuZeroAgent:
             if tuple(np.shape(_np(sd[k]))) != tuple(shape):
                 raise ValueError(f"shape mismatch for {k}: {np.shape(_np(sd[k]))} vs {shape}")
         self._sd = {k: _np(sd[k]).copy() for k, _ in spec}
-        self.packed = PackedNets(self._sd, self.cfg, self.dtype, self.device)
+        self.packed = PackedNets(self._sd, self.cfg, self.dtype, self.device, self.dyn_dtype)
         self._runners = {}
 
     def eval_mode(self):

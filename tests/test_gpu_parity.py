@@ -736,3 +736,42 @@ def test_test_simulation_matches_oracle():
         assert len(frames[b]) == len(oframes[b])
         if frames[b]:
             np.testing.assert_array_equal(np.stack([f.numpy() for f in frames[b]]), np.stack(oframes[b]))
+
+
+@pytest.mark.parametrize("B,variant", [(64, 1), (2048, 0)])
+def test_fp16_dynamics_step(B, variant):
+    """BASELINE config 5's fp16 dynamics net: the fused dynamics step with fp16 LDS images / weights
+    / MFMA (latents in and out bf16) against the f32 path of the same weights; its error must not
+    exceed the all-bf16 step's (fp16 keeps 3 more mantissa bits)."""
+    from mzba import _lib as L
+    from mzba.agent import MuZeroAgent
+    mcfg = default_config()["model"]
+    sd = init_state_dict(mcfg, 9)
+    S1, n = 3, 20 * 256
+    g = torch.Generator().manual_seed(B + 1)
+    pool0 = torch.rand(B, S1 + 1, n, generator=g).to(torch.bfloat16).cuda()
+    slot = torch.randint(0, S1, (B,), generator=g, dtype=torch.int32).cuda()
+    act = torch.randint(0, 3, (B,), generator=g, dtype=torch.int32).cuda()
+    res = {}
+    for tag, dt, dyn in (("f32", "f32", None), ("bf16", "bf16", None), ("fp16", "bf16", "fp16")):
+        ag = MuZeroAgent(mcfg, dtype=dt, dyn_dtype=dyn)
+        ag.load_state_dict(sd)
+        L.call("mzba_tower_set_variant", variant)
+        try:
+            rn = ag.runner(B, 16, 20)
+        finally:
+            L.call("mzba_tower_set_variant", 0)
+        tdt = torch.float32 if dt == "f32" else torch.bfloat16
+        pool = pool0.to(tdt)
+        out = torch.empty(B, n, dtype=tdt, device="cuda")
+        r, rl = torch.full((B,), float("nan"), device="cuda"), torch.full((B, 11), float("nan"), device="cuda")
+        if dyn:
+            assert rn.fused_ok() and rn.tower_plan == (variant or 2)
+        rn.dynamics(pool, act, out, r, rl, slot=slot, env_stride=(S1 + 1) * n, slot_stride=n, pool=pool,
+                    pool_env_stride=(S1 + 1) * n, pool_slot=S1)
+        torch.cuda.synchronize()
+        res[tag] = [t.float().cpu() for t in (out, rl)]
+    for i, nm in enumerate(("latent", "reward_logits")):
+        e16 = (res["fp16"][i] - res["f32"][i]).abs().max().item()
+        eb = (res["bf16"][i] - res["f32"][i]).abs().max().item()
+        assert torch.isfinite(res["fp16"][i]).all() and e16 <= max(eb, 1e-2), (nm, e16, eb)
