@@ -304,6 +304,9 @@ int mzba_conv_pack_bf16(const float* w, void* out, int Cout, int taps, int Cin, 
 /* Conv2d weight / bias gradient: dw [Cout][ks*ks][Cin] += sum_m dy[m][co] * x_tap[m][ci],
  * db [Cout] += sum_m dy[m][co] (db may be NULL). x NHWC [B][H][W][Cin], dy [B][H][W][Cout]. */
 long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks);
+/* bf16 3x3 weight-gradient kernel choice: 1 (default) whole zero-bordered images per tile, all 9 taps;
+ * 0 one tap per tile (the kernel used for 1x1 and f32). */
+int mzba_conv_wgrad_set_variant(int v);
 int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
                     float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream);
 /* nn.AvgPool2d(2, 2) backward: dx [B][H][W][C] = dy[y/2][x/2] / 4. */

@@ -543,6 +543,205 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(const bf16_t* __re
   }
 }
 
+// bf16 3x3 weight gradient over whole images: one workgroup = a 64 (co) x 64 (ci) tile for ALL 9
+// taps, over E envs per LDS stage. Each env's image is staged once with a zero border (Hp = H + 2,
+// Wp = W + 2 rows of 64 channels); the contraction index k runs over the H x Wp interior-row
+// positions (border columns carry dY = 0), so tap (dy, dx) is the constant row offset
+// dy * Wp + dx into the bordered X image: every 4-row transposed-read block stays contiguous and
+// dY / X are read from HBM once per tile instead of once per tap.
+constexpr int WI_LD = 80;        // bf16 per LDS row (160 B, the transposed-read bank layout above)
+constexpr int WI_LEAD = 8;       // zero rows before the X images (tap offsets reach -Wp - 1)
+constexpr int WI_PF = 12;        // staging chunks per thread (KS + XR <= 384 rows)
+
+struct WgImg {
+  int B, H, W, Cin, Cout, E, KS, XR, stages_per_split;
+};
+
+MZ_DEV bf16x8_t tr_frag_at(const bf16_t* lo_base, const bf16_t* hi_base) {
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(lo_base));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(hi_base));
+  typedef short v8s __attribute__((ext_vector_type(8)));
+  const v8s r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+template <bool PF>
+__global__ __launch_bounds__(256) void conv_wgrad_img_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
+                                                             WgImg a, float* __restrict__ part,
+                                                             float* __restrict__ bpart) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds_img[];
+  bf16_t* ldy = lds_img;                                   // [KS][WI_LD]
+  bf16_t* lx = lds_img + (size_t)(a.KS + WI_LEAD) * WI_LD;  // [XR + 64][WI_LD], preceded by WI_LEAD zero rows
+  __shared__ float bred[32][64];
+  const int H = a.H, W = a.W, Wp = W + 2, Hp = H + 2, HWp = H * Wp, HpWp = Hp * Wp;
+  const int nci = (a.Cin + 63) / 64;
+  const int cit = blockIdx.x % nci, cot = blockIdx.x / nci;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ch = tid & 7;  // 16-B chunk (8 channels) every staging chunk of this thread holds
+  const int co_s = cot * 64 + ch * 8, ci_s = cit * 64 + ch * 8;
+  const bool do_bias = bpart && cit == 0;
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  // zero the lead rows and the tail margin of the X region once
+  for (int i = tid; i < WI_LEAD * 8; i += 256)
+    *reinterpret_cast<uint4*>(lds_img + (size_t)(a.KS + i / 8) * WI_LD + (i & 7) * 8) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 64 * 8; i += 256)
+    *reinterpret_cast<uint4*>(lx + (size_t)(a.XR + i / 8) * WI_LD + (i & 7) * 8) = make_uint4(0, 0, 0, 0);
+  f32x4_t acc[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int nst_total = (a.B + a.E - 1) / a.E;
+  const int st0 = blockIdx.y * a.stages_per_split, st1 = min(nst_total, st0 + a.stages_per_split);
+  // stage staging through registers. PF: the next stage's HBM loads are in flight during this
+  // stage's MFMAs (WI_PF chunks of 16 B per thread cover KS + XR rows x 8 chunks); otherwise the
+  // stage is loaded in batches of WI_PF chunks after the previous one is consumed.
+  const int nchunk = (a.KS + a.XR) * 8;
+  uint4 pf[WI_PF];
+  auto load_chunks = [&](int st, int base) {
+    const int b0 = st * a.E;
+#pragma unroll
+    for (int u = 0; u < WI_PF; ++u) {
+      const int i = base + u * 256 + tid;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (i < a.KS * 8) {  // dY rows: k = e*HWp + y*Wp + xp (xp in 1..W real, 0 / W+1 border)
+        const int r = i >> 3;
+        const int e = r / HWp, w = r - e * HWp, y = w / Wp, xp = w - y * Wp;
+        const int b = b0 + e;
+        if (e < a.E && b < a.B && xp >= 1 && xp <= W && co_s < a.Cout)
+          v = *reinterpret_cast<const uint4*>(dy + ((size_t)(b * H + y) * W + xp - 1) * a.Cout + co_s);
+      } else if (i < nchunk) {  // X rows: bordered images, row e*HpWp + yp*Wp + xp
+        const int r = (i >> 3) - a.KS;
+        const int e = r / HpWp, rem = r - e * HpWp, yp = rem / Wp, xp = rem - yp * Wp;
+        const int b = b0 + e;
+        if (b < a.B && yp >= 1 && yp <= H && xp >= 1 && xp <= W && ci_s < a.Cin)
+          v = *reinterpret_cast<const uint4*>(x + ((size_t)(b * H + yp - 1) * W + xp - 1) * a.Cin + ci_s);
+      }
+      pf[u] = v;
+    }
+  };
+  auto store_chunks = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < WI_PF; ++u) {
+      const int i = base + u * 256 + tid;
+      if (i < a.KS * 8) {
+        *reinterpret_cast<uint4*>(ldy + (size_t)(i >> 3) * WI_LD + ch * 8) = pf[u];
+        if (do_bias) {
+          const bf16_t* h = reinterpret_cast<const bf16_t*>(&pf[u]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bacc[j] += bf16_to_f32(h[j]);
+        }
+      } else if (i < nchunk) {
+        *reinterpret_cast<uint4*>(lx + (size_t)((i >> 3) - a.KS) * WI_LD + ch * 8) = pf[u];
+      }
+    }
+  };
+  if (PF && st0 < st1) load_chunks(st0, 0);
+  for (int st = st0; st < st1; ++st) {
+    __syncthreads();  // previous stage fully consumed
+    if (PF) {
+      store_chunks(0);
+    } else {
+      for (int base = 0; base < nchunk; base += WI_PF * 256) {
+        load_chunks(st, base);
+        store_chunks(base);
+      }
+    }
+    __syncthreads();
+    if (PF && st + 1 < st1) load_chunks(st + 1, 0);
+    for (int ks = 0; ks < a.KS / 32; ++ks) {
+      // this lane's transposed-read rows for the two 4-row blocks of k step ks
+      const int r0 = ks * 32 + 4 * g + q, r1 = r0 + 16;
+      const int e0 = min(r0 / HWp, a.E - 1), e1 = min(r1 / HWp, a.E - 1);
+      const int x0 = e0 * HpWp + Wp + (r0 - e0 * HWp), x1 = e1 * HpWp + Wp + (r1 - e1 * HWp);
+      bf16x8_t af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = wr * 32 + i * 16 + 4 * pp;
+        af[i] = tr_frag_at(ldy + (size_t)r0 * WI_LD + c, ldy + (size_t)r1 * WI_LD + c);
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int off = (t / 3 - 1) * Wp + (t % 3 - 1);
+        bf16x8_t bfr[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = wc * 32 + j * 16 + 4 * pp;
+          bfr[j] = tr_frag_at(lx + (ptrdiff_t)(x0 + off) * WI_LD + c, lx + (ptrdiff_t)(x1 + off) * WI_LD + c);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[t][i][j], 0, 0, 0);
+      }
+    }
+  }
+  const size_t K = (size_t)9 * a.Cin;
+  float* outp = part + (size_t)blockIdx.y * a.Cout * K;
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ci = cit * 64 + wc * 32 + j * 16 + fr;
+        if (ci >= a.Cin) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = cot * 64 + wr * 32 + i * 16 + 4 * fk + r;
+          if (co < a.Cout) outp[(size_t)co * K + (size_t)t * a.Cin + ci] = acc[t][i][j][r];
+        }
+      }
+  if (do_bias) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bred[tid >> 3][ch * 8 + j] = bacc[j];
+    __syncthreads();
+    if (tid < 64) {
+      float sum = 0.f;
+      for (int r = 0; r < 32; ++r) sum += bred[r][tid];
+      const int co = cot * 64 + tid;
+      if (co < a.Cout) bpart[(size_t)blockIdx.y * a.Cout + co] = sum;
+    }
+  }
+}
+
+// geometry of the image-stage weight gradient (E envs per stage within the LDS budget)
+struct WgPlan {
+  WgImg a;
+  int nsplit;
+  size_t lds;
+  bool pf;  // the whole stage fits the register prefetch
+};
+static bool wgrad_img_plan(int B, int H, int W, int Cin, int Cout, WgPlan& p) {
+  const int Wp = W + 2, HWp = H * Wp, HpWp = (H + 2) * Wp;
+  if (HWp % 4) return false;
+  int E = 1;
+  auto rows = [&](int e) { return ((e * HWp + 31) / 32 * 32) + WI_LEAD + e * HpWp + 64; };
+  auto staged = [&](int e) { return (e * HWp + 31) / 32 * 32 + e * HpWp; };
+  while (E < 16 && E * 2 <= B && (size_t)rows(E * 2) * WI_LD * 2 <= 64 * 1024 && staged(E * 2) * 8 <= WI_PF * 256) E *= 2;
+  if ((size_t)rows(E) * WI_LD * 2 > 150 * 1024) return false;
+  p.pf = staged(E) * 8 <= WI_PF * 256;
+  const int tiles = ((Cout + 63) / 64) * ((Cin + 63) / 64);
+  const int stages = (B + E - 1) / E;
+  int nsplit = (256 + tiles - 1) / tiles;
+  if (nsplit > stages) nsplit = stages;
+  const int sps = (stages + nsplit - 1) / nsplit;
+  nsplit = (stages + sps - 1) / sps;
+  p.a = WgImg{B, H, W, Cin, Cout, E, (E * HWp + 31) / 32 * 32, E * HpWp, sps};
+  p.nsplit = nsplit;
+  p.lds = (size_t)rows(E) * WI_LD * 2;
+  return true;
+}
+
 // acc[i] += sum_s part[s][i] (split order)
 __global__ void sum_partials_kernel(const float* __restrict__ part, int nsplit, size_t n, float* __restrict__ acc) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -958,10 +1157,21 @@ int mzba_conv_pack_bf16(const float* w, void* out, int Cout, int taps, int Cin, 
   return 0;
 }
 
+static int g_wgrad_img = 1;
+// 1 (default): bf16 3x3 weight gradients on the whole-image kernel; 0: the per-tap kernel
+int mzba_conv_wgrad_set_variant(int v) {
+  if (v != 0 && v != 1) return -1;
+  g_wgrad_img = v;
+  return 0;
+}
+
 long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks) {
   const long long M = (long long)B * H * W;
   const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64) * ks * ks;
-  return wgrad_splits(M, tiles) * ((long long)Cout * ks * ks * Cin + Cout) * 4;
+  long long n = wgrad_splits(M, tiles);
+  WgPlan p;
+  if (ks == 3 && Cin % 8 == 0 && Cout % 8 == 0 && wgrad_img_plan(B, H, W, Cin, Cout, p) && p.nsplit > n) n = p.nsplit;
+  return n * ((long long)Cout * ks * ks * Cin + Cout) * 4;
 }
 
 int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
@@ -978,6 +1188,39 @@ int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int 
   float* part = (float*)ws;
   float* bpart = db ? part + nsplit * nw : nullptr;
   MZ_CHECK_ARG(dtype == 0 || dtype == 1, -9);
+  WgPlan ip;
+  // the whole-image kernel wins where an image has many pixels per tap re-read (8x10: 216 vs 270 us,
+  // 16x20: 155 vs 284 us at B = 512); at 4x5 the per-tap kernel is faster (87 vs 96 us,
+  // tools/bench_wgrad.py)
+  if (dtype == 1 && ks == 3 && g_wgrad_img && H * W >= 64 && wgrad_img_plan(B, H, W, Cin, Cout, ip)) {
+    static bool attr = false;  // the 16x20 images need more than the default 64 KB of dynamic LDS
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_img_kernel<false>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_img_kernel<true>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+    const size_t nwi = (size_t)Cout * 9 * Cin;
+    float* ipart = (float*)ws;
+    float* ibpart = db ? ipart + (size_t)ip.nsplit * nwi : nullptr;
+    const dim3 grid(((Cout + 63) / 64) * ((Cin + 63) / 64), ip.nsplit);
+    if (ip.pf)
+      hipLaunchKernelGGL(conv_wgrad_img_kernel<true>, grid, dim3(256), ip.lds, stream, (const bf16_t*)x,
+                         (const bf16_t*)dy, ip.a, ipart, ibpart);
+    else
+      hipLaunchKernelGGL(conv_wgrad_img_kernel<false>, grid, dim3(256), ip.lds, stream, (const bf16_t*)x,
+                         (const bf16_t*)dy, ip.a, ipart, ibpart);
+    hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(nwi)), dim3(256), 0, stream, (const float*)ipart, ip.nsplit,
+                       nwi, dw);
+    if (db)
+      hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(Cout)), dim3(256), 0, stream, (const float*)ibpart,
+                         ip.nsplit, (size_t)Cout, db);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  }
   {
     if (dtype == 1)
       hipLaunchKernelGGL(conv_wgrad_bf16_kernel, dim3((unsigned)tiles, (unsigned)nsplit), dim3(256), 0, stream,
