@@ -76,15 +76,25 @@ def run_env(args, world, rank, local):
     acts = torch.randint(0, 3, (args.warmup + args.steps, B), device=dev, generator=g)
     for i in range(args.warmup):
         env.step(acts[i], i == 0)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # the K timed steps (one mzba_env_step_compact launch each) replay as one HIP graph, as the
+    # acting loop does: eager ctypes launches from Python (~20 us each) would be the bound
+    stream = torch.cuda.Stream(device=dev)
+    stream.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(stream):
+        with torch.cuda.graph(graph, stream=stream):
+            for i in range(args.steps):
+                env.step(acts[args.warmup + i], False)
+        graph.replay()  # untimed: one pass of the captured steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(torch.cuda.current_stream())
-        env.step(acts[args.warmup + i], False)
-        ev[i][1].record(torch.cuda.current_stream())
+    with torch.cuda.stream(stream):
+        ev[0][0].record(stream)
+        graph.replay()
+        ev[0][1].record(stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -93,7 +103,7 @@ def run_env(args, world, rank, local):
         tt = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
-    kms = float(np.median([a.elapsed_time(c) for a, c in ev]))
+    kms = ev[0][0].elapsed_time(ev[0][1]) / args.steps  # per launch, inter-launch gaps included
     achieved = B * env_bytes(H, W) / (kms * 1e-3) / 1e9
     traffic = None  # PMC bytes per launch (tools/gpu_round.sh), when measured for this geometry
     tpath = os.path.join(ROOT, "profiles", "env_hbm_traffic.json")
@@ -187,7 +197,7 @@ def run_learner(args, world, rank, local):
         tt = torch.tensor([dtt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dtt = float(tt.item())
-    kms = float(np.median([a.elapsed_time(c) for a, c in ev]))
+    kms = ev[0][0].elapsed_time(ev[0][1]) / args.steps  # per launch, inter-launch gaps included
     fl = ln.flops_per_minibatch(B)
     peak = 157.3 if dt == "f32" else PEAK_BF16_TFLOPS
     achieved = fl / (kms * 1e-3) / 1e12
@@ -302,8 +312,7 @@ def main():
         nb = min(args.cpu_envs, B)
         cs = loop.cs
         x32 = torch.empty(B * 320 * cs, dtype=torch.float32, device=agent.device)
-        L.call("mzba_build_rep_input", L.ptr(loop.env.cur_frame), L.ptr(loop.env.hist_frames),
-               L.ptr(loop.env.hist_actions), L.ptr(loop.env.hist_len), loop.Lh, L.ptr(x32), 0, B, 320, cs, L.stream())
+        loop.env.build_rep_input(x32, cs, False)
         sid = loop.search_id
         t_before = loop.t
         one_step()

@@ -35,13 +35,17 @@ int mzba_env_step_planes(const float* state, float* next_state, const int64_t* a
 /* RLSystem.convert_to_grayscale (train_torch.py:334-358): (B,3,H,W) -> (B,1,H,W) f32. */
 int mzba_grayscale_planes(const float* state, float* gray, int B, int H, int W, hipStream_t stream);
 
-/* Compact env for the fused acting loop: same rules as mzba_env_step_planes on SoA scalars
+/* Frame storage (reset / step / rep input / current frame): cur_src (u8[B], may be NULL) selects
+ * single-write mode — a frame recorded into the history ring is not also copied to cur_frame;
+ * cur_src[b] = 1 says env b's current frame is the ring's newest entry, 0 that it is cur_frame[b]
+ * (a done env: history frozen, frame live). With cur_src = NULL cur_frame always holds it.
+ * Compact env for the fused acting loop: same rules as mzba_env_step_planes on SoA scalars
  * (paddle col, ball x/y, dx, dy, done) + a brick bitmask (nw u64 words per env over the brick rows).
  * Reset also does _pad_initial_state (train_torch.py:313-332): frame-history ring filled with
  * g(s0) (L-1 frames of H*W u8 gray codes), action ring (L) filled with pad_action (0 for the acting
  * loop, 1 for run_test_simulation, train_torch.py:545), hist_len = 0. */
 int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
-                           uint64_t* bricks, int nw, uint8_t* cur_frame, uint8_t* hist_frames,
+                           uint64_t* bricks, int nw, uint8_t* cur_frame, uint8_t* cur_src, uint8_t* hist_frames,
                            uint8_t* hist_actions, int32_t* hist_len, int L, int B, int H, int W, int paddle_width,
                            int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
                            int pad_action, hipStream_t stream);
@@ -55,10 +59,13 @@ int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* d
  * env, bit 1 = record env 0's action for every env (run_test_simulation, train_torch.py:594-598). */
 int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
                           uint64_t* bricks, int nw, const int64_t* action, float* reward, float* valid,
-                          uint8_t* cur_frame, uint8_t* hist_frames, uint8_t* hist_actions, int32_t* hist_len, int L,
-                          uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
+                          uint8_t* cur_frame, uint8_t* cur_src, uint8_t* hist_frames, uint8_t* hist_actions,
+                          int32_t* hist_len, int L, uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
                           int first_step, int B, int H, int W, int paddle_width, int brick_rows,
                           const float* rewards4, const int32_t* ctx, int rec_flags, hipStream_t stream);
+
+/* Diagnostics: envs per workgroup of mzba_env_step_compact (0 = automatic). */
+int mzba_env_set_block_envs(int E);
 
 /* compact -> reference planes (B,3,H,W) f32. */
 int mzba_compact_to_planes(const int32_t* paddle, const int32_t* bx, const int32_t* by, const uint8_t* done,
@@ -68,9 +75,13 @@ int mzba_compact_to_planes(const int32_t* paddle, const int32_t* bx, const int32
 /* RLSystem._prepare_mcts_input + _encode_actions (train_torch.py:259-293) for all envs:
  * NHWC out [B][HW][Cs] (f32 or bf16): L-1 ring frames oldest first, the current frame, L action
  * planes a/3, zero padding to Cs. */
-int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* hist_frames, const uint8_t* hist_actions,
-                         const int32_t* hist_len, int L, void* out, int out_bf16, int B, int HW, int Cs,
-                         hipStream_t stream);
+int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* cur_src, const uint8_t* hist_frames,
+                         const uint8_t* hist_actions, const int32_t* hist_len, int L, void* out, int out_bf16, int B,
+                         int HW, int Cs, hipStream_t stream);
+
+/* Every env's current frame [B][HW] u8 gray codes (for host readers: frame logging, tests). */
+int mzba_env_current_frame(const uint8_t* cur_frame, const uint8_t* cur_src, const uint8_t* hist_frames,
+                           const int32_t* hist_len, int L, uint8_t* out, int B, int HW, hipStream_t stream);
 
 /* ---- networks (src/networks.py) -------------------------------------------------------- */
 

@@ -160,7 +160,20 @@ struct Compact {
 
 // History ring (train_torch.py:313-332 pad, :204-209 record, :259-293 read):
 //   frames[b][L-1][HW] u8 gray codes, actions[b][L] u8, hlen[b] = records pushed so far.
-struct History { uint8_t* frames; uint8_t* actions; int32_t* hlen; int L; };
+// cur_src (optional, single-write mode): cur_src[b] = 1 when env b's current frame is the
+// ring's newest entry (it was recorded by the last step / reset), 0 when it is cur_frame[b]
+// (a done env: history frozen, frame live). Every frame is then written to HBM exactly once.
+// cur_src == NULL: cur_frame always holds the current frame (a recorded frame is written twice).
+struct History { uint8_t* frames; uint8_t* actions; int32_t* hlen; int L; uint8_t* cur_src; };
+
+// where env b's current frame lives (see History)
+MZ_DEV const uint8_t* current_frame_ptr(const uint8_t* cur_frame, const History& h, size_t b, int HW) {
+  if (h.cur_src && h.cur_src[b]) {
+    const int slot = (h.hlen[b] + h.L - 2) % (h.L - 1);  // newest ring entry
+    return h.frames + (b * (h.L - 1) + slot) * (size_t)HW;
+  }
+  return cur_frame + b * (size_t)HW;
+}
 
 // Trajectory sink (replay_buffer.py:17-35 ObservationTrajectory.add_observation),
 // per acting step t: rec_action[t][b] u8, rec_reward[t][b] f32, rec_mask[t][b] u8; the
@@ -180,6 +193,7 @@ __global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_f
   if (threadIdx.x == 0) {
     cs.paddle[b] = ppos; cs.bx[b] = col; cs.by[b] = by; cs.dx[b] = dx; cs.dy[b] = -1.0f; cs.done[b] = 0;
     hist.hlen[b] = 0;
+    if (hist.cur_src) hist.cur_src[b] = 1;  // current = g(s0) = the ring's newest pad frame
   }
   for (int w = threadIdx.x; w < cs.nw; w += blockDim.x) {
     uint64_t m = 0;
@@ -193,7 +207,7 @@ __global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_f
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
     int y = p / W, x = p - y * W;
     uint8_t c = gray_code(y == H - 1 && x >= ppos && x < ppos + pw, y == by && x == col, y < brick_rows);
-    cf[p] = c;
+    if (!hist.cur_src) cf[p] = c;
     for (int k = 0; k < hist.L - 1; ++k) hist.frames[((size_t)b * (hist.L - 1) + k) * HW + p] = c;
   }
   for (int k = threadIdx.x; k < hist.L; k += blockDim.x) hist.actions[(size_t)b * hist.L + k] = (uint8_t)pad_action;
@@ -204,7 +218,7 @@ __global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_f
 // them into the history ring when the env is recorded this step. E (<= 256) is chosen by the
 // launcher so that the grid fills the chip and a block has ~1-4 stores per lane.
 template <int MAXW>
-__global__ __launch_bounds__(256) void env_step_compact_kernel(
+__global__ __launch_bounds__(256, 8) void env_step_compact_kernel(
     Compact cs, const int64_t* __restrict__ action, float* __restrict__ reward, float* __restrict__ valid,
     uint8_t* __restrict__ cur_frame, History hist, Sink sink, int first_step_arg, int B, int H, int W, int pw,
     int brick_rows, RewardCfg rc, const int32_t* __restrict__ ctx, int E, int rec_flags) {
@@ -219,10 +233,12 @@ __global__ __launch_bounds__(256) void env_step_compact_kernel(
   __shared__ int s_paddle[256], s_bx[256], s_by[256];
   __shared__ uint64_t s_br[256][MAXW];
   __shared__ uint8_t s_done[256], s_rec[256];
+  __shared__ int s_slot[256], s_slot_hl[256];
   const int t = threadIdx.x;
   const int b = blockIdx.x * E + t;
   const int nw = cs.nw;
   if (t < E && b < B) {
+    const int hl = hist.hlen[b];  // loaded with the state: no second round trip when recording
     const bool was_done = cs.done[b] != 0;
     const int p0 = was_done ? 0 : cs.paddle[b];  // argmax of an empty row is 0 (:177)
     const int64_t a = action[b];
@@ -298,53 +314,52 @@ __global__ __launch_bounds__(256) void env_step_compact_kernel(
 #pragma unroll
     for (int w = 0; w < MAXW; ++w) s_br[t][w] = br[w];
     if (rec) {
-      int hl = hist.hlen[b];
       hist.actions[(size_t)b * hist.L + (hl % hist.L)] = (uint8_t)ra;
+      s_slot[t] = hl % (hist.L - 1);
+      s_slot_hl[t] = hl;
     }
   }
   __syncthreads();
   // phase 2: render. Frame rows are HW bytes; lanes write 16 B (HW % 16 == 0 required).
+  // A pixel's code depends on its index p alone: brick bit p of the mask (bit = row*W + col),
+  // paddle iff p in [(H-1)*W + paddle, +pw), ball iff p == by*W + bx. So a 16-pixel chunk is
+  // three 16-bit masks spread to bytes — no per-pixel division, no branch on the region.
   const int HW = H * W;
   const int chunks = HW / 16;
   const int nenv = min(E, B - blockIdx.x * E);
+  const uint32_t inv_chunks = 0xffffffffu / (uint32_t)chunks + 1u;  // exact i / chunks for i < 2^32 / chunks
   for (int i = t; i < nenv * chunks; i += 256) {
-    const int e = i / chunks, c = i - e * chunks;
+    const int e = (int)__umulhi((uint32_t)i, inv_chunks), c = i - e * chunks;
     const int gb = blockIdx.x * E + e;
-    uint32_t wv[4] = {0u, 0u, 0u, 0u};
-    // most chunks lie between the brick rows and the paddle row: all zero unless the ball is there
     const int p0 = c * 16;
-    const int ballp = s_by[e] * W + s_bx[e];
-    const bool plain = p0 >= brick_rows * W && p0 + 16 <= (H - 1) * W;
-    if (plain) {
-      const int o = ballp - p0;
-      if (o >= 0 && o < 16) wv[o >> 2] = (uint32_t)gray_code(false, true, false) << (8 * (o & 3));
-    } else {
+    uint32_t brk16 = 0;
+    if ((p0 >> 6) < nw) brk16 = (uint32_t)(s_br[e][p0 >> 6] >> (p0 & 48)) & 0xffffu;  // p0 % 16 == 0: one word
+    const int plo = s_paddle[e] < 0 ? 0x7fff0000 : (H - 1) * W + s_paddle[e] - p0;
+    const int lo = max(plo, 0), hi = min(plo + pw, 16);
+    const uint32_t pad16 = lo < hi ? ((1u << hi) - 1u) & ~((1u << lo) - 1u) : 0u;
+    const int bo = s_by[e] * W + s_bx[e] - p0;
+    const uint32_t ball16 = (bo >= 0 && bo < 16) ? (1u << bo) : 0u;
+    uint32_t wv[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t word = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          int p = p0 + q * 4 + k;
-          int py = p / W, px = p - py * W;
-          bool pad = s_paddle[e] >= 0 && py == H - 1 && px >= s_paddle[e] && px < s_paddle[e] + pw;
-          bool ball = p == ballp;
-          bool brk = false;
-          if (py < brick_rows) { int bit = py * W + px; brk = (s_br[e][bit >> 6] >> (bit & 63)) & 1ull; }
-          word |= (uint32_t)gray_code(pad, ball, brk) << (8 * k);
-        }
-        wv[q] = word;
-      }
+    for (int q = 0; q < 4; ++q) {  // nibble n -> 4 bytes holding n's bits: (n * 0x204081) & 0x01010101
+      const uint32_t nb = ((brk16 >> (4 * q)) & 15u) * 0x204081u & 0x01010101u;
+      const uint32_t nl = ((ball16 >> (4 * q)) & 15u) * 0x204081u & 0x01010101u;
+      const uint32_t np = ((pad16 >> (4 * q)) & 15u) * 0x204081u & 0x01010101u;
+      wv[q] = (nb << 2) | (nl << 1) | np;  // gray_code(paddle, ball, brick)
     }
     uint4 v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-    *reinterpret_cast<uint4*>(cur_frame + (size_t)gb * HW + c * 16) = v;
     if (sink.frame) *reinterpret_cast<uint4*>(sink.frame + (size_t)gb * HW + c * 16) = v;
     if (s_rec[e]) {
-      int hl = hist.hlen[gb];
-      *reinterpret_cast<uint4*>(hist.frames + ((size_t)gb * (hist.L - 1) + (hl % (hist.L - 1))) * HW + c * 16) = v;
+      *reinterpret_cast<uint4*>(hist.frames + ((size_t)gb * (hist.L - 1) + s_slot[e]) * HW + c * 16) = v;
+      if (!hist.cur_src) *reinterpret_cast<uint4*>(cur_frame + (size_t)gb * HW + c * 16) = v;
+    } else {
+      *reinterpret_cast<uint4*>(cur_frame + (size_t)gb * HW + c * 16) = v;
     }
   }
-  __syncthreads();
-  if (t < E && b < B && s_rec[t]) hist.hlen[b] = hist.hlen[b] + 1;
+  if (t < E && b < B) {
+    if (s_rec[t]) hist.hlen[b] = s_slot_hl[t] + 1;  // phase 2 reads hlen only through s_slot
+    if (hist.cur_src) hist.cur_src[b] = s_rec[t];
+  }
 }
 
 // compact -> planes (for parity checks and the drop-in API)
@@ -402,7 +417,7 @@ __global__ void build_rep_input_kernel(const uint8_t* __restrict__ cur_frame, Hi
       const int c = ch * 8 + j;
       float x = 0.f;
       if (c < L - 1) x = lut[hist.frames[(b * (L - 1) + ((hl + c) % (L - 1))) * HW + p] & 7];
-      else if (c == L - 1) x = lut[cur_frame[b * HW + p] & 7];
+      else if (c == L - 1) x = lut[current_frame_ptr(cur_frame, hist, b, HW)[p] & 7];
       else if (c < 2 * L) x = (float)hist.actions[b * L + ((hl + c - L) % L)] / 3.0f;
       v[j] = x;
     }
@@ -421,10 +436,26 @@ __global__ void build_rep_input_kernel(const uint8_t* __restrict__ cur_frame, Hi
   }
 }
 
+// materialise every env's current frame (single-write mode keeps it in the ring or cur_frame)
+__global__ void current_frame_kernel(const uint8_t* __restrict__ cur_frame, History hist, uint8_t* __restrict__ out,
+                                     int B, int HW) {
+  const int b = blockIdx.x;
+  const uint8_t* src = current_frame_ptr(cur_frame, hist, b, HW);
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) out[(size_t)b * HW + p] = src[p];
+}
+
 }  // namespace
+
+static int g_block_envs = 0;  // 0 = automatic (mzba_env_set_block_envs, diagnostics)
 
 // =============================================================================== C ABI
 extern "C" {
+
+int mzba_env_set_block_envs(int E) {
+  MZ_CHECK_ARG(E >= 0 && E <= 256, -1);
+  g_block_envs = E;
+  return 0;
+}
 
 int mzba_env_reset_planes(float* state, int64_t* ball_dx, float* ball_dy, int B, int H, int W, int paddle_width,
                           int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
@@ -457,14 +488,14 @@ int mzba_grayscale_planes(const float* state, float* gray, int B, int H, int W, 
 }
 
 int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
-                           uint64_t* bricks, int nw, uint8_t* cur_frame, uint8_t* hist_frames,
+                           uint64_t* bricks, int nw, uint8_t* cur_frame, uint8_t* cur_src, uint8_t* hist_frames,
                            uint8_t* hist_actions, int32_t* hist_len, int L, int B, int H, int W, int paddle_width,
                            int brick_rows, uint64_t seed, int episode, int env_offset, const int32_t* params,
                            int pad_action, hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && L >= 2 && nw * 64 >= brick_rows * W && nw <= 4 && (H * W) % 16 == 0 && pad_action >= 0 &&
                pad_action < 3, -1);
   Compact cs{paddle, bx, by, dx, dy, done, bricks, nw};
-  History h{hist_frames, hist_actions, hist_len, L};
+  History h{hist_frames, hist_actions, hist_len, L, cur_src};
   hipLaunchKernelGGL(env_reset_compact_kernel, dim3(B), dim3(256), 0, stream, cs, cur_frame, h, pad_action, B, H, W,
                      paddle_width, brick_rows, seed, episode, env_offset, params);
   MZ_LAUNCH_CHECK();
@@ -473,20 +504,21 @@ int mzba_env_reset_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* d
 
 int mzba_env_step_compact(int32_t* paddle, int32_t* bx, int32_t* by, int32_t* dx, float* dy, uint8_t* done,
                           uint64_t* bricks, int nw, const int64_t* action, float* reward, float* valid,
-                          uint8_t* cur_frame, uint8_t* hist_frames, uint8_t* hist_actions, int32_t* hist_len, int L,
-                          uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
+                          uint8_t* cur_frame, uint8_t* cur_src, uint8_t* hist_frames, uint8_t* hist_actions,
+                          int32_t* hist_len, int L, uint8_t* rec_action, float* rec_reward, uint8_t* rec_mask, uint8_t* rec_frame,
                           int first_step, int B, int H, int W, int paddle_width, int brick_rows,
                           const float* rewards4, const int32_t* ctx, int rec_flags, hipStream_t stream) {
-  MZ_CHECK_ARG(B > 0 && L >= 2 && nw >= 1 && nw <= 4 && nw * 64 >= brick_rows * W && (H * W) % 16 == 0 && rewards4,
-               -1);
+  MZ_CHECK_ARG(B > 0 && L >= 2 && nw >= 1 && nw <= 4 && nw * 64 >= brick_rows * W && (H * W) % 16 == 0 &&
+               H * W <= 65536 && rewards4, -1);  // H*W bound: the render loop's reciprocal division
   Compact cs{paddle, bx, by, dx, dy, done, bricks, nw};
-  History h{hist_frames, hist_actions, hist_len, L};
+  History h{hist_frames, hist_actions, hist_len, L, cur_src};
   Sink sk{rec_action, rec_reward, rec_mask, rec_frame};
   RewardCfg rc{rewards4[0], rewards4[1], rewards4[2], rewards4[3]};
   // envs per block: ~<= 4 16-B render stores per lane, and >= ~512 blocks when B allows
   const int chunks = H * W / 16;
   int E = 1;
   while (E < 256 && 2 * E * chunks <= 1024 && 2 * E * 512 <= B) E *= 2;
+  if (g_block_envs > 0) E = g_block_envs;
   dim3 grid((B + E - 1) / E);
   if (nw == 1)
     hipLaunchKernelGGL(env_step_compact_kernel<1>, grid, dim3(256), 0, stream, cs, action, reward, valid, cur_frame,
@@ -509,11 +541,11 @@ int mzba_compact_to_planes(const int32_t* paddle, const int32_t* bx, const int32
   return 0;
 }
 
-int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* hist_frames, const uint8_t* hist_actions,
-                         const int32_t* hist_len, int L, void* out, int out_bf16, int B, int HW, int Cs,
-                         hipStream_t stream) {
+int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* cur_src, const uint8_t* hist_frames,
+                         const uint8_t* hist_actions, const int32_t* hist_len, int L, void* out, int out_bf16, int B,
+                         int HW, int Cs, hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && Cs >= 2 * L && Cs % 8 == 0, -1);
-  History h{(uint8_t*)hist_frames, (uint8_t*)hist_actions, (int32_t*)hist_len, L};
+  History h{(uint8_t*)hist_frames, (uint8_t*)hist_actions, (int32_t*)hist_len, L, (uint8_t*)cur_src};
   size_t n = (size_t)B * HW * (Cs / 8);
   unsigned grid = (unsigned)((n + 255) / 256);
   if (grid > 16384) grid = 16384;
@@ -523,6 +555,15 @@ int mzba_build_rep_input(const uint8_t* cur_frame, const uint8_t* hist_frames, c
   else
     hipLaunchKernelGGL(build_rep_input_kernel<float>, dim3(grid), dim3(256), 0, stream, cur_frame, h, (float*)out,
                        B, HW, Cs);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_env_current_frame(const uint8_t* cur_frame, const uint8_t* cur_src, const uint8_t* hist_frames,
+                           const int32_t* hist_len, int L, uint8_t* out, int B, int HW, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && L >= 2 && HW > 0 && out, -1);
+  History h{(uint8_t*)hist_frames, nullptr, (int32_t*)hist_len, L, (uint8_t*)cur_src};
+  hipLaunchKernelGGL(current_frame_kernel, dim3(B), dim3(256), 0, stream, cur_frame, h, out, B, HW);
   MZ_LAUNCH_CHECK();
   return 0;
 }

@@ -24,10 +24,12 @@ SIGNATURES = {
     "mzba_env_reset_planes": [P, P, P, I, I, I, I, I, U64, I, I, P, P],
     "mzba_env_step_planes": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "mzba_grayscale_planes": [P, P, I, I, I, P],
-    "mzba_env_reset_compact": [P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, U64, I, I, P, I, P],
-    "mzba_env_step_compact": [P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, P, P, I, P],
+    "mzba_env_reset_compact": [P, P, P, P, P, P, P, I, P, P, P, P, P, I, I, I, I, I, I, U64, I, I, P, I, P],
+    "mzba_env_step_compact": [P, P, P, P, P, P, P, I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, I, I, I, I, I, P, P, I, P],
     "mzba_compact_to_planes": [P, P, P, P, P, I, P, I, I, I, I, I, P],
-    "mzba_build_rep_input": [P, P, P, P, I, P, I, I, I, I, P],
+    "mzba_build_rep_input": [P, P, P, P, P, I, P, I, I, I, I, P],
+    "mzba_env_current_frame": [P, P, P, P, I, P, I, I, P],
+    "mzba_env_set_block_envs": [I],
     "mzba_conv2d": [I, P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
     "mzba_conv_lat_supported": [I, I, I, I, I],
     "mzba_conv_lat_set_variant": [I],

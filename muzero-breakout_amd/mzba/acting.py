@@ -96,7 +96,7 @@ class ActingLoop:
         if episode is not None:
             self.episode = episode
         self.env.reset(self.episode, params)
-        self.frame0 = self.env.cur_frame.clone()
+        self.frame0 = self.env.current_frame()
         self.episode += 1
         self.t = 0
         self.ctx.copy_(torch.tensor([self.search_id, self.step_index, 0], dtype=torch.int32))
@@ -198,7 +198,7 @@ def run_test_simulation(cfg, agent, batch=2, seed=0, episode=0, max_steps_test=2
             break
         loop.act(eager=True)
         done = loop.env.done.cpu().numpy().astype(bool)
-        cur = loop.env.cur_frame.view(batch, -1).cpu().numpy()
+        cur = loop.env.current_frame().view(batch, -1).cpu().numpy()
         for b in range(batch):  # :583-585
             if not done[b]:
                 frames[b].append(torch.from_numpy(lut[cur[b] & 7].reshape(1, H, W)))

@@ -125,7 +125,7 @@ class CompactBreakout:
     """Device-resident compact env state for B envs + frame-history ring of length L."""
 
     def __init__(self, cfg_env, B, L_hist, height=16, width=20, paddle_width=6, brick_rows=3, seed=0, env_offset=0,
-                 device="cuda", pad_action=0, rec_flags=0):
+                 device="cuda", pad_action=0, rec_flags=0, single_write=True):
         L.require_gpu()
         self.B, self.H, self.W = B, height, width
         self.pw, self.brick_rows = paddle_width, brick_rows
@@ -144,7 +144,10 @@ class CompactBreakout:
         self.nw = (brick_rows * width + 63) // 64
         self.bricks = torch.zeros(B * self.nw, dtype=torch.int64, device=dev)
         HW = height * width
+        # single-write frame storage (include/mzba.h): a recorded frame lives only in the history
+        # ring; cur_frame holds the live frames of done envs; cur_src[b] says which
         self.cur_frame = torch.zeros(B * HW, dtype=torch.uint8, device=dev)
+        self.cur_src = torch.ones(B, dtype=torch.uint8, device=dev) if single_write else None
         self.hist_frames = torch.zeros(B * (L_hist - 1) * HW, dtype=torch.uint8, device=dev)
         self.hist_actions = torch.zeros(B * L_hist, dtype=torch.uint8, device=dev)
         self.hist_len = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -159,7 +162,8 @@ class CompactBreakout:
         pr = None
         if params is not None:
             pr = torch.as_tensor(np.asarray(params, dtype=np.int32), device=self.device).contiguous()
-        L.call("mzba_env_reset_compact", *self._state_ptrs(), L.ptr(self.cur_frame), L.ptr(self.hist_frames),
+        L.call("mzba_env_reset_compact", *self._state_ptrs(), L.ptr(self.cur_frame), L.ptr(self.cur_src),
+               L.ptr(self.hist_frames),
                L.ptr(self.hist_actions), L.ptr(self.hist_len), self.Lh, self.B, self.H, self.W, self.pw,
                self.brick_rows, self.seed, episode, self.env_offset, L.ptr(pr), self.pad_action, L.stream())
         self.valid.fill_(1.0)
@@ -175,8 +179,8 @@ class CompactBreakout:
                 ra, rr, rm = rec["action"][t], rec["reward"][t], rec["mask"][t]
                 rf = rec["frame"][t] if rec.get("frame") is not None else None
         L.call("mzba_env_step_compact", *self._state_ptrs(), L.ptr(action), L.ptr(self.reward), L.ptr(self.valid),
-               L.ptr(self.cur_frame), L.ptr(self.hist_frames), L.ptr(self.hist_actions), L.ptr(self.hist_len), self.Lh,
-               L.ptr(ra), L.ptr(rr), L.ptr(rm), L.ptr(rf), 1 if first_step else 0, self.B, self.H, self.W, self.pw,
+               L.ptr(self.cur_frame), L.ptr(self.cur_src), L.ptr(self.hist_frames), L.ptr(self.hist_actions),
+               L.ptr(self.hist_len), self.Lh, L.ptr(ra), L.ptr(rr), L.ptr(rm), L.ptr(rf), 1 if first_step else 0, self.B, self.H, self.W, self.pw,
                self.brick_rows, self.rewards4, L.ptr(ctx), self.rec_flags, L.stream())
 
     def to_planes(self):
@@ -186,5 +190,13 @@ class CompactBreakout:
         return planes
 
     def build_rep_input(self, out, cs, bf16):
-        L.call("mzba_build_rep_input", L.ptr(self.cur_frame), L.ptr(self.hist_frames), L.ptr(self.hist_actions),
-               L.ptr(self.hist_len), self.Lh, L.ptr(out), 1 if bf16 else 0, self.B, self.H * self.W, cs, L.stream())
+        L.call("mzba_build_rep_input", L.ptr(self.cur_frame), L.ptr(self.cur_src), L.ptr(self.hist_frames),
+               L.ptr(self.hist_actions), L.ptr(self.hist_len), self.Lh, L.ptr(out), 1 if bf16 else 0, self.B,
+               self.H * self.W, cs, L.stream())
+
+    def current_frame(self):
+        """Every env's current u8 gray-code frame, (B*H*W,) on the device."""
+        out = torch.empty(self.B * self.H * self.W, dtype=torch.uint8, device=self.device)
+        L.call("mzba_env_current_frame", L.ptr(self.cur_frame), L.ptr(self.cur_src), L.ptr(self.hist_frames),
+               L.ptr(self.hist_len), self.Lh, L.ptr(out), self.B, self.H * self.W, L.stream())
+        return out

@@ -117,7 +117,7 @@ def test_env_compact_matches_planes_and_reference(tag):
         np.testing.assert_array_equal(env.reward.cpu().numpy(), d["rewards"][t])
         np.testing.assert_array_equal(env.done.cpu().numpy().astype(bool), d["dones"][t])
         np.testing.assert_array_equal(env.valid.cpu().numpy(), d["valids"][t])
-        g = lut[env.cur_frame.view(B, H * W).cpu().numpy() & 7].reshape(B, 1, H, W)
+        g = lut[env.current_frame().view(B, H * W).cpu().numpy() & 7].reshape(B, 1, H, W)
         np.testing.assert_array_equal(g, convert_to_grayscale(ref))
 
 
@@ -150,12 +150,15 @@ def _oracle_history(B, L, H, W, steps, seed):
     return trajs, convert_to_grayscale(s), acts
 
 
+@pytest.mark.parametrize("single_write", [True, False])
 @pytest.mark.parametrize("L,steps", [(32, 0), (32, 5), (32, 45), (4, 7), (4, 120)])
-def test_rep_input_builder(L, steps):
-    from mzba.env import CompactBreakout
+def test_rep_input_builder(L, steps, single_write):
+    """single_write: recorded frames only in the ring (cur_src) vs also copied to cur_frame;
+    (4, 120) leaves most envs done, so both frame locations are read."""
+    from mzba.env import CompactBreakout, gray_lut
     B, H, W, seed = 16, 16, 20, 11
     trajs, cur, acts = _oracle_history(B, L, H, W, steps, seed)
-    env = CompactBreakout(ENV_CFG, B, L, H, W, seed=seed)
+    env = CompactBreakout(ENV_CFG, B, L, H, W, seed=seed, single_write=single_write)
     env.reset(0)
     for t in range(steps):
         env.step(dev(acts[t]), t == 0)
@@ -166,6 +169,11 @@ def test_rep_input_builder(L, steps):
     ref = np.stack([prepare_mcts_input(cur[b], trajs[b], L) for b in range(B)])
     np.testing.assert_array_equal(got[:, : 2 * L], ref)
     assert not got[:, 2 * L:].any()
+    lut = gray_lut()
+    np.testing.assert_array_equal(lut[env.current_frame().view(B, H, W).cpu().numpy() & 7], cur[:, 0])
+    if single_write and steps in (5, 120):  # both frame locations exercised
+        src = env.cur_src.cpu().numpy()
+        assert (src == 1).all() if steps == 5 else (src == 0).all(), src
 
 
 # ------------------------------------------------------------------------------ nets
