@@ -197,7 +197,7 @@ def run_learner(args, world, rank, local):
         tt = torch.tensor([dtt], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dtt = float(tt.item())
-    kms = ev[0][0].elapsed_time(ev[0][1]) / args.steps  # per launch, inter-launch gaps included
+    kms = float(np.median([a.elapsed_time(c) for a, c in ev]))
     fl = ln.flops_per_minibatch(B)
     peak = 157.3 if dt == "f32" else PEAK_BF16_TFLOPS
     achieved = fl / (kms * 1e-3) / 1e12

@@ -320,6 +320,12 @@ long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int k
 int mzba_conv_wgrad_set_variant(int v);
 int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
                     float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream);
+/* The same over nseg (<= 8) (x, dY) segments of B envs each, reduced in one contraction (the K
+ * unrolled uses of one weight; ws sized by mzba_conv_wgrad_ws_bytes(nseg * B, ...)). xs / dys:
+ * host arrays of device pointers. */
+int mzba_conv_wgrad_segs(int dtype, const void* const* xs, const void* const* dys, int nseg, int B, int H, int W,
+                         int Cin, int Cout, int ks, float* dw, float* db, void* ws, long long ws_bytes,
+                         hipStream_t stream);
 /* nn.AvgPool2d(2, 2) backward: dx [B][H][W][C] = dy[y/2][x/2] / 4. */
 int mzba_avgpool2_backward(int dtype, const void* dy, void* dx, int B, int H, int W, int C, hipStream_t stream);
 /* y += x (n elements). */

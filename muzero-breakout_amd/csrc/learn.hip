@@ -553,8 +553,14 @@ constexpr int WI_LD = 80;        // bf16 per LDS row (160 B, the transposed-read
 constexpr int WI_LEAD = 8;       // zero rows before the X images (tap offsets reach -Wp - 1)
 constexpr int WI_PF = 12;        // staging chunks per thread (KS + XR <= 384 rows)
 
+// up to WG_MAXSEG (x, dY) segments of Bseg envs each form one contraction (env b = seg * Bseg + b'):
+// the K unrolled uses of one latent conv reduce in a single launch (learner._flush_wgrad)
+constexpr int WG_MAXSEG = 8;
 struct WgImg {
   int B, H, W, Cin, Cout, E, KS, XR, stages_per_split;
+  int Bseg;
+  const bf16_t* xs[WG_MAXSEG];
+  const bf16_t* dys[WG_MAXSEG];
 };
 
 MZ_DEV bf16x8_t tr_frag_at(const bf16_t* lo_base, const bf16_t* hi_base) {
@@ -566,8 +572,7 @@ MZ_DEV bf16x8_t tr_frag_at(const bf16_t* lo_base, const bf16_t* hi_base) {
 }
 
 template <bool PF>
-__global__ __launch_bounds__(256) void conv_wgrad_img_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ dy,
-                                                             WgImg a, float* __restrict__ part,
+__global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __restrict__ part,
                                                              float* __restrict__ bpart) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds_img[];
   bf16_t* ldy = lds_img;                                   // [KS][WI_LD]
@@ -602,26 +607,57 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(const bf16_t* __res
   // stage staging through registers. PF: the next stage's HBM loads are in flight during this
   // stage's MFMAs (WI_PF chunks of 16 B per thread cover KS + XR rows x 8 chunks); otherwise the
   // stage is loaded in batches of WI_PF chunks after the previous one is consumed.
+  // A stage = E consecutive envs of one segment (the planner makes E divide Bseg), so a chunk's
+  // source is the stage's env-0 base + an offset that is the same for every stage: the per-chunk
+  // index math (divisions by the bordered geometry) runs once per thread, not once per stage.
   const int nchunk = (a.KS + a.XR) * 8;
+  const size_t img_x = (size_t)H * W * a.Cin, img_dy = (size_t)H * W * a.Cout;
+  int soff[WI_PF];      // element offset from the stage's env-0 base, -1 = zero chunk
+  uint32_t sdy = 0u;    // bit u: chunk u is a dY chunk
+  for (int u = 0; u < WI_PF; ++u) {
+    int off = -1;
+    const int i = u * 256 + tid;
+    if (i < a.KS * 8) {  // dY rows: k = e*HWp + y*Wp + xp (xp in 1..W real, 0 / W+1 border)
+      const int r = i >> 3;
+      const int e = r / HWp, w = r - e * HWp, y = w / Wp, xp = w - y * Wp;
+      if (e < a.E && xp >= 1 && xp <= W && co_s < a.Cout) off = (int)(e * img_dy + (size_t)(y * W + xp - 1) * a.Cout + co_s);
+      sdy |= 1u << u;
+    } else if (i < nchunk) {  // X rows: bordered images, row e*HpWp + yp*Wp + xp
+      const int r = (i >> 3) - a.KS;
+      const int e = r / HpWp, rem = r - e * HpWp, yp = rem / Wp, xp = rem - yp * Wp;
+      if (yp >= 1 && yp <= H && xp >= 1 && xp <= W && ci_s < a.Cin)
+        off = (int)(e * img_x + (size_t)((yp - 1) * W + xp - 1) * a.Cin + ci_s);
+    }
+    soff[u] = off;
+  }
   uint4 pf[WI_PF];
   auto load_chunks = [&](int st, int base) {
-    const int b0 = st * a.E;
+    const int b0 = st * a.E, sg = b0 / a.Bseg, bl = b0 - sg * a.Bseg;
+    const bf16_t* xb = a.xs[sg] + (size_t)bl * img_x;
+    const bf16_t* db = a.dys[sg] + (size_t)bl * img_dy;
+    if (base == 0) {
 #pragma unroll
-    for (int u = 0; u < WI_PF; ++u) {
+      for (int u = 0; u < WI_PF; ++u) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (soff[u] >= 0) v = *reinterpret_cast<const uint4*>(((sdy >> u) & 1u ? db : xb) + soff[u]);
+        pf[u] = v;
+      }
+      return;
+    }
+#pragma unroll
+    for (int u = 0; u < WI_PF; ++u) {  // batched (non-PF) plans: chunks beyond the first batch
       const int i = base + u * 256 + tid;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (i < a.KS * 8) {  // dY rows: k = e*HWp + y*Wp + xp (xp in 1..W real, 0 / W+1 border)
+      if (i < a.KS * 8) {
         const int r = i >> 3;
         const int e = r / HWp, w = r - e * HWp, y = w / Wp, xp = w - y * Wp;
-        const int b = b0 + e;
-        if (e < a.E && b < a.B && xp >= 1 && xp <= W && co_s < a.Cout)
-          v = *reinterpret_cast<const uint4*>(dy + ((size_t)(b * H + y) * W + xp - 1) * a.Cout + co_s);
-      } else if (i < nchunk) {  // X rows: bordered images, row e*HpWp + yp*Wp + xp
+        if (e < a.E && xp >= 1 && xp <= W && co_s < a.Cout)
+          v = *reinterpret_cast<const uint4*>(db + e * img_dy + (size_t)(y * W + xp - 1) * a.Cout + co_s);
+      } else if (i < nchunk) {
         const int r = (i >> 3) - a.KS;
         const int e = r / HpWp, rem = r - e * HpWp, yp = rem / Wp, xp = rem - yp * Wp;
-        const int b = b0 + e;
-        if (b < a.B && yp >= 1 && yp <= H && xp >= 1 && xp <= W && ci_s < a.Cin)
-          v = *reinterpret_cast<const uint4*>(x + ((size_t)(b * H + yp - 1) * W + xp - 1) * a.Cin + ci_s);
+        if (yp >= 1 && yp <= H && xp >= 1 && xp <= W && ci_s < a.Cin)
+          v = *reinterpret_cast<const uint4*>(xb + e * img_x + (size_t)((yp - 1) * W + xp - 1) * a.Cin + ci_s);
       }
       pf[u] = v;
     }
@@ -721,13 +757,14 @@ struct WgPlan {
   size_t lds;
   bool pf;  // the whole stage fits the register prefetch
 };
-static bool wgrad_img_plan(int B, int H, int W, int Cin, int Cout, WgPlan& p) {
+// B = all envs (nseg * Bseg); a stage's E envs never straddle a segment (E divides Bseg)
+static bool wgrad_img_plan(int B, int Bseg, int H, int W, int Cin, int Cout, WgPlan& p) {
   const int Wp = W + 2, HWp = H * Wp, HpWp = (H + 2) * Wp;
-  if (HWp % 4) return false;
+  if (HWp % 4 || Bseg <= 0 || B % Bseg) return false;
   int E = 1;
   auto rows = [&](int e) { return ((e * HWp + 31) / 32 * 32) + WI_LEAD + e * HpWp + 64; };
   auto staged = [&](int e) { return (e * HWp + 31) / 32 * 32 + e * HpWp; };
-  while (E < 16 && E * 2 <= B && (size_t)rows(E * 2) * WI_LD * 2 <= 64 * 1024 && staged(E * 2) * 8 <= WI_PF * 256) E *= 2;
+  while (E < 16 && Bseg % (E * 2) == 0 && (size_t)rows(E * 2) * WI_LD * 2 <= 64 * 1024 && staged(E * 2) * 8 <= WI_PF * 256) E *= 2;
   if ((size_t)rows(E) * WI_LD * 2 > 150 * 1024) return false;
   p.pf = staged(E) * 8 <= WI_PF * 256;
   const int tiles = ((Cout + 63) / 64) * ((Cin + 63) / 64);
@@ -736,7 +773,7 @@ static bool wgrad_img_plan(int B, int H, int W, int Cin, int Cout, WgPlan& p) {
   if (nsplit > stages) nsplit = stages;
   const int sps = (stages + nsplit - 1) / nsplit;
   nsplit = (stages + sps - 1) / sps;
-  p.a = WgImg{B, H, W, Cin, Cout, E, (E * HWp + 31) / 32 * 32, E * HpWp, sps};
+  p.a = WgImg{B, H, W, Cin, Cout, E, (E * HWp + 31) / 32 * 32, E * HpWp, sps, Bseg, {}, {}};
   p.nsplit = nsplit;
   p.lds = (size_t)rows(E) * WI_LD * 2;
   return true;
@@ -1158,9 +1195,10 @@ int mzba_conv_pack_bf16(const float* w, void* out, int Cout, int taps, int Cin, 
 }
 
 static int g_wgrad_img = 1;
-// 1 (default): bf16 3x3 weight gradients on the whole-image kernel; 0: the per-tap kernel
+// 1 (default): bf16 3x3 weight gradients on the whole-image kernel where it wins (see
+// wgrad_img_eligible); 2: whole-image kernel for every supported shape; 0: per-tap kernel only
 int mzba_conv_wgrad_set_variant(int v) {
-  if (v != 0 && v != 1) return -1;
+  if (v < 0 || v > 2) return -1;
   g_wgrad_img = v;
   return 0;
 }
@@ -1170,29 +1208,32 @@ long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int k
   const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64) * ks * ks;
   long long n = wgrad_splits(M, tiles);
   WgPlan p;
-  if (ks == 3 && Cin % 8 == 0 && Cout % 8 == 0 && wgrad_img_plan(B, H, W, Cin, Cout, p) && p.nsplit > n) n = p.nsplit;
+  if (ks == 3 && Cin % 8 == 0 && Cout % 8 == 0 && wgrad_img_plan(B, 1, H, W, Cin, Cout, p) && p.nsplit > n) n = p.nsplit;
   return n * ((long long)Cout * ks * ks * Cin + Cout) * 4;
 }
 
-int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
-                    float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream) {
-  MZ_CHECK_ARG(x && dy && dw && ws && B > 0 && (ks == 1 || ks == 3) && Cin % 4 == 0 && Cout % 4 == 0, -1);
+// the whole-image kernel over nseg segments of B envs (false: shape not supported by it)
+static bool wgrad_img_eligible(int dtype, int nseg, int B, int H, int W, int Cin, int Cout, int ks, WgPlan& ip) {
+  // it wins where an image has many pixels per tap re-read (8x10: 216 vs 270 us, 16x20: 155 vs
+  // 284 us at B = 512) and, at 4x5, once the K unrolled uses of a conv reduce in one launch
+  // (per-tap kernel: 87 us per use; 5 x 512 at 256 -> 256: 265 vs 399 us). Not for a ragged
+  // channel tile at 4x5: the dynamics ConvBlock's 264 input channels (256 + action planes,
+  // padded) lose (540 vs 456 us; tools/bench_wgrad_segs.py)
+  if (dtype != 1 || ks != 3 || !g_wgrad_img || Cin % 8 || Cout % 8) return false;
+  if (H * W < 64 && !(g_wgrad_img == 2 || (nseg * B >= 2048 && Cin % 64 == 0 && Cout % 64 == 0))) return false;
+  return wgrad_img_plan(nseg * B, B, H, W, Cin, Cout, ip);
+}
+
+static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, int nseg, int B, int H, int W, int Cin,
+                      int Cout, int ks, float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream) {
+  MZ_CHECK_ARG(xs && dys && dw && ws && B > 0 && nseg >= 1 && nseg <= WG_MAXSEG && (ks == 1 || ks == 3) &&
+               Cin % 4 == 0 && Cout % 4 == 0, -1);
   MZ_CHECK_ARG(dtype == 0 || (Cin % 8 == 0 && Cout % 8 == 0), -1);
-  const long long M = (long long)B * H * W;
-  const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64) * ks * ks;
-  const long long nsplit = wgrad_splits(M, tiles);
-  const int step = dtype ? WB_M : WG_ROWS;
-  const int rps = (int)(((M + nsplit - 1) / nsplit + step - 1) / step * step);
-  const size_t nw = (size_t)Cout * ks * ks * Cin;
-  MZ_CHECK_ARG(mzba_conv_wgrad_ws_bytes(B, H, W, Cin, Cout, ks) <= ws_bytes, -2);
-  float* part = (float*)ws;
-  float* bpart = db ? part + nsplit * nw : nullptr;
   MZ_CHECK_ARG(dtype == 0 || dtype == 1, -9);
+  for (int i = 0; i < nseg; ++i) MZ_CHECK_ARG(xs[i] && dys[i], -1);
+  MZ_CHECK_ARG(mzba_conv_wgrad_ws_bytes(nseg * B, H, W, Cin, Cout, ks) <= ws_bytes, -2);
   WgPlan ip;
-  // the whole-image kernel wins where an image has many pixels per tap re-read (8x10: 216 vs 270 us,
-  // 16x20: 155 vs 284 us at B = 512); at 4x5 the per-tap kernel is faster (87 vs 96 us,
-  // tools/bench_wgrad.py)
-  if (dtype == 1 && ks == 3 && g_wgrad_img && H * W >= 64 && wgrad_img_plan(B, H, W, Cin, Cout, ip)) {
+  if (wgrad_img_eligible(dtype, nseg, B, H, W, Cin, Cout, ks, ip)) {
     static bool attr = false;  // the 16x20 images need more than the default 64 KB of dynamic LDS
     if (!attr) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_img_kernel<false>),
@@ -1203,16 +1244,19 @@ int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int 
       if (e != hipSuccess) return (int)e;
       attr = true;
     }
+    ip.a.Bseg = B;
+    for (int i = 0; i < nseg; ++i) {
+      ip.a.xs[i] = (const bf16_t*)xs[i];
+      ip.a.dys[i] = (const bf16_t*)dys[i];
+    }
     const size_t nwi = (size_t)Cout * 9 * Cin;
     float* ipart = (float*)ws;
     float* ibpart = db ? ipart + (size_t)ip.nsplit * nwi : nullptr;
     const dim3 grid(((Cout + 63) / 64) * ((Cin + 63) / 64), ip.nsplit);
     if (ip.pf)
-      hipLaunchKernelGGL(conv_wgrad_img_kernel<true>, grid, dim3(256), ip.lds, stream, (const bf16_t*)x,
-                         (const bf16_t*)dy, ip.a, ipart, ibpart);
+      hipLaunchKernelGGL(conv_wgrad_img_kernel<true>, grid, dim3(256), ip.lds, stream, ip.a, ipart, ibpart);
     else
-      hipLaunchKernelGGL(conv_wgrad_img_kernel<false>, grid, dim3(256), ip.lds, stream, (const bf16_t*)x,
-                         (const bf16_t*)dy, ip.a, ipart, ibpart);
+      hipLaunchKernelGGL(conv_wgrad_img_kernel<false>, grid, dim3(256), ip.lds, stream, ip.a, ipart, ibpart);
     hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(nwi)), dim3(256), 0, stream, (const float*)ipart, ip.nsplit,
                        nwi, dw);
     if (db)
@@ -1221,21 +1265,41 @@ int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int 
     MZ_LAUNCH_CHECK();
     return 0;
   }
-  {
+  // per-tap tile kernels, one launch pair per segment (accumulated into dw / db in segment order)
+  const long long M = (long long)B * H * W;
+  const long long tiles = (long long)((Cout + 63) / 64) * ((Cin + 63) / 64) * ks * ks;
+  const long long nsplit = wgrad_splits(M, tiles);
+  const int step = dtype ? WB_M : WG_ROWS;
+  const int rps = (int)(((M + nsplit - 1) / nsplit + step - 1) / step * step);
+  const size_t nw = (size_t)Cout * ks * ks * Cin;
+  float* part = (float*)ws;
+  float* bpart = db ? part + nsplit * nw : nullptr;
+  for (int i = 0; i < nseg; ++i) {
     if (dtype == 1)
       hipLaunchKernelGGL(conv_wgrad_bf16_kernel, dim3((unsigned)tiles, (unsigned)nsplit), dim3(256), 0, stream,
-                         (const bf16_t*)x, (const bf16_t*)dy, B, H, W, Cin, Cout, ks, rps, part, bpart);
+                         (const bf16_t*)xs[i], (const bf16_t*)dys[i], B, H, W, Cin, Cout, ks, rps, part, bpart);
     else
       hipLaunchKernelGGL(conv_wgrad_kernel<float>, dim3((unsigned)tiles, (unsigned)nsplit), dim3(256), 0, stream,
-                         (const float*)x, (const float*)dy, B, H, W, Cin, Cout, ks, rps, part, bpart);
+                         (const float*)xs[i], (const float*)dys[i], B, H, W, Cin, Cout, ks, rps, part, bpart);
     hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(nw)), dim3(256), 0, stream, (const float*)part,
                        (int)nsplit, nw, dw);
     if (db)
       hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(Cout)), dim3(256), 0, stream, (const float*)bpart,
                          (int)nsplit, (size_t)Cout, db);
-    MZ_LAUNCH_CHECK();
-    return 0;
   }
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
+                    float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream) {
+  return wgrad_core(dtype, &x, &dy, 1, B, H, W, Cin, Cout, ks, dw, db, ws, ws_bytes, stream);
+}
+
+int mzba_conv_wgrad_segs(int dtype, const void* const* xs, const void* const* dys, int nseg, int B, int H, int W,
+                         int Cin, int Cout, int ks, float* dw, float* db, void* ws, long long ws_bytes,
+                         hipStream_t stream) {
+  return wgrad_core(dtype, xs, dys, nseg, B, H, W, Cin, Cout, ks, dw, db, ws, ws_bytes, stream);
 }
 
 int mzba_avgpool2_backward(int dtype, const void* dy, void* dx, int B, int H, int W, int C, hipStream_t stream) {

@@ -66,6 +66,7 @@ SIGNATURES = {
     "mzba_conv_pack_bf16": [P, P, I, I, I, I, I, I, I, LL, P],
     "mzba_conv_wgrad_set_variant": [I],
     "mzba_conv_wgrad": [I, P, P, I, I, I, I, I, I, P, P, P, LL, P],
+    "mzba_conv_wgrad_segs": [I, P, P, I, I, I, I, I, I, I, P, P, P, LL, P],
     "mzba_avgpool2_backward": [I, P, P, I, I, I, I, P],
     "mzba_axpy": [I, P, P, LL, P],
     "mzba_scale_forward": [I, P, P, P, P, I, I, I, P],

@@ -20,6 +20,7 @@ trained weights load into the acting agent (`load_latest_weights`, train_torch.p
 dtype "f32" is the parity path; "bf16" stores activations and conv weights in bf16 (MFMA
 bf16) with f32 statistics, gradients, Adam state and master weights.
 """
+import ctypes
 from collections import OrderedDict
 
 import numpy as np
@@ -93,8 +94,10 @@ class Learner:
     `training_stage(replay, num_batches, minibatch_size)` = the whole loop.
     """
 
-    def __init__(self, mcfg, state_dict=None, K=5, dtype="f32", lr=None, seed=0, device="cuda"):
+    def __init__(self, mcfg, state_dict=None, K=5, dtype="f32", lr=None, seed=0, device="cuda", defer_wgrad=True):
         L.require_gpu()
+        self.defer_wgrad = defer_wgrad
+        self._pending = None
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.m, self.K, self.device = mcfg, K, torch.device(device)
@@ -361,10 +364,31 @@ class Learner:
         return dt
 
     def _wgrad(self, c, x, dy, B, H, W):
+        if self._pending is not None and (H, W) == self.lat:
+            # latent convs run K times per minibatch with the same weights: their weight gradients
+            # are reduced in one contraction over the K (x, dY) pairs after the unrolled backward
+            self._pending.setdefault(id(c), (c, []))[1].append((x, dy))
+            return
         nb = L.lib().mzba_conv_wgrad_ws_bytes(B, H, W, c.cin_p, c.cout, c.ks)
         ws = self._scratch("wg", nb)
         L.call("mzba_conv_wgrad", self.dt, L.ptr(x), L.ptr(dy), B, H, W, c.cin_p, c.cout, c.ks, L.ptr(c.dw),
                L.ptr(c.db), L.ptr(ws), ws.numel(), L.stream())
+
+    def _flush_wgrad(self, B):
+        """mzba_conv_wgrad_segs over every deferred latent conv (segments in backward order, so
+        per-segment kernels accumulate exactly as the immediate calls would)."""
+        H, W = self.lat
+        for c, segs in self._pending.values():
+            for i in range(0, len(segs), 8):
+                part = segs[i:i + 8]
+                n = len(part)
+                xs = (ctypes.c_void_p * n)(*[t.data_ptr() for t, _ in part])
+                dys = (ctypes.c_void_p * n)(*[t.data_ptr() for _, t in part])
+                nb = L.lib().mzba_conv_wgrad_ws_bytes(n * B, H, W, c.cin_p, c.cout, c.ks)
+                ws = self._scratch("wg", nb)
+                L.call("mzba_conv_wgrad_segs", self.dt, xs, dys, n, B, H, W, c.cin_p, c.cout, c.ks, L.ptr(c.dw),
+                       L.ptr(c.db), L.ptr(ws), ws.numel(), L.stream())
+        self._pending = {}
 
     def _dgrad(self, c, dy, B, H, W, acc=None):
         """Input gradient of conv c (first cin_used channels); added into `acc` when given."""
@@ -464,6 +488,7 @@ class Learner:
         s = L.stream()
         self.G.zero_()
         self._scale_idx = []
+        self._pending = {} if self.defer_wgrad else None
         self._prepare_packs()
         # ---- forward (_k_step_rollout)
         cin_p = self.rep[0][1].cin_p
@@ -547,6 +572,8 @@ class Learner:
             if not self.pred_res:
                 L.call("mzba_axpy", self.dt, L.ptr(gh), L.ptr(gp), gh.numel(), s)
             unroll[k] = None
+        if self._pending:
+            self._flush_wgrad(B)
         # representation: scale -> [pool | res | conv] reversed
         gx = self._scale_bwd(rep_scale, gh, B)
         for kind, mod, sv in reversed(tape):

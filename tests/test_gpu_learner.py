@@ -21,6 +21,7 @@ and bounded by 2 lr against the reference (first-step updates are ~lr * sign(g))
 statistics (forward only): rtol 1e-4 vs the reference. Step 2 starts from the reference's
 post-step-1 parameters, running stats and Adam moments (teacher forcing).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -308,3 +309,70 @@ def test_learner_bf16_conv_packs(case, flip):
     ref = ref.permute(0, 2, 3, 1)
     err = (out.cpu().double() - ref).abs().max().item()
     assert err <= 1e-2 * ref.abs().max().item(), (err, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("case", [("bf16", 1, 5, 512, 4, 5, 256, 256), ("bf16", 2, 3, 7, 4, 5, 64, 64),
+                                  ("bf16", 1, 3, 7, 4, 5, 64, 64), ("f32", 1, 2, 6, 4, 5, 40, 24),
+                                  ("bf16", 2, 8, 16, 8, 10, 128, 128)])
+def test_conv_wgrad_segs_matches_torch(case):
+    """mzba_conv_wgrad_segs (the learner's deferred latent weight gradient: K (x, dY) pairs in
+    one contraction) against the torch fp32 weight gradient of the concatenated segments.
+    variant 1 = automatic (5 x 512 envs at 4x5 -> whole-image kernel, small batches -> one
+    per-tap launch pair per segment), 2 = whole-image kernel forced."""
+    from mzba import _lib as L
+    dt, var, nseg, B, H, W, Cin, Cout = case
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(nseg * 1000 + B)
+    tdt = torch.float32 if dt == "f32" else torch.bfloat16
+    xs = [torch.randn(B, H, W, Cin, generator=g, device=dev).to(tdt) for _ in range(nseg)]
+    dys = [torch.randn(B, H, W, Cout, generator=g, device=dev).to(tdt) for _ in range(nseg)]
+    dw0 = torch.randn(Cout, 9, Cin, generator=g, device=dev)
+    db0 = torch.randn(Cout, generator=g, device=dev)
+    dw, db = dw0.clone(), db0.clone()
+    nb = L.lib().mzba_conv_wgrad_ws_bytes(nseg * B, H, W, Cin, Cout, 3)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    xp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in xs])
+    dp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in dys])
+    L.call("mzba_conv_wgrad_set_variant", var)
+    try:
+        L.call("mzba_conv_wgrad_segs", 0 if dt == "f32" else 1, xp, dp, nseg, B, H, W, Cin, Cout, 3, L.ptr(dw),
+               L.ptr(db), L.ptr(ws), nb, L.stream())
+    finally:
+        L.call("mzba_conv_wgrad_set_variant", 1)
+    x = torch.cat(xs).float().permute(0, 3, 1, 2)
+    dy = torch.cat(dys).float().permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dy, padding=1)
+    ref = ref.permute(0, 2, 3, 1).reshape(Cout, 9, Cin) + dw0
+    refb = dy.sum(dim=(0, 2, 3)) + db0
+    tol = 1e-4 if dt == "f32" else 2e-3
+    assert (dw - ref).abs().max().item() <= tol * ref.abs().max().item()
+    assert (db - refb).abs().max().item() <= tol * refb.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_learner_deferred_wgrad(dt):
+    """Deferring the latent weight gradients to one segmented contraction after the unrolled
+    backward: f32 (per-segment launches in backward order) is bit-identical to the immediate
+    calls; bf16 with the whole-image kernel forced differs only in f32 summation order."""
+    from mzba import _lib as L
+    from mzba.config import learner_model_cfg
+    from mzba.learner import Learner
+    from mzba.weights import init_state_dict
+    mcfg = learner_model_cfg()
+    ring = _random_ring(64, mcfg["state_history_length"], 5, 3)
+    out = {}
+    L.call("mzba_conv_wgrad_set_variant", 2 if dt == "bf16" else 1)
+    try:
+        for defer in (False, True):
+            ln = Learner(mcfg, init_state_dict(mcfg, 8), K=5, dtype=dt, defer_wgrad=defer)
+            out[defer] = (ln.train_minibatch(ring, ring.slots()).cpu().numpy(), ln.gradients())
+            del ln
+    finally:
+        L.call("mzba_conv_wgrad_set_variant", 1)
+    np.testing.assert_array_equal(out[True][0], out[False][0])
+    for k, g0 in out[False][1].items():
+        g1 = out[True][1][k]
+        if dt == "f32":
+            assert torch.equal(g0, g1), k
+        else:
+            assert (g1 - g0).abs().max().item() <= 1e-4 * g0.abs().max().item() + 1e-7, k
