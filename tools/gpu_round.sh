@@ -6,7 +6,8 @@ TAG=${1:-run}
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1 && echo "pytest ok"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 && echo "pytest ok"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo "smoke ok"
 tail -2 $O/pytest.log
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err && echo "bench ok"
 cat $O/bench.json
