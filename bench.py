@@ -180,6 +180,10 @@ def run_learner(args, world, rank, local):
     slots = [torch.randperm(cap, device=dev, generator=g)[:B].to(torch.int32) for _ in range(args.warmup + args.steps)]
     for i in range(args.warmup):
         ln.train_minibatch(ring, slots[i])
+    if not args.no_graph:  # the whole minibatch as one HIP graph (after an eager one: packs, scratch)
+        if args.warmup == 0:
+            ln.train_minibatch(ring, slots[0])
+        ln.capture(ring, B)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -238,6 +242,7 @@ def run_learner(args, world, rank, local):
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
                          "traffic": None, "flop_per_minibatch": fl, "avg_launch_ms": kms},
             "loss": float(loss[0]),
+            "launch": "eager" if args.no_graph else "hip-graph replay of the whole minibatch",
             "cpu_baseline": cpu,
         }))
     if world > 1:

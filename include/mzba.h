@@ -100,7 +100,8 @@ int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_
  * followed by 8*64*8 padding elements (the weight ring prefetches 8 k steps past the end; see
  * DESIGN.md §conv_lat); a workgroup keeps E = 160/(H*W) envs' activations in LDS. */
 int mzba_conv_lat_supported(int H, int W, int Cin, int Cout, int ks);
-/* Kernel shape selection for A/B experiments (0 = default 8-wave kernel, 1 = 4-wave 2-tile kernel). */
+/* Kernel shape selection for A/B experiments (0 = default 8-wave kernel, with 3-row-tile workgroups
+ * where the 5-tile grid would leave CUs idle; 1 = 4-wave 2-tile kernel; 2 = 5-row-tile workgroups only). */
 int mzba_conv_lat_set_variant(int v);
 int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                   const void* wf, const float* bias, const float* act_bias, const int32_t* act, int A,
@@ -359,6 +360,10 @@ int mzba_learner_loss(const float* logit_r, const float* logit_v, const float* l
  * neg_step = -lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t) in double (python float semantics). */
 int mzba_adam(float* p, const float* grad, float* m, float* v, long long n, float neg_step, float one_m_b1, float b2,
               float one_m_b2, float bc2_sqrt, float eps, float weight_decay, hipStream_t stream);
+/* The same with the scalars in device memory: scalars = {neg_step, 1-b1, b2, 1-b2, bc2_sqrt, eps,
+ * weight_decay} (f32[7]), so a captured minibatch graph replays with per-step bias corrections. */
+int mzba_adam_dev(float* p, const float* grad, float* m, float* v, long long n, const float* scalars,
+                  hipStream_t stream);
 /* Representation input of a minibatch (_prepare_minibatch + _encode_actions, train_torch.py:437-470,
  * 279-293) straight from the replay ring: out [B][HW][Cp] = (lut[frame code] x L, a/3 x L, 0...). */
 int mzba_learner_input(int dtype, const uint8_t* states, const int64_t* past_actions, const int32_t* slots,

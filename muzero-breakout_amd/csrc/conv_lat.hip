@@ -61,10 +61,10 @@ struct LatArgs {
 // reduced through LDS; (2) finish 16-B output chunks: + residual, ReLU, bf16, 16-B stores.
 // Bias and the per-(pixel, action) bias were folded into the accumulator init.
 constexpr int EPT_MAX = 10;
-template <int NT>
+template <int NT, int MR = MAXROWS>
 __device__ __forceinline__ void lat_res_prefetch(const LatArgs& a, uint4 (&rv)[EPT_MAX], int rows, int env0, int HW,
                                                  int tid) {
-  constexpr int EPT = (MAXROWS * 16 + NT - 1) / NT;
+  constexpr int EPT = (MR * 16 + NT - 1) / NT;
   const int ncols = min(128, a.Cout - blockIdx.y * 128);
   const int ncb = ncols / 8;
   const int nchunks = rows * ncb;
@@ -79,10 +79,10 @@ __device__ __forceinline__ void lat_res_prefetch(const LatArgs& a, uint4 (&rv)[E
     }
   }
 }
-template <int NT>
+template <int NT, int MR = MAXROWS>
 __device__ __forceinline__ void lat_epilogue(const LatArgs& a, const float* ot, const uint4 (&rv)[EPT_MAX], int rows,
                                              int env0, int HW, int tid) {
-  constexpr int EPT = (MAXROWS * 16 + NT - 1) / NT;
+  constexpr int EPT = (MR * 16 + NT - 1) / NT;
   const int ncols = min(128, a.Cout - blockIdx.y * 128);
   const int ncb = ncols / 8;
   const int nchunks = rows * ncb;
@@ -128,8 +128,11 @@ __device__ __forceinline__ float lat_acc_init(const LatArgs& a, float bias_n, in
   return v;
 }
 
-template <int KS, int CIN, int WAVES, int DMAX>
+// RT: 32-row tiles per workgroup (5: E*HW <= 160; 3: E*HW <= 96, twice the workgroups for the
+// learner's B = 512 latent convs, whose 5-tile grid fills only half the CUs)
+template <int KS, int CIN, int WAVES, int DMAX, int RT = R>
 __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs a) {
+  constexpr int MAXROWS = 32 * RT;
   constexpr int KSPLIT = WAVES / 4;      // channel groups per tap (1: 4 waves, 2: 8 waves)
   constexpr int NC = CIN / 16;           // k steps per tap
   constexpr int NH = NC / KSPLIT;        // k steps per tap per wave
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
   static_assert(NH % D == 0, "ring / tap alignment");
   constexpr int LDS_A = (MAXROWS + 1) * ROWB, LDS_C = MAXROWS * 128 * 4;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_A > LDS_C ? LDS_A : LDS_C];
-  __shared__ long long envoff[32 * R];
+  __shared__ long long envoff[32 * RT];
   const int HW = a.H * a.W;
   const int env0 = blockIdx.x * a.E;
   const int nenv = min(a.E, a.B - env0);
@@ -197,19 +200,19 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
   MZ_STAMP(1);
 
   const int l32 = lane & 31, h = lane >> 5;
-  f32x16 acc[R];
+  f32x16 acc[RT];
 #pragma unroll
-  for (int rt = 0; rt < R; ++rt)
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       acc[rt][i] = (active && kh == 0) ? lat_acc_init(a, bias_n, rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h, rows,
                                                      ct * 32 + l32, env0, HW)
                                        : 0.f;
   if (active) {
-    int ry[R], rx[R], rbase[R];
-    bool rval[R];
+    int ry[RT], rx[RT], rbase[RT];
+    bool rval[RT];
 #pragma unroll
-    for (int rt = 0; rt < R; ++rt) {
+    for (int rt = 0; rt < RT; ++rt) {
       const int m = rt * 32 + l32;
       rval[rt] = m < rows;
       const int e = m / HW, p = m - (m / HW) * HW;
@@ -218,10 +221,10 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
       rbase[rt] = e * HW;
     }
     // LDS byte offset of this lane's source row for tap t, and its chunk swizzle (<< 4)
-    auto tap_rows = [&](int tap, int (&off)[R], int (&sw)[R]) {
+    auto tap_rows = [&](int tap, int (&off)[RT], int (&sw)[RT]) {
       const int ky = tap / KS - PAD, kx = tap % KS - PAD;
 #pragma unroll
-      for (int rt = 0; rt < R; ++rt) {
+      for (int rt = 0; rt < RT; ++rt) {
         const int sy = ry[rt] + ky, sx = rx[rt] + kx;
         const bool ok = rval[rt] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
         const int r = ok ? rbase[rt] + sy * a.W + sx : MAXROWS;
@@ -230,11 +233,11 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
       }
     };
     const int cbase = kh * (2 * NH) + h;  // 16-B chunk of this lane's 8 channels at step 0 of a tap
-    int offc[R], swc[R], offn[R], swn[R];
+    int offc[RT], swc[RT], offn[RT], swn[RT];
     tap_rows(0, offc, swc);
-    bf16x8 afc[R], afn[R];
+    bf16x8 afc[RT], afn[RT];
 #pragma unroll
-    for (int rt = 0; rt < R; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
       afc[rt] = *reinterpret_cast<const bf16x8*>(lds + offc[rt] + ((cbase << 4) ^ swc[rt]));
     for (int tap = 0; tap < KS * KS; ++tap) {
       // next tap's source rows (the last tap re-reads its own rows: harmless, branch-free)
@@ -252,7 +255,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
         // MFMA on this step's fragment, then issue the next step's read of the same row tile:
         // it has the 4 following MFMAs (~128 cycles) to land.
 #pragma unroll
-        for (int rt = 0; rt < R; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
 #if defined(MZ_LAT_ABLATE) && MZ_LAT_ABLATE == 3
           asm volatile("" ::"v"(afc[rt]), "v"(bfr));  // ablation: no MFMA
 #else
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
         // interleave {MFMA, DS read, VALU} x R, then the weight load; the reads' consumers are
         // behind the step barrier, so no MFMA waits on a read issued in its own step
 #pragma unroll
-        for (int rt = 0; rt < R; ++rt) {
+        for (int rt = 0; rt < RT; ++rt) {
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
@@ -276,10 +279,10 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int rt = 0; rt < R; ++rt) afc[rt] = afn[rt];
+        for (int rt = 0; rt < RT; ++rt) afc[rt] = afn[rt];
       }
 #pragma unroll
-      for (int rt = 0; rt < R; ++rt) { offc[rt] = offn[rt]; swc[rt] = swn[rt]; }
+      for (int rt = 0; rt < RT; ++rt) { offc[rt] = offn[rt]; swc[rt] = swn[rt]; }
     }
   }
 
@@ -288,20 +291,20 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
   // + bias (+ act bias) (+ residual, 16-B loads), ReLU, bf16, 16-B stores.
   MZ_STAMP(3);
   uint4 rv[EPT_MAX];
-  lat_res_prefetch<NT>(a, rv, rows, env0, HW, tid);
+  lat_res_prefetch<NT, MAXROWS>(a, rv, rows, env0, HW, tid);
   __syncthreads();  // every wave is done reading the A tile
   MZ_STAMP(4);
   float* ot = reinterpret_cast<float*>(lds);
   if (active && kh == 0) {
 #pragma unroll
-    for (int rt = 0; rt < R; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) ot[(rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 128 + wq * 32 + l32] = acc[rt][r];
   }
   __syncthreads();
   if (active && kh == 1 && KSPLIT == 2) {
 #pragma unroll
-    for (int rt = 0; rt < R; ++rt)
+    for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         float* p = ot + (rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 128 + wq * 32 + l32;
@@ -309,7 +312,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
       }
   }
   __syncthreads();
-  lat_epilogue<NT>(a, ot, rv, rows, env0, HW, tid);
+  lat_epilogue<NT, MAXROWS>(a, ot, rv, rows, env0, HW, tid);
   MZ_STAMP(5);
 }
 
@@ -497,10 +500,23 @@ static int g_lat_variant = 0;  // kernel shape (experiments): see mzba_conv_lat_
 
 extern "C" {
 
-// 0: 8 waves (2 per SIMD: 4 column tiles x 2 channel halves), the default;
-// 1: 4 waves with 2 column tiles each (conv_lat2_kernel, experiment). Same weight packing.
+static int lat_ncu() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// 0: 8 waves (2 per SIMD: 4 column tiles x 2 channel halves), the default (3-row-tile workgroups
+//    where the 5-tile grid would leave CUs idle);
+// 1: 4 waves with 2 column tiles each (conv_lat2_kernel, experiment). Same weight packing;
+// 2: the default kernel with 5-row-tile workgroups only (A/B reference).
 int mzba_conv_lat_set_variant(int v) {
-  if (v < 0 || v > 1) return -1;
+  if (v < 0 || v > 2) return -1;
   g_lat_variant = v;
   return 0;
 }
@@ -526,22 +542,34 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
   MZ_CHECK_ARG(B > 0 && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
   MZ_CHECK_ARG(!act_bias || (act && A > 0), -3);
   const int HW = H * W;
-  const int E = (32 * R) / HW;
+  const int ny = (Cout + 127) / 128;
+  int E = (32 * R) / HW;
+  // 3-tile workgroups (E3 envs) when the 5-tile grid leaves CUs idle and the smaller tiles add
+  // workgroups (learner B = 512 at 4x5: 128 -> 256); the per-element arithmetic is the same
+  const int E3 = (32 * 3) / HW;
+  const bool rt3 = g_lat_variant == 0 && E3 >= 1 && (long long)((B + E - 1) / E) * ny < lat_ncu() &&
+                   (B + E3 - 1) / E3 > (B + E - 1) / E && Cin >= 128;
+  if (rt3) E = E3;
   LatArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (const bf16_t*)wf, bias, act_bias, act, A,
             (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, relu, E};
-  dim3 grid((B + E - 1) / E, (Cout + 127) / 128);
+  dim3 grid((B + E - 1) / E, ny);
   const int v = g_lat_variant;
 #define MZ_LAT(KS_, CIN_, W_, D_) \
   if (ks == KS_ && Cin == CIN_) { hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, W_, D_>), grid, dim3(64 * W_), 0, stream, a); }
+#define MZ_LAT3(KS_, CIN_) \
+  if (ks == KS_ && Cin == CIN_) { hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, 8, 8, 3>), grid, dim3(512), 0, stream, a); }
   if (v == 1) {
     if (ks == 3 && Cin == 256) hipLaunchKernelGGL((conv_lat2_kernel<3, 256>), grid, dim3(256), 0, stream, a);
     else if (ks == 1 && Cin == 256) hipLaunchKernelGGL((conv_lat2_kernel<1, 256>), grid, dim3(256), 0, stream, a);
     else return -4;
+  } else if (rt3) {
+    MZ_LAT3(3, 256) else MZ_LAT3(1, 256) else MZ_LAT3(3, 128) else MZ_LAT3(1, 128)
   } else {
     MZ_LAT(3, 256, 8, 8) else MZ_LAT(1, 256, 8, 8) else MZ_LAT(3, 128, 8, 8) else MZ_LAT(1, 128, 8, 8)
     else MZ_LAT(3, 64, 8, 8) else MZ_LAT(1, 64, 8, 8)
   }
 #undef MZ_LAT
+#undef MZ_LAT3
   MZ_LAUNCH_CHECK();
   return 0;
 }

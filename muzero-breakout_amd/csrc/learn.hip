@@ -1056,6 +1056,22 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ gra
   }
 }
 
+// the same with the step-dependent scalars read from device memory (sc = {neg_step, 1-b1, b2, 1-b2,
+// bc2s, eps, wd}): a captured minibatch graph replays with the host refreshing sc per step
+__global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__ grad, float* __restrict__ m,
+                                float* __restrict__ v, size_t n, const float* __restrict__ sc) {
+  const float neg_step = sc[0], one_m_b1 = sc[1], b2 = sc[2], one_m_b2 = sc[3], bc2s = sc[4], eps = sc[5], wd = sc[6];
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float pv = p[i];
+    const float g = grad[i] + wd * pv;
+    const float mv = m[i] + one_m_b1 * (g - m[i]);
+    const float vv = v[i] * b2 + (one_m_b2 * g) * g;
+    m[i] = mv;
+    v[i] = vv;
+    p[i] = pv + (neg_step * mv) / (sqrtf(vv) / bc2s + eps);
+  }
+}
+
 // ------------------------------------------------------------------ learner inputs
 // rep input [B][HW][Cp]: channel c < L = lut[frame code], L <= c < 2L = a/3 (train_torch.py:279-293,
 // 437-470), zero beyond 2L. states u8 ring [cap][L][HW], past_actions i64 ring [cap][L].
@@ -1406,6 +1422,16 @@ int mzba_adam(float* p, const float* grad, float* m, float* v, long long n, floa
   if (n == 0) return 0;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, stream, p, grad, m, v, (size_t)n, neg_step,
                      one_m_b1, b2, one_m_b2, bc2_sqrt, eps, weight_decay);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_adam_dev(float* p, const float* grad, float* m, float* v, long long n, const float* scalars,
+                  hipStream_t stream) {
+  MZ_CHECK_ARG(p && grad && m && v && scalars && n >= 0, -1);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, stream, p, grad, m, v, (size_t)n,
+                     scalars);
   MZ_LAUNCH_CHECK();
   return 0;
 }

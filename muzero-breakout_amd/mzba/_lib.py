@@ -76,6 +76,7 @@ SIGNATURES = {
     "mzba_linear_backward": [I, P, P, P, P, I, P, P, I, I, I, P, LL, P],
     "mzba_learner_loss": [P, P, P, P, P, P, P, I, I, I, I, F, F, P, P, P, P, P],
     "mzba_adam": [P, P, P, P, LL, F, F, F, F, F, F, F, P],
+    "mzba_adam_dev": [P, P, P, P, LL, P, P],
     "mzba_learner_input": [I, P, P, P, P, P, I, I, I, I, P],
     "mzba_dyn_input": [I, P, P, P, I, I, P, I, I, I, I, I, P],
 }

@@ -98,6 +98,8 @@ class Learner:
         L.require_gpu()
         self.defer_wgrad = defer_wgrad
         self._pending = None
+        self._graph = None        # captured minibatch (capture()), replayed by train_minibatch
+        self._capturing = False
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' or 'bf16'")
         self.m, self.K, self.device = mcfg, K, torch.device(device)
@@ -156,6 +158,7 @@ class Learner:
 
     def load_state_dict(self, sd):
         """Reference `MuZeroAgent.state_dict()` keys / shapes (also resets the Adam state)."""
+        self._graph = None  # the running-stat tensors below are new: a captured graph would miss them
         with torch.no_grad():
             self.P.zero_()
             for key, p in self.params.items():
@@ -478,7 +481,46 @@ class Learner:
     def train_minibatch(self, ring, slots):
         """One `_training_stage` iteration on replay windows `slots` (i32 ring rows) of `ring`
         (a DeviceReplayBuffer, or any object with the same `_ring` dict). Returns the device
-        loss vector (total, reward, value, policy)."""
+        loss vector (total, reward, value, policy). Replays the captured graph (capture()) when
+        it was captured for this ring and minibatch size."""
+        if self._graph is not None and ring is self._g_ring and slots.numel() == self._g_slots.numel():
+            self._g_slots.copy_(slots.to(device=self.device, dtype=torch.int32))
+            self.step_count += 1
+            self._adam_sc.copy_(torch.tensor(self._adam_scalars(self.step_count), dtype=torch.float32))
+            self._graph.replay()
+            for k, d in self._nbt_step.items():
+                self.nbt[k] += d
+            return self._g_loss
+        return self._minibatch(ring, slots)
+
+    def _adam_scalars(self, t):
+        b1, b2 = BETAS
+        return [-(self.lr / (1 - b1 ** t)), 1 - b1, b2, 1 - b2, (1 - b2 ** t) ** 0.5, ADAM_EPS, WEIGHT_DECAY]
+
+    def capture(self, ring, B):
+        """Capture one minibatch of B windows of `ring` as a HIP graph (torch.cuda.graph: every
+        activation in the graph's private pool; slots read from a static buffer, Adam's bias
+        corrections from a device scalar block), so a minibatch is one graph launch from the
+        host. Call after at least one eager minibatch of the same size (weight packs and scratch
+        buffers allocated). Replays are launch-for-launch the eager minibatch (bit-identical)."""
+        self._graph = None
+        self._g_slots = torch.zeros(B, dtype=torch.int32, device=self.device)
+        self._adam_sc = torch.zeros(7, dtype=torch.float32, device=self.device)
+        nbt0, step0 = dict(self.nbt), self.step_count
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        self._capturing = True
+        try:
+            with torch.cuda.graph(g):
+                loss = self._minibatch(ring, self._g_slots)
+        finally:
+            self._capturing = False
+        # capture records launches without running them: undo its host-side counters
+        self._nbt_step = {k: self.nbt[k] - nbt0[k] for k in self.nbt}
+        self.nbt, self.step_count = nbt0, step0
+        self._graph, self._g_ring, self._g_loss = g, ring, loss
+
+    def _minibatch(self, ring, slots):
         g = ring._ring
         slots = slots.to(device=self.device, dtype=torch.int32).contiguous()
         B, K, Lh = slots.numel(), self.K, self.hist
@@ -591,10 +633,12 @@ class Learner:
                 gx = self._dgrad(mod, gx, B, hh2, ww2) if mod is not self.rep[0][1] else None
         # ---- Adam (networks.py:268)
         self.step_count += 1
-        t = self.step_count
-        b1, b2 = BETAS
-        L.call("mzba_adam", L.ptr(self.P), L.ptr(self.G), L.ptr(self.M1), L.ptr(self.M2), self.n_flat,
-               -(self.lr / (1 - b1 ** t)), 1 - b1, b2, 1 - b2, (1 - b2 ** t) ** 0.5, ADAM_EPS, WEIGHT_DECAY, s)
+        if self._capturing:
+            L.call("mzba_adam_dev", L.ptr(self.P), L.ptr(self.G), L.ptr(self.M1), L.ptr(self.M2), self.n_flat,
+                   L.ptr(self._adam_sc), s)
+        else:
+            L.call("mzba_adam", L.ptr(self.P), L.ptr(self.G), L.ptr(self.M1), L.ptr(self.M2), self.n_flat,
+                   *self._adam_scalars(self.step_count), s)
         return loss
 
     def flops_per_minibatch(self, B):

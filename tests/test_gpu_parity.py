@@ -417,6 +417,36 @@ def test_acting_loop_f32_matches_oracle_episode():
         np.testing.assert_allclose(trajs[b].values[L_:], np.array(otrajs[b].values[L_:], np.float32), rtol=1e-4, atol=1e-5)
 
 
+def test_acting_loop_84x84_config3_geometry_matches_oracle():
+    """BASELINE config 3's geometry as a parity case: 84x84 frames (parallel_breakout.py reads
+    self.height / self.width everywhere), 4-frame stack (8 input planes), latent 21x21 after the
+    two avg-pools, reduced-width f32 nets; trajectories, visit counts, rewards and frames equal
+    the oracle's run_episode at the same size (injected noise)."""
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingLoop
+    cfg = _small_cfg(8)
+    mcfg = cfg["model"]
+    mcfg["latent_resolution"] = [21, 21]
+    sd = init_state_dict(mcfg, 11)
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(sd)
+    B, seed, T = 3, 77, 5
+    loop = ActingLoop(cfg, ag, B, seed=seed, max_steps=T, height=84, width=84)
+    loop.noise_log = []
+    trajs = loop.run_episode(0)
+    noises = [n.cpu().numpy() for n in loop.noise_log]
+    otrajs, _ = run_episode(cfg, sd, seed, 0, lambda sid, n: noises[sid], B, max_steps=T, height=84, width=84)
+    L_ = mcfg["state_history_length"]
+    for b in range(B):
+        assert trajs[b].length == otrajs[b].length
+        np.testing.assert_array_equal(trajs[b].actions, otrajs[b].actions)
+        np.testing.assert_array_equal(np.stack([c.numpy() for c in trajs[b].visit_counts[L_:]]),
+                                      np.stack(otrajs[b].visit_counts[L_:]) if otrajs[b].length else np.zeros((0, 3)))
+        np.testing.assert_array_equal(np.array(trajs[b].rewards[L_:], np.float32), np.array(otrajs[b].rewards[L_:], np.float32))
+        np.testing.assert_array_equal(np.stack([s.numpy() for s in trajs[b].states]), np.stack(otrajs[b].states))
+        np.testing.assert_allclose(trajs[b].values[L_:], np.array(otrajs[b].values[L_:], np.float32), rtol=1e-4, atol=1e-5)
+
+
 def _pack_wf(wp, cout):
     K = wp.shape[1]
     wf = wp.reshape(cout // 32, 32, K // 16, 2, 8).transpose(0, 2, 3, 1, 4).reshape(-1)
@@ -424,6 +454,7 @@ def _pack_wf(wp, cout):
 
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,ks", [(7, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 3), (9, 4, 5, 256, 128, 3),
+                                                (512, 4, 5, 256, 256, 3), (511, 4, 5, 128, 256, 1),
                                                 (13, 4, 5, 256, 256, 1), (5, 8, 10, 256, 256, 3), (3, 4, 5, 64, 64, 3),
                                                 (17, 4, 5, 64, 32, 1), (4, 8, 10, 128, 128, 3)])
 def test_conv_lat_vs_torch(B, H, W, Cin, Cout, ks):
@@ -455,6 +486,17 @@ def test_conv_lat_vs_torch(B, H, W, Cin, Cout, ks):
            Cout, ks, 1, L.stream())
     err = (out.float().cpu() - ref).abs().max().item() / max(1.0, ref.abs().max().item())
     assert err < 1e-2, err
+    # 3-row-tile workgroups (chosen where the 5-tile grid leaves CUs idle) vs 5-tile ones: the
+    # per-element arithmetic is the same, so the outputs are bit-identical
+    out5 = torch.empty_like(out)
+    L.call("mzba_conv_lat_set_variant", 2)
+    try:
+        L.call("mzba_conv_lat", L.ptr(d["pool"]), S1 * H * W * Cin, L.ptr(d["slot"]), H * W * Cin, L.ptr(wf),
+               L.ptr(d["b"]), L.ptr(d["ab"]), L.ptr(d["act"]), A, L.ptr(d["res"]), L.ptr(out5), B, H, W, Cin,
+               Cout, ks, 1, L.stream())
+    finally:
+        L.call("mzba_conv_lat_set_variant", 0)
+    assert torch.equal(out, out5)
 
 
 def test_acting_graph_replay_matches_eager():
