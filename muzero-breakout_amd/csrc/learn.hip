@@ -636,12 +636,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
     const bf16_t* xb = a.xs[sg] + (size_t)bl * img_x;
     const bf16_t* db = a.dys[sg] + (size_t)bl * img_dy;
     if (base == 0) {
+      // unconditional loads (zero chunks read the stage base, then select): a load under a
+      // branch is waited for inside the branch, which serialised the 12 loads of a stage
 #pragma unroll
-      for (int u = 0; u < WI_PF; ++u) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (soff[u] >= 0) v = *reinterpret_cast<const uint4*>(((sdy >> u) & 1u ? db : xb) + soff[u]);
-        pf[u] = v;
-      }
+      for (int u = 0; u < WI_PF; ++u)
+        pf[u] = *reinterpret_cast<const uint4*>(((sdy >> u) & 1u ? db : xb) + (soff[u] >= 0 ? soff[u] : 0));
+#pragma unroll
+      for (int u = 0; u < WI_PF; ++u)
+        if (soff[u] < 0) pf[u] = make_uint4(0, 0, 0, 0);
       return;
     }
 #pragma unroll
@@ -702,20 +704,26 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
         const int c = wr * 32 + i * 16 + 4 * pp;
         af[i] = tr_frag_at(ldy + (size_t)r0 * WI_LD + c, ldy + (size_t)r1 * WI_LD + c);
       }
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
+      // B fragments one tap ahead: tap t + 1's transposed reads are in flight during tap t's MFMAs
+      auto bload = [&](int t, bf16x8_t (&b)[2]) {
         const int off = (t / 3 - 1) * Wp + (t % 3 - 1);
-        bf16x8_t bfr[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int c = wc * 32 + j * 16 + 4 * pp;
-          bfr[j] = tr_frag_at(lx + (ptrdiff_t)(x0 + off) * WI_LD + c, lx + (ptrdiff_t)(x1 + off) * WI_LD + c);
+          b[j] = tr_frag_at(lx + (ptrdiff_t)(x0 + off) * WI_LD + c, lx + (ptrdiff_t)(x1 + off) * WI_LD + c);
         }
+      };
+      bf16x8_t bcur[2], bnxt[2];
+      bload(0, bcur);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t + 1 < 9) bload(t + 1, bnxt);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j)
-            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[t][i][j], 0, 0, 0);
+            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[t][i][j], 0, 0, 0);
+        if (t + 1 < 9) { bcur[0] = bnxt[0]; bcur[1] = bnxt[1]; }
       }
     }
   }
@@ -769,6 +777,7 @@ static bool wgrad_img_plan(int B, int Bseg, int H, int W, int Cin, int Cout, WgP
   p.pf = staged(E) * 8 <= WI_PF * 256;
   const int tiles = ((Cout + 63) / 64) * ((Cin + 63) / 64);
   const int stages = (B + E - 1) / E;
+  // one workgroup per CU (two per CU measured slower: the extra split partials cost more)
   int nsplit = (256 + tiles - 1) / tiles;
   if (nsplit > stages) nsplit = stages;
   const int sps = (stages + nsplit - 1) / nsplit;
@@ -1230,13 +1239,12 @@ long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int k
 
 // the whole-image kernel over nseg segments of B envs (false: shape not supported by it)
 static bool wgrad_img_eligible(int dtype, int nseg, int B, int H, int W, int Cin, int Cout, int ks, WgPlan& ip) {
-  // it wins where an image has many pixels per tap re-read (8x10: 216 vs 270 us, 16x20: 155 vs
-  // 284 us at B = 512) and, at 4x5, once the K unrolled uses of a conv reduce in one launch
-  // (per-tap kernel: 87 us per use; 5 x 512 at 256 -> 256: 265 vs 399 us). Not for a ragged
-  // channel tile at 4x5: the dynamics ConvBlock's 264 input channels (256 + action planes,
-  // padded) lose (540 vs 456 us; tools/bench_wgrad_segs.py)
+  // it wins where an image has many pixels per tap re-read (8x10: 138 vs 277 us, 16x20: 153 vs
+  // 283 us at B = 512) and, at 4x5, once the K unrolled uses of a conv reduce in one launch
+  // (per-tap kernel: 80 us per use; 5 x 512 at 256 -> 256: 188 vs 401 us, and 362 vs 464 us for
+  // the dynamics ConvBlock's 264 input channels; tools/bench_wgrad_segs.py)
   if (dtype != 1 || ks != 3 || !g_wgrad_img || Cin % 8 || Cout % 8) return false;
-  if (H * W < 64 && !(g_wgrad_img == 2 || (nseg * B >= 2048 && Cin % 64 == 0 && Cout % 64 == 0))) return false;
+  if (H * W < 64 && !(g_wgrad_img == 2 || nseg * B >= 2048)) return false;
   return wgrad_img_plan(nseg * B, B, H, W, Cin, Cout, ip);
 }
 
