@@ -107,6 +107,17 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
                   const void* wf, const float* bias, const float* act_bias, const int32_t* act, int A,
                   const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
                   hipStream_t stream);
+/* Learner (bf16, no bias fold, no ReLU): conv_lat of an NHWC batch with the consuming BatchNorm's
+ * per-workgroup batch statistics computed in the epilogue (replaces bn_stats_partial /
+ * bn_backward's partial pass, learn.hip). mode 1: part[chunk][Cout] = (mean, M2) of the bf16
+ * outputs over the chunk's rows (-> mzba_bn_stats_final); mode 2: out = bf16(conv + res) * [y > 0]
+ * (the ReLU mask of the BN output y) and part[chunk][Cout] = (sum g, sum g (x - mean)) with x the
+ * BN input, mean = stats row 0 (-> mzba_bn_backward_final). Cout % 128 == 0; res may alias out.
+ * mzba_conv_lat_bn_chunks gives the chunk count (part has nchunk * Cout float2) and rows per chunk. */
+int mzba_conv_lat_bn_chunks(int B, int H, int W, int Cin, int Cout, int ks, int* nchunk, int* rpc);
+int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const void* res, void* out, int B, int H,
+                     int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
+                     const float* mean, hipStream_t stream);
 
 /* Fused residual tower: nblocks ResidualBlock(256) on the 4x5 latent in ONE launch (networks.py:19-35,
  * 124-131, 190-197); a workgroup keeps 4 (or, for B >= 8 x CUs, 8) envs' activations in LDS for the
@@ -304,6 +315,15 @@ int mzba_bn_apply(int dtype, const void* x, const float* stats, const void* res,
  * C % 4 == 0; ws >= ceil(M/64)*C*8 + 12*C bytes. */
 int mzba_bn_backward(int dtype, void* dy, const void* y, const void* x, const float* stats, int M, int C,
                      float* dgamma, float* dbeta, void* dx, void* ws, long long ws_bytes, hipStream_t stream);
+/* The final passes of mzba_bn_stats / mzba_bn_backward from per-chunk partials computed elsewhere
+ * (mzba_conv_lat_bn): chunk k covers rows [k*rpc, min(M, (k+1)*rpc)). backward: g is already
+ * ReLU-masked; ws >= 12*C bytes. */
+int mzba_bn_stats_final(const float* part, int nchunk, int rpc, int M, int C, float eps, float momentum,
+                        const float* gamma, const float* beta, float* stats, float* run_mean, float* run_var,
+                        hipStream_t stream);
+int mzba_bn_backward_final(int dtype, const void* g, const void* x, const float* stats, const float* part, int nchunk,
+                           int M, int C, float* dgamma, float* dbeta, void* dx, void* ws, long long ws_bytes,
+                           hipStream_t stream);
 /* Weight packs from the f32 master weights w [Cout][taps][Cin]: flip = 0: cast copy (forward);
  * flip = 1: wt [cin_used][taps][Cout] = w[co][taps-1-tap][ci] (the input-gradient convolution). */
 int mzba_conv_wpack(int dtype, const float* w, void* wt, int Cout, int taps, int Cin, int cin_used, int flip,

@@ -55,6 +55,15 @@ struct LatArgs {
   const bf16_t* res;      // optional [B*HW][Cout]
   bf16_t* out;            // [B*HW][Cout]
   int B, H, W, Cin, Cout, ks, relu, E;
+  // learner: the consuming BatchNorm's batch statistics in the epilogue (mzba_conv_lat_bn), per
+  // workgroup (chunk = blockIdx.x, its rows): smode 1: part[chunk][n] = (mean, M2) of the bf16
+  // outputs; smode 2: the output becomes g = out * [sy > 0] and part[chunk][n] = (sum g,
+  // sum g (sx - smean[n])) — bn_stats_partial / bn_bwd_partial (learn.hip) without their launches
+  int smode;
+  float2* part;
+  const bf16_t* sy;
+  const bf16_t* sx;
+  const float* smean;
 };
 
 // epilogue: (1) issue the residual loads (16 B per lane) so they land while the f32 tile is
@@ -80,12 +89,21 @@ __device__ __forceinline__ void lat_res_prefetch(const LatArgs& a, uint4 (&rv)[E
   }
 }
 template <int NT, int MR = MAXROWS>
-__device__ __forceinline__ void lat_epilogue(const LatArgs& a, const float* ot, const uint4 (&rv)[EPT_MAX], int rows,
+__device__ __forceinline__ void lat_epilogue(const LatArgs& a, float* ot, const uint4 (&rv)[EPT_MAX], int rows,
                                              int env0, int HW, int tid) {
   constexpr int EPT = (MR * 16 + NT - 1) / NT;
   const int ncols = min(128, a.Cout - blockIdx.y * 128);
   const int ncb = ncols / 8;
   const int nchunks = rows * ncb;
+  // smode 2: this thread's chunk column is fixed (ncb = 16 divides NT): register partial sums
+  float sg[8], sd[8], mu[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { sg[j] = 0.f; sd[j] = 0.f; mu[j] = 0.f; }
+  if (a.smode == 2) {
+    const int n0 = blockIdx.y * 128 + (tid % ncb) * 8;
+    const float4 m0 = *reinterpret_cast<const float4*>(a.smean + n0), m1 = *reinterpret_cast<const float4*>(a.smean + n0 + 4);
+    mu[0] = m0.x; mu[1] = m0.y; mu[2] = m0.z; mu[3] = m0.w; mu[4] = m1.x; mu[5] = m1.y; mu[6] = m1.z; mu[7] = m1.w;
+  }
 #pragma unroll
   for (int u = 0; u < EPT; ++u) {
     const int i = u * NT + tid;
@@ -111,7 +129,69 @@ __device__ __forceinline__ void lat_epilogue(const LatArgs& a, const float* ot, 
     o.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
     o.z = (uint32_t)f32_to_bf16(v[4]) | ((uint32_t)f32_to_bf16(v[5]) << 16);
     o.w = (uint32_t)f32_to_bf16(v[6]) | ((uint32_t)f32_to_bf16(v[7]) << 16);
+    if (a.smode == 1) {  // the stored (bf16-rounded) values back into the tile for the column pass
+      const uint32_t w[4] = {o.x, o.y, o.z, o.w};
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = bf16_to_f32((bf16_t)(w[j >> 1] >> (16 * (j & 1))));
+      *reinterpret_cast<float4*>(ot + row * 128 + cc * 8) = make_float4(r[0], r[1], r[2], r[3]);
+      *reinterpret_cast<float4*>(ot + row * 128 + cc * 8 + 4) = make_float4(r[4], r[5], r[6], r[7]);
+    } else if (a.smode == 2) {  // ReLU mask of the BN output, masked g stored, partial sums
+      const uint4 yv = *reinterpret_cast<const uint4*>(a.sy + m * a.Cout + n0);
+      const uint4 xv = *reinterpret_cast<const uint4*>(a.sx + m * a.Cout + n0);
+      const uint32_t w[4] = {o.x, o.y, o.z, o.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w}, xw[4] = {xv.x, xv.y, xv.z, xv.w};
+      uint32_t ow[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int sh = 16 * (j & 1);
+        const bool keep = bf16_to_f32((bf16_t)(yw[j >> 1] >> sh)) > 0.f;
+        const uint32_t gb = keep ? ((w[j >> 1] >> sh) & 0xffffu) : 0u;
+        ow[j >> 1] |= gb << sh;
+        const float g = bf16_to_f32((bf16_t)gb);
+        sg[j] += g;
+        sd[j] += g * (bf16_to_f32((bf16_t)(xw[j >> 1] >> sh)) - mu[j]);
+      }
+      o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    }
     *reinterpret_cast<uint4*>(a.out + m * a.Cout + n0) = o;
+  }
+  if (a.smode == 0) return;
+  __syncthreads();  // the tile holds the rounded outputs (1) / every thread is done with it (2)
+  float* pf = reinterpret_cast<float*>(a.part) + 2 * ((size_t)blockIdx.x * a.Cout + blockIdx.y * 128);
+  if (a.smode == 1) {  // (mean, M2) per column over the rows, NT / 128 threads per column
+    constexpr int TPC = NT / 128;
+    const int col = tid / TPC, q = tid % TPC;
+    float s = 0.f;
+    if (col < ncols)
+      for (int r = q; r < rows; r += TPC) s += ot[r * 128 + col];
+#pragma unroll
+    for (int o = 1; o < TPC; o <<= 1) s += __shfl_xor(s, o);
+    const float mean = s / rows;
+    float m2 = 0.f;
+    if (col < ncols)
+      for (int r = q; r < rows; r += TPC) {
+        const float d = ot[r * 128 + col] - mean;
+        m2 += d * d;
+      }
+#pragma unroll
+    for (int o = 1; o < TPC; o <<= 1) m2 += __shfl_xor(m2, o);
+    if (q == 0 && col < ncols) { pf[2 * col] = mean; pf[2 * col + 1] = m2; }
+    return;
+  }
+  // smode 2: the NT / ncb threads of a chunk column reduce through the tile, in thread order
+  constexpr int G = NT / 16;
+  float* rg = ot;              // [G][128]
+  float* rd = ot + G * 128;    // [G][128]
+  const int grp = tid / ncb, cc = tid % ncb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { rg[grp * 128 + cc * 8 + j] = sg[j]; rd[grp * 128 + cc * 8 + j] = sd[j]; }
+  __syncthreads();
+  if (tid < 2 * 128) {
+    const int col = tid & 127;
+    const float* src = tid < 128 ? rg : rd;
+    float t = 0.f;
+    for (int k = 0; k < G; ++k) t += src[k * 128 + col];
+    if (col < ncols) pf[2 * col + (tid >> 7)] = t;
   }
 }
 
@@ -535,30 +615,31 @@ int mzba_conv_lat_supported(int H, int W, int Cin, int Cout, int ks) {
   return 1;
 }
 
-int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
-                  const void* wf, const float* bias, const float* act_bias, const int32_t* act, int A,
-                  const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
-                  hipStream_t stream) {
-  MZ_CHECK_ARG(B > 0 && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
-  MZ_CHECK_ARG(!act_bias || (act && A > 0), -3);
+// workgroup geometry: envs per workgroup and whether the 3-row-tile kernel runs
+static void lat_geometry(int B, int H, int W, int Cin, int Cout, int& E, bool& rt3) {
   const int HW = H * W;
   const int ny = (Cout + 127) / 128;
-  int E = (32 * R) / HW;
+  E = (32 * R) / HW;
   // 3-tile workgroups (E3 envs) when the 5-tile grid leaves CUs idle and the smaller tiles add
   // workgroups (learner B = 512 at 4x5: 128 -> 256); the per-element arithmetic is the same
   const int E3 = (32 * 3) / HW;
-  const bool rt3 = g_lat_variant == 0 && E3 >= 1 && (long long)((B + E - 1) / E) * ny < lat_ncu() &&
-                   (B + E3 - 1) / E3 > (B + E - 1) / E && Cin >= 128;
+  rt3 = g_lat_variant == 0 && E3 >= 1 && (long long)((B + E - 1) / E) * ny < lat_ncu() &&
+        (B + E3 - 1) / E3 > (B + E - 1) / E && Cin >= 128;
   if (rt3) E = E3;
-  LatArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (const bf16_t*)wf, bias, act_bias, act, A,
-            (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, relu, E};
-  dim3 grid((B + E - 1) / E, ny);
+}
+
+static int lat_launch(LatArgs& a, hipStream_t stream) {
+  bool rt3;
+  lat_geometry(a.B, a.H, a.W, a.Cin, a.Cout, a.E, rt3);
+  const int ks = a.ks, Cin = a.Cin;
+  dim3 grid((a.B + a.E - 1) / a.E, (a.Cout + 127) / 128);
   const int v = g_lat_variant;
 #define MZ_LAT(KS_, CIN_, W_, D_) \
   if (ks == KS_ && Cin == CIN_) { hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, W_, D_>), grid, dim3(64 * W_), 0, stream, a); }
 #define MZ_LAT3(KS_, CIN_) \
   if (ks == KS_ && Cin == CIN_) { hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, 8, 8, 3>), grid, dim3(512), 0, stream, a); }
   if (v == 1) {
+    if (a.smode) return -4;  // the fused statistics ride on the 8-wave kernel only
     if (ks == 3 && Cin == 256) hipLaunchKernelGGL((conv_lat2_kernel<3, 256>), grid, dim3(256), 0, stream, a);
     else if (ks == 1 && Cin == 256) hipLaunchKernelGGL((conv_lat2_kernel<1, 256>), grid, dim3(256), 0, stream, a);
     else return -4;
@@ -572,6 +653,38 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
 #undef MZ_LAT3
   MZ_LAUNCH_CHECK();
   return 0;
+}
+
+int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
+                  const void* wf, const float* bias, const float* act_bias, const int32_t* act, int A,
+                  const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
+                  hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
+  MZ_CHECK_ARG(!act_bias || (act && A > 0), -3);
+  LatArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (const bf16_t*)wf, bias, act_bias, act, A,
+            (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, relu, 0};
+  return lat_launch(a, stream);
+}
+
+int mzba_conv_lat_bn_chunks(int B, int H, int W, int Cin, int Cout, int ks, int* nchunk, int* rpc) {
+  MZ_CHECK_ARG(B > 0 && nchunk && rpc && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
+  int E;
+  bool rt3;
+  lat_geometry(B, H, W, Cin, Cout, E, rt3);
+  *nchunk = (B + E - 1) / E;
+  *rpc = E * H * W;
+  return 0;
+}
+
+int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const void* res, void* out, int B, int H,
+                     int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
+                     const float* mean, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && in && wf && bias && out && part && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
+  MZ_CHECK_ARG(Cout % 128 == 0 && (mode == 1 || (mode == 2 && y && x && mean)), -3);
+  LatArgs a{(const bf16_t*)in, (long long)H * W * Cin, nullptr, 0, (const bf16_t*)wf, bias, nullptr, nullptr, 0,
+            (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, 0, 0,
+            mode, (float2*)part, (const bf16_t*)y, (const bf16_t*)x, mean};
+  return lat_launch(a, stream);
 }
 
 }  // extern "C"

@@ -1153,6 +1153,35 @@ int mzba_bn_stats(int dtype, const void* x, int M, int C, float eps, float momen
   });
 }
 
+int mzba_bn_stats_final(const float* part, int nchunk, int rpc, int M, int C, float eps, float momentum,
+                        const float* gamma, const float* beta, float* stats, float* run_mean, float* run_var,
+                        hipStream_t stream) {
+  MZ_CHECK_ARG(part && stats && gamma && beta && nchunk > 0 && rpc > 0 && M > 0 && C > 0 &&
+               (long long)nchunk * rpc >= M && (long long)(nchunk - 1) * rpc < M, -1);
+  hipLaunchKernelGGL(bn_stats_final_kernel, dim3(C), dim3(64), 0, stream, (const float2*)part, nchunk, rpc, M, C, eps,
+                     momentum, gamma, beta, stats, run_mean, run_var);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_bn_backward_final(int dtype, const void* g, const void* x, const float* stats, const float* part, int nchunk,
+                           int M, int C, float* dgamma, float* dbeta, void* dx, void* ws, long long ws_bytes,
+                           hipStream_t stream) {
+  MZ_CHECK_ARG(g && x && stats && part && dgamma && dbeta && dx && ws && nchunk > 0 && M > 0 && C > 0 && C % 4 == 0,
+               -1);
+  MZ_CHECK_ARG(3LL * C * 4 <= ws_bytes, -2);
+  float* coef = (float*)ws;
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(64), 0, stream, (const float2*)part, nchunk, M, C, stats,
+                       dgamma, dbeta, coef);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for((size_t)M * C / 4)), dim3(256), 0, stream, (const T*)g,
+                       (const T*)x, stats, (const float*)coef, (T*)dx, M, C);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
 int mzba_bn_apply(int dtype, const void* x, const float* stats, const void* res, int relu, void* out, int M, int C,
                   hipStream_t stream) {
   MZ_CHECK_ARG(x && stats && out && M > 0 && C > 0 && C % 4 == 0, -1);

@@ -94,9 +94,14 @@ class Learner:
     `training_stage(replay, num_batches, minibatch_size)` = the whole loop.
     """
 
-    def __init__(self, mcfg, state_dict=None, K=5, dtype="f32", lr=None, seed=0, device="cuda", defer_wgrad=True):
+    def __init__(self, mcfg, state_dict=None, K=5, dtype="f32", lr=None, seed=0, device="cuda", defer_wgrad=True,
+                 fuse_bn=True):
         L.require_gpu()
         self.defer_wgrad = defer_wgrad
+        # bf16: BN batch statistics computed in the epilogue of the conv_lat launch that produces the
+        # BN's input (forward) / output gradient (backward) — mzba_conv_lat_bn
+        self.fuse_bn = fuse_bn
+        self._gpart = {}
         self._pending = None
         self._graph = None        # captured minibatch (capture()), replayed by train_minibatch
         self._capturing = False
@@ -340,18 +345,39 @@ class Learner:
             L.call("mzba_conv2d", self.dt, L.ptr(x), H * W * cin, None, 0, L.ptr(w), L.ptr(bias), None, None, 0,
                    L.ptr(res), L.ptr(out), B, H, W, cin, cout, ks, 0, s)
 
-    def _conv(self, c, x, B, H, W):
-        t = self._act(B * H * W, c.cout)
-        self._run_conv(c.fkind, x, c.cin_p, c.w if self.dt == 0 else c.wf, c.b, None, t, B, H, W, c.cout, c.ks)
-        return t
+    def _fusable(self, kind, cout):
+        return self.fuse_bn and self.dt == 1 and kind == "lat" and cout % 128 == 0
 
-    def _bn(self, c, t, res=None, relu=True):
+    def _lat_bn(self, x, w, bias, res, out, B, H, W, cin, cout, ks, mode, y=None, t=None, stats=None):
+        """mzba_conv_lat_bn: the conv plus its consumer BN's per-workgroup partial statistics."""
+        nc, rpc = ctypes.c_int(), ctypes.c_int()
+        L.call("mzba_conv_lat_bn_chunks", B, H, W, cin, cout, ks, ctypes.byref(nc), ctypes.byref(rpc))
+        part = torch.empty(nc.value * cout * 2, dtype=torch.float32, device=self.device)
+        L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(w), L.ptr(bias), L.ptr(res), L.ptr(out), B, H, W, cin, cout, ks, mode,
+               L.ptr(part), L.ptr(y), L.ptr(t), L.ptr(stats), L.stream())
+        return part, nc.value, rpc.value
+
+    def _conv(self, c, x, B, H, W, bn=False):
+        """Forward conv; bn: a BatchNorm consumes the output (its statistics may ride on the conv).
+        Returns (output, fused partials or None)."""
+        t = self._act(B * H * W, c.cout)
+        if bn and self._fusable(c.fkind, c.cout):
+            return t, self._lat_bn(x, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1)
+        self._run_conv(c.fkind, x, c.cin_p, c.w if self.dt == 0 else c.wf, c.b, None, t, B, H, W, c.cout, c.ks)
+        return t, None
+
+    def _bn(self, c, t, res=None, relu=True, fpart=None):
         M = t.shape[0]
         stats = torch.empty(4, c.cout, dtype=torch.float32, device=self.device)
         rm, rv = self.run[c.bn_key]
-        ws = self._scratch("bn", ((M + 63) // 64) * c.cout * 8 + 12 * c.cout)
-        L.call("mzba_bn_stats", self.dt, L.ptr(t), M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma), L.ptr(c.beta),
-               L.ptr(stats), L.ptr(rm), L.ptr(rv), L.ptr(ws), ws.numel(), L.stream())
+        if fpart is not None:
+            part, nc, rpc = fpart
+            L.call("mzba_bn_stats_final", L.ptr(part), nc, rpc, M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma),
+                   L.ptr(c.beta), L.ptr(stats), L.ptr(rm), L.ptr(rv), L.stream())
+        else:
+            ws = self._scratch("bn", ((M + 63) // 64) * c.cout * 8 + 12 * c.cout)
+            L.call("mzba_bn_stats", self.dt, L.ptr(t), M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma), L.ptr(c.beta),
+                   L.ptr(stats), L.ptr(rm), L.ptr(rv), L.ptr(ws), ws.numel(), L.stream())
         self.nbt[c.bn_key] += 1
         y = self._act(M, c.cout)
         L.call("mzba_bn_apply", self.dt, L.ptr(t), L.ptr(stats), L.ptr(res), int(relu), L.ptr(y), M, c.cout,
@@ -361,6 +387,12 @@ class Learner:
     def _bn_bwd(self, c, dy, y, t, stats):
         M = t.shape[0]
         dt = self._act(M, c.cout)
+        e = self._gpart.pop(id(dy), None)
+        if e is not None and e[0] is dy and e[1] is y:  # dy came masked, partials from its producing conv
+            ws = self._scratch("bnf", 12 * c.cout)
+            L.call("mzba_bn_backward_final", self.dt, L.ptr(dy), L.ptr(t), L.ptr(stats), L.ptr(e[2]), e[3], M, c.cout,
+                   L.ptr(c.dgamma), L.ptr(c.dbeta), L.ptr(dt), L.ptr(ws), ws.numel(), L.stream())
+            return dt
         ws = self._scratch("bn", ((M + 63) // 64) * c.cout * 8 + 12 * c.cout)
         L.call("mzba_bn_backward", self.dt, L.ptr(dy), L.ptr(y), L.ptr(t), L.ptr(stats), M, c.cout, L.ptr(c.dgamma),
                L.ptr(c.dbeta), L.ptr(dt), L.ptr(ws), ws.numel(), L.stream())
@@ -393,10 +425,17 @@ class Learner:
                        L.ptr(c.db), L.ptr(ws), ws.numel(), L.stream())
         self._pending = {}
 
-    def _dgrad(self, c, dy, B, H, W, acc=None):
-        """Input gradient of conv c (first cin_used channels); added into `acc` when given."""
+    def _dgrad(self, c, dy, B, H, W, acc=None, bn=None):
+        """Input gradient of conv c (first cin_used channels); added into `acc` when given.
+        bn = (BN conv, its output y, its input t, its stats): the BatchNorm whose output gradient this
+        is — its ReLU mask and partial sums then ride on this conv (consumed by _bn_bwd)."""
         cu = min(c.cin, self.c1) if c is self.dyn_block else c.cin_p
         out = acc if acc is not None else self._act(B * H * W, cu)
+        if bn is not None and self._fusable(c.dkind, cu):
+            _, y, t, st = bn
+            part, nc, _ = self._lat_bn(dy, c.wt, self._zero, acc, out, B, H, W, c.cout, cu, c.ks, 2, y, t, st)
+            self._gpart[id(out)] = (out, y, part, nc)
+            return out
         self._run_conv(c.dkind, dy, c.cout, c.wt, self._zero, acc, out, B, H, W, cu, c.ks)
         return out
 
@@ -417,40 +456,46 @@ class Learner:
     # -- blocks: forward returns (out, saved); backward takes the output gradient ------------------------
     def _res_fwd(self, r, x, B, H, W):
         c1, c2 = r
-        t1 = self._conv(c1, x, B, H, W)
-        a1, s1 = self._bn(c1, t1)
-        t2 = self._conv(c2, a1, B, H, W)
-        out, s2 = self._bn(c2, t2, res=x)
+        t1, p1 = self._conv(c1, x, B, H, W, bn=True)
+        a1, s1 = self._bn(c1, t1, fpart=p1)
+        t2, p2 = self._conv(c2, a1, B, H, W, bn=True)
+        out, s2 = self._bn(c2, t2, res=x, fpart=p2)
         return out, (x, t1, a1, s1, t2, s2, out)
 
-    def _res_bwd(self, r, sv, g, gx, B, H, W):
+    @staticmethod
+    def _res_in_bn(r, sv):
+        """The BN that consumes a residual block's output gradient first (conv2's): (conv, y, t, stats)."""
+        x, t1, a1, s1, t2, s2, out = sv
+        return (r[1], out, t2, s2)
+
+    def _res_bwd(self, r, sv, g, gx, B, H, W, nxt=None):
         """g: gradient of the block output (overwritten with the ReLU-masked gradient);
         gx: existing gradient of the block input or None. Returns the input gradient."""
         c1, c2 = r
         x, t1, a1, s1, t2, s2, out = sv
         dt2 = self._bn_bwd(c2, g, out, t2, s2)           # g <- g * [out > 0]
         self._wgrad(c2, a1, dt2, B, H, W)
-        da1 = self._dgrad(c2, dt2, B, H, W)
+        da1 = self._dgrad(c2, dt2, B, H, W, bn=(c1, a1, t1, s1))
         del dt2
         dt1 = self._bn_bwd(c1, da1, a1, t1, s1)
         del da1
         self._wgrad(c1, x, dt1, B, H, W)
         if gx is None:                                     # skip path: the masked g itself
-            return self._dgrad(c1, dt1, B, H, W, acc=g)
+            return self._dgrad(c1, dt1, B, H, W, acc=g, bn=nxt)
         self._dgrad(c1, dt1, B, H, W, acc=gx)
         L.call("mzba_axpy", self.dt, L.ptr(gx), L.ptr(g), gx.numel(), L.stream())
         return gx
 
     def _block_fwd(self, c, x, B, H, W):  # ConvBlock: conv -> BN -> ReLU
-        t = self._conv(c, x, B, H, W)
-        y, s = self._bn(c, t)
+        t, p = self._conv(c, x, B, H, W, bn=True)
+        y, s = self._bn(c, t, fpart=p)
         return y, (x, t, s, y)
 
-    def _block_bwd(self, c, sv, g, B, H, W, acc=None):
+    def _block_bwd(self, c, sv, g, B, H, W, acc=None, nxt=None):
         x, t, s, y = sv
         dt = self._bn_bwd(c, g, y, t, s)
         self._wgrad(c, x, dt, B, H, W)
-        return self._dgrad(c, dt, B, H, W, acc=acc)
+        return self._dgrad(c, dt, B, H, W, acc=acc, bn=nxt)
 
     def _scale_fwd(self, h, B):
         hw, C = h.shape[0] // B, h.shape[1]
@@ -531,6 +576,7 @@ class Learner:
         self.G.zero_()
         self._scale_idx = []
         self._pending = {} if self.defer_wgrad else None
+        self._gpart = {}
         self._prepare_packs()
         # ---- forward (_k_step_rollout)
         cin_p = self.rep[0][1].cin_p
@@ -540,7 +586,7 @@ class Learner:
         tape, h, hh, ww = [], x, H, W
         for kind, mod in self.rep:
             if kind == "conv":
-                y = self._conv(mod, h, B, hh, ww)
+                y, _ = self._conv(mod, h, B, hh, ww)
                 tape.append(("conv", mod, (h, hh, ww)))
                 h = y
             elif kind == "res":
@@ -597,20 +643,24 @@ class Learner:
             # dynamics k: scale -> reward head -> res blocks -> conv block
             gx = self._scale_bwd(u["ssc"], gh, B) if gh is not None else None
             dyr = self._linear_bwd(self.dyn_rlin[0], u["yr"], dlr[k], B, self.dyn_rlin[1], self.ns)
-            gx = self._block_bwd(self.dyn_rconv, u["srew"], dyr, B, hl, wl, acc=gx)
+            xb, tb, sb, yb = u["sblk"]
+            dcons = [(self.dyn_block, yb, tb, sb)] + [self._res_in_bn(r, sv) for r, sv in zip(self.dyn_res, u["dsv"])]
+            gx = self._block_bwd(self.dyn_rconv, u["srew"], dyr, B, hl, wl, acc=gx, nxt=dcons[-1])
             del dyr
-            for r, sv in zip(reversed(self.dyn_res), reversed(u["dsv"])):
-                gx = self._res_bwd(r, sv, gx, None, B, hl, wl)
+            for i in reversed(range(len(self.dyn_res))):
+                gx = self._res_bwd(self.dyn_res[i], u["dsv"][i], gx, None, B, hl, wl, nxt=dcons[i])
             gh = self._block_bwd(self.dyn_block, u["sblk"], gx, B, hl, wl)  # d h_k (first c1 channels)
             del gx
             # prediction k: heads -> res blocks, accumulating into d h_k
             dyv = self._linear_bwd(self.pred_vlin[0], u["yv"], dlv[k], B, self.pred_vlin[1], self.ns)
             gp = self._block_bwd(self.pred_vconv, u["sval"], dyv, B, hl, wl)
             dyp = self._linear_bwd(self.pred_plin[0], u["yp"], dlp[k], B, self.pred_plin[1], self.na)
-            self._block_bwd(self.pred_pconv, u["spol"], dyp, B, hl, wl, acc=gp)
+            pcons = [self._res_in_bn(r, sv) for r, sv in zip(self.pred_res, u["psv"])]
+            self._block_bwd(self.pred_pconv, u["spol"], dyp, B, hl, wl, acc=gp, nxt=pcons[-1] if pcons else None)
             del dyv, dyp
             for i in reversed(range(len(self.pred_res))):
-                gp = self._res_bwd(self.pred_res[i], u["psv"][i], gp, gh if i == 0 else None, B, hl, wl)
+                gp = self._res_bwd(self.pred_res[i], u["psv"][i], gp, gh if i == 0 else None, B, hl, wl,
+                                   nxt=pcons[i - 1] if i > 0 else None)
             if not self.pred_res:
                 L.call("mzba_axpy", self.dt, L.ptr(gh), L.ptr(gp), gh.numel(), s)
             unroll[k] = None
@@ -618,7 +668,10 @@ class Learner:
             self._flush_wgrad(B)
         # representation: scale -> [pool | res | conv] reversed
         gx = self._scale_bwd(rep_scale, gh, B)
-        for kind, mod, sv in reversed(tape):
+        for ti in reversed(range(len(tape))):
+            kind, mod, sv = tape[ti]
+            prev = tape[ti - 1] if ti > 0 else None
+            nxt = self._res_in_bn(prev[1], prev[2][0]) if prev is not None and prev[0] == "res" else None
             if kind == "pool":
                 hh2, ww2, C = sv
                 dx = self._act(B * hh2 * ww2, C)
@@ -626,7 +679,7 @@ class Learner:
                 gx = dx
             elif kind == "res":
                 svr, hh2, ww2 = sv
-                gx = self._res_bwd(mod, svr, gx, None, B, hh2, ww2)
+                gx = self._res_bwd(mod, svr, gx, None, B, hh2, ww2, nxt=nxt)
             else:
                 xin, hh2, ww2 = sv
                 self._wgrad(mod, xin, gx, B, hh2, ww2)

@@ -404,3 +404,94 @@ def test_learner_graph_replay_matches_eager(dt):
         assert torch.equal(torch.as_tensor(sa[k]), torch.as_tensor(sb[k])), k
     assert torch.equal(a.M1, b.M1) and torch.equal(a.M2, b.M2)
     assert a.step_count == b.step_count == 4
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,ks", [(512, 4, 5, 256, 256, 3), (37, 4, 5, 256, 128, 3),
+                                                (19, 4, 5, 128, 256, 1), (64, 8, 10, 256, 256, 3)])
+def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks):
+    """mzba_conv_lat_bn (the BatchNorm statistics in the conv epilogue) against the conv followed by
+    the separate BN passes: mode 1 -> mzba_bn_stats_final equals mzba_bn_stats (same bf16 values,
+    different chunking: f32 rounding only); mode 2 -> the masked output equals bn_backward's in-place
+    mask bit for bit, dgamma / dbeta / dx within f32 rounding."""
+    from mzba import _lib as L
+    from mzba.agent import pack_lat
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(B + Cout)
+    x = torch.randn(B * H * W, Cin, generator=g).to(torch.bfloat16).to(dev)
+    w = torch.randn(Cout, Cin, ks, ks, generator=g) / (Cin * ks * ks) ** 0.5
+    wf = torch.from_numpy(pack_lat(w.permute(0, 2, 3, 1).reshape(Cout, -1).numpy(), Cout, ks, Cin)).to(torch.bfloat16).to(dev)
+    bias = torch.randn(Cout, generator=g).to(dev) * 0.1
+    M = B * H * W
+    nc, rpc = ctypes.c_int(), ctypes.c_int()
+    L.call("mzba_conv_lat_bn_chunks", B, H, W, Cin, Cout, ks, ctypes.byref(nc), ctypes.byref(rpc))
+    part = torch.empty(nc.value * Cout * 2, device=dev)
+    t = torch.empty(M, Cout, dtype=torch.bfloat16, device=dev)
+    L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), None, L.ptr(t), B, H, W, Cin, Cout, ks, 1,
+           L.ptr(part), None, None, None, L.stream())
+    t_ref = torch.empty_like(t)
+    L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, None, L.ptr(t_ref),
+           B, H, W, Cin, Cout, ks, 0, L.stream())
+    assert torch.equal(t, t_ref)
+    gamma, beta = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    st1, st2 = torch.empty(4, Cout, device=dev), torch.empty(4, Cout, device=dev)
+    rm1, rv1, rm2, rv2 = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev), torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    L.call("mzba_bn_stats_final", L.ptr(part), nc.value, rpc.value, M, Cout, 1e-5, 0.1, L.ptr(gamma), L.ptr(beta),
+           L.ptr(st1), L.ptr(rm1), L.ptr(rv1), L.stream())
+    ws = torch.empty(((M + 63) // 64) * Cout * 8 + 12 * Cout, dtype=torch.uint8, device=dev)
+    L.call("mzba_bn_stats", 1, L.ptr(t), M, Cout, 1e-5, 0.1, L.ptr(gamma), L.ptr(beta), L.ptr(st2), L.ptr(rm2),
+           L.ptr(rv2), L.ptr(ws), ws.numel(), L.stream())
+    torch.testing.assert_close(st1, st2, rtol=2e-6, atol=2e-6)
+    torch.testing.assert_close(rv1, rv2, rtol=2e-6, atol=2e-6)
+    # mode 2: this conv produces the output gradient of a BN (input bx, output by, stats st2)
+    by = torch.relu(torch.randn(M, Cout, generator=g)).to(torch.bfloat16).to(dev)
+    bx = torch.randn(M, Cout, generator=g).to(torch.bfloat16).to(dev)
+    acc = torch.randn(M, Cout, generator=g).to(torch.bfloat16).to(dev)
+    g1, g2 = acc.clone(), acc.clone()
+    L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), L.ptr(g1), L.ptr(g1), B, H, W, Cin, Cout, ks, 2,
+           L.ptr(part), L.ptr(by), L.ptr(bx), L.ptr(st2), L.stream())
+    L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, L.ptr(g2), L.ptr(g2),
+           B, H, W, Cin, Cout, ks, 0, L.stream())
+    dg1, db1, dg2, db2 = (torch.zeros(Cout, device=dev) for _ in range(4))
+    dx1, dx2 = torch.empty_like(bx), torch.empty_like(bx)
+    L.call("mzba_bn_backward_final", 1, L.ptr(g1), L.ptr(bx), L.ptr(st2), L.ptr(part), nc.value, M, Cout, L.ptr(dg1),
+           L.ptr(db1), L.ptr(dx1), L.ptr(ws), ws.numel(), L.stream())
+    L.call("mzba_bn_backward", 1, L.ptr(g2), L.ptr(by), L.ptr(bx), L.ptr(st2), M, Cout, L.ptr(dg2), L.ptr(db2),
+           L.ptr(dx2), L.ptr(ws), ws.numel(), L.stream())
+    assert torch.equal(g1, g2)  # the masked gradient
+    torch.testing.assert_close(dg1, dg2, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db1, db2, rtol=1e-4, atol=1e-3)
+    assert (dx1.float() - dx2.float()).abs().max().item() <= 1e-2 * dx2.float().abs().max().item()
+
+
+def test_learner_fused_bn_statistics_track_separate_passes():
+    """bf16 learner with the BN statistics in the conv epilogues vs the separate BN passes: the same
+    algorithm with different f32 summation chunks, so some bf16 activations round the other way
+    and the two bf16 runs differ at bf16-noise scale. Checked: losses within 2e-3 relative;
+    per-tensor gradient cosine fused vs separate >= 0.98 (median >= 0.99); and the fused run is as
+    close to the f32 parity path as the separate-pass run is (median cosine within 0.01, min
+    within 0.05) — a wiring error (wrong consumer BN, mask or chunk) would fall far below."""
+    from mzba.config import learner_model_cfg
+    from mzba.learner import Learner
+    from mzba.weights import init_state_dict
+    mcfg = learner_model_cfg()
+    mcfg["latent_channels"] = [128, 128]
+    ring = _random_ring(64, mcfg["state_history_length"], 5, 21)
+    out = {}
+    for tag, dt, fuse in (("sep", "bf16", False), ("fused", "bf16", True), ("f32", "f32", False)):
+        ln = Learner(mcfg, init_state_dict(mcfg, 4), K=5, dtype=dt, fuse_bn=fuse)
+        out[tag] = (ln.train_minibatch(ring, ring.slots()).cpu(), ln.gradients())
+        del ln
+    torch.testing.assert_close(out["fused"][0], out["sep"][0], rtol=2e-3, atol=1e-5)
+
+    def cosines(a, b):
+        c = {}
+        for k, g0 in out[b][1].items():
+            if _pre_bn_bias(k) or g0.abs().max() == 0:
+                continue
+            c[k] = torch.nn.functional.cosine_similarity(g0.flatten().double(), out[a][1][k].flatten().double(),
+                                                         dim=0).item()
+        return np.array(list(c.values()))
+    fs, ff, sf = cosines("fused", "sep"), cosines("fused", "f32"), cosines("sep", "f32")
+    print("fused~sep", np.median(fs), fs.min(), "fused~f32", np.median(ff), ff.min(), "sep~f32", np.median(sf), sf.min())
+    assert fs.min() >= 0.98 and np.median(fs) >= 0.99
+    assert np.median(ff) >= np.median(sf) - 0.01 and ff.min() >= sf.min() - 0.05
