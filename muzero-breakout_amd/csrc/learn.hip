@@ -571,18 +571,24 @@ MZ_DEV bf16x8_t tr_frag_at(const bf16_t* lo_base, const bf16_t* hi_base) {
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// 8 waves: waves 4 tg .. 4 tg + 3 own taps [5 tg, min(9, 5 tg + 5)) of the tile (two waves per
+// SIMD to hide the LDS read latency; the tap groups write disjoint partials, so no reduction)
+constexpr int WI_NT = 512;
+constexpr int WI_PFN = WI_PF * 256 / WI_NT;  // staging chunks per thread
+constexpr size_t WI_LDS_MAX = 140 * 1024;     // dynamic LDS (+ 16 KB static bias scratch <= 160 KB)
 template <bool PF>
-__global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __restrict__ part,
-                                                             float* __restrict__ bpart) {
+__global__ __launch_bounds__(WI_NT) void conv_wgrad_img_kernel(WgImg a, float* __restrict__ part,
+                                                               float* __restrict__ bpart) {
   extern __shared__ __attribute__((aligned(16))) bf16_t lds_img[];
   bf16_t* ldy = lds_img;                                   // [KS][WI_LD]
   bf16_t* lx = lds_img + (size_t)(a.KS + WI_LEAD) * WI_LD;  // [XR + 64][WI_LD], preceded by WI_LEAD zero rows
-  __shared__ float bred[32][64];
+  __shared__ float bred[WI_NT / 8][64];
   const int H = a.H, W = a.W, Wp = W + 2, Hp = H + 2, HWp = H * Wp, HpWp = Hp * Wp;
   const int nci = (a.Cin + 63) / 64;
   const int cit = blockIdx.x % nci, cot = blockIdx.x / nci;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int tg = wave >> 2, wr = (wave >> 1) & 1, wc = wave & 1;
+  const int tap0 = 5 * tg, ntap = tg ? 4 : 5;
   const int ch = tid & 7;  // 16-B chunk (8 channels) every staging chunk of this thread holds
   const int co_s = cot * 64 + ch * 8, ci_s = cit * 64 + ch * 8;
   const bool do_bias = bpart && cit == 0;
@@ -590,13 +596,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
 #pragma unroll
   for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
   // zero the lead rows and the tail margin of the X region once
-  for (int i = tid; i < WI_LEAD * 8; i += 256)
+  for (int i = tid; i < WI_LEAD * 8; i += WI_NT)
     *reinterpret_cast<uint4*>(lds_img + (size_t)(a.KS + i / 8) * WI_LD + (i & 7) * 8) = make_uint4(0, 0, 0, 0);
-  for (int i = tid; i < 64 * 8; i += 256)
+  for (int i = tid; i < 64 * 8; i += WI_NT)
     *reinterpret_cast<uint4*>(lx + (size_t)(a.XR + i / 8) * WI_LD + (i & 7) * 8) = make_uint4(0, 0, 0, 0);
-  f32x4_t acc[9][2][2];
+  f32x4_t acc[5][2][2];
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int t = 0; t < 5; ++t)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -612,11 +618,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
   // index math (divisions by the bordered geometry) runs once per thread, not once per stage.
   const int nchunk = (a.KS + a.XR) * 8;
   const size_t img_x = (size_t)H * W * a.Cin, img_dy = (size_t)H * W * a.Cout;
-  int soff[WI_PF];      // element offset from the stage's env-0 base, -1 = zero chunk
+  int soff[WI_PFN];     // element offset from the stage's env-0 base, -1 = zero chunk
   uint32_t sdy = 0u;    // bit u: chunk u is a dY chunk
-  for (int u = 0; u < WI_PF; ++u) {
+  for (int u = 0; u < WI_PFN; ++u) {
     int off = -1;
-    const int i = u * 256 + tid;
+    const int i = u * WI_NT + tid;
     if (i < a.KS * 8) {  // dY rows: k = e*HWp + y*Wp + xp (xp in 1..W real, 0 / W+1 border)
       const int r = i >> 3;
       const int e = r / HWp, w = r - e * HWp, y = w / Wp, xp = w - y * Wp;
@@ -630,7 +636,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
     }
     soff[u] = off;
   }
-  uint4 pf[WI_PF];
+  uint4 pf[WI_PFN];
   auto load_chunks = [&](int st, int base) {
     const int b0 = st * a.E, sg = b0 / a.Bseg, bl = b0 - sg * a.Bseg;
     const bf16_t* xb = a.xs[sg] + (size_t)bl * img_x;
@@ -639,16 +645,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
       // unconditional loads (zero chunks read the stage base, then select): a load under a
       // branch is waited for inside the branch, which serialised the 12 loads of a stage
 #pragma unroll
-      for (int u = 0; u < WI_PF; ++u)
+      for (int u = 0; u < WI_PFN; ++u)
         pf[u] = *reinterpret_cast<const uint4*>(((sdy >> u) & 1u ? db : xb) + (soff[u] >= 0 ? soff[u] : 0));
 #pragma unroll
-      for (int u = 0; u < WI_PF; ++u)
+      for (int u = 0; u < WI_PFN; ++u)
         if (soff[u] < 0) pf[u] = make_uint4(0, 0, 0, 0);
       return;
     }
 #pragma unroll
-    for (int u = 0; u < WI_PF; ++u) {  // batched (non-PF) plans: chunks beyond the first batch
-      const int i = base + u * 256 + tid;
+    for (int u = 0; u < WI_PFN; ++u) {  // batched (non-PF) plans: chunks beyond the first batch
+      const int i = base + u * WI_NT + tid;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (i < a.KS * 8) {
         const int r = i >> 3;
@@ -666,8 +672,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
   };
   auto store_chunks = [&](int base) {
 #pragma unroll
-    for (int u = 0; u < WI_PF; ++u) {
-      const int i = base + u * 256 + tid;
+    for (int u = 0; u < WI_PFN; ++u) {
+      const int i = base + u * WI_NT + tid;
       if (i < a.KS * 8) {
         *reinterpret_cast<uint4*>(ldy + (size_t)(i >> 3) * WI_LD + ch * 8) = pf[u];
         if (do_bias) {
@@ -686,7 +692,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
     if (PF) {
       store_chunks(0);
     } else {
-      for (int base = 0; base < nchunk; base += WI_PF * 256) {
+      for (int base = 0; base < nchunk; base += WI_PFN * WI_NT) {
         load_chunks(st, base);
         store_chunks(base);
       }
@@ -714,16 +720,18 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
         }
       };
       bf16x8_t bcur[2], bnxt[2];
-      bload(0, bcur);
+      bload(tap0, bcur);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        if (t + 1 < 9) bload(t + 1, bnxt);
+      for (int tt = 0; tt < 5; ++tt) {
+        if (tt < ntap) {  // wave-uniform: tap group 1 has 4 taps
+          if (tt + 1 < ntap) bload(tap0 + tt + 1, bnxt);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[t][i][j], 0, 0, 0);
-        if (t + 1 < 9) { bcur[0] = bnxt[0]; bcur[1] = bnxt[1]; }
+            for (int j = 0; j < 2; ++j)
+              acc[tt][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[tt][i][j], 0, 0, 0);
+          if (tt + 1 < ntap) { bcur[0] = bnxt[0]; bcur[1] = bnxt[1]; }
+        }
       }
     }
   }
@@ -731,17 +739,19 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
   float* outp = part + (size_t)blockIdx.y * a.Cout * K;
   const int fr = lane & 15, fk = lane >> 4;
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int tt = 0; tt < 5; ++tt)
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
+        const int t = tap0 + tt;
         const int ci = cit * 64 + wc * 32 + j * 16 + fr;
+        if (tt >= ntap) continue;
         if (ci >= a.Cin) continue;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int co = cot * 64 + wr * 32 + i * 16 + 4 * fk + r;
-          if (co < a.Cout) outp[(size_t)co * K + (size_t)t * a.Cin + ci] = acc[t][i][j][r];
+          if (co < a.Cout) outp[(size_t)co * K + (size_t)t * a.Cin + ci] = acc[tt][i][j][r];
         }
       }
   if (do_bias) {
@@ -751,7 +761,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_img_kernel(WgImg a, float* __r
     __syncthreads();
     if (tid < 64) {
       float sum = 0.f;
-      for (int r = 0; r < 32; ++r) sum += bred[r][tid];
+      for (int r = 0; r < WI_NT / 8; ++r) sum += bred[r][tid];
       const int co = cot * 64 + tid;
       if (co < a.Cout) bpart[(size_t)blockIdx.y * a.Cout + co] = sum;
     }
@@ -773,7 +783,7 @@ static bool wgrad_img_plan(int B, int Bseg, int H, int W, int Cin, int Cout, WgP
   auto rows = [&](int e) { return ((e * HWp + 31) / 32 * 32) + WI_LEAD + e * HpWp + 64; };
   auto staged = [&](int e) { return (e * HWp + 31) / 32 * 32 + e * HpWp; };
   while (E < 16 && Bseg % (E * 2) == 0 && (size_t)rows(E * 2) * WI_LD * 2 <= 64 * 1024 && staged(E * 2) * 8 <= WI_PF * 256) E *= 2;
-  if ((size_t)rows(E) * WI_LD * 2 > 150 * 1024) return false;
+  if ((size_t)rows(E) * WI_LD * 2 > WI_LDS_MAX) return false;
   p.pf = staged(E) * 8 <= WI_PF * 256;
   const int tiles = ((Cout + 63) / 64) * ((Cin + 63) / 64);
   const int stages = (B + E - 1) / E;
@@ -1290,10 +1300,10 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
     static bool attr = false;  // the 16x20 images need more than the default 64 KB of dynamic LDS
     if (!attr) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_img_kernel<false>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)WI_LDS_MAX);
       if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_img_kernel<true>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)WI_LDS_MAX);
       if (e != hipSuccess) return (int)e;
       attr = true;
     }
@@ -1307,9 +1317,9 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
     float* ibpart = db ? ipart + (size_t)ip.nsplit * nwi : nullptr;
     const dim3 grid(((Cout + 63) / 64) * ((Cin + 63) / 64), ip.nsplit);
     if (ip.pf)
-      hipLaunchKernelGGL(conv_wgrad_img_kernel<true>, grid, dim3(256), ip.lds, stream, ip.a, ipart, ibpart);
+      hipLaunchKernelGGL(conv_wgrad_img_kernel<true>, grid, dim3(WI_NT), ip.lds, stream, ip.a, ipart, ibpart);
     else
-      hipLaunchKernelGGL(conv_wgrad_img_kernel<false>, grid, dim3(256), ip.lds, stream, ip.a, ipart, ibpart);
+      hipLaunchKernelGGL(conv_wgrad_img_kernel<false>, grid, dim3(WI_NT), ip.lds, stream, ip.a, ipart, ibpart);
     hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(nwi)), dim3(256), 0, stream, (const float*)ipart, ip.nsplit,
                        nwi, dw);
     if (db)
