@@ -918,9 +918,12 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const T* __restrict__ x
   for (int o = 0; o < 16; ++o) acc[o] = 0.f;
   for (int k = threadIdx.x; k < K; k += 256) {
     const float v = ld(xb + k);
+    float wv[16];  // unconditional loads (rows >= O re-read row 0): a load under `if (o < O)` is
+#pragma unroll     // waited for inside its branch, which serialised the 16 loads
+    for (int o = 0; o < 16; ++o) wv[o] = w[(size_t)(o < O ? o : 0) * K + k];
 #pragma unroll
     for (int o = 0; o < 16; ++o)
-      if (o < O) acc[o] += v * w[(size_t)o * K + k];
+      if (o < O) acc[o] += v * wv[o];
   }
   __shared__ float red[4][16];
   const int w_ = threadIdx.x >> 6;
