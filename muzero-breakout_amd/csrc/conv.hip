@@ -81,6 +81,7 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
   }
 
   uint4 ra[4], rb[4];
+  bool oka[4], okb[4];
   // each 16-B chunk j of a K-step resolves its own tap (Cin % EPC == 0: a chunk never
   // straddles two taps), so Cin need not be a multiple of BK
   auto load_tile = [&](int ks) {
@@ -88,23 +89,25 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
     const bool kok = k < Ktot;
     const int tap = k / a.Cin, c = k - tap * a.Cin;
     const int ky = tap / a.ks - pad, kx = tap % a.ks - pad;
+    // unconditional loads from a clamped (valid) address; the zero select happens at the LDS
+    // store (store_tile), after the MFMAs: hipcc waits for a load under a branch inside the
+    // branch, which serialised the 8 loads of a K-step and exposed their latency
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int sy = ay[i] + ky, sx = ax[i] + kx;
-      bool ok = kok && mval[i] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(abase[i] + ((long long)(sy * a.W + sx) * a.Cin + c))
-                 : make_uint4(0, 0, 0, 0);
+      oka[i] = kok && mval[i] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
+      ra[i] = *reinterpret_cast<const uint4*>(abase[i] + (oka[i] ? (long long)(sy * a.W + sx) * a.Cin + c : 0));
       int n = n0 + r0 + 32 * i;
-      rb[i] = kok && n < a.Cout ? *reinterpret_cast<const uint4*>(wgt + ((long long)n * Ktot + k))
-                                : make_uint4(0, 0, 0, 0);
+      okb[i] = kok && n < a.Cout;
+      rb[i] = *reinterpret_cast<const uint4*>(wgt + (okb[i] ? (long long)n * Ktot + k : 0));
     }
   };
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       int row = r0 + 32 * i;
-      *reinterpret_cast<uint4*>(&lds[buf][0][swz(row, j)]) = ra[i];
-      *reinterpret_cast<uint4*>(&lds[buf][1][swz(row, j)]) = rb[i];
+      *reinterpret_cast<uint4*>(&lds[buf][0][swz(row, j)]) = oka[i] ? ra[i] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(&lds[buf][1][swz(row, j)]) = okb[i] ? rb[i] : make_uint4(0, 0, 0, 0);
     }
   };
 
