@@ -158,24 +158,35 @@ __device__ __forceinline__ void lat_epilogue(const LatArgs& a, float* ot, const 
   if (a.smode == 0) return;
   __syncthreads();  // the tile holds the rounded outputs (1) / every thread is done with it (2)
   float* pf = reinterpret_cast<float*>(a.part) + 2 * ((size_t)blockIdx.x * a.Cout + blockIdx.y * 128);
-  if (a.smode == 1) {  // (mean, M2) per column over the rows, NT / 128 threads per column
-    constexpr int TPC = NT / 128;
-    const int col = tid / TPC, q = tid % TPC;
+  if (a.smode == 1) {  // (mean, M2) per column over the rows: NT / 128 row groups, lanes = columns
+    constexpr int TPC = NT / 128;  // (a wave reads 64 consecutive columns of one row: conflict-free)
+    const int col = tid % 128, q = tid / 128;
+    float* red = ot + MR * 128;    // [TPC][128] after the tile (LDS_C covers MR rows; see caller)
     float s = 0.f;
     if (col < ncols)
       for (int r = q; r < rows; r += TPC) s += ot[r * 128 + col];
+    red[q * 128 + col] = s;
+    __syncthreads();
+    float tot = 0.f;
 #pragma unroll
-    for (int o = 1; o < TPC; o <<= 1) s += __shfl_xor(s, o);
-    const float mean = s / rows;
+    for (int k = 0; k < TPC; ++k) tot += red[k * 128 + col];
+    const float mean = tot / rows;
     float m2 = 0.f;
     if (col < ncols)
       for (int r = q; r < rows; r += TPC) {
         const float d = ot[r * 128 + col] - mean;
         m2 += d * d;
       }
+    __syncthreads();
+    red[q * 128 + col] = m2;
+    __syncthreads();
+    if (q == 0 && col < ncols) {
+      float t2 = 0.f;
 #pragma unroll
-    for (int o = 1; o < TPC; o <<= 1) m2 += __shfl_xor(m2, o);
-    if (q == 0 && col < ncols) { pf[2 * col] = mean; pf[2 * col + 1] = m2; }
+      for (int k = 0; k < TPC; ++k) t2 += red[k * 128 + col];
+      pf[2 * col] = mean;
+      pf[2 * col + 1] = t2;
+    }
     return;
   }
   // smode 2: the NT / ncb threads of a chunk column reduce through the tile, in thread order
@@ -224,7 +235,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
   constexpr int PAD = KS / 2;
   constexpr int NT = 64 * WAVES;
   static_assert(NH % D == 0, "ring / tap alignment");
-  constexpr int LDS_A = (MAXROWS + 1) * ROWB, LDS_C = MAXROWS * 128 * 4;
+  constexpr int LDS_A = (MAXROWS + 1) * ROWB, LDS_C = (MAXROWS + NT / 128) * 128 * 4;  // + BN-stats scratch
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_A > LDS_C ? LDS_A : LDS_C];
   __shared__ long long envoff[32 * RT];
   const int HW = a.H * a.W;
