@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--cpu-envs", type=int, default=16, help="bounded oracle sample (cpu_baseline + match rate)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
+    ap.add_argument("--tower-variant", type=int, default=0, help="tower kernel (mzba_tower_set_variant; 0 = by batch)")
     ap.add_argument("--workload", default="acting", choices=["acting", "env", "learner"],
                     help="acting: the whole acting loop (headline); env: env step + render + frame stack only "
                          "(configs 1/3, HBM roofline)")
@@ -279,6 +280,8 @@ def main():
     from mzba.shard import TrajectoryGather
     from mzba import _lib as L
 
+    if args.tower_variant:
+        L.call("mzba_tower_set_variant", args.tower_variant)
     cfg = default_config()
     cfg["num_simulations"] = args.sims
     mcfg = cfg["model"]

@@ -154,10 +154,12 @@ int mzba_replay_write(const uint8_t* action, const float* reward, const uint8_t*
 int mzba_replay_states(const uint8_t* states, const int32_t* slots, int n, const float* lut8, float* out, int hist,
                        int HW, hipStream_t stream);
 
-/* kernel choice for experiments/tests: 0 by batch (default), 1 four-env kernel, 2 eight-env kernel */
+/* kernel choice for experiments/tests: 0 by batch (default), 1 four-env 8-wave kernel, 2 eight-env
+ * kernel, 3 four-env 4-wave kernel */
 int mzba_tower_set_variant(int v);
-/* kernel mzba_tower runs for batch B: 1 four-env (workgroup = 4 envs, 8 waves), 2 eight-env (B >= 8 x CUs;
- * workgroup = 8 envs, 4 waves: half the weight stream per env). Both take agent.pack_tower_conv weights. */
+/* kernel mzba_tower runs for batch B: 1 four-env (workgroup = 4 envs, 8 waves of 32 output channels) below
+ * 8 x CUs envs, else 2 eight-env (workgroup = 8 envs, 4 waves: half the weight stream per env); 3 = the
+ * four-env 4-wave kernel (64 channels per wave; by variant only). All take agent.pack_tower_conv weights. */
 int mzba_tower_plan(int B);
 /* device scratch bytes mzba_tower needs for batch B (0 for both kernels; the ws argument may be null) */
 long long mzba_tower_ws_bytes(int B);

@@ -113,10 +113,16 @@ struct TowerArgs {
 MZ_DEV int trow(int e, int p) { return (p % 5) * 16 + (p / 5) * 4 + e; }
 MZ_DEV int toff(int row, int chunk) { return row * TROWB + ((chunk ^ (row & 15)) << 4); }
 
+// 4-wave kernel geometry: NQ env quads per workgroup (2: the 8-env kernel; 1: 4 envs, every wave
+// 4 column tiles of 5 row tiles — half the LDS A reads per MFMA of the 8-wave 4-env kernel)
+template <int NQ>
+struct T8 {
+  static constexpr int E = 4 * NQ, ROWS = 80 * NQ, NRT = 5 * NQ, NT = 256, CT = 4;  // 4 waves
+  static constexpr int IMG = ROWS * TROWB;                   // 40 / 80 KB
+  static constexpr int LZ = IMG, BYTES = IMG + 16 * TROWB;   // + 16 zero rows
+};
 namespace t8 {
-constexpr int E = 8, ROWS = 160, NRT = 10, NT = 256, CT = 4;  // 4 waves
-constexpr int IMG = ROWS * TROWB;                       // 80 KB
-constexpr int LZ = IMG, BYTES = IMG + 16 * TROWB;       // + 16 zero rows
+constexpr int NT = 256, CT = 4;
 // LDS row of (env e, latent position p = 5y + x): env quad (e >> 2) owns tiles 5 (e >> 2) .. +4
 MZ_DEV int row8(int e, int p) { return (e >> 2) * 80 + (p % 5) * 16 + (p / 5) * 4 + (e & 3); }
 }  // namespace t8
@@ -507,11 +513,11 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
 // One activation image: a conv reads it whole, then (after a barrier) its output overwrites it in
 // place; conv1 first lifts the block input at its own output positions into registers (the residual).
 
-template <int EL, int DX>
+template <int EL, int NQ, int DX>
 __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
-                                          uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[t8::NRT][t8::CT], int lane) {
+                                          uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
   constexpr int NX = DX == 0 ? 5 : 4;   // active x tiles per env quad
-  constexpr int NA = 2 * NX;            // active tiles
+  constexpr int NA = NQ * NX;           // active tiles
   constexpr int A0 = DX < 0 ? 1 : 0;    // first accumulator x tile
   constexpr int S0 = DX > 0 ? 1 : 0;    // first source x tile
   constexpr int SB = (DX + 1) * 24;     // first k step of this column shift
@@ -565,14 +571,14 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 }
 
 // the 8 k steps of a 1x1 conv on the 8-env image (centre tap: all 10 tiles, every row valid)
-template <int EL>
+template <int EL, int NQ>
 __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
-                                              uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[t8::NRT][t8::CT], int lane) {
+                                              uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
   const int q = lane >> 4, key = lane & 15;
   const int base = key * TROWB, sw = key << 4;
-  typename Elt<EL>::v8 afc[t8::NRT], afn[t8::NRT];
+  typename Elt<EL>::v8 afc[T8<NQ>::NRT], afn[T8<NQ>::NRT];
 #pragma unroll
-  for (int j = 0; j < t8::NRT; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
+  for (int j = 0; j < T8<NQ>::NRT; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     typename Elt<EL>::v8 w[t8::CT];
@@ -582,7 +588,7 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
       if (c + TD < 8) bq[ct][c % TD] = wp[ct][(size_t)(c + TD) * 64];
     }
 #pragma unroll
-    for (int j = 0; j < t8::NRT; ++j) {
+    for (int j = 0; j < T8<NQ>::NRT; ++j) {
 #pragma unroll
       for (int ct = 0; ct < t8::CT; ++ct)
         acc[j][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[j][ct]);
@@ -590,18 +596,18 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
         afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
     }
 #pragma unroll
-    for (int j = 0; j < t8::NRT; ++j) afc[j] = afn[j];
+    for (int j = 0; j < T8<NQ>::NRT; ++j) afc[j] = afn[j];
   }
 }
 
 // k loop of one conv over the 8-env image: this wave's 4 channel tiles ct0..ct0+3 of a weight pack
 // with `tns` k steps per tile (72: 3x3, 8: 1x1). D[pack channel 16 ct + 4q + i][row 16 rt + l16].
 // MODE 0: acc starts at bias; 1: bias + res (registers); 2: bias + act_bias[pos][act[env]].
-template <int EL, int MODE, bool CENTER>
+template <int EL, int NQ, int MODE, bool CENTER>
 __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const uint4* __restrict__ wconv, int tns,
                                            int ct0, const float* __restrict__ bconv, const float* __restrict__ actb,
-                                           const int* acts, int A, const uint2 (&res)[t8::NRT][t8::CT],
-                                           f32x4 (&acc)[t8::NRT][t8::CT], int lane) {
+                                           const int* acts, int A, const uint2 (&res)[T8<NQ>::NRT][t8::CT],
+                                           f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
   const int q = lane >> 4, l16 = lane & 15;
   const uint4* wp[t8::CT];
   uint4 bq[t8::CT][TD];
@@ -616,7 +622,7 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
     const int n = (ct0 + ct) * 16 + 4 * q;
     const float4 b4 = *reinterpret_cast<const float4*>(bconv + n);
 #pragma unroll
-    for (int rt = 0; rt < t8::NRT; ++rt) {
+    for (int rt = 0; rt < T8<NQ>::NRT; ++rt) {
       f32x4 v = {b4.x, b4.y, b4.z, b4.w};
       if (MODE == 1) {
         const uint2 r = res[rt][ct];
@@ -631,22 +637,22 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
     }
   }
   if (CENTER) {
-    tower8_center<EL>(lds, wp, bq, acc, lane);
+    tower8_center<EL, NQ>(lds, wp, bq, acc, lane);
   } else {
-    tower8_dx<EL, -1>(lds, wp, bq, acc, lane);
-    tower8_dx<EL, 0>(lds, wp, bq, acc, lane);
-    tower8_dx<EL, 1>(lds, wp, bq, acc, lane);
+    tower8_dx<EL, NQ, -1>(lds, wp, bq, acc, lane);
+    tower8_dx<EL, NQ, 0>(lds, wp, bq, acc, lane);
+    tower8_dx<EL, NQ, 1>(lds, wp, bq, acc, lane);
   }
 }
 
 // ReLU -> bf16 -> the image at channel nout + 16 (ct0 + ct) + 4q (8-byte stores, in place after a
 // barrier); SAVE: first lift the image's values there into res (the block input = conv2's residual)
-template <int EL, bool SAVE>
-__device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, const f32x4 (&acc)[t8::NRT][t8::CT],
-                                                 uint2 (&res)[t8::NRT][t8::CT], int nout, int ct0, int lane) {
+template <int EL, int NQ, bool SAVE>
+__device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, const f32x4 (&acc)[T8<NQ>::NRT][t8::CT],
+                                                 uint2 (&res)[T8<NQ>::NRT][t8::CT], int nout, int ct0, int lane) {
   const int q = lane >> 4, l16 = lane & 15;
 #pragma unroll
-  for (int rt = 0; rt < t8::NRT; ++rt)
+  for (int rt = 0; rt < T8<NQ>::NRT; ++rt)
 #pragma unroll
     for (int ct = 0; ct < t8::CT; ++ct) {
       const int n = nout + (ct0 + ct) * 16 + 4 * q;
@@ -660,20 +666,21 @@ __device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, cons
 }
 
 // _scale_state over the 8-env image: 32 threads per env, 20 chunks each; bf16 to out (+ pool slot)
-template <int EL>
+template <int EL, int NQ>
 __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* __restrict__ lds, int env0, int nenv,
                                              int tid) {
-  const int e = tid >> 5, t = tid & 31;
+  constexpr int TPE = t8::NT / T8<NQ>::E;  // threads per env (32 or 64), one wave holds whole envs
+  const int e = tid / TPE, t = tid % TPE;
   float mn = INFINITY, mx = -INFINITY;
-  for (int u = 0; u < 20; ++u) {
-    const int i = u * 32 + t, p = i >> 5, c = i & 31;
+  for (int u = 0; u < 640 / TPE; ++u) {
+    const int i = u * TPE + t, p = i >> 5, c = i & 31;
     const uint4 v = *reinterpret_cast<const uint4*>(lds + toff(t8::row8(e, p), c));
     float f[8];
     unpack8<EL>(v, f);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { mn = fminf(mn, f[j]); mx = fmaxf(mx, f[j]); }
   }
-  for (int o = 16; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
+  for (int o = TPE / 2; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
   if (e >= nenv) return;
   const float den = (mx - mn) + 1e-8f;
   const int b = env0 + e;
@@ -681,8 +688,8 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
   bf16_t* o2 = a.x.pool ? reinterpret_cast<bf16_t*>(a.x.pool) + (size_t)b * a.x.pool_env_stride +
                               (size_t)a.x.pool_slot * 20 * TC
                         : nullptr;
-  for (int u = 0; u < 20; ++u) {
-    const int i = u * 32 + t, p = i >> 5, c = i & 31;
+  for (int u = 0; u < 640 / TPE; ++u) {
+    const int i = u * TPE + t, p = i >> 5, c = i & 31;
     float f[8];
     unpack8<EL>(*reinterpret_cast<const uint4*>(lds + toff(t8::row8(e, p), c)), f);
     const uint4 r = make_uint4(pack_bf16x2((f[0] - mn) / den, (f[1] - mn) / den), pack_bf16x2((f[2] - mn) / den, (f[3] - mn) / den),
@@ -693,31 +700,31 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
 }
 
 // one residual-tower conv (in place): k loop, barrier, write back, barrier
-template <int EL, bool RESID>
+template <int EL, int NQ, bool RESID>
 __device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const uint4* __restrict__ wconv,
-                                            const float* __restrict__ bconv, uint2 (&res)[t8::NRT][t8::CT],
+                                            const float* __restrict__ bconv, uint2 (&res)[T8<NQ>::NRT][t8::CT],
                                             int lane, int wave) {
-  f32x4 acc[t8::NRT][t8::CT];
-  tower8_acc<EL, RESID ? 1 : 0, false>(lds, wconv, TNS, wave * t8::CT, bconv, nullptr, nullptr, 0, res, acc, lane);
+  f32x4 acc[T8<NQ>::NRT][t8::CT];
+  tower8_acc<EL, NQ, RESID ? 1 : 0, false>(lds, wconv, TNS, wave * t8::CT, bconv, nullptr, nullptr, 0, res, acc, lane);
   __syncthreads();  // every wave has read the whole image
-  tower8_writeback<EL, !RESID>(lds, acc, res, 0, wave * t8::CT, lane);
+  tower8_writeback<EL, NQ, !RESID>(lds, acc, res, 0, wave * t8::CT, lane);
   __syncthreads();
 }
 
-template <int EL>
+template <int EL, int NQ>
 __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[t8::BYTES];
-  __shared__ long long envoff[t8::E];
-  __shared__ int acts[t8::E];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[T8<NQ>::BYTES];
+  __shared__ long long envoff[T8<NQ>::E];
+  __shared__ int acts[T8<NQ>::E];
   __shared__ float part[4 * 8 * 16];  // head partial sums [wave][env][output]
   __shared__ float lg[2 * 8 * 16];    // head logits [head][env][output]
   __shared__ float dec[2][8][4];      // decoded head outputs [head][env][output]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int env0 = blockIdx.x * t8::E;
-  const int nenv = min(t8::E, a.B - env0);
+  const int env0 = blockIdx.x * T8<NQ>::E;
+  const int nenv = min(T8<NQ>::E, a.B - env0);
   const int rows = nenv * 20;
   const bool pro = a.x.w0 != nullptr;
-  if (tid < t8::E) {
+  if (tid < T8<NQ>::E) {
     const int b = env0 + (tid < nenv ? tid : 0);
     long long off = (long long)b * a.in_env_stride;
     if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
@@ -725,9 +732,9 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     acts[tid] = pro ? a.x.act[b] : 0;
   }
   __syncthreads();
-  {  // stage X: 160 rows x 32 chunks = 5120 chunks, 20 per thread (two batches of 10)
+  {  // stage X: ROWS x 32 chunks, 10 per thread per batch (NQ batches)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NQ; ++h) {
       uint4 v[10];
 #pragma unroll
       for (int u = 0; u < 10; ++u) {
@@ -746,51 +753,51 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) *reinterpret_cast<uint4*>(lds + t8::LZ + (u * t8::NT + tid) * 16) = make_uint4(0, 0, 0, 0);
+    for (int u = 0; u < 2; ++u) *reinterpret_cast<uint4*>(lds + T8<NQ>::LZ + (u * t8::NT + tid) * 16) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
-  uint2 res[t8::NRT][t8::CT];
+  uint2 res[T8<NQ>::NRT][t8::CT];
   if (pro) {  // dynamics ConvBlock (in place)
-    f32x4 acc[t8::NRT][t8::CT];
-    tower8_acc<EL, 2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), TNS, wave * t8::CT, a.x.b0, a.x.act_bias, acts,
+    f32x4 acc[T8<NQ>::NRT][t8::CT];
+    tower8_acc<EL, NQ, 2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), TNS, wave * t8::CT, a.x.b0, a.x.act_bias, acts,
                          a.x.A, res, acc, lane);
     __syncthreads();
-    tower8_writeback<EL, false>(lds, acc, res, 0, wave * t8::CT, lane);
+    tower8_writeback<EL, NQ, false>(lds, acc, res, 0, wave * t8::CT, lane);
     __syncthreads();
   }
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;
   for (int blk = 0; blk < a.nblocks; ++blk) {
-    tower8_conv<EL, false>(lds, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, res, lane, wave);
-    tower8_conv<EL, true>(lds, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, res, lane, wave);
+    tower8_conv<EL, NQ, false>(lds, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, res, lane, wave);
+    tower8_conv<EL, NQ, true>(lds, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, res, lane, wave);
   }
   if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1, the scaled latent from X, then Linear + decode
-    f32x4 acc[t8::NRT][t8::CT];
-    tower8_acc<EL, 0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, wave * t8::CT, a.x.be1, nullptr, nullptr, 0,
+    f32x4 acc[T8<NQ>::NRT][t8::CT];
+    tower8_acc<EL, NQ, 0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, wave * t8::CT, a.x.be1, nullptr, nullptr, 0,
                         res, acc, lane);
     __syncthreads();
-    tower8_scale<EL>(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
+    tower8_scale<EL, NQ>(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
     __syncthreads();
-    tower8_writeback<EL, false>(lds, acc, res, 0, wave * t8::CT, lane);
+    tower8_writeback<EL, NQ, false>(lds, acc, res, 0, wave * t8::CT, lane);
     __syncthreads();
     const int hc0[2] = {0, 0}, hC[2] = {TC, 0}, kind[2] = {1, 0};
-    tower_heads<EL, t8::E, 4, true>(a, lds, 0, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    tower_heads<EL, T8<NQ>::E, 4, true>(a, lds, 0, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     return;
   }
   if (a.x.epilogue == 2) {  // prediction: policy 3x3 (waves 0-1) -> [0,128), value 1x1 (waves 2-3) -> [128,256)
-    f32x4 acc[t8::NRT][t8::CT];
+    f32x4 acc[T8<NQ>::NRT][t8::CT];
     const int ct0 = (wave & 1) * t8::CT;
     if (wave < 2)
-      tower8_acc<EL, 0, false>(lds, reinterpret_cast<const uint4*>(a.x.we3), TNS, ct0, a.x.be3, nullptr, nullptr, 0, res,
+      tower8_acc<EL, NQ, 0, false>(lds, reinterpret_cast<const uint4*>(a.x.we3), TNS, ct0, a.x.be3, nullptr, nullptr, 0, res,
                            acc, lane);
     else
-      tower8_acc<EL, 0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, ct0, a.x.be1, nullptr, nullptr, 0, res, acc,
+      tower8_acc<EL, NQ, 0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, ct0, a.x.be1, nullptr, nullptr, 0, res, acc,
                           lane);
     __syncthreads();
-    tower8_writeback<EL, false>(lds, acc, res, wave < 2 ? 0 : 128, ct0, lane);
+    tower8_writeback<EL, NQ, false>(lds, acc, res, wave < 2 ? 0 : 128, ct0, lane);
     __syncthreads();
     const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
-    tower_heads<EL, t8::E, 4, true>(a, lds, 0, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
+    tower_heads<EL, T8<NQ>::E, 4, true>(a, lds, 0, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
       __syncthreads();
       if (tid < nenv) {
@@ -802,7 +809,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     return;
   }
 #pragma unroll 4
-  for (int u = 0; u < 20; ++u) {
+  for (int u = 0; u < 10 * NQ; ++u) {
     const int i = u * t8::NT + tid;
     const int r = i >> 5, c = i & 31;
     if (r < rows)
@@ -811,7 +818,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   }
 }
 
-static int g_tower_variant = 0;  // 0 auto, 1 four-env kernel, 2 eight-env kernel
+static int g_tower_variant = 0;  // 0 auto, 1 four-env kernel, 2 eight-env kernel, 3 four-env 4-wave
 
 static int tower_ncu() {
   static int ncu = 0;
@@ -827,15 +834,20 @@ static int tower_ncu() {
 
 extern "C" {
 
-// 0: pick by batch (default), 1: force the 4-env kernel, 2: force the 8-env kernel
+// 0: pick by batch (default), 1: force the 4-env kernel, 2: force the 8-env kernel, 3: the 4-env
+// 4-wave kernel (the 8-env kernel's structure on one env quad)
 int mzba_tower_set_variant(int v) {
-  if (v < 0 || v > 2) return -1;
+  if (v < 0 || v > 3) return -1;
   g_tower_variant = v;
   return 0;
 }
 
-// kernel used for batch B: 1 four-env, 2 eight-env (B >= 8 x CUs: it halves the per-env weight stream
-// but needs that many envs to fill the chip). Both take agent.pack_tower_conv weights.
+// kernel used for batch B: 2 eight-env (B >= 8 x CUs: it halves the per-env weight stream but needs
+// that many envs to fill the chip), else 1 four-env 8-wave. Variant 3 = four-env 4-wave (the 8-env
+// kernel's structure on one env quad: each wave 4 column tiles x 5 row tiles, half the LDS A reads
+// per MFMA of kernel 1): 478 vs 510 us per plain 14-block tower at B = 1024 (tools/bench_conv.py
+// tower), but equal in the acting loop's fused steps (19.1k env-steps/s both, same box), so kernel 1
+// stays the default. All take agent.pack_tower_conv weights.
 int mzba_tower_plan(int B) {
   if (B <= 0) return -1;
   if (g_tower_variant) return g_tower_variant;
@@ -860,7 +872,9 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
   (void)ws;
   (void)ws_bytes;
   if (plan == 2) {
-    hipLaunchKernelGGL(tower8_kernel<0>, dim3((B + t8::E - 1) / t8::E), dim3(t8::NT), 0, stream, a);
+    hipLaunchKernelGGL((tower8_kernel<0, 2>), dim3((B + 7) / 8), dim3(t8::NT), 0, stream, a);
+  } else if (plan == 3) {
+    hipLaunchKernelGGL((tower8_kernel<0, 1>), dim3((B + 3) / 4), dim3(t8::NT), 0, stream, a);
   } else {
     hipLaunchKernelGGL(tower_kernel<0>, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
   }
@@ -874,7 +888,7 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
                      hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && wf16 && bias && ext, -1);
   const int plan = mzba_tower_plan(B);
-  MZ_CHECK_ARG(plan == 1 || plan == 2, -4);
+  MZ_CHECK_ARG(plan >= 1 && plan <= 3, -4);
   const mzba_tower_ext& x = *ext;
   MZ_CHECK_ARG(x.epilogue >= 0 && x.epilogue <= 2 && (x.elem == 0 || x.elem == 1), -2);
   MZ_CHECK_ARG(!x.w0 || (x.b0 && x.act_bias && x.act && x.A > 0), -3);
@@ -896,12 +910,14 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
     a.tree_gamma = t.gamma;
     a.tree_r = t.r;
   }
-  const dim3 g8((B + t8::E - 1) / t8::E), g4((B + TE - 1) / TE);
+  const dim3 g8((B + 7) / 8), g4((B + TE - 1) / TE);
   if (x.elem == 1) {
-    if (plan == 2) hipLaunchKernelGGL(tower8_kernel<1>, g8, dim3(t8::NT), 0, stream, a);
+    if (plan == 2) hipLaunchKernelGGL((tower8_kernel<1, 2>), g8, dim3(t8::NT), 0, stream, a);
+    else if (plan == 3) hipLaunchKernelGGL((tower8_kernel<1, 1>), g4, dim3(t8::NT), 0, stream, a);
     else hipLaunchKernelGGL(tower_kernel<1>, g4, dim3(TNT), 0, stream, a);
   } else {
-    if (plan == 2) hipLaunchKernelGGL(tower8_kernel<0>, g8, dim3(t8::NT), 0, stream, a);
+    if (plan == 2) hipLaunchKernelGGL((tower8_kernel<0, 2>), g8, dim3(t8::NT), 0, stream, a);
+    else if (plan == 3) hipLaunchKernelGGL((tower8_kernel<0, 1>), g4, dim3(t8::NT), 0, stream, a);
     else hipLaunchKernelGGL(tower_kernel<0>, g4, dim3(TNT), 0, stream, a);
   }
   MZ_LAUNCH_CHECK();

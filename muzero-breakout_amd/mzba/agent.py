@@ -342,7 +342,7 @@ class NetRunner:
                0, B, n, L.stream())
 
     def fused_ok(self):
-        return self.use_fused and self.use_tower and self.p.fused is not None and self.tower_plan in (1, 2)
+        return self.use_fused and self.use_tower and self.p.fused is not None and self.tower_plan in (1, 2, 3)
 
     def _ext(self, epilogue):
         p, f = self.p, self.p.fused

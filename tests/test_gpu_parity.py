@@ -214,7 +214,7 @@ def test_nets_bf16_close():
     assert np.abs(rl.cpu().numpy() - d["r1"]).max() < 0.05
 
 
-@pytest.mark.parametrize("B,variant", [(13, 1), (1024, 1), (13, 2), (2048, 0)])
+@pytest.mark.parametrize("B,variant", [(13, 1), (1024, 1), (13, 2), (2048, 0), (13, 3), (1024, 3)])
 def test_fused_steps_match_unfused(B, variant):
     """mzba_tower_fused (dynamics ConvBlock + tower + reward head + scale in one launch; tower +
     policy/value heads in one launch) vs the per-layer launch sequence, both bf16, same inputs;
@@ -571,7 +571,7 @@ def test_dropin_modules_resolve_via_get_class():
     assert tuple(s.shape) == e.state_shape
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("B,nblocks,gather", [(4, 1, False), (13, 3, True), (1024, 2, False)])
 def test_tower_matches_conv_chain(B, nblocks, gather, variant):
     """Fused tower (activations LDS-resident across blocks) vs torch fp32 residual blocks with
@@ -728,7 +728,7 @@ def test_checkpoint_reference_format_roundtrip(tmp_path):
     assert buf.get_reward_sums() == buf2.get_reward_sums()
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_tree_step_fused_into_prediction_is_identical(variant):
     """backup(sim) + select(sim + 1) inside the fused prediction launch == the separate tree
     kernels: same visit counts, values and tie-break draws, bit for bit (bf16 nets)."""

@@ -74,7 +74,7 @@ def run_tower(B, nblocks, iters=20, variant=0):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "tower":
         for s in [(1024, 1), (1024, 14), (2048, 14), (4096, 14)]:
-            for v in (1, 2):
+            for v in (1, 2, 3):
                 print(json.dumps(run_tower(*s, variant=v)))
         print(json.dumps(run(1024, 4, 5, 256, 256, 3, "lat")))
         sys.exit(0)
