@@ -551,7 +551,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_bf16_kernel(const bf16_t* __re
 // dY / X are read from HBM once per tile instead of once per tap.
 constexpr int WI_LD = 80;        // bf16 per LDS row (160 B, the transposed-read bank layout above)
 constexpr int WI_LEAD = 8;       // zero rows before the X images (tap offsets reach -Wp - 1)
-constexpr int WI_PF = 12;        // staging chunks per thread (KS + XR <= 384 rows)
+constexpr int WI_PF = 24;        // staging chunks per 256 threads (KS + XR <= 768 rows)
 
 // up to WG_MAXSEG (x, dY) segments of Bseg envs each form one contraction (env b = seg * Bseg + b'):
 // the K unrolled uses of one latent conv reduce in a single launch (learner._flush_wgrad)
@@ -782,7 +782,7 @@ static bool wgrad_img_plan(int B, int Bseg, int H, int W, int Cin, int Cout, WgP
   int E = 1;
   auto rows = [&](int e) { return ((e * HWp + 31) / 32 * 32) + WI_LEAD + e * HpWp + 64; };
   auto staged = [&](int e) { return (e * HWp + 31) / 32 * 32 + e * HpWp; };
-  while (E < 16 && Bseg % (E * 2) == 0 && (size_t)rows(E * 2) * WI_LD * 2 <= 64 * 1024 && staged(E * 2) * 8 <= WI_PF * 256) E *= 2;
+  while (E < 16 && Bseg % (E * 2) == 0 && (size_t)rows(E * 2) * WI_LD * 2 <= WI_LDS_MAX && staged(E * 2) * 8 <= WI_PF * 256) E *= 2;
   if ((size_t)rows(E) * WI_LD * 2 > WI_LDS_MAX) return false;
   p.pf = staged(E) * 8 <= WI_PF * 256;
   const int tiles = ((Cout + 63) / 64) * ((Cin + 63) / 64);
