@@ -257,6 +257,25 @@ def cfg_name(B, S, dyn=None):
     return {(1024, 50): "config 2", (4096, 50): "config 4 (per-GPU share)"}.get((B, S), "custom")
 
 
+def step_flops(p, H, W, S):
+    """Algorithmic FLOPs of one acting env-step: representation + root prediction +
+    S x (dynamics + prediction), convs and linear heads, at this geometry (72.17 G at 16x20, S=50)."""
+    c0, c1, hw = p.c0, p.c1, p.lh * p.lw
+    fl, hh, ww, cin = 0.0, H, W, 2 * p.L
+    for kind, layer in p.rep:
+        if kind == "pool":
+            hh, ww = hh // 2, ww // 2
+            continue
+        for c in ([layer] if kind == "conv" else list(layer)):
+            ci = cin if c is p.rep[0][1] else c["cin"]
+            fl += 2.0 * hh * ww * c["cout"] * c["ks"] ** 2 * ci
+    conv = lambda ci, co, ks: 2.0 * hw * co * ks * ks * ci  # noqa: E731
+    pred = 2 * len(p.pred) * conv(c1, c1, 3) + conv(c1, c1 // 2, 3) + conv(c1, c1 // 2, 1) + \
+        2.0 * hw * (c1 // 2) * (3 + p.ns)
+    dyn = conv(c1 + 3, c1, 3) + 2 * len(p.dyn) * conv(c1, c1, 3) + conv(c1, c1, 1) + 2.0 * hw * c1 * p.ns
+    return fl + pred + S * (dyn + pred)
+
+
 def conv_flops(B, hw, C):
     return 2.0 * B * hw * C * 9 * C
 
@@ -286,11 +305,18 @@ def main():
     cfg["num_simulations"] = args.sims
     mcfg = cfg["model"]
     B = args.envs
+    # frame geometry: 16x20 / 32-frame stack (the reference's), or --height/--width/--hist for
+    # config 3's acting geometry (84x84, 4-frame stack, latent 21x21 after the two pools)
+    H, W = args.height or 16, args.width or 20
+    custom_geom = (H, W) != (16, 20)
+    if custom_geom:
+        mcfg["state_history_length"] = args.hist
+        mcfg["latent_resolution"] = [H // 4, W // 4]
     sd = init_state_dict(mcfg, args.seed)
     agent = MuZeroAgent(mcfg, dtype=args.dtype, device=f"cuda:{local}", dyn_dtype=args.dyn_dtype)
     agent.load_state_dict(sd)
-    loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B)
-    gather = TrajectoryGather(world, rank, RECORD_K, B, 16 * 20, f"cuda:{local}")
+    loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B, height=H, width=W)
+    gather = TrajectoryGather(world, rank, RECORD_K, B, H * W, f"cuda:{local}")
     loop.reset(0)
     last_flush = [0]
 
@@ -315,7 +341,7 @@ def main():
 
     # ---- visit-count match + CPU baseline on a bounded sample (rank 0, N=1 only) -------
     cpu_info, match, match_f32 = None, None, None
-    want_cpu = rank == 0 and world == 1 and not args.no_cpu
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu and not custom_geom
     if want_cpu:
         nb = min(args.cpu_envs, B)
         cs = loop.cs
@@ -405,14 +431,17 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype + ("; dynamics fp16" if args.dyn_dtype == "fp16" else ""),
             "data": "synthetic: seeded random-init reference-architecture nets, seeded Breakout episodes",
-            "config": {"workload": f"{cfg_name(B, args.sims, args.dyn_dtype)}: {B} envs/GPU x {args.sims} MCTS sims, 16x20 Breakout, "
-                                   "32-frame stack",
+            "config": {"workload": (f"{cfg_name(B, args.sims, args.dyn_dtype)}: {B} envs/GPU x {args.sims} MCTS sims, "
+                                    "16x20 Breakout, 32-frame stack") if not custom_geom else
+                                   (f"config 3 acting geometry: {B} envs/GPU x {args.sims} MCTS sims, {H}x{W} Breakout, "
+                                    f"{args.hist}-frame stack, latent {H // 4}x{W // 4} (generic conv kernels)"),
                        "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
                        "parallelism": f"env-sharded x{world}, RCCL all-gather of trajectory records"},
             "roofline": {"bound": "mfma",
                          "kernel": "tower_kernel (fused 14-block residual tower, bf16 3x3 256->256 convs, M=B*20,"
                                    " N=256, K=2304 each)" if tower_launch_ms else
-                                   "conv_lat_kernel<3,256> bf16 3x3 256->256 (M=B*20,N=256,K=2304)",
+                                   (f"latent residual conv bf16 3x3 256->256 (M=B*{p.lh * p.lw},N=256,K=2304; "
+                                    f"{'conv_lat' if p.lh * p.lw <= 160 else 'conv_igemm'} kernel)"),
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": traffic,
                          "flop_per_conv": fl, "avg_ms_per_conv": conv_ms, "avg_launch_ms": tower_launch_ms or conv_ms,
@@ -421,8 +450,9 @@ def main():
             "visit_count_match": match,
             "visit_count_match_f32_path": match_f32,
             "launch": "eager" if args.no_graph else "hip-graph replay (probe step eager)",
-            "whole_step_mfma_frac": (B * world * (3.4446e9 + 0.6738e9 + args.sims * 1.3610e9) * args.steps / dt / 1e12)
+            "whole_step_mfma_frac": (B * world * step_flops(agent.packed, H, W, args.sims) * args.steps / dt / 1e12)
                                     / (PEAK_BF16_TFLOPS * world),
+            "flop_per_env_step": step_flops(agent.packed, H, W, args.sims),
         }
         print(json.dumps(out))
     if world > 1:
