@@ -91,6 +91,9 @@ int mzba_env_current_frame(const uint8_t* cur_frame, const uint8_t* cur_src, con
  * parent latents from the node pool). w: [Cout][ks*ks*Cin] (tap-major, K-contiguous). bias f32.
  * act_bias f32 [HW][A][Cout] + act i32[B]: the dynamics net's one-hot action planes
  * (mcts.py:252-268). res: residual [B*HW][Cout] (may alias out). Cin % (dtype ? 8 : 4) == 0, Cout % 4 == 0. */
+/* 1 (default): bf16 convs over >= 64K pixels with Cout % 256 == 0 (no action bias / slot gather) run on
+ * a 256-pixel x 256-channel tile kernel (large images: config 3's 84x84 / 21x21); 0: always the generic one. */
+int mzba_conv2d_set_variant(int v);
 int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                 const void* w, const float* bias, const float* act_bias, const int32_t* act, int A, const void* res,
                 void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream);

@@ -199,6 +199,129 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
   }
 }
 
+// Large-image bf16 conv (config 3 geometry: 84x84 / 42x42 images, 21x21 latents; M = B*H*W in the
+// millions): one workgroup = 256 pixels x 256 output channels, 8 waves (2 pixel halves x 4 channel
+// quarters), each 128 x 64 = 8 x 4 tiles of v_mfma_f32_16x16x32_bf16 with the WEIGHTS as the A
+// operand, so a lane's accumulator holds 4 consecutive channels of one pixel (8-byte bf16 stores).
+// K-step = 64 (tap-resolved 16-B chunks as conv_igemm); operands global -> VGPR -> LDS (double
+// buffer, one barrier per K-step); loads unconditional from clamped addresses, zero select at the
+// LDS store, so they stay in flight under the previous step's MFMAs. Each staged pixel row is read
+// by all 256 channels of the tile (conv_igemm's 128 x 128 tile loads it twice).
+namespace big {
+constexpr int BM = 256, BN = 256, NT = 512, BK = 64, ROWB = 128;
+constexpr int TILE = BM * ROWB;  // 32 KB per operand per stage
+}
+
+__global__ __launch_bounds__(big::NT, 1) void conv_big_bf16_kernel(ConvArgs a) {
+  using big::NT; using big::BK; using big::TILE;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_big[];  // [2 stages][A | W]
+  const int HW = a.H * a.W;
+  const int M = a.B * HW;
+  const int m0 = blockIdx.x * big::BM, n0 = blockIdx.y * big::BN;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;  // pixel half (128), channel quarter (64)
+  const int pad = a.ks / 2;
+  const int Ktot = a.ks * a.ks * a.Cin;
+  const int nK = (Ktot + BK - 1) / BK;
+  const int j = tid & 7, r0 = tid >> 3;  // staging: chunk j of rows r0 + 64 i
+  const bf16_t* in = (const bf16_t*)a.in;
+  const bf16_t* wgt = (const bf16_t*)a.w;
+  const bf16_t* abase[4];
+  int ay[4], ax[4];
+  bool mval[4], nval[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + r0 + 64 * i;
+    mval[i] = m < M;
+    const int mm = mval[i] ? m : 0;
+    const int b = mm / HW, p = mm - b * HW;
+    ay[i] = p / a.W;
+    ax[i] = p - ay[i] * a.W;
+    abase[i] = in + (long long)b * a.in_env_stride;
+    nval[i] = n0 + r0 + 64 * i < a.Cout;
+  }
+  uint4 ra[4], rb[4];
+  bool oka[4], okb[4];
+  auto load_tile = [&](int ks) {
+    const int k = ks * BK + j * 8;
+    const bool kok = k < Ktot;
+    const int tap = k / a.Cin, c = k - tap * a.Cin;
+    const int ky = tap / a.ks - pad, kx = tap % a.ks - pad;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int sy = ay[i] + ky, sx = ax[i] + kx;
+      oka[i] = kok && mval[i] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
+      ra[i] = *reinterpret_cast<const uint4*>(abase[i] + (oka[i] ? (long long)(sy * a.W + sx) * a.Cin + c : 0));
+      okb[i] = kok && nval[i];
+      rb[i] = *reinterpret_cast<const uint4*>(wgt + (okb[i] ? (long long)(n0 + r0 + 64 * i) * Ktot + k : 0));
+    }
+  };
+  auto store_tile = [&](int buf) {
+    uint8_t* la = lds_big + buf * 2 * TILE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = r0 + 64 * i;
+      *reinterpret_cast<uint4*>(la + swz(row, j)) = oka[i] ? ra[i] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(la + TILE + swz(row, j)) = okb[i] ? rb[i] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  f32x4 acc[8][4];  // [pixel tile][channel tile]: D[channel 4q + i][pixel l16]
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int ks = 0; ks < nK; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nK) load_tile(ks + 1);
+    const uint8_t* la = lds_big + buf * 2 * TILE;
+    const uint8_t* lw = la + TILE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 wf[4], xf[8];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        wf[ni] = *reinterpret_cast<const bf16x8*>(lw + swz(wn * 64 + ni * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+        xf[mi] = *reinterpret_cast<const bf16x8*>(la + swz(wm * 128 + mi * 16 + fr, kk * 4 + fq));
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], xf[mi], acc[mi][ni], 0, 0, 0);
+    }
+    if (ks + 1 < nK) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+  // epilogue: lane holds channels n .. n+3 of pixel m: + bias (+ residual), ReLU, 8-byte stores
+  bf16_t* out = (bf16_t*)a.out;
+  const bf16_t* res = (const bf16_t*)a.res;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = n0 + wn * 64 + ni * 16 + 4 * fq;
+    if (n >= a.Cout) continue;
+    const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int m = m0 + wm * 128 + mi * 16 + fr;
+      if (m >= M) continue;
+      float v0 = acc[mi][ni][0] + bb.x, v1 = acc[mi][ni][1] + bb.y, v2 = acc[mi][ni][2] + bb.z,
+            v3 = acc[mi][ni][3] + bb.w;
+      if (res) {
+        const uint2 r = *reinterpret_cast<const uint2*>(res + (long long)m * a.Cout + n);
+        v0 += bf16_to_f32((bf16_t)(r.x & 0xffffu)); v1 += bf16_to_f32((bf16_t)(r.x >> 16));
+        v2 += bf16_to_f32((bf16_t)(r.y & 0xffffu)); v3 += bf16_to_f32((bf16_t)(r.y >> 16));
+      }
+      if (a.relu) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
+      *reinterpret_cast<uint2*>(out + (long long)m * a.Cout + n) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+    }
+  }
+}
+
 // 2x2 average pool, NHWC (networks.py:44 nn.AvgPool2d(2, 2))
 template <typename T>
 __global__ void avgpool2_kernel(const T* __restrict__ in, T* __restrict__ out, int B, int H, int W, int C) {
@@ -297,9 +420,25 @@ __global__ __launch_bounds__(256) void scale_state_big_kernel(const T* __restric
   }
 }
 
+static int g_conv_big = 1;  // 1: large bf16 convs on conv_big_bf16_kernel (mzba_conv2d_set_variant)
+
 template <typename T>
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   const int M = a.B * a.H * a.W;
+  // large images: 256 x 256 tiles (the 4x5 / 8x10 / 16x20 convs have their own kernels)
+  if (sizeof(T) == 2 && g_conv_big && a.Cout % 256 == 0 && !a.act_bias && !a.slot && M >= 64 * 1024) {
+    static bool attr = false;
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_big_bf16_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 4 * big::TILE);
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+    dim3 grid((M + big::BM - 1) / big::BM, a.Cout / big::BN);
+    hipLaunchKernelGGL(conv_big_bf16_kernel, grid, dim3(big::NT), 4 * big::TILE, s, a);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  }
   dim3 grid((M + BM - 1) / BM, (a.Cout + BN - 1) / BN);
   hipLaunchKernelGGL(conv_igemm_kernel<T>, grid, dim3(NT), 0, s, a);
   MZ_LAUNCH_CHECK();
@@ -309,6 +448,14 @@ int launch_conv(const ConvArgs& a, hipStream_t s) {
 }  // namespace
 
 extern "C" {
+
+// 1 (default): bf16 convs with M >= 64K pixels, Cout % 256 == 0, no action bias / slot gather on the
+// 256 x 256 large-image kernel; 0: always conv_igemm
+int mzba_conv2d_set_variant(int v) {
+  if (v < 0 || v > 1) return -1;
+  g_conv_big = v;
+  return 0;
+}
 
 // dtype: 0 = f32 (parity), 1 = bf16
 int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,

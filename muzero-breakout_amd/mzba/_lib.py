@@ -31,6 +31,7 @@ SIGNATURES = {
     "mzba_env_current_frame": [P, P, P, P, I, P, I, I, P],
     "mzba_env_set_block_envs": [I],
     "mzba_conv2d": [I, P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
+    "mzba_conv2d_set_variant": [I],
     "mzba_conv_lat_supported": [I, I, I, I, I],
     "mzba_conv_lat_set_variant": [I],
     "mzba_conv_lat": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],

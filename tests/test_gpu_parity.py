@@ -310,6 +310,38 @@ def test_conv_kernel_vs_torch_fp32_random():
             assert err < tol, (B, H, W, Cin, Cout, ks, dt, err)
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,ks,relu", [(150, 21, 21, 256, 256, 3, 1), (12, 84, 84, 128, 256, 3, 0),
+                                                     (40, 42, 42, 256, 256, 1, 1), (130, 21, 21, 64, 512, 3, 1)])
+def test_conv_big_kernel_vs_torch_fp32(B, H, W, Cin, Cout, ks, relu):
+    """The 256 x 256 large-image bf16 conv (mzba_conv2d on >= 64K pixels: config 3's 84x84 / 42x42
+    images and 21x21 latents) vs a torch fp32 conv of the same bf16 operands (+ bias, residual,
+    ReLU), ragged pixel counts; and close to the generic kernel (variant 0)."""
+    from mzba import _lib as L
+    g = torch.Generator(device="cuda").manual_seed(B + Cin)
+    dev = torch.device("cuda")
+    x = torch.randn(B, H, W, Cin, generator=g, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Cout, ks, ks, Cin, generator=g, device=dev) / (Cin * ks * ks) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g, device=dev)
+    res = torch.randn(B, H, W, Cout, generator=g, device=dev).to(torch.bfloat16)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=ks // 2)
+    ref = ref.permute(0, 2, 3, 1) + res.float()
+    if relu:
+        ref = torch.relu(ref)
+    outs = []
+    for variant in (1, 0):
+        out = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=dev)
+        L.call("mzba_conv2d_set_variant", variant)
+        try:
+            L.call("mzba_conv2d", 1, L.ptr(x), H * W * Cin, None, 0, L.ptr(w), L.ptr(b), None, None, 0, L.ptr(res),
+                   L.ptr(out), B, H, W, Cin, Cout, ks, relu, L.stream())
+        finally:
+            L.call("mzba_conv2d_set_variant", 1)
+        outs.append(out.float())
+    scale = ref.abs().max().item()
+    assert (outs[0] - ref).abs().max().item() <= 1e-2 * scale  # bf16 output rounding
+    assert (outs[0] - outs[1]).abs().max().item() <= 1e-2 * scale
+
+
 # ------------------------------------------------------------------------------ MCTS
 @pytest.mark.parametrize("tag", ["b16_s50", "b4_s200"])
 def test_mcts_replay_bit_exact(tag):
