@@ -288,11 +288,13 @@ __global__ __launch_bounds__(big::NT, 1) void conv_big_bf16_kernel(ConvArgs a) {
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
         xf[mi] = *reinterpret_cast<const bf16x8*>(la + swz(wm * 128 + mi * 16 + fr, kk * 4 + fq));
+      __builtin_amdgcn_s_setprio(1);  // keep the MFMA cluster together (cdna_hip_programming T5)
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], xf[mi], acc[mi][ni], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     if (ks + 1 < nK) store_tile(buf ^ 1);
     __syncthreads();
