@@ -110,17 +110,21 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
                   const void* wf, const float* bias, const float* act_bias, const int32_t* act, int A,
                   const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
                   hipStream_t stream);
-/* Learner (bf16, no bias fold, no ReLU): conv_lat of an NHWC batch with the consuming BatchNorm's
+/* Learner (bf16, no bias fold, no ReLU): conv_lat of an NHWC batch (optionally applying the PRODUCING
+ * BatchNorm while staging: pstats != NULL -> the conv input is y = [prelu](in * alpha + beta' [+ pres]),
+ * alpha / beta' = pstats rows 2 / 3, and y is stored to pout, replacing mzba_bn_apply) with the consuming BatchNorm's
  * per-workgroup batch statistics computed in the epilogue (replaces bn_stats_partial /
  * bn_backward's partial pass, learn.hip). mode 1: part[chunk][Cout] = (mean, M2) of the bf16
  * outputs over the chunk's rows (-> mzba_bn_stats_final); mode 2: out = bf16(conv + res) * [y > 0]
  * (the ReLU mask of the BN output y) and part[chunk][Cout] = (sum g, sum g (x - mean)) with x the
- * BN input, mean = stats row 0 (-> mzba_bn_backward_final). Cout % 128 == 0; res may alias out.
+ * BN input, mean = stats row 0 (-> mzba_bn_backward_final); mode 0: no statistics. Cout % 128 == 0;
+ * res may alias out.
  * mzba_conv_lat_bn_chunks gives the chunk count (part has nchunk * Cout float2) and rows per chunk. */
 int mzba_conv_lat_bn_chunks(int B, int H, int W, int Cin, int Cout, int ks, int* nchunk, int* rpc);
 int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const void* res, void* out, int B, int H,
                      int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
-                     const float* mean, hipStream_t stream);
+                     const float* mean, const float* pstats, const void* pres, int prelu, void* pout,
+                     hipStream_t stream);
 
 /* Fused residual tower: nblocks ResidualBlock(256) on the 4x5 latent in ONE launch (networks.py:19-35,
  * 124-131, 190-197); a workgroup keeps 4 (or, for B >= 8 x CUs, 8) envs' activations in LDS for the

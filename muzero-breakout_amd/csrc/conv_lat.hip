@@ -64,6 +64,13 @@ struct LatArgs {
   const bf16_t* sy;
   const bf16_t* sx;
   const float* smean;
+  // learner: the producing BatchNorm's apply in the staging (pstats != null): the staged input is
+  // y = [prelu](in * alpha + beta' [+ pres]) with alpha / beta' = pstats rows 2 / 3, and the
+  // workgroups of column block 0 also store y to pout (the BN output the backward needs)
+  const float* pstats;
+  const bf16_t* pres;
+  int prelu;
+  bf16_t* pout;
 };
 
 // epilogue: (1) issue the residual loads (16 B per lane) so they land while the f32 tile is
@@ -238,6 +245,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
   constexpr int LDS_A = (MAXROWS + 1) * ROWB, LDS_C = (MAXROWS + NT / 128) * 128 * 4;  // + BN-stats scratch
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_A > LDS_C ? LDS_A : LDS_C];
   __shared__ long long envoff[32 * RT];
+  __shared__ float s_ab[2][CIN];  // BN apply prologue: alpha, beta'
   const int HW = a.H * a.W;
   const int env0 = blockIdx.x * a.E;
   const int nenv = min(a.E, a.B - env0);
@@ -262,6 +270,8 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
     if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
     envoff[tid] = off;
   }
+  if (a.pstats)
+    for (int c = tid; c < CIN; c += NT) { s_ab[0][c] = a.pstats[2 * CIN + c]; s_ab[1][c] = a.pstats[3 * CIN + c]; }
   __syncthreads();
   // ---- stage the block's input activations (and the zero row) into LDS
   constexpr int TOTAL = (MAXROWS + 1) * NCHUNK;
@@ -277,6 +287,43 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
       const int e = rr / HW, p = rr - (rr / HW) * HW;
       v[u] = *reinterpret_cast<const uint4*>(a.in + envoff[e] + (long long)p * CIN + c * 8);
       if (!ok) v[u] = make_uint4(0, 0, 0, 0);
+    }
+    if (a.pstats) {  // BN apply (learner): rows are contiguous NHWC, env stride HW * CIN
+      uint4 rv[PER];
+      if (a.pres) {
+#pragma unroll
+        for (int u = 0; u < PER; ++u) {
+          const int i = u * NT + tid;
+          const int r = i / NCHUNK, c = i % NCHUNK;
+          const int rr = (i < TOTAL && r < rows) ? r : 0;
+          rv[u] = *reinterpret_cast<const uint4*>(a.pres + ((long long)env0 * HW + rr) * CIN + c * 8);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int i = u * NT + tid;
+        const int r = i / NCHUNK, c = i % NCHUNK;
+        if (!(i < TOTAL && r < rows)) continue;
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        uint32_t rw[4] = {0u, 0u, 0u, 0u};
+        if (a.pres) { rw[0] = rv[u].x; rw[1] = rv[u].y; rw[2] = rv[u].z; rw[3] = rv[u].w; }
+        uint32_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int ch = c * 8 + 2 * q;
+          float y0 = bf16_to_f32((bf16_t)(w[q] & 0xffffu)) * s_ab[0][ch] + s_ab[1][ch];
+          float y1 = bf16_to_f32((bf16_t)(w[q] >> 16)) * s_ab[0][ch + 1] + s_ab[1][ch + 1];
+          if (a.pres) {
+            y0 = y0 + bf16_to_f32((bf16_t)(rw[q] & 0xffffu));
+            y1 = y1 + bf16_to_f32((bf16_t)(rw[q] >> 16));
+          }
+          if (a.prelu) { y0 = fmaxf(y0, 0.f); y1 = fmaxf(y1, 0.f); }
+          o[q] = (uint32_t)f32_to_bf16(y0) | ((uint32_t)f32_to_bf16(y1) << 16);
+        }
+        v[u] = make_uint4(o[0], o[1], o[2], o[3]);
+        if (blockIdx.y == 0)
+          *reinterpret_cast<uint4*>(a.pout + ((long long)env0 * HW + r) * CIN + c * 8) = v[u];
+      }
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -689,12 +736,15 @@ int mzba_conv_lat_bn_chunks(int B, int H, int W, int Cin, int Cout, int ks, int*
 
 int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const void* res, void* out, int B, int H,
                      int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
-                     const float* mean, hipStream_t stream) {
-  MZ_CHECK_ARG(B > 0 && in && wf && bias && out && part && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
-  MZ_CHECK_ARG(Cout % 128 == 0 && (mode == 1 || (mode == 2 && y && x && mean)), -3);
+                     const float* mean, const float* pstats, const void* pres, int prelu, void* pout,
+                     hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && in && wf && bias && out && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
+  MZ_CHECK_ARG(Cout % 128 == 0 && (mode == 0 || (part && (mode == 1 || (mode == 2 && y && x && mean)))), -3);
+  MZ_CHECK_ARG(!pstats || pout, -3);
   LatArgs a{(const bf16_t*)in, (long long)H * W * Cin, nullptr, 0, (const bf16_t*)wf, bias, nullptr, nullptr, 0,
             (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, 0, 0,
-            mode, (float2*)part, (const bf16_t*)y, (const bf16_t*)x, mean};
+            mode, (float2*)part, (const bf16_t*)y, (const bf16_t*)x, mean,
+            pstats, (const bf16_t*)pres, prelu, (bf16_t*)pout};
   return lat_launch(a, stream);
 }
 

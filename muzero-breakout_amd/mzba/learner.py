@@ -102,6 +102,7 @@ class Learner:
         # BN's input (forward) / output gradient (backward) — mzba_conv_lat_bn
         self.fuse_bn = fuse_bn
         self._gpart = {}
+        self._lazy = {}  # BN outputs whose apply rides on the consuming conv_lat (id(y) -> (y, t, stats, res, relu))
         self._pending = None
         self._graph = None        # captured minibatch (capture()), replayed by train_minibatch
         self._capturing = False
@@ -348,21 +349,38 @@ class Learner:
     def _fusable(self, kind, cout):
         return self.fuse_bn and self.dt == 1 and kind == "lat" and cout % 128 == 0
 
-    def _lat_bn(self, x, w, bias, res, out, B, H, W, cin, cout, ks, mode, y=None, t=None, stats=None):
-        """mzba_conv_lat_bn: the conv plus its consumer BN's per-workgroup partial statistics."""
+    def _lat_bn(self, x, w, bias, res, out, B, H, W, cin, cout, ks, mode, y=None, t=None, stats=None, pro=None):
+        """mzba_conv_lat_bn: the conv plus its consumer BN's per-workgroup partial statistics;
+        pro = (stats, res, relu, y) of the producing BN applied while staging (x is then its input t)."""
         nc, rpc = ctypes.c_int(), ctypes.c_int()
         L.call("mzba_conv_lat_bn_chunks", B, H, W, cin, cout, ks, ctypes.byref(nc), ctypes.byref(rpc))
         part = torch.empty(nc.value * cout * 2, dtype=torch.float32, device=self.device)
+        ps, pr, prelu, po = pro if pro is not None else (None, None, 0, None)
         L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(w), L.ptr(bias), L.ptr(res), L.ptr(out), B, H, W, cin, cout, ks, mode,
-               L.ptr(part), L.ptr(y), L.ptr(t), L.ptr(stats), L.stream())
+               L.ptr(part), L.ptr(y), L.ptr(t), L.ptr(stats), L.ptr(ps), L.ptr(pr), int(prelu), L.ptr(po), L.stream())
         return part, nc.value, rpc.value
+
+    def _materialize(self, y):
+        """Run the deferred apply of BN output y (when no conv_lat consumed it)."""
+        e = self._lazy.pop(id(y), None)
+        if e is not None and e[0] is y:
+            _, t, stats, res, relu = e
+            L.call("mzba_bn_apply", self.dt, L.ptr(t), L.ptr(stats), L.ptr(res), int(relu), L.ptr(y), t.shape[0],
+                   t.shape[1], L.stream())
+        return y
 
     def _conv(self, c, x, B, H, W, bn=False):
         """Forward conv; bn: a BatchNorm consumes the output (its statistics may ride on the conv).
+        A deferred BN output x is applied while staging when both ride on conv_lat.
         Returns (output, fused partials or None)."""
         t = self._act(B * H * W, c.cout)
         if bn and self._fusable(c.fkind, c.cout):
+            e = self._lazy.pop(id(x), None)
+            if e is not None and e[0] is x:  # x = [relu](t' * alpha + beta' [+ res]) computed in the staging
+                _, tp, st, res, relu = e
+                return t, self._lat_bn(tp, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1, pro=(st, res, relu, x))
             return t, self._lat_bn(x, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1)
+        self._materialize(x)
         self._run_conv(c.fkind, x, c.cin_p, c.w if self.dt == 0 else c.wf, c.b, None, t, B, H, W, c.cout, c.ks)
         return t, None
 
@@ -370,10 +388,14 @@ class Learner:
         M = t.shape[0]
         stats = torch.empty(4, c.cout, dtype=torch.float32, device=self.device)
         rm, rv = self.run[c.bn_key]
-        if fpart is not None:
+        if fpart is not None:  # statistics from the producing conv; the apply is deferred to the consumer
             part, nc, rpc = fpart
             L.call("mzba_bn_stats_final", L.ptr(part), nc, rpc, M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma),
                    L.ptr(c.beta), L.ptr(stats), L.ptr(rm), L.ptr(rv), L.stream())
+            self.nbt[c.bn_key] += 1
+            y = self._act(M, c.cout)
+            self._lazy[id(y)] = (y, t, stats, res, relu)
+            return y, stats
         else:
             ws = self._scratch("bn", ((M + 63) // 64) * c.cout * 8 + 12 * c.cout)
             L.call("mzba_bn_stats", self.dt, L.ptr(t), M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma), L.ptr(c.beta),
@@ -440,6 +462,7 @@ class Learner:
         return out
 
     def _linear(self, key, x, B, cin, O, out):
+        self._materialize(x)
         K = self.lat[0] * self.lat[1] * cin
         L.call("mzba_linear_forward", self.dt, L.ptr(x), L.ptr(self._view(key + ".weight")),
                L.ptr(self._view(key + ".bias")), L.ptr(out), B, K, O, L.stream())
@@ -498,6 +521,7 @@ class Learner:
         return self._dgrad(c, dt, B, H, W, acc=acc, bn=nxt)
 
     def _scale_fwd(self, h, B):
+        self._materialize(h)
         hw, C = h.shape[0] // B, h.shape[1]
         out = self._act(h.shape[0], C)
         mm = torch.empty(B, 2, dtype=torch.float32, device=self.device)
@@ -577,6 +601,7 @@ class Learner:
         self._scale_idx = []
         self._pending = {} if self.defer_wgrad else None
         self._gpart = {}
+        self._lazy = {}
         self._prepare_packs()
         # ---- forward (_k_step_rollout)
         cin_p = self.rep[0][1].cin_p
@@ -594,6 +619,7 @@ class Learner:
                 tape.append(("res", mod, (sv, hh, ww)))
             else:
                 y = self._act(B * (hh // 2) * (ww // 2), h.shape[1])
+                self._materialize(h)
                 L.call("mzba_avgpool2", self.dt, L.ptr(h), L.ptr(y), B, hh, ww, h.shape[1], s)
                 tape.append(("pool", None, (hh, ww, h.shape[1])))
                 h, hh, ww = y, hh // 2, ww // 2
@@ -616,6 +642,7 @@ class Learner:
             self._linear(self.pred_vlin[0], yv, B, self.pred_vlin[1], self.ns, lv_all[k])
             # dynamics(h_k, a_k)
             xin = self._act(B * HWl, cdyn)
+            self._materialize(h)
             L.call("mzba_dyn_input", self.dt, L.ptr(h), L.ptr(g["future_actions"]), L.ptr(slots), K, k, L.ptr(xin),
                    B, HWl, self.c1, self.A, cdyn, s)
             xd, sblk = self._block_fwd(self.dyn_block, xin, B, hl, wl)
@@ -629,6 +656,8 @@ class Learner:
             unroll.append(dict(p_in=p_in, psv=psv, xp=xp, spol=spol, sval=sval, yp=yp, yv=yv, sblk=sblk, dsv=dsv,
                                xd=xd, yr=yr, srew=srew, ssc=ssc))
             h = h_next
+        for y in [e[0] for e in self._lazy.values()]:  # every BN output the backward reads exists
+            self._materialize(y)
         # ---- loss_fn
         dlr, dlv, dlp = torch.empty_like(lr_all), torch.empty_like(lv_all), torch.empty_like(lp_all)
         loss = torch.empty(4, device=self.device)

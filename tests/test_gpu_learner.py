@@ -427,7 +427,7 @@ def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks):
     part = torch.empty(nc.value * Cout * 2, device=dev)
     t = torch.empty(M, Cout, dtype=torch.bfloat16, device=dev)
     L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), None, L.ptr(t), B, H, W, Cin, Cout, ks, 1,
-           L.ptr(part), None, None, None, L.stream())
+           L.ptr(part), None, None, None, None, None, 0, None, L.stream())
     t_ref = torch.empty_like(t)
     L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, None, L.ptr(t_ref),
            B, H, W, Cin, Cout, ks, 0, L.stream())
@@ -448,7 +448,7 @@ def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks):
     acc = torch.randn(M, Cout, generator=g).to(torch.bfloat16).to(dev)
     g1, g2 = acc.clone(), acc.clone()
     L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), L.ptr(g1), L.ptr(g1), B, H, W, Cin, Cout, ks, 2,
-           L.ptr(part), L.ptr(by), L.ptr(bx), L.ptr(st2), L.stream())
+           L.ptr(part), L.ptr(by), L.ptr(bx), L.ptr(st2), None, None, 0, None, L.stream())
     L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, L.ptr(g2), L.ptr(g2),
            B, H, W, Cin, Cout, ks, 0, L.stream())
     dg1, db1, dg2, db2 = (torch.zeros(Cout, device=dev) for _ in range(4))
@@ -458,6 +458,18 @@ def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks):
     L.call("mzba_bn_backward", 1, L.ptr(g2), L.ptr(by), L.ptr(bx), L.ptr(st2), M, Cout, L.ptr(dg2), L.ptr(db2),
            L.ptr(dx2), L.ptr(ws), ws.numel(), L.stream())
     assert torch.equal(g1, g2)  # the masked gradient
+    # producing-BN apply in the staging: x itself is a BN input with stats st2 (Cin == Cout cases),
+    # y = relu(x * alpha + beta' + res) both stored (pout) and convolved; vs mzba_bn_apply + conv_lat
+    if Cin == Cout:
+        resx = torch.randn(M, Cin, generator=g).to(torch.bfloat16).to(dev)
+        y_p, y_a = torch.empty_like(x), torch.empty_like(x)
+        t_p, t_a = torch.empty_like(t), torch.empty_like(t)
+        L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), None, L.ptr(t_p), B, H, W, Cin, Cout, ks, 1,
+               L.ptr(part), None, None, None, L.ptr(st2), L.ptr(resx), 1, L.ptr(y_p), L.stream())
+        L.call("mzba_bn_apply", 1, L.ptr(x), L.ptr(st2), L.ptr(resx), 1, L.ptr(y_a), M, Cin, L.stream())
+        L.call("mzba_conv_lat", L.ptr(y_a), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, None,
+               L.ptr(t_a), B, H, W, Cin, Cout, ks, 0, L.stream())
+        assert torch.equal(y_p, y_a) and torch.equal(t_p, t_a)
     torch.testing.assert_close(dg1, dg2, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db1, db2, rtol=1e-4, atol=1e-3)
     assert (dx1.float() - dx2.float()).abs().max().item() <= 1e-2 * dx2.float().abs().max().item()
