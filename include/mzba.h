@@ -119,12 +119,15 @@ int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, 
  * (the ReLU mask of the BN output y) and part[chunk][Cout] = (sum g, sum g (x - mean)) with x the
  * BN input, mean = stats row 0 (-> mzba_bn_backward_final); mode 0: no statistics. Cout % 128 == 0;
  * res may alias out.
+ * Backward prologue (pcoef != NULL): the staged input is the BN input gradient dt = ((g - (x - mean) k)
+ * - mean_g) alpha of g = in and x = pres (mean, alpha = pstats rows 0, 2; mean_g, k = pcoef rows 0, 1
+ * from mzba_bn_backward_coef), stored to pout (replacing mzba_bn_backward_final's apply).
  * mzba_conv_lat_bn_chunks gives the chunk count (part has nchunk * Cout float2) and rows per chunk. */
 int mzba_conv_lat_bn_chunks(int B, int H, int W, int Cin, int Cout, int ks, int* nchunk, int* rpc);
 int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const void* res, void* out, int B, int H,
                      int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
                      const float* mean, const float* pstats, const void* pres, int prelu, void* pout,
-                     hipStream_t stream);
+                     const float* pcoef, hipStream_t stream);
 
 /* Fused residual tower: nblocks ResidualBlock(256) on the 4x5 latent in ONE launch (networks.py:19-35,
  * 124-131, 190-197); a workgroup keeps 4 (or, for B >= 8 x CUs, 8) envs' activations in LDS for the
@@ -333,6 +336,12 @@ int mzba_bn_stats_final(const float* part, int nchunk, int rpc, int M, int C, fl
 int mzba_bn_backward_final(int dtype, const void* g, const void* x, const float* stats, const float* part, int nchunk,
                            int M, int C, float* dgamma, float* dbeta, void* dx, void* ws, long long ws_bytes,
                            hipStream_t stream);
+/* mzba_bn_backward_final split in two: coef (dgamma / dbeta += and coef[3][C] = (mean_g, k,
+ * gamma*invstd)) and apply (dx = ((g - (x - mean) k) - mean_g) gamma invstd). */
+int mzba_bn_backward_apply(int dtype, const void* g, const void* x, const float* stats, const float* coef, void* dx,
+                           int M, int C, hipStream_t stream);
+int mzba_bn_backward_coef(const float* part, int nchunk, int M, int C, const float* stats, float* dgamma, float* dbeta,
+                          float* coef, hipStream_t stream);
 /* Weight packs from the f32 master weights w [Cout][taps][Cin]: flip = 0: cast copy (forward);
  * flip = 1: wt [cin_used][taps][Cout] = w[co][taps-1-tap][ci] (the input-gradient convolution). */
 int mzba_conv_wpack(int dtype, const float* w, void* wt, int Cout, int taps, int Cin, int cin_used, int flip,

@@ -71,6 +71,10 @@ struct LatArgs {
   const bf16_t* pres;
   int prelu;
   bf16_t* pout;
+  // backward (pcoef != null): the staged input is the BN input gradient dt = ((g - (x - mean) k) -
+  // mean_g) alpha of the BN output gradient g = in and BN input x = pres (mean / alpha = pstats rows
+  // 0 / 2, mean_g / k = pcoef rows 0 / 1: mzba_bn_backward_coef), also stored to pout
+  const float* pcoef;
 };
 
 // epilogue: (1) issue the residual loads (16 B per lane) so they land while the f32 tile is
@@ -245,7 +249,7 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
   constexpr int LDS_A = (MAXROWS + 1) * ROWB, LDS_C = (MAXROWS + NT / 128) * 128 * 4;  // + BN-stats scratch
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_A > LDS_C ? LDS_A : LDS_C];
   __shared__ long long envoff[32 * RT];
-  __shared__ float s_ab[2][CIN];  // BN apply prologue: alpha, beta'
+  __shared__ float s_ab[4][CIN];  // BN prologue: alpha, beta' (forward) / mean, alpha, mean_g, k (backward)
   const int HW = a.H * a.W;
   const int env0 = blockIdx.x * a.E;
   const int nenv = min(a.E, a.B - env0);
@@ -270,8 +274,13 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
     if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
     envoff[tid] = off;
   }
-  if (a.pstats)
+  if (a.pstats && !a.pcoef)
     for (int c = tid; c < CIN; c += NT) { s_ab[0][c] = a.pstats[2 * CIN + c]; s_ab[1][c] = a.pstats[3 * CIN + c]; }
+  if (a.pcoef)
+    for (int c = tid; c < CIN; c += NT) {
+      s_ab[0][c] = a.pstats[c]; s_ab[1][c] = a.pstats[2 * CIN + c];
+      s_ab[2][c] = a.pcoef[c]; s_ab[3][c] = a.pcoef[CIN + c];
+    }
   __syncthreads();
   // ---- stage the block's input activations (and the zero row) into LDS
   constexpr int TOTAL = (MAXROWS + 1) * NCHUNK;
@@ -311,13 +320,21 @@ __global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int ch = c * 8 + 2 * q;
-          float y0 = bf16_to_f32((bf16_t)(w[q] & 0xffffu)) * s_ab[0][ch] + s_ab[1][ch];
-          float y1 = bf16_to_f32((bf16_t)(w[q] >> 16)) * s_ab[0][ch + 1] + s_ab[1][ch + 1];
-          if (a.pres) {
-            y0 = y0 + bf16_to_f32((bf16_t)(rw[q] & 0xffffu));
-            y1 = y1 + bf16_to_f32((bf16_t)(rw[q] >> 16));
+          float y0, y1;
+          if (a.pcoef) {  // bn_bwd_apply's expression, same op order
+            const float g0 = bf16_to_f32((bf16_t)(w[q] & 0xffffu)), g1 = bf16_to_f32((bf16_t)(w[q] >> 16));
+            const float x0 = bf16_to_f32((bf16_t)(rw[q] & 0xffffu)), x1 = bf16_to_f32((bf16_t)(rw[q] >> 16));
+            y0 = ((g0 - (x0 - s_ab[0][ch]) * s_ab[3][ch]) - s_ab[2][ch]) * s_ab[1][ch];
+            y1 = ((g1 - (x1 - s_ab[0][ch + 1]) * s_ab[3][ch + 1]) - s_ab[2][ch + 1]) * s_ab[1][ch + 1];
+          } else {
+            y0 = bf16_to_f32((bf16_t)(w[q] & 0xffffu)) * s_ab[0][ch] + s_ab[1][ch];
+            y1 = bf16_to_f32((bf16_t)(w[q] >> 16)) * s_ab[0][ch + 1] + s_ab[1][ch + 1];
+            if (a.pres) {
+              y0 = y0 + bf16_to_f32((bf16_t)(rw[q] & 0xffffu));
+              y1 = y1 + bf16_to_f32((bf16_t)(rw[q] >> 16));
+            }
+            if (a.prelu) { y0 = fmaxf(y0, 0.f); y1 = fmaxf(y1, 0.f); }
           }
-          if (a.prelu) { y0 = fmaxf(y0, 0.f); y1 = fmaxf(y1, 0.f); }
           o[q] = (uint32_t)f32_to_bf16(y0) | ((uint32_t)f32_to_bf16(y1) << 16);
         }
         v[u] = make_uint4(o[0], o[1], o[2], o[3]);
@@ -737,14 +754,15 @@ int mzba_conv_lat_bn_chunks(int B, int H, int W, int Cin, int Cout, int ks, int*
 int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const void* res, void* out, int B, int H,
                      int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
                      const float* mean, const float* pstats, const void* pres, int prelu, void* pout,
-                     hipStream_t stream) {
+                     const float* pcoef, hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && in && wf && bias && out && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
   MZ_CHECK_ARG(Cout % 128 == 0 && (mode == 0 || (part && (mode == 1 || (mode == 2 && y && x && mean)))), -3);
   MZ_CHECK_ARG(!pstats || pout, -3);
+  MZ_CHECK_ARG(!pcoef || (pstats && pres), -3);
   LatArgs a{(const bf16_t*)in, (long long)H * W * Cin, nullptr, 0, (const bf16_t*)wf, bias, nullptr, nullptr, 0,
             (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, 0, 0,
             mode, (float2*)part, (const bf16_t*)y, (const bf16_t*)x, mean,
-            pstats, (const bf16_t*)pres, prelu, (bf16_t*)pout};
+            pstats, (const bf16_t*)pres, prelu, (bf16_t*)pout, pcoef};
   return lat_launch(a, stream);
 }
 

@@ -1195,6 +1195,27 @@ int mzba_bn_backward_final(int dtype, const void* g, const void* x, const float*
   });
 }
 
+int mzba_bn_backward_apply(int dtype, const void* g, const void* x, const float* stats, const float* coef, void* dx,
+                           int M, int C, hipStream_t stream) {
+  MZ_CHECK_ARG(g && x && stats && coef && dx && M > 0 && C > 0 && C % 4 == 0, -1);
+  return dispatch(dtype, [&](auto t) {
+    using T = decltype(t);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for((size_t)M * C / 4)), dim3(256), 0, stream, (const T*)g,
+                       (const T*)x, stats, coef, (T*)dx, M, C);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  });
+}
+
+int mzba_bn_backward_coef(const float* part, int nchunk, int M, int C, const float* stats, float* dgamma, float* dbeta,
+                          float* coef, hipStream_t stream) {
+  MZ_CHECK_ARG(part && stats && dgamma && dbeta && coef && nchunk > 0 && M > 0 && C > 0, -1);
+  hipLaunchKernelGGL(bn_bwd_final_kernel, dim3(C), dim3(64), 0, stream, (const float2*)part, nchunk, M, C, stats,
+                     dgamma, dbeta, coef);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
 int mzba_bn_apply(int dtype, const void* x, const float* stats, const void* res, int relu, void* out, int M, int C,
                   hipStream_t stream) {
   MZ_CHECK_ARG(x && stats && out && M > 0 && C > 0 && C % 4 == 0, -1);

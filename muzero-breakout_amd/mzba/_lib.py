@@ -65,7 +65,9 @@ SIGNATURES = {
     "mzba_bn_stats_final": [P, I, I, I, I, F, F, P, P, P, P, P, P],
     "mzba_bn_backward_final": [I, P, P, P, P, I, I, I, P, P, P, P, LL, P],
     "mzba_conv_lat_bn_chunks": [I, I, I, I, I, I, P, P],
-    "mzba_conv_lat_bn": [P, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P, I, P, P],
+    "mzba_conv_lat_bn": [P, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P, I, P, P, P],
+    "mzba_bn_backward_coef": [P, I, I, I, P, P, P, P, P],
+    "mzba_bn_backward_apply": [I, P, P, P, P, P, I, I, P],
     "mzba_conv_wpack": [I, P, P, I, I, I, I, I, P],
     "mzba_conv_wgrad_ws_bytes": [I, I, I, I, I, I],
     "mzba_conv_pack_bf16": [P, P, I, I, I, I, I, I, I, LL, P],

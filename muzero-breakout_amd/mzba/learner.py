@@ -103,6 +103,7 @@ class Learner:
         self.fuse_bn = fuse_bn
         self._gpart = {}
         self._lazy = {}  # BN outputs whose apply rides on the consuming conv_lat (id(y) -> (y, t, stats, res, relu))
+        self._lazyb = {}  # BN input gradients likewise (id(dt) -> (dt, g, t, stats, coef))
         self._pending = None
         self._graph = None        # captured minibatch (capture()), replayed by train_minibatch
         self._capturing = False
@@ -355,9 +356,10 @@ class Learner:
         nc, rpc = ctypes.c_int(), ctypes.c_int()
         L.call("mzba_conv_lat_bn_chunks", B, H, W, cin, cout, ks, ctypes.byref(nc), ctypes.byref(rpc))
         part = torch.empty(nc.value * cout * 2, dtype=torch.float32, device=self.device)
-        ps, pr, prelu, po = pro if pro is not None else (None, None, 0, None)
+        ps, pr, prelu, po, pc = pro if pro is not None else (None, None, 0, None, None)
         L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(w), L.ptr(bias), L.ptr(res), L.ptr(out), B, H, W, cin, cout, ks, mode,
-               L.ptr(part), L.ptr(y), L.ptr(t), L.ptr(stats), L.ptr(ps), L.ptr(pr), int(prelu), L.ptr(po), L.stream())
+               L.ptr(part), L.ptr(y), L.ptr(t), L.ptr(stats), L.ptr(ps), L.ptr(pr), int(prelu), L.ptr(po), L.ptr(pc),
+               L.stream())
         return part, nc.value, rpc.value
 
     def _materialize(self, y):
@@ -369,6 +371,15 @@ class Learner:
                    t.shape[1], L.stream())
         return y
 
+    def _materialize_b(self, dt):
+        """Run the deferred apply of BN input gradient dt (when no conv_lat consumed it)."""
+        e = self._lazyb.pop(id(dt), None)
+        if e is not None and e[0] is dt:
+            _, g, t, stats, coef = e
+            L.call("mzba_bn_backward_apply", self.dt, L.ptr(g), L.ptr(t), L.ptr(stats), L.ptr(coef), L.ptr(dt),
+                   t.shape[0], t.shape[1], L.stream())
+        return dt
+
     def _conv(self, c, x, B, H, W, bn=False):
         """Forward conv; bn: a BatchNorm consumes the output (its statistics may ride on the conv).
         A deferred BN output x is applied while staging when both ride on conv_lat.
@@ -378,7 +389,8 @@ class Learner:
             e = self._lazy.pop(id(x), None)
             if e is not None and e[0] is x:  # x = [relu](t' * alpha + beta' [+ res]) computed in the staging
                 _, tp, st, res, relu = e
-                return t, self._lat_bn(tp, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1, pro=(st, res, relu, x))
+                return t, self._lat_bn(tp, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1,
+                                       pro=(st, res, relu, x, None))
             return t, self._lat_bn(x, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1)
         self._materialize(x)
         self._run_conv(c.fkind, x, c.cin_p, c.w if self.dt == 0 else c.wf, c.b, None, t, B, H, W, c.cout, c.ks)
@@ -410,6 +422,13 @@ class Learner:
         M = t.shape[0]
         dt = self._act(M, c.cout)
         e = self._gpart.pop(id(dy), None)
+        if e is not None and e[0] is dy and e[1] is y and self.dt == 1:
+            # dy came masked with partials from its producing conv; the apply rides on the consumer
+            coef = torch.empty(3 * c.cout, dtype=torch.float32, device=self.device)
+            L.call("mzba_bn_backward_coef", L.ptr(e[2]), e[3], M, c.cout, L.ptr(stats), L.ptr(c.dgamma),
+                   L.ptr(c.dbeta), L.ptr(coef), L.stream())
+            self._lazyb[id(dt)] = (dt, dy, t, stats, coef)
+            return dt
         if e is not None and e[0] is dy and e[1] is y:  # dy came masked, partials from its producing conv
             ws = self._scratch("bnf", 12 * c.cout)
             L.call("mzba_bn_backward_final", self.dt, L.ptr(dy), L.ptr(t), L.ptr(stats), L.ptr(e[2]), e[3], M, c.cout,
@@ -421,6 +440,7 @@ class Learner:
         return dt
 
     def _wgrad(self, c, x, dy, B, H, W):
+        self._materialize_b(dy)
         if self._pending is not None and (H, W) == self.lat:
             # latent convs run K times per minibatch with the same weights: their weight gradients
             # are reduced in one contraction over the K (x, dY) pairs after the unrolled backward
@@ -453,10 +473,23 @@ class Learner:
         is — its ReLU mask and partial sums then ride on this conv (consumed by _bn_bwd)."""
         cu = min(c.cin, self.c1) if c is self.dyn_block else c.cin_p
         out = acc if acc is not None else self._act(B * H * W, cu)
-        if bn is not None and self._fusable(c.dkind, cu):
-            _, y, t, st = bn
-            part, nc, _ = self._lat_bn(dy, c.wt, self._zero, acc, out, B, H, W, c.cout, cu, c.ks, 2, y, t, st)
-            self._gpart[id(out)] = (out, y, part, nc)
+        lb = self._lazyb.get(id(dy))
+        pro = None
+        if lb is not None and lb[0] is dy and self._fusable(c.dkind, cu):  # dy computed while staging
+            self._lazyb.pop(id(dy))
+            _, gp, tp, stp, coef = lb
+            pro, src = (stp, tp, 0, dy, coef), gp
+        else:
+            self._materialize_b(dy)
+            src = dy
+        if (bn is not None or pro is not None) and self._fusable(c.dkind, cu):
+            if bn is not None:
+                _, y, t, st = bn
+                part, nc, _ = self._lat_bn(src, c.wt, self._zero, acc, out, B, H, W, c.cout, cu, c.ks, 2, y, t, st,
+                                           pro=pro)
+                self._gpart[id(out)] = (out, y, part, nc)
+            else:
+                self._lat_bn(src, c.wt, self._zero, acc, out, B, H, W, c.cout, cu, c.ks, 0, pro=pro)
             return out
         self._run_conv(c.dkind, dy, c.cout, c.wt, self._zero, acc, out, B, H, W, cu, c.ks)
         return out
@@ -497,15 +530,18 @@ class Learner:
         c1, c2 = r
         x, t1, a1, s1, t2, s2, out = sv
         dt2 = self._bn_bwd(c2, g, out, t2, s2)           # g <- g * [out > 0]
-        self._wgrad(c2, a1, dt2, B, H, W)
+        # input gradient first: it computes a deferred dt while staging, then the weight gradient reads it
         da1 = self._dgrad(c2, dt2, B, H, W, bn=(c1, a1, t1, s1))
+        self._wgrad(c2, a1, dt2, B, H, W)
         del dt2
         dt1 = self._bn_bwd(c1, da1, a1, t1, s1)
         del da1
-        self._wgrad(c1, x, dt1, B, H, W)
         if gx is None:                                     # skip path: the masked g itself
-            return self._dgrad(c1, dt1, B, H, W, acc=g, bn=nxt)
+            out = self._dgrad(c1, dt1, B, H, W, acc=g, bn=nxt)
+            self._wgrad(c1, x, dt1, B, H, W)
+            return out
         self._dgrad(c1, dt1, B, H, W, acc=gx)
+        self._wgrad(c1, x, dt1, B, H, W)
         L.call("mzba_axpy", self.dt, L.ptr(gx), L.ptr(g), gx.numel(), L.stream())
         return gx
 
@@ -517,8 +553,9 @@ class Learner:
     def _block_bwd(self, c, sv, g, B, H, W, acc=None, nxt=None):
         x, t, s, y = sv
         dt = self._bn_bwd(c, g, y, t, s)
+        out = self._dgrad(c, dt, B, H, W, acc=acc, bn=nxt)
         self._wgrad(c, x, dt, B, H, W)
-        return self._dgrad(c, dt, B, H, W, acc=acc, bn=nxt)
+        return out
 
     def _scale_fwd(self, h, B):
         self._materialize(h)
@@ -602,6 +639,7 @@ class Learner:
         self._pending = {} if self.defer_wgrad else None
         self._gpart = {}
         self._lazy = {}
+        self._lazyb = {}
         self._prepare_packs()
         # ---- forward (_k_step_rollout)
         cin_p = self.rep[0][1].cin_p
@@ -693,6 +731,8 @@ class Learner:
             if not self.pred_res:
                 L.call("mzba_axpy", self.dt, L.ptr(gh), L.ptr(gp), gh.numel(), s)
             unroll[k] = None
+        for dt in [e[0] for e in self._lazyb.values()]:
+            self._materialize_b(dt)
         if self._pending:
             self._flush_wgrad(B)
         # representation: scale -> [pool | res | conv] reversed

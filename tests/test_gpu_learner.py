@@ -427,7 +427,7 @@ def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks):
     part = torch.empty(nc.value * Cout * 2, device=dev)
     t = torch.empty(M, Cout, dtype=torch.bfloat16, device=dev)
     L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), None, L.ptr(t), B, H, W, Cin, Cout, ks, 1,
-           L.ptr(part), None, None, None, None, None, 0, None, L.stream())
+           L.ptr(part), None, None, None, None, None, 0, None, None, L.stream())
     t_ref = torch.empty_like(t)
     L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, None, L.ptr(t_ref),
            B, H, W, Cin, Cout, ks, 0, L.stream())
@@ -448,7 +448,7 @@ def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks):
     acc = torch.randn(M, Cout, generator=g).to(torch.bfloat16).to(dev)
     g1, g2 = acc.clone(), acc.clone()
     L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), L.ptr(g1), L.ptr(g1), B, H, W, Cin, Cout, ks, 2,
-           L.ptr(part), L.ptr(by), L.ptr(bx), L.ptr(st2), None, None, 0, None, L.stream())
+           L.ptr(part), L.ptr(by), L.ptr(bx), L.ptr(st2), None, None, 0, None, None, L.stream())
     L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, L.ptr(g2), L.ptr(g2),
            B, H, W, Cin, Cout, ks, 0, L.stream())
     dg1, db1, dg2, db2 = (torch.zeros(Cout, device=dev) for _ in range(4))
@@ -465,11 +465,26 @@ def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks):
         y_p, y_a = torch.empty_like(x), torch.empty_like(x)
         t_p, t_a = torch.empty_like(t), torch.empty_like(t)
         L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), None, L.ptr(t_p), B, H, W, Cin, Cout, ks, 1,
-               L.ptr(part), None, None, None, L.ptr(st2), L.ptr(resx), 1, L.ptr(y_p), L.stream())
+               L.ptr(part), None, None, None, L.ptr(st2), L.ptr(resx), 1, L.ptr(y_p), None, L.stream())
         L.call("mzba_bn_apply", 1, L.ptr(x), L.ptr(st2), L.ptr(resx), 1, L.ptr(y_a), M, Cin, L.stream())
         L.call("mzba_conv_lat", L.ptr(y_a), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, None,
                L.ptr(t_a), B, H, W, Cin, Cout, ks, 0, L.stream())
         assert torch.equal(y_p, y_a) and torch.equal(t_p, t_a)
+        # backward: x is a BN output gradient g (BN input bx, stats st2); the staged input is
+        # dt = ((g - (bx - mean) k) - mean_g) alpha with coef from mzba_bn_backward_coef
+        coef = torch.empty(3 * Cin, device=dev)
+        dgc, dbc = torch.zeros(Cin, device=dev), torch.zeros(Cin, device=dev)
+        L.call("mzba_bn_backward_coef", L.ptr(part), nc.value, M, Cin, L.ptr(st2), L.ptr(dgc), L.ptr(dbc), L.ptr(coef),
+               L.stream())
+        d_p, d_a = torch.empty_like(x), torch.empty_like(x)
+        o_p, o_a = torch.empty_like(t), torch.empty_like(t)
+        L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), None, L.ptr(o_p), B, H, W, Cin, Cout, ks, 0,
+               None, None, None, None, L.ptr(st2), L.ptr(bx), 0, L.ptr(d_p), L.ptr(coef), L.stream())
+        L.call("mzba_bn_backward_apply", 1, L.ptr(x), L.ptr(bx), L.ptr(st2), L.ptr(coef), L.ptr(d_a), M, Cin,
+               L.stream())
+        L.call("mzba_conv_lat", L.ptr(d_a), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, None,
+               L.ptr(o_a), B, H, W, Cin, Cout, ks, 0, L.stream())
+        assert torch.equal(d_p, d_a) and torch.equal(o_p, o_a)
     torch.testing.assert_close(dg1, dg2, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db1, db2, rtol=1e-4, atol=1e-3)
     assert (dx1.float() - dx2.float()).abs().max().item() <= 1e-2 * dx2.float().abs().max().item()
