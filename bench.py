@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-envs", type=int, default=16, help="bounded oracle sample (cpu_baseline + match rate)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
+    ap.add_argument("--learner-streams", type=int, default=2, choices=[1, 2],
+                    help="learner: 2 = prediction nets on a side stream beside the dynamics chain")
     ap.add_argument("--tower-variant", type=int, default=0, help="tower kernel (mzba_tower_set_variant; 0 = by batch)")
     ap.add_argument("--workload", default="acting", choices=["acting", "env", "learner"],
                     help="acting: the whole acting loop (headline); env: env step + render + frame stack only "
@@ -177,7 +179,7 @@ def run_learner(args, world, rank, local):
         "targets": torch.randn(cap, K, device=dev, generator=g) * 2,
         "counts": torch.randint(0, 51, (cap, K, 3), device=dev, generator=g).float() + 1,
     }
-    ln = Learner(mcfg, init_state_dict(mcfg, args.seed), K=K, dtype=dt, device=dev)
+    ln = Learner(mcfg, init_state_dict(mcfg, args.seed), K=K, dtype=dt, device=dev, streams=args.learner_streams)
     slots = [torch.randperm(cap, device=dev, generator=g)[:B].to(torch.int32) for _ in range(args.warmup + args.steps)]
     for i in range(args.warmup):
         ln.train_minibatch(ring, slots[i])
@@ -244,6 +246,7 @@ def run_learner(args, world, rank, local):
                          "traffic": None, "flop_per_minibatch": fl, "avg_launch_ms": kms},
             "loss": float(loss[0]),
             "launch": "eager" if args.no_graph else "hip-graph replay of the whole minibatch",
+            "streams": args.learner_streams,
             "cpu_baseline": cpu,
         }))
     if world > 1:

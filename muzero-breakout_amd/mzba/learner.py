@@ -20,6 +20,7 @@ trained weights load into the acting agent (`load_latest_weights`, train_torch.p
 dtype "f32" is the parity path; "bf16" stores activations and conv weights in bf16 (MFMA
 bf16) with f32 statistics, gradients, Adam state and master weights.
 """
+import contextlib
 import ctypes
 from collections import OrderedDict
 
@@ -95,8 +96,17 @@ class Learner:
     """
 
     def __init__(self, mcfg, state_dict=None, K=5, dtype="f32", lr=None, seed=0, device="cuda", defer_wgrad=True,
-                 fuse_bn=True):
+                 fuse_bn=True, streams=2):
         L.require_gpu()
+        # streams=2: the prediction net of every unrolled step runs on a side stream, concurrently
+        # with the dynamics chain (forward: prediction(h_k) beside dynamics(h_k); backward: all
+        # prediction backwards beside the dynamics chain). Same launches, same per-stream order:
+        # results are bit-identical to streams=1.
+        if streams not in (1, 2):
+            raise ValueError("streams must be 1 or 2")
+        self.streams = streams
+        self._side_stream = None
+        self._tag = ""
         self.defer_wgrad = defer_wgrad
         # bf16: BN batch statistics computed in the epilogue of the conv_lat launch that produces the
         # BN's input (forward) / output gradient (backward) — mzba_conv_lat_bn
@@ -292,6 +302,7 @@ class Learner:
 
     # -- scratch -------------------------------------------------------------------------------
     def _scratch(self, name, nbytes):
+        name += self._tag  # one set per stream
         t = self._ws.get(name)
         if t is None or t.numel() < nbytes:
             t = torch.empty(int(nbytes), dtype=torch.uint8, device=self.device)
@@ -300,6 +311,40 @@ class Learner:
 
     def _act(self, rows, c):
         return torch.empty(rows, c, dtype=self.tdtype, device=self.device)
+
+    @contextlib.contextmanager
+    def _side(self):
+        """Issue the enclosed launches on the side stream (after everything issued so far on the
+        main stream); the BN outputs / input gradients they leave deferred are applied there too."""
+        if self.streams == 1:
+            yield
+            return
+        main = torch.cuda.current_stream(self.device)
+        if self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(self.device)
+        side = self._side_stream
+        side.wait_stream(main)
+        lz, lzb = set(self._lazy), set(self._lazyb)
+        self._tag = "@side"
+        try:
+            with torch.cuda.stream(side):
+                yield
+                for k in [k for k in self._lazy if k not in lz]:
+                    self._materialize(self._lazy[k][0])
+                for k in [k for k in self._lazyb if k not in lzb]:
+                    self._materialize_b(self._lazyb[k][0])
+        finally:
+            self._tag = ""
+
+    def _join(self, *shared):
+        """Main stream waits for the side stream; tensors crossing streams are recorded on both."""
+        if self.streams == 1:
+            return
+        main, side = torch.cuda.current_stream(self.device), self._side_stream
+        main.wait_stream(side)
+        for t in shared:
+            t.record_stream(side)
+            t.record_stream(main)
 
     # -- primitive ops ----------------------------------------------------------------------------
     def _prepare_packs(self):
@@ -667,17 +712,21 @@ class Learner:
         lp_all = torch.empty(K, B, self.na, device=self.device)
         unroll = []
         cdyn = self.dyn_block.cin_p
+        crossing = [lp_all, lv_all]
         for k in range(K):
-            # prediction(h_k)
+            # prediction(h_k) (side stream)
             p_in, psv = h, []
             xp = h
-            for r in self.pred_res:
-                xp, sv = self._res_fwd(r, xp, B, hl, wl)
-                psv.append(sv)
-            yp, spol = self._block_fwd(self.pred_pconv, xp, B, hl, wl)
-            self._linear(self.pred_plin[0], yp, B, self.pred_plin[1], self.na, lp_all[k])
-            yv, sval = self._block_fwd(self.pred_vconv, xp, B, hl, wl)
-            self._linear(self.pred_vlin[0], yv, B, self.pred_vlin[1], self.ns, lv_all[k])
+            self._materialize(h)
+            crossing.append(h)
+            with self._side():
+                for r in self.pred_res:
+                    xp, sv = self._res_fwd(r, xp, B, hl, wl)
+                    psv.append(sv)
+                yp, spol = self._block_fwd(self.pred_pconv, xp, B, hl, wl)
+                self._linear(self.pred_plin[0], yp, B, self.pred_plin[1], self.na, lp_all[k])
+                yv, sval = self._block_fwd(self.pred_vconv, xp, B, hl, wl)
+                self._linear(self.pred_vlin[0], yv, B, self.pred_vlin[1], self.ns, lv_all[k])
             # dynamics(h_k, a_k)
             xin = self._act(B * HWl, cdyn)
             self._materialize(h)
@@ -694,6 +743,7 @@ class Learner:
             unroll.append(dict(p_in=p_in, psv=psv, xp=xp, spol=spol, sval=sval, yp=yp, yv=yv, sblk=sblk, dsv=dsv,
                                xd=xd, yr=yr, srew=srew, ssc=ssc))
             h = h_next
+        self._join(*crossing)
         for y in [e[0] for e in self._lazy.values()]:  # every BN output the backward reads exists
             self._materialize(y)
         # ---- loss_fn
@@ -704,6 +754,28 @@ class Learner:
                L.ptr(dlr), L.ptr(dlv), L.ptr(dlp), L.ptr(loss), s)
         self.last_logits = (lr_all, lv_all, lp_all)
         # ---- backward
+        # prediction k: heads -> res blocks -> d h_k (prediction part); independent of the dynamics
+        # chain, so all K run first (side stream) and the chain adds them in
+        gps, crossing = [None] * K, [dlp, dlv]
+        with self._side():
+            for k in reversed(range(K)):
+                u = unroll[k]
+                dyv = self._linear_bwd(self.pred_vlin[0], u["yv"], dlv[k], B, self.pred_vlin[1], self.ns)
+                gp = self._block_bwd(self.pred_vconv, u["sval"], dyv, B, hl, wl)
+                dyp = self._linear_bwd(self.pred_plin[0], u["yp"], dlp[k], B, self.pred_plin[1], self.na)
+                pcons = [self._res_in_bn(r, sv) for r, sv in zip(self.pred_res, u["psv"])]
+                self._block_bwd(self.pred_pconv, u["spol"], dyp, B, hl, wl, acc=gp, nxt=pcons[-1] if pcons else None)
+                del dyv, dyp
+                for i in reversed(range(len(self.pred_res))):
+                    gp = self._res_bwd(self.pred_res[i], u["psv"][i], gp, None, B, hl, wl,
+                                       nxt=pcons[i - 1] if i > 0 else None)
+                self._materialize_b(gp)
+                gps[k] = gp
+                if self.streams == 2:
+                    ev = torch.cuda.Event()
+                    ev.record(self._side_stream)
+                    gps[k] = (gp, ev)
+                crossing.append(gp)
         gh = None  # gradient of h_{k+1} (scaled latent)
         for k in reversed(range(K)):
             u = unroll[k]
@@ -718,19 +790,15 @@ class Learner:
                 gx = self._res_bwd(self.dyn_res[i], u["dsv"][i], gx, None, B, hl, wl, nxt=dcons[i])
             gh = self._block_bwd(self.dyn_block, u["sblk"], gx, B, hl, wl)  # d h_k (first c1 channels)
             del gx
-            # prediction k: heads -> res blocks, accumulating into d h_k
-            dyv = self._linear_bwd(self.pred_vlin[0], u["yv"], dlv[k], B, self.pred_vlin[1], self.ns)
-            gp = self._block_bwd(self.pred_vconv, u["sval"], dyv, B, hl, wl)
-            dyp = self._linear_bwd(self.pred_plin[0], u["yp"], dlp[k], B, self.pred_plin[1], self.na)
-            pcons = [self._res_in_bn(r, sv) for r, sv in zip(self.pred_res, u["psv"])]
-            self._block_bwd(self.pred_pconv, u["spol"], dyp, B, hl, wl, acc=gp, nxt=pcons[-1] if pcons else None)
-            del dyv, dyp
-            for i in reversed(range(len(self.pred_res))):
-                gp = self._res_bwd(self.pred_res[i], u["psv"][i], gp, gh if i == 0 else None, B, hl, wl,
-                                   nxt=pcons[i - 1] if i > 0 else None)
-            if not self.pred_res:
-                L.call("mzba_axpy", self.dt, L.ptr(gh), L.ptr(gp), gh.numel(), s)
+            self._materialize_b(gh)
+            gp = gps[k]
+            if isinstance(gp, tuple):
+                gp, ev = gp
+                torch.cuda.current_stream(self.device).wait_event(ev)
+            L.call("mzba_axpy", self.dt, L.ptr(gh), L.ptr(gp), gh.numel(), s)  # d h_k += prediction part
+            gps[k] = None
             unroll[k] = None
+        self._join(*crossing)
         for dt in [e[0] for e in self._lazyb.values()]:
             self._materialize_b(dt)
         if self._pending:

@@ -406,6 +406,38 @@ def test_learner_graph_replay_matches_eager(dt):
     assert a.step_count == b.step_count == 4
 
 
+@pytest.mark.parametrize("dt,ch", [("f32", 32), ("bf16", 32), ("bf16", 128)])
+def test_learner_side_stream_matches_one_stream(dt, ch):
+    """streams=2 (prediction nets on a side stream beside the dynamics chain, forward and backward)
+    issues the same launches in the same per-stream order as streams=1: losses, parameters, Adam
+    moments and BN running statistics bit-identical over 3 minibatches, eager and graph-replayed.
+    ch = 128 runs the fused conv_lat + BN path (deferred BN applies crossing the side stream)."""
+    from mzba.config import learner_model_cfg
+    from mzba.learner import Learner
+    from mzba.weights import init_state_dict
+    mcfg = learner_model_cfg()
+    mcfg["latent_channels"] = [ch, ch]
+    ring = _random_ring(64, mcfg["state_history_length"], 5, 13)
+    gen = torch.Generator().manual_seed(7)
+    slots = [torch.randperm(64, generator=gen)[:32].to(torch.int32) for _ in range(4)]
+    a = Learner(mcfg, init_state_dict(mcfg, 6), K=5, dtype=dt, streams=1)
+    b = Learner(mcfg, init_state_dict(mcfg, 6), K=5, dtype=dt, streams=2)
+    c = Learner(mcfg, init_state_dict(mcfg, 6), K=5, dtype=dt, streams=2)
+    la = [a.train_minibatch(ring, s).cpu().clone() for s in slots]
+    lb = [b.train_minibatch(ring, s).cpu().clone() for s in slots]
+    lc = [c.train_minibatch(ring, slots[0]).cpu().clone()]
+    c.capture(ring, 32)
+    lc += [c.train_minibatch(ring, s).cpu().clone() for s in slots[1:]]
+    for x, y, z in zip(la, lb, lc):
+        assert torch.equal(x, y) and torch.equal(x, z), (x, y, z)
+    sa, sb, sc = a.state_dict(), b.state_dict(), c.state_dict()
+    for k in sa:
+        assert torch.equal(torch.as_tensor(sa[k]), torch.as_tensor(sb[k])), k
+        assert torch.equal(torch.as_tensor(sa[k]), torch.as_tensor(sc[k])), k
+    assert torch.equal(a.M1, b.M1) and torch.equal(a.M2, b.M2)
+    assert torch.equal(a.M1, c.M1) and torch.equal(a.M2, c.M2)
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,ks", [(512, 4, 5, 256, 256, 3), (37, 4, 5, 256, 128, 3),
                                                 (19, 4, 5, 128, 256, 1), (64, 8, 10, 256, 256, 3)])
 def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks):
