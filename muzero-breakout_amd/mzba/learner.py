@@ -496,11 +496,12 @@ class Learner:
         L.call("mzba_conv_wgrad", self.dt, L.ptr(x), L.ptr(dy), B, H, W, c.cin_p, c.cout, c.ks, L.ptr(c.dw),
                L.ptr(c.db), L.ptr(ws), ws.numel(), L.stream())
 
-    def _flush_wgrad(self, B):
-        """mzba_conv_wgrad_segs over every deferred latent conv (segments in backward order, so
-        per-segment kernels accumulate exactly as the immediate calls would)."""
+    def _flush_wgrad(self, B, convs=None):
+        """mzba_conv_wgrad_segs over every deferred latent conv (or those in `convs`; segments in
+        backward order, so per-segment kernels accumulate exactly as the immediate calls would)."""
         H, W = self.lat
-        for c, segs in self._pending.values():
+        keys = [k for k in self._pending if convs is None or any(k == id(c) for c in convs)]
+        for c, segs in [self._pending.pop(k) for k in keys]:
             for i in range(0, len(segs), 8):
                 part = segs[i:i + 8]
                 n = len(part)
@@ -510,7 +511,9 @@ class Learner:
                 ws = self._scratch("wg", nb)
                 L.call("mzba_conv_wgrad_segs", self.dt, xs, dys, n, B, H, W, c.cin_p, c.cout, c.ks, L.ptr(c.dw),
                        L.ptr(c.db), L.ptr(ws), ws.numel(), L.stream())
-        self._pending = {}
+                if self.streams == 2:  # segments may come from the other stream: free them after this one
+                    for t in (u for p in part for u in p):
+                        t.record_stream(torch.cuda.current_stream(self.device))
 
     def _dgrad(self, c, dy, B, H, W, acc=None, bn=None):
         """Input gradient of conv c (first cin_used channels); added into `acc` when given.
@@ -555,6 +558,12 @@ class Learner:
         return dx
 
     # -- blocks: forward returns (out, saved); backward takes the output gradient ------------------------
+    def _pred_convs(self):
+        cs = [self.pred_pconv, self.pred_vconv]
+        for r in self.pred_res:
+            cs += list(r)
+        return cs
+
     def _res_fwd(self, r, x, B, H, W):
         c1, c2 = r
         t1, p1 = self._conv(c1, x, B, H, W, bn=True)
@@ -776,6 +785,8 @@ class Learner:
                     ev.record(self._side_stream)
                     gps[k] = (gp, ev)
                 crossing.append(gp)
+            if self._pending is not None:  # prediction weight gradients, still beside the dynamics chain
+                self._flush_wgrad(B, self._pred_convs())
         gh = None  # gradient of h_{k+1} (scaled latent)
         for k in reversed(range(K)):
             u = unroll[k]
@@ -801,8 +812,9 @@ class Learner:
         self._join(*crossing)
         for dt in [e[0] for e in self._lazyb.values()]:
             self._materialize_b(dt)
-        if self._pending:
-            self._flush_wgrad(B)
+        if self._pending:  # dynamics weight gradients beside the representation backward
+            with self._side():
+                self._flush_wgrad(B)
         # representation: scale -> [pool | res | conv] reversed
         gx = self._scale_bwd(rep_scale, gh, B)
         for ti in reversed(range(len(tape))):
@@ -821,6 +833,7 @@ class Learner:
                 xin, hh2, ww2 = sv
                 self._wgrad(mod, xin, gx, B, hh2, ww2)
                 gx = self._dgrad(mod, gx, B, hh2, ww2) if mod is not self.rep[0][1] else None
+        self._join()
         # ---- Adam (networks.py:268)
         self.step_count += 1
         if self._capturing:
