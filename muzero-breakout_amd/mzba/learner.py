@@ -558,12 +558,6 @@ class Learner:
         return dx
 
     # -- blocks: forward returns (out, saved); backward takes the output gradient ------------------------
-    def _pred_convs(self):
-        cs = [self.pred_pconv, self.pred_vconv]
-        for r in self.pred_res:
-            cs += list(r)
-        return cs
-
     def _res_fwd(self, r, x, B, H, W):
         c1, c2 = r
         t1, p1 = self._conv(c1, x, B, H, W, bn=True)
@@ -785,8 +779,6 @@ class Learner:
                     ev.record(self._side_stream)
                     gps[k] = (gp, ev)
                 crossing.append(gp)
-            if self._pending is not None:  # prediction weight gradients, still beside the dynamics chain
-                self._flush_wgrad(B, self._pred_convs())
         gh = None  # gradient of h_{k+1} (scaled latent)
         for k in reversed(range(K)):
             u = unroll[k]
@@ -812,7 +804,9 @@ class Learner:
         self._join(*crossing)
         for dt in [e[0] for e in self._lazyb.values()]:
             self._materialize_b(dt)
-        if self._pending:  # dynamics weight gradients beside the representation backward
+        # every latent weight gradient, beside the representation backward (not earlier: the 256-workgroup
+        # contractions beside the dynamics chain slow the chain more than they gain, 32.5 vs 33.2 ms)
+        if self._pending:
             with self._side():
                 self._flush_wgrad(B)
         # representation: scale -> [pool | res | conv] reversed
