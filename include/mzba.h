@@ -106,6 +106,8 @@ int mzba_conv_lat_supported(int H, int W, int Cin, int Cout, int ks);
 /* Kernel shape selection for A/B experiments (0 = default 8-wave kernel, with 3-row-tile workgroups
  * where the 5-tile grid would leave CUs idle; 1 = 4-wave 2-tile kernel; 2 = 5-row-tile workgroups only). */
 int mzba_conv_lat_set_variant(int v);
+/* current conv_lat variant (the learner switches to 5-row tiles for its two-stream minibatch and back) */
+int mzba_conv_lat_get_variant(void);
 int mzba_conv_lat(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                   const void* wf, const float* bias, const float* act_bias, const int32_t* act, int A,
                   const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,

@@ -675,6 +675,7 @@ int mzba_conv_lat_set_variant(int v) {
   g_lat_variant = v;
   return 0;
 }
+int mzba_conv_lat_get_variant(void) { return g_lat_variant; }
 
 #ifdef MZ_LAT_STAMPS
 int mzba_lat_stamps_read(unsigned long long* host, int n) {

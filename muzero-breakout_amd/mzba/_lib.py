@@ -34,6 +34,7 @@ SIGNATURES = {
     "mzba_conv2d_set_variant": [I],
     "mzba_conv_lat_supported": [I, I, I, I, I],
     "mzba_conv_lat_set_variant": [I],
+    "mzba_conv_lat_get_variant": [],
     "mzba_conv_lat": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
     "mzba_tower": [P, LL, P, LL, P, P, P, I, I, P, LL, P],
     "mzba_tower_plan": [I],
@@ -110,7 +111,7 @@ class TowerExt(ctypes.Structure):
 
 
 # entry points that return something other than a status code
-RESTYPES = {"mzba_tower_ws_bytes": LL, "mzba_tower_plan": I, "mzba_conv_wgrad_ws_bytes": LL,
+RESTYPES = {"mzba_tower_ws_bytes": LL, "mzba_tower_plan": I, "mzba_conv_lat_get_variant": I, "mzba_conv_wgrad_ws_bytes": LL,
             "mzba_linear_ws_bytes": LL}
 
 

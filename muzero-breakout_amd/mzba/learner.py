@@ -96,7 +96,7 @@ class Learner:
     """
 
     def __init__(self, mcfg, state_dict=None, K=5, dtype="f32", lr=None, seed=0, device="cuda", defer_wgrad=True,
-                 fuse_bn=True, streams=2):
+                 fuse_bn=True, streams=2, lat_rows=None):
         L.require_gpu()
         # streams=2: the prediction net of every unrolled step runs on a side stream, concurrently
         # with the dynamics chain (forward: prediction(h_k) beside dynamics(h_k); backward: all
@@ -106,6 +106,12 @@ class Learner:
             raise ValueError("streams must be 1 or 2")
         self.streams = streams
         self._side_stream = None
+        # conv_lat workgroup rows for the bf16 latent convs: 3-row tiles fill the CUs a lone B = 512
+        # conv leaves idle; with two streams the other chain fills them and 5-row tiles (less weight
+        # streaming per row) win — 31.6 vs 32.5 ms (two streams), 42.2 vs 37.9 ms (one stream)
+        if lat_rows not in (None, 3, 5):
+            raise ValueError("lat_rows must be None, 3 or 5")
+        self.lat_rows = lat_rows if lat_rows is not None else (5 if streams == 2 else 3)
         self._tag = ""
         self.defer_wgrad = defer_wgrad
         # bf16: BN batch statistics computed in the epilogue of the conv_lat launch that produces the
@@ -675,6 +681,19 @@ class Learner:
         self._graph, self._g_ring, self._g_loss = g, ring, loss
 
     def _minibatch(self, ring, slots):
+        """One minibatch with conv_lat set to this learner's tile rows (variant 2 = 5-row tiles only,
+        0 = auto), restored afterwards; a captured graph keeps the shapes it recorded."""
+        prev = L.lib().mzba_conv_lat_get_variant()
+        want = 2 if self.lat_rows == 5 else 0
+        if prev not in (0, 2) or prev == want:
+            return self._minibatch_body(ring, slots)
+        L.call("mzba_conv_lat_set_variant", want)
+        try:
+            return self._minibatch_body(ring, slots)
+        finally:
+            L.call("mzba_conv_lat_set_variant", prev)
+
+    def _minibatch_body(self, ring, slots):
         g = ring._ring
         slots = slots.to(device=self.device, dtype=torch.int32).contiguous()
         B, K, Lh = slots.numel(), self.K, self.hist
