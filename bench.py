@@ -1,11 +1,12 @@
 """Headline benchmark: whole-node env-steps/s of the MuZero-Breakout acting loop.
 
-Workload (BASELINE.json configs[1]): 1024 parallel envs per GPU x 50 MCTS sims,
-random-init reference-architecture nets (state_dict format, seeded), bf16 on MFMA.
+Workload (BASELINE.json north_star): 4096 parallel envs per GPU x 50 MCTS sims on one MI355X
+(= config 4's per-GPU share; --envs 1024 is config 2), random-init reference-architecture nets
+(state_dict format, seeded), bf16 on MFMA.
 One "step" = one acting step over all envs of a GPU: rep-input assembly ->
 representation -> 50 x (select, dynamics, prediction, backup) -> sampling -> env step
 + render + history + trajectory record; every RECORD_K steps the records are gathered
-(RCCL all-gather for N>1) into rank 0's pinned host buffer (the replay-buffer sink).
+(RCCL gather to rank 0 for N>1) into rank 0's pinned host buffer (the replay-buffer sink).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
@@ -35,12 +36,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--envs", type=int, default=1024, help="envs per GPU")
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (north_star: 4096)")
     ap.add_argument("--sims", type=int, default=50)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--dyn-dtype", default=None, choices=[None, "fp16"], help="fp16 dynamics net (config 5)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-envs", type=int, default=16, help="bounded oracle sample (cpu_baseline + match rate)")
+    ap.add_argument("--cpu-envs", type=int, default=256,
+                    help="bounded CPU sample (cpu_baseline + match rate): ~10 s of the CPU port on 16 host cores")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
     ap.add_argument("--learner-streams", type=int, default=2, choices=[1, 2],
@@ -257,7 +259,8 @@ def cfg_name(B, S, dyn=None):
     """Which BASELINE config an acting-loop run is (per-GPU batch, sims, dynamics precision)."""
     if (B, S) == (4096, 200):
         return "config 5" if dyn == "fp16" else "config 5 geometry (bf16 dynamics)"
-    return {(1024, 50): "config 2", (4096, 50): "config 4 (per-GPU share)"}.get((B, S), "custom")
+    return {(1024, 50): "config 2",
+            (4096, 50): "north_star (4096 envs x 50 sims on 1 MI355X; = config 4's per-GPU share)"}.get((B, S), "custom")
 
 
 def step_flops(p, H, W, S):
@@ -277,6 +280,20 @@ def step_flops(p, H, W, S):
         2.0 * hw * (c1 // 2) * (3 + p.ns)
     dyn = conv(c1 + 3, c1, 3) + 2 * len(p.dyn) * conv(c1, c1, 3) + conv(c1, c1, 1) + 2.0 * hw * c1 * p.ns
     return fl + pred + S * (dyn + pred)
+
+
+def tower_traffic(B, fused_tower):
+    """PMC HBM bytes per launch of the dominant kernel at this batch (profiles/tower_hbm_traffic.json,
+    written by tools/pmc_summarize.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)."""
+    tpath = os.path.join(ROOT, "profiles", "tower_hbm_traffic.json")
+    if not (fused_tower and os.path.exists(tpath)):
+        return None, None
+    from mzba import _lib as L
+    kname = {2: "tower8_kernel<0, 2>", 3: "tower8_kernel<0, 1>"}.get(L.lib().mzba_tower_plan(B), "tower_kernel<0>")
+    for rec in json.load(open(tpath))["records"]:
+        if rec.get("envs") == B and rec.get("kernel_name") == kname:
+            return rec.get("bytes_per_launch"), rec
+    return None, None
 
 
 def conv_flops(B, hw, C):
@@ -315,10 +332,15 @@ def main():
     if custom_geom:
         mcfg["state_history_length"] = args.hist
         mcfg["latent_resolution"] = [H // 4, W // 4]
-    sd = init_state_dict(mcfg, args.seed)
     agent = MuZeroAgent(mcfg, dtype=args.dtype, device=f"cuda:{local}", dyn_dtype=args.dyn_dtype)
+    if world > 1:  # rank 0 holds the (learner's) weights; the target-net refresh hands them out
+        from mzba.shard import broadcast_state_dict
+        sd = broadcast_state_dict(mcfg, init_state_dict(mcfg, args.seed) if rank == 0 else None, agent.device)
+        sd = {k: v.numpy() for k, v in sd.items()}
+    else:
+        sd = init_state_dict(mcfg, args.seed)
     agent.load_state_dict(sd)
-    loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B, height=H, width=W)
+    loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B, height=H, width=W, n_envs_total=world * B)
     gather = TrajectoryGather(world, rank, RECORD_K, B, H * W, f"cuda:{local}")
     loop.reset(0)
     last_flush = [0]
@@ -357,12 +379,16 @@ def main():
         gpu_counts = loop.rec["counts"][t_before].cpu().numpy()[:nb] if loop.t == t_before + 1 else None
         noise = loop.ws.tree.noise.cpu().numpy()[:nb]
         x = x32.view(B, 16, 20, cs)[:nb, :, :, : 2 * loop.Lh].permute(0, 3, 1, 2).cpu().numpy()
-        from oracle import nets as N
-        from oracle.mcts import MCTSOracle, NetModel
+        # the reference's CPU structure: torch-CPU f32 nets (the reference's own ops,
+        # eval-mode BN) batched over the envs, per-env dict trees walked serially in Python
+        from oracle.mcts import MCTSOracle
+        from oracle.nets_torch import TorchNetModel
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
         nthreads = torch.get_num_threads()
+        model = TorchNetModel(sd, mcfg)
         t0 = time.perf_counter()
-        h = N.create_hidden_state_root(x, sd, mcfg)
-        _, oc = MCTSOracle(cfg, NetModel(sd, mcfg), args.seed).search(h, noise, sid)
+        h = model.representation(np.ascontiguousarray(x)).numpy()
+        _, oc = MCTSOracle(cfg, model, args.seed).search(h, noise, sid)
         cpu_s = time.perf_counter() - t0
         if gpu_counts is not None:
             match = float((gpu_counts == oc).all(1).mean())
@@ -376,7 +402,8 @@ def main():
         _, c32 = s32.search(h32)
         match_f32 = float((c32.numpy() == oc).all(1).mean())
         cpu_info = {"value": nb / cpu_s, "unit": "env-steps/s", "cores": nthreads, "kind": "port",
-                    "sample": f"oracle (numpy f32) representation + {args.sims}-sim search for {nb} envs of the "
+                    "sample": f"oracle port of the reference acting step (torch-CPU f32 nets = the reference's ops, "
+                              f"per-env Python trees): representation + {args.sims}-sim search for {nb} envs of the "
                               f"bench's own state, 1 acting step ({cpu_s:.1f} s)"}
 
     # ---- timed region ---------------------------------------------------------------------
@@ -410,16 +437,7 @@ def main():
     p = agent.packed
     fl = conv_flops(B, p.lh * p.lw, p.c1)
     achieved = fl / (conv_ms * 1e-3) / 1e12 if conv_ms else None
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "conv_hbm_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            tj = json.load(open(tpath))
-            want = "tower_kernel" if any(n > 1 for _, _, n in probe) else "conv_lat_kernel"
-            if tj.get("envs") == B and tj.get("kernel", "").startswith(want):
-                traffic = tj.get("bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_rec = tower_traffic(B, any(n > 1 for _, _, n in probe))
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -439,7 +457,7 @@ def main():
                                    (f"config 3 acting geometry: {B} envs/GPU x {args.sims} MCTS sims, {H}x{W} Breakout, "
                                     f"{args.hist}-frame stack, latent {H // 4}x{W // 4} (generic conv kernels)"),
                        "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
-                       "parallelism": f"env-sharded x{world}, RCCL all-gather of trajectory records"},
+                       "parallelism": f"env-sharded x{world}, RCCL gather of trajectory records to rank 0, target-net broadcast"},
             "roofline": {"bound": "mfma",
                          "kernel": "tower_kernel (fused 14-block residual tower, bf16 3x3 256->256 convs, M=B*20,"
                                    " N=256, K=2304 each)" if tower_launch_ms else
@@ -447,10 +465,14 @@ def main():
                                     f"{'conv_lat' if p.lh * p.lw <= 160 else 'conv_igemm'} kernel)"),
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": traffic,
+                         "traffic_algorithmic_bytes": traffic_rec and traffic_rec.get("algorithmic_bytes"),
+                         "traffic_source": traffic_rec and "profiles/tower_hbm_traffic.json",
                          "flop_per_conv": fl, "avg_ms_per_conv": conv_ms, "avg_launch_ms": tower_launch_ms or conv_ms,
                          "launches_timed": len(probe)},
             "cpu_baseline": cpu_info,
             "visit_count_match": match,
+            "visit_count_match_sample": (f"{min(args.cpu_envs, B)} envs, bf16 HIP path vs the f32 CPU port (same keyed "
+                                         "noise / tie-breaks)") if match is not None else None,
             "visit_count_match_f32_path": match_f32,
             "launch": "eager" if args.no_graph else "hip-graph replay (probe step eager)",
             "whole_step_mfma_frac": (B * world * step_flops(agent.packed, H, W, args.sims) * args.steps / dt / 1e12)

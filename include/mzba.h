@@ -272,11 +272,13 @@ int mzba_heads_bf16(int nheads, const void* x0, const void* w0, const float* b0,
 int mzba_mcts_node_bytes(void);
 
 /* _initialize_trees + _expand_root_nodes (mcts.py:73-134): root P = f32(w_pol*pi) + f32(w_noise*noise),
- * noise = noise_in or Dirichlet(alpha) from Philox stream 2 (written to noise_out), first ucb_action. */
+ * noise = noise_in or Dirichlet(alpha) from Philox stream 2 (written to noise_out), first ucb_action.
+ * w_dev (optional, device f32[2]) replaces (w_pol, w_noise): the train loop's noise_weight schedule
+ * (train_torch.py:134-135) then needs no new graph capture. */
 int mzba_mcts_root(void* nodes, float* root_sum, uint32_t* calls, int32_t* leaf_parent, int32_t* leaf_action,
                    int32_t* depth, int32_t* path, const float* sqrt_tab, const float* c_tab, int B, int S,
                    int env_offset, int search_id, uint64_t seed, const int32_t* ctx, const float* v_root, const float* pi_root,
-                   const float* noise_in, float* noise_out, float w_pol, float w_noise, float alpha,
+                   const float* noise_in, float* noise_out, float w_pol, float w_noise, const float* w_dev, float alpha,
                    hipStream_t stream);
 
 /* _select_nodes (mcts.py:136-182) for simulation sim >= 1 (ucb_action :281-298). */
@@ -296,10 +298,21 @@ int mzba_mcts_results(void* nodes, float* root_sum, uint32_t* calls, int32_t* le
                       int env_offset, int search_id, uint64_t seed, const int32_t* ctx, int64_t* counts, float* values,
                       hipStream_t stream);
 
-/* Temperature sampling (train_torch.py:191-198): p = counts^(1/T)/sum, inverse CDF of
- * u = Philox uniform(env+env_offset, stream 3, step, 0). */
-int mzba_sample_actions(const int64_t* counts, int64_t* action, int B, float temperature, int env_offset, int step,
+/* Temperature sampling (train_torch.py:191-198 `visit_counts ** (1/self.temperature)` / sum(dim=1) then
+ * Categorical(probs[i]).sample()): probs bit-identical to torch's CPU evaluation on the reference's whole
+ * (n_envs_total, 3) int64 batch tensor (csrc/torch_pow.h: SLEEF powf_u10 on its first
+ * 3n - 3n % vec_block elements, f32(pow(double)) on the rest; vec_block = 32 for the AVX512 host the
+ * fixtures came from, 16 for AVX2), then the inverse CDF of u = Philox uniform(env + env_offset,
+ * stream 3, step, 0). inv_t = 1/T in double (Python's `1/self.temperature`); inv_t_dev (optional,
+ * device f64[1]) overrides it (graph-replayable temperature schedule). probs_out (optional) f32[B][3]. */
+int mzba_sample_actions(const int64_t* counts, int64_t* action, float* probs_out, int B, double inv_t,
+                        const double* inv_t_dev, int n_envs_total, int vec_block, int env_offset, int step,
                         uint64_t seed, const int32_t* ctx, hipStream_t stream);
+
+/* torch's CPU `int64 counts ** e` (the power of mzba_sample_actions) for n elements at flat positions
+ * [start, start + n) of a tensor of n_total elements: out f32[n]. Exposed for the parity tests. */
+int mzba_torch_pow(const int64_t* counts, float* out, long long n, double e, long long start, long long n_total,
+                   int vec_block, hipStream_t stream);
 
 /* Trajectory-sink row of the search results: rec_counts[t][b] = counts[b], rec_values[t][b] = values[b],
  * t = ctx ? ctx[2] : t (replay_buffer.py:17-35 visit_counts / values). */

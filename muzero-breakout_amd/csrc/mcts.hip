@@ -13,6 +13,7 @@
 //   G = f32(f32(G * f32(gamma)) + r); Q = f32(f32(f32(N) * Q) + G) / f32(N + 1) (mcts.py:231-233)
 // Tie-breaks draw best[randbelow(len(best))] from Philox (env, STREAM_TIE, search_id, k).
 #include "common.h"
+#include "torch_pow.h"
 #include "tree_dev.h"
 
 namespace {
@@ -57,9 +58,13 @@ struct NormalGen {
 
 __global__ void root_init_kernel(TreeArgs t, const float* __restrict__ v_root, const float* __restrict__ pi_root,
                                  const float* __restrict__ noise_in, float* __restrict__ noise_out, float w_pol,
-                                 float w_noise, float alpha) {
+                                 float w_noise, const float* __restrict__ w_dev, float alpha) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= t.B) return;
+  if (w_dev) {  // (f32(1 - noise_weight), f32(noise_weight)) from the device: graph-replayable schedule
+    w_pol = w_dev[0];
+    w_noise = w_dev[1];
+  }
   float nz[3];
   if (noise_in) {
     nz[0] = noise_in[b * 3]; nz[1] = noise_in[b * 3 + 1]; nz[2] = noise_in[b * 3 + 2];
@@ -117,28 +122,42 @@ __global__ void results_kernel(TreeArgs t, int64_t* __restrict__ counts, float* 
   values[b] = (float)((double)t.root_sum[b] / (double)t.S);
 }
 
-// train_torch.py:191-198 with inverse-CDF sampling on u = uniform(env, STREAM_SAMPLE, step, 0)
-__global__ void sample_kernel(const int64_t* __restrict__ counts, int64_t* __restrict__ action, int B, float inv_t,
-                              int env_offset, int step_arg, uint64_t seed, const int32_t* __restrict__ ctx) {
+// train_torch.py:191-198: p = counts ** (1/T) / sum with torch's CPU arithmetic bit for bit
+// (torch_pow.h; the env's flat position 3 * (env_offset + b) + a in the reference's whole batch tensor
+// of n_total envs picks the SLEEF vector lane or the scalar double lane), then the inverse CDF of
+// u = uniform(env, STREAM_SAMPLE, step, 0) in place of Categorical(probs).sample().
+// 1/T (double) comes from inv_t_dev[0] when given (one captured graph replays any temperature).
+__global__ void sample_kernel(const int64_t* __restrict__ counts, int64_t* __restrict__ action,
+                              float* __restrict__ probs_out, int B, double inv_t_arg,
+                              const double* __restrict__ inv_t_dev, long long nvec, int env_offset, int step_arg,
+                              uint64_t seed, const int32_t* __restrict__ ctx) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int step = ctx ? ctx[1] : step_arg;
+  const double e = inv_t_dev ? inv_t_dev[0] : inv_t_arg;
   float vt[3];
-  for (int a = 0; a < 3; ++a) {
-    float c = (float)counts[b * 3 + a];
-    vt[a] = inv_t == 1.0f ? c : powf(c, inv_t);
-  }
-  const float s = (vt[0] + vt[1]) + vt[2];
+  for (int a = 0; a < 3; ++a)
+    vt[a] = mzpow::torch_cpu_pow(counts[b * 3 + a], e, 3LL * (b + env_offset) + a, nvec);
+  const float s = (vt[0] + vt[1]) + vt[2];  // train_torch.py:193 sum(dim=1): ((c0 + c1) + c2)
   const float u = mz_uniform((uint32_t)(b + env_offset), MZ_STREAM_SAMPLE, (uint32_t)step, 0u, seed);
   float cdf = 0.f;
   int chosen = -1, last = 0;
   for (int a = 0; a < 3; ++a) {
-    float p = vt[a] / s;
+    const float p = vt[a] / s;
+    if (probs_out) probs_out[b * 3 + a] = p;
     if (p > 0.f) last = a;
     cdf = cdf + p;
     if (chosen < 0 && u < cdf) chosen = a;
   }
   action[b] = chosen >= 0 ? chosen : last;
+}
+
+// torch's CPU int64 ** e (torch_pow.h) for n elements at flat positions [start, start + n) of a tensor
+// with vector-lane prefix nvec: the device pow exposed for exhaustive parity tests
+__global__ void torch_pow_kernel(const int64_t* __restrict__ counts, float* __restrict__ out, long long n, double e,
+                                 long long start, long long nvec) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = mzpow::torch_cpu_pow(counts[i], e, start + i, nvec);
 }
 
 // acting-loop records of the search results at row ctx[2] (train_torch.py:204-208 sink)
@@ -180,10 +199,10 @@ extern "C" {
 int mzba_mcts_node_bytes() { return (int)sizeof(Node); }
 
 int mzba_mcts_root(MZ_TREE_PARAMS, const float* v_root, const float* pi_root, const float* noise_in,
-                   float* noise_out, float w_pol, float w_noise, float alpha, hipStream_t stream) {
+                   float* noise_out, float w_pol, float w_noise, const float* w_dev, float alpha, hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && S > 0, -1);
   hipLaunchKernelGGL(root_init_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, MZ_TREE_ARGS, v_root, pi_root,
-                     noise_in, noise_out, w_pol, w_noise, alpha);
+                     noise_in, noise_out, w_pol, w_noise, w_dev, alpha);
   MZ_LAUNCH_CHECK();
   return 0;
 }
@@ -210,12 +229,23 @@ int mzba_mcts_results(MZ_TREE_PARAMS, int64_t* counts, float* values, hipStream_
   return 0;
 }
 
-int mzba_sample_actions(const int64_t* counts, int64_t* action, int B, float temperature, int env_offset, int step,
+int mzba_sample_actions(const int64_t* counts, int64_t* action, float* probs_out, int B, double inv_t,
+                        const double* inv_t_dev, int n_envs_total, int vec_block, int env_offset, int step,
                         uint64_t seed, const int32_t* ctx, hipStream_t stream) {
-  MZ_CHECK_ARG(B > 0 && temperature > 0.f, -1);
-  float inv_t = (float)(1.0 / (double)temperature);
-  hipLaunchKernelGGL(sample_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, counts, action, B, inv_t,
-                     env_offset, step, seed, ctx);
+  MZ_CHECK_ARG(B > 0 && counts && action && (inv_t_dev || inv_t > 0.0) && vec_block > 0 && env_offset >= 0 &&
+                   n_envs_total >= env_offset + B, -1);
+  const long long n = 3LL * n_envs_total;
+  hipLaunchKernelGGL(sample_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, counts, action, probs_out, B, inv_t,
+                     inv_t_dev, n - n % vec_block, env_offset, step, seed, ctx);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_torch_pow(const int64_t* counts, float* out, long long n, double e, long long start, long long n_total,
+                   int vec_block, hipStream_t stream) {
+  MZ_CHECK_ARG(n > 0 && counts && out && vec_block > 0 && start >= 0 && n_total >= start + n, -1);
+  hipLaunchKernelGGL(torch_pow_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, counts, out, n, e,
+                     start, n_total - n_total % vec_block);
   MZ_LAUNCH_CHECK();
   return 0;
 }

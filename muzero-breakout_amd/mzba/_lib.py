@@ -18,6 +18,7 @@ I = ctypes.c_int
 LL = ctypes.c_longlong
 U64 = ctypes.c_uint64
 F = ctypes.c_float
+D = ctypes.c_double
 
 # name -> argtypes (all return int: 0 ok, <0 bad argument, >0 hipError_t)
 SIGNATURES = {
@@ -52,11 +53,12 @@ SIGNATURES = {
     "mzba_support_decode": [P, P, I, I, F, F, P],
     "mzba_heads_bf16": [I, P, P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, F, I, P],
     "mzba_mcts_node_bytes": [],
-    "mzba_mcts_root": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P, P, F, F, F, P],
+    "mzba_mcts_root": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P, P, F, F, P, F, P],
     "mzba_mcts_select": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, I, P],
     "mzba_mcts_backup": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, I, P, P, P, F, P],
     "mzba_mcts_results": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P],
-    "mzba_sample_actions": [P, P, I, F, I, I, U64, P, P],
+    "mzba_sample_actions": [P, P, P, I, D, P, I, I, I, I, U64, P, P],
+    "mzba_torch_pow": [P, P, LL, D, LL, LL, I, P],
     "mzba_record_results": [P, P, P, P, I, I, P, P],
     "mzba_ctx_advance": [P, P],
     # learner (learn.hip)
@@ -127,6 +129,27 @@ def lib():
             fn.restype = RESTYPES.get(name, ctypes.c_int)
         _lib = L
     return _lib
+
+
+OPS_PATH = os.path.join(_HERE, "libmzba_torch.so")
+_ops = None
+
+
+def ops():
+    """torch.ops.mz: the TORCH_LIBRARY(mz) custom ops of csrc/torch_ops.cpp (libmzba_torch.so,
+    linked to libmzba.so) — the drop-in classes dispatch through these."""
+    global _ops
+    if _ops is None:
+        lib()
+        if not os.path.exists(OPS_PATH):
+            raise RuntimeError(f"mzba: torch op library not built ({OPS_PATH}); run __graft_entry__.build()")
+        torch.ops.load_library(OPS_PATH)
+        _ops = torch.ops.mz
+    return _ops
+
+
+TORCH_OPS = ["env_reset_", "env_step", "grayscale", "mcts_root_", "mcts_select_", "mcts_backup_", "mcts_results_",
+             "sample_actions", "support_decode"]
 
 
 def exported_symbols():

@@ -6,7 +6,7 @@ representation + min-max scaling (:254) -> latent MCTS (:256) -> temperature
 sampling (:191-198) -> env step + gray render + history push + trajectory record
 (:201-209). Everything stays on the device; the per-step records land in a device
 trajectory sink (replay_buffer.py:ObservationTrajectory fields) that is copied to the
-host once per episode (or all-gathered over RCCL for multi-GPU runs).
+host once per episode (or gathered to rank 0 over RCCL for multi-GPU runs).
 """
 import numpy as np
 import torch
@@ -54,12 +54,28 @@ class ActingLoop:
 
     MAX_STEPS = 261  # train_torch.py:186 `length_counter > 260`
 
+    # torch's CPU pow takes 2 x Vectorized<float>::size() elements per vector iteration; 32 on the
+    # AVX512 host the reference fixtures were generated on (16 on an AVX2 host), csrc/torch_pow.h
+    VEC_BLOCK = 32
+
     def __init__(self, cfg, agent, B, seed=0, env_offset=0, temperature=1.0, height=16, width=20,
-                 record_frames=True, max_steps=MAX_STEPS, pad_action=0, rec_flags=0):
+                 record_frames=True, max_steps=MAX_STEPS, pad_action=0, rec_flags=0, n_envs_total=None,
+                 rep_agent=None):
+        """`n_envs_total`: envs of the whole (sharded) batch, the reference's visit_counts tensor
+        (default env_offset + B); `rep_agent`: the net of the root representation when it differs
+        from the search's (run_test_simulation: learner net for the root, target net in the search)."""
         self.cfg, self.agent, self.B = cfg, agent, B
         self.seed, self.env_offset = seed, env_offset
-        self.temperature = temperature
+        self.n_envs_total = env_offset + B if n_envs_total is None else n_envs_total
         self.max_steps = max_steps
+        dev = agent.device
+        # graph-replayable schedule values (train_torch.py:129-135): 1/T in double for the sampling
+        # kernel, (f32(1 - noise_weight), f32(noise_weight)) for the root expansion
+        self.inv_t_dev = torch.ones(1, dtype=torch.float64, device=dev)
+        self.root_w_dev = torch.zeros(2, dtype=torch.float32, device=dev)
+        self._temperature = None
+        self._noise_weight = None
+        self.temperature = temperature
         mcfg = cfg["model"]
         self.Lh = mcfg["state_history_length"]
         self.H, self.W = height, width
@@ -71,7 +87,10 @@ class ActingLoop:
         p = agent.packed
         self.cs = (2 * self.Lh + 63) // 64 * 64
         self.rep_in = torch.empty(B * height * width * self.cs, dtype=p.tdt, device=dev)
-        self.rep_runner = agent.runner(B, height, width)
+        self.rep_agent = agent if rep_agent is None else rep_agent
+        if self.rep_agent.packed.tdt != p.tdt or self.rep_agent.device != dev:
+            raise ValueError("rep_agent must share the search agent's device and dtype")
+        self.rep_runner = self.rep_agent.runner(B, height, width)
         self.action = torch.zeros(B, dtype=torch.int64, device=dev)
         T = max_steps
         self.rec = {
@@ -83,6 +102,11 @@ class ActingLoop:
             "values": torch.zeros(T, B, dtype=torch.float32, device=dev),
         }
         self.noise_log = None  # optional list: per-step Dirichlet noise used (parity tests)
+        # optional callable (search_id, B) -> f32 (B, 3): root Dirichlet noise injected in place of the
+        # device draw (replaying the reference's fixtures, whose noise came from their own generator);
+        # steps then run eagerly
+        self.inject_noise = None
+        self._noise_in = None
         self.search_id = 0
         self.step_index = 0
         self.episode = 0
@@ -90,6 +114,23 @@ class ActingLoop:
         # value is read from here, so one captured HIP graph replays every acting step
         self.ctx = torch.zeros(3, dtype=torch.int32, device=dev)
         self.graph = None
+
+    @property
+    def temperature(self):
+        return self._temperature
+
+    @temperature.setter
+    def temperature(self, t):
+        """train_torch.py:129-132; the captured step graph reads 1/T from inv_t_dev."""
+        if t != self._temperature:
+            self._temperature = t
+            self.inv_t_dev.fill_(1.0 / t)  # Python's `1/self.temperature` (double), train_torch.py:192
+
+    def _sync_noise_weight(self):
+        w = self.search.noise_weight  # train_torch.py:134-135 sets it on the search object
+        if w != self._noise_weight:
+            self._noise_weight = w
+            self.root_w_dev.copy_(torch.tensor([np.float32(1 - w), np.float32(w)], dtype=torch.float32))
 
     def reset(self, episode=None, params=None):
         """_acting_stage :166-167: env.reset + _pad_initial_state."""
@@ -108,16 +149,20 @@ class ActingLoop:
         # _prepare_mcts_input + create_hidden_state_root -> pool slot 0
         env.build_rep_input(self.rep_in, self.cs, self.agent.dtype == "bf16")
         self.rep_runner.representation(self.rep_in, ws.cur, pool=ws.pool, pool_env_stride=(ws.S + 1) * n)
-        values, counts = ws.run(self.search_id, None, ctx=self.ctx)
-        L.call("mzba_sample_actions", L.ptr(counts), L.ptr(self.action), self.B, float(self.temperature),
-               self.env_offset, self.step_index, self.seed, L.ptr(self.ctx), L.stream())
+        values, counts = ws.run(self.search_id, self._noise_in, ctx=self.ctx, w_dev=self.root_w_dev)
+        L.call("mzba_sample_actions", L.ptr(counts), L.ptr(self.action), None, self.B, 1.0 / self.temperature,
+               L.ptr(self.inv_t_dev), self.n_envs_total, self.VEC_BLOCK, self.env_offset, self.step_index, self.seed,
+               L.ptr(self.ctx), L.stream())
         L.call("mzba_record_results", L.ptr(counts), L.ptr(values), L.ptr(self.rec["counts"]),
                L.ptr(self.rec["values"]), self.B, 0, L.ptr(self.ctx), L.stream())
         env.step(self.action, False, self.rec, 0, ctx=self.ctx)
         L.call("mzba_ctx_advance", L.ptr(self.ctx), L.stream())
 
     def capture(self):
-        """Capture one acting step (~S x 65 launches) into a HIP graph; act() then replays it."""
+        """Capture one acting step (~S x 65 launches) into a HIP graph; act() then replays it.
+        Temperature and noise weight are read from device buffers, so the graph stays valid across
+        the reference's schedule."""
+        self._sync_noise_weight()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
@@ -128,6 +173,11 @@ class ActingLoop:
 
     def act(self, eager=False):
         """One acting step t (no host synchronisation)."""
+        self._sync_noise_weight()
+        if self.inject_noise is not None:
+            nz = np.ascontiguousarray(self.inject_noise(self.search_id, self.B), dtype=np.float32)
+            self._noise_in = torch.from_numpy(nz).to(self.agent.device)
+            eager = True
         if self.graph is not None and not eager and self.noise_log is None:
             self.graph.replay()
         else:
@@ -178,15 +228,17 @@ class ActingLoop:
 
 
 def run_test_simulation(cfg, agent, batch=2, seed=0, episode=0, max_steps_test=200, temperature=0.1,
-                        log_noise=False):
+                        log_noise=False, rep_agent=None):
     """RLSystem.run_test_simulation (train_torch.py:530-610) on the device: `batch` envs played
-    with the given agent at temperature 0.1 until all are done or after max_steps_test + 1 steps,
-    with the reference's quirks (padding action 1, every env recorded every step with env 0's
-    action). Returns (ObservationTrajectory per env, frames per env: the grayscale (1, H, W)
-    frames of the steps after which the env was still live — what the reference logs — and the
-    loop). The reference writes the frames of env 0 to tensorboard; logging is left to the caller."""
+    at temperature 0.1 until all are done or after max_steps_test + 1 steps, with the reference's
+    quirks (padding action 1, every env recorded every step with env 0's action). `agent` is the
+    search's net (self.latent_mcts holds the target net, train_torch.py:91) and `rep_agent` the
+    root representation's (self.mu_zero, the learner net, :567; default: `agent`). Returns
+    (ObservationTrajectory per env, frames per env: the grayscale (1, H, W) frames of the steps
+    after which the env was still live — what the reference logs — and the loop). The reference
+    writes the frames of env 0 to tensorboard; logging is left to the caller."""
     loop = ActingLoop(cfg, agent, batch, seed=seed, temperature=temperature, max_steps=max_steps_test + 1,
-                      pad_action=1, rec_flags=3)
+                      pad_action=1, rec_flags=3, rep_agent=rep_agent)
     loop.noise_log = [] if log_noise else None
     loop.reset(episode)
     H, W = loop.H, loop.W
@@ -224,14 +276,10 @@ class ActingStage:
 
     @temperature.setter
     def temperature(self, t):
-        if t != self.loop.temperature:
-            self.loop.graph = None  # the sampling kernel's 1/T is a launch argument
-        self.loop.temperature = t
+        self.loop.temperature = t  # a device value: the captured step graph stays valid
 
     def set_noise_weight(self, w):
-        if w != self.loop.search.noise_weight:
-            self.loop.graph = None
-        self.loop.search.noise_weight = w
+        self.loop.search.noise_weight = w  # copied to the device before the next step
 
     def run(self):
         out = []

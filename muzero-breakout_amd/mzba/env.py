@@ -39,7 +39,6 @@ class BreakoutEnvironment:
         self.seed = seed
         self.env_offset = env_offset
         self.episode = 0
-        self._err = torch.zeros(1, dtype=torch.int32, device=self.device)
 
     @property
     def action_space_size(self):
@@ -48,10 +47,6 @@ class BreakoutEnvironment:
     @property
     def state_shape(self):
         return (self.batch, 3, self.height, self.width)
-
-    def _rewards4(self):
-        return (ctypes.c_float * 4)(self.paddle_hit_reward, self.brick_hit_reward, self.game_lost_reward,
-                                    self.game_won_reward)
 
     def reset(self, params=None):
         """parallel_breakout.py:107-139. `params` (optional int32 (4,B): paddle offset,
@@ -63,8 +58,8 @@ class BreakoutEnvironment:
         pr = None
         if params is not None:
             pr = torch.as_tensor(np.asarray(params, dtype=np.int32), device=self.device).contiguous()
-        L.call("mzba_env_reset_planes", L.ptr(state), L.ptr(self.ball_dx), L.ptr(self.ball_dy), B, H, W,
-               self.paddle_width, self.brick_rows, self.seed, self.episode, self.env_offset, L.ptr(pr), L.stream())
+        L.ops().env_reset_(state, self.ball_dx, self.ball_dy, self.paddle_width, self.brick_rows, self.seed,
+                           self.episode, self.env_offset, pr)
         self.episode += 1
         return state, 0
 
@@ -76,24 +71,23 @@ class BreakoutEnvironment:
         return valid
 
     def step(self, state, action, done_mask):
-        B, H, W = self.batch, self.height, self.width
+        """parallel_breakout.py:158-254 through torch.ops.mz.env_step (done mutated in place and
+        returned, the reference's done_mask aliasing); CPU tensors are accepted like the reference's."""
+        B = self.batch
         out_dev = state.device
         s = state.to(self.device, torch.float32).contiguous()
         a = action.to(self.device, torch.int64).contiguous()
-        d = done_mask.to(self.device)
-        d8 = d.to(torch.uint8).contiguous()
+        on_dev = done_mask.device == self.device and done_mask.dtype == torch.bool and done_mask.is_contiguous()
+        d = done_mask if on_dev else done_mask.to(self.device, torch.bool).contiguous()
         dx = torch.as_tensor(self.ball_dx, device=self.device).to(torch.int64).expand(B).contiguous()
         dy = torch.as_tensor(self.ball_dy, device=self.device).to(torch.float32).expand(B).contiguous()
-        ns = torch.empty_like(s)
-        reward = torch.empty(B, dtype=torch.float32, device=self.device)
-        valid = torch.empty(B, 3, dtype=torch.float32, device=self.device)
-        self._err.zero_()
-        L.call("mzba_env_step_planes", L.ptr(s), L.ptr(ns), L.ptr(a), L.ptr(d8), L.ptr(dx), L.ptr(dy), L.ptr(reward),
-               L.ptr(valid), B, H, W, self.paddle_width, self._rewards4(), L.ptr(self._err), L.stream())
-        if int(self._err.item()) != 0:
-            raise IndexError("BreakoutEnvironment.step: every env must hold exactly one ball (parallel_breakout.py:189)")
+        r4 = [float(self.paddle_hit_reward), float(self.brick_hit_reward), float(self.game_lost_reward),
+              float(self.game_won_reward)]
+        # a malformed state raises IndexError (TORCH_CHECK_INDEX), the reference's error type
+        ns, reward, d, valid, dx, dy = L.ops().env_step(s, a, d, dx, dy, self.paddle_width, r4)
         self.ball_dx, self.ball_dy = dx, dy
-        done_mask.copy_(d8.to(torch.bool))  # in place, like `done_mask |= ...` (:204, :247)
+        if not on_dev:
+            done_mask.copy_(d)  # in place, like `done_mask |= ...` (:204, :247)
         return ns.to(out_dev), reward.to(out_dev), done_mask, valid.to(out_dev)
 
     def render(self, state):
@@ -102,10 +96,7 @@ class BreakoutEnvironment:
 
 def grayscale(state):
     """train_torch.py:334-358 on the device: (B,3,H,W) -> (B,1,H,W)."""
-    B, _, H, W = state.shape
-    g = torch.empty(B, 1, H, W, dtype=torch.float32, device=state.device)
-    L.call("mzba_grayscale_planes", L.ptr(state.contiguous()), L.ptr(g), B, H, W, L.stream())
-    return g
+    return L.ops().grayscale(state.contiguous())
 
 
 GRAY_LUT = None

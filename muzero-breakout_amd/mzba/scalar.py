@@ -51,10 +51,7 @@ class ScalarTransforms:
         """utils.py:74-81 on the HIP path: (..., n) f32 logits -> (...) decoded scalars."""
         L.require_gpu()
         x = logits.to("cuda", torch.float32).contiguous()
-        n = x.shape[-1]
-        out = torch.empty(x.shape[:-1], dtype=torch.float32, device="cuda")
-        L.call("mzba_support_decode", L.ptr(x), L.ptr(out), max(1, out.numel()), n, float(self.supports_min),
-               float(self.supports_max), L.stream())
+        out = L.ops().support_decode(x, float(self.supports_min), float(self.supports_max))
         return out.to(logits.device)
 
 

@@ -50,24 +50,23 @@ class TreeState:
                           L.ptr(r))
 
     def args(self, env_offset, search_id, seed, ctx=None):
-        """ctx: optional device int32[3] step context (its [0] overrides search_id; graph replay)."""
-        return (L.ptr(self.nodes), L.ptr(self.root_sum), L.ptr(self.calls), L.ptr(self.leaf_parent),
-                L.ptr(self.leaf_action), L.ptr(self.depth), L.ptr(self.path), L.ptr(self.sqrt_tab),
-                L.ptr(self.c_tab), self.B, self.S, env_offset, search_id, seed, L.ptr(ctx))
+        """Tree arguments of the torch.ops.mz tree ops (csrc/torch_ops.cpp). ctx: optional device
+        int32[3] step context (its [0] overrides search_id; graph replay)."""
+        return (self.nodes, self.root_sum, self.calls, self.leaf_parent, self.leaf_action, self.depth, self.path,
+                self.sqrt_tab, self.c_tab, self.S, env_offset, search_id, seed, ctx)
 
-    # individual kernels -----------------------------------------------------------------
-    def root(self, tree_args, v_root, pi_root, noise_in, w_pol, w_noise, alpha):
-        L.call("mzba_mcts_root", *tree_args, L.ptr(v_root), L.ptr(pi_root), L.ptr(noise_in), L.ptr(self.noise),
-               w_pol, w_noise, alpha, L.stream())
+    # individual kernels, dispatched as torch custom ops -----------------------------------------
+    def root(self, tree_args, v_root, pi_root, noise_in, w_pol, w_noise, alpha, w_dev=None):
+        L.ops().mcts_root_(*tree_args, v_root, pi_root, noise_in, self.noise, w_pol, w_noise, w_dev, alpha)
 
     def select(self, tree_args, sim):
-        L.call("mzba_mcts_select", *tree_args, sim, L.stream())
+        L.ops().mcts_select_(*tree_args, sim)
 
     def backup(self, tree_args, sim, r, v, pi, gamma):
-        L.call("mzba_mcts_backup", *tree_args, sim, L.ptr(r), L.ptr(v), L.ptr(pi), gamma, L.stream())
+        L.ops().mcts_backup_(*tree_args, sim, r, v, pi, gamma)
 
     def results(self, tree_args):
-        L.call("mzba_mcts_results", *tree_args, L.ptr(self.counts), L.ptr(self.values), L.stream())
+        L.ops().mcts_results_(*tree_args, self.values, self.counts)
 
 
 class MCTSSearchVec:
@@ -146,9 +145,10 @@ class SearchWorkspace:
     def root_slot(self):
         return self.pool.view(self.B, self.S + 1, self.n)[:, 0]
 
-    def run(self, search_id, noise=None, ctx=None):
+    def run(self, search_id, noise=None, ctx=None, w_dev=None):
         """mcts.py:24-71 on the device. Root latent must be in pool slot 0. With `ctx` the
-        search id is read on the device (HIP-graph replayable launch sequence)."""
+        search id is read on the device (HIP-graph replayable launch sequence); `w_dev` (device
+        f32[2]) supplies the root mixing weights (f32(1 - noise_weight), f32(noise_weight))."""
         s = self.s
         B, S, n = self.B, self.S, self.n
         ta = self.tree.args(s.env_offset, search_id, s.seed, ctx)
@@ -158,7 +158,7 @@ class SearchWorkspace:
         rn.prediction(self.cur, self.pi, self.v)  # _expand_root_nodes mcts.py:95-100
         w_pol = float(np.float32(1 - s.noise_weight))
         w_noise = float(np.float32(s.noise_weight))
-        self.tree.root(ta, self.v, self.pi, noise, w_pol, w_noise, s.dirchlet_alpha)
+        self.tree.root(ta, self.v, self.pi, noise, w_pol, w_noise, s.dirchlet_alpha, w_dev)
         gamma = float(np.float32(s.discount))
         env_stride = (S + 1) * n
         fused = rn.fused_ok() and self.use_tree_fusion

@@ -1,18 +1,30 @@
-"""Env sharding across ranks + the one exchange step: trajectory records -> rank 0.
+"""Env sharding across ranks: the trajectory sink (records -> rank 0) and the target-net
+refresh (rank 0's weights -> every rank).
 
 Envs are independent during acting (BN in eval mode, per-env min-max scaling, no
 cross-env term in step or search — SURVEY §8(e)), so rank r simply owns global envs
 [r*B, (r+1)*B) and every random draw is keyed by the GLOBAL env id: results are
-identical for any world size. The only collective is the reference's sink: each
-rank's per-step ObservationTrajectory rows (replay_buffer.py:17-35) are packed into
-one byte slab per k steps and all-gathered (RCCL over xGMI with backend "nccl"; gloo
-in the CPU tests) into rank 0, which copies them to pinned host memory.
+identical for any world size. Two collectives, both where the reference has a real
+exchange:
+  * the sink — each rank's per-step ObservationTrajectory rows (replay_buffer.py:17-35)
+    are packed into one byte slab per k steps and GATHERED to rank 0 (RCCL over xGMI
+    with backend "nccl"; gloo in the CPU tests): only rank 0 consumes records (its host
+    replay buffer), so a gather moves 1/N of an all-gather's bytes; rank 0 copies them
+    to pinned host memory behind an event;
+  * the target-net refresh (train_torch.py:137-139, load_latest_weights :361-367) — rank 0
+    holds the learner's state_dict, one flat f32 broadcast (+ one int64 broadcast for the
+    BN batch counters) hands it to every acting rank, which re-packs its agent.
 
 Record layout per (step, env), little-endian, REC_BYTES = 28 + HW:
   action u8 | mask u8 | pad u16 | reward f32 | value f32 | counts i32[3] | pad u32 | frame u8[HW]
 """
+from collections import OrderedDict
+
+import numpy as np
 import torch
 import torch.distributed as dist
+
+from .weights import state_dict_spec
 
 HDR = 28
 
@@ -54,33 +66,78 @@ def unpack_records(buf):
 
 
 class TrajectoryGather:
-    """All-gather of packed record slabs into rank 0's host buffer (pinned)."""
+    """Gather of packed record slabs to rank 0, then into its pinned host buffer."""
 
     def __init__(self, world_size, rank, k_steps, B, hw, device, pin=True):
         self.ws, self.rank, self.k, self.B, self.hw = world_size, rank, k_steps, B, hw
         self.device = torch.device(device)
         self.slab = torch.zeros(k_steps, B, rec_bytes(hw), dtype=torch.uint8, device=self.device)
-        self.gathered = torch.zeros(world_size, k_steps, B, rec_bytes(hw), dtype=torch.uint8, device=self.device)
-        self.host = None
+        self.gathered = self.host = self.copied = None
         if rank == 0:
+            self.gathered = torch.zeros(world_size, k_steps, B, rec_bytes(hw), dtype=torch.uint8, device=self.device)
             self.host = torch.zeros(world_size, k_steps, B, rec_bytes(hw), dtype=torch.uint8,
                                     pin_memory=pin and self.device.type == "cuda")
 
     def exchange(self, rec, t0, t1):
+        """Records of steps [t0, t1) (t1 - t0 <= k) of every rank -> rank 0. Every rank calls it."""
         n = t1 - t0
         pack_records(rec, t0, t1, self.slab[:n])
         if self.ws > 1:
-            if dist.get_backend() == "nccl":  # RCCL over xGMI: one flat all-gather
-                dist.all_gather_into_tensor(self.gathered.view(-1), self.slab.view(-1))
-            else:  # gloo (CPU tests)
-                dist.all_gather(list(self.gathered.unbind(0)), self.slab)
-        else:
+            gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
+            dist.gather(self.slab, gl, dst=0)
+        elif self.rank == 0:
             self.gathered[0].copy_(self.slab)
         if self.rank == 0:
             self.host.copy_(self.gathered, non_blocking=True)
+            if self.device.type == "cuda":  # host_records() waits for exactly this copy
+                self.copied = torch.cuda.Event()
+                self.copied.record()
         return n
 
     def host_records(self, n):
         """rank 0: dict of (n, world*B, ...) in global env order."""
+        if self.copied is not None:
+            self.copied.synchronize()
         h = self.host[:, :n].permute(1, 0, 2, 3).reshape(n, self.ws * self.B, -1)
         return unpack_records(h)
+
+
+def broadcast_state_dict(mcfg, state_dict, device, src=0):
+    """Target-net refresh across ranks (train_torch.py:137-139, :361-367): `src` passes the learner's
+    reference-format state_dict (tensors or arrays), the other ranks pass None; every rank returns
+    the same OrderedDict of CPU tensors in networks.py key order. Two collectives: the float
+    entries flattened into one f32 buffer, the BN `num_batches_tracked` counters into one int64."""
+    rank = dist.get_rank()
+    spec = state_dict_spec(mcfg)
+    fkeys = [(k, s) for k, s in spec if not k.endswith("num_batches_tracked")]
+    ikeys = [k for k, _ in spec if k.endswith("num_batches_tracked")]
+    nf = sum(int(np.prod(s)) for _, s in fkeys)
+    dev = torch.device(device)
+    fbuf = torch.empty(nf, dtype=torch.float32, device=dev)
+    ibuf = torch.zeros(max(len(ikeys), 1), dtype=torch.int64, device=dev)
+    if rank == src:
+        if state_dict is None:
+            raise ValueError("broadcast_state_dict: the source rank must pass the state_dict")
+        fbuf.copy_(torch.cat([torch.as_tensor(np.asarray(state_dict[k]), dtype=torch.float32).reshape(-1)
+                              for k, _ in fkeys]))
+        if ikeys:
+            ibuf.copy_(torch.tensor([int(np.asarray(state_dict[k])) for k in ikeys], dtype=torch.int64))
+    dist.broadcast(fbuf, src)
+    dist.broadcast(ibuf, src)
+    fh, ih = fbuf.cpu(), ibuf.cpu()
+    out, o = OrderedDict(), 0
+    for k, s in spec:
+        if k.endswith("num_batches_tracked"):
+            out[k] = ih[ikeys.index(k)].clone()
+        else:
+            n = int(np.prod(s))
+            out[k] = fh[o:o + n].view(s).clone()
+            o += n
+    return out
+
+
+def refresh_target(agent, mcfg, state_dict, device, src=0):
+    """The acting ranks' target net <- rank src's learner weights (load_latest_weights)."""
+    sd = broadcast_state_dict(mcfg, state_dict, device, src)
+    agent.load_state_dict({k: v.numpy() for k, v in sd.items()})
+    return sd

@@ -18,13 +18,22 @@ from . import nets as N
 f32 = np.float32
 
 
-def sample_actions(counts, temperature, u):
-    """train_torch.py:192-198 with inverse-CDF sampling on injected u (f32)."""
-    c = counts.astype(np.float32)
-    inv = f32(1.0 / temperature)
-    vt = c if inv == f32(1.0) else np.power(c, inv).astype(np.float32)
+def sample_probs(counts, temperature, vec_block=None, env_offset=0, n_envs_total=None):
+    """train_torch.py:192-193 bit for bit: `visit_counts ** (1/self.temperature)` on the whole (B, 3)
+    int64 batch tensor (torch's CPU pow, restated in oracle/torch_pow.c: the element's position in the
+    tensor decides between SLEEF's vector powf and the scalar double pow), then the f32 row sum
+    ((c0 + c1) + c2, torch's order for a size-3 dim) and the f32 division."""
+    from .torch_pow import pow_counts, VEC_BLOCK
+    vt = pow_counts(counts, 1.0 / temperature, VEC_BLOCK if vec_block is None else vec_block, env_offset,
+                    n_envs_total)
     s = (vt[:, 0] + vt[:, 1]) + vt[:, 2]
-    probs = (vt / s[:, None]).astype(np.float32)
+    return (vt / s[:, None]).astype(np.float32)
+
+
+def sample_actions(counts, temperature, u, vec_block=None, env_offset=0, n_envs_total=None):
+    """train_torch.py:192-198 with inverse-CDF sampling on injected u (f32) in place of
+    `Categorical(probs[i]).sample()`. A shard passes its env_offset and the global env count."""
+    probs = sample_probs(counts, temperature, vec_block, env_offset, n_envs_total)
     B = counts.shape[0]
     out = np.zeros(B, dtype=np.int64)
     for b in range(B):
@@ -75,8 +84,9 @@ def prepare_mcts_input(cur_gray, traj, L, n_actions=3):
 
 
 def run_episode(cfg, sd, seed, episode, noise_fn, n_parallel, max_steps=261, temperature=1.0,
-                search_id0=0, step0=0, height=None, width=None, env_offset=0, on_step=None):
-    """One `_acting_stage` episode (train_torch.py:164-233) for `n_parallel` envs.
+                search_id0=0, step0=0, height=None, width=None, env_offset=0, on_step=None, n_envs_total=None):
+    """One `_acting_stage` episode (train_torch.py:164-233) for `n_parallel` envs (a shard of
+    `n_envs_total` starting at global env `env_offset`; default: the whole batch).
 
     Returns (trajectories, per-step log dict)."""
     mcfg = cfg["model"]
@@ -104,7 +114,7 @@ def run_episode(cfg, sd, seed, episode, noise_fn, n_parallel, max_steps=261, tem
         noise = noise_fn(sid, n_parallel)
         values, counts = search.search(h, noise, sid, env_offset)
         u = R.uniform(np.arange(n_parallel) + env_offset, R.STREAM_SAMPLE, step0 + t, 0, seed)
-        action = sample_actions(counts, temperature, u)
+        action = sample_actions(counts, temperature, u, env_offset=env_offset, n_envs_total=n_envs_total)
         state, reward, done, valid = env.step(state, action, done)
         warp = convert_to_grayscale(state)
         rec = ~prev_done
@@ -121,10 +131,13 @@ def run_episode(cfg, sd, seed, episode, noise_fn, n_parallel, max_steps=261, tem
 
 
 def run_test_simulation(cfg, sd, seed, episode, noise_fn, batch=2, max_steps_test=200, temperature=0.1,
-                        search_id0=0, step0=0):
+                        search_id0=0, step0=0, sd_rep=None):
     """RLSystem.run_test_simulation (train_torch.py:530-610) with injected randomness: padding
     action 1 (:545), temperature 0.1 sampling (:571-579), frames kept while the env is live
-    (:583-585), and every env's trajectory extended every step with env 0's action (:594-598)."""
+    (:583-585), and every env's trajectory extended every step with env 0's action (:594-598).
+    The root latent comes from the learner net `sd_rep` (self.mu_zero, :567) and the search runs
+    the target net `sd` (self.latent_mcts holds mu_zero_target, :91); sd_rep=None: the same net."""
+    sd_rep = sd if sd_rep is None else sd_rep
     mcfg = cfg["model"]
     L = mcfg["state_history_length"]
     env = BreakoutEnvOracle({**cfg["environment"], "n_parallel": batch})
@@ -139,7 +152,7 @@ def run_test_simulation(cfg, sd, seed, episode, noise_fn, batch=2, max_steps_tes
         if step_i > max_steps_test:
             break
         x = np.stack([prepare_mcts_input(warp[b], trajs[b], L) for b in range(batch)])
-        h = N.create_hidden_state_root(x, sd, mcfg)
+        h = N.create_hidden_state_root(x, sd_rep, mcfg)
         sid = search_id0 + step_i
         values, counts = search.search(h, noise_fn(sid, batch), sid, 0)
         u = R.uniform(np.arange(batch), R.STREAM_SAMPLE, step0 + step_i, 0, seed)

@@ -203,6 +203,7 @@ def small_model_cfg(cfg):
 
 
 def load_agent(mcfg, seed):
+    reference_modules()
     from src.networks import MuZeroAgent
     agent = MuZeroAgent(mcfg)
     sd = init_state_dict(mcfg, seed)
@@ -248,6 +249,7 @@ class SearchInjector:
     and records decoded outputs in call order."""
 
     def __init__(self, seed):
+        reference_modules()
         import src.mcts as mm
         self.mm, self.seed = mm, seed
         self.search_id = -1
@@ -350,11 +352,11 @@ def make_mcts(cfg):
 
 
 # --------------------------------------------------------------------------------------
-def make_acting(cfg):
+def make_acting(cfg, B=4, temperature=1.0, name="acting_small_b4"):
     """One reference `_acting_stage` episode (B=4, small nets) with injected RNG."""
+    reference_modules()
     import train_torch as tt
     mcfg = small_model_cfg(cfg)
-    B = 4
     c = {**cfg, "n_parallel": B, "model": mcfg, "num_episodes": 1,
          "environment": {**cfg["environment"], "n_parallel": B}}
     inj_reset = ResetInjector(SEED)
@@ -390,6 +392,7 @@ def make_acting(cfg):
     sys_.mu_zero_target.load_state_dict(sd_t)
     sys_.mu_zero.load_state_dict(sd_t)
     sys_.mu_zero_target.eval_mode()
+    sys_.temperature = temperature
     state, _ = sys_.environment.reset()
     sys_._pad_initial_state(sys_.convert_to_grayscale(state))
     sys_._run_episode(state)
@@ -409,11 +412,183 @@ def make_acting(cfg):
         rews[b, :n] = [float(r) for r in t.rewards[L:]]
         cnts[b, :n] = np.stack([v.numpy() for v in t.visit_counts[L:]])
         vals[b, :n] = [float(v) for v in t.values[L:]]
-    np.savez_compressed(os.path.join(HERE, "acting_small_b4.npz"), seed=SEED, B=B, lengths=np.array(lens),
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), seed=SEED, B=B, lengths=np.array(lens), temperature=temperature,
                         actions=acts, frames=frames, rewards=rews, counts=cnts, values=vals,
                         n_searches=sinj.search_id + 1,
                         noise=np.stack([dirichlet_noise(i, B) for i in range(sinj.search_id + 1)]))
     print("acting", "lengths", lens, "reward sums", [float(t.reward_sum) for t in trajs])
+
+
+def reference_modules():
+    """The build ships regular packages `src`, `environment`, `utils`, `replay_buffer`
+    (muzero-breakout_amd/) that would shadow the reference's modules of the same names: import the
+    reference's with the build off the path (idempotent)."""
+    if getattr(reference_modules, "_done", False):
+        return
+    saved = sys.path[:]
+    sys.path = [q for q in sys.path if not q.rstrip("/").endswith("muzero-breakout_amd")]
+    names = ("src", "utils", "train_torch", "environment", "replay_buffer")
+    for m in [m for m in sys.modules if m in names or any(m.startswith(n + ".") for n in names)]:
+        del sys.modules[m]
+    import train_torch  # noqa: F401
+    import src.mcts  # noqa: F401
+    import environment.parallel_breakout  # noqa: F401
+    sys.path = saved
+    reference_modules._done = True
+
+
+def temperature_schedule(iterations=700):
+    """RLSystem.train (train_torch.py:129-132): once training_iteration > 10 every iteration does
+    `self.temperature *= 0.996; self.temperature = max(self.temperature, 0.1)` (Python floats).
+    Entry k = the temperature after k decays."""
+    t, out = 1.0, [1.0]
+    for _ in range(iterations):
+        t *= 0.996
+        t = max(t, 0.1)
+        out.append(t)
+    return out
+
+
+def make_sampling(cfg):
+    """The reference's temperature step (train_torch.py:192-193 `visit_counts ** (1/self.temperature)`,
+    `/ visit_counts_temp.sum(dim=1, keepdim=True)`) evaluated by torch on this CPU on whole int64
+    (B, 3) batch tensors, for temperatures of the reference's own schedule, plus the injected inverse-CDF
+    choice the acting fixtures use. Batch sizes cover every lane class of torch's CPU pow: B = 4096
+    (3B % 32 == 0: all SLEEF vector lanes), 1029 (15 scalar tail lanes), 12 (4 tail), 2 (all tail)."""
+    sched = temperature_schedule()
+    ks = [0, 1, 2, 3, 10, 37, 100, 150, 250, 400, 500, 573, 574, 575, 700]
+    temps = [sched[k] for k in ks] + [0.5, 0.25, 2.0 / 3.0]
+    g = np.random.Generator(np.random.PCG64(SEED + 11))
+    out = dict(seed=SEED, temps=np.array(temps, np.float64), sched_k=np.array(ks + [-1, -1, -1]),
+               vec_block=32, cpu_capability=torch.backends.cpu.get_cpu_capability())
+    for name, B, S in (("b4096", 4096, 50), ("b1029", 1029, 200), ("b12", 12, 50), ("b2", 2, 50)):
+        p = g.dirichlet([0.3, 0.3, 0.3], B)
+        counts = np.stack([g.multinomial(S, p[b]) for b in range(B)]).astype(np.int64)
+        counts[: min(B, 8)] = np.array([[S, 0, 0], [0, S, 0], [0, 0, S], [S - 1, 1, 0], [1, 0, S - 1],
+                                        [S // 3, S // 3, S - 2 * (S // 3)], [0, S // 2, S - S // 2],
+                                        [S - 2, 1, 1]])[: min(B, 8)]
+        out[f"{name}/counts"] = counts
+        vc = torch.from_numpy(counts)
+        for i, T in enumerate(temps):
+            vt = vc ** (1 / T)                                   # train_torch.py:192
+            probs = vt / vt.sum(dim=1, keepdim=True)              # train_torch.py:193
+            u = R.uniform(np.arange(B), R.STREAM_SAMPLE, i, 0, SEED)
+            pr = probs.numpy().astype(np.float32)
+            act = np.zeros(B, np.int64)
+            for b in range(B):  # the acting fixtures' injected Categorical.sample (inverse CDF)
+                cdf, chosen, last = np.float32(0), -1, 0
+                for a in range(3):
+                    if pr[b, a] > 0:
+                        last = a
+                    cdf = np.float32(cdf + pr[b, a])
+                    if chosen < 0 and u[b] < cdf:
+                        chosen = a
+                act[b] = chosen if chosen >= 0 else last
+            out[f"{name}/t{i}/pow"] = vt.numpy()
+            out[f"{name}/t{i}/probs"] = pr
+            out[f"{name}/t{i}/action"] = act
+    # the pow alone over every count 0..1023 and every schedule exponent (4096-element tensors: all
+    # vector lanes; and the same values as 31-element tensors: all scalar lanes), as checksums
+    base = torch.arange(1024, dtype=torch.int64)
+    uniq = sorted(set(sched))
+    ex_vec, ex_sc = [], []
+    for T in uniq:
+        v = (base.repeat(4) ** (1 / T))[:1024].numpy()
+        s = torch.cat([(base[i:i + 31] ** (1 / T)) for i in range(0, 1024, 31)]).numpy()
+        ex_vec.append(v.view(np.uint32).astype(np.uint64).sum())
+        ex_sc.append(s.view(np.uint32).astype(np.uint64).sum())
+    out["sched_temps"] = np.array(uniq, np.float64)
+    out["sched_pow_vec_u32sum"] = np.array(ex_vec, np.uint64)
+    out["sched_pow_scalar_u32sum"] = np.array(ex_sc, np.uint64)
+    np.savez_compressed(os.path.join(HERE, "sampling.npz"), **out)
+    print("sampling", len(temps), "temperatures;", torch.backends.cpu.get_cpu_capability())
+
+
+def make_acting_temperature(cfg):
+    """One reference `_run_episode` (B = 12, small nets) at a decayed temperature of the reference's
+    schedule (150 decays, T ~ 0.548): 3B = 36 elements -> 32 SLEEF vector lanes + 4 scalar lanes."""
+    make_acting(cfg, B=12, temperature=temperature_schedule()[150], name="acting_small_b12_t150")
+
+
+def make_test_sim(cfg):
+    """RLSystem.run_test_simulation(batch=2) (train_torch.py:530-610) with injected RNG, small nets,
+    a learner net (representation) different from the target net (search), n_parallel = batch = 2
+    (the reference resets the whole env batch, :541, and steps it with `batch` actions, :581: only
+    n_parallel == batch runs). Records every ObservationTrajectory it builds, the frames it logs
+    (env 0, :603-605), and its per-step visit counts and actions."""
+    reference_modules()
+    import train_torch as tt
+    mcfg = small_model_cfg(cfg)
+    B = 2
+    c = {**cfg, "n_parallel": B, "model": mcfg, "environment": {**cfg["environment"], "n_parallel": B}}
+    inj_reset = ResetInjector(SEED + 3)
+    Env = patched_env_class(inj_reset)
+    sinj = SearchInjector(SEED + 3)
+    sinj.noise = dirichlet_noise
+    ncat = [0]
+    probs_log = []
+
+    class InjCategorical:
+        def __init__(self, probs):
+            self.p = probs.detach().numpy().astype(np.float32)
+            probs_log.append(self.p.copy())
+
+        def sample(self):
+            k = ncat[0]
+            ncat[0] += 1
+            env, step = k % B, k // B
+            u = R.uniform(np.array([env]), R.STREAM_SAMPLE, step, 0, SEED + 3)[0]
+            cdf, chosen, last = np.float32(0), -1, 0
+            for a in range(3):
+                if self.p[a] > 0:
+                    last = a
+                cdf = np.float32(cdf + self.p[a])
+                if chosen < 0 and u < cdf:
+                    chosen = a
+            return torch.tensor(chosen if chosen >= 0 else last)
+
+    trajs = []
+
+    class RecTraj(tt.ObservationTrajectory):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            trajs.append(self)
+
+    images = []
+
+    class Writer:
+        def add_image(self, tag, frame, global_step=None, dataformats=None):
+            images.append(np.asarray(frame).copy())
+
+        def __getattr__(self, name):
+            return lambda *a, **k: None
+
+    tt.torch = Proxy(torch, distributions=Proxy(torch.distributions, Categorical=InjCategorical))
+    tt.ObservationTrajectory = RecTraj
+    tt.get_class = lambda mod, name: {"MCTSSearchVec": sinj.Search, "BreakoutEnvironment": Env}.get(
+        name, getattr(__import__(mod, fromlist=[name]), name))
+    sys_ = tt.RLSystem(c)
+    sys_.filewriter = Writer()
+    sd_t = {k: torch.from_numpy(np.asarray(v)) for k, v in init_state_dict(mcfg, SEED + 4).items()}
+    sd_l = {k: torch.from_numpy(np.asarray(v)) for k, v in init_state_dict(mcfg, SEED + 5).items()}
+    sys_.mu_zero_target.load_state_dict(sd_t)
+    sys_.mu_zero.load_state_dict(sd_l)
+    sys_.mu_zero_target.eval_mode()
+    sys_.run_test_simulation(B)
+    L = mcfg["state_history_length"]
+    n = trajs[0].length
+    assert all(t.length == n for t in trajs)
+    out = dict(seed=SEED + 3, B=B, target_seed=SEED + 4, learner_seed=SEED + 5, n_steps=n,
+               actions=np.array([[int(a) for a in t.actions] for t in trajs]),
+               rewards=np.array([[float(r) for r in t.rewards[L:]] for t in trajs], np.float32),
+               counts=np.stack([np.stack([np.asarray(v) for v in t.visit_counts[L:]]) for t in trajs]).astype(np.int64),
+               values=np.array([[float(v) for v in t.values[L:]] for t in trajs], np.float32),
+               states=np.stack([np.stack([np.asarray(s).reshape(16, 20) for s in t.states[L - 1:]]) for t in trajs]),
+               env0_frames=np.stack(images).reshape(len(images), 16, 20) if images else np.zeros((0, 16, 20), np.float32),
+               probs=np.stack(probs_log).reshape(-1, B, 3),
+               noise=np.stack([dirichlet_noise(i, B) for i in range(sinj.search_id + 1)]))
+    np.savez_compressed(os.path.join(HERE, "test_sim_b2.npz"), **out)
+    print("test_sim steps", n, "env0 frames", len(images), "reward sums", [float(t.reward_sum) for t in trajs])
 
 
 def make_replay(cfg):
@@ -517,16 +692,9 @@ def make_learner(cfg):
     from init_state_dict weights: a narrow config stored in full (logits, losses, every
     gradient, parameters and BN running stats after each step) and the full config at B = 4
     stored as per-tensor checksums plus sampled entries."""
-    # the build ships a regular package `src` (muzero-breakout_amd/src) that would shadow the
-    # reference's namespace package: import the reference modules with the build off the path
-    saved = sys.path[:]
-    sys.path = [q for q in sys.path if not q.rstrip("/").endswith("muzero-breakout_amd")]
-    for m in [m for m in sys.modules if m in ("src", "utils", "train_torch") or m.startswith("src.")]:
-        del sys.modules[m]
+    reference_modules()
     from utils import ScalarTransforms
     from src.networks import MuZeroAgent
-    import train_torch  # noqa: F401
-    sys.path = saved
     K = cfg["num_unroll_steps"]
     for tag, mcfg, B, full in (("small", learner_model_cfg(cfg), 8, True),
                                ("full", {**cfg["model"], "device": "cpu"}, 4, False)):
@@ -593,7 +761,8 @@ def make_learner(cfg):
 
 if __name__ == "__main__":
     cfg = ref_harness.load_config()
-    which = sys.argv[1:] or ["env", "fuzz", "nets", "mcts", "acting", "replay", "learner"]
+    which = sys.argv[1:] or ["env", "fuzz", "nets", "mcts", "acting", "replay", "learner", "sampling", "acting_t",
+                             "test_sim"]
     if "env" in which:
         make_env(cfg)
     if "fuzz" in which:
@@ -608,3 +777,9 @@ if __name__ == "__main__":
         make_replay(cfg)
     if "learner" in which:
         make_learner(cfg)
+    if "sampling" in which:
+        make_sampling(cfg)
+    if "acting_t" in which:
+        make_acting_temperature(cfg)
+    if "test_sim" in which:
+        make_test_sim(cfg)

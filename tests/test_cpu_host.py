@@ -78,3 +78,15 @@ def test_ucb_tables_double_precision():
         assert sq[n].item() == float(np.float32(math.sqrt(n)))
         assert ct[n].item() == float(np.float32(1.25 + math.log((n + 19652.0 + 1) / 19652.0)))
     del torch
+
+
+def test_torch_custom_ops_registered():
+    """libmzba_torch.so registers TORCH_LIBRARY(mz) with the drop-in surface of SURVEY §8(b);
+    env_step declares the reference's done_mask aliasing (Tensor(a!) done -> Tensor(a!))."""
+    from mzba import _lib
+    ops = _lib.ops()
+    for name in _lib.TORCH_OPS:
+        assert hasattr(ops, name), name
+    sch = str(ops.env_step.default._schema)
+    assert "Tensor(a!) done" in sch and "Tensor(a!) done_out" in sch, sch
+    assert "Tensor(h!) values" in str(ops.mcts_results_.default._schema)

@@ -1,15 +1,16 @@
-"""CPU, world_size 2 over gloo: the trajectory exchange step (mzba/shard.py) gathers every
-rank's packed records into rank 0 in global env order, and the record packing round-trips."""
+"""CPU, world_size 2 over gloo: the two collectives of mzba/shard.py as bench.py runs them for
+N > 1 — the target-net refresh (rank 0's state_dict broadcast to every rank, train_torch.py:137-139)
+and the trajectory sink (every rank's packed records gathered to rank 0 in global env order) — and
+the record packing round trip."""
 import os
 import socket
 
 import numpy as np
-import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from mzba.shard import TrajectoryGather, pack_records, unpack_records
+from mzba.shard import TrajectoryGather, broadcast_state_dict, pack_records, unpack_records
 
 
 def _rec(T, B, hw, rank):
@@ -24,6 +25,11 @@ def _rec(T, B, hw, rank):
     }
 
 
+def _mcfg():
+    from mzba.config import default_config, small_model_cfg
+    return small_model_cfg(default_config())
+
+
 def test_pack_roundtrip():
     r = _rec(5, 7, 320, 0)
     u = unpack_records(pack_records(r, 1, 4))
@@ -34,18 +40,28 @@ def test_pack_roundtrip():
 def _worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mzba.weights import init_state_dict
+    # target-net refresh: only rank 0 holds the learner's weights
+    sd = init_state_dict(_mcfg(), 3) if rank == 0 else None
+    if rank == 0:
+        sd["dyn_net.conv_block.bn.num_batches_tracked"] = np.array(17, np.int64)
+    got_sd = broadcast_state_dict(_mcfg(), sd, "cpu")
     T, B, hw = 6, 5, 320
     rec = _rec(T, B, hw, rank)
     g = TrajectoryGather(world, rank, 4, B, hw, "cpu", pin=False)
     n = g.exchange(rec, 2, 6)
+    res = {"sd": {k: v.numpy() for k, v in got_sd.items()}}
     if rank == 0:
-        got = g.host_records(n)
-        out.put({k: v.numpy() for k, v in got.items()})
+        assert g.gathered is not None and g.host is not None
+        res["rec"] = {k: v.numpy() for k, v in g.host_records(n).items()}
+    else:
+        assert g.gathered is None and g.host is None  # gather to the root: nothing lands here
+    out.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gather_world2_global_env_order():
+def test_broadcast_and_gather_world2():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -54,14 +70,21 @@ def test_gather_world2_global_env_order():
     ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    got = q.get(timeout=120)
+    got = dict(q.get(timeout=180) for _ in range(2))
     for p in ps:
         p.join(timeout=120)
         assert p.exitcode == 0
+    from mzba.weights import init_state_dict
+    want_sd = init_state_dict(_mcfg(), 3)
+    want_sd["dyn_net.conv_block.bn.num_batches_tracked"] = np.array(17, np.int64)
+    for r in range(2):
+        assert list(got[r]["sd"]) == list(want_sd)
+        for k, v in want_sd.items():
+            np.testing.assert_array_equal(got[r]["sd"][k], v, err_msg=f"rank {r} {k}")
     ref = [_rec(6, 5, 320, r) for r in range(2)]
     for k in ("action", "mask", "reward", "values", "counts", "frame"):
         want = np.concatenate([ref[r][k][2:6].numpy() for r in range(2)], axis=1)
-        np.testing.assert_array_equal(got[k], want, err_msg=k)
+        np.testing.assert_array_equal(got[0]["rec"][k], want, err_msg=k)
 
 
 def test_rng_keyed_on_global_env():
@@ -74,3 +97,14 @@ def test_rng_keyed_on_global_env():
         part = BreakoutEnvOracle({**cfg, "n_parallel": 8}).reset_params(5, 3, env_offset=8 * r)
         for a, b in zip(part, full):
             np.testing.assert_array_equal(a, b[8 * r: 8 * r + 8])
+
+
+def test_sharded_sampling_oracle_equals_global():
+    """The temperature step on a shard (its env_offset in the global (n, 3) batch tensor) equals the
+    global step's rows: which torch pow lane an element takes depends on its global position."""
+    from oracle.acting import sample_probs
+    c = np.random.default_rng(0).integers(0, 51, (1029, 3))
+    full = sample_probs(c, 0.7)
+    for off, n in ((0, 515), (515, 514)):
+        np.testing.assert_array_equal(sample_probs(c[off:off + n], 0.7, env_offset=off, n_envs_total=1029)
+                                      .view(np.uint32), full[off:off + n].view(np.uint32))

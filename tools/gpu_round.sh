@@ -1,37 +1,31 @@
 #!/bin/bash
-# One gpurun call: GPU parity tests, bench, kernel-trace stats, PMC passes on the dominant kernel.
-# usage (from the repo root on the box): bash tools/gpu_round.sh TAG
-set -e
+# One gpurun call: GPU parity tests, smoke, the headline bench (north_star 4096 x 50) and config 2
+# (1024 x 50), kernel-trace stats, and PMC passes (FETCH_SIZE / WRITE_SIZE, separate runs) on the
+# dominant kernel inside the bench. Any failing or timed-out step ends the script (set -e).
+# usage (from the repo root on the box): bash tools/gpu_round.sh TAG [skip-tests]
+set -euo pipefail
 TAG=${1:-run}
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 && echo "pytest ok"
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo "smoke ok"
-tail -2 $O/pytest.log
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err && echo "bench ok"
+if [ "${2:-}" != "skip-tests" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+  tail -2 $O/pytest.log
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+  tail -1 $O/smoke.log
+fi
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 cat $O/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu > $O/prof.log 2>&1 && echo "prof ok"
-python3 tools/rocpd_report.py stats $O/prof $O/kernel_stats.csv
-timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 tools/pmc_conv.py 1024 tower 14 > $O/pmc_f.log 2>&1 && echo "pmc fetch ok"
-timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 tools/pmc_conv.py 1024 tower 14 > $O/pmc_w.log 2>&1 && echo "pmc write ok"
-python3 tools/pmc_summarize.py $O/pmc_fetch $O/pmc_write 1024 $O/tower_hbm_traffic.json tower 14
-rm -rf $O/pmc_fetch $O/pmc_write
-# HBM traffic of the env render kernel (config 3 geometry)
-timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/env_fetch -o run -- python3 bench.py --workload env --envs 4096 --height 84 --width 84 --hist 4 --steps 30 --warmup 5 --no-cpu > $O/env_f.log 2>&1 && echo "env fetch ok"
-timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/env_write -o run -- python3 bench.py --workload env --envs 4096 --height 84 --width 84 --hist 4 --steps 30 --warmup 5 --no-cpu > $O/env_w.log 2>&1 && echo "env write ok"
-python3 - "$O" <<'PY'
-import sys, json, statistics
-sys.path.insert(0, "tools")
-from rocpd_report import counter_values
-o = sys.argv[1]
-f = counter_values(o + "/env_fetch", "FETCH_SIZE", "env_step_compact_kernel")
-w = counter_values(o + "/env_write", "WRITE_SIZE", "env_step_compact_kernel")
-res = {"kernel": "env_step_compact_kernel", "envs": 4096, "H": 84, "W": 84,
-       "fetch_bytes": statistics.median(f[10:]) * 1024 * 2 if f else None,
-       "write_bytes": statistics.median(w[10:]) * 1024 if w else None, "algorithmic_bytes": 4096 * 7104,
-       "n_samples": [len(f), len(w)], "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, median of launches 11..35, FETCH x2"}
-json.dump(res, open(o + "/env_hbm_traffic.json", "w"), indent=1)
-print(json.dumps(res))
-PY
-rm -rf $O/env_fetch $O/env_write
+timeout -k 10 300 python bench.py --envs 1024 --steps 10 --warmup 3 --no-cpu > $O/bench_1024.json 2> $O/bench_1024.err
+cat $O/bench_1024.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu > $O/prof.log 2>&1
+python3 tools/rocpd_report.py stats $O/prof $O/kernel_stats_4096.csv
+rm -rf $O/prof
+for B in 4096 1024; do
+  K=$(python3 -c "import sys; sys.path.insert(0,'muzero-breakout_amd'); from mzba import _lib as L; print({2: 'tower8_kernel<0, 2>', 3: 'tower8_kernel<0, 1>'}.get(L.lib().mzba_tower_plan($B), 'tower_kernel<0>'))")
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 bench.py --envs $B --steps 1 --warmup 1 --no-graph --no-cpu > $O/pmc_f_$B.log 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 bench.py --envs $B --steps 1 --warmup 1 --no-graph --no-cpu > $O/pmc_w_$B.log 2>&1
+  python3 tools/pmc_tower_bench.py $O/pmc_fetch $O/pmc_write $B "$K" $O/tower_hbm_traffic.json
+  rm -rf $O/pmc_fetch $O/pmc_write
+done
+echo "round script done"
