@@ -651,7 +651,11 @@ __global__ __launch_bounds__(256, 1) void conv_lat2_kernel(LatArgs a) {
 
 }  // namespace
 
-static int g_lat_variant = 0;  // kernel shape (experiments): see mzba_conv_lat_set_variant
+// kernel shape, see mzba_conv_lat_set_variant. Per host thread: the learner brackets a minibatch
+// with set/restore, and mzba_conv_lat_bn_chunks (which sizes the caller's partial-statistics buffer)
+// and the launch that fills it must see the same value even if another host thread (acting beside
+// learning) sets its own.
+static thread_local int g_lat_variant = 0;
 
 extern "C" {
 

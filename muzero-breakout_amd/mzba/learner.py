@@ -106,12 +106,14 @@ class Learner:
             raise ValueError("streams must be 1 or 2")
         self.streams = streams
         self._side_stream = None
-        # conv_lat workgroup rows for the bf16 latent convs: 3-row tiles fill the CUs a lone B = 512
-        # conv leaves idle; with two streams the other chain fills them and 5-row tiles (less weight
-        # streaming per row) win — 31.6 vs 32.5 ms (two streams), 42.2 vs 37.9 ms (one stream)
-        if lat_rows not in (None, 3, 5):
-            raise ValueError("lat_rows must be None, 3 or 5")
-        self.lat_rows = lat_rows if lat_rows is not None else (5 if streams == 2 else 3)
+        # conv_lat workgroup rows for the bf16 latent convs: "auto" lets conv_lat take 3-row tiles where
+        # a lone B = 512 conv's 5-row grid would leave CUs idle; with two streams the other chain fills
+        # them and forced 5-row tiles (less weight streaming per row) win — 31.6 vs 32.5 ms (two
+        # streams), 42.2 vs 37.9 ms (one stream). The choice is a per-host-thread conv_lat setting
+        # (thread_local in csrc/conv_lat.hip) bracketed around each minibatch.
+        if lat_rows not in (None, "auto", 5):
+            raise ValueError('lat_rows must be None, "auto" or 5')
+        self.lat_rows = lat_rows if lat_rows is not None else (5 if streams == 2 else "auto")
         self._tag = ""
         self.defer_wgrad = defer_wgrad
         # bf16: BN batch statistics computed in the epilogue of the conv_lat launch that produces the

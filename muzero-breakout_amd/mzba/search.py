@@ -109,6 +109,8 @@ class MCTSSearchVec:
         B = hidden_state.shape[0]
         ws = self.workspace(B)
         ws.load_root(hidden_state)
+        if noise is not None:  # injected Dirichlet rows (B, 3), any array-like
+            noise = torch.as_tensor(np.asarray(noise, dtype=np.float32), device=ws.agent.device).contiguous()
         values, counts = ws.run(self.search_id, noise)
         self.search_id += 1
         return values.cpu(), counts.cpu()

@@ -90,3 +90,18 @@ def test_torch_custom_ops_registered():
     sch = str(ops.env_step.default._schema)
     assert "Tensor(a!) done" in sch and "Tensor(a!) done_out" in sch, sch
     assert "Tensor(h!) values" in str(ops.mcts_results_.default._schema)
+
+
+def test_default_checkpoint_optimizer_state_loads_into_reference_adam():
+    """Without a learner, save_checkpoint writes a fresh Adam state that the reference's
+    `optimizer.load_state_dict` (train_torch.py:646) accepts: one group, every parameter."""
+    import torch
+    from mzba.checkpoint import fresh_optimizer_state
+    from mzba.config import default_config
+    from mzba.weights import state_dict_spec
+    mcfg = default_config()["model"]
+    params = [torch.nn.Parameter(torch.zeros(1)) for k, _ in state_dict_spec(mcfg)
+              if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))]
+    opt = torch.optim.Adam(params, lr=mcfg["learning_rate"], weight_decay=1e-4)
+    opt.load_state_dict(fresh_optimizer_state(mcfg))
+    assert opt.param_groups[0]["weight_decay"] == 1e-4 and len(opt.param_groups[0]["params"]) == len(params)

@@ -196,6 +196,30 @@ def test_learner_state_and_optimizer_roundtrip():
         torch.testing.assert_close(v, sd2[k], rtol=0, atol=0, msg=k)
 
 
+def test_checkpoint_carries_learner_optimizer_state(tmp_path):
+    """save_checkpoint(learner=...) writes the learner's Adam state in the reference's format;
+    load_checkpoint(learner=...) restores weights and moments, so training continues bit-identically."""
+    from mzba.agent import MuZeroAgent
+    from mzba.checkpoint import save_checkpoint, load_checkpoint
+    from mzba.config import learner_model_cfg
+    from mzba.learner import Learner, MinibatchRing
+    from mzba.weights import init_state_dict
+    z = np.load(os.path.join(GOLDEN, "learner_small.npz"))
+    mcfg = learner_model_cfg()
+    ln = Learner(mcfg, init_state_dict(mcfg, 3), K=int(z["K"]))
+    ring = MinibatchRing(_mb(z, 1))
+    ln.train_minibatch(ring, ring.slots())
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(ln.state_dict())
+    p = str(tmp_path / "ck.pth")
+    save_checkpoint(p, ag, learner=ln, training_iteration=1)
+    ln2 = Learner(mcfg, init_state_dict(mcfg, 99), K=int(z["K"]))
+    load_checkpoint(p, learner=ln2)
+    a = ln.train_minibatch(ring, ring.slots()).cpu()
+    b = ln2.train_minibatch(ring, ring.slots()).cpu()
+    torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
 def _random_ring(B, L, K, seed):
     from mzba.learner import MinibatchRing
     g = np.random.default_rng(seed)
@@ -551,7 +575,7 @@ def test_learner_fused_bn_statistics_track_separate_passes():
     # another chunking is another bf16-noise realisation); the 5-row tiling's partial statistics are
     # checked against the separate passes directly (test_conv_lat_bn_matches_separate_passes[2-...])
     for tag, dt, fuse in (("sep", "bf16", False), ("fused", "bf16", True), ("f32", "f32", False)):
-        ln = Learner(mcfg, init_state_dict(mcfg, 4), K=5, dtype=dt, fuse_bn=fuse, lat_rows=3)
+        ln = Learner(mcfg, init_state_dict(mcfg, 4), K=5, dtype=dt, fuse_bn=fuse, lat_rows="auto")
         out[tag] = (ln.train_minibatch(ring, ring.slots()).cpu(), ln.gradients())
         del ln
     torch.testing.assert_close(out["fused"][0], out["sep"][0], rtol=2e-3, atol=1e-5)

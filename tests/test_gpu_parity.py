@@ -1005,6 +1005,12 @@ def test_checkpoint_reference_format_roundtrip(tmp_path):
     assert set(raw) == {"model_state_dict", "optimizer_state_dict", "training_iteration", "acting_step", "iteration",
                         "replay_buffer"}
     assert set(raw["replay_buffer"]) == set(REPLAY_KEYS)
+    # the reference's _load_weights does optimizer.load_state_dict(...) on Adam(mu_zero.parameters()):
+    # the default-saved optimizer state must load into an Adam over parameters of those shapes
+    from mzba.weights import state_dict_spec
+    params = [torch.nn.Parameter(torch.zeros(s)) for k, s in state_dict_spec(mcfg)
+              if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))]
+    torch.optim.Adam(params, lr=mcfg["learning_rate"], weight_decay=1e-4).load_state_dict(raw["optimizer_state_dict"])
     np.testing.assert_array_equal(torch.stack(raw["replay_buffer"]["state_buffer"]).numpy(), d["states"])
     np.testing.assert_array_equal(torch.stack(raw["replay_buffer"]["bootstrapped_values"]).numpy(), d["targets"])
     ag2 = MuZeroAgent(mcfg, dtype="f32")
