@@ -513,8 +513,42 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
 // One activation image: a conv reads it whole, then (after a barrier) its output overwrites it in
 // place; conv1 first lifts the block input at its own output positions into registers (the residual).
 
+// ReLU of two packed bf16 / fp16 values: the sign bit is the int16 sign, so max(i16, 0) zeroes
+// negatives (and -0). relu(round(x)) == round(relu(x)) for round-to-nearest, so this equals the
+// f32 ReLU before the conversion, bit for bit (one v_pk_max_i16 instead of two v_max_f32).
+MZ_DEV uint32_t relu_pk(uint32_t u) {
+  uint32_t r;
+  asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(u));
+  return r;
+}
+
+// A wave's view of a weight pack: the pack, its k steps per column tile and the wave's first column
+// tile. Everything but the lane's 16-B offset is wave-uniform, so the loads address off SGPRs.
+struct WNext {
+  __amdgpu_buffer_rsrc_t rs;  // buffer resource over the pack at the wave's first column tile
+  int tstride;                // bytes per column tile (k steps x 1 KB)
+  // 16-B fragment of k step `step` of the wave's column tile + ct, this lane: buffer load with the
+  // lane's offset in one VGPR and the (ct, step) offset in an SGPR
+  MZ_DEV uint4 ld(int ct, int step, int lane) const {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, ct * tstride + step * 1024, 0));
+  }
+  // the same for a 3x3 pack (72 k steps per tile)
+  MZ_DEV uint4 ld3(int ct, int step, int lane) const {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, ct * (TNS * 1024) + step * 1024, 0));
+  }
+};
+MZ_DEV WNext wnext(const void* w, int tns, int ct0) {
+  const uint4* p = reinterpret_cast<const uint4*>(w) + (size_t)ct0 * tns * 64;
+  return WNext{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(p), 0, 0x7fffffff, 0x00020000), tns * 1024};
+}
+
+// Weight ring of one wave: its 4 column tiles x TD k steps in flight (bq). The ring runs across
+// conv boundaries: the last TD loads of a 3x3 conv fetch the NEXT conv's first k steps (`wn`, the
+// next pack at this wave's first column tile + lane, `tnsn` k steps per tile), so those loads fly
+// through the epilogue and both barriers (a workgroup barrier waits for LDS, not for vmcnt) and the
+// next conv's first MFMAs find their weights in registers.
 template <int EL, int NQ, int DX>
-__device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
+__device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
                                           uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
   constexpr int NX = DX == 0 ? 5 : 4;   // active x tiles per env quad
   constexpr int NA = NQ * NX;           // active tiles
@@ -541,7 +575,14 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 #pragma unroll
       for (int ct = 0; ct < t8::CT; ++ct) {
         w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
-        bq[ct][c % TD] = wp[ct][(size_t)(s + TD) * 64];
+        if (DX == 1 && c + TD >= NC) {  // the last TD steps of dy = +1 fetch the next conv's first steps
+          const bool last = dyi == 2;
+          const __amdgpu_buffer_rsrc_t rs = last ? nxt.rs : cur.rs;
+          const int so = last ? ct * nxt.tstride + (c + TD - NC) * 1024 : ct * (TNS * 1024) + (s + TD) * 1024;
+          bq[ct][c % TD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
+        } else {
+          bq[ct][c % TD] = cur.ld3(ct, s + TD, lane);
+        }
       }
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
@@ -570,9 +611,10 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
   }
 }
 
-// the 8 k steps of a 1x1 conv on the 8-env image (centre tap: all 10 tiles, every row valid)
+// the 8 k steps of a 1x1 conv on the 8-env image (centre tap: all 10 tiles, every row valid); always
+// the last conv of a launch, so the ring is not continued
 template <int EL, int NQ>
-__device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, const uint4* const (&wp)[t8::CT],
+__device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, const WNext& cur,
                                               uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
   const int q = lane >> 4, key = lane & 15;
   const int base = key * TROWB, sw = key << 4;
@@ -585,7 +627,7 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
 #pragma unroll
     for (int ct = 0; ct < t8::CT; ++ct) {
       w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
-      if (c + TD < 8) bq[ct][c % TD] = wp[ct][(size_t)(c + TD) * 64];
+      if (c + TD < 8) bq[ct][c % TD] = cur.ld(ct, c + TD, lane);
     }
 #pragma unroll
     for (int j = 0; j < T8<NQ>::NRT; ++j) {
@@ -600,23 +642,26 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
   }
 }
 
-// k loop of one conv over the 8-env image: this wave's 4 channel tiles ct0..ct0+3 of a weight pack
-// with `tns` k steps per tile (72: 3x3, 8: 1x1). D[pack channel 16 ct + 4q + i][row 16 rt + l16].
+// the first TD k steps of a pack into the ring (the kernel's first conv; later convs are fetched by
+// their predecessor)
+MZ_DEV void tower8_preload(uint4 (&bq)[t8::CT][TD], const WNext& p, int lane) {
+#pragma unroll
+  for (int ct = 0; ct < t8::CT; ++ct)
+#pragma unroll
+    for (int i = 0; i < TD; ++i) bq[ct][i] = p.ld(ct, i, lane);
+}
+
+// k loop of one conv over the 8-env image: this wave's 4 channel tiles cur.ct0..+3 of a weight pack
+// with cur.tns k steps per tile (72: 3x3, 8: 1x1), weights already in the ring; a 3x3 conv leaves the
+// ring holding `nxt`'s first k steps. D[pack channel 16 ct + 4q + i][row 16 rt + l16].
 // MODE 0: acc starts at bias; 1: bias + res (registers); 2: bias + act_bias[pos][act[env]].
+// bconv: the conv's bias (LDS for the tower convs, global for the prologue / epilogue convs).
 template <int EL, int NQ, int MODE, bool CENTER>
-__device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const uint4* __restrict__ wconv, int tns,
+__device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
                                            int ct0, const float* __restrict__ bconv, const float* __restrict__ actb,
                                            const int* acts, int A, const uint2 (&res)[T8<NQ>::NRT][t8::CT],
-                                           f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
+                                           uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
   const int q = lane >> 4, l16 = lane & 15;
-  const uint4* wp[t8::CT];
-  uint4 bq[t8::CT][TD];
-#pragma unroll
-  for (int ct = 0; ct < t8::CT; ++ct) {
-    wp[ct] = wconv + (size_t)(ct0 + ct) * tns * 64 + lane;
-#pragma unroll
-    for (int i = 0; i < TD; ++i) bq[ct][i] = wp[ct][(size_t)i * 64];
-  }
 #pragma unroll
   for (int ct = 0; ct < t8::CT; ++ct) {
     const int n = (ct0 + ct) * 16 + 4 * q;
@@ -637,11 +682,11 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
     }
   }
   if (CENTER) {
-    tower8_center<EL, NQ>(lds, wp, bq, acc, lane);
+    tower8_center<EL, NQ>(lds, cur, bq, acc, lane);
   } else {
-    tower8_dx<EL, NQ, -1>(lds, wp, bq, acc, lane);
-    tower8_dx<EL, NQ, 0>(lds, wp, bq, acc, lane);
-    tower8_dx<EL, NQ, 1>(lds, wp, bq, acc, lane);
+    tower8_dx<EL, NQ, -1>(lds, cur, nxt, bq, acc, lane);
+    tower8_dx<EL, NQ, 0>(lds, cur, nxt, bq, acc, lane);
+    tower8_dx<EL, NQ, 1>(lds, cur, nxt, bq, acc, lane);
   }
 }
 
@@ -659,8 +704,8 @@ __device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, cons
       uint2* p = reinterpret_cast<uint2*>(lds + toff(rt * 16 + l16, n >> 3) + ((n & 7) << 1));
       if (SAVE) res[rt][ct] = *p;
       uint2 o;
-      o.x = Elt<EL>::pack2(fmaxf(acc[rt][ct][0], 0.f), fmaxf(acc[rt][ct][1], 0.f));
-      o.y = Elt<EL>::pack2(fmaxf(acc[rt][ct][2], 0.f), fmaxf(acc[rt][ct][3], 0.f));
+      o.x = relu_pk(Elt<EL>::pack2(acc[rt][ct][0], acc[rt][ct][1]));
+      o.y = relu_pk(Elt<EL>::pack2(acc[rt][ct][2], acc[rt][ct][3]));
       *p = o;
     }
 }
@@ -701,15 +746,18 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
 
 // one residual-tower conv (in place): k loop, barrier, write back, barrier
 template <int EL, int NQ, bool RESID>
-__device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const uint4* __restrict__ wconv,
+__device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt, int ct0,
                                             const float* __restrict__ bconv, uint2 (&res)[T8<NQ>::NRT][t8::CT],
-                                            int lane, int wave) {
+                                            uint4 (&bq)[t8::CT][TD], int lane) {
   f32x4 acc[T8<NQ>::NRT][t8::CT];
-  tower8_acc<EL, NQ, RESID ? 1 : 0, false>(lds, wconv, TNS, wave * t8::CT, bconv, nullptr, nullptr, 0, res, acc, lane);
+  tower8_acc<EL, NQ, RESID ? 1 : 0, false>(lds, cur, nxt, ct0, bconv, nullptr, nullptr, 0, res, bq, acc, lane);
   __syncthreads();  // every wave has read the whole image
-  tower8_writeback<EL, NQ, !RESID>(lds, acc, res, 0, wave * t8::CT, lane);
+  tower8_writeback<EL, NQ, !RESID>(lds, acc, res, 0, ct0, lane);
   __syncthreads();
 }
+
+// tower convs' biases staged in LDS (dynamic shared memory after the image): 2 nblocks x 256 f32
+constexpr int T8_MAX_BLOCKS = 24;
 
 template <int EL, int NQ>
 __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
@@ -719,17 +767,36 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   __shared__ float part[4 * 8 * 16];  // head partial sums [wave][env][output]
   __shared__ float lg[2 * 8 * 16];    // head logits [head][env][output]
   __shared__ float dec[2][8][4];      // decoded head outputs [head][env][output]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  extern __shared__ __attribute__((aligned(16))) float biasl[];  // [2 nblocks][256]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int env0 = blockIdx.x * T8<NQ>::E;
   const int nenv = min(T8<NQ>::E, a.B - env0);
   const int rows = nenv * 20;
   const bool pro = a.x.w0 != nullptr;
+  const int ctw = wave * t8::CT;
+  const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
+  constexpr size_t WCONV = (size_t)16 * TNS * 64;
+  // the weight ring's first k steps fly while the image is staged
+  uint4 bq[t8::CT][TD];
+  const WNext first = wnext(pro ? a.x.w0 : a.wf, TNS, ctw);
+  tower8_preload(bq, first, lane);
+  // where each wave's ring goes after the last tower conv: the epilogue conv it runs
+  WNext epi = first;
+  if (a.x.epilogue == 1) epi = wnext(a.x.we1, 8, ctw);
+  if (a.x.epilogue == 2) epi = wave < 2 ? wnext(a.x.we3, TNS, (wave & 1) * t8::CT) : wnext(a.x.we1, 8, (wave & 1) * t8::CT);
+  const int ct_epi = a.x.epilogue == 2 ? (wave & 1) * t8::CT : ctw;
   if (tid < T8<NQ>::E) {
     const int b = env0 + (tid < nenv ? tid : 0);
     long long off = (long long)b * a.in_env_stride;
     if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
     envoff[tid] = off;
     acts[tid] = pro ? a.x.act[b] : 0;
+  }
+  {  // tower biases -> LDS
+    const int n4 = a.nblocks * 2 * TC / 4;
+    for (int i = tid; i < n4; i += t8::NT)
+      reinterpret_cast<float4*>(biasl)[i] = reinterpret_cast<const float4*>(a.bias)[i];
   }
   __syncthreads();
   {  // stage X: ROWS x 32 chunks, 10 per thread per batch (NQ batches)
@@ -759,26 +826,24 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   uint2 res[T8<NQ>::NRT][t8::CT];
   if (pro) {  // dynamics ConvBlock (in place)
     f32x4 acc[T8<NQ>::NRT][t8::CT];
-    tower8_acc<EL, NQ, 2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), TNS, wave * t8::CT, a.x.b0, a.x.act_bias, acts,
-                         a.x.A, res, acc, lane);
+    tower8_acc<EL, NQ, 2, false>(lds, first, wnext(a.wf, TNS, ctw), ctw, a.x.b0, a.x.act_bias, acts, a.x.A, res, bq, acc, lane);
     __syncthreads();
-    tower8_writeback<EL, NQ, false>(lds, acc, res, 0, wave * t8::CT, lane);
+    tower8_writeback<EL, NQ, false>(lds, acc, res, 0, ctw, lane);
     __syncthreads();
   }
-  const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
-  constexpr size_t WCONV = (size_t)16 * TNS * 64;
   for (int blk = 0; blk < a.nblocks; ++blk) {
-    tower8_conv<EL, NQ, false>(lds, wf + (2 * blk) * WCONV, a.bias + (2 * blk) * TC, res, lane, wave);
-    tower8_conv<EL, NQ, true>(lds, wf + (2 * blk + 1) * WCONV, a.bias + (2 * blk + 1) * TC, res, lane, wave);
+    const WNext c1 = wnext(wf + (2 * blk) * WCONV, TNS, ctw), c2 = wnext(wf + (2 * blk + 1) * WCONV, TNS, ctw);
+    const WNext c3 = blk + 1 < a.nblocks ? wnext(wf + (2 * blk + 2) * WCONV, TNS, ctw) : epi;
+    tower8_conv<EL, NQ, false>(lds, c1, c2, ctw, biasl + (2 * blk) * TC, res, bq, lane);
+    tower8_conv<EL, NQ, true>(lds, c2, c3, ctw, biasl + (2 * blk + 1) * TC, res, bq, lane);
   }
   if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1, the scaled latent from X, then Linear + decode
     f32x4 acc[T8<NQ>::NRT][t8::CT];
-    tower8_acc<EL, NQ, 0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, wave * t8::CT, a.x.be1, nullptr, nullptr, 0,
-                        res, acc, lane);
+    tower8_acc<EL, NQ, 0, true>(lds, epi, epi, ctw, a.x.be1, nullptr, nullptr, 0, res, bq, acc, lane);
     __syncthreads();
     tower8_scale<EL, NQ>(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
     __syncthreads();
-    tower8_writeback<EL, NQ, false>(lds, acc, res, 0, wave * t8::CT, lane);
+    tower8_writeback<EL, NQ, false>(lds, acc, res, 0, ctw, lane);
     __syncthreads();
     const int hc0[2] = {0, 0}, hC[2] = {TC, 0}, kind[2] = {1, 0};
     tower_heads<EL, T8<NQ>::E, 4, true>(a, lds, 0, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
@@ -786,15 +851,12 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   }
   if (a.x.epilogue == 2) {  // prediction: policy 3x3 (waves 0-1) -> [0,128), value 1x1 (waves 2-3) -> [128,256)
     f32x4 acc[T8<NQ>::NRT][t8::CT];
-    const int ct0 = (wave & 1) * t8::CT;
     if (wave < 2)
-      tower8_acc<EL, NQ, 0, false>(lds, reinterpret_cast<const uint4*>(a.x.we3), TNS, ct0, a.x.be3, nullptr, nullptr, 0, res,
-                           acc, lane);
+      tower8_acc<EL, NQ, 0, false>(lds, epi, epi, ct_epi, a.x.be3, nullptr, nullptr, 0, res, bq, acc, lane);
     else
-      tower8_acc<EL, NQ, 0, true>(lds, reinterpret_cast<const uint4*>(a.x.we1), 8, ct0, a.x.be1, nullptr, nullptr, 0, res, acc,
-                          lane);
+      tower8_acc<EL, NQ, 0, true>(lds, epi, epi, ct_epi, a.x.be1, nullptr, nullptr, 0, res, bq, acc, lane);
     __syncthreads();
-    tower8_writeback<EL, NQ, false>(lds, acc, res, wave < 2 ? 0 : 128, ct0, lane);
+    tower8_writeback<EL, NQ, false>(lds, acc, res, wave < 2 ? 0 : 128, ct_epi, lane);
     __syncthreads();
     const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
     tower_heads<EL, T8<NQ>::E, 4, true>(a, lds, 0, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
@@ -819,6 +881,8 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
 }
 
 static int g_tower_variant = 0;  // 0 auto, 1 four-env kernel, 2 eight-env kernel, 3 four-env 4-wave
+
+static size_t t8_dyn_lds(int nblocks) { return (size_t)nblocks * 2 * TC * sizeof(float); }
 
 static int tower_ncu() {
   static int ncu = 0;
@@ -867,14 +931,15 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && out && wf16 && bias, -1);
   const int plan = mzba_tower_plan(B);
   MZ_CHECK_ARG(plan > 0, -2);
+  MZ_CHECK_ARG(plan == 1 || nblocks <= T8_MAX_BLOCKS, -5);  // tower8: bias table in LDS
   TowerArgs a{(const bf16_t*)in, in_env_stride, slot, in_slot_stride, (bf16_t*)out, (const bf16_t*)wf16, bias,
               nblocks, B, mzba_tower_ext{}, TreeArgs{}, 0, 0, 0.f, nullptr};
   (void)ws;
   (void)ws_bytes;
   if (plan == 2) {
-    hipLaunchKernelGGL((tower8_kernel<0, 2>), dim3((B + 7) / 8), dim3(t8::NT), 0, stream, a);
+    hipLaunchKernelGGL((tower8_kernel<0, 2>), dim3((B + 7) / 8), dim3(t8::NT), t8_dyn_lds(nblocks), stream, a);
   } else if (plan == 3) {
-    hipLaunchKernelGGL((tower8_kernel<0, 1>), dim3((B + 3) / 4), dim3(t8::NT), 0, stream, a);
+    hipLaunchKernelGGL((tower8_kernel<0, 1>), dim3((B + 3) / 4), dim3(t8::NT), t8_dyn_lds(nblocks), stream, a);
   } else {
     hipLaunchKernelGGL(tower_kernel<0>, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
   }
@@ -889,6 +954,7 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && wf16 && bias && ext, -1);
   const int plan = mzba_tower_plan(B);
   MZ_CHECK_ARG(plan >= 1 && plan <= 3, -4);
+  MZ_CHECK_ARG(plan == 1 || nblocks <= T8_MAX_BLOCKS, -5);  // tower8: bias table in LDS
   const mzba_tower_ext& x = *ext;
   MZ_CHECK_ARG(x.epilogue >= 0 && x.epilogue <= 2 && (x.elem == 0 || x.elem == 1), -2);
   MZ_CHECK_ARG(!x.w0 || (x.b0 && x.act_bias && x.act && x.A > 0), -3);
@@ -912,12 +978,12 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
   }
   const dim3 g8((B + 7) / 8), g4((B + TE - 1) / TE);
   if (x.elem == 1) {
-    if (plan == 2) hipLaunchKernelGGL((tower8_kernel<1, 2>), g8, dim3(t8::NT), 0, stream, a);
-    else if (plan == 3) hipLaunchKernelGGL((tower8_kernel<1, 1>), g4, dim3(t8::NT), 0, stream, a);
+    if (plan == 2) hipLaunchKernelGGL((tower8_kernel<1, 2>), g8, dim3(t8::NT), t8_dyn_lds(nblocks), stream, a);
+    else if (plan == 3) hipLaunchKernelGGL((tower8_kernel<1, 1>), g4, dim3(t8::NT), t8_dyn_lds(nblocks), stream, a);
     else hipLaunchKernelGGL(tower_kernel<1>, g4, dim3(TNT), 0, stream, a);
   } else {
-    if (plan == 2) hipLaunchKernelGGL((tower8_kernel<0, 2>), g8, dim3(t8::NT), 0, stream, a);
-    else if (plan == 3) hipLaunchKernelGGL((tower8_kernel<0, 1>), g4, dim3(t8::NT), 0, stream, a);
+    if (plan == 2) hipLaunchKernelGGL((tower8_kernel<0, 2>), g8, dim3(t8::NT), t8_dyn_lds(nblocks), stream, a);
+    else if (plan == 3) hipLaunchKernelGGL((tower8_kernel<0, 1>), g4, dim3(t8::NT), t8_dyn_lds(nblocks), stream, a);
     else hipLaunchKernelGGL(tower_kernel<0>, g4, dim3(TNT), 0, stream, a);
   }
   MZ_LAUNCH_CHECK();
