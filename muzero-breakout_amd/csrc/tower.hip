@@ -109,6 +109,29 @@ struct TowerArgs {
   const float* tree_r;
 };
 
+#ifdef TOWER_STAMPS
+// diagnostic build only (make tower-stamps -> libmzba_tstamp.so, tools/stamp_tower.py): s_memtime at
+// the phase boundaries of every conv, per workgroup and wave; slot 2 + 6 ci + phase for conv ci
+// (phase 0 k loop start, 1/2/3 after the dx = -1/0/+1 taps, 4 after the first barrier, 5 after the
+// write-back barrier); 0 entry, 1 after staging, TST_N - 3/-2 s_memrealtime at entry / exit, TST_N - 1 exit
+constexpr int TST_N = 192, TST_WG = 1024;
+__device__ unsigned long long mz_tower_stamps[TST_WG * 4][TST_N];
+MZ_DEV void tstamp(int k, bool real = false) {
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < TST_WG && k < TST_N)
+    mz_tower_stamps[blockIdx.x * 4 + (threadIdx.x >> 6)][k] =
+        real ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+}
+#define TSTAMP(k) tstamp(k)
+#define TSTAMP_END() (tstamp(TST_N - 2, true), tstamp(TST_N - 1))
+#else
+#define TSTAMP(k) \
+  do {            \
+  } while (0)
+#define TSTAMP_END() \
+  do {               \
+  } while (0)
+#endif
+
 // LDS row of (env e, latent position p = 5y + x) and the byte offset of (row, 16-B chunk)
 MZ_DEV int trow(int e, int p) { return (p % 5) * 16 + (p / 5) * 4 + e; }
 MZ_DEV int toff(int row, int chunk) { return row * TROWB + ((chunk ^ (row & 15)) << 4); }
@@ -581,7 +604,11 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
           const int so = last ? ct * nxt.tstride + (c + TD - NC) * 1024 : ct * (TNS * 1024) + (s + TD) * 1024;
           bq[ct][c % TD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
         } else {
+#if TOWER_ABLATE == 1  // diagnostic only: weights from one L1-resident pair of k steps
+          bq[ct][c % TD] = cur.ld3(ct, (s + TD) & 1, lane);
+#else
           bq[ct][c % TD] = cur.ld3(ct, s + TD, lane);
+#endif
         }
       }
 #pragma unroll
@@ -590,19 +617,28 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 #pragma unroll
         for (int ct = 0; ct < t8::CT; ++ct)
           acc[at][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[at][ct]);
-        if (c + 1 < NC)
+        if (TOWER_ABLATE == 2)  // diagnostic only: no LDS A reads inside the loop
+          afn[j] = afc[j];
+        else if (c + 1 < NC)
           afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, base, tst) + (((4 * (c + 1) + q) << 4) ^ sw));
         else
           afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, nbase, ntst) + ((q << 4) ^ nsw));
       }
+      // schedule: every A read of the next k step in the first NA MFMA slots (the compiler orders a
+      // step's independent MFMAs freely, so the next step may open with any tile: its reads must have
+      // landed by then), the weight loads next, then the remaining MFMAs
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-        if (j < t8::CT) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
+#pragma unroll
+      for (int ct = 0; ct < t8::CT; ++ct) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NA * t8::CT - NA - 2 * t8::CT, 0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NA; ++j) afc[j] = afn[j];
@@ -660,8 +696,10 @@ template <int EL, int NQ, int MODE, bool CENTER>
 __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
                                            int ct0, const float* __restrict__ bconv, const float* __restrict__ actb,
                                            const int* acts, int A, const uint2 (&res)[T8<NQ>::NRT][t8::CT],
-                                           uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
+                                           uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane,
+                                           int ci = 0) {
   const int q = lane >> 4, l16 = lane & 15;
+  TSTAMP(2 + 6 * ci);
 #pragma unroll
   for (int ct = 0; ct < t8::CT; ++ct) {
     const int n = (ct0 + ct) * 16 + 4 * q;
@@ -685,9 +723,12 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
     tower8_center<EL, NQ>(lds, cur, bq, acc, lane);
   } else {
     tower8_dx<EL, NQ, -1>(lds, cur, nxt, bq, acc, lane);
+    TSTAMP(3 + 6 * ci);
     tower8_dx<EL, NQ, 0>(lds, cur, nxt, bq, acc, lane);
+    TSTAMP(4 + 6 * ci);
     tower8_dx<EL, NQ, 1>(lds, cur, nxt, bq, acc, lane);
   }
+  TSTAMP(5 + 6 * ci);
 }
 
 // ReLU -> bf16 -> the image at channel nout + 16 (ct0 + ct) + 4q (8-byte stores, in place after a
@@ -748,12 +789,14 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
 template <int EL, int NQ, bool RESID>
 __device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt, int ct0,
                                             const float* __restrict__ bconv, uint2 (&res)[T8<NQ>::NRT][t8::CT],
-                                            uint4 (&bq)[t8::CT][TD], int lane) {
+                                            uint4 (&bq)[t8::CT][TD], int lane, int ci) {
   f32x4 acc[T8<NQ>::NRT][t8::CT];
-  tower8_acc<EL, NQ, RESID ? 1 : 0, false>(lds, cur, nxt, ct0, bconv, nullptr, nullptr, 0, res, bq, acc, lane);
+  tower8_acc<EL, NQ, RESID ? 1 : 0, false>(lds, cur, nxt, ct0, bconv, nullptr, nullptr, 0, res, bq, acc, lane, ci);
   __syncthreads();  // every wave has read the whole image
+  TSTAMP(6 + 6 * ci);
   tower8_writeback<EL, NQ, !RESID>(lds, acc, res, 0, ct0, lane);
   __syncthreads();
+  TSTAMP(7 + 6 * ci);
 }
 
 // tower convs' biases staged in LDS (dynamic shared memory after the image): 2 nblocks x 256 f32
@@ -779,6 +822,10 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   constexpr size_t WCONV = (size_t)16 * TNS * 64;
   // the weight ring's first k steps fly while the image is staged
   uint4 bq[t8::CT][TD];
+  TSTAMP(0);
+#ifdef TOWER_STAMPS
+  tstamp(TST_N - 3, true);
+#endif
   const WNext first = wnext(pro ? a.x.w0 : a.wf, TNS, ctw);
   tower8_preload(bq, first, lane);
   // where each wave's ring goes after the last tower conv: the epilogue conv it runs
@@ -823,6 +870,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     for (int u = 0; u < 2; ++u) *reinterpret_cast<uint4*>(lds + T8<NQ>::LZ + (u * t8::NT + tid) * 16) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
+  TSTAMP(1);
   uint2 res[T8<NQ>::NRT][t8::CT];
   if (pro) {  // dynamics ConvBlock (in place)
     f32x4 acc[T8<NQ>::NRT][t8::CT];
@@ -834,8 +882,8 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   for (int blk = 0; blk < a.nblocks; ++blk) {
     const WNext c1 = wnext(wf + (2 * blk) * WCONV, TNS, ctw), c2 = wnext(wf + (2 * blk + 1) * WCONV, TNS, ctw);
     const WNext c3 = blk + 1 < a.nblocks ? wnext(wf + (2 * blk + 2) * WCONV, TNS, ctw) : epi;
-    tower8_conv<EL, NQ, false>(lds, c1, c2, ctw, biasl + (2 * blk) * TC, res, bq, lane);
-    tower8_conv<EL, NQ, true>(lds, c2, c3, ctw, biasl + (2 * blk + 1) * TC, res, bq, lane);
+    tower8_conv<EL, NQ, false>(lds, c1, c2, ctw, biasl + (2 * blk) * TC, res, bq, lane, 2 * blk);
+    tower8_conv<EL, NQ, true>(lds, c2, c3, ctw, biasl + (2 * blk + 1) * TC, res, bq, lane, 2 * blk + 1);
   }
   if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1, the scaled latent from X, then Linear + decode
     f32x4 acc[T8<NQ>::NRT][t8::CT];
@@ -878,6 +926,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
       *reinterpret_cast<uint4*>(a.out + (long long)(env0 + r / 20) * 20 * TC + (r % 20) * TC + c * 8) =
           Elt<EL>::to_bf16(*reinterpret_cast<const uint4*>(lds + toff(t8::row8(r / 20, r % 20), c)));
   }
+  TSTAMP_END();
 }
 
 static int g_tower_variant = 0;  // 0 auto, 1 four-env kernel, 2 eight-env kernel, 3 four-env 4-wave
@@ -897,6 +946,12 @@ static int tower_ncu() {
 }  // namespace
 
 extern "C" {
+
+#ifdef TOWER_STAMPS
+int mzba_tower_stamps_read(unsigned long long* host, int nrows) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mz_tower_stamps), sizeof(unsigned long long) * TST_N * nrows);
+}
+#endif
 
 // 0: pick by batch (default), 1: force the 4-env kernel, 2: force the 8-env kernel, 3: the 4-env
 // 4-wave kernel (the 8-env kernel's structure on one env quad)
