@@ -169,16 +169,17 @@ int mzba_replay_states(const uint8_t* states, const int32_t* slots, int n, const
 /* kernel choice for experiments/tests: 0 by batch (default), 1 four-env 8-wave kernel, 2 eight-env
  * kernel, 3 four-env 4-wave kernel */
 int mzba_tower_set_variant(int v);
-/* kernel mzba_tower runs for batch B: 1 four-env (workgroup = 4 envs, 8 waves of 32 output channels) below
- * 8 x CUs envs, else 2 eight-env (workgroup = 8 envs, 4 waves: half the weight stream per env); 3 = the
- * four-env 4-wave kernel (64 channels per wave; by variant only). All take agent.pack_tower_conv weights. */
+/* kernel mzba_tower runs for batch B: 3 four-env 4-wave (workgroup = 4 envs, 4 waves of 64 output channels)
+ * below 8 x CUs envs, else 2 eight-env (workgroup = 8 envs, 4 waves: half the weight stream per env);
+ * 1 = the four-env 8-wave kernel (32 channels per wave; by variant only). All take agent.pack_tower_conv
+ * weights. The 4-wave kernels stage the tower biases in LDS: nblocks <= 24 (else -5). */
 int mzba_tower_plan(int B);
 /* device scratch bytes mzba_tower needs for batch B (0 for both kernels; the ws argument may be null) */
 long long mzba_tower_ws_bytes(int B);
 int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride, void* out,
                const void* wf16, const float* bias, int nblocks, int B, void* ws, long long ws_bytes,
                hipStream_t stream);
-/* Fused per-simulation nets around the tower (4-env kernel, plan 1): the dynamics ConvBlock
+/* Fused per-simulation nets around the tower (every plan): the dynamics ConvBlock
  * before it and the reward / policy / value heads after it run in the same launch, so one
  * dynamics step and one prediction step are one kernel each (networks.py:151-167, 200-241,
  * 314-328; utils.py:74-81). */

@@ -68,6 +68,17 @@ template <int EL> MZ_DEV void unpack8(uint4 v, float (&f)[8]) {
   f[4] = Elt<EL>::lo(v.z); f[5] = Elt<EL>::hi(v.z); f[6] = Elt<EL>::lo(v.w); f[7] = Elt<EL>::hi(v.w);
 }
 
+// an MFMA B fragment shifted by 4 columns inside each 16-lane row (zeros shifted in): the same tile
+// read one latent row up / down (columns = image rows 4y + e)
+template <int EL> MZ_DEV typename Elt<EL>::v8 dpp_shl4(typename Elt<EL>::v8 v) {
+  int4 i = __builtin_bit_cast(int4, v);
+  i.x = __builtin_amdgcn_update_dpp(0, i.x, 0x104, 0xf, 0xf, true);
+  i.y = __builtin_amdgcn_update_dpp(0, i.y, 0x104, 0xf, 0xf, true);
+  i.z = __builtin_amdgcn_update_dpp(0, i.z, 0x104, 0xf, 0xf, true);
+  i.w = __builtin_amdgcn_update_dpp(0, i.w, 0x104, 0xf, 0xf, true);
+  return __builtin_bit_cast(typename Elt<EL>::v8, i);
+}
+
 constexpr int TE = 4;              // envs per workgroup
 constexpr int TROWS = 80;          // TE * 20 (4x5 latent)
 constexpr int TC = 256;            // channels
@@ -619,6 +630,8 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
           acc[at][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[at][ct]);
         if (TOWER_ABLATE == 2)  // diagnostic only: no LDS A reads inside the loop
           afn[j] = afc[j];
+        else if (TOWER_ABLATE == 3 && c % 3 != 0)  // diagnostic only: 2 of 3 A fragments by DPP row shift
+          afn[j] = dpp_shl4<EL>(afc[j]);
         else if (c + 1 < NC)
           afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, base, tst) + (((4 * (c + 1) + q) << 4) ^ sw));
         else
@@ -962,15 +975,15 @@ int mzba_tower_set_variant(int v) {
 }
 
 // kernel used for batch B: 2 eight-env (B >= 8 x CUs: it halves the per-env weight stream but needs
-// that many envs to fill the chip), else 1 four-env 8-wave. Variant 3 = four-env 4-wave (the 8-env
-// kernel's structure on one env quad: each wave 4 column tiles x 5 row tiles, half the LDS A reads
-// per MFMA of kernel 1): 478 vs 510 us per plain 14-block tower at B = 1024 (tools/bench_conv.py
-// tower), but equal in the acting loop's fused steps (19.1k env-steps/s both, same box), so kernel 1
-// stays the default. All take agent.pack_tower_conv weights.
+// that many envs to fill the chip), else 3 four-env 4-wave (the 8-env kernel's code on one env quad:
+// each wave 4 column tiles x 5 row tiles). Kernel 1 (four-env 8-wave) stays selectable: it was the
+// default below 8 x CUs until the 4-wave kernels got the cross-conv weight ring and front-loaded A
+// reads (B = 1024 acting loop, same box: 20.2k env-steps/s on kernel 1, 20.9k on kernel 3,
+// profiles/r02/plan3_1024/). All take agent.pack_tower_conv weights.
 int mzba_tower_plan(int B) {
   if (B <= 0) return -1;
   if (g_tower_variant) return g_tower_variant;
-  return B >= 8 * tower_ncu() ? 2 : 1;
+  return B >= 8 * tower_ncu() ? 2 : 3;
 }
 
 // device workspace bytes mzba_tower needs for batch B (0 for both current kernels)
