@@ -665,6 +665,10 @@ class Learner:
         corrections from a device scalar block), so a minibatch is one graph launch from the
         host. Call after at least one eager minibatch of the same size (weight packs and scratch
         buffers allocated). Replays are launch-for-launch the eager minibatch (bit-identical)."""
+        if self.streams == 2 and self._side_stream is None:
+            # the side stream must exist (default priority, created by an eager minibatch) before
+            # capture: no stream is created or re-prioritised inside torch.cuda.graph (DESIGN.md §10)
+            raise RuntimeError("Learner.capture: run one eager minibatch of this size first")
         self._graph = None
         self._g_slots = torch.zeros(B, dtype=torch.int32, device=self.device)
         self._adam_sc = torch.zeros(7, dtype=torch.float32, device=self.device)

@@ -287,6 +287,108 @@ def test_fused_steps_match_unfused(B, variant):
     assert torch.equal(res[True][0], res[True][1])  # scaled latent also written to the pool slot
 
 
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+class _Bf16StepRef:
+    """Plain torch fp32 reference of the fused bf16 dynamics / prediction steps (CPU), rounding to
+    bf16 exactly where the kernels store bf16: BN folded in f64 (networks.py:7-35 eval) then weights
+    rounded f64 -> f32 -> bf16, every ReLU output (the LDS images) rounded to bf16, f32 everywhere
+    else (accumulators, biases, the action-plane bias table, Linear heads, min-max scale)."""
+
+    def __init__(self, sd, mcfg):
+        self.sd = {k: np.asarray(v, np.float64) for k, v in sd.items()}
+        self.c1 = mcfg["latent_channels"][1]
+        self.nd = mcfg["dynamics_network"]["num_res_blocks"]
+        self.np_ = mcfg["prediction_network"]["num_res_blocks"]
+
+    def _fold(self, p, bn):
+        s = self.sd
+        a = s[bn + ".weight"] / np.sqrt(s[bn + ".running_var"] + 1e-5)
+        w = s[p + ".weight"] * a[:, None, None, None]
+        b = s[p + ".bias"] * a + (s[bn + ".bias"] - s[bn + ".running_mean"] * a)
+        return torch.tensor(w, dtype=torch.float32), torch.tensor(b, dtype=torch.float32)
+
+    def _conv(self, x, p, bn, pad, extra=None):
+        w, b = self._fold(p, bn)
+        y = torch.nn.functional.conv2d(x, _bf(w[:, : x.shape[1]]), b, padding=pad)
+        return y if extra is None else y + extra
+
+    def _lin(self, x, p):
+        return torch.nn.functional.linear(x.flatten(1), _bf(torch.tensor(self.sd[p + ".weight"], dtype=torch.float32)),
+                                          torch.tensor(self.sd[p + ".bias"], dtype=torch.float32))
+
+    def _tower(self, x, prefix, n):
+        for i in range(n):
+            p = f"{prefix}.{i}"
+            t = _bf(torch.relu(self._conv(x, p + ".conv1", p + ".bn1", 1)))
+            x = _bf(torch.relu(self._conv(t, p + ".conv2", p + ".bn2", 1, extra=x)))
+        return x
+
+    def dynamics(self, h, act):
+        """h: bf16-valued f32 NCHW latent, act: i64[B] -> scaled latent (bf16 values), reward logits."""
+        w, _ = self._fold("dyn_net.conv_block.conv", "dyn_net.conv_block.bn")
+        planes = torch.nn.functional.one_hot(act, 3).float()[:, :, None, None].expand(-1, -1, *h.shape[2:])
+        # the 3 action channels stay f32 (the kernels' per-(pixel, action) bias table)
+        ab = torch.nn.functional.conv2d(planes, w[:, self.c1:], None, padding=1)
+        x = _bf(torch.relu(self._conv(h, "dyn_net.conv_block.conv", "dyn_net.conv_block.bn", 1, extra=ab)))
+        x = self._tower(x, "dyn_net.res_blocks", self.nd)
+        r = _bf(torch.relu(self._conv(x, "dyn_net.reward_head.0.conv", "dyn_net.reward_head.0.bn", 0)))
+        rl = self._lin(r, "dyn_net.reward_head.2")
+        f = x.flatten(1)
+        mn, mx = f.min(1).values[:, None, None, None], f.max(1).values[:, None, None, None]
+        return _bf((x - mn) / ((mx - mn) + 1e-8)), rl
+
+    def prediction(self, h):
+        x = self._tower(h, "pred_net.res_blocks", self.np_)
+        p = _bf(torch.relu(self._conv(x, "pred_net.policy_head.0.conv", "pred_net.policy_head.0.bn", 1)))
+        v = _bf(torch.relu(self._conv(x, "pred_net.value_head.0.conv", "pred_net.value_head.0.bn", 0)))
+        return self._lin(p, "pred_net.policy_head.2"), self._lin(v, "pred_net.value_head.2")
+
+
+@pytest.mark.parametrize("B,variant", [(13, 1), (64, 2), (13, 3), (64, 0)])
+def test_fused_bf16_steps_vs_torch_fp32(B, variant):
+    """The fused bf16 dynamics and prediction launches (ConvBlock + 14 residual blocks + heads +
+    min-max scale in one launch each) against a plain torch fp32 evaluation of the same folded,
+    bf16-rounded weights with bf16 activations where the kernels keep bf16 (_Bf16StepRef). The
+    remaining differences are f32 summation order inside a conv, each worth at most one bf16 ulp
+    of an activation; the tolerance, 2e-2 of the tensor's magnitude for the scaled latent and the
+    logits, is the one test_tower_matches_conv_chain uses for the plain tower."""
+    from mzba import _lib as L
+    from mzba.agent import MuZeroAgent
+    mcfg = default_config()["model"]
+    sd = init_state_dict(mcfg, 7)
+    ag = MuZeroAgent(mcfg, dtype="bf16")
+    ag.load_state_dict(sd)
+    L.call("mzba_tower_set_variant", variant)
+    try:
+        rn = ag.runner(B, 16, 20)
+    finally:
+        L.call("mzba_tower_set_variant", 0)
+    assert rn.fused_ok() and rn.tower_plan == (variant or L.lib().mzba_tower_plan(B))
+    n = 20 * 256
+    g = torch.Generator().manual_seed(B + variant)
+    src = torch.rand(B, n, generator=g).to(torch.bfloat16)
+    act = torch.randint(0, 3, (B,), generator=g)
+    lat = torch.empty(B, n, dtype=torch.bfloat16, device="cuda")
+    f = lambda *s: torch.full(s, float("nan"), device="cuda")  # noqa: E731
+    r, rl, pi, v, plg, vlg = f(B), f(B, 11), f(B, 3), f(B), f(B, 3), f(B, 11)
+    rn.dynamics(src.cuda(), act.to(torch.int32).cuda(), lat, r, rl)
+    rn.prediction(lat, pi, v, plg, vlg)
+    torch.cuda.synchronize()
+    ref = _Bf16StepRef(sd, mcfg)
+    nchw = lambda t: t.float().cpu().view(B, 4, 5, 256).permute(0, 3, 1, 2)  # noqa: E731
+    h_ref, rl_ref = ref.dynamics(nchw(src), act)
+    pl_ref, vl_ref = ref.prediction(nchw(lat))  # the kernel's own latent: isolates the prediction step
+    for nm, got, want in (("latent", nchw(lat), h_ref), ("reward_logits", rl.cpu(), rl_ref),
+                          ("policy_logits", plg.cpu(), pl_ref), ("value_logits", vlg.cpu(), vl_ref)):
+        assert torch.isfinite(got).all(), nm
+        err = (got - want).abs().max().item() / max(1.0, want.abs().max().item())
+        print(f"bf16 fused step vs torch fp32 [B={B}, variant={variant}] {nm}: {err:.2e}")
+        assert err < 2e-2, (nm, err)
+
+
 @pytest.mark.parametrize("Cin,Cout,resid,relu", [(128, 128, False, True), (128, 256, False, False),
                                                    (256, 256, True, True), (256, 128, False, True)])
 def test_band_conv_vs_torch_fp32(Cin, Cout, resid, relu):
