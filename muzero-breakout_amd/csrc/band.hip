@@ -99,14 +99,20 @@ __device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, const u
         else
           afn[t] = *reinterpret_cast<const bf16x8*>(lds + nbase + t * ntst + ((q << 4) ^ nsw));
       }
+      // every A read of the next k step in the first XT MFMA slots: the compiler orders a step's
+      // independent MFMAs freely, so the next step may open with any tile (tower.hip tower8_dx)
 #pragma unroll
       for (int t = 0; t < XT; ++t) {
-        __builtin_amdgcn_sched_group_barrier(0x008, CTW / 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, CTW - CTW / 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-        if (t < CTW) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
+#pragma unroll
+      for (int ct = 0; ct < CTW; ++ct) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, XT * CTW - XT - CTW, 0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < XT; ++t) afc[t] = afn[t];
