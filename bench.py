@@ -288,12 +288,17 @@ def tower_traffic(B, fused_tower):
     tpath = os.path.join(ROOT, "profiles", "tower_hbm_traffic.json")
     if not (fused_tower and os.path.exists(tpath)):
         return None, None
-    from mzba import _lib as L
-    kname = {2: "tower8_kernel<0, 2>", 3: "tower8_kernel<0, 1>"}.get(L.lib().mzba_tower_plan(B), "tower_kernel<0>")
+    kname = tower_kernel_name(B)
     for rec in json.load(open(tpath))["records"]:
         if rec.get("envs") == B and rec.get("kernel_name") == kname:
             return rec.get("bytes_per_launch"), rec
     return None, None
+
+
+def tower_kernel_name(B):
+    """The kernel mzba_tower_plan picks for batch B (tower.hip)."""
+    from mzba import _lib as L
+    return {2: "tower8_kernel<0, 2>", 3: "tower8_kernel<0, 1>"}.get(L.lib().mzba_tower_plan(B), "tower_kernel<0>")
 
 
 def conv_flops(B, hw, C):
@@ -459,8 +464,8 @@ def main():
                        "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
                        "parallelism": f"env-sharded x{world}, RCCL gather of trajectory records to rank 0, target-net broadcast"},
             "roofline": {"bound": "mfma",
-                         "kernel": "tower_kernel (fused 14-block residual tower, bf16 3x3 256->256 convs, M=B*20,"
-                                   " N=256, K=2304 each)" if tower_launch_ms else
+                         "kernel": (f"{tower_kernel_name(B)} (fused dynamics / prediction step: 14-block residual "
+                                    "tower, bf16 3x3 256->256 convs, M=B*20, N=256, K=2304 each)") if tower_launch_ms else
                                    (f"latent residual conv bf16 3x3 256->256 (M=B*{p.lh * p.lw},N=256,K=2304; "
                                     f"{'conv_lat' if p.lh * p.lw <= 160 else 'conv_igemm'} kernel)"),
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
