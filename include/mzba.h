@@ -234,6 +234,8 @@ typedef struct mzba_tower_ext {
   const mzba_tree_step* tree;  /* epilogue 2 only, may be NULL */
   int elem;                    /* LDS image / weight element type: 0 bf16, 1 fp16 (weights w0, we1, we3, lw and
                                   the tower packs in fp16; latents in / out stay bf16) */
+  int plan;                    /* tower kernel: 0 = mzba_tower_plan(B) at launch; 1 / 2 / 3 = that kernel (the
+                                  runner records the plan it packed for and launches exactly that one) */
 } mzba_tower_ext;
 int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                      void* out, const void* wf16, const float* bias, int nblocks, int B,

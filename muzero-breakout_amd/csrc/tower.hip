@@ -581,9 +581,9 @@ MZ_DEV WNext wnext(const void* w, int tns, int ct0) {
 // next pack at this wave's first column tile + lane, `tnsn` k steps per tile), so those loads fly
 // through the epilogue and both barriers (a workgroup barrier waits for LDS, not for vmcnt) and the
 // next conv's first MFMAs find their weights in registers.
-template <int EL, int NQ, int DX>
+template <int EL, int NQ, int DX, int CT = t8::CT>
 __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
-                                          uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
+                                          uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
   constexpr int NX = DX == 0 ? 5 : 4;   // active x tiles per env quad
   constexpr int NA = NQ * NX;           // active tiles
   constexpr int A0 = DX < 0 ? 1 : 0;    // first accumulator x tile
@@ -605,9 +605,9 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int s = SB + dyi * NC + c;
-      typename Elt<EL>::v8 w[t8::CT];
+      typename Elt<EL>::v8 w[CT];
 #pragma unroll
-      for (int ct = 0; ct < t8::CT; ++ct) {
+      for (int ct = 0; ct < CT; ++ct) {
         w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
         if (DX == 1 && c + TD >= NC) {  // the last TD steps of dy = +1 fetch the next conv's first steps
           const bool last = dyi == 2;
@@ -626,7 +626,7 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
       for (int j = 0; j < NA; ++j) {
         const int at = (j / NX) * 5 + A0 + (j % NX);
 #pragma unroll
-        for (int ct = 0; ct < t8::CT; ++ct)
+        for (int ct = 0; ct < CT; ++ct)
           acc[at][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[at][ct]);
         if (TOWER_ABLATE == 2)  // diagnostic only: no LDS A reads inside the loop
           afn[j] = afc[j];
@@ -647,11 +647,11 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       }
 #pragma unroll
-      for (int ct = 0; ct < t8::CT; ++ct) {
+      for (int ct = 0; ct < CT; ++ct) {
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
-      __builtin_amdgcn_sched_group_barrier(0x008, NA * t8::CT - NA - 2 * t8::CT, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NA * CT - NA - 2 * CT, 0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NA; ++j) afc[j] = afn[j];
@@ -662,9 +662,9 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 
 // the 8 k steps of a 1x1 conv on the 8-env image (centre tap: all 10 tiles, every row valid); always
 // the last conv of a launch, so the ring is not continued
-template <int EL, int NQ>
+template <int EL, int NQ, int CT = t8::CT>
 __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, const WNext& cur,
-                                              uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane) {
+                                              uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
   const int q = lane >> 4, key = lane & 15;
   const int base = key * TROWB, sw = key << 4;
   typename Elt<EL>::v8 afc[T8<NQ>::NRT], afn[T8<NQ>::NRT];
@@ -672,16 +672,16 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
   for (int j = 0; j < T8<NQ>::NRT; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + ((q << 4) ^ sw));
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    typename Elt<EL>::v8 w[t8::CT];
+    typename Elt<EL>::v8 w[CT];
 #pragma unroll
-    for (int ct = 0; ct < t8::CT; ++ct) {
+    for (int ct = 0; ct < CT; ++ct) {
       w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
       if (c + TD < 8) bq[ct][c % TD] = cur.ld(ct, c + TD, lane);
     }
 #pragma unroll
     for (int j = 0; j < T8<NQ>::NRT; ++j) {
 #pragma unroll
-      for (int ct = 0; ct < t8::CT; ++ct)
+      for (int ct = 0; ct < CT; ++ct)
         acc[j][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[j][ct]);
       if (c + 1 < 8)
         afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * 16 * TROWB + (((4 * (c + 1) + q) << 4) ^ sw));
@@ -693,9 +693,10 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
 
 // the first TD k steps of a pack into the ring (the kernel's first conv; later convs are fetched by
 // their predecessor)
-MZ_DEV void tower8_preload(uint4 (&bq)[t8::CT][TD], const WNext& p, int lane) {
+template <int CT = t8::CT>
+MZ_DEV void tower8_preload(uint4 (&bq)[CT][TD], const WNext& p, int lane) {
 #pragma unroll
-  for (int ct = 0; ct < t8::CT; ++ct)
+  for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
     for (int i = 0; i < TD; ++i) bq[ct][i] = p.ld(ct, i, lane);
 }
@@ -705,16 +706,16 @@ MZ_DEV void tower8_preload(uint4 (&bq)[t8::CT][TD], const WNext& p, int lane) {
 // ring holding `nxt`'s first k steps. D[pack channel 16 ct + 4q + i][row 16 rt + l16].
 // MODE 0: acc starts at bias; 1: bias + res (registers); 2: bias + act_bias[pos][act[env]].
 // bconv: the conv's bias (LDS for the tower convs, global for the prologue / epilogue convs).
-template <int EL, int NQ, int MODE, bool CENTER>
+template <int EL, int NQ, int MODE, bool CENTER, int CT = t8::CT>
 __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
                                            int ct0, const float* __restrict__ bconv, const float* __restrict__ actb,
                                            const int* acts, int A, const uint2 (&res)[T8<NQ>::NRT][t8::CT],
-                                           uint4 (&bq)[t8::CT][TD], f32x4 (&acc)[T8<NQ>::NRT][t8::CT], int lane,
+                                           uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane,
                                            int ci = 0) {
   const int q = lane >> 4, l16 = lane & 15;
   TSTAMP(2 + 6 * ci);
 #pragma unroll
-  for (int ct = 0; ct < t8::CT; ++ct) {
+  for (int ct = 0; ct < CT; ++ct) {
     const int n = (ct0 + ct) * 16 + 4 * q;
     const float4 b4 = *reinterpret_cast<const float4*>(bconv + n);
 #pragma unroll
@@ -733,27 +734,27 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
     }
   }
   if (CENTER) {
-    tower8_center<EL, NQ>(lds, cur, bq, acc, lane);
+    tower8_center<EL, NQ, CT>(lds, cur, bq, acc, lane);
   } else {
-    tower8_dx<EL, NQ, -1>(lds, cur, nxt, bq, acc, lane);
+    tower8_dx<EL, NQ, -1, CT>(lds, cur, nxt, bq, acc, lane);
     TSTAMP(3 + 6 * ci);
-    tower8_dx<EL, NQ, 0>(lds, cur, nxt, bq, acc, lane);
+    tower8_dx<EL, NQ, 0, CT>(lds, cur, nxt, bq, acc, lane);
     TSTAMP(4 + 6 * ci);
-    tower8_dx<EL, NQ, 1>(lds, cur, nxt, bq, acc, lane);
+    tower8_dx<EL, NQ, 1, CT>(lds, cur, nxt, bq, acc, lane);
   }
   TSTAMP(5 + 6 * ci);
 }
 
 // ReLU -> bf16 -> the image at channel nout + 16 (ct0 + ct) + 4q (8-byte stores, in place after a
 // barrier); SAVE: first lift the image's values there into res (the block input = conv2's residual)
-template <int EL, int NQ, bool SAVE>
-__device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, const f32x4 (&acc)[T8<NQ>::NRT][t8::CT],
+template <int EL, int NQ, bool SAVE, int CT = t8::CT>
+__device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, const f32x4 (&acc)[T8<NQ>::NRT][CT],
                                                  uint2 (&res)[T8<NQ>::NRT][t8::CT], int nout, int ct0, int lane) {
   const int q = lane >> 4, l16 = lane & 15;
 #pragma unroll
   for (int rt = 0; rt < T8<NQ>::NRT; ++rt)
 #pragma unroll
-    for (int ct = 0; ct < t8::CT; ++ct) {
+    for (int ct = 0; ct < CT; ++ct) {
       const int n = nout + (ct0 + ct) * 16 + 4 * q;
       uint2* p = reinterpret_cast<uint2*>(lds + toff(rt * 16 + l16, n >> 3) + ((n & 7) << 1));
       if (SAVE) res[rt][ct] = *p;
@@ -844,8 +845,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   // where each wave's ring goes after the last tower conv: the epilogue conv it runs
   WNext epi = first;
   if (a.x.epilogue == 1) epi = wnext(a.x.we1, 8, ctw);
-  if (a.x.epilogue == 2) epi = wave < 2 ? wnext(a.x.we3, TNS, (wave & 1) * t8::CT) : wnext(a.x.we1, 8, (wave & 1) * t8::CT);
-  const int ct_epi = a.x.epilogue == 2 ? (wave & 1) * t8::CT : ctw;
+  // (epilogue 2 reloads its own 2-tile ring: the last tower conv's continuation loads re-read `first`)
   if (tid < T8<NQ>::E) {
     const int b = env0 + (tid < nenv ? tid : 0);
     long long off = (long long)b * a.in_env_stride;
@@ -910,14 +910,19 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     tower_heads<EL, T8<NQ>::E, 4, true>(a, lds, 0, 1, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     return;
   }
-  if (a.x.epilogue == 2) {  // prediction: policy 3x3 (waves 0-1) -> [0,128), value 1x1 (waves 2-3) -> [128,256)
-    f32x4 acc[T8<NQ>::NRT][t8::CT];
-    if (wave < 2)
-      tower8_acc<EL, NQ, 0, false>(lds, epi, epi, ct_epi, a.x.be3, nullptr, nullptr, 0, res, bq, acc, lane);
-    else
-      tower8_acc<EL, NQ, 0, true>(lds, epi, epi, ct_epi, a.x.be1, nullptr, nullptr, 0, res, bq, acc, lane);
+  if (a.x.epilogue == 2) {  // prediction: policy 3x3 256->128 -> [0,128), value 1x1 256->128 -> [128,256),
+    // each wave 2 of the 8 column tiles of both (balanced: a 3x3 on two waves beside a 1x1 on the other
+    // two left two SIMDs idle for most of a conv)
+    const int ctp = wave * 2;
+    f32x4 accp[T8<NQ>::NRT][2], accv[T8<NQ>::NRT][2];
+    uint4 bq2[2][TD];
+    const WNext wp3 = wnext(a.x.we3, TNS, ctp), wv1 = wnext(a.x.we1, 8, ctp);
+    tower8_preload<2>(bq2, wp3, lane);
+    tower8_acc<EL, NQ, 0, false, 2>(lds, wp3, wv1, ctp, a.x.be3, nullptr, nullptr, 0, res, bq2, accp, lane);
+    tower8_acc<EL, NQ, 0, true, 2>(lds, wv1, wv1, ctp, a.x.be1, nullptr, nullptr, 0, res, bq2, accv, lane);
     __syncthreads();
-    tower8_writeback<EL, NQ, false>(lds, acc, res, wave < 2 ? 0 : 128, ct_epi, lane);
+    tower8_writeback<EL, NQ, false, 2>(lds, accp, res, 0, ctp, lane);
+    tower8_writeback<EL, NQ, false, 2>(lds, accv, res, 128, ctp, lane);
     __syncthreads();
     const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
     tower_heads<EL, T8<NQ>::E, 4, true>(a, lds, 0, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
@@ -1020,7 +1025,7 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
                      void* out, const void* wf16, const float* bias, int nblocks, int B, const mzba_tower_ext* ext,
                      hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && wf16 && bias && ext, -1);
-  const int plan = mzba_tower_plan(B);
+  const int plan = ext->plan ? ext->plan : mzba_tower_plan(B);
   MZ_CHECK_ARG(plan >= 1 && plan <= 3, -4);
   MZ_CHECK_ARG(plan == 1 || nblocks <= T8_MAX_BLOCKS, -5);  // tower8: bias table in LDS
   const mzba_tower_ext& x = *ext;

@@ -109,7 +109,7 @@ class TowerExt(ctypes.Structure):
                 ("lw", P * 2), ("lb", P * 2), ("lO", I * 2),
                 ("logits", P * 2), ("dec", P * 2),
                 ("pool", P), ("pool_env_stride", LL), ("pool_slot", I),
-                ("smin", F), ("smax", F), ("tree", ctypes.POINTER(TreeStep)), ("elem", I)]
+                ("smin", F), ("smax", F), ("tree", ctypes.POINTER(TreeStep)), ("elem", I), ("plan", I)]
 
 
 # entry points that return something other than a status code

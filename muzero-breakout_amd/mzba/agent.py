@@ -348,6 +348,7 @@ class NetRunner:
         p, f = self.p, self.p.fused
         x = L.TowerExt()
         x.epilogue = epilogue
+        x.plan = self.tower_plan  # the kernel this runner was built for, whatever the global variant now says
         x.smin, x.smax = float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"])
         if epilogue == 1:
             d16 = f.get("dyn16")
