@@ -140,6 +140,8 @@ int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const vo
  * band), 160 rows x Cout, weights in the tower packing (agent.pack_tower_conv, + 8 KB pad).
  * out = [relu](conv(in) + bias [+ res]); NHWC bf16, env strides 320*Cin / 320*Cout; out may alias res. */
 int mzba_conv_band_supported(int H, int W, int Cin, int Cout, int ks);
+/* band width of mzba_conv_band: 5 output columns per workgroup (default; two workgroups per CU) or 10 */
+int mzba_conv_band_set_xt(int xt);
 int mzba_conv_band(const void* in, const void* wf16, const float* bias, const void* res, void* out, int B, int H,
                    int W, int Cin, int Cout, int relu, hipStream_t stream);
 

@@ -24,14 +24,17 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 constexpr int BH = 16, BW = 20;      // image
-constexpr int XT = 10;               // output columns per workgroup
-constexpr int NSRC = XT + 2;         // staged source columns (with the halo)
 constexpr int BNT = 256;             // 4 waves
-constexpr int TDB = 4;               // weight ring depth (k steps)
 constexpr unsigned long long SIG = 0x93f5a4260ce8b7d1ull;  // nibble j: image row of B column j
 constexpr unsigned long long KEY = 0x35a0e1879df426bcull;  // nibble y: swizzle key of image row y
 
 MZ_DEV int nib(unsigned long long t, int i) { return (int)((t >> (4 * i)) & 15); }
+
+// 16-B weight fragment of k step `step` of column tile `ct` (TNS k steps per tile), this lane
+template <int TNS>
+MZ_DEV uint4 wld(__amdgpu_buffer_rsrc_t rs, int ct, int step, int lane) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (ct * TNS + step) * 1024, 0));
+}
 
 struct BandArgs {
   const bf16_t* in;   // [B][320][Cin]
@@ -42,8 +45,10 @@ struct BandArgs {
   int B, relu;
 };
 
-template <int CIN, int COUT>
+template <int CIN, int COUT, int XT>
 struct BandGeo {
+  static constexpr int TDB = XT == 10 ? 4 : 2;     // weight ring depth (k steps; 2 at two workgroups per CU)
+  static constexpr int NSRC = XT + 2;              // staged source columns (with the halo)
   static constexpr int RB = CIN * 2;               // LDS bytes per source row
   static constexpr int NCH = CIN / 8;              // 16-B chunks per source row
   static constexpr int NC = CIN / 32;              // k steps per tap
@@ -57,11 +62,12 @@ struct BandGeo {
 };
 
 // the 3 dy x NC k steps of column shift DX
-template <int CIN, int COUT, int DX>
-__device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, const uint4* const (&wp)[COUT / 64],
-                                        uint4 (&bq)[COUT / 64][TDB], f32x4 (&acc)[XT][COUT / 64], int lane) {
-  using G = BandGeo<CIN, COUT>;
-  constexpr int CTW = G::CTW, NC = G::NC;
+template <int CIN, int COUT, int XT, int DX>
+__device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, __amdgpu_buffer_rsrc_t wrs,
+                                        uint4 (&bq)[COUT / 64][BandGeo<CIN, COUT, XT>::TDB], f32x4 (&acc)[XT][COUT / 64],
+                                        int lane) {
+  using G = BandGeo<CIN, COUT, XT>;
+  constexpr int CTW = G::CTW, NC = G::NC, TDB = G::TDB;
   constexpr int SB = (DX + 1) * 3 * NC;
   const int q = lane >> 4, ys = nib(SIG, lane & 15);
   auto rows = [&](int dy, int& base, int& tst, int& sw) {
@@ -87,7 +93,7 @@ __device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, const u
 #pragma unroll
       for (int ct = 0; ct < CTW; ++ct) {
         w[ct] = __builtin_bit_cast(bf16x8, bq[ct][c % TDB]);
-        bq[ct][c % TDB] = wp[ct][(size_t)(s + TDB) * 64];
+        bq[ct][c % TDB] = wld<G::TNS>(wrs, ct, s + TDB, lane);
       }
 #pragma unroll
       for (int t = 0; t < XT; ++t) {
@@ -121,18 +127,21 @@ __device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, const u
   }
 }
 
-template <int CIN, int COUT>
-__global__ __launch_bounds__(BNT, 1) void band_conv_kernel(BandArgs a) {
-  using G = BandGeo<CIN, COUT>;
+// XT output columns per workgroup (10: one workgroup per CU at Cin 256; 5: two per CU, so one
+// workgroup's band staging / epilogue runs beside the other's MFMAs)
+template <int CIN, int COUT, int XT>
+__global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandArgs a) {
+  using G = BandGeo<CIN, COUT, XT>;
+  constexpr int NSRC = G::NSRC, NB = BW / XT;
   constexpr int CTW = G::CTW;
   __shared__ __attribute__((aligned(16))) uint8_t lds[G::BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x >> 1, x0 = (blockIdx.x & 1) * XT;
+  const int b = blockIdx.x / NB, x0 = (blockIdx.x % NB) * XT;
   // stage the band: NSRC*16 rows x NCH chunks (UB loads in flight per thread), then the zero block
   {
     constexpr int N = NSRC * 16 * G::NCH;
     constexpr int UB = N % (8 * BNT) == 0 ? 8 : 4;
-    static_assert(N % (UB * BNT) == 0, "staging batches");
+    constexpr bool EXACT = N % (UB * BNT) == 0;  // else the last batch is partial (guarded)
     const bf16_t* src = a.in + (size_t)b * BH * BW * CIN;
 #pragma unroll 1
     for (int i0 = 0; i0 < N; i0 += UB * BNT) {
@@ -142,36 +151,39 @@ __global__ __launch_bounds__(BNT, 1) void band_conv_kernel(BandArgs a) {
         const int i = i0 + u * BNT + tid;
         const int row = i / G::NCH, ch = i % G::NCH;
         const int x = x0 - 1 + (row >> 4), y = row & 15;
-        const bool ok = (unsigned)x < (unsigned)BW;
-        v[u] = *reinterpret_cast<const uint4*>(src + ((size_t)(y * BW + (ok ? x : 0)) * CIN + ch * 8));
+        const bool ok = (unsigned)x < (unsigned)BW && (EXACT || i < N);
+        v[u] = *reinterpret_cast<const uint4*>(src + ((size_t)(y * BW + (ok ? x : 0)) * CIN + (ok ? ch * 8 : 0)));
         if (!ok) v[u] = make_uint4(0, 0, 0, 0);
       }
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
         const int i = i0 + u * BNT + tid;
         const int row = i / G::NCH, ch = i % G::NCH;
-        *reinterpret_cast<uint4*>(lds + row * G::RB + ((ch ^ nib(KEY, row & 15)) << 4)) = v[u];
+        if (EXACT || i < N) *reinterpret_cast<uint4*>(lds + row * G::RB + ((ch ^ nib(KEY, row & 15)) << 4)) = v[u];
       }
     }
     for (int i = tid; i < 16 * G::NCH; i += BNT) *reinterpret_cast<uint4*>(lds + G::LZ + i * 16) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
-  const uint4* wp[CTW];
+  // this wave's column tiles of the weight pack through a wave-uniform buffer resource (one VGPR for
+  // the lane offset; the (tile, step) offset in an SGPR)
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint4*>(reinterpret_cast<const uint4*>(a.wf) + (size_t)__builtin_amdgcn_readfirstlane(wave * CTW) * G::TNS * 64),
+      0, 0x7fffffff, 0x00020000);
+  constexpr int TDB = G::TDB;
   uint4 bq[CTW][TDB];
 #pragma unroll
-  for (int ct = 0; ct < CTW; ++ct) {
-    wp[ct] = reinterpret_cast<const uint4*>(a.wf) + (size_t)(wave * CTW + ct) * G::TNS * 64 + lane;
+  for (int ct = 0; ct < CTW; ++ct)
 #pragma unroll
-    for (int i = 0; i < TDB; ++i) bq[ct][i] = wp[ct][(size_t)i * 64];
-  }
+    for (int i = 0; i < TDB; ++i) bq[ct][i] = wld<G::TNS>(wrs, ct, i, lane);
   f32x4 acc[XT][CTW];
 #pragma unroll
   for (int t = 0; t < XT; ++t)
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  band_dx<CIN, COUT, -1>(lds, wp, bq, acc, lane);
-  band_dx<CIN, COUT, 0>(lds, wp, bq, acc, lane);
-  band_dx<CIN, COUT, 1>(lds, wp, bq, acc, lane);
+  band_dx<CIN, COUT, XT, -1>(lds, wrs, bq, acc, lane);
+  band_dx<CIN, COUT, XT, 0>(lds, wrs, bq, acc, lane);
+  band_dx<CIN, COUT, XT, 1>(lds, wrs, bq, acc, lane);
   __syncthreads();  // the band is no longer read
   // output tile in LDS: row 16 t + y, 16-B chunks swizzled by KEY[y]
   constexpr int ONCH = COUT / 8;
@@ -218,7 +230,18 @@ __global__ __launch_bounds__(BNT, 1) void band_conv_kernel(BandArgs a) {
 
 }  // namespace
 
+static int g_band_xt = 5;  // output columns per workgroup (mzba_conv_band_set_xt)
+
 extern "C" {
+
+// band width (output columns per workgroup): 5 (default: two workgroups per CU, one's band staging and
+// epilogue beside the other's MFMAs; B = 4096, isolated: 256->256 1247 -> 1218 us, 128->128 423 -> 378,
+// 128->256 787 -> 691, profiles/r02/band_xt/) or 10 (one workgroup per CU at Cin 256)
+int mzba_conv_band_set_xt(int xt) {
+  if (xt != 5 && xt != 10) return -1;
+  g_band_xt = xt;
+  return 0;
+}
 
 int mzba_conv_band_supported(int H, int W, int Cin, int Cout, int ks) {
   return H == BH && W == BW && ks == 3 && (Cin == 128 || Cin == 256) && (Cout == 128 || Cout == 256);
@@ -230,11 +253,18 @@ int mzba_conv_band(const void* in, const void* wf16, const float* bias, const vo
                    int W, int Cin, int Cout, int relu, hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && in && wf16 && bias && out && in != out && mzba_conv_band_supported(H, W, Cin, Cout, 3), -1);
   BandArgs a{(const bf16_t*)in, (const bf16_t*)wf16, bias, (const bf16_t*)res, (bf16_t*)out, B, relu};
-  dim3 grid(2 * B);
-  if (Cin == 256 && Cout == 256) hipLaunchKernelGGL((band_conv_kernel<256, 256>), grid, dim3(BNT), 0, stream, a);
-  else if (Cin == 128 && Cout == 256) hipLaunchKernelGGL((band_conv_kernel<128, 256>), grid, dim3(BNT), 0, stream, a);
-  else if (Cin == 128 && Cout == 128) hipLaunchKernelGGL((band_conv_kernel<128, 128>), grid, dim3(BNT), 0, stream, a);
-  else hipLaunchKernelGGL((band_conv_kernel<256, 128>), grid, dim3(BNT), 0, stream, a);
+  const bool narrow = g_band_xt == 5;
+  dim3 grid((narrow ? 4 : 2) * B);
+#define MZ_BAND(CI, CO)                                                                                   \
+  do {                                                                                                     \
+    if (narrow) hipLaunchKernelGGL((band_conv_kernel<CI, CO, 5>), grid, dim3(BNT), 0, stream, a);          \
+    else hipLaunchKernelGGL((band_conv_kernel<CI, CO, 10>), grid, dim3(BNT), 0, stream, a);                \
+  } while (0)
+  if (Cin == 256 && Cout == 256) MZ_BAND(256, 256);
+  else if (Cin == 128 && Cout == 256) MZ_BAND(128, 256);
+  else if (Cin == 128 && Cout == 128) MZ_BAND(128, 128);
+  else MZ_BAND(256, 128);
+#undef MZ_BAND
   MZ_LAUNCH_CHECK();
   return 0;
 }

@@ -42,6 +42,7 @@ SIGNATURES = {
     "mzba_tower_ws_bytes": [I],
     "mzba_tower_fused": [P, LL, P, LL, P, P, P, I, I, P, P],
     "mzba_conv_band_supported": [I, I, I, I, I],
+    "mzba_conv_band_set_xt": [I],
     "mzba_replay_plan": [P, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P],
     "mzba_replay_write": [P, P, P, P, P, P, P, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, I, I, I, I, P, P],
     "mzba_replay_states": [P, P, I, P, P, I, I, P],

@@ -391,8 +391,10 @@ def test_fused_bf16_steps_vs_torch_fp32(B, variant):
 
 @pytest.mark.parametrize("Cin,Cout,resid,relu", [(128, 128, False, True), (128, 256, False, False),
                                                    (256, 256, True, True), (256, 128, False, True)])
-def test_band_conv_vs_torch_fp32(Cin, Cout, resid, relu):
-    """16x20 band kernel vs a plain torch fp32 conv (bf16-rounded operands), incl. residual + ReLU."""
+@pytest.mark.parametrize("xt", [10, 5])
+def test_band_conv_vs_torch_fp32(Cin, Cout, resid, relu, xt):
+    """16x20 band kernel (10- and 5-column bands) vs a plain torch fp32 conv (bf16-rounded operands),
+    incl. residual + ReLU."""
     from mzba import _lib as L
     from mzba.agent import pack_tower_conv, LAT_PAD_ELEMS
     B, H, W = 5, 16, 20
@@ -409,8 +411,12 @@ def test_band_conv_vs_torch_fp32(Cin, Cout, resid, relu):
              .to(torch.bfloat16).cuda(), b=b.cuda(), r=res.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda())
     out = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device="cuda")
     assert L.lib().mzba_conv_band_supported(H, W, Cin, Cout, 3)
-    L.call("mzba_conv_band", L.ptr(d["x"]), L.ptr(d["w"]), L.ptr(d["b"]), L.ptr(d["r"]) if resid else None,
-           L.ptr(out), B, H, W, Cin, Cout, 1 if relu else 0, L.stream())
+    L.call("mzba_conv_band_set_xt", xt)
+    try:
+        L.call("mzba_conv_band", L.ptr(d["x"]), L.ptr(d["w"]), L.ptr(d["b"]), L.ptr(d["r"]) if resid else None,
+               L.ptr(out), B, H, W, Cin, Cout, 1 if relu else 0, L.stream())
+    finally:
+        L.call("mzba_conv_band_set_xt", 5)
     got = out.float().cpu().permute(0, 3, 1, 2)
     err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
     assert err < 1e-2, err
