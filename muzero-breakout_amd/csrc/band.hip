@@ -47,10 +47,16 @@ struct BandArgs {
 
 template <int CIN, int COUT, int XT>
 struct BandGeo {
-  static constexpr int TDB = XT == 10 ? 4 : 2;     // weight ring depth (k steps; 2 at two workgroups per CU)
+  // weight ring depth (k steps; 2 at two workgroups per CU). Ring slot = step % TDB is taken as
+  // c % TDB inside a tap, so TDB must divide the NC = Cin / 32 steps of a tap
+  static constexpr int TDB = (XT == 10 ? 4 : 2) < CIN / 32 ? (XT == 10 ? 4 : 2) : CIN / 32;
+  static_assert((CIN / 32) % TDB == 0, "ring slot restarts at every tap");
   static constexpr int NSRC = XT + 2;              // staged source columns (with the halo)
-  static constexpr int RB = CIN * 2;               // LDS bytes per source row
-  static constexpr int NCH = CIN / 8;              // 16-B chunks per source row
+  // LDS bytes per source row: at Cin 64 the row is padded to 128 channels, so a chunk index XORed
+  // with the 4-bit row key stays inside the row (staging and reads use the same mapping; the pad
+  // chunks are never read)
+  static constexpr int RB = (CIN < 128 ? 128 : CIN) * 2;
+  static constexpr int NCH = CIN / 8;              // 16-B chunks per source row (staged)
   static constexpr int NC = CIN / 32;              // k steps per tap
   static constexpr int TNS = 9 * NC;               // k steps per channel tile
   static constexpr int CTW = COUT / 64;            // 16-channel tiles per wave
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
         if (EXACT || i < N) *reinterpret_cast<uint4*>(lds + row * G::RB + ((ch ^ nib(KEY, row & 15)) << 4)) = v[u];
       }
     }
-    for (int i = tid; i < 16 * G::NCH; i += BNT) *reinterpret_cast<uint4*>(lds + G::LZ + i * 16) = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < G::RB; i += BNT) *reinterpret_cast<uint4*>(lds + G::LZ + i * 16) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
   // this wave's column tiles of the weight pack through a wave-uniform buffer resource (one VGPR for
@@ -244,7 +250,8 @@ int mzba_conv_band_set_xt(int xt) {
 }
 
 int mzba_conv_band_supported(int H, int W, int Cin, int Cout, int ks) {
-  return H == BH && W == BW && ks == 3 && (Cin == 128 || Cin == 256) && (Cout == 128 || Cout == 256);
+  return H == BH && W == BW && ks == 3 && ((Cin == 64 && Cout == 128) || ((Cin == 128 || Cin == 256) &&
+                                                                           (Cout == 128 || Cout == 256)));
 }
 
 // 3x3 conv, stride 1, pad 1, on B images of 16x20 (NHWC bf16, env stride 320*Cin / 320*Cout):
@@ -263,6 +270,7 @@ int mzba_conv_band(const void* in, const void* wf16, const float* bias, const vo
   if (Cin == 256 && Cout == 256) MZ_BAND(256, 256);
   else if (Cin == 128 && Cout == 256) MZ_BAND(128, 256);
   else if (Cin == 128 && Cout == 128) MZ_BAND(128, 128);
+  else if (Cin == 64) MZ_BAND(64, 128);
   else MZ_BAND(256, 128);
 #undef MZ_BAND
   MZ_LAUNCH_CHECK();

@@ -189,7 +189,7 @@ class PackedNets:
         if self.dtype == "bf16" and cout % 32 == 0 and cin_p in (64, 128, 256):
             layer["wf"] = torch.tensor(pack_lat(wp.reshape(cout, -1), cout, k, cin_p),
                                        dtype=torch.float32).to(self.tdt).to(self.device)
-        if band and self.dtype == "bf16" and k == 3 and cin in (128, 256) and cout in (128, 256):
+        if band and self.dtype == "bf16" and k == 3 and L.lib().mzba_conv_band_supported(16, 20, cin, cout, 3):
             # representation convs at full resolution: the band kernel's packing (tower order)
             layer["wt"] = torch.tensor(np.concatenate([pack_tower_conv(w), np.zeros(LAT_PAD_ELEMS)]),
                                        dtype=torch.float32).to(self.tdt).to(self.device)

@@ -389,7 +389,7 @@ def test_fused_bf16_steps_vs_torch_fp32(B, variant):
         assert err < 2e-2, (nm, err)
 
 
-@pytest.mark.parametrize("Cin,Cout,resid,relu", [(128, 128, False, True), (128, 256, False, False),
+@pytest.mark.parametrize("Cin,Cout,resid,relu", [(64, 128, False, False), (128, 128, False, True), (128, 256, False, False),
                                                    (256, 256, True, True), (256, 128, False, True)])
 @pytest.mark.parametrize("xt", [10, 5])
 def test_band_conv_vs_torch_fp32(Cin, Cout, resid, relu, xt):
