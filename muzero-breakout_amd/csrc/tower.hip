@@ -163,11 +163,11 @@ MZ_DEV int row8(int e, int p) { return (e >> 2) * 80 + (p % 5) * 16 + (p / 5) * 
 
 // A-row addressing of this lane for latent row shift dy: byte offset of its row in source
 // tile 0 (or of its zero-block row), the per-tile stride (0 for zero rows) and the swizzle key
-MZ_DEV void tap_rows(int srcimg, int y, int e, int dy, int& base, int& tstride, int& sw) {
+MZ_DEV void tap_rows(int srcimg, int y, int e, int dy, int& base, int& tstride, int& sw, int zblk = LDS_Z) {
   const int yy = y + dy;
   const bool ok = (unsigned)yy < 4u;
   const int key = ((yy & 3) << 2) | e;
-  base = ok ? srcimg + key * TROWB : LDS_Z + key * TROWB;
+  base = ok ? srcimg + key * TROWB : zblk + key * TROWB;
   tstride = ok ? 16 * TROWB : 0;
   sw = key << 4;
 }
@@ -591,7 +591,7 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
   constexpr int SB = (DX + 1) * 24;     // first k step of this column shift
   const int q = lane >> 4, y = (lane & 15) >> 2, e = lane & 3;
   int base, tst, sw;
-  tap_rows(S0 * 16 * TROWB, y, e, -1, base, tst, sw);
+  tap_rows(S0 * 16 * TROWB, y, e, -1, base, tst, sw, T8<NQ>::LZ);  // this image's own zero block
   // active tile j: quad j / NX, x tile j % NX -> source tile index (in 16-row tiles from S0)
   auto soff = [&](int j, int b, int ts) { return b + ((j / NX) * 5 + (j % NX)) * ts; };
   typename Elt<EL>::v8 afc[NA], afn[NA];
@@ -601,7 +601,7 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 #pragma unroll 1
   for (int dyi = 0; dyi < 3; ++dyi) {
     int nbase, ntst, nsw;
-    tap_rows(S0 * 16 * TROWB, y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+    tap_rows(S0 * 16 * TROWB, y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw, T8<NQ>::LZ);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int s = SB + dyi * NC + c;
