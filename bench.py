@@ -311,8 +311,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # production: one rank per GPU over RCCL. Rehearsal on a one-GPU box (MZBA_DIST_REHEARSAL=1):
+        # every rank on cuda:0, gloo collectives — the same code path minus RCCL itself
+        if os.environ.get("MZBA_DIST_REHEARSAL") == "1":
+            local = 0
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.workload == "env":
         return run_env(args, world, rank, local)
     if args.workload == "learner":

@@ -83,8 +83,15 @@ class TrajectoryGather:
         n = t1 - t0
         pack_records(rec, t0, t1, self.slab[:n])
         if self.ws > 1:
-            gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
-            dist.gather(self.slab, gl, dst=0)
+            if dist.get_backend() == "gloo" and self.device.type == "cuda":
+                # gloo gathers host tensors only (CPU tests, and bench.py's one-GPU rehearsal)
+                gl = [torch.empty_like(self.slab, device="cpu") for _ in range(self.ws)] if self.rank == 0 else None
+                dist.gather(self.slab.cpu(), gl, dst=0)
+                if self.rank == 0:
+                    self.gathered.copy_(torch.stack(gl))
+            else:
+                gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
+                dist.gather(self.slab, gl, dst=0)
         elif self.rank == 0:
             self.gathered[0].copy_(self.slab)
         if self.rank == 0:
