@@ -243,6 +243,14 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
                      void* out, const void* wf16, const float* bias, int nblocks, int B,
                      const mzba_tower_ext* ext, hipStream_t stream);
 
+/* Representation tail in one launch (networks.py:86-99, 271-280, 314-328): AvgPool2d of the 16x20
+ * activations after the last full-resolution block (in [B][320][256] bf16), nblocks ResidualBlock(256)
+ * at 8x10 (wf16: their 2 nblocks convs BN-folded in the tower packing, back to back + 8 KB pad; bias
+ * [2 nblocks][256] f32), AvgPool2d to 4x5, _scale_state; the root latent to out [B][20][256] bf16 and,
+ * when pool != NULL, to pool + b * pool_env_stride. nblocks <= 24. */
+int mzba_rep_tail(const void* in, void* out, void* pool, long long pool_env_stride, const void* wf16,
+                  const float* bias, int nblocks, int B, hipStream_t stream);
+
 /* nn.AvgPool2d(2, 2) (networks.py:44), NHWC. */
 int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream);
 

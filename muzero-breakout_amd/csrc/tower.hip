@@ -161,6 +161,18 @@ constexpr int NT = 256, CT = 4;
 MZ_DEV int row8(int e, int p) { return (e >> 2) * 80 + (p % 5) * 16 + (p / 5) * 4 + (e & 3); }
 }  // namespace t8
 
+// Image geometry of the 4-wave kernels: GROUPS groups of TX 16-row tiles; a tile is one latent
+// column x of EG envs x YS latent rows (row in tile = EG * y + e); a 3x3 tap (dy, dx) maps tile x to
+// tile x + dx whole and shifts rows by EG * dy; rows leaving y = 0..YS-1 read the zero block (LZ) at
+// the row key ((y + dy) mod YS) * EG + e, so every ds_read_b128 lane group hits 16 distinct keys.
+template <int NQ>
+struct Geo45 {  // the 4x5 latent: NQ env quads, 5 tiles each (tower8_kernel)
+  static constexpr int GROUPS = NQ, TX = 5, EG = 4, YS = 4, LZ = T8<NQ>::LZ;
+};
+struct Geo810 {  // the 8x10 latent of the representation tail: 2 envs, 10 tiles (rep_tail_kernel)
+  static constexpr int GROUPS = 1, TX = 10, EG = 2, YS = 8, LZ = 160 * TROWB;
+};
+
 // A-row addressing of this lane for latent row shift dy: byte offset of its row in source
 // tile 0 (or of its zero-block row), the per-tile stride (0 for zero rows) and the swizzle key
 MZ_DEV void tap_rows(int srcimg, int y, int e, int dy, int& base, int& tstride, int& sw, int zblk = LDS_Z) {
@@ -581,19 +593,30 @@ MZ_DEV WNext wnext(const void* w, int tns, int ct0) {
 // next pack at this wave's first column tile + lane, `tnsn` k steps per tile), so those loads fly
 // through the epilogue and both barriers (a workgroup barrier waits for LDS, not for vmcnt) and the
 // next conv's first MFMAs find their weights in registers.
-template <int EL, int NQ, int DX, int CT = t8::CT>
+template <int EL, int NQ, int DX, int CT = t8::CT, class G = Geo45<NQ>>
 __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
                                           uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
-  constexpr int NX = DX == 0 ? 5 : 4;   // active x tiles per env quad
-  constexpr int NA = NQ * NX;           // active tiles
-  constexpr int A0 = DX < 0 ? 1 : 0;    // first accumulator x tile
-  constexpr int S0 = DX > 0 ? 1 : 0;    // first source x tile
-  constexpr int SB = (DX + 1) * 24;     // first k step of this column shift
-  const int q = lane >> 4, y = (lane & 15) >> 2, e = lane & 3;
+  static_assert(G::GROUPS * G::TX == T8<NQ>::NRT, "geometry and accumulator tiles");
+  constexpr int TX = G::TX, EG = G::EG, YS = G::YS;
+  constexpr int NX = DX == 0 ? TX : TX - 1;  // active x tiles per group
+  constexpr int NA = G::GROUPS * NX;         // active tiles
+  constexpr int A0 = DX < 0 ? 1 : 0;         // first accumulator x tile
+  constexpr int S0 = DX > 0 ? 1 : 0;         // first source x tile
+  constexpr int SB = (DX + 1) * 24;          // first k step of this column shift
+  const int q = lane >> 4, y = (lane & 15) / EG, e = lane & (EG - 1);
+  // A-row addressing of this lane for latent row shift dy (zero rows: this image's own zero block)
+  auto rows = [&](int dy, int& b, int& ts, int& w) {
+    const int yy = y + dy;
+    const bool ok = (unsigned)yy < (unsigned)YS;
+    const int key = (yy & (YS - 1)) * EG + e;
+    b = ok ? S0 * 16 * TROWB + key * TROWB : G::LZ + key * TROWB;
+    ts = ok ? 16 * TROWB : 0;
+    w = key << 4;
+  };
   int base, tst, sw;
-  tap_rows(S0 * 16 * TROWB, y, e, -1, base, tst, sw, T8<NQ>::LZ);  // this image's own zero block
-  // active tile j: quad j / NX, x tile j % NX -> source tile index (in 16-row tiles from S0)
-  auto soff = [&](int j, int b, int ts) { return b + ((j / NX) * 5 + (j % NX)) * ts; };
+  rows(-1, base, tst, sw);
+  // active tile j: group j / NX, x tile j % NX -> source tile index (in 16-row tiles from S0)
+  auto soff = [&](int j, int b, int ts) { return b + ((j / NX) * TX + (j % NX)) * ts; };
   typename Elt<EL>::v8 afc[NA], afn[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, base, tst) + ((q << 4) ^ sw));
@@ -601,7 +624,7 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
 #pragma unroll 1
   for (int dyi = 0; dyi < 3; ++dyi) {
     int nbase, ntst, nsw;
-    tap_rows(S0 * 16 * TROWB, y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw, T8<NQ>::LZ);
+    rows(dyi < 2 ? dyi : 1, nbase, ntst, nsw);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int s = SB + dyi * NC + c;
@@ -624,7 +647,7 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
       }
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
-        const int at = (j / NX) * 5 + A0 + (j % NX);
+        const int at = (j / NX) * TX + A0 + (j % NX);
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct)
           acc[at][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[at][ct]);
@@ -706,7 +729,7 @@ MZ_DEV void tower8_preload(uint4 (&bq)[CT][TD], const WNext& p, int lane) {
 // ring holding `nxt`'s first k steps. D[pack channel 16 ct + 4q + i][row 16 rt + l16].
 // MODE 0: acc starts at bias; 1: bias + res (registers); 2: bias + act_bias[pos][act[env]].
 // bconv: the conv's bias (LDS for the tower convs, global for the prologue / epilogue convs).
-template <int EL, int NQ, int MODE, bool CENTER, int CT = t8::CT>
+template <int EL, int NQ, int MODE, bool CENTER, int CT = t8::CT, class G = Geo45<NQ>>
 __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
                                            int ct0, const float* __restrict__ bconv, const float* __restrict__ actb,
                                            const int* acts, int A, const uint2 (&res)[T8<NQ>::NRT][t8::CT],
@@ -736,11 +759,11 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
   if (CENTER) {
     tower8_center<EL, NQ, CT>(lds, cur, bq, acc, lane);
   } else {
-    tower8_dx<EL, NQ, -1, CT>(lds, cur, nxt, bq, acc, lane);
+    tower8_dx<EL, NQ, -1, CT, G>(lds, cur, nxt, bq, acc, lane);
     TSTAMP(3 + 6 * ci);
-    tower8_dx<EL, NQ, 0, CT>(lds, cur, nxt, bq, acc, lane);
+    tower8_dx<EL, NQ, 0, CT, G>(lds, cur, nxt, bq, acc, lane);
     TSTAMP(4 + 6 * ci);
-    tower8_dx<EL, NQ, 1, CT>(lds, cur, nxt, bq, acc, lane);
+    tower8_dx<EL, NQ, 1, CT, G>(lds, cur, nxt, bq, acc, lane);
   }
   TSTAMP(5 + 6 * ci);
 }
@@ -800,12 +823,12 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
 }
 
 // one residual-tower conv (in place): k loop, barrier, write back, barrier
-template <int EL, int NQ, bool RESID>
+template <int EL, int NQ, bool RESID, class G = Geo45<NQ>>
 __device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt, int ct0,
                                             const float* __restrict__ bconv, uint2 (&res)[T8<NQ>::NRT][t8::CT],
                                             uint4 (&bq)[t8::CT][TD], int lane, int ci) {
   f32x4 acc[T8<NQ>::NRT][t8::CT];
-  tower8_acc<EL, NQ, RESID ? 1 : 0, false>(lds, cur, nxt, ct0, bconv, nullptr, nullptr, 0, res, bq, acc, lane, ci);
+  tower8_acc<EL, NQ, RESID ? 1 : 0, false, t8::CT, G>(lds, cur, nxt, ct0, bconv, nullptr, nullptr, 0, res, bq, acc, lane, ci);
   __syncthreads();  // every wave has read the whole image
   TSTAMP(6 + 6 * ci);
   tower8_writeback<EL, NQ, !RESID>(lds, acc, res, 0, ct0, lane);
@@ -947,6 +970,125 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   TSTAMP_END();
 }
 
+// ---------------------------------------------------------------------------------------------
+// Representation tail (networks.py:86-99 after the 16x20 blocks, :271-280, _scale_state :314-328) in
+// ONE launch: AvgPool2d 16x20 -> 8x10 while staging, nblocks ResidualBlock(256) at 8x10 with the
+// activations LDS-resident, AvgPool2d -> 4x5 and the per-env min-max scale in the epilogue; the root
+// latent goes to `out` and to node-pool slot 0. A workgroup owns 2 envs = 160 rows x 256 channels
+// (Geo810: a 16-row tile is one latent column x of 2 envs x 8 rows) and runs tower8_kernel's k loop,
+// weight ring and in-place convs. Pooling follows avgpool2_kernel's op order ((a + b) + c) + d, / 4,
+// bf16; the scale follows scale_state_kernel: the unfused launch sequence, fused.
+struct RepTailArgs {
+  const bf16_t* in;          // [B][320][256]: the activations after the last 16x20 block
+  bf16_t* out;               // [B][20][256] scaled root latent
+  bf16_t* pool;              // optional: env b's slot 0 at pool + b * pool_env_stride
+  long long pool_env_stride;
+  const bf16_t* wf;          // 2 nblocks convs in the tower packing, back to back (+ pad)
+  const float* bias;         // [2 nblocks][256]
+  int nblocks, B;
+};
+
+__global__ __launch_bounds__(t8::NT, 1) void rep_tail_kernel(RepTailArgs a) {
+  using G = Geo810;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::LZ + 16 * TROWB];  // image | 16 zero rows
+  __shared__ float mm[2][2][2];                                             // [env][wave of env][min, max]
+  extern __shared__ __attribute__((aligned(16))) float biasl[];             // [2 nblocks][256]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int env0 = blockIdx.x * 2;
+  const int nenv = min(2, a.B - env0);
+  const int ctw = wave * t8::CT;
+  const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
+  constexpr size_t WCONV = (size_t)16 * TNS * 64;
+  uint4 bq[t8::CT][TD];
+  tower8_preload(bq, wnext(a.wf, TNS, ctw), lane);  // flies while the input is pooled and staged
+  {
+    const int n4 = a.nblocks * 2 * TC / 4;
+    for (int i = tid; i < n4; i += t8::NT) reinterpret_cast<float4*>(biasl)[i] = reinterpret_cast<const float4*>(a.bias)[i];
+  }
+  // stage: 2 envs x 80 pooled positions x 32 chunks, 4 per thread per batch (4 x 16-B loads each)
+#pragma unroll 1
+  for (int i0 = 0; i0 < 2 * 80 * 32; i0 += 4 * t8::NT) {
+    uint4 v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * t8::NT + tid, e = i / 2560, r = i - e * 2560, pp = r >> 5, c = r & 31;
+      const int yo = pp / 10, xo = pp - yo * 10;
+      const int eb = env0 + (e < nenv ? e : 0);
+      const bf16_t* src = a.in + (size_t)eb * 320 * TC + (size_t)(2 * yo * 20 + 2 * xo) * TC + c * 8;
+      v[u][0] = *reinterpret_cast<const uint4*>(src);
+      v[u][1] = *reinterpret_cast<const uint4*>(src + TC);
+      v[u][2] = *reinterpret_cast<const uint4*>(src + 20 * TC);
+      v[u][3] = *reinterpret_cast<const uint4*>(src + 21 * TC);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * t8::NT + tid, e = i / 2560, r = i - e * 2560, pp = r >> 5, c = r & 31;
+      const int yo = pp / 10, xo = pp - yo * 10;
+      float f0[8], f1[8], f2[8], f3[8];
+      unpack8<0>(v[u][0], f0); unpack8<0>(v[u][1], f1); unpack8<0>(v[u][2], f2); unpack8<0>(v[u][3], f3);
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (((f0[j] + f1[j]) + f2[j]) + f3[j]) / 4.0f;
+      uint4 w = make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]),
+                           pack_bf16x2(o[6], o[7]));
+      if (e >= nenv) w = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(lds + toff(xo * 16 + yo * 2 + e, c)) = w;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) *reinterpret_cast<uint4*>(lds + G::LZ + (u * t8::NT + tid) * 16) = make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  uint2 res[T8<2>::NRT][t8::CT];
+  for (int blk = 0; blk < a.nblocks; ++blk) {
+    const WNext c1 = wnext(wf + (2 * blk) * WCONV, TNS, ctw), c2 = wnext(wf + (2 * blk + 1) * WCONV, TNS, ctw);
+    const WNext c3 = blk + 1 < a.nblocks ? wnext(wf + (2 * blk + 2) * WCONV, TNS, ctw) : c1;  // last: harmless
+    tower8_conv<0, 2, false, G>(lds, c1, c2, ctw, biasl + (2 * blk) * TC, res, bq, lane, 2 * blk);
+    tower8_conv<0, 2, true, G>(lds, c2, c3, ctw, biasl + (2 * blk + 1) * TC, res, bq, lane, 2 * blk + 1);
+  }
+  // epilogue: AvgPool2d 8x10 -> 4x5 (bf16), per-env min / max, the scaled latent. 128 threads per env,
+  // 5 of its 640 chunks each
+  const int e = tid >> 7, t = tid & 127;
+  uint4 pv[5];
+  float mn = INFINITY, mx = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int i = u * 128 + t, pp = i >> 5, c = i & 31, y4 = pp / 5, x4 = pp - y4 * 5;
+    const int r00 = (2 * x4) * 16 + (2 * y4) * 2 + e;  // (2y, 2x); +16: x + 1; +2: y + 1
+    float f0[8], f1[8], f2[8], f3[8];
+    unpack8<0>(*reinterpret_cast<const uint4*>(lds + toff(r00, c)), f0);
+    unpack8<0>(*reinterpret_cast<const uint4*>(lds + toff(r00 + 16, c)), f1);
+    unpack8<0>(*reinterpret_cast<const uint4*>(lds + toff(r00 + 2, c)), f2);
+    unpack8<0>(*reinterpret_cast<const uint4*>(lds + toff(r00 + 18, c)), f3);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (((f0[j] + f1[j]) + f2[j]) + f3[j]) / 4.0f;
+    pv[u] = make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
+    float g[8];
+    unpack8<0>(pv[u], g);  // min / max of the bf16 pooled values, as scale_state_kernel reads them
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { mn = fminf(mn, g[j]); mx = fmaxf(mx, g[j]); }
+  }
+  for (int o = 32; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
+  if (lane == 0) { mm[e][(t >> 6)][0] = mn; mm[e][(t >> 6)][1] = mx; }
+  __syncthreads();
+  mn = fminf(mm[e][0][0], mm[e][1][0]);
+  mx = fmaxf(mm[e][0][1], mm[e][1][1]);
+  if (e >= nenv) return;
+  const float den = (mx - mn) + 1e-8f;
+  const int b = env0 + e;
+#pragma unroll
+  for (int u = 0; u < 5; ++u) {
+    const int i = u * 128 + t;
+    float g[8];
+    unpack8<0>(pv[u], g);
+    const uint4 r = make_uint4(pack_bf16x2((g[0] - mn) / den, (g[1] - mn) / den), pack_bf16x2((g[2] - mn) / den, (g[3] - mn) / den),
+                               pack_bf16x2((g[4] - mn) / den, (g[5] - mn) / den), pack_bf16x2((g[6] - mn) / den, (g[7] - mn) / den));
+    *reinterpret_cast<uint4*>(a.out + (size_t)b * 20 * TC + i * 8) = r;
+    if (a.pool) *reinterpret_cast<uint4*>(a.pool + (size_t)b * a.pool_env_stride + i * 8) = r;
+  }
+}
+
 static int g_tower_variant = 0;  // 0 auto, 1 four-env kernel, 2 eight-env kernel, 3 four-env 4-wave
 
 static size_t t8_dyn_lds(int nblocks) { return (size_t)nblocks * 2 * TC * sizeof(float); }
@@ -1016,6 +1158,16 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
   } else {
     hipLaunchKernelGGL(tower_kernel<0>, dim3((B + TE - 1) / TE), dim3(TNT), 0, stream, a);
   }
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+// Representation tail (see include/mzba.h): 16x20 activations -> scaled 4x5 root latent, one launch.
+int mzba_rep_tail(const void* in, void* out, void* pool, long long pool_env_stride, const void* wf16,
+                  const float* bias, int nblocks, int B, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && nblocks >= 1 && nblocks <= T8_MAX_BLOCKS && in && out && wf16 && bias && in != out, -1);
+  RepTailArgs a{(const bf16_t*)in, (bf16_t*)out, (bf16_t*)pool, pool_env_stride, (const bf16_t*)wf16, bias, nblocks, B};
+  hipLaunchKernelGGL(rep_tail_kernel, dim3((B + 1) / 2), dim3(t8::NT), t8_dyn_lds(nblocks), stream, a);
   MZ_LAUNCH_CHECK();
   return 0;
 }

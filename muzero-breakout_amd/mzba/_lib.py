@@ -41,6 +41,7 @@ SIGNATURES = {
     "mzba_tower_plan": [I],
     "mzba_tower_ws_bytes": [I],
     "mzba_tower_fused": [P, LL, P, LL, P, P, P, I, I, P, P],
+    "mzba_rep_tail": [P, P, P, LL, P, P, I, I, P],
     "mzba_conv_band_supported": [I, I, I, I, I],
     "mzba_conv_band_set_xt": [I],
     "mzba_replay_plan": [P, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P],
@@ -124,7 +125,12 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"mzba: HIP library not built ({LIB_PATH}); run __graft_entry__.build() / make -C csrc")
         L = ctypes.CDLL(LIB_PATH)
+        # A/B tooling only (an older build that predates an entry point): MZBA_LIB_PARTIAL=1 skips
+        # symbols the library does not export; the product binds every declared symbol or fails
+        partial = os.environ.get("MZBA_LIB_PARTIAL") == "1"
         for name, argt in SIGNATURES.items():
+            if partial and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = RESTYPES.get(name, ctypes.c_int)

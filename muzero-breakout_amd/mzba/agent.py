@@ -106,6 +106,7 @@ class PackedNets:
                                    self._bn(sd, "pred_net.value_head.0.bn"))
         self.val_lin = self._linear(sd["pred_net.value_head.2.weight"], sd["pred_net.value_head.2.bias"], self.c1 // 2)
         self.fused = self._fused(sd, w[:, :cmain])
+        self.rep_tail = self._rep_tail(sd)
 
     def _fused(self, sd, w0):
         """Weights of the fused dynamics / prediction steps (mzba_tower_fused): the dynamics
@@ -148,6 +149,33 @@ class PackedNets:
             out["dyn16"] = {"w0": pack3(w0 * a0[:, None, None, None], torch.float16), "rw": pack1(rw, torch.float16),
                             "lw": lw}
         return out
+
+    def _rep_tail(self, sd):
+        """Weights of the fused representation tail (mzba_rep_tail): the residual blocks between the
+        two final AvgPool2d of rep_layout, BN folded, in the tower packing (bf16, 256 channels, 16x20
+        input -> 8x10 -> 4x5 latent)."""
+        lay = rep_layout(self.mcfg)
+        if not (self.dtype == "bf16" and self.c1 == 256 and (self.lh, self.lw) == (4, 5) and len(lay) >= 3
+                and lay[-1][0] == "pool"):
+            return None
+        i = len(lay) - 2
+        blocks = []
+        while i >= 0 and lay[i][0] == "res":
+            blocks.insert(0, lay[i][1])
+            i -= 1
+        if i < 0 or lay[i][0] != "pool" or not 1 <= len(blocks) <= 24:
+            return None
+        ws, bs = [], []
+        for j in blocks:
+            for k in (1, 2):
+                p = f"rep_net.blocks.{j}"
+                alpha, beta = self._bn(sd, f"{p}.bn{k}")
+                ws.append(sd[f"{p}.conv{k}.weight"] * alpha[:, None, None, None])
+                bs.append(sd[f"{p}.conv{k}.bias"] * alpha + beta)
+        wf = np.concatenate([pack_tower_conv(w) for w in ws] + [np.zeros(LAT_PAD_ELEMS)])
+        return {"n": len(blocks), "first": len(lay) - 2 - len(blocks),  # rep_layout index of the first pool
+                "wf": torch.tensor(wf, dtype=torch.float32).to(self.tdt).to(self.device),
+                "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device)}
 
     # -- packing helpers ---------------------------------------------------------------
     @staticmethod
@@ -262,6 +290,9 @@ class NetRunner:
         self.use_tower = True  # dyn/pred residual towers as one fused launch each (bf16, C=256, 4x5)
         self.use_fused = True  # ... with the dynamics ConvBlock and the heads inside (4-env kernel)
         self.use_band = True  # 16x20 representation convs on the band kernel
+        # the 8x10 blocks between the two pools + scale as one launch (bf16); an A/B run against an
+        # older library build (MZBA_LIB_PARTIAL) falls back to the launch sequence
+        self.use_rep_tail = hasattr(L.lib(), "mzba_rep_tail")
         self.tower_plan = self.tower_ws = None
         if packed.tower_ok:
             self.tower_plan = L.lib().mzba_tower_plan(B)
@@ -322,7 +353,12 @@ class NetRunner:
         B, H, W = self.B, self.H, self.W
         cur, bufs = x_in, [self.r_a, self.r_b]
         which = 0
-        for kind, layer in self.p.rep:
+        tail = self.p.rep_tail if (self.use_rep_tail and (H, W) == (16, 20)) else None
+        for li, (kind, layer) in enumerate(self.p.rep):
+            if tail is not None and li == tail["first"]:  # pool + 8x10 blocks + pool + scale: one launch
+                L.call("mzba_rep_tail", L.ptr(cur), L.ptr(out_latent), L.ptr(pool), pool_env_stride,
+                       L.ptr(tail["wf"]), L.ptr(tail["b"]), tail["n"], B, L.stream())
+                return
             if kind == "conv":
                 dst = bufs[which]
                 self.conv(cur, layer, dst, B, H, W, relu=False)

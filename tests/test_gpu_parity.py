@@ -389,6 +389,62 @@ def test_fused_bf16_steps_vs_torch_fp32(B, variant):
         assert err < 2e-2, (nm, err)
 
 
+@pytest.mark.parametrize("B", [1, 13, 256])
+def test_rep_tail_vs_torch_fp32(B):
+    """mzba_rep_tail (AvgPool2d 16x20 -> 8x10, the 3 ResidualBlock(256) at 8x10, AvgPool2d -> 4x5 and
+    _scale_state in one launch, networks.py:86-99, 314-328) against a plain torch fp32 evaluation with
+    bf16 rounding where the unfused launch sequence stores bf16 (pooled maps, ReLU outputs, scaled
+    latent); and the whole representation net with the fused tail against the unfused launches.
+    Tolerance 2e-2 absolute on the [0, 1] scaled latent (f32 summation order inside the convs); odd B
+    leaves the last workgroup one env short."""
+    from mzba import _lib as L
+    from mzba.agent import MuZeroAgent
+    from mzba.weights import rep_layout
+    mcfg = default_config()["model"]
+    sd = init_state_dict(mcfg, 11)
+    ag = MuZeroAgent(mcfg, dtype="bf16")
+    ag.load_state_dict(sd)
+    tail = ag.packed.rep_tail
+    assert tail is not None and tail["n"] == 3
+    g = torch.Generator().manual_seed(B)
+    x = torch.rand(B, 320, 256, generator=g).to(torch.bfloat16)
+    out = torch.full((B, 20, 256), float("nan"), device="cuda").to(torch.bfloat16)
+    pool = torch.zeros(B, 3, 20, 256, device="cuda").to(torch.bfloat16)
+    L.call("mzba_rep_tail", L.ptr(x.cuda()), L.ptr(out), L.ptr(pool), 3 * 20 * 256, L.ptr(tail["wf"]), L.ptr(tail["b"]),
+           3, B, L.stream())
+    torch.cuda.synchronize()
+    ref = _Bf16StepRef(sd, mcfg)
+    lay = rep_layout(mcfg)
+    h = x.float().view(B, 16, 20, 256).permute(0, 3, 1, 2)
+    pool2 = lambda t: _bf((((t[:, :, 0::2, 0::2] + t[:, :, 0::2, 1::2]) + t[:, :, 1::2, 0::2]) + t[:, :, 1::2, 1::2]) / 4.0)  # noqa: E731
+    h = pool2(h)
+    for j in [i for k, i in lay[tail["first"] + 1: -1]]:
+        p = f"rep_net.blocks.{j}"
+        t = _bf(torch.relu(ref._conv(h, p + ".conv1", p + ".bn1", 1)))
+        h = _bf(torch.relu(ref._conv(t, p + ".conv2", p + ".bn2", 1, extra=h)))
+    h = pool2(h)
+    f = h.flatten(1)
+    mn, mx = f.min(1).values[:, None, None, None], f.max(1).values[:, None, None, None]
+    want = _bf((h - mn) / ((mx - mn) + 1e-8))
+    got = out.float().cpu().view(B, 4, 5, 256).permute(0, 3, 1, 2)
+    assert torch.isfinite(got).all()
+    err = (got - want).abs().max().item()
+    print(f"rep tail vs torch fp32 [B={B}]: {err:.2e}")
+    assert err < 2e-2, err
+    assert torch.equal(pool[:, 0].cpu(), out.cpu())  # slot 0 of the node pool = the root latent
+    # the whole representation net, fused tail vs the unfused launches (same bf16 weights)
+    xs = torch.rand(B, 64, 16, 20, generator=g).cuda()
+    rn = ag.runner(B, 16, 20)
+    lat = {}
+    for fused in (True, False):
+        rn.use_rep_tail = fused
+        lat[fused] = ag.create_hidden_state_root(xs).float().cpu()
+    rn.use_rep_tail = True
+    d = (lat[True] - lat[False]).abs().max().item()
+    print(f"representation, fused tail vs unfused [B={B}]: {d:.2e}")
+    assert d < 2e-2, d
+
+
 @pytest.mark.parametrize("Cin,Cout,resid,relu", [(64, 128, False, False), (128, 128, False, True), (128, 256, False, False),
                                                    (256, 256, True, True), (256, 128, False, True)])
 @pytest.mark.parametrize("xt", [10, 5])

@@ -4,7 +4,7 @@
 # GRBM counter pass per library on the isolated B = 4096 tower. Any failing step ends the script.
 # usage (repo root on the box): bash tools/gpu_ab.sh TAG
 set -euo pipefail
-export TMPDIR=/tmp
+export TMPDIR=/tmp MZBA_LIB_PARTIAL=1
 O=gpurun_out/$1
 M=$PWD/muzero-breakout_amd/mzba
 mkdir -p $O
