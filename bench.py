@@ -478,6 +478,10 @@ def main():
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": traffic,
                          "traffic_algorithmic_bytes": traffic_rec and traffic_rec.get("algorithmic_bytes"),
+                         # the floor with per-XCD L2s: every one of the 8 XCDs fetches the tower's weights
+                         # once (33 MB each), the latents once in all
+                         "traffic_per_xcd_floor_bytes": traffic_rec and (
+                             traffic_rec.get("algorithmic_bytes") + 7 * (2 * 14 * 256 * 2304 * 2)),
                          "traffic_source": traffic_rec and "profiles/tower_hbm_traffic.json",
                          "flop_per_conv": fl, "avg_ms_per_conv": conv_ms, "avg_launch_ms": tower_launch_ms or conv_ms,
                          "launches_timed": len(probe)},
