@@ -213,6 +213,18 @@ __global__ void env_reset_compact_kernel(Compact cs, uint8_t* __restrict__ cur_f
   for (int k = threadIdx.x; k < hist.L; k += blockDim.x) hist.actions[(size_t)b * hist.L + k] = (uint8_t)pad_action;
 }
 
+// one 16-B chunk of a rendered frame: a non-temporal store (written once, read by a later launch
+// at most once: 84x84 B=4096 10.3 -> 8.6 us per graph-replayed step)
+MZ_DEV void frame_store(uint8_t* p, uint4 v) {
+#ifndef MZ_ENV_TEMPORAL
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+#else
+  *reinterpret_cast<uint4*>(p) = v;
+#endif
+}
+
 // Phase 1: one thread per env, all rules on the compact state (same op order as above).
 // Phase 2: the block renders its E envs' frames (16 B per lane per store) and pushes
 // them into the history ring when the env is recorded this step. E (<= 256) is chosen by the
@@ -223,13 +235,23 @@ __global__ __launch_bounds__(256, 8) void env_step_compact_kernel(
     uint8_t* __restrict__ cur_frame, History hist, Sink sink, int first_step_arg, int B, int H, int W, int pw,
     int brick_rows, RewardCfg rc, const int32_t* __restrict__ ctx, int E, int rec_flags) {
   // graph replay: the episode row t comes from the device context; the sink pointers are the
-  // (T, B, ...) bases and row t is selected here; t == 0 is the first step
-  const int first_step = ctx ? (ctx[2] == 0) : first_step_arg;
-  if (ctx) {
-    const long long t = ctx[2];
-    if (sink.action) { sink.action += t * B; sink.reward += t * B; sink.mask += t * B; }
-    if (sink.frame) sink.frame += t * B * H * W;
-  }
+  // (T, B, ...) bases and row t is selected here; t == 0 is the first step.
+  // Every load of phase 1 (ctx, the env's state, its history length, its action) is issued
+  // unconditionally and before the first use of any of them: one memory round trip ahead of the
+  // render stores, not three (a conditional paddle load behind `done`, the ctx load ahead of both
+  // serialised them: 10.5 -> see DESIGN.md §3.3).
+  // ctx[2] through a vector load (a VGPR zero index): a scalar load would put its round trip
+  // ahead of the state loads (s_waitcnt lgkmcnt(0) also waits for the kernel arguments)
+  int vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  // every kernel argument into SGPRs here: left to itself the compiler loads them in four
+  // groups, each behind its own s_waitcnt (four scalar-cache round trips ahead of the first
+  // state load)
+  asm volatile("" ::"s"(cs.paddle), "s"(cs.bx), "s"(cs.by), "s"(cs.dx), "s"(cs.dy), "s"(cs.done), "s"(cs.bricks),
+               "s"(cs.nw), "s"(action), "s"(reward), "s"(valid), "s"(cur_frame));
+  asm volatile("" ::"s"(hist.frames), "s"(hist.actions), "s"(hist.hlen), "s"(hist.L), "s"(hist.cur_src),
+               "s"(sink.action), "s"(sink.reward), "s"(sink.mask), "s"(sink.frame), "s"(ctx), "s"(E), "s"(B));
+  const int ctx_t = ctx ? ctx[2 + vzero] : 0;
   __shared__ int s_paddle[256], s_bx[256], s_by[256];
   __shared__ uint64_t s_br[256][MAXW];
   __shared__ uint8_t s_done[256], s_rec[256];
@@ -238,19 +260,24 @@ __global__ __launch_bounds__(256, 8) void env_step_compact_kernel(
   const int b = blockIdx.x * E + t;
   const int nw = cs.nw;
   if (t < E && b < B) {
-    const int hl = hist.hlen[b];  // loaded with the state: no second round trip when recording
-    const bool was_done = cs.done[b] != 0;
-    const int p0 = was_done ? 0 : cs.paddle[b];  // argmax of an empty row is 0 (:177)
+    const int hl = hist.hlen[b];
+    const uint8_t done8 = cs.done[b];
+    const int paddle_ld = cs.paddle[b];
     const int64_t a = action[b];
-    int pnew = p0 + (a == 0 ? -1 : (a == 2 ? 1 : 0));
-    pnew = pnew < 0 ? 0 : (pnew > W - pw ? W - pw : pnew);
     const int x = cs.bx[b], y = cs.by[b];
-    const float ball_x = (float)x, ball_y = (float)y;
     int dx = cs.dx[b];
     float dy = cs.dy[b];
     uint64_t br[MAXW];
 #pragma unroll
-    for (int w = 0; w < MAXW; ++w) br[w] = w < nw ? cs.bricks[(size_t)b * nw + w] : 0ull;
+    for (int w = 0; w < MAXW; ++w) br[w] = cs.bricks[(size_t)b * nw + (w < nw ? w : nw - 1)];
+#pragma unroll
+    for (int w = 0; w < MAXW; ++w) br[w] = w < nw ? br[w] : 0ull;
+    const int first_step = ctx ? (ctx_t == 0) : first_step_arg;
+    const bool was_done = done8 != 0;
+    const int p0 = was_done ? 0 : paddle_ld;  // argmax of an empty row is 0 (:177)
+    int pnew = p0 + (a == 0 ? -1 : (a == 2 ? 1 : 0));
+    pnew = pnew < 0 ? 0 : (pnew > W - pw ? W - pw : pnew);
+    const float ball_x = (float)x, ball_y = (float)y;
     const bool wall = (ball_x + (float)dx < 0.f) || (ball_x + (float)dx >= (float)W);
     if (wall) dx = -dx;
     float ny = ball_y + dy;
@@ -308,7 +335,8 @@ __global__ __launch_bounds__(256, 8) void env_step_compact_kernel(
     const bool rec = (rec_flags & 1) ? true : (first_step ? !dfin : !was_done);
     const int64_t ra = (rec_flags & 2) ? action[0] : a;
     if (sink.action) {
-      sink.action[b] = (uint8_t)ra; sink.reward[b] = r; sink.mask[b] = rec ? 1 : 0;
+      const size_t row = (size_t)ctx_t * B;  // ctx_t = 0 without a device context
+      sink.action[row + b] = (uint8_t)ra; sink.reward[row + b] = r; sink.mask[row + b] = rec ? 1 : 0;
     }
     s_paddle[t] = dfin ? -1 : pnew; s_bx[t] = ix; s_by[t] = fy; s_done[t] = dfin; s_rec[t] = rec;
 #pragma unroll
@@ -326,7 +354,8 @@ __global__ __launch_bounds__(256, 8) void env_step_compact_kernel(
   // three 16-bit masks spread to bytes — no per-pixel division, no branch on the region.
   const int HW = H * W;
   const int chunks = HW / 16;
-  const int nenv = min(E, B - blockIdx.x * E);
+  const int nenv = min(E, B - (int)blockIdx.x * E);
+  uint8_t* const sink_frame = sink.frame ? sink.frame + (size_t)ctx_t * B * HW : nullptr;
   const uint32_t inv_chunks = 0xffffffffu / (uint32_t)chunks + 1u;  // exact i / chunks for i < 2^32 / chunks
   for (int i = t; i < nenv * chunks; i += 256) {
     const int e = (int)__umulhi((uint32_t)i, inv_chunks), c = i - e * chunks;
@@ -348,12 +377,12 @@ __global__ __launch_bounds__(256, 8) void env_step_compact_kernel(
       wv[q] = (nb << 2) | (nl << 1) | np;  // gray_code(paddle, ball, brick)
     }
     uint4 v = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-    if (sink.frame) *reinterpret_cast<uint4*>(sink.frame + (size_t)gb * HW + c * 16) = v;
+    if (sink_frame) frame_store(sink_frame + (size_t)gb * HW + c * 16, v);
     if (s_rec[e]) {
-      *reinterpret_cast<uint4*>(hist.frames + ((size_t)gb * (hist.L - 1) + s_slot[e]) * HW + c * 16) = v;
-      if (!hist.cur_src) *reinterpret_cast<uint4*>(cur_frame + (size_t)gb * HW + c * 16) = v;
+      frame_store(hist.frames + ((size_t)gb * (hist.L - 1) + s_slot[e]) * HW + c * 16, v);
+      if (!hist.cur_src) frame_store(cur_frame + (size_t)gb * HW + c * 16, v);
     } else {
-      *reinterpret_cast<uint4*>(cur_frame + (size_t)gb * HW + c * 16) = v;
+      frame_store(cur_frame + (size_t)gb * HW + c * 16, v);
     }
   }
   if (t < E && b < B) {

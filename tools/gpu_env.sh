@@ -14,7 +14,7 @@ else
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 fi
 tail -2 $O/pytest.log
-EB="bench.py --workload env --envs 4096 --height 84 --width 84 --hist 4 --steps 30 --warmup 5"
+EB="bench.py --workload env --envs 4096 --height 84 --width 84 --hist 4 --steps 200 --warmup 5"
 timeout -k 10 200 python $EB > $O/env_bench.json 2> $O/env_bench.err
 cat $O/env_bench.json
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/env_prof -o run -- python3 $EB --no-cpu > $O/env_prof.log 2>&1
