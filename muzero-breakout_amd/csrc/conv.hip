@@ -17,6 +17,7 @@
 // over the LDS banks. bf16 uses v_mfma_f32_16x16x32_bf16; the f32 parity path uses
 // v_mfma_f32_16x16x4_f32 (exact f32 fma chain).
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
@@ -171,14 +172,45 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
     __syncthreads();
   }
 
-  // epilogue: D[row = 4*fq + r][col = fr] of each 16x16 tile
+  // epilogue: D[row = 4*fq + r][col = fr] of each 16x16 tile. Per channel tile, every action-bias /
+  // residual load of the lane's 16 outputs is issued (from clamped addresses) before the first use,
+  // op order unchanged ((((acc + act_bias) + bias) + res), ReLU): the per-element form waited one
+  // memory round trip per output (two with the action index), 64 per lane.
   T* out = (T*)a.out;
   const T* res = (const T*)a.res;
+  int mrow[4][4], arow[4][4];  // [mi][r]: pixel row (clamped), action-bias row p * A + act[env]
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mrow[mi][r] = min(m0 + wm * 64 + mi * 16 + fq * 4 + r, M - 1);
+  if (a.act_bias) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = mrow[mi][r] / HW, p = mrow[mi][r] - b * HW;
+        arow[mi][r] = p * a.A + a.act[b];
+      }
+  }
 #pragma unroll
   for (int ni = 0; ni < 4; ++ni) {
     const int n = n0 + wn * 64 + ni * 16 + fr;
+    const int nc = min(n, a.Cout - 1);
+    const float bn = a.bias[nc];
+    float ab[4][4], rv[4][4];
+    if (a.act_bias) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ab[mi][r] = a.act_bias[(long long)arow[mi][r] * a.Cout + nc];
+    }
+    if (res) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rv[mi][r] = ElemIO<T>::load(res + (long long)mrow[mi][r] * a.Cout + nc);
+    }
     if (n >= a.Cout) continue;
-    const float bn = a.bias[n];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
 #pragma unroll
@@ -186,12 +218,9 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
         const int m = m0 + wm * 64 + mi * 16 + fq * 4 + r;
         if (m >= M) continue;
         float v = acc[mi][ni][r];
-        if (a.act_bias) {
-          int b = m / HW, p = m - b * HW;
-          v = v + a.act_bias[((long long)p * a.A + a.act[b]) * a.Cout + n];
-        }
+        if (a.act_bias) v = v + ab[mi][r];
         v = v + bn;
-        if (res) v = v + ElemIO<T>::load(res + (long long)m * a.Cout + n);
+        if (res) v = v + rv[mi][r];
         if (a.relu) v = fmaxf(v, 0.f);
         ElemIO<T>::store(out + (long long)m * a.Cout + n, v);
       }
@@ -201,19 +230,22 @@ __global__ __launch_bounds__(NT, 2) void conv_igemm_kernel(ConvArgs a) {
 
 // Large-image bf16 conv (config 3 geometry: 84x84 / 42x42 images, 21x21 latents; M = B*H*W in the
 // millions): one workgroup = 256 pixels x 256 output channels, 8 waves (2 pixel halves x 4 channel
-// quarters), each 128 x 64 = 8 x 4 tiles of v_mfma_f32_16x16x32_bf16 with the WEIGHTS as the A
-// operand, so a lane's accumulator holds 4 consecutive channels of one pixel (8-byte bf16 stores).
-// K-step = 64 (tap-resolved 16-B chunks as conv_igemm); operands global -> VGPR -> LDS (double
-// buffer, one barrier per K-step); loads unconditional from clamped addresses, zero select at the
-// LDS store, so they stay in flight under the previous step's MFMAs. Each staged pixel row is read
-// by all 256 channels of the tile (conv_igemm's 128 x 128 tile loads it twice).
+// quarters, two per SIMD), each 128 x 64 = 8 x 4 tiles of v_mfma_f32_16x16x32_bf16 with the WEIGHTS as
+// the A operand, so a lane's accumulator holds 4 consecutive channels of one pixel (8-byte bf16
+// stores). K step = 64 (one tap, a 64-channel block: Cin % 64 == 0), walked with scalar counters.
+// Staging global -> VGPR -> LDS (two LDS stages, one barrier per step), loads from clamped addresses
+// with a zero select at the LDS write (out-of-image taps); weights through a buffer resource.
+// The epilogue issues every bias / residual load before the first use: the per-element form waited
+// for one memory round trip per (pixel tile, channel tile), 32 per workgroup, about as long as the
+// whole k loop (+20 % on the 21x21 latent conv, profiles/r02/conv_big/).
 namespace big {
 constexpr int BM = 256, BN = 256, NT = 512, BK = 64, ROWB = 128;
-constexpr int TILE = BM * ROWB;  // 32 KB per operand per stage
+constexpr int TILE = BM * ROWB;     // 32 KB per operand per stage
+constexpr int RPT = BM / (NT / 8);  // staged rows per thread per operand (4)
 }
 
 __global__ __launch_bounds__(big::NT, 1) void conv_big_bf16_kernel(ConvArgs a) {
-  using big::NT; using big::BK; using big::TILE;
+  using big::NT; using big::BK; using big::TILE; using big::RPT;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_big[];  // [2 stages][A | W]
   const int HW = a.H * a.W;
   const int M = a.B * HW;
@@ -221,48 +253,63 @@ __global__ __launch_bounds__(big::NT, 1) void conv_big_bf16_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;  // pixel half (128), channel quarter (64)
   const int pad = a.ks / 2;
-  const int Ktot = a.ks * a.ks * a.Cin;
-  const int nK = (Ktot + BK - 1) / BK;
+  const int Ktot = a.ks * a.ks * a.Cin;  // Cin % 64 == 0 (launcher): a K step lies within one tap
+  const int nK = Ktot / BK;
   const int j = tid & 7, r0 = tid >> 3;  // staging: chunk j of rows r0 + 64 i
-  const bf16_t* in = (const bf16_t*)a.in;
-  const bf16_t* wgt = (const bf16_t*)a.w;
-  const bf16_t* abase[4];
-  int ay[4], ax[4];
-  bool mval[4], nval[4];
+  // per staged pixel row: its offset in 16-B units (the address every out-of-image tap falls back
+  // to) and (y, x) packed
+  int aoff[RPT], ayx[RPT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < RPT; ++i) {
     const int m = m0 + r0 + 64 * i;
-    mval[i] = m < M;
-    const int mm = mval[i] ? m : 0;
-    const int b = mm / HW, p = mm - b * HW;
-    ay[i] = p / a.W;
-    ax[i] = p - ay[i] * a.W;
-    abase[i] = in + (long long)b * a.in_env_stride;
-    nval[i] = n0 + r0 + 64 * i < a.Cout;
+    const int mm = m < M ? m : 0;
+    const int bb = mm / HW, p = mm - bb * HW;
+    const int y = p / a.W;
+    ayx[i] = m < M ? (y << 16) | (p - y * a.W) : 0x7fff7fff;  // invalid rows: no tap in the image
+    aoff[i] = (int)(((long long)bb * a.in_env_stride + (long long)p * a.Cin) >> 3);
   }
-  uint4 ra[4], rb[4];
-  bool oka[4], okb[4];
-  auto load_tile = [&](int ks) {
-    const int k = ks * BK + j * 8;
-    const bool kok = k < Ktot;
-    const int tap = k / a.Cin, c = k - tap * a.Cin;
-    const int ky = tap / a.ks - pad, kx = tap % a.ks - pad;
+  const uint4* in16 = reinterpret_cast<const uint4*>(a.in) + j;
+  // weights through a buffer resource over this workgroup's 256 rows (Cout % 256 == 0): the lane's
+  // row / chunk offset in one VGPR, the row group and K step in the scalar offset
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>((const bf16_t*)a.w + (long long)n0 * Ktot), 0, big::BN * Ktot * 2, 0x00020000);
+  const int wvoff = (r0 * Ktot + j * 8) * 2;
+  uint4 ra[2][RPT], rb[RPT];
+  uint32_t oka[2];
+  // walk state of the next activation step (lc, lky, lkx) and the next weight step (lw)
+  int lc = 0, lky = -pad, lkx = -pad, lw = 0;
+  auto load_a = [&](auto setc) {
+    constexpr int set = decltype(setc)::value;
+    const int toff = ((lky * a.W + lkx) * a.Cin + lc) >> 3;
+    uint32_t ok = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int sy = ay[i] + ky, sx = ax[i] + kx;
-      oka[i] = kok && mval[i] && sy >= 0 && sy < a.H && sx >= 0 && sx < a.W;
-      ra[i] = *reinterpret_cast<const uint4*>(abase[i] + (oka[i] ? (long long)(sy * a.W + sx) * a.Cin + c : 0));
-      okb[i] = kok && nval[i];
-      rb[i] = *reinterpret_cast<const uint4*>(wgt + (okb[i] ? (long long)(n0 + r0 + 64 * i) * Ktot + k : 0));
+    for (int i = 0; i < RPT; ++i) {
+      const int sy = (ayx[i] >> 16) + lky, sx = (ayx[i] & 0xffff) + lkx;
+      const bool o = (unsigned)sy < (unsigned)a.H && (unsigned)sx < (unsigned)a.W;
+      ok |= (o ? 1u : 0u) << i;
+      ra[set][i] = in16[aoff[i] + (o ? toff : 0)];
+    }
+    oka[set] = ok;
+    lc += BK;
+    if (lc == a.Cin) {
+      lc = 0;
+      if (++lkx > pad) { lkx = -pad; ++lky; }
     }
   };
-  auto store_tile = [&](int buf) {
+  auto load_w = [&]() {
+#pragma unroll
+    for (int i = 0; i < RPT; ++i)
+      rb[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff, (64 * i * Ktot + lw) * 2, 0));
+    lw += BK;
+  };
+  auto store_tile = [&](auto setc, int buf) {
+    constexpr int set = decltype(setc)::value;
     uint8_t* la = lds_big + buf * 2 * TILE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < RPT; ++i) {
       const int row = r0 + 64 * i;
-      *reinterpret_cast<uint4*>(la + swz(row, j)) = oka[i] ? ra[i] : make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(la + TILE + swz(row, j)) = okb[i] ? rb[i] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(la + swz(row, j)) = ((oka[set] >> i) & 1) ? ra[set][i] : make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(la + TILE + swz(row, j)) = rb[i];
     }
   };
   f32x4 acc[8][4];  // [pixel tile][channel tile]: D[channel 4q + i][pixel l16]
@@ -270,21 +317,28 @@ __global__ __launch_bounds__(big::NT, 1) void conv_big_bf16_kernel(ConvArgs a) {
   for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-  load_tile(0);
-  store_tile(0);
+  load_a(std::integral_constant<int, 0>{});
+  load_w();
+  if (nK > 1) load_a(std::integral_constant<int, 1>{});
+  store_tile(std::integral_constant<int, 0>{}, 0);
   __syncthreads();
   const int fr = lane & 15, fq = lane >> 4;
-  for (int ks = 0; ks < nK; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < nK) load_tile(ks + 1);
-    const uint8_t* la = lds_big + buf * 2 * TILE;
-    const uint8_t* lw = la + TILE;
+  // one K step on LDS stage SET; activation register set SET was written at the end of the previous
+  // step and is refilled with step ks + 2; the weight set with step ks + 1. (The compiler's wait
+  // counting merges the paths of the two conditions and waits for every older load before these are
+  // issued: in effect one step of lead, as before; a branch-free form of the loop spills.)
+  auto step = [&](int ks, auto setc) {
+    constexpr int SET = decltype(setc)::value;
+    if (ks + 2 < nK) load_a(setc);
+    if (ks + 1 < nK) load_w();
+    const uint8_t* la = lds_big + SET * 2 * TILE;
+    const uint8_t* lwt = la + TILE;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 wf[4], xf[8];
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni)
-        wf[ni] = *reinterpret_cast<const bf16x8*>(lw + swz(wn * 64 + ni * 16 + fr, kk * 4 + fq));
+        wf[ni] = *reinterpret_cast<const bf16x8*>(lwt + swz(wn * 64 + ni * 16 + fr, kk * 4 + fq));
 #pragma unroll
       for (int mi = 0; mi < 8; ++mi)
         xf[mi] = *reinterpret_cast<const bf16x8*>(la + swz(wm * 128 + mi * 16 + fr, kk * 4 + fq));
@@ -296,30 +350,53 @@ __global__ __launch_bounds__(big::NT, 1) void conv_big_bf16_kernel(ConvArgs a) {
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ni], xf[mi], acc[mi][ni], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
     }
-    if (ks + 1 < nK) store_tile(buf ^ 1);
+    if (ks + 1 < nK) store_tile(std::integral_constant<int, 1 - SET>{}, 1 - SET);
     __syncthreads();
+  };
+  for (int ks = 0; ks < nK; ks += 2) {
+    step(ks, std::integral_constant<int, 0>{});
+    if (ks + 1 < nK) step(ks + 1, std::integral_constant<int, 1>{});
   }
-  // epilogue: lane holds channels n .. n+3 of pixel m: + bias (+ residual), ReLU, 8-byte stores
+  // epilogue: lane holds channels n .. n+3 of pixel m: + bias (+ residual), ReLU, 8-byte stores.
+  // Every bias / residual load is issued (from clamped rows) before the first use: written per
+  // element (load, add, store) the compiler waited vmcnt(0) 32 times per workgroup, one round trip
+  // each (as long as the whole k loop).
   bf16_t* out = (bf16_t*)a.out;
   const bf16_t* res = (const bf16_t*)a.res;
+  float4 bb[4];
 #pragma unroll
-  for (int ni = 0; ni < 4; ++ni) {
-    const int n = n0 + wn * 64 + ni * 16 + 4 * fq;
-    if (n >= a.Cout) continue;
-    const float4 bb = *reinterpret_cast<const float4*>(a.bias + n);
+  for (int ni = 0; ni < 4; ++ni) bb[ni] = *reinterpret_cast<const float4*>(a.bias + n0 + wn * 64 + ni * 16 + 4 * fq);
+  uint2 rv[8][4];
+  if (res) {
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi) {
-      const int m = m0 + wm * 128 + mi * 16 + fr;
-      if (m >= M) continue;
-      float v0 = acc[mi][ni][0] + bb.x, v1 = acc[mi][ni][1] + bb.y, v2 = acc[mi][ni][2] + bb.z,
-            v3 = acc[mi][ni][3] + bb.w;
-      if (res) {
-        const uint2 r = *reinterpret_cast<const uint2*>(res + (long long)m * a.Cout + n);
-        v0 += bf16_to_f32((bf16_t)(r.x & 0xffffu)); v1 += bf16_to_f32((bf16_t)(r.x >> 16));
-        v2 += bf16_to_f32((bf16_t)(r.y & 0xffffu)); v3 += bf16_to_f32((bf16_t)(r.y >> 16));
-      }
+      const int m = min(m0 + wm * 128 + mi * 16 + fr, M - 1);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+        rv[mi][ni] = *reinterpret_cast<const uint2*>(res + (long long)m * a.Cout + n0 + wn * 64 + ni * 16 + 4 * fq);
+    }
+  } else {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) rv[mi][ni] = make_uint2(0x80008000u, 0x80008000u);  // bf16 -0
+  }
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = m0 + wm * 128 + mi * 16 + fr;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + wn * 64 + ni * 16 + 4 * fq;
+      const uint2 r = rv[mi][ni];
+      // (acc + bias) + residual: the residual-free form adds -0, which leaves every value (and the
+      // sign of a zero) unchanged
+      float v0 = (acc[mi][ni][0] + bb[ni].x) + bf16_to_f32((bf16_t)(r.x & 0xffffu));
+      float v1 = (acc[mi][ni][1] + bb[ni].y) + bf16_to_f32((bf16_t)(r.x >> 16));
+      float v2 = (acc[mi][ni][2] + bb[ni].z) + bf16_to_f32((bf16_t)(r.y & 0xffffu));
+      float v3 = (acc[mi][ni][3] + bb[ni].w) + bf16_to_f32((bf16_t)(r.y >> 16));
       if (a.relu) { v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f); }
-      *reinterpret_cast<uint2*>(out + (long long)m * a.Cout + n) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+      if (m < M)
+        *reinterpret_cast<uint2*>(out + (long long)m * a.Cout + n) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
     }
   }
 }
@@ -428,7 +505,10 @@ template <typename T>
 int launch_conv(const ConvArgs& a, hipStream_t s) {
   const int M = a.B * a.H * a.W;
   // large images: 256 x 256 tiles (the 4x5 / 8x10 / 16x20 convs have their own kernels)
-  if (sizeof(T) == 2 && g_conv_big && a.Cout % 256 == 0 && !a.act_bias && !a.slot && M >= 64 * 1024) {
+  // conv_big addresses activation rows in 16-B units with 32-bit offsets
+  const bool span32 = ((long long)a.B * a.in_env_stride) / 8 < 0x7fff0000LL;
+  if (sizeof(T) == 2 && g_conv_big && a.Cout % 256 == 0 && a.Cin % 64 == 0 && !a.act_bias && !a.slot &&
+      M >= 64 * 1024 && span32) {
     static bool attr = false;
     if (!attr) {
       const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_big_bf16_kernel),
