@@ -474,7 +474,7 @@ def main():
                          "kernel": (f"{tower_kernel_name(B)} (fused dynamics / prediction step: 14-block residual "
                                     "tower, bf16 3x3 256->256 convs, M=B*20, N=256, K=2304 each)") if tower_launch_ms else
                                    (f"latent residual conv bf16 3x3 256->256 (M=B*{p.lh * p.lw},N=256,K=2304; "
-                                    f"{'conv_lat' if p.lh * p.lw <= 160 else 'conv_igemm'} kernel)"),
+                                    f"{'conv_lat' if p.lh * p.lw <= 160 else ('conv_big_bf16' if B * p.lh * p.lw >= 65536 and args.dtype == 'bf16' else 'conv_igemm')} kernel)"),
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": traffic,
                          "traffic_algorithmic_bytes": traffic_rec and traffic_rec.get("algorithmic_bytes"),
