@@ -143,14 +143,16 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
   __shared__ __attribute__((aligned(16))) uint8_t lds[G::BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / NB, x0 = (blockIdx.x % NB) * XT;
-  // stage the band: NSRC*16 rows x NCH chunks (UB loads in flight per thread), then the zero block
+  // stage the band: NSRC*16 rows x NCH chunks, then the zero block. Every load of the band is in
+  // flight at once (one memory round trip; batches of 4 per thread behind a `#pragma unroll 1` waited
+  // once per batch)
   {
     constexpr int N = NSRC * 16 * G::NCH;
-    constexpr int UB = N % (8 * BNT) == 0 ? 8 : 4;
+    constexpr int UB = (N + BNT - 1) / BNT;
     constexpr bool EXACT = N % (UB * BNT) == 0;  // else the last batch is partial (guarded)
     const bf16_t* src = a.in + (size_t)b * BH * BW * CIN;
-#pragma unroll 1
-    for (int i0 = 0; i0 < N; i0 += UB * BNT) {
+    {
+      const int i0 = 0;
       uint4 v[UB];
 #pragma unroll
       for (int u = 0; u < UB; ++u) {
@@ -194,21 +196,33 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
   // output tile in LDS: row 16 t + y, 16-B chunks swizzled by KEY[y]
   constexpr int ONCH = COUT / 8;
   bf16_t* gout = a.out + (size_t)b * BH * BW * COUT;
-  if (a.res) {  // stage the residual tile (coalesced)
+  if (a.res) {  // stage the residual tile (coalesced): every load in flight, then the LDS writes
     const bf16_t* gres = a.res + (size_t)b * BH * BW * COUT;
-    for (int i = tid; i < XT * 16 * ONCH; i += BNT) {
+    constexpr int NR = XT * 16 * ONCH, UR = (NR + BNT - 1) / BNT;
+    uint4 rv[UR];
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      const int i = min(u * BNT + tid, NR - 1);
       const int row = i / ONCH, ch = i % ONCH, t = row >> 4, y = row & 15;
-      *reinterpret_cast<uint4*>(lds + row * G::OB + ((ch ^ nib(KEY, y)) << 4)) =
-          *reinterpret_cast<const uint4*>(gres + (size_t)(y * BW + x0 + t) * COUT + ch * 8);
+      rv[u] = *reinterpret_cast<const uint4*>(gres + (size_t)(y * BW + x0 + t) * COUT + ch * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < UR; ++u) {
+      const int i = u * BNT + tid;
+      const int row = i / ONCH, ch = i % ONCH, y = row & 15;
+      if (NR % BNT == 0 || i < NR) *reinterpret_cast<uint4*>(lds + row * G::OB + ((ch ^ nib(KEY, y)) << 4)) = rv[u];
     }
     __syncthreads();
   }
   {
     const int q = lane >> 4, ys = nib(SIG, lane & 15), ky = nib(KEY, ys);
+    float4 bias4[CTW];  // every bias load in flight before the first use
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) bias4[ct] = *reinterpret_cast<const float4*>(a.bias + (wave * CTW + ct) * 16 + 4 * q);
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) {
       const int n = (wave * CTW + ct) * 16 + 4 * q;  // D[channel n + i][column j = lane & 15]
-      const float4 b4 = *reinterpret_cast<const float4*>(a.bias + n);
+      const float4 b4 = bias4[ct];
 #pragma unroll
       for (int t = 0; t < XT; ++t) {
         uint2* p = reinterpret_cast<uint2*>(lds + (t * 16 + ys) * G::OB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1));
