@@ -354,14 +354,33 @@ __device__ __forceinline__ void tower_heads(const TowerArgs& a, const uint8_t* _
     const bf16_t* wr = reinterpret_cast<const bf16_t*>(a.x.lw[hd]) + (size_t)el * K;
     const int er = el < nenv ? el : 0;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int s = wave; s < nk; s += NW) {
-      const int k = s * 32 + q * 8;
-      const int pos = k / C, c = hc0[hd] + (k - pos * C);
-      const int row = R8 ? t8::row8(er, pos) : trow(er, pos);
-      typename Elt<EL>::v8 av = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + img + toff(row, c >> 3));
-      if (el >= NE) av = typename Elt<EL>::v8{};
-      const typename Elt<EL>::v8 bv = *reinterpret_cast<const typename Elt<EL>::v8*>(wr + k);
-      acc = Elt<EL>::mfma(av, bv, acc);
+    // the wave's k steps s = wave + NW u in batches of HU: every weight load of a batch in flight
+    // before its first MFMA (one loop iteration per k step waited one L2 round trip each: 20-40
+    // per head and wave), MFMAs in the same order as before
+    constexpr int HU = 10;
+    for (int s0 = wave; s0 < nk; s0 += NW * HU) {
+      typename Elt<EL>::v8 bv[HU];
+#pragma unroll
+      for (int u = 0; u < HU; ++u) {
+        const int s = min(s0 + u * NW, nk - 1);
+        bv[u] = *reinterpret_cast<const typename Elt<EL>::v8*>(wr + s * 32 + q * 8);
+      }
+      auto kstep = [&](int u) {
+        const int k = (s0 + u * NW) * 32 + q * 8;
+        const int pos = k / C, c = hc0[hd] + (k - pos * C);
+        const int row = R8 ? t8::row8(er, pos) : trow(er, pos);
+        typename Elt<EL>::v8 av = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + img + toff(row, c >> 3));
+        if (el >= NE) av = typename Elt<EL>::v8{};
+        acc = Elt<EL>::mfma(av, bv[u], acc);
+      };
+      if (s0 + (HU - 1) * NW < nk) {  // whole batch (always, for K = 20 x 128 / 256 and NW = 4 / 8)
+#pragma unroll
+        for (int u = 0; u < HU; ++u) kstep(u);
+      } else {
+#pragma unroll
+        for (int u = 0; u < HU; ++u)
+          if (s0 + u * NW < nk) kstep(u);
+      }
     }
     if (4 * q < NE)  // D[row = env 4q + i][col = output el]
 #pragma unroll
