@@ -87,8 +87,9 @@ __global__ void root_init_kernel(TreeArgs t, const float* __restrict__ v_root, c
     nd.child[a] = -1;
   }
   nd.pad = 0;
-  t.calls[b] = 0;
-  const int a0 = ucb_select(nd, t, b);  // mcts.py:124
+  uint32_t k = 0;
+  const int a0 = ucb_select(nd, t, b, t.sqrt_tab, t.c_tab, k);  // mcts.py:124
+  t.calls[b] = k;
   t.nodes[(size_t)b * (t.S + 1)] = nd;
   t.root_sum[b] = v_root[b];  // mcts.py:110
   t.leaf_parent[b] = 0;

@@ -966,14 +966,23 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     tower8_writeback<EL, NQ, false, 2>(lds, accp, res, 0, ctp, lane);
     tower8_writeback<EL, NQ, false, 2>(lds, accv, res, 128, ctp, lane);
     __syncthreads();
+    // the ucb factor tables go to LDS for the tree walk (`part` is free after the heads): loaded
+    // here, stored after the heads, so the walk's per-level table reads are LDS reads
+    const int ntab = a.tree.S + 1;
+    const bool tab_lds = a.tree_on && ntab <= t8::NT;
+    float tsq = 0.f, tct = 0.f;
+    if (tab_lds && tid < ntab) { tsq = a.tree.sqrt_tab[tid]; tct = a.tree.c_tab[tid]; }
     const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
     tower_heads<EL, T8<NQ>::E, 4, true>(a, lds, 0, 2, hc0, hC, kind, part, lg, dec, env0, nenv, tid);
     if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
       __syncthreads();
+      if (tab_lds && tid < ntab) { part[tid] = tsq; part[ntab + tid] = tct; }
+      __syncthreads();
       if (tid < nenv) {
         const int b = env0 + tid;
         tree_backup_env(a.tree, a.tree_sim, b, a.tree_r[b], dec[1][tid][0], &dec[0][tid][0], a.tree_gamma);
-        if (a.tree_sim + 1 < a.tree.S) tree_select_env(a.tree, a.tree_sim + 1, b);
+        if (a.tree_sim + 1 < a.tree.S)
+          tree_select_env(a.tree, a.tree_sim + 1, b, tab_lds ? part : nullptr, tab_lds ? part + ntab : nullptr);
       }
     }
     return;
