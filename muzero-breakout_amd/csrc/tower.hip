@@ -882,24 +882,35 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
 #ifdef TOWER_STAMPS
   tstamp(TST_N - 3, true);
 #endif
+  // prologue loads in one round trip: the env's node-pool slot and action first (the oldest loads,
+  // so waiting for them leaves the rest in flight), then the weight ring's first k steps and every
+  // tower bias (at most BPT float4 per thread) before any of them is used. A per-element bias loop
+  // (load, LDS store) waited one round trip per iteration, 7 at 14 blocks, behind the ring loads.
+  int slot_b = 0, act_b = 0;
+  const int b_own = env0 + (tid < nenv ? tid : 0);
+  if (tid < T8<NQ>::E) {
+    if (a.slot) slot_b = a.slot[b_own];
+    if (pro) act_b = a.x.act[b_own];
+  }
   const WNext first = wnext(pro ? a.x.w0 : a.wf, TNS, ctw);
   tower8_preload(bq, first, lane);
   // where each wave's ring goes after the last tower conv: the epilogue conv it runs
   WNext epi = first;
   if (a.x.epilogue == 1) epi = wnext(a.x.we1, 8, ctw);
   // (epilogue 2 reloads its own 2-tile ring: the last tower conv's continuation loads re-read `first`)
+  constexpr int BPT = (T8_MAX_BLOCKS * 2 * TC / 4 + t8::NT - 1) / t8::NT;
+  const int n4 = a.nblocks * 2 * TC / 4;
+  float4 bv[BPT];
+#pragma unroll
+  for (int u = 0; u < BPT; ++u)
+    bv[u] = reinterpret_cast<const float4*>(a.bias)[min(u * t8::NT + tid, n4 - 1)];
   if (tid < T8<NQ>::E) {
-    const int b = env0 + (tid < nenv ? tid : 0);
-    long long off = (long long)b * a.in_env_stride;
-    if (a.slot) off += (long long)a.slot[b] * a.in_slot_stride;
-    envoff[tid] = off;
-    acts[tid] = pro ? a.x.act[b] : 0;
+    envoff[tid] = (long long)b_own * a.in_env_stride + (long long)slot_b * a.in_slot_stride;
+    acts[tid] = act_b;
   }
-  {  // tower biases -> LDS
-    const int n4 = a.nblocks * 2 * TC / 4;
-    for (int i = tid; i < n4; i += t8::NT)
-      reinterpret_cast<float4*>(biasl)[i] = reinterpret_cast<const float4*>(a.bias)[i];
-  }
+#pragma unroll
+  for (int u = 0; u < BPT; ++u)
+    if (u * t8::NT + tid < n4) reinterpret_cast<float4*>(biasl)[u * t8::NT + tid] = bv[u];
   __syncthreads();
   {  // stage X: ROWS x 32 chunks, 10 per thread per batch (NQ batches)
 #pragma unroll
