@@ -900,6 +900,8 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   // (epilogue 2 reloads its own 2-tile ring: the last tower conv's continuation loads re-read `first`)
   constexpr int BPT = (T8_MAX_BLOCKS * 2 * TC / 4 + t8::NT - 1) / t8::NT;
   const int n4 = a.nblocks * 2 * TC / 4;
+  // (indices past the table are clamped to its last element, loads and stores alike: a store under
+  // a condition makes the compiler sink its load into the branch and wait for it there)
   float4 bv[BPT];
 #pragma unroll
   for (int u = 0; u < BPT; ++u)
@@ -909,8 +911,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     acts[tid] = act_b;
   }
 #pragma unroll
-  for (int u = 0; u < BPT; ++u)
-    if (u * t8::NT + tid < n4) reinterpret_cast<float4*>(biasl)[u * t8::NT + tid] = bv[u];
+  for (int u = 0; u < BPT; ++u) reinterpret_cast<float4*>(biasl)[min(u * t8::NT + tid, n4 - 1)] = bv[u];
   __syncthreads();
   {  // stage X: ROWS x 32 chunks, 10 per thread per batch (NQ batches)
 #pragma unroll
