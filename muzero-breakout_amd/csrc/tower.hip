@@ -775,6 +775,14 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
       acc[rt][ct] = v;
     }
   }
+  // the initialised accumulators pinned to AGPRs before the k loops: left to the register
+  // allocator, the init values stayed in VGPRs and the dx = -1 / 0 loops of the tower convs copied
+  // 44-184 accumulator registers between the files on every dy iteration (v_accvgpr_read/write,
+  // up to 0.7 extra VALU per MFMA); with the pin every k loop is copy-free
+#pragma unroll
+  for (int rt = 0; rt < T8<NQ>::NRT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) asm volatile("" : "+a"(acc[rt][ct]));
   if (CENTER) {
     tower8_center<EL, NQ, CT>(lds, cur, bq, acc, lane);
   } else {
@@ -793,12 +801,19 @@ template <int EL, int NQ, bool SAVE, int CT = t8::CT>
 __device__ __forceinline__ void tower8_writeback(uint8_t* __restrict__ lds, const f32x4 (&acc)[T8<NQ>::NRT][CT],
                                                  uint2 (&res)[T8<NQ>::NRT][t8::CT], int nout, int ct0, int lane) {
   const int q = lane >> 4, l16 = lane & 15;
+  // row rt * 16 + l16 has swizzle key l16 for every rt: the lane's byte offset per column tile is
+  // computed once, the row tile is an immediate (toff per element re-derived it, 5 VALU per store)
+  int cofs[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int n = nout + (ct0 + ct) * 16 + 4 * q;
+    cofs[ct] = l16 * TROWB + (((n >> 3) ^ l16) << 4) + ((n & 7) << 1);
+  }
 #pragma unroll
   for (int rt = 0; rt < T8<NQ>::NRT; ++rt)
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      const int n = nout + (ct0 + ct) * 16 + 4 * q;
-      uint2* p = reinterpret_cast<uint2*>(lds + toff(rt * 16 + l16, n >> 3) + ((n & 7) << 1));
+      uint2* p = reinterpret_cast<uint2*>(lds + rt * 16 * TROWB + cofs[ct]);
       if (SAVE) res[rt][ct] = *p;
       uint2 o;
       o.x = relu_pk(Elt<EL>::pack2(acc[rt][ct][0], acc[rt][ct][1]));

@@ -1,9 +1,9 @@
 # A/B of two library builds on one box (headline acting bench, interleaved) after the whole GPU suite
 set -euo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/ab_prologue2
+O=gpurun_out/ab_agpr
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "fused or tower or fp16 or acting or episode or mcts or search" > $O/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 tail -2 $O/pytest.log
 for i in 1 2; do
   for lib in libmzba_prev.so libmzba.so; do
