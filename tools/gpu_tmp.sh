@@ -1,13 +1,11 @@
-# A/B of two library builds on one box (headline acting bench, interleaved) after the whole GPU suite
+# tower8 k-step schedule variants: phase stamps of the isolated tower (diagnostic builds), interleaved
 set -euo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/ab_agpr
+O=gpurun_out/sched
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
-tail -2 $O/pytest.log
 for i in 1 2; do
-  for lib in libmzba_prev.so libmzba.so; do
-    MZBA_LIB=$PWD/muzero-breakout_amd/mzba/$lib timeout -k 10 300 python bench.py --steps 6 --warmup 2 --no-cpu > $O/bench_${lib}_$i.json 2> $O/bench_${lib}_$i.err
-    python3 -c "import json,sys; d=json.load(open('$O/bench_${lib}_$i.json')); print('$lib', $i, round(d['value'],1), round(d['ms_per_step'],2), round(d['roofline']['frac'],4))"
+  for lib in libmzba_tstamp.so libmzba_tstamp_s1.so libmzba_tstamp_s2.so; do
+    TSTAMP_LIB=$lib timeout -k 10 120 python tools/stamp_tower.py 4096 14 $O/stamps_${lib}_$i.json > $O/log_${lib}_$i.txt 2>&1
+    python3 -c "import json; d=json.load(open('$O/stamps_${lib}_$i.json')); print('$lib', $i, d['launch_us'], d['cycles_per_conv'], round(d['clock_ghz'],3), d['phase_cycles'])"
   done
 done
