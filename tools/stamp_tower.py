@@ -76,6 +76,26 @@ def main():
            "kernel_cycles_per_wg": float(np.median(a[:, TST_N - 1] - a[:, 0])),
            "wave_skew_at_barrier1": float(np.median(
                np.ptp(a.reshape(-1, 4, TST_N)[:, :, 5 + 6 * 10], axis=1)))}
+    # launch timeline from the wave-0 real-time stamps (100 MHz, chip-wide): workgroup start / end
+    # relative to the first start, durations, and the span the launch adds beyond its workgroups
+    w0 = a.reshape(-1, 4, TST_N)[:, 0, :]
+    t0, t1 = w0[:, TST_N - 3] * 10e-3, w0[:, TST_N - 2] * 10e-3  # us
+    t1 = t1 - t0.min()
+    t0 = t0 - t0.min()
+    dur = t1 - t0
+    order = np.argsort(t0)
+    first, second = order[: len(order) // 2], order[len(order) // 2:]
+    out["timeline_us"] = {
+        "span": float(t1.max()), "wg_duration_min_med_max": [float(dur.min()), float(np.median(dur)), float(dur.max())],
+        "round1_start_spread": float(np.ptp(t0[first])), "round1_end_min_max": [float(t1[first].min()), float(t1[first].max())],
+        "round2_start_min_max": [float(t0[second].min()), float(t0[second].max())],
+        "round2_end_min_med_max": [float(t1[second].min()), float(np.median(t1[second])), float(t1[second].max())],
+        # workgroup i runs on XCD i % 8 (round-robin dispatch): per-XCD median duration and last end
+        "xcd_median_duration": [float(np.median(dur[x::8])) for x in range(8)],
+        "xcd_last_end": [float(t1[x::8].max()) for x in range(8)],
+        "xcd_clock_ghz": [float(np.median(((a.reshape(-1, 4, TST_N)[x::8, 0, TST_N - 1] - a.reshape(-1, 4, TST_N)[x::8, 0, 0])
+                                            / (w0[x::8, TST_N - 2] - w0[x::8, TST_N - 3]) * 0.1))) for x in range(8)],
+    }
     print(json.dumps(out))
     if len(sys.argv) > 3:
         json.dump(out, open(sys.argv[3], "w"), indent=1)
