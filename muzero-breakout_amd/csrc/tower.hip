@@ -592,6 +592,7 @@ MZ_DEV uint32_t relu_pk(uint32_t u) {
 struct WNext {
   __amdgpu_buffer_rsrc_t rs;  // buffer resource over the pack at the wave's first column tile
   int tstride;                // bytes per column tile (k steps x 1 KB)
+  int s0;                     // pack step of the conv's first ring entry (3x3: 24, dx = 0 first; 1x1: 0)
   // 16-B fragment of k step `step` of the wave's column tile + ct, this lane: buffer load with the
   // lane's offset in one VGPR and the (ct, step) offset in an SGPR
   MZ_DEV uint4 ld(int ct, int step, int lane) const {
@@ -604,80 +605,72 @@ struct WNext {
 };
 MZ_DEV WNext wnext(const void* w, int tns, int ct0) {
   const uint4* p = reinterpret_cast<const uint4*>(w) + (size_t)ct0 * tns * 64;
-  return WNext{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(p), 0, 0x7fffffff, 0x00020000), tns * 1024};
+  return WNext{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(p), 0, 0x7fffffff, 0x00020000), tns * 1024,
+               tns == TNS ? 24 : 0};
 }
 
-// Weight ring of one wave: its 4 column tiles x TD k steps in flight (bq). The ring runs across
-// conv boundaries: the last TD loads of a 3x3 conv fetch the NEXT conv's first k steps (`wn`, the
-// next pack at this wave's first column tile + lane, `tnsn` k steps per tile), so those loads fly
-// through the epilogue and both barriers (a workgroup barrier waits for LDS, not for vmcnt) and the
-// next conv's first MFMAs find their weights in registers.
-template <int EL, int NQ, int DX, int CT = t8::CT, class G = Geo45<NQ>>
-__device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
+// Weight ring of one wave: its CT column tiles x TD k-step entries in flight (bq). A 3x3 conv walks
+// its 72 k steps as a sequence of entries: the dx = 0 taps first (entries 0..23 = pack steps 24..47,
+// dy-major, 8 channel steps per dy), then the dx = -1 and dx = +1 taps merged (entries 24..71: per
+// (dy, channel step) the dx = -1 step, then the dx = +1 step: pack steps 0, 48, 1, 49, ...). The
+// ring runs across conv boundaries: the last TD entries of a 3x3 conv fetch the NEXT conv's first
+// entries (`nxt`: pack steps nxt.s0 .. +TD-1), so those loads fly through the epilogue and both
+// barriers (a workgroup barrier waits for LDS, not for vmcnt) and the next conv's first MFMAs find
+// their weights in registers.
+static_assert(TD % 2 == 0, "the merged dx = -1 / +1 phase consumes entries in pairs");
+
+// A-row addressing of lane (y, e) for latent row shift dy over a whole image (every tile a source):
+// byte offset of its row in tile 0 (or of its zero-block row), the per-tile stride (0 for zero rows)
+// and the swizzle key
+template <class G>
+MZ_DEV void t8_rows(int y, int e, int dy, int& b, int& ts, int& w) {
+  const int yy = y + dy;
+  const bool ok = (unsigned)yy < (unsigned)G::YS;
+  const int key = (yy & (G::YS - 1)) * G::EG + e;
+  b = ok ? key * TROWB : G::LZ + key * TROWB;
+  ts = ok ? 16 * TROWB : 0;
+  w = key << 4;
+}
+
+// the dx = 0 taps (entries 0..23): every tile is a source and an output, 10 A reads feed 40 MFMAs
+template <int EL, int NQ, int CT = t8::CT, class G = Geo45<NQ>>
+__device__ __forceinline__ void tower8_d0(const uint8_t* __restrict__ lds, const WNext& cur,
                                           uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
   static_assert(G::GROUPS * G::TX == T8<NQ>::NRT, "geometry and accumulator tiles");
-  constexpr int TX = G::TX, EG = G::EG, YS = G::YS;
-  constexpr int NX = DX == 0 ? TX : TX - 1;  // active x tiles per group
-  constexpr int NA = G::GROUPS * NX;         // active tiles
-  constexpr int A0 = DX < 0 ? 1 : 0;         // first accumulator x tile
-  constexpr int S0 = DX > 0 ? 1 : 0;         // first source x tile
-  constexpr int SB = (DX + 1) * 24;          // first k step of this column shift
-  const int q = lane >> 4, y = (lane & 15) / EG, e = lane & (EG - 1);
-  // A-row addressing of this lane for latent row shift dy (zero rows: this image's own zero block)
-  auto rows = [&](int dy, int& b, int& ts, int& w) {
-    const int yy = y + dy;
-    const bool ok = (unsigned)yy < (unsigned)YS;
-    const int key = (yy & (YS - 1)) * EG + e;
-    b = ok ? S0 * 16 * TROWB + key * TROWB : G::LZ + key * TROWB;
-    ts = ok ? 16 * TROWB : 0;
-    w = key << 4;
-  };
+  constexpr int NA = G::GROUPS * G::TX, NC = TC / 32;
+  const int q = lane >> 4, y = (lane & 15) / G::EG, e = lane & (G::EG - 1);
   int base, tst, sw;
-  rows(-1, base, tst, sw);
-  // active tile j: group j / NX, x tile j % NX -> source tile index (in 16-row tiles from S0)
-  auto soff = [&](int j, int b, int ts) { return b + ((j / NX) * TX + (j % NX)) * ts; };
+  t8_rows<G>(y, e, -1, base, tst, sw);
   typename Elt<EL>::v8 afc[NA], afn[NA];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, base, tst) + ((q << 4) ^ sw));
-  constexpr int NC = TC / 32;
+  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + ((q << 4) ^ sw));
 #pragma unroll 1
   for (int dyi = 0; dyi < 3; ++dyi) {
     int nbase, ntst, nsw;
-    rows(dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+    t8_rows<G>(y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+    const bool last = dyi == 2;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      const int s = SB + dyi * NC + c;
       typename Elt<EL>::v8 w[CT];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
-        if (DX == 1 && c + TD >= NC) {  // the last TD steps of dy = +1 fetch the next conv's first steps
-          const bool last = dyi == 2;
-          const __amdgpu_buffer_rsrc_t rs = last ? nxt.rs : cur.rs;
-          const int so = last ? ct * nxt.tstride + (c + TD - NC) * 1024 : ct * (TNS * 1024) + (s + TD) * 1024;
-          bq[ct][c % TD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
-        } else {
-#if TOWER_ABLATE == 1  // diagnostic only: weights from one L1-resident pair of k steps
-          bq[ct][c % TD] = cur.ld3(ct, (s + TD) & 1, lane);
-#else
-          bq[ct][c % TD] = cur.ld3(ct, s + TD, lane);
-#endif
+        // entry dyi * 8 + c + TD: pack step 24 + that, or at dy = +1 the merged phase's first entries
+        int so = ct * (TNS * 1024) + (24 + dyi * NC + c + TD) * 1024;
+        if (c + TD >= NC) {
+          const int m = c + TD - NC;
+          so = last ? ct * (TNS * 1024) + ((m & 1) * 48 + (m >> 1)) * 1024 : so;
         }
+        bq[ct][c % TD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cur.rs, lane * 16, so, 0));
       }
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
-        const int at = (j / NX) * TX + A0 + (j % NX);
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-          acc[at][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[at][ct]);
-        if (TOWER_ABLATE == 2)  // diagnostic only: no LDS A reads inside the loop
-          afn[j] = afc[j];
-        else if (TOWER_ABLATE == 3 && c % 3 != 0)  // diagnostic only: 2 of 3 A fragments by DPP row shift
-          afn[j] = dpp_shl4<EL>(afc[j]);
-        else if (c + 1 < NC)
-          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, base, tst) + (((4 * (c + 1) + q) << 4) ^ sw));
+        for (int ct = 0; ct < CT; ++ct) acc[j][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[j][ct]);
+        if (c + 1 < NC)
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
         else
-          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + soff(j, nbase, ntst) + ((q << 4) ^ nsw));
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
       }
       // schedule: every A read of the next k step in the first NA MFMA slots (the compiler orders a
       // step's independent MFMAs freely, so the next step may open with any tile: its reads must have
@@ -694,6 +687,81 @@ __device__ __forceinline__ void tower8_dx(const uint8_t* __restrict__ lds, const
         __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
       __builtin_amdgcn_sched_group_barrier(0x008, NA * CT - NA - 2 * CT, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) afc[j] = afn[j];
+    }
+    base = nbase; tst = ntst; sw = nsw;
+  }
+}
+
+// the dx = -1 and dx = +1 taps merged (entries 24..71): per (dy, channel step) every tile is read
+// once and feeds both shifts — source tile x with the dx = -1 weights into output tile x + 1 and
+// with the dx = +1 weights into output tile x - 1 (within its group). 10 A reads + 8 weight
+// fragments feed 64 MFMAs per step at NQ = 2 (separate dx = -1 / +1 loops: 2 x (8 A reads + 4
+// fragments) for 2 x 32 MFMAs, and 24 more k steps per conv, each with its fixed cost)
+template <int EL, int NQ, int CT = t8::CT, class G = Geo45<NQ>>
+__device__ __forceinline__ void tower8_dpm(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
+                                           uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
+  constexpr int TX = G::TX, NA = G::GROUPS * TX, NC = TC / 32;
+  constexpr int NM = G::GROUPS * (TX - 1) * 2 * CT;  // MFMAs per merged step
+  static_assert(NM >= NA + 4 * CT, "schedule groups");
+  const int q = lane >> 4, y = (lane & 15) / G::EG, e = lane & (G::EG - 1);
+  int base, tst, sw;
+  t8_rows<G>(y, e, -1, base, tst, sw);
+  typename Elt<EL>::v8 afc[NA], afn[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + ((q << 4) ^ sw));
+#pragma unroll 1
+  for (int dyi = 0; dyi < 3; ++dyi) {
+    int nbase, ntst, nsw;
+    t8_rows<G>(y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+    const bool last = dyi == 2;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      typename Elt<EL>::v8 wm[CT], wp[CT];
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int slot = (2 * c + d) % TD;
+          (d ? wp : wm)[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][slot]);
+          // entry 2 (dyi * 8 + c) + d + TD of this phase: pack step 48 d + dyi * 8 + c + TD / 2, or at
+          // dy = +1 past the conv's end the next conv's entry nn = 2 c + d + TD - 16
+          int so = ct * (TNS * 1024) + (48 * d + dyi * NC + c + TD / 2) * 1024;
+          __amdgpu_buffer_rsrc_t rs = cur.rs;
+          if (2 * c + d + TD >= 2 * NC) {
+            const int nn = 2 * c + d + TD - 2 * NC;
+            so = last ? ct * nxt.tstride + (nxt.s0 + nn) * 1024 : so;
+            rs = last ? nxt.rs : cur.rs;
+          }
+          bq[ct][slot] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
+        }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int g0 = (j / TX) * TX, x = j % TX;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          if (x + 1 < TX) acc[g0 + x + 1][ct] = Elt<EL>::mfma(wm[ct], afc[j], acc[g0 + x + 1][ct]);
+          if (x >= 1) acc[g0 + x - 1][ct] = Elt<EL>::mfma(wp[ct], afc[j], acc[g0 + x - 1][ct]);
+        }
+        if (c + 1 < NC)
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
+        else
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+      }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 2 * CT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NM - NA - 4 * CT, 0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NA; ++j) afc[j] = afn[j];
@@ -733,14 +801,14 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
   }
 }
 
-// the first TD k steps of a pack into the ring (the kernel's first conv; later convs are fetched by
-// their predecessor)
+// the first TD ring entries of a pack (the kernel's first conv; later convs are fetched by their
+// predecessor)
 template <int CT = t8::CT>
 MZ_DEV void tower8_preload(uint4 (&bq)[CT][TD], const WNext& p, int lane) {
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-    for (int i = 0; i < TD; ++i) bq[ct][i] = p.ld(ct, i, lane);
+    for (int i = 0; i < TD; ++i) bq[ct][i] = p.ld(ct, p.s0 + i, lane);
 }
 
 // k loop of one conv over the 8-env image: this wave's 4 channel tiles cur.ct0..+3 of a weight pack
@@ -786,11 +854,10 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
   if (CENTER) {
     tower8_center<EL, NQ, CT>(lds, cur, bq, acc, lane);
   } else {
-    tower8_dx<EL, NQ, -1, CT, G>(lds, cur, nxt, bq, acc, lane);
+    tower8_d0<EL, NQ, CT, G>(lds, cur, bq, acc, lane);
     TSTAMP(3 + 6 * ci);
-    tower8_dx<EL, NQ, 0, CT, G>(lds, cur, nxt, bq, acc, lane);
     TSTAMP(4 + 6 * ci);
-    tower8_dx<EL, NQ, 1, CT, G>(lds, cur, nxt, bq, acc, lane);
+    tower8_dpm<EL, NQ, CT, G>(lds, cur, nxt, bq, acc, lane);
   }
   TSTAMP(5 + 6 * ci);
 }
