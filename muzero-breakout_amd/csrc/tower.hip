@@ -90,6 +90,12 @@ constexpr int TNS = 9 * TC / 32;   // 72 k steps per 3x3 conv
 #endif
 constexpr int TD = TOWER_TD;       // weight ring depth (k steps); must divide the 8 steps of a tap
 static_assert(8 % TD == 0, "ring index restarts at every tap");
+// tower8 k loop per kernel: the 8-env kernel (NQ = 2, and the representation tail's 2-env 8x10
+// geometry) walks all three column shifts in one pass with a ring of 3 entries (one k step ahead); the
+// one-quad kernel (NQ = 1: half the MFMAs per k step, weight-stream bound) keeps two passes (dx = 0,
+// then dx = -1 / +1 merged) and a ring of TD entries: one pass with a 3-entry ring was 6 % slower there
+template <int NQ> constexpr bool t8all = NQ == 2;
+template <int NQ> constexpr int t8d = t8all<NQ> ? 3 : TD;  // ring depth in entries
 #ifndef TOWER_ABLATE
 #define TOWER_ABLATE 0  // diagnostic builds only (make tower-variants): 1 hot weights, 2 no LDS A reads,
                         // 3 duplicate weight streams (waves w, w+4), 4 = 3 with waves 4-7 started late
@@ -592,7 +598,7 @@ MZ_DEV uint32_t relu_pk(uint32_t u) {
 struct WNext {
   __amdgpu_buffer_rsrc_t rs;  // buffer resource over the pack at the wave's first column tile
   int tstride;                // bytes per column tile (k steps x 1 KB)
-  int s0;                     // pack step of the conv's first ring entry (3x3: 24, dx = 0 first; 1x1: 0)
+  int s0;                     // 3x3 pack: 24 (ring entries in the order below); 1x1 pack: 0 (entry n = step n)
   // 16-B fragment of k step `step` of the wave's column tile + ct, this lane: buffer load with the
   // lane's offset in one VGPR and the (ct, step) offset in an SGPR
   MZ_DEV uint4 ld(int ct, int step, int lane) const {
@@ -608,16 +614,22 @@ MZ_DEV WNext wnext(const void* w, int tns, int ct0) {
   return WNext{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(p), 0, 0x7fffffff, 0x00020000), tns * 1024,
                tns == TNS ? 24 : 0};
 }
+// pack step of ring entry n (< ring depth) of a conv: 3x3 packs walk dx = 0 first (steps 24, 25, ...),
+// or in one pass the three shifts of each (dy, channel step) together (steps 0, 24, 48, 1, 25, 49, ...)
+template <bool ALL>
+MZ_DEV int t8_first(const WNext& p, int n) {
+  return ALL ? (p.s0 ? 24 * (n % 3) + n / 3 : n) : p.s0 + n;
+}
 
-// Weight ring of one wave: its CT column tiles x TD k-step entries in flight (bq). A 3x3 conv walks
+// Weight ring of one wave: its CT column tiles x RD k-step entries in flight (bq). A two-pass 3x3 conv walks
 // its 72 k steps as a sequence of entries: the dx = 0 taps first (entries 0..23 = pack steps 24..47,
 // dy-major, 8 channel steps per dy), then the dx = -1 and dx = +1 taps merged (entries 24..71: per
 // (dy, channel step) the dx = -1 step, then the dx = +1 step: pack steps 0, 48, 1, 49, ...). The
-// ring runs across conv boundaries: the last TD entries of a 3x3 conv fetch the NEXT conv's first
-// entries (`nxt`: pack steps nxt.s0 .. +TD-1), so those loads fly through the epilogue and both
+// ring runs across conv boundaries: the last RD entries of a 3x3 conv fetch the NEXT conv's first
+// entries (`nxt`, t8_first), so those loads fly through the epilogue and both
 // barriers (a workgroup barrier waits for LDS, not for vmcnt) and the next conv's first MFMAs find
 // their weights in registers.
-static_assert(TD % 2 == 0, "the merged dx = -1 / +1 phase consumes entries in pairs");
+static_assert(TD % 2 == 0, "the merged dx = -1 / +1 pass consumes entries in pairs");
 
 // A-row addressing of lane (y, e) for latent row shift dy over a whole image (every tile a source):
 // byte offset of its row in tile 0 (or of its zero-block row), the per-tile stride (0 for zero rows)
@@ -635,7 +647,8 @@ MZ_DEV void t8_rows(int y, int e, int dy, int& b, int& ts, int& w) {
 // the dx = 0 taps (entries 0..23): every tile is a source and an output, 10 A reads feed 40 MFMAs
 template <int EL, int NQ, int CT = t8::CT, class G = Geo45<NQ>>
 __device__ __forceinline__ void tower8_d0(const uint8_t* __restrict__ lds, const WNext& cur,
-                                          uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
+                                          uint4 (&bq)[CT][t8d<NQ>], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
+  constexpr int RD = t8d<NQ>;
   static_assert(G::GROUPS * G::TX == T8<NQ>::NRT, "geometry and accumulator tiles");
   constexpr int NA = G::GROUPS * G::TX, NC = TC / 32;
   const int q = lane >> 4, y = (lane & 15) / G::EG, e = lane & (G::EG - 1);
@@ -654,14 +667,14 @@ __device__ __forceinline__ void tower8_d0(const uint8_t* __restrict__ lds, const
       typename Elt<EL>::v8 w[CT];
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
-        w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
-        // entry dyi * 8 + c + TD: pack step 24 + that, or at dy = +1 the merged phase's first entries
-        int so = ct * (TNS * 1024) + (24 + dyi * NC + c + TD) * 1024;
-        if (c + TD >= NC) {
-          const int m = c + TD - NC;
+        w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % RD]);
+        // entry dyi * 8 + c + RD: pack step 24 + that, or at dy = +1 the merged phase's first entries
+        int so = ct * (TNS * 1024) + (24 + dyi * NC + c + RD) * 1024;
+        if (c + RD >= NC) {
+          const int m = c + RD - NC;
           so = last ? ct * (TNS * 1024) + ((m & 1) * 48 + (m >> 1)) * 1024 : so;
         }
-        bq[ct][c % TD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cur.rs, lane * 16, so, 0));
+        bq[ct][c % RD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cur.rs, lane * 16, so, 0));
       }
 #pragma unroll
       for (int j = 0; j < NA; ++j) {
@@ -702,7 +715,8 @@ __device__ __forceinline__ void tower8_d0(const uint8_t* __restrict__ lds, const
 // fragments) for 2 x 32 MFMAs, and 24 more k steps per conv, each with its fixed cost)
 template <int EL, int NQ, int CT = t8::CT, class G = Geo45<NQ>>
 __device__ __forceinline__ void tower8_dpm(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
-                                           uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
+                                           uint4 (&bq)[CT][t8d<NQ>], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
+  constexpr int RD = t8d<NQ>;
   constexpr int TX = G::TX, NA = G::GROUPS * TX, NC = TC / 32;
   constexpr int NM = G::GROUPS * (TX - 1) * 2 * CT;  // MFMAs per merged step
   static_assert(NM >= NA + 4 * CT, "schedule groups");
@@ -724,15 +738,15 @@ __device__ __forceinline__ void tower8_dpm(const uint8_t* __restrict__ lds, cons
       for (int d = 0; d < 2; ++d)
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          const int slot = (2 * c + d) % TD;
+          const int slot = (2 * c + d) % RD;
           (d ? wp : wm)[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][slot]);
-          // entry 2 (dyi * 8 + c) + d + TD of this phase: pack step 48 d + dyi * 8 + c + TD / 2, or at
-          // dy = +1 past the conv's end the next conv's entry nn = 2 c + d + TD - 16
-          int so = ct * (TNS * 1024) + (48 * d + dyi * NC + c + TD / 2) * 1024;
+          // entry 2 (dyi * 8 + c) + d + RD of this phase: pack step 48 d + dyi * 8 + c + RD / 2, or at
+          // dy = +1 past the conv's end the next conv's entry nn = 2 c + d + RD - 16
+          int so = ct * (TNS * 1024) + (48 * d + dyi * NC + c + RD / 2) * 1024;
           __amdgpu_buffer_rsrc_t rs = cur.rs;
-          if (2 * c + d + TD >= 2 * NC) {
-            const int nn = 2 * c + d + TD - 2 * NC;
-            so = last ? ct * nxt.tstride + (nxt.s0 + nn) * 1024 : so;
+          if (2 * c + d + RD >= 2 * NC) {
+            const int nn = 2 * c + d + RD - 2 * NC;
+            so = last ? ct * nxt.tstride + t8_first<t8all<NQ>>(nxt, nn) * 1024 : so;
             rs = last ? nxt.rs : cur.rs;
           }
           bq[ct][slot] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
@@ -770,11 +784,86 @@ __device__ __forceinline__ void tower8_dpm(const uint8_t* __restrict__ lds, cons
   }
 }
 
+// all three column shifts in one pass (NQ = 2): per (dy, channel step) every tile is read once
+// and feeds dx = 0 (output x), dx = -1 (output x + 1) and dx = +1 (output x - 1); 24 k steps per conv
+template <int EL, int NQ, int CT = t8::CT, class G = Geo45<NQ>>
+__device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
+                                            uint4 (&bq)[CT][t8d<NQ>], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
+  constexpr int RD = t8d<NQ>;
+  constexpr int TX = G::TX, NA = G::GROUPS * TX, NC = TC / 32;
+  constexpr int NM = G::GROUPS * (3 * TX - 2) * CT;  // MFMAs per step
+  static_assert(RD % 3 == 0 && NM >= NA + 6 * CT, "ring triples, schedule groups");
+  const int q = lane >> 4, y = (lane & 15) / G::EG, e = lane & (G::EG - 1);
+  int base, tst, sw;
+  t8_rows<G>(y, e, -1, base, tst, sw);
+  typename Elt<EL>::v8 afc[NA], afn[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + ((q << 4) ^ sw));
+#pragma unroll 1
+  for (int dyi = 0; dyi < 3; ++dyi) {
+    int nbase, ntst, nsw;
+    t8_rows<G>(y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+    const bool last = dyi == 2;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      typename Elt<EL>::v8 w[3][CT];
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          const int slot = (3 * c + d) % RD;
+          w[d][ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][slot]);
+          // entry 3 (dyi * 8 + c) + d + RD: pack step 24 d + dyi * 8 + c + RD / 3, or at dy = +1 past
+          // the conv's end the next conv's entry nn = 3 c + d + RD - 24
+          int so = ct * (TNS * 1024) + (24 * d + dyi * NC + c + RD / 3) * 1024;
+          __amdgpu_buffer_rsrc_t rs = cur.rs;
+          if (3 * c + d + RD >= 3 * NC) {
+            const int nn = 3 * c + d + RD - 3 * NC;
+            so = last ? ct * nxt.tstride + t8_first<t8all<NQ>>(nxt, nn) * 1024 : so;
+            rs = last ? nxt.rs : cur.rs;
+          }
+          bq[ct][slot] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
+        }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int g0 = (j / TX) * TX, x = j % TX;
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          acc[g0 + x][ct] = Elt<EL>::mfma(w[1][ct], afc[j], acc[g0 + x][ct]);
+          if (x + 1 < TX) acc[g0 + x + 1][ct] = Elt<EL>::mfma(w[0][ct], afc[j], acc[g0 + x + 1][ct]);
+          if (x >= 1) acc[g0 + x - 1][ct] = Elt<EL>::mfma(w[2][ct], afc[j], acc[g0 + x - 1][ct]);
+        }
+        if (c + 1 < NC)
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
+        else
+          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+      }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 3 * CT; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NM - NA - 6 * CT, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) afc[j] = afn[j];
+    }
+    base = nbase; tst = ntst; sw = nsw;
+  }
+}
+
 // the 8 k steps of a 1x1 conv on the 8-env image (centre tap: all 10 tiles, every row valid); always
 // the last conv of a launch, so the ring is not continued
 template <int EL, int NQ, int CT = t8::CT>
 __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, const WNext& cur,
-                                              uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
+                                              uint4 (&bq)[CT][t8d<NQ>], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
+  constexpr int RD = t8d<NQ>;
   const int q = lane >> 4, key = lane & 15;
   const int base = key * TROWB, sw = key << 4;
   typename Elt<EL>::v8 afc[T8<NQ>::NRT], afn[T8<NQ>::NRT];
@@ -785,8 +874,8 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
     typename Elt<EL>::v8 w[CT];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) {
-      w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % TD]);
-      if (c + TD < 8) bq[ct][c % TD] = cur.ld(ct, c + TD, lane);
+      w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % RD]);
+      if (c + RD < 8) bq[ct][c % RD] = cur.ld(ct, c + RD, lane);
     }
 #pragma unroll
     for (int j = 0; j < T8<NQ>::NRT; ++j) {
@@ -801,14 +890,14 @@ __device__ __forceinline__ void tower8_center(const uint8_t* __restrict__ lds, c
   }
 }
 
-// the first TD ring entries of a pack (the kernel's first conv; later convs are fetched by their
+// the first ring entries of a pack (the kernel's first conv; later convs are fetched by their
 // predecessor)
-template <int CT = t8::CT>
-MZ_DEV void tower8_preload(uint4 (&bq)[CT][TD], const WNext& p, int lane) {
+template <int CT, int NQ>
+MZ_DEV void tower8_preload(uint4 (&bq)[CT][t8d<NQ>], const WNext& p, int lane) {
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-    for (int i = 0; i < TD; ++i) bq[ct][i] = p.ld(ct, p.s0 + i, lane);
+    for (int i = 0; i < t8d<NQ>; ++i) bq[ct][i] = p.ld(ct, t8_first<t8all<NQ>>(p, i), lane);
 }
 
 // k loop of one conv over the 8-env image: this wave's 4 channel tiles cur.ct0..+3 of a weight pack
@@ -820,7 +909,7 @@ template <int EL, int NQ, int MODE, bool CENTER, int CT = t8::CT, class G = Geo4
 __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
                                            int ct0, const float* __restrict__ bconv, const float* __restrict__ actb,
                                            const int* acts, int A, const uint2 (&res)[T8<NQ>::NRT][t8::CT],
-                                           uint4 (&bq)[CT][TD], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane,
+                                           uint4 (&bq)[CT][t8d<NQ>], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane,
                                            int ci = 0) {
   const int q = lane >> 4, l16 = lane & 15;
   TSTAMP(2 + 6 * ci);
@@ -854,10 +943,16 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
   if (CENTER) {
     tower8_center<EL, NQ, CT>(lds, cur, bq, acc, lane);
   } else {
-    tower8_d0<EL, NQ, CT, G>(lds, cur, bq, acc, lane);
-    TSTAMP(3 + 6 * ci);
-    TSTAMP(4 + 6 * ci);
-    tower8_dpm<EL, NQ, CT, G>(lds, cur, nxt, bq, acc, lane);
+    if constexpr (t8all<NQ>) {
+      TSTAMP(3 + 6 * ci);
+      TSTAMP(4 + 6 * ci);
+      tower8_dall<EL, NQ, CT, G>(lds, cur, nxt, bq, acc, lane);
+    } else {
+      tower8_d0<EL, NQ, CT, G>(lds, cur, bq, acc, lane);
+      TSTAMP(3 + 6 * ci);
+      TSTAMP(4 + 6 * ci);
+      tower8_dpm<EL, NQ, CT, G>(lds, cur, nxt, bq, acc, lane);
+    }
   }
   TSTAMP(5 + 6 * ci);
 }
@@ -927,7 +1022,7 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
 template <int EL, int NQ, bool RESID, class G = Geo45<NQ>>
 __device__ __forceinline__ void tower8_conv(uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt, int ct0,
                                             const float* __restrict__ bconv, uint2 (&res)[T8<NQ>::NRT][t8::CT],
-                                            uint4 (&bq)[t8::CT][TD], int lane, int ci) {
+                                            uint4 (&bq)[t8::CT][t8d<NQ>], int lane, int ci) {
   f32x4 acc[T8<NQ>::NRT][t8::CT];
   tower8_acc<EL, NQ, RESID ? 1 : 0, false, t8::CT, G>(lds, cur, nxt, ct0, bconv, nullptr, nullptr, 0, res, bq, acc, lane, ci);
   __syncthreads();  // every wave has read the whole image
@@ -959,7 +1054,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;
   // the weight ring's first k steps fly while the image is staged
-  uint4 bq[t8::CT][TD];
+  uint4 bq[t8::CT][t8d<NQ>];
   TSTAMP(0);
 #ifdef TOWER_STAMPS
   tstamp(TST_N - 3, true);
@@ -975,7 +1070,7 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     if (pro) act_b = a.x.act[b_own];
   }
   const WNext first = wnext(pro ? a.x.w0 : a.wf, TNS, ctw);
-  tower8_preload(bq, first, lane);
+  tower8_preload<t8::CT, NQ>(bq, first, lane);
   // where each wave's ring goes after the last tower conv: the epilogue conv it runs
   WNext epi = first;
   if (a.x.epilogue == 1) epi = wnext(a.x.we1, 8, ctw);
@@ -1051,9 +1146,9 @@ __global__ __launch_bounds__(t8::NT, 1) void tower8_kernel(TowerArgs a) {
     // two left two SIMDs idle for most of a conv)
     const int ctp = wave * 2;
     f32x4 accp[T8<NQ>::NRT][2], accv[T8<NQ>::NRT][2];
-    uint4 bq2[2][TD];
+    uint4 bq2[2][t8d<NQ>];
     const WNext wp3 = wnext(a.x.we3, TNS, ctp), wv1 = wnext(a.x.we1, 8, ctp);
-    tower8_preload<2>(bq2, wp3, lane);
+    tower8_preload<2, NQ>(bq2, wp3, lane);
     tower8_acc<EL, NQ, 0, false, 2>(lds, wp3, wv1, ctp, a.x.be3, nullptr, nullptr, 0, res, bq2, accp, lane);
     tower8_acc<EL, NQ, 0, true, 2>(lds, wv1, wv1, ctp, a.x.be1, nullptr, nullptr, 0, res, bq2, accv, lane);
     __syncthreads();
@@ -1122,8 +1217,8 @@ __global__ __launch_bounds__(t8::NT, 1) void rep_tail_kernel(RepTailArgs a) {
   const int ctw = wave * t8::CT;
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;
-  uint4 bq[t8::CT][TD];
-  tower8_preload(bq, wnext(a.wf, TNS, ctw), lane);  // flies while the input is pooled and staged
+  uint4 bq[t8::CT][t8d<2>];
+  tower8_preload<t8::CT, 2>(bq, wnext(a.wf, TNS, ctw), lane);  // flies while the input is pooled and staged
   {
     const int n4 = a.nblocks * 2 * TC / 4;
     for (int i = tid; i < n4; i += t8::NT) reinterpret_cast<float4*>(biasl)[i] = reinterpret_cast<const float4*>(a.bias)[i];
