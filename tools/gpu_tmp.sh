@@ -1,20 +1,8 @@
-# tower8: one-pass k loop at NQ = 2 (ring 3), two passes at NQ = 1: full GPU suite + smoke, then A/B
-# against the previous commit's build (libmzba_base.so)
+# round run on the one-pass tower (profiles/r02/r2j) + tower8 phase stamps at B = 4096
 set -euo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/mix
-mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -2 $O/pytest.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
-tail -1 $O/smoke.log
-export MZBA_LIB_PARTIAL=1
-M=$PWD/muzero-breakout_amd/mzba
-bash tools/ab_tower.sh $O/conv libmzba_base.so libmzba.so
-for B in 4096 1024; do
-  for lib in libmzba_base.so libmzba.so libmzba_base.so libmzba.so; do
-    MZBA_LIB=$M/$lib timeout -k 10 300 python bench.py --envs $B --steps 6 --warmup 2 --no-cpu > $O/bench_${B}_$lib.json 2> $O/bench_${B}_$lib.err
-    python3 -c "import json; d=json.load(open('$O/bench_${B}_$lib.json')); print($B, '$lib', round(d['value'],1), round(d['roofline']['frac'],4), round(d['whole_step_mfma_frac'],4))"
-  done
-done
-echo "mix done"
+bash tools/gpu_round.sh r2j
+O=gpurun_out/r2j
+timeout -k 10 120 python tools/stamp_tower.py 4096 14 $O/stamps_4096.json > $O/stamps_log.txt 2>&1 || { tail $O/stamps_log.txt; exit 1; }
+python3 -c "import json; d=json.load(open('$O/stamps_4096.json')); print(d['launch_us'], d['clock_ghz'], d['cycles_per_conv'], d['mfma_frac_in_conv'], d['phase_cycles'])"
+echo "r2j done"

@@ -5,7 +5,7 @@ make -C muzero-breakout_amd/csrc tower-stamps -> libmzba_tstamp.so).
 
 Runs the plain tower (8-env kernel, random bf16 weights / inputs) 30 times, reads the stamps of the
 last launch and prints per-conv medians (over workgroups and waves) of: the k loop split by column
-shift (dx = -1 / 0 / +1), the wait at the first barrier, the write-back + second barrier, the
+pass (one pass over all three column shifts in the 8-env kernel), the wait at the first barrier, the write-back + second barrier, the
 in-kernel clock (s_memtime / s_memrealtime x 100 MHz), and the MFMA-only floor of a conv
 (2496 v_mfma_f32_16x16x32_bf16 per wave x 16 cycles). The stamps' own cost perturbs the phases a
 little; the shares are what count."""
@@ -57,9 +57,9 @@ def main():
     for ci in range(nconv):
         s = a[:, 2 + 6 * ci: 8 + 6 * ci]
         nxt = a[:, 2 + 6 * (ci + 1)] if ci + 1 < nconv else a[:, TST_N - 1]
-        ph[:, ci, 0] = s[:, 1] - s[:, 0]  # bias init + dx -1
-        ph[:, ci, 1] = s[:, 2] - s[:, 1]  # dx 0
-        ph[:, ci, 2] = s[:, 3] - s[:, 2]  # dx +1
+        ph[:, ci, 0] = s[:, 1] - s[:, 0]  # bias init (+ the dx 0 pass of a two-pass k loop)
+        ph[:, ci, 1] = s[:, 2] - s[:, 1]  # (empty since the passes were merged)
+        ph[:, ci, 2] = s[:, 3] - s[:, 2]  # the one-pass k loop (or the dx -1 / +1 pass)
         ph[:, ci, 3] = s[:, 4] - s[:, 3]  # first barrier wait
         ph[:, ci, 4] = s[:, 5] - s[:, 4]  # write-back + second barrier
         ph[:, ci, 5] = nxt - s[:, 5]      # to the next conv's start
@@ -68,10 +68,11 @@ def main():
     floor = 2496 * 16
     out = {"B": B, "nblocks": nb, "launch_us": ev[0].elapsed_time(ev[1]) * 1e3, "clock_ghz": float(clock),
            "cycles_per_conv": conv, "mfma_floor_cycles": floor, "mfma_frac_in_conv": floor / conv,
-           "phase_cycles": {"dx-1 (+bias init)": float(med[0]), "dx0": float(med[1]), "dx+1": float(med[2]),
+           "phase_cycles": {"bias init (+ dx0 pass if two-pass)": float(med[0]), "-": float(med[1]),
+                            "k loop (one pass; dx-1/+1 pass if two-pass)": float(med[2]),
                             "barrier1_wait": float(med[3]), "writeback+barrier2": float(med[4]),
                             "to_next_conv": float(med[5])},
-           "mfma_floor_per_phase": {"dx-1": 8 * 24 * 4 * 16, "dx0": 10 * 24 * 4 * 16, "dx+1": 8 * 24 * 4 * 16},
+           "mfma_floor_k_loop": 2496 * 16,
            "staging_cycles": float(np.median(a[:, 1] - a[:, 0])),
            "kernel_cycles_per_wg": float(np.median(a[:, TST_N - 1] - a[:, 0])),
            "wave_skew_at_barrier1": float(np.median(
