@@ -91,11 +91,14 @@ constexpr int TNS = 9 * TC / 32;   // 72 k steps per 3x3 conv
 constexpr int TD = TOWER_TD;       // weight ring depth (k steps); must divide the 8 steps of a tap
 static_assert(8 % TD == 0, "ring index restarts at every tap");
 // tower8 k loop per kernel: the 8-env kernel (NQ = 2, and the representation tail's 2-env 8x10
-// geometry) walks all three column shifts in one pass with a ring of 3 entries (one k step ahead); the
+// geometry) walks all three column shifts in one pass with a ring of 6 entries (two k steps); the
 // one-quad kernel (NQ = 1: half the MFMAs per k step, weight-stream bound) keeps two passes (dx = 0,
-// then dx = -1 / +1 merged) and a ring of TD entries: one pass with a 3-entry ring was 6 % slower there
-template <int NQ> constexpr bool t8all = NQ == 2;
-template <int NQ> constexpr int t8d = t8all<NQ> ? 3 : TD;  // ring depth in entries
+// then dx = -1 / +1 merged) and a ring of TD entries
+#ifndef TOWER_Q1_ALL
+#define TOWER_Q1_ALL 0  // experiment: the one-pass loop at NQ = 1 too, ring depth TOWER_Q1_ALL (6 / 12)
+#endif
+template <int NQ> constexpr bool t8all = NQ == 2 || TOWER_Q1_ALL;
+template <int NQ> constexpr int t8d = NQ == 2 ? 6 : (TOWER_Q1_ALL ? TOWER_Q1_ALL : TD);  // ring depth in entries
 #ifndef TOWER_ABLATE
 #define TOWER_ABLATE 0  // diagnostic builds only (make tower-variants): 1 hot weights, 2 no LDS A reads,
                         // 3 duplicate weight streams (waves w, w+4), 4 = 3 with waves 4-7 started late
@@ -792,7 +795,7 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
   constexpr int RD = t8d<NQ>;
   constexpr int TX = G::TX, NA = G::GROUPS * TX, NC = TC / 32;
   constexpr int NM = G::GROUPS * (3 * TX - 2) * CT;  // MFMAs per step
-  static_assert(RD % 3 == 0 && NM >= NA + 6 * CT, "ring triples, schedule groups");
+  static_assert(RD % 3 == 0 && NM / CT >= NA, "ring triples, schedule groups");
   const int q = lane >> 4, y = (lane & 15) / G::EG, e = lane & (G::EG - 1);
   int base, tst, sw;
   t8_rows<G>(y, e, -1, base, tst, sw);
@@ -806,50 +809,56 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
     const bool last = dyi == 2;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-      typename Elt<EL>::v8 w[3][CT];
+      // column-tile major: the MFMAs of column tile ct (dx = 0 over all tiles, then dx = -1, dx = +1),
+      // then that tile's three ring slots are reloaded with the entries of the step after next (their
+      // registers are free once its MFMAs have issued: no copies, a ring of two steps in the same
+      // registers); the next step's A reads ride in the first column tile's MFMA slots
 #pragma unroll
-      for (int d = 0; d < 3; ++d)
+      for (int ct = 0; ct < CT; ++ct) {
+        typename Elt<EL>::v8 w[3];
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          const int slot = (3 * c + d) % RD;
-          w[d][ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][slot]);
+        for (int d = 0; d < 3; ++d) w[d] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][(3 * c + d) % RD]);
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          acc[j][ct] = Elt<EL>::mfma(w[1], afc[j], acc[j][ct]);
+          if (ct == 0) {
+            if (c + 1 < NC)
+              afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
+            else
+              afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NA; ++j)
+          if (j % TX + 1 < TX) acc[j + 1][ct] = Elt<EL>::mfma(w[0], afc[j], acc[j + 1][ct]);
+#pragma unroll
+        for (int j = 0; j < NA; ++j)
+          if (j % TX >= 1) acc[j - 1][ct] = Elt<EL>::mfma(w[2], afc[j], acc[j - 1][ct]);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
           // entry 3 (dyi * 8 + c) + d + RD: pack step 24 d + dyi * 8 + c + RD / 3, or at dy = +1 past
           // the conv's end the next conv's entry nn = 3 c + d + RD - 24
           int so = ct * (TNS * 1024) + (24 * d + dyi * NC + c + RD / 3) * 1024;
           __amdgpu_buffer_rsrc_t rs = cur.rs;
           if (3 * c + d + RD >= 3 * NC) {
             const int nn = 3 * c + d + RD - 3 * NC;
-            so = last ? ct * nxt.tstride + t8_first<t8all<NQ>>(nxt, nn) * 1024 : so;
+            so = last ? ct * nxt.tstride + t8_first<true>(nxt, nn) * 1024 : so;
             rs = last ? nxt.rs : cur.rs;
           }
-          bq[ct][slot] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
+          bq[ct][(3 * c + d) % RD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
         }
+        if (ct == 0) {
 #pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const int g0 = (j / TX) * TX, x = j % TX;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          acc[g0 + x][ct] = Elt<EL>::mfma(w[1][ct], afc[j], acc[g0 + x][ct]);
-          if (x + 1 < TX) acc[g0 + x + 1][ct] = Elt<EL>::mfma(w[0][ct], afc[j], acc[g0 + x + 1][ct]);
-          if (x >= 1) acc[g0 + x - 1][ct] = Elt<EL>::mfma(w[2][ct], afc[j], acc[g0 + x - 1][ct]);
+          for (int j = 0; j < NA; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, NM / CT - NA, 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, NM / CT, 0);
         }
-        if (c + 1 < NC)
-          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
-        else
-          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+        __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
       }
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 3 * CT; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, NM - NA - 6 * CT, 0);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NA; ++j) afc[j] = afn[j];
