@@ -90,15 +90,9 @@ constexpr int TNS = 9 * TC / 32;   // 72 k steps per 3x3 conv
 #endif
 constexpr int TD = TOWER_TD;       // weight ring depth (k steps); must divide the 8 steps of a tap
 static_assert(8 % TD == 0, "ring index restarts at every tap");
-// tower8 k loop per kernel: the 8-env kernel (NQ = 2, and the representation tail's 2-env 8x10
-// geometry) walks all three column shifts in one pass with a ring of 6 entries (two k steps); the
-// one-quad kernel (NQ = 1: half the MFMAs per k step, weight-stream bound) keeps two passes (dx = 0,
-// then dx = -1 / +1 merged) and a ring of TD entries
-#ifndef TOWER_Q1_ALL
-#define TOWER_Q1_ALL 0  // experiment: the one-pass loop at NQ = 1 too, ring depth TOWER_Q1_ALL (6 / 12)
-#endif
-template <int NQ> constexpr bool t8all = NQ == 2 || TOWER_Q1_ALL;
-template <int NQ> constexpr int t8d = NQ == 2 ? 6 : (TOWER_Q1_ALL ? TOWER_Q1_ALL : TD);  // ring depth in entries
+// tower8 weight ring depth in entries (one entry = one 1 KB fragment per column tile): two k steps of
+// the one-pass k loop (3 column shifts each); a ring entry count must divide the 24 of a dy
+template <int NQ> constexpr int t8d = 6;
 #ifndef TOWER_ABLATE
 #define TOWER_ABLATE 0  // diagnostic builds only (make tower-variants): 1 hot weights, 2 no LDS A reads,
                         // 3 duplicate weight streams (waves w, w+4), 4 = 3 with waves 4-7 started late
@@ -601,7 +595,7 @@ MZ_DEV uint32_t relu_pk(uint32_t u) {
 struct WNext {
   __amdgpu_buffer_rsrc_t rs;  // buffer resource over the pack at the wave's first column tile
   int tstride;                // bytes per column tile (k steps x 1 KB)
-  int s0;                     // 3x3 pack: 24 (ring entries in the order below); 1x1 pack: 0 (entry n = step n)
+  int s0;                     // nonzero: a 3x3 pack (ring entries in the order below); 0: a 1x1 pack
   // 16-B fragment of k step `step` of the wave's column tile + ct, this lane: buffer load with the
   // lane's offset in one VGPR and the (ct, step) offset in an SGPR
   MZ_DEV uint4 ld(int ct, int step, int lane) const {
@@ -617,22 +611,16 @@ MZ_DEV WNext wnext(const void* w, int tns, int ct0) {
   return WNext{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(p), 0, 0x7fffffff, 0x00020000), tns * 1024,
                tns == TNS ? 24 : 0};
 }
-// pack step of ring entry n (< ring depth) of a conv: 3x3 packs walk dx = 0 first (steps 24, 25, ...),
-// or in one pass the three shifts of each (dy, channel step) together (steps 0, 24, 48, 1, 25, 49, ...)
-template <bool ALL>
-MZ_DEV int t8_first(const WNext& p, int n) {
-  return ALL ? (p.s0 ? 24 * (n % 3) + n / 3 : n) : p.s0 + n;
-}
+// pack step of ring entry n (< ring depth) of a conv: 3x3 packs walk the three column shifts of each
+// (dy, channel step) together (steps 0, 24, 48, 1, 25, 49, ...), 1x1 packs their steps in order
+MZ_DEV int t8_first(const WNext& p, int n) { return p.s0 ? 24 * (n % 3) + n / 3 : n; }
 
-// Weight ring of one wave: its CT column tiles x RD k-step entries in flight (bq). A two-pass 3x3 conv walks
-// its 72 k steps as a sequence of entries: the dx = 0 taps first (entries 0..23 = pack steps 24..47,
-// dy-major, 8 channel steps per dy), then the dx = -1 and dx = +1 taps merged (entries 24..71: per
-// (dy, channel step) the dx = -1 step, then the dx = +1 step: pack steps 0, 48, 1, 49, ...). The
-// ring runs across conv boundaries: the last RD entries of a 3x3 conv fetch the NEXT conv's first
-// entries (`nxt`, t8_first), so those loads fly through the epilogue and both
-// barriers (a workgroup barrier waits for LDS, not for vmcnt) and the next conv's first MFMAs find
-// their weights in registers.
-static_assert(TD % 2 == 0, "the merged dx = -1 / +1 pass consumes entries in pairs");
+// Weight ring of one wave: its CT column tiles x RD entries in flight (bq). A 3x3 conv walks its 72
+// pack k steps (dx, dy, channel step) as 24 k-loop steps (dy, channel step) of 3 entries each, one per
+// column shift: pack steps 0, 24, 48, 1, 25, 49, ... The ring runs across conv boundaries: the last RD
+// entries of a 3x3 conv fetch the NEXT conv's first entries (`nxt`, t8_first), so those loads fly
+// through the epilogue and both barriers (a workgroup barrier waits for LDS, not for vmcnt) and the
+// next conv's first MFMAs find their weights in registers.
 
 // A-row addressing of lane (y, e) for latent row shift dy over a whole image (every tile a source):
 // byte offset of its row in tile 0 (or of its zero-block row), the per-tile stride (0 for zero rows)
@@ -647,148 +635,9 @@ MZ_DEV void t8_rows(int y, int e, int dy, int& b, int& ts, int& w) {
   w = key << 4;
 }
 
-// the dx = 0 taps (entries 0..23): every tile is a source and an output, 10 A reads feed 40 MFMAs
-template <int EL, int NQ, int CT = t8::CT, class G = Geo45<NQ>>
-__device__ __forceinline__ void tower8_d0(const uint8_t* __restrict__ lds, const WNext& cur,
-                                          uint4 (&bq)[CT][t8d<NQ>], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
-  constexpr int RD = t8d<NQ>;
-  static_assert(G::GROUPS * G::TX == T8<NQ>::NRT, "geometry and accumulator tiles");
-  constexpr int NA = G::GROUPS * G::TX, NC = TC / 32;
-  const int q = lane >> 4, y = (lane & 15) / G::EG, e = lane & (G::EG - 1);
-  int base, tst, sw;
-  t8_rows<G>(y, e, -1, base, tst, sw);
-  typename Elt<EL>::v8 afc[NA], afn[NA];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + ((q << 4) ^ sw));
-#pragma unroll 1
-  for (int dyi = 0; dyi < 3; ++dyi) {
-    int nbase, ntst, nsw;
-    t8_rows<G>(y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw);
-    const bool last = dyi == 2;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      typename Elt<EL>::v8 w[CT];
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        w[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][c % RD]);
-        // entry dyi * 8 + c + RD: pack step 24 + that, or at dy = +1 the merged phase's first entries
-        int so = ct * (TNS * 1024) + (24 + dyi * NC + c + RD) * 1024;
-        if (c + RD >= NC) {
-          const int m = c + RD - NC;
-          so = last ? ct * (TNS * 1024) + ((m & 1) * 48 + (m >> 1)) * 1024 : so;
-        }
-        bq[ct][c % RD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(cur.rs, lane * 16, so, 0));
-      }
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) acc[j][ct] = Elt<EL>::mfma(w[ct], afc[j], acc[j][ct]);
-        if (c + 1 < NC)
-          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
-        else
-          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
-      }
-      // schedule: every A read of the next k step in the first NA MFMA slots (the compiler orders a
-      // step's independent MFMAs freely, so the next step may open with any tile: its reads must have
-      // landed by then), the weight loads next, then the remaining MFMAs
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-#pragma unroll
-      for (int ct = 0; ct < CT; ++ct) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, NA * CT - NA - 2 * CT, 0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < NA; ++j) afc[j] = afn[j];
-    }
-    base = nbase; tst = ntst; sw = nsw;
-  }
-}
-
-// the dx = -1 and dx = +1 taps merged (entries 24..71): per (dy, channel step) every tile is read
-// once and feeds both shifts — source tile x with the dx = -1 weights into output tile x + 1 and
-// with the dx = +1 weights into output tile x - 1 (within its group). 10 A reads + 8 weight
-// fragments feed 64 MFMAs per step at NQ = 2 (separate dx = -1 / +1 loops: 2 x (8 A reads + 4
-// fragments) for 2 x 32 MFMAs, and 24 more k steps per conv, each with its fixed cost)
-template <int EL, int NQ, int CT = t8::CT, class G = Geo45<NQ>>
-__device__ __forceinline__ void tower8_dpm(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
-                                           uint4 (&bq)[CT][t8d<NQ>], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
-  constexpr int RD = t8d<NQ>;
-  constexpr int TX = G::TX, NA = G::GROUPS * TX, NC = TC / 32;
-  constexpr int NM = G::GROUPS * (TX - 1) * 2 * CT;  // MFMAs per merged step
-  static_assert(NM >= NA + 4 * CT, "schedule groups");
-  const int q = lane >> 4, y = (lane & 15) / G::EG, e = lane & (G::EG - 1);
-  int base, tst, sw;
-  t8_rows<G>(y, e, -1, base, tst, sw);
-  typename Elt<EL>::v8 afc[NA], afn[NA];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) afc[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + ((q << 4) ^ sw));
-#pragma unroll 1
-  for (int dyi = 0; dyi < 3; ++dyi) {
-    int nbase, ntst, nsw;
-    t8_rows<G>(y, e, dyi < 2 ? dyi : 1, nbase, ntst, nsw);
-    const bool last = dyi == 2;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      typename Elt<EL>::v8 wm[CT], wp[CT];
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          const int slot = (2 * c + d) % RD;
-          (d ? wp : wm)[ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][slot]);
-          // entry 2 (dyi * 8 + c) + d + RD of this phase: pack step 48 d + dyi * 8 + c + RD / 2, or at
-          // dy = +1 past the conv's end the next conv's entry nn = 2 c + d + RD - 16
-          int so = ct * (TNS * 1024) + (48 * d + dyi * NC + c + RD / 2) * 1024;
-          __amdgpu_buffer_rsrc_t rs = cur.rs;
-          if (2 * c + d + RD >= 2 * NC) {
-            const int nn = 2 * c + d + RD - 2 * NC;
-            so = last ? ct * nxt.tstride + t8_first<t8all<NQ>>(nxt, nn) * 1024 : so;
-            rs = last ? nxt.rs : cur.rs;
-          }
-          bq[ct][slot] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
-        }
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const int g0 = (j / TX) * TX, x = j % TX;
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) {
-          if (x + 1 < TX) acc[g0 + x + 1][ct] = Elt<EL>::mfma(wm[ct], afc[j], acc[g0 + x + 1][ct]);
-          if (x >= 1) acc[g0 + x - 1][ct] = Elt<EL>::mfma(wp[ct], afc[j], acc[g0 + x - 1][ct]);
-        }
-        if (c + 1 < NC)
-          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
-        else
-          afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
-      }
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 2 * CT; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, NM - NA - 4 * CT, 0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < NA; ++j) afc[j] = afn[j];
-    }
-    base = nbase; tst = ntst; sw = nsw;
-  }
-}
-
-// all three column shifts in one pass (NQ = 2): per (dy, channel step) every tile is read once
-// and feeds dx = 0 (output x), dx = -1 (output x + 1) and dx = +1 (output x - 1); 24 k steps per conv
+// One k-loop pass over all three column shifts: per (dy, channel step) every tile is read from LDS
+// once and feeds dx = 0 (output x), dx = -1 (output x + 1) and dx = +1 (output x - 1) within its
+// group; 24 k steps per conv (three loops, one per shift, took 72 steps and 624 A reads per conv)
 template <int EL, int NQ, int CT = t8::CT, class G = Geo45<NQ>>
 __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, const WNext& cur, const WNext& nxt,
                                             uint4 (&bq)[CT][t8d<NQ>], f32x4 (&acc)[T8<NQ>::NRT][CT], int lane) {
@@ -842,7 +691,7 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
           __amdgpu_buffer_rsrc_t rs = cur.rs;
           if (3 * c + d + RD >= 3 * NC) {
             const int nn = 3 * c + d + RD - 3 * NC;
-            so = last ? ct * nxt.tstride + t8_first<true>(nxt, nn) * 1024 : so;
+            so = last ? ct * nxt.tstride + t8_first(nxt, nn) * 1024 : so;
             rs = last ? nxt.rs : cur.rs;
           }
           bq[ct][(3 * c + d) % RD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
@@ -906,7 +755,7 @@ MZ_DEV void tower8_preload(uint4 (&bq)[CT][t8d<NQ>], const WNext& p, int lane) {
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-    for (int i = 0; i < t8d<NQ>; ++i) bq[ct][i] = p.ld(ct, t8_first<t8all<NQ>>(p, i), lane);
+    for (int i = 0; i < t8d<NQ>; ++i) bq[ct][i] = p.ld(ct, t8_first(p, i), lane);
 }
 
 // k loop of one conv over the 8-env image: this wave's 4 channel tiles cur.ct0..+3 of a weight pack
@@ -952,16 +801,9 @@ __device__ __forceinline__ void tower8_acc(const uint8_t* __restrict__ lds, cons
   if (CENTER) {
     tower8_center<EL, NQ, CT>(lds, cur, bq, acc, lane);
   } else {
-    if constexpr (t8all<NQ>) {
-      TSTAMP(3 + 6 * ci);
-      TSTAMP(4 + 6 * ci);
-      tower8_dall<EL, NQ, CT, G>(lds, cur, nxt, bq, acc, lane);
-    } else {
-      tower8_d0<EL, NQ, CT, G>(lds, cur, bq, acc, lane);
-      TSTAMP(3 + 6 * ci);
-      TSTAMP(4 + 6 * ci);
-      tower8_dpm<EL, NQ, CT, G>(lds, cur, nxt, bq, acc, lane);
-    }
+    TSTAMP(3 + 6 * ci);
+    TSTAMP(4 + 6 * ci);
+    tower8_dall<EL, NQ, CT, G>(lds, cur, nxt, bq, acc, lane);
   }
   TSTAMP(5 + 6 * ci);
 }
