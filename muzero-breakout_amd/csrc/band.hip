@@ -52,6 +52,9 @@ struct BandGeo {
   static constexpr int TDB = (XT == 10 ? 4 : 2) < CIN / 32 ? (XT == 10 ? 4 : 2) : CIN / 32;
   static_assert((CIN / 32) % TDB == 0, "ring slot restarts at every tap");
   static constexpr int NSRC = XT + 2;              // staged source columns (with the halo)
+  // one-pass weight ring (band_all): 3 entries (dx = -1, 0, +1) per k step; two steps in flight, one
+  // where two workgroups per CU leave 256 registers per lane for 4 column tiles (6 entries spilled 52)
+  static constexpr int RDB = (XT == 5 && COUT == 256) ? 3 : 6;
   // LDS bytes per source row: at Cin 64 the row is padded to 128 channels, so a chunk index XORed
   // with the 4-bit row key stays inside the row (staging and reads use the same mapping; the pad
   // chunks are never read)
@@ -133,6 +136,97 @@ __device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, __amdgp
   }
 }
 
+#ifndef BAND_ONEPASS
+#define BAND_ONEPASS 1  // 0: the three per-shift k loops (band_dx) everywhere, for A/B builds
+#endif
+// the one pass runs the Cout 256 convs (B = 4096 isolated: 256->256 1202 -> 1131 us, 128->256 675 ->
+// 639 us); at Cout 128 it was 3 % slower (358 -> 370 us at 128->128), so those keep the three loops
+template <int COUT> constexpr bool band_one = BAND_ONEPASS && COUT == 256;
+
+// pack step of one-pass ring entry e = 3 (dyi * NC + c) + d (d = dx + 1)
+template <int NC>
+MZ_DEV int band_step(int e) { return (e % 3) * 3 * NC + e / 3; }
+
+// One k-loop pass over all three column shifts (tower.hip tower8_dall): per (dy, channel step) the
+// XT + 2 source columns are read from LDS once; output column t takes dx = -1 from source t, dx = 0
+// from t + 1, dx = +1 from t + 2. Column-tile major: a column tile's 3 x XT MFMAs, then its three
+// ring slots reloaded RDB / 3 steps ahead (free registers once the MFMAs have issued: no copies)
+template <int CIN, int COUT, int XT>
+__device__ __forceinline__ void band_all(const uint8_t* __restrict__ lds, __amdgpu_buffer_rsrc_t wrs,
+                                         uint4 (&bq)[COUT / 64][BandGeo<CIN, COUT, XT>::RDB], f32x4 (&acc)[XT][COUT / 64],
+                                         int lane) {
+  using G = BandGeo<CIN, COUT, XT>;
+  constexpr int CTW = G::CTW, NC = G::NC, NS = XT + 2, RDB = G::RDB;
+  static_assert((3 * NC) % RDB == 0 && 3 * XT >= NS, "ring slot restarts at every dy; schedule groups");
+  const int q = lane >> 4, ys = nib(SIG, lane & 15);
+  auto rows = [&](int dy, int& base, int& tst, int& sw) {
+    const int yy = ys + dy;
+    const bool ok = (unsigned)yy < (unsigned)BH;
+    base = ok ? yy * G::RB : G::LZ + (yy & 15) * G::RB;
+    tst = ok ? 16 * G::RB : 0;
+    sw = nib(KEY, yy & 15) << 4;
+  };
+  int base, tst, sw;
+  rows(-1, base, tst, sw);
+  bf16x8 afc[NS], afn[NS];
+#pragma unroll
+  for (int j = 0; j < NS; ++j) afc[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * tst + ((q << 4) ^ sw));
+#pragma unroll 1
+  for (int dyi = 0; dyi < 3; ++dyi) {
+    int nbase, ntst, nsw;
+    rows(dyi < 2 ? dyi : 1, nbase, ntst, nsw);
+    const bool last = dyi == 2;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+#pragma unroll
+      for (int ct = 0; ct < CTW; ++ct) {
+        bf16x8 w[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) w[d] = __builtin_bit_cast(bf16x8, bq[ct][(3 * c + d) % RDB]);
+#pragma unroll
+        for (int t = 0; t < XT; ++t) acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], afc[t + 1], acc[t][ct], 0, 0, 0);
+        if (ct == 0) {
+#pragma unroll
+          for (int j = 0; j < NS; ++j) {
+            if (c + 1 < NC)
+              afn[j] = *reinterpret_cast<const bf16x8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
+            else
+              afn[j] = *reinterpret_cast<const bf16x8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < XT; ++t) acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], afc[t], acc[t][ct], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < XT; ++t) acc[t][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], afc[t + 2], acc[t][ct], 0, 0, 0);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          // RDB / 3 steps ahead (pack step 3 NC d + dyi NC + c + RDB / 3); past the conv's end (dy = +1,
+          // last channel steps) the current step is re-read instead (in range, never used)
+          const int nxt = (ct * G::TNS + d * 3 * NC + dyi * NC + c + RDB / 3) * 1024;
+          const int cur = (ct * G::TNS + d * 3 * NC + dyi * NC + c) * 1024;
+          const int so = (c + RDB / 3 >= NC && last) ? cur : nxt;
+          bq[ct][(3 * c + d) % RDB] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, so, 0));
+        }
+        if (ct == 0) {
+#pragma unroll
+          for (int j = 0; j < NS; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * XT - NS, 0);
+        } else {
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * XT, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NS; ++j) afc[j] = afn[j];
+    }
+    base = nbase; tst = ntst; sw = nsw;
+  }
+}
+
 // XT output columns per workgroup (10: one workgroup per CU at Cin 256; 5: two per CU, so one
 // workgroup's band staging / epilogue runs beside the other's MFMAs)
 template <int CIN, int COUT, int XT>
@@ -178,20 +272,24 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint4*>(reinterpret_cast<const uint4*>(a.wf) + (size_t)__builtin_amdgcn_readfirstlane(wave * CTW) * G::TNS * 64),
       0, 0x7fffffff, 0x00020000);
-  constexpr int TDB = G::TDB;
+  constexpr int TDB = band_one<COUT> ? G::RDB : G::TDB;
   uint4 bq[CTW][TDB];
 #pragma unroll
   for (int ct = 0; ct < CTW; ++ct)
 #pragma unroll
-    for (int i = 0; i < TDB; ++i) bq[ct][i] = wld<G::TNS>(wrs, ct, i, lane);
+    for (int i = 0; i < TDB; ++i) bq[ct][i] = wld<G::TNS>(wrs, ct, band_one<COUT> ? band_step<G::NC>(i) : i, lane);
   f32x4 acc[XT][CTW];
 #pragma unroll
   for (int t = 0; t < XT; ++t)
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-  band_dx<CIN, COUT, XT, -1>(lds, wrs, bq, acc, lane);
-  band_dx<CIN, COUT, XT, 0>(lds, wrs, bq, acc, lane);
-  band_dx<CIN, COUT, XT, 1>(lds, wrs, bq, acc, lane);
+  if constexpr (band_one<COUT>) {
+    band_all<CIN, COUT, XT>(lds, wrs, bq, acc, lane);
+  } else {
+    band_dx<CIN, COUT, XT, -1>(lds, wrs, bq, acc, lane);
+    band_dx<CIN, COUT, XT, 0>(lds, wrs, bq, acc, lane);
+    band_dx<CIN, COUT, XT, 1>(lds, wrs, bq, acc, lane);
+  }
   __syncthreads();  // the band is no longer read
   // output tile in LDS: row 16 t + y, 16-B chunks swizzled by KEY[y]
   constexpr int ONCH = COUT / 8;
