@@ -88,14 +88,15 @@ constexpr int TNS = 9 * TC / 32;   // 72 k steps per 3x3 conv
 #ifndef TOWER_TD
 #define TOWER_TD 4
 #endif
-constexpr int TD = TOWER_TD;       // weight ring depth (k steps); must divide the 8 steps of a tap
+constexpr int TD = TOWER_TD;       // 4-env 8-wave kernel's weight ring depth (k steps); divides a tap's 8
 static_assert(8 % TD == 0, "ring index restarts at every tap");
 // tower8 weight ring depth in entries (one entry = one 1 KB fragment per column tile): two k steps of
 // the one-pass k loop (3 column shifts each); a ring entry count must divide the 24 of a dy
 template <int NQ> constexpr int t8d = 6;
 #ifndef TOWER_ABLATE
-#define TOWER_ABLATE 0  // diagnostic builds only (make tower-variants): 1 hot weights, 2 no LDS A reads,
-                        // 3 duplicate weight streams (waves w, w+4), 4 = 3 with waves 4-7 started late
+#define TOWER_ABLATE 0  // diagnostic builds of the 4-env 8-wave kernel only (make tower-variants): 1 hot
+                        // weights, 2 no LDS A reads, 3 duplicate weight streams (waves w, w+4), 4 = 3 with
+                        // waves 4-7 started late (tower8's own ablations went with its three-pass loop)
 #endif
 #if TOWER_ABLATE == 3 || TOWER_ABLATE == 4
 #define TOWER_CT0(wave) (2 * ((wave) & 3))
