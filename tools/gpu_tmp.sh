@@ -1,11 +1,8 @@
-# round run on the round's last tree (profiles/r02/r2l): GPU suite, smoke, headline + config 2, kernel
-# stats, tower PMC traffic; then the learner bench and the tower phase stamps
+# SQ / GRBM counters of the isolated B = 4096 tower on the round's last tree (MFMA busy, waits, clock)
 set -euo pipefail
 export TMPDIR=/tmp
-bash tools/gpu_round.sh r2l
-O=gpurun_out/r2l
-timeout -k 10 300 python bench.py --workload learner > $O/learner_bench.json 2> $O/learner_bench.err
-cat $O/learner_bench.json
-timeout -k 10 120 python tools/stamp_tower.py 4096 14 $O/stamps_4096.json > $O/stamps_log.txt 2>&1 || { tail $O/stamps_log.txt; exit 1; }
-python3 -c "import json; d=json.load(open('$O/stamps_4096.json')); print(d['launch_us'], d['clock_ghz'], d['cycles_per_conv'], d['mfma_frac_in_conv'])"
-echo "r2l done"
+O=gpurun_out/sq_r2l
+mkdir -p $O
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-trace -d $O/sq -o run -- python3 tools/pmc_conv.py 4096 tower 14 > $O/sq.log 2>&1
+python3 tools/pmc_sq.py $O/sq tower8 $O/sq_summary.json
+echo "sq done"
