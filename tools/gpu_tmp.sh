@@ -1,8 +1,12 @@
-# SQ / GRBM counters of the isolated B = 4096 tower on the round's last tree (MFMA busy, waits, clock)
+# final confirmation on the committed tree: GPU suite, smoke, default bench
 set -euo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/sq_r2l
+O=gpurun_out/final
 mkdir -p $O
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE --kernel-trace -d $O/sq -o run -- python3 tools/pmc_conv.py 4096 tower 14 > $O/sq.log 2>&1
-python3 tools/pmc_sq.py $O/sq tower8 $O/sq_summary.json
-echo "sq done"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
+python3 -c "import json; d=json.load(open('$O/bench.json')); print(round(d['value'],1), round(d['roofline']['frac'],4), round(d['whole_step_mfma_frac'],4), d['cpu_baseline']['value'])"
+echo "final done"
