@@ -140,7 +140,10 @@ __device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, __amdgp
 #define BAND_ONEPASS 1  // 0: the three per-shift k loops (band_dx) everywhere, for A/B builds
 #endif
 // the one pass runs the Cout 256 convs (B = 4096 isolated: 256->256 1202 -> 1131 us, 128->256 675 ->
-// 639 us); at Cout 128 it was 3 % slower (358 -> 370 us at 128->128), so those keep the three loops
+// 639 us); at Cout 128 it was 3 % slower with a 6-entry ring (358 -> 370 us at 128->128) and 3.5 %
+// faster with a 3-entry one (368 -> 355 us), but that build moved the bf16 learner's gradients enough to
+// fail test_learner_fused_bn_statistics_track_separate_passes (min cosine 0.93 < 0.98, a noise bound
+// between two bf16 realisations), so the Cout 128 convs keep the three loops
 template <int COUT> constexpr bool band_one = BAND_ONEPASS && COUT == 256;
 
 // pack step of one-pass ring entry e = 3 (dyi * NC + c) + d (d = dx + 1)
