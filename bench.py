@@ -442,14 +442,14 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     value = world * B * args.steps / dt
-    # probe entries: (start, end, convs in the launch); per-conv average over the latent residual convs
-    conv_ms = (float(sum(a.elapsed_time(b) for a, b, _ in probe) / sum(n for _, _, n in probe))) if probe else None
-    tower_launch_ms = (float(np.mean([a.elapsed_time(b) for a, b, n in probe if n > 1]))
-                       if any(n > 1 for _, _, n in probe) else None)
+    runner.probe_collect()  # probe entries: (ms, convs in the launch), HIP events on the launch stream
+    # per-conv average over the latent residual convs
+    conv_ms = (float(sum(ms for ms, _ in probe) / sum(n for _, n in probe))) if probe else None
+    tower_launch_ms = (float(np.mean([ms for ms, n in probe if n > 1])) if any(n > 1 for _, n in probe) else None)
     p = agent.packed
     fl = conv_flops(B, p.lh * p.lw, p.c1)
     achieved = fl / (conv_ms * 1e-3) / 1e12 if conv_ms else None
-    traffic, traffic_rec = tower_traffic(B, any(n > 1 for _, _, n in probe))
+    traffic, traffic_rec = tower_traffic(B, any(n > 1 for _, n in probe))
     if rank == 0:
         out = {
             "metric": METRIC,

@@ -156,7 +156,10 @@ def ops():
 
 
 TORCH_OPS = ["env_reset_", "env_step", "grayscale", "mcts_root_", "mcts_select_", "mcts_backup_", "mcts_results_",
-             "sample_actions", "support_decode"]
+             "sample_actions", "support_decode",
+             # the nets (csrc/net_ops.cpp): reference surface + NHWC acting forms + fused tree step
+             "representation", "dynamics", "prediction", "representation_", "dynamics_", "prediction_",
+             "prediction_tree_"]
 
 
 def exported_symbols():

@@ -7,7 +7,6 @@ per-(pixel, action) bias table, and the Linear heads permuted from torch's (c,h,
 flatten order to the NHWC (h,w,c) order. Activations are NHWC on the device in bf16
 (throughput path) or f32 (parity path), computed by the HIP kernels in libmzba.so.
 """
-import ctypes
 import math
 
 import numpy as np
@@ -107,6 +106,91 @@ class PackedNets:
         self.val_lin = self._linear(sd["pred_net.value_head.2.weight"], sd["pred_net.value_head.2.bias"], self.c1 // 2)
         self.fused = self._fused(sd, w[:, :cmain])
         self.rep_tail = self._rep_tail(sd)
+        self.native = self._native()
+
+    def _native(self):
+        """The torch custom class `mz.NetPack` (csrc/net_ops.cpp) over these device tensors (shared,
+        not copied): what the torch.ops.mz net ops read."""
+        L.ops()
+        n = torch.classes.mz.NetPack()
+        n.set_meta(DT_CODE[self.dtype], self.c0, self.c1, self.L, self.lh, self.lw, self.ns,
+                   float(self.mcfg["supports_min"]), float(self.mcfg["supports_max"]), self.dyn_fp16)
+
+        def conv(name, c):
+            n.add_conv(name, c["w"], c["b"], c.get("wf"), c.get("wt"), c.get("act_bias"), c["cin"], c["cout"], c["ks"],
+                       c.get("A", 0))
+
+        for i, (kind, layer) in enumerate(self.rep):
+            if kind == "conv":
+                conv(f"rep.{i}", layer)
+                n.add_rep("conv", f"rep.{i}", "")
+            elif kind == "res":
+                conv(f"rep.{i}.1", layer[0])
+                conv(f"rep.{i}.2", layer[1])
+                n.add_rep("res", f"rep.{i}.1", f"rep.{i}.2")
+            else:
+                n.add_rep("pool", "", "")
+        conv("dyn0", self.dyn0)
+        for nm, blocks in (("dyn", self.dyn), ("pred", self.pred)):
+            for k, (c1, c2) in enumerate(blocks):
+                conv(f"{nm}.{k}.1", c1)
+                conv(f"{nm}.{k}.2", c2)
+            n.set_int(f"n_{nm}", len(blocks))
+        for nm in ("rew_conv", "pol_conv", "val_conv"):
+            conv(nm, getattr(self, nm))
+        for nm in ("rew_lin", "pol_lin", "val_lin"):
+            li = getattr(self, nm)
+            n.add_linear(nm, li["w"], li["b"], li.get("wb"), li["K"], li["O"])
+        for nm in ("dyn_tower", "pred_tower"):
+            tw = getattr(self, nm)
+            if tw is not None:
+                n.set_tensor(nm + ".wf", tw["wf"])
+                n.set_tensor(nm + ".b", tw["b"])
+                n.set_int(nm + ".n", tw["n"])
+        if self.dyn_tower is not None and "wf16" in self.dyn_tower:
+            n.set_tensor("dyn_tower.wf16", self.dyn_tower["wf16"])
+        if self.fused is not None:
+            for k, t in self.fused.items():
+                if isinstance(t, torch.Tensor):
+                    n.set_tensor("fused." + k, t)
+            n.set_int("fused.A", self.fused["A"])
+            for k, t in self.fused.get("dyn16", {}).items():
+                n.set_tensor("fused16." + k, t)
+        if self.rep_tail is not None:
+            n.set_tensor("rep_tail.wf", self.rep_tail["wf"])
+            n.set_tensor("rep_tail.b", self.rep_tail["b"])
+            n.set_int("rep_tail.n", self.rep_tail["n"])
+            n.set_int("rep_tail.first", self.rep_tail["first"])
+        return n
+
+    def device_tensors(self):
+        """Every device tensor of the pack, in a fixed order (refresh_from copies them pairwise)."""
+        out = []
+
+        def walk(x):
+            if isinstance(x, torch.Tensor):
+                out.append(x)
+            elif isinstance(x, dict):
+                for k in sorted(x):
+                    walk(x[k])
+            elif isinstance(x, (list, tuple)):
+                for y in x:
+                    walk(y)
+
+        for nm in ("rep", "dyn0", "dyn", "rew_conv", "rew_lin", "pred", "dyn_tower", "pred_tower", "pol_conv",
+                   "pol_lin", "val_conv", "val_lin", "fused", "rep_tail"):
+            walk(getattr(self, nm))
+        return out
+
+    def refresh_from(self, other):
+        """Copy another pack of the same configuration into this one's device buffers in place (the
+        target-net refresh, train_torch.py:361-367): every pointer stays valid, so live runners and
+        captured acting-step graphs run the new weights from their next launch on."""
+        mine, theirs = self.device_tensors(), other.device_tensors()
+        if len(mine) != len(theirs) or any(a.shape != b.shape or a.dtype != b.dtype for a, b in zip(mine, theirs)):
+            raise ValueError("refresh_from: the packs differ in configuration")
+        for a, b in zip(mine, theirs):
+            a.copy_(b)
 
     def _fused(self, sd, w0):
         """Weights of the fused dynamics / prediction steps (mzba_tower_fused): the dynamics
@@ -140,7 +224,7 @@ class PackedNets:
         out = {"w0": pack3(w0 * a0[:, None, None, None]), "b0": self.dyn0["b"], "act_bias": self.dyn0["act_bias"],
                "A": self.dyn0["A"], "rw": pack1(rw), "rb": dev(rb), "pw": pack3(pw), "pb": dev(pb),
                "vw": pack1(vw), "vb": dev(vb)}
-        if self.dyn_fp16:  # the dynamics step's fp16 weights (tower packs: tower_weights(..., fp16=True))
+        if self.dyn_fp16:  # the dynamics step's fp16 weights (its tower pack: dyn_tower['wf16'])
             w = sd["dyn_net.reward_head.2.weight"]  # the reward Linear in the heads' (position, channel) order
             O, K = w.shape
             lw = np.zeros((16, K))
@@ -237,16 +321,14 @@ class PackedNets:
                 alpha, beta = self._bn(sd, f"{p}.bn{k}")
                 ws.append(sd[f"{p}.conv{k}.weight"] * alpha[:, None, None, None])
                 bs.append(sd[f"{p}.conv{k}.bias"] * alpha + beta)
-        return {"w": ws, "wf": {}, "n": n,
-                "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device)}
-
-    def tower_weights(self, tw, plan, fp16=False):
-        """Device weights of a tower in the packing of mzba_tower's plan (cached per plan and dtype)."""
-        key = (plan, fp16)
-        if key not in tw["wf"]:
-            wf = np.concatenate([pack_tower_conv(w) for w in tw["w"]] + [np.zeros(LAT_PAD_ELEMS)])
-            tw["wf"][key] = torch.tensor(wf, dtype=torch.float32).to(torch.float16 if fp16 else self.tdt).to(self.device)
-        return tw["wf"][key]
+        # every tower kernel (plans 1-3) takes the same packing: all convs back to back, + the ring's
+        # 8 padding k steps; the fp16 dynamics net (config 5) has its own copy
+        wf = np.concatenate([pack_tower_conv(w) for w in ws] + [np.zeros(LAT_PAD_ELEMS)])
+        tw = {"n": n, "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device),
+              "wf": torch.tensor(wf, dtype=torch.float32).to(self.tdt).to(self.device)}
+        if self.dyn_fp16 and prefix.startswith("dyn"):
+            tw["wf16"] = torch.tensor(wf, dtype=torch.float32).to(torch.float16).to(self.device)
+        return tw
 
     def _linear(self, w, b, c):
         O, K = w.shape
@@ -262,228 +344,82 @@ class PackedNets:
 
 
 class NetRunner:
-    """Launch sequences for the three nets on NHWC device buffers (workspace per B)."""
+    """The launch sequences of the three nets for one batch (B, H, W): a thin handle on the native
+    `mz.NetRunner` (csrc/net_ops.cpp), whose torch custom ops run every launch on torch's current
+    stream — representation_ / dynamics_ / prediction_ / prediction_tree_ (`torch.ops.mz`)."""
+
+    FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail")
 
     def __init__(self, packed, B, H, W):
         self.p = packed
         self.B, self.H, self.W = B, H, W
-        dev, tdt = packed.device, packed.tdt
-        c0, c1 = packed.c0, packed.c1
-        cmax = max(c0, c1, _round64(2 * packed.L))
-        HW = H * W
-        self.HW = HW
+        self.HW = H * W
         self.lhw = packed.lh * packed.lw
-        z = lambda *s: torch.empty(*s, dtype=tdt, device=dev)  # noqa: E731
-        self.r_a = z(B * HW * cmax)
-        self.r_t = z(B * HW * cmax)
-        self.r_b = z(B * HW * cmax)
-        self.x = z(B * self.lhw * c1)
-        self.t = z(B * self.lhw * c1)
-        self.rc = z(B * self.lhw * c1)
-        self.pc = z(B * self.lhw * (c1 // 2))
-        self.vc = z(B * self.lhw * (c1 // 2))
-        self.dt = DT_CODE[packed.dtype]
-        # optional live probe: list that receives (start, end) HIP events around every
-        # latent-resolution residual conv (the dominant kernel shape M=B*h*w, N=C, K=9C)
-        self.probe = None
-        self.use_lat = True  # latent-resolution bf16 convs on conv_lat (False: generic implicit GEMM)
-        self.use_tower = True  # dyn/pred residual towers as one fused launch each (bf16, C=256, 4x5)
-        self.use_fused = True  # ... with the dynamics ConvBlock and the heads inside (4-env kernel)
-        self.use_band = True  # 16x20 representation convs on the band kernel
-        # the 8x10 blocks between the two pools + scale as one launch (bf16); an A/B run against an
-        # older library build (MZBA_LIB_PARTIAL) falls back to the launch sequence
-        self.use_rep_tail = hasattr(L.lib(), "mzba_rep_tail")
-        self.tower_plan = self.tower_ws = None
-        if packed.tower_ok:
-            self.tower_plan = L.lib().mzba_tower_plan(B)
-            nb = L.lib().mzba_tower_ws_bytes(B)
-            self.tower_ws = torch.zeros(max(nb, 16), dtype=torch.uint8, device=dev)
-            self.tower_ws_bytes = nb
+        self.native = packed.native.runner(B, H, W)
+        self.tower_plan = self.native.plan() or None  # the kernel this runner launches (fixed at creation)
+        self._probe = None
 
-    # -- primitives --------------------------------------------------------------------
-    def conv(self, x, layer, out, B, H, W, res=None, relu=True, slot=None, env_stride=None, slot_stride=0, act=None):
-        s = L.stream()
-        env_stride = H * W * layer["cin"] if env_stride is None else env_stride
-        ab = layer.get("act_bias")
-        if ("wt" in layer and self.use_band and slot is None and env_stride == H * W * layer["cin"] and ab is None
-                and L.lib().mzba_conv_band_supported(H, W, layer["cin"], layer["cout"], layer["ks"])):
-            L.call("mzba_conv_band", L.ptr(x), L.ptr(layer["wt"]), L.ptr(layer["b"]), L.ptr(res), L.ptr(out), B, H, W,
-                   layer["cin"], layer["cout"], 1 if relu else 0, s)
-            return
-        if "wf" in layer and self.use_lat and L.lib().mzba_conv_lat_supported(H, W, layer["cin"], layer["cout"],
-                                                                             layer["ks"]):
-            L.call("mzba_conv_lat", L.ptr(x), env_stride, L.ptr(slot), slot_stride, L.ptr(layer["wf"]),
-                   L.ptr(layer["b"]), L.ptr(ab), L.ptr(act) if ab is not None else None, layer.get("A", 0),
-                   L.ptr(res), L.ptr(out), B, H, W, layer["cin"], layer["cout"], layer["ks"], 1 if relu else 0, s)
-            return
-        L.call("mzba_conv2d", self.dt, L.ptr(x), env_stride, L.ptr(slot), slot_stride, L.ptr(layer["w"]),
-               L.ptr(layer["b"]), L.ptr(ab), L.ptr(act) if ab is not None else None, layer.get("A", 0),
-               L.ptr(res), L.ptr(out), B, H, W, layer["cin"], layer["cout"], layer["ks"], 1 if relu else 0, s)
+    # kernel switches (tests / A-B runs): use_lat, use_tower, use_fused, use_band, use_rep_tail
+    def __getattr__(self, k):
+        if k in NetRunner.FLAGS:
+            return self.native.get_flag(k)
+        raise AttributeError(k)
 
-    def tower(self, tw, x, out):
-        """All residual blocks of a dyn/pred tower in one launch (activations stay in LDS).
-        `out` may alias `x` (every workgroup stages its envs before any of them is written)."""
-        pr = self.probe
-        if pr is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        wf = self.p.tower_weights(tw, self.tower_plan)
-        L.call("mzba_tower", L.ptr(x), 20 * 256, None, 0, L.ptr(out), L.ptr(wf), L.ptr(tw["b"]), tw["n"],
-               self.B, L.ptr(self.tower_ws), self.tower_ws_bytes, L.stream())
-        if pr is not None:
-            e1.record()
-            pr.append((e0, e1, 2 * tw["n"]))
+    def __setattr__(self, k, v):
+        if k in NetRunner.FLAGS:
+            self.native.set_flag(k, bool(v))
+        else:
+            object.__setattr__(self, k, v)
 
-    def resblock(self, blk, x, t, out, B, H, W):
-        """networks.py:31-35; out may alias x (in-place residual)."""
-        pr = self.probe if (H, W) == (self.p.lh, self.p.lw) else None
-        if pr is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        self.conv(x, blk[0], t, B, H, W, relu=True)
-        if pr is not None:
-            e1.record()
-            pr.append((e0, e1, 1))
-        self.conv(t, blk[1], out, B, H, W, res=x, relu=True)
+    # live probe: HIP events around every tower launch / latent-resolution residual conv of the
+    # eager launches issued while `probe` is a list; probe_collect() appends (ms, convs) to it
+    @property
+    def probe(self):
+        return self._probe
 
-    # -- nets ----------------------------------------------------------------------------
+    @probe.setter
+    def probe(self, lst):
+        if lst is not None:
+            self._probe_dst = lst
+        self._probe = lst
+        self.native.set_probe(lst is not None)
+
+    def probe_collect(self):
+        """Wait for the recorded events and append (milliseconds, convs in the launch) entries."""
+        ms, n = self.native.probe_read()
+        dst = getattr(self, "_probe_dst", None)
+        out = list(zip(ms, n))
+        if dst is not None:
+            dst.extend(out)
+        return out
+
+    def fused_ok(self):
+        return self.native.fused_ok()
+
+    # -- nets (torch.ops.mz) -------------------------------------------------------------------
     def representation(self, x_in, out_latent, pool=None, pool_env_stride=0):
         """RepresentationNetwork + _scale_state (networks.py:94-99, 271-280).
         x_in: [B][H*W][Cin_pad] NHWC. Writes the scaled latent to out_latent (and pool slot 0)."""
-        B, H, W = self.B, self.H, self.W
-        cur, bufs = x_in, [self.r_a, self.r_b]
-        which = 0
-        tail = self.p.rep_tail if (self.use_rep_tail and (H, W) == (16, 20)) else None
-        for li, (kind, layer) in enumerate(self.p.rep):
-            if tail is not None and li == tail["first"]:  # pool + 8x10 blocks + pool + scale: one launch
-                L.call("mzba_rep_tail", L.ptr(cur), L.ptr(out_latent), L.ptr(pool), pool_env_stride,
-                       L.ptr(tail["wf"]), L.ptr(tail["b"]), tail["n"], B, L.stream())
-                return
-            if kind == "conv":
-                dst = bufs[which]
-                self.conv(cur, layer, dst, B, H, W, relu=False)
-                cur = dst
-                which ^= 1
-            elif kind == "res":
-                self.resblock(layer, cur, self.r_t, cur, B, H, W)
-            else:
-                dst = bufs[which]
-                C = self.p.c1
-                L.call("mzba_avgpool2", self.dt, L.ptr(cur), L.ptr(dst), B, H, W, C, L.stream())
-                H, W = H // 2, W // 2
-                cur = dst
-                which ^= 1
-        n = H * W * self.p.c1
-        L.call("mzba_scale_state", self.dt, L.ptr(cur), L.ptr(out_latent), L.ptr(pool), pool_env_stride, None, 0,
-               0, B, n, L.stream())
-
-    def fused_ok(self):
-        return self.use_fused and self.use_tower and self.p.fused is not None and self.tower_plan in (1, 2, 3)
-
-    def _ext(self, epilogue):
-        p, f = self.p, self.p.fused
-        x = L.TowerExt()
-        x.epilogue = epilogue
-        x.plan = self.tower_plan  # the kernel this runner was built for, whatever the global variant now says
-        x.smin, x.smax = float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"])
-        if epilogue == 1:
-            d16 = f.get("dyn16")
-            x.w0, x.b0, x.act_bias, x.A = L.ptr(d16["w0"] if d16 else f["w0"]), L.ptr(f["b0"]), L.ptr(f["act_bias"]), f["A"]
-            x.we1, x.be1 = L.ptr(d16["rw"] if d16 else f["rw"]), L.ptr(f["rb"])
-            x.lw[0], x.lb[0], x.lO[0] = L.ptr(d16["lw"] if d16 else p.rew_lin["wb"]), L.ptr(p.rew_lin["b"]), p.rew_lin["O"]
-            x.elem = 1 if d16 else 0
-        else:
-            x.we3, x.be3, x.we1, x.be1 = L.ptr(f["pw"]), L.ptr(f["pb"]), L.ptr(f["vw"]), L.ptr(f["vb"])
-            x.lw[0], x.lb[0], x.lO[0] = L.ptr(p.pol_lin["wb"]), L.ptr(p.pol_lin["b"]), p.pol_lin["O"]
-            x.lw[1], x.lb[1], x.lO[1] = L.ptr(p.val_lin["wb"]), L.ptr(p.val_lin["b"]), p.val_lin["O"]
-        return x
-
-    def _fused_call(self, tw, src, env_stride, slot, slot_stride, out, x):
-        pr = self.probe
-        if pr is not None:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        wf = self.p.tower_weights(tw, self.tower_plan, fp16=bool(x.elem))
-        L.call("mzba_tower_fused", L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(out), L.ptr(wf),
-               L.ptr(tw["b"]), tw["n"], self.B, ctypes.byref(x), L.stream())
-        if pr is not None:
-            e1.record()
-            pr.append((e0, e1, 2 * tw["n"] + (1 if x.w0 else 0)))
+        L.ops().representation_(self.native, x_in, out_latent, pool, pool_env_stride)
 
     def dynamics(self, parent_src, act, out_latent, r_dec, r_logits=None, slot=None, env_stride=None, slot_stride=0,
                  pool=None, pool_env_stride=0, pool_slot=0):
         """DynamicsNetwork + _scale_state (networks.py:151-167, 282-298) on NHWC latents.
         parent_src (+ slot gather) -> out_latent (scaled), r_dec (decoded reward)."""
-        B, H, W = self.B, self.p.lh, self.p.lw
-        p = self.p
-        if self.fused_ok():  # one launch: ConvBlock + 14 blocks + reward head + scale
-            x = self._ext(1)
-            x.act = L.ptr(act)
-            x.logits[0], x.dec[0] = L.ptr(r_logits), L.ptr(r_dec)
-            x.pool, x.pool_env_stride, x.pool_slot = L.ptr(pool), pool_env_stride, pool_slot
-            self._fused_call(p.dyn_tower, parent_src, H * W * p.c1 if env_stride is None else env_stride, slot,
-                             slot_stride, out_latent, x)
-            return
-        if p.dyn_fp16:
-            raise RuntimeError("the fp16 dynamics net runs on the fused dynamics step only (fused_ok() is False)")
-        self.conv(parent_src, p.dyn0, self.x, B, H, W, relu=True, slot=slot, env_stride=env_stride,
-                  slot_stride=slot_stride, act=act)
-        if p.dyn_tower is not None and self.use_tower:
-            self.tower(p.dyn_tower, self.x, self.x)
-        else:
-            for blk in p.dyn:
-                self.resblock(blk, self.x, self.t, self.x, B, H, W)
-        self.conv(self.x, p.rew_conv, self.rc, B, H, W, relu=True)
-        rl = p.rew_lin
-        if "wb" in rl:
-            L.call("mzba_heads_bf16", 1, L.ptr(self.rc), L.ptr(rl["wb"]), L.ptr(rl["b"]), rl["K"], rl["O"], 1,
-                   L.ptr(r_logits), L.ptr(r_dec), None, None, None, 0, 0, 0, None, None,
-                   float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B, L.stream())
-        else:
-            L.call("mzba_heads", self.dt, 1, L.ptr(self.rc), L.ptr(rl["w"]), L.ptr(rl["b"]), rl["K"], rl["O"], 1,
-                   L.ptr(r_logits), L.ptr(r_dec), None, None, None, 0, 0, 0, None, None,
-                   float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B, L.stream())
-        n = H * W * p.c1
-        L.call("mzba_scale_state", self.dt, L.ptr(self.x), L.ptr(out_latent), L.ptr(pool), pool_env_stride, None,
-               pool_slot, n, B, n, L.stream())
+        L.ops().dynamics_(self.native, parent_src, 0 if env_stride is None else env_stride, slot, slot_stride, act,
+                          out_latent, r_dec, r_logits, pool, pool_env_stride, pool_slot)
 
     def prediction(self, h, pi, v, p_logits=None, v_logits=None, tree=None):
         """PredictionNetwork (networks.py:225-241) + decode (mcts.py:97-100, 197-199).
-        tree: optional L.TreeStep — on the fused path the same launch then runs this simulation's
-        backup and the next selection (mcts.py:136-234); the caller checks fused_ok() first."""
-        B, H, W = self.B, self.p.lh, self.p.lw
-        p = self.p
-        if self.fused_ok():  # one launch: 14 blocks + policy / value heads (+ tree step)
-            x = self._ext(2)
-            x.logits[0], x.dec[0] = L.ptr(p_logits), L.ptr(pi)
-            x.logits[1], x.dec[1] = L.ptr(v_logits), L.ptr(v)
-            if tree is not None:
-                x.tree = ctypes.pointer(tree)
-            self._fused_call(p.pred_tower, h, H * W * p.c1, None, 0, None, x)
+        tree: optional (tree_args, sim, gamma, r) — the same launch then runs this simulation's backup
+        and the next selection (mcts.py:136-234; fused path only, mz::prediction_tree_)."""
+        if tree is None:
+            L.ops().prediction_(self.native, h, pi, v, p_logits, v_logits)
             return
-        if tree is not None:
-            raise RuntimeError("the tree step rides on the fused prediction launch only")
-        cur = h
-        if p.pred_tower is not None and self.use_tower:
-            self.tower(p.pred_tower, cur, self.x)
-            cur = self.x
-        else:
-            for i, blk in enumerate(p.pred):
-                self.resblock(blk, cur, self.t, self.x, B, H, W)
-                cur = self.x
-        self.conv(cur, p.pol_conv, self.pc, B, H, W, relu=True)
-        self.conv(cur, p.val_conv, self.vc, B, H, W, relu=True)
-        pl, vl = p.pol_lin, p.val_lin
-        if "wb" in pl and "wb" in vl:
-            L.call("mzba_heads_bf16", 2, L.ptr(self.pc), L.ptr(pl["wb"]), L.ptr(pl["b"]), pl["K"], pl["O"], 0,
-                   L.ptr(p_logits), L.ptr(pi), L.ptr(self.vc), L.ptr(vl["wb"]), L.ptr(vl["b"]), vl["K"], vl["O"], 1,
-                   L.ptr(v_logits), L.ptr(v), float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B,
-                   L.stream())
-            return
-        L.call("mzba_heads", self.dt, 2, L.ptr(self.pc), L.ptr(pl["w"]), L.ptr(pl["b"]), pl["K"], pl["O"], 0,
-               L.ptr(p_logits), L.ptr(pi), L.ptr(self.vc), L.ptr(vl["w"]), L.ptr(vl["b"]), vl["K"], vl["O"], 1,
-               L.ptr(v_logits), L.ptr(v), float(p.mcfg["supports_min"]), float(p.mcfg["supports_max"]), B,
-               L.stream())
+        if p_logits is not None or v_logits is not None:
+            raise ValueError("the tree step does not return logits")
+        tree_args, sim, gamma, r = tree
+        L.ops().prediction_tree_(self.native, h, pi, v, *tree_args, sim, gamma, r)
 
 
 class MuZeroAgent:
@@ -516,8 +452,11 @@ class MuZeroAgent:
             if tuple(np.shape(_np(sd[k]))) != tuple(shape):
                 raise ValueError(f"shape mismatch for {k}: {np.shape(_np(sd[k]))} vs {shape}")
         self._sd = {k: _np(sd[k]).copy() for k, _ in spec}
-        self.packed = PackedNets(self._sd, self.cfg, self.dtype, self.device, self.dyn_dtype)
-        self._runners = {}
+        packed = PackedNets(self._sd, self.cfg, self.dtype, self.device, self.dyn_dtype)
+        if self.packed is None:
+            self.packed = packed
+        else:  # a refresh: new weights into the existing buffers, live loops and graphs keep working
+            self.packed.refresh_from(packed)
 
     def eval_mode(self):
         pass  # BN always uses running stats on this path (networks.py:336-342)
@@ -528,49 +467,18 @@ class MuZeroAgent:
             self._runners[key] = NetRunner(self.packed, B, H, W)
         return self._runners[key]
 
-    # NCHW <-> NHWC glue (API surface only; the acting loop stays NHWC) ------------------
-    def _nhwc(self, x, cpad=None):
-        B, C, H, W = x.shape
-        cp = cpad or C
-        out = torch.zeros(B, H, W, cp, dtype=self.packed.tdt, device=self.device)
-        out[..., :C] = x.to(self.device).permute(0, 2, 3, 1).to(self.packed.tdt)
-        return out
-
-    def _nchw(self, x, B, C, H, W):
-        return x.view(B, H, W, C).permute(0, 3, 1, 2).float().contiguous()
-
+    # reference API on NCHW tensors: the torch.ops.mz net ops (csrc/net_ops.cpp) -----------------
     def create_hidden_state_root(self, state):
         """networks.py:271-280: (B, 2L, H, W) -> scaled latent (B, C, h, w)."""
-        B, C, H, W = state.shape
-        r = self.runner(B, H, W)
-        x = self._nhwc(state, _round64(C))
-        out = torch.empty(B * r.lhw * self.packed.c1, dtype=self.packed.tdt, device=self.device)
-        r.representation(x, out)
-        return self._nchw(out, B, self.packed.c1, self.packed.lh, self.packed.lw)
+        return L.ops().representation(self.packed.native, state.to(self.device))
 
     def hidden_state_transition(self, prev_hidden_state, action):
         """networks.py:282-298: action = one-hot planes (B, A, h, w) -> (h', reward logits)."""
-        B = prev_hidden_state.shape[0]
-        r = self.runner(B, *self._rep_hw())
-        x = self._nhwc(prev_hidden_state)
-        act = action.to(self.device)[:, :, 0, 0].argmax(dim=1).to(torch.int32).contiguous()
-        out = torch.empty(B * r.lhw * self.packed.c1, dtype=self.packed.tdt, device=self.device)
-        rdec = torch.empty(B, dtype=torch.float32, device=self.device)
-        rlog = torch.empty(B, self.packed.ns, dtype=torch.float32, device=self.device)
-        r.dynamics(x, act, out, rdec, rlog)
-        return self._nchw(out, B, self.packed.c1, self.packed.lh, self.packed.lw), rlog
+        return L.ops().dynamics(self.packed.native, prev_hidden_state.to(self.device), action.to(self.device))
 
     def evaluate_state(self, hidden_state):
         """networks.py:300-312 -> (policy logits (B,3), value logits (B,11))."""
-        B = hidden_state.shape[0]
-        r = self.runner(B, *self._rep_hw())
-        x = self._nhwc(hidden_state)
-        pi = torch.empty(B, 3, dtype=torch.float32, device=self.device)
-        v = torch.empty(B, dtype=torch.float32, device=self.device)
-        pl = torch.empty(B, 3, dtype=torch.float32, device=self.device)
-        vl = torch.empty(B, self.packed.ns, dtype=torch.float32, device=self.device)
-        r.prediction(x, pi, v, pl, vl)
-        return pl, vl
+        return L.ops().prediction(self.packed.native, hidden_state.to(self.device))
 
     def _rep_hw(self):
         return (self.packed.lh * 4, self.packed.lw * 4)

@@ -1,8 +1,10 @@
 """Latent MCTS on the MI355X path (mirror of src/mcts.py:MCTSSearchVec).
 
-The whole search runs on the device with no host synchronisation: per simulation
-one select kernel (all envs' tree walks), the dynamics net gathered from the latent
-node pool by the selected parent slots, the prediction net, and one backup kernel.
+The whole search runs on the device with no host synchronisation, every launch a torch custom op
+(`torch.ops.mz`): per simulation the fused dynamics step (`dynamics_`, parent latents gathered from
+the node pool by the selected slots) and the fused prediction step that also backs up the
+simulation and selects the next leaf (`prediction_tree_`); unfused, one select kernel, the
+prediction net and one backup kernel.
 The launch sequence is identical for every call of a given (B, S), so the acting loop
 can capture it in a HIP graph.
 """
@@ -41,13 +43,6 @@ class TreeState:
         self.counts = torch.empty(B, 3, dtype=torch.int64, device=device)
         self.values = torch.empty(B, dtype=torch.float32, device=device)
         self.noise = torch.empty(B, 3, dtype=torch.float32, device=device)
-
-    def step(self, env_offset, search_id, seed, ctx, sim, gamma, r):
-        """The same tree arguments as mzba_tree_step (fused prediction + backup + next select)."""
-        return L.TreeStep(L.ptr(self.nodes), L.ptr(self.root_sum), L.ptr(self.calls), L.ptr(self.leaf_parent),
-                          L.ptr(self.leaf_action), L.ptr(self.depth), L.ptr(self.path), L.ptr(self.sqrt_tab),
-                          L.ptr(self.c_tab), self.B, self.S, env_offset, search_id, seed, L.ptr(ctx), sim, gamma,
-                          L.ptr(r))
 
     def args(self, env_offset, search_id, seed, ctx=None):
         """Tree arguments of the torch.ops.mz tree ops (csrc/torch_ops.cpp). ctx: optional device
@@ -171,8 +166,7 @@ class SearchWorkspace:
                         env_stride=env_stride, slot_stride=n, pool=self.pool, pool_env_stride=env_stride,
                         pool_slot=sim + 1)
             if fused:  # prediction + backup(sim) + select(sim + 1) in one launch
-                rn.prediction(self.cur, self.pi, self.v,
-                              tree=self.tree.step(s.env_offset, search_id, s.seed, ctx, sim, gamma, self.r))
+                rn.prediction(self.cur, self.pi, self.v, tree=(ta, sim, gamma, self.r))
             else:
                 rn.prediction(self.cur, self.pi, self.v)
                 self.tree.backup(ta, sim, self.r, self.v, self.pi, gamma)

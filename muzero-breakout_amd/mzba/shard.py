@@ -144,7 +144,9 @@ def broadcast_state_dict(mcfg, state_dict, device, src=0):
 
 
 def refresh_target(agent, mcfg, state_dict, device, src=0):
-    """The acting ranks' target net <- rank src's learner weights (load_latest_weights)."""
+    """The acting ranks' target net <- rank src's learner weights (load_latest_weights). The agent
+    copies them into its packed device buffers in place (MuZeroAgent.load_state_dict), so acting
+    loops already built on it — and their captured step graphs — run the new weights next step."""
     sd = broadcast_state_dict(mcfg, state_dict, device, src)
     agent.load_state_dict({k: v.numpy() for k, v in sd.items()})
     return sd

@@ -92,6 +92,31 @@ def test_torch_custom_ops_registered():
     assert "Tensor(h!) values" in str(ops.mcts_results_.default._schema)
 
 
+def test_net_ops_schemas_declare_their_writes():
+    """The nets as custom ops (csrc/net_ops.cpp): the reference surface takes the weight pack
+    (mz.NetPack) and returns new tensors; the NHWC acting forms and the fused prediction + tree step
+    declare every buffer they write as Tensor(x!) — the tree buffers of prediction_tree_ included —
+    and nothing they only read."""
+    import torch
+    from mzba import _lib
+    ops = _lib.ops()
+    assert "__torch__.torch.classes.mz.NetPack nets" in str(ops.representation.default._schema)
+    for name, writes, reads in (
+            ("dynamics_", ["out", "r_dec", "r_logits", "pool"], ["src", "act", "slot"]),
+            ("prediction_", ["pi", "v", "p_logits", "v_logits"], ["h"]),
+            ("prediction_tree_", ["pi", "v", "nodes", "root_sum", "calls", "leaf_parent", "leaf_action", "depth",
+                                  "path"], ["h", "sqrt_tab", "c_tab", "r", "ctx"]),
+            ("representation_", ["out", "pool"], ["x"])):
+        args = {a.name: a for a in getattr(ops, name).default._schema.arguments}
+        for w in writes:
+            assert args[w].alias_info is not None and args[w].alias_info.is_write, (name, w)
+        for r in reads:
+            assert args[r].alias_info is None, (name, r)
+    p = torch.classes.mz.NetPack()
+    p.set_int("k", 7)
+    assert p.get_int("k") == 7 and not p.fused_ok()
+
+
 def test_default_checkpoint_optimizer_state_loads_into_reference_adam():
     """Without a learner, save_checkpoint writes a fresh Adam state that the reference's
     `optimizer.load_state_dict` (train_torch.py:646) accepts: one group, every parameter."""
