@@ -45,6 +45,8 @@ def parse():
                     help="bounded CPU sample (cpu_baseline + match rate): ~10 s of the CPU port on 16 host cores")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the f32 parity-path replay of the first timed step (full-batch visit-count match)")
     ap.add_argument("--learner-streams", type=int, default=2, choices=[1, 2],
                     help="learner: 2 = prediction nets on a side stream beside the dynamics chain")
     ap.add_argument("--tower-variant", type=int, default=0, help="tower kernel (mzba_tower_set_variant; 0 = by batch)")
@@ -305,6 +307,77 @@ def conv_flops(B, hw, C):
     return 2.0 * B * hw * C * 9 * C
 
 
+PEAK_F32_TFLOPS = 157.3  # MI355X dense f32 MFMA (MI355X_MICROARCH.md chip table)
+
+
+def want_parity(args, rank, world, custom_geom):
+    return rank == 0 and world == 1 and not args.no_parity and not custom_geom and args.dtype != "f32"
+
+
+LOOP_STATE = ("paddle", "bx", "by", "dx", "dy", "done", "bricks", "cur_frame", "cur_src", "hist_frames", "hist_actions",
+              "hist_len", "reward", "valid")
+
+
+def snapshot_loop(loop):
+    """Device copies of everything an acting step reads: the compact env state, the frame-history
+    ring and the step context (search id, step index, record row)."""
+    env = loop.env
+    snap = {k: getattr(env, k).clone() for k in LOOP_STATE if getattr(env, k) is not None}
+    snap["ctx"] = loop.ctx.clone()
+    snap["ids"] = (loop.search_id, loop.step_index, loop.t)
+    return snap
+
+
+def restore_loop(loop, snap):
+    for k in LOOP_STATE:
+        if k in snap:
+            getattr(loop.env, k).copy_(snap[k])
+    loop.ctx.copy_(snap["ctx"])
+    loop.search_id, loop.step_index, loop.t = snap["ids"]
+
+
+def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
+    """The first timed step replayed on the f32 parity path (networks within 1e-5 of the reference,
+    bit-exact trees): the same env state, search id and keyed randomness as the benchmarked step.
+    Returns the fraction of all B envs whose visit counts equal the benchmarked step's, and the parity
+    path's own throughput (second replay, timed with HIP events) against the dense f32 MFMA peak."""
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingLoop
+    ag32 = MuZeroAgent(mcfg, dtype="f32", device=loop.agent.device)
+    ag32.load_state_dict(sd)
+    l32 = ActingLoop(cfg, ag32, B, seed=args.seed, env_offset=loop.env_offset, height=H, width=W,
+                     n_envs_total=loop.n_envs_total)
+    l32.temperature = loop.temperature
+    l32.search.noise_weight = loop.search.noise_weight
+    l32.reset(0)
+    counts, ms = [], []
+    for _ in range(2):  # the first replay also warms the f32 path (scratch, code objects)
+        restore_loop(l32, snap)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        l32.act(eager=True)
+        e1.record()
+        torch.cuda.synchronize()
+        ms.append(e0.elapsed_time(e1))
+        counts.append(l32.rec["counts"][t0].cpu().numpy())
+    c16 = loop.rec["counts"][t0].cpu().numpy()
+    same = (counts[-1] == c16).all(1)
+    v16, v32 = loop.rec["values"][t0].cpu().numpy(), l32.rec["values"][t0].cpu().numpy()
+    eps = B / (ms[-1] * 1e-3)
+    fl = step_flops(ag32.packed, H, W, args.sims)
+    out = {"match": float(same.mean()),
+           "path": {"dtype": "f32", "value": eps, "unit": "env-steps/s", "ms_per_step": ms[-1],
+                    "achieved_tflops": eps * fl / 1e12, "peak": PEAK_F32_TFLOPS,
+                    "frac": eps * fl / 1e12 / PEAK_F32_TFLOPS,
+                    "deterministic": bool((counts[0] == counts[1]).all()),
+                    "value_max_abs_diff_where_counts_agree": float(np.abs(v16 - v32)[same].max()) if same.any() else None,
+                    "what": "one acting step of the same envs on the f32 parity path (f32 MFMA convs, separate "
+                            "launches per layer), eager, HIP events around the step"}}
+    del l32, ag32
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -360,6 +433,7 @@ def main():
     def one_step(eager=False):
         if loop.t >= loop.max_steps or (loop.t > 0 and loop.all_done()):
             flush()
+            gather.fence()  # the new episode rewrites record row 0..: after the last pack
             loop.reset()
             last_flush[0] = 0
         loop.act(eager=eager)
@@ -418,6 +492,10 @@ def main():
                               f"per-env Python trees): representation + {args.sims}-sim search for {nb} envs of the "
                               f"bench's own state, 1 acting step ({cpu_s:.1f} s)"}
 
+    # the state before the first timed step: the f32 parity path replays that step afterwards
+    snap = snapshot_loop(loop) if want_parity(args, rank, world, custom_geom) else None
+    t_snap = loop.t
+
     # ---- timed region ---------------------------------------------------------------------
     probe = []
     runner = loop.ws.runner
@@ -446,6 +524,9 @@ def main():
     # per-conv average over the latent residual convs
     conv_ms = (float(sum(ms for ms, _ in probe) / sum(n for _, n in probe))) if probe else None
     tower_launch_ms = (float(np.mean([ms for ms, n in probe if n > 1])) if any(n > 1 for _, n in probe) else None)
+    parity = None
+    if snap is not None:  # after the timed region: nothing here is timed in `value`
+        parity = f32_parity_path(cfg, mcfg, sd, loop, snap, t_snap, args, B, H, W)
     p = agent.packed
     fl = conv_flops(B, p.lh * p.lw, p.c1)
     achieved = fl / (conv_ms * 1e-3) / 1e12 if conv_ms else None
@@ -490,6 +571,13 @@ def main():
             "visit_count_match_sample": (f"{min(args.cpu_envs, B)} envs, bf16 HIP path vs the f32 CPU port (same keyed "
                                          "noise / tie-breaks)") if match is not None else None,
             "visit_count_match_f32_path": match_f32,
+            # every env of the first timed step: the benchmarked bf16 path against this build's f32
+            # parity path (1e-5 nets, bit-exact trees) replaying that step from the same state
+            "visit_count_match_full": parity and parity["match"],
+            "visit_count_match_full_sample": parity and (
+                f"all {B} envs of the first timed step: {args.dtype} HIP path vs the f32 HIP parity path from the "
+                "same env state, search id and keyed noise / tie-breaks"),
+            "parity_path": parity and parity["path"],
             "launch": "eager" if args.no_graph else "hip-graph replay (probe step eager)",
             "whole_step_mfma_frac": (B * world * step_flops(agent.packed, H, W, args.sims) * args.steps / dt / 1e12)
                                     / (PEAK_BF16_TFLOPS * world),

@@ -18,6 +18,7 @@ exchange:
 Record layout per (step, env), little-endian, REC_BYTES = 28 + HW:
   action u8 | mask u8 | pad u16 | reward f32 | value f32 | counts i32[3] | pad u32 | frame u8[HW]
 """
+import contextlib
 from collections import OrderedDict
 
 import numpy as np
@@ -66,40 +67,67 @@ def unpack_records(buf):
 
 
 class TrajectoryGather:
-    """Gather of packed record slabs to rank 0, then into its pinned host buffer."""
+    """Gather of packed record slabs to rank 0, then into its pinned host buffer.
+
+    On a GPU the whole exchange (pack, RCCL gather, D2H copy) runs on a side stream behind an event
+    recorded on the acting stream, so it overlaps the next acting steps; `fence()` makes the acting
+    stream wait for the last pack before record rows are reused (a new episode restarts at row 0)."""
 
     def __init__(self, world_size, rank, k_steps, B, hw, device, pin=True):
         self.ws, self.rank, self.k, self.B, self.hw = world_size, rank, k_steps, B, hw
         self.device = torch.device(device)
         self.slab = torch.zeros(k_steps, B, rec_bytes(hw), dtype=torch.uint8, device=self.device)
         self.gathered = self.host = self.copied = None
+        self.side = self.packed = None
         if rank == 0:
             self.gathered = torch.zeros(world_size, k_steps, B, rec_bytes(hw), dtype=torch.uint8, device=self.device)
             self.host = torch.zeros(world_size, k_steps, B, rec_bytes(hw), dtype=torch.uint8,
                                     pin_memory=pin and self.device.type == "cuda")
 
     def exchange(self, rec, t0, t1):
-        """Records of steps [t0, t1) (t1 - t0 <= k) of every rank -> rank 0. Every rank calls it."""
+        """Records of steps [t0, t1) (t1 - t0 <= k) of every rank -> rank 0. Every rank calls it.
+        With torch.distributed initialised the collective runs at any world size (RCCL on the
+        device with backend "nccl"; gloo moves host copies)."""
         n = t1 - t0
-        pack_records(rec, t0, t1, self.slab[:n])
-        if self.ws > 1:
-            if dist.get_backend() == "gloo" and self.device.type == "cuda":
-                # gloo gathers host tensors only (CPU tests, and bench.py's one-GPU rehearsal)
-                gl = [torch.empty_like(self.slab, device="cpu") for _ in range(self.ws)] if self.rank == 0 else None
-                dist.gather(self.slab.cpu(), gl, dst=0)
-                if self.rank == 0:
-                    self.gathered.copy_(torch.stack(gl))
-            else:
-                gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
-                dist.gather(self.slab, gl, dst=0)
-        elif self.rank == 0:
-            self.gathered[0].copy_(self.slab)
-        if self.rank == 0:
-            self.host.copy_(self.gathered, non_blocking=True)
-            if self.device.type == "cuda":  # host_records() waits for exactly this copy
-                self.copied = torch.cuda.Event()
-                self.copied.record()
+        cuda = self.device.type == "cuda"
+        if cuda:
+            if self.side is None:
+                self.side = torch.cuda.Stream(device=self.device)
+            ready = torch.cuda.Event()
+            ready.record()  # every record row written so far (acting stream)
+            self.side.wait_event(ready)
+            stream = torch.cuda.stream(self.side)
+        else:
+            stream = contextlib.nullcontext()
+        with stream:
+            pack_records(rec, t0, t1, self.slab[:n])
+            if cuda:
+                self.packed = torch.cuda.Event()
+                self.packed.record()
+            if dist.is_available() and dist.is_initialized():
+                if dist.get_backend() == "gloo" and cuda:
+                    # gloo gathers host tensors only (CPU tests, and bench.py's one-GPU rehearsal)
+                    gl = [torch.empty_like(self.slab, device="cpu") for _ in range(self.ws)] if self.rank == 0 else None
+                    dist.gather(self.slab.cpu(), gl, dst=0)
+                    if self.rank == 0:
+                        self.gathered.copy_(torch.stack(gl))
+                else:
+                    gl = list(self.gathered.unbind(0)) if self.rank == 0 else None
+                    dist.gather(self.slab, gl, dst=0)
+            elif self.rank == 0:
+                self.gathered[0].copy_(self.slab)
+            if self.rank == 0:
+                self.host.copy_(self.gathered, non_blocking=True)
+                if cuda:  # host_records() waits for exactly this copy
+                    self.copied = torch.cuda.Event()
+                    self.copied.record()
         return n
+
+    def fence(self):
+        """The acting stream waits until the last exchange has packed its rows (call before the
+        record rows are overwritten, e.g. before ActingLoop.reset)."""
+        if self.packed is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.packed)
 
     def host_records(self, n):
         """rank 0: dict of (n, world*B, ...) in global env order."""

@@ -148,13 +148,18 @@ def test_config5_acting_step_4096x200_fp16_and_bf16_vs_f32_path():
     """Config 5 end to end: one acting step of 4096 envs x 200 sims with the full-width nets, the
     dynamics net in fp16 (the config's precision, tower8_kernel<1,2>) and in bf16, each against the
     same step on the f32 parity path (same state, same keyed noise and tie-breaks). Every count row
-    sums to 200. Stated bound: at least 80 % of envs with identical visit counts (bf16/fp16 rounding
-    in 2 x 14-block towers moves PUCT decisions that are close; 200 sims give the trees more such
-    decisions than 50 do), and where counts agree the root values agree within 0.05 absolute."""
+    sums to 200.
+    Stated bound: reduced-precision rounding in the 2 x 14-block towers moves PUCT decisions that are
+    close, and every moved decision of the 200 changes the final counts, so exact agreement falls with
+    S (measured at 1024 envs, tools/parity_sweep.py: 0.80 / 0.55 / 0.12 of envs at S = 50 / 100 / 200
+    for bf16) while the counts stay close (L1 distance of the count rows: mean 2.9, max 10 of 200).
+    Asserted: mean L1 distance <= 0.03 S, max <= 0.1 S, the most-visited action equal in >= 85 % of
+    envs, root values within 0.02; and the fp16 dynamics net is at least as close to f32 as bf16 in
+    root value (mean |dv| <= 1.1x bf16's; measured 0.00074 vs 0.00132)."""
     from mzba.agent import MuZeroAgent
     from mzba.acting import ActingLoop
     cfg = default_config()
-    cfg["num_simulations"] = 200
+    S = cfg["num_simulations"] = 200
     sd = init_state_dict(cfg["model"], 6)
     B = 4096
     out = {}
@@ -169,12 +174,18 @@ def test_config5_acting_step_4096x200_fp16_and_bf16_vs_f32_path():
         out[name] = {k: v[0].cpu().numpy() for k, v in loop.rec.items() if v is not None}
         del loop, ag
         torch.cuda.empty_cache()
-    c32 = out["f32"]["counts"]
-    assert (c32.sum(1) == 200).all()
+    c32, v32 = out["f32"]["counts"], out["f32"]["values"]
+    assert (c32.sum(1) == S).all()
+    dv = {}
     for name in ("bf16", "fp16dyn"):
         c = out[name]["counts"]
-        assert (c.sum(1) == 200).all(), name
-        same = (c == c32).all(1)
-        print(f"config 5 {name} vs f32 path visit-count agreement at 4096 x 200: {same.mean():.4f}")
-        assert same.mean() >= 0.80, (name, same.mean())
-        assert np.abs(out[name]["values"][same] - out["f32"]["values"][same]).max() <= 0.05, name
+        assert (c.sum(1) == S).all(), name
+        l1 = np.abs(c - c32).sum(1)
+        top = (c.argmax(1) == c32.argmax(1)).mean()
+        dv[name] = np.abs(out[name]["values"] - v32)
+        print(f"config 5 {name} vs f32 path at 4096 x 200: exact {(l1 == 0).mean():.4f}, L1 mean {l1.mean():.2f} "
+              f"max {l1.max()}, top action {top:.4f}, |dv| mean {dv[name].mean():.2e} max {dv[name].max():.2e}")
+        assert l1.mean() <= 0.03 * S and l1.max() <= 0.1 * S, (name, l1.mean(), l1.max())
+        assert top >= 0.85, (name, top)
+        assert dv[name].max() <= 0.02, name
+    assert dv["fp16dyn"].mean() <= 1.1 * dv["bf16"].mean(), (dv["fp16dyn"].mean(), dv["bf16"].mean())

@@ -1195,15 +1195,16 @@ def test_checkpoint_reference_format_roundtrip(tmp_path):
     assert buf.get_reward_sums() == buf2.get_reward_sums()
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
-def test_tree_step_fused_into_prediction_is_identical(variant):
+@pytest.mark.parametrize("variant,S", [(1, 12), (2, 12), (3, 12), (2, 200), (3, 200)])
+def test_tree_step_fused_into_prediction_is_identical(variant, S):
     """backup(sim) + select(sim + 1) inside the fused prediction launch == the separate tree
-    kernels: same visit counts, values and tie-break draws, bit for bit (bf16 nets)."""
+    kernels: same visit counts, values and tie-break draws, bit for bit (bf16 nets), at 12 and at
+    config 5's 200 simulations (201-node trees)."""
     from mzba import _lib as L
     from mzba.agent import MuZeroAgent
     from mzba.search import MCTSSearchVec
     cfg = default_config()
-    cfg["num_simulations"] = 12
+    cfg["num_simulations"] = S
     mcfg = cfg["model"]
     ag = MuZeroAgent(mcfg, dtype="bf16")
     ag.load_state_dict(init_state_dict(mcfg, 4))
