@@ -313,19 +313,20 @@ int mzba_mcts_results(void* nodes, float* root_sum, uint32_t* calls, int32_t* le
 
 /* Temperature sampling (train_torch.py:191-198 `visit_counts ** (1/self.temperature)` / sum(dim=1) then
  * Categorical(probs[i]).sample()): probs bit-identical to torch's CPU evaluation on the reference's whole
- * (n_envs_total, 3) int64 batch tensor (csrc/torch_pow.h: SLEEF powf_u10 on its first
- * 3n - 3n % vec_block elements, f32(pow(double)) on the rest; vec_block = 32 for the AVX512 host the
- * fixtures came from, 16 for AVX2), then the inverse CDF of u = Philox uniform(env + env_offset,
+ * (n_envs_total, 3) int64 batch tensor (csrc/torch_pow.h: SLEEF powf_u10 on the vectorized part, f32(pow(double))
+ * on the scalar tails; vec_block = 32 for the AVX512 host the fixtures came from, 16 for AVX2; pow_threads =
+ * the reference process's intra-op threads: from 32768 elements on, torch splits the tensor into per-thread
+ * chunks, each with its own scalar tail), then the inverse CDF of u = Philox uniform(env + env_offset,
  * stream 3, step, 0). inv_t = 1/T in double (Python's `1/self.temperature`); inv_t_dev (optional,
  * device f64[1]) overrides it (graph-replayable temperature schedule). probs_out (optional) f32[B][3]. */
 int mzba_sample_actions(const int64_t* counts, int64_t* action, float* probs_out, int B, double inv_t,
-                        const double* inv_t_dev, int n_envs_total, int vec_block, int env_offset, int step,
-                        uint64_t seed, const int32_t* ctx, hipStream_t stream);
+                        const double* inv_t_dev, int n_envs_total, int vec_block, int pow_threads, int env_offset,
+                        int step, uint64_t seed, const int32_t* ctx, hipStream_t stream);
 
 /* torch's CPU `int64 counts ** e` (the power of mzba_sample_actions) for n elements at flat positions
  * [start, start + n) of a tensor of n_total elements: out f32[n]. Exposed for the parity tests. */
 int mzba_torch_pow(const int64_t* counts, float* out, long long n, double e, long long start, long long n_total,
-                   int vec_block, hipStream_t stream);
+                   int vec_block, int pow_threads, hipStream_t stream);
 
 /* Trajectory-sink row of the search results: rec_counts[t][b] = counts[b], rec_values[t][b] = values[b],
  * t = ctx ? ctx[2] : t (replay_buffer.py:17-35 visit_counts / values). */

@@ -45,6 +45,31 @@ struct BandArgs {
   int B, relu;
 };
 
+#ifndef BAND_ONEPASS
+#define BAND_ONEPASS 1  // 0: the three per-shift k loops (band_dx) everywhere, for A/B builds
+#endif
+#ifndef BAND_ONEPASS128
+#define BAND_ONEPASS128 1  // the Cout 128 convs on the one pass too (3-entry ring at 5 columns); 0: A/B build
+#endif
+
+#ifdef BAND_STAMPS
+// diagnostic build only (make band-stamps -> libmzba_bstamp.so, tools/stamp_band.py): s_memtime at the
+// phase boundaries, per workgroup and wave: 0 entry, 1 band staged, 2 k loop done, 3 residual staged,
+// 4 epilogue in LDS, 5 exit; 6 / 7 s_memrealtime at entry / exit (100 MHz)
+constexpr int BST_N = 8, BST_WG = 8192;
+__device__ unsigned long long mz_band_stamps[BST_WG * 4][BST_N];
+MZ_DEV void bstamp(int k, bool real = false) {
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < BST_WG)
+    mz_band_stamps[blockIdx.x * 4 + (threadIdx.x >> 6)][k] =
+        real ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+}
+#define BSTAMP(k) bstamp(k)
+#define BSTAMP_REAL(k) bstamp(k, true)
+#else
+#define BSTAMP(k) ((void)0)
+#define BSTAMP_REAL(k) ((void)0)
+#endif
+
 template <int CIN, int COUT, int XT>
 struct BandGeo {
   // weight ring depth (k steps; 2 at two workgroups per CU). Ring slot = step % TDB is taken as
@@ -54,7 +79,7 @@ struct BandGeo {
   static constexpr int NSRC = XT + 2;              // staged source columns (with the halo)
   // one-pass weight ring (band_all): 3 entries (dx = -1, 0, +1) per k step; two steps in flight, one
   // where two workgroups per CU leave 256 registers per lane for 4 column tiles (6 entries spilled 52)
-  static constexpr int RDB = (XT == 5 && COUT == 256) ? 3 : 6;
+  static constexpr int RDB = (XT == 5 && (COUT == 256 || BAND_ONEPASS128)) ? 3 : 6;
   // LDS bytes per source row: at Cin 64 the row is padded to 128 channels, so a chunk index XORed
   // with the 4-bit row key stays inside the row (staging and reads use the same mapping; the pad
   // chunks are never read)
@@ -136,15 +161,13 @@ __device__ __forceinline__ void band_dx(const uint8_t* __restrict__ lds, __amdgp
   }
 }
 
-#ifndef BAND_ONEPASS
-#define BAND_ONEPASS 1  // 0: the three per-shift k loops (band_dx) everywhere, for A/B builds
-#endif
-// the one pass runs the Cout 256 convs (B = 4096 isolated: 256->256 1202 -> 1131 us, 128->256 675 ->
-// 639 us); at Cout 128 it was 3 % slower with a 6-entry ring (358 -> 370 us at 128->128) and 3.5 %
-// faster with a 3-entry one (368 -> 355 us), but that build moved the bf16 learner's gradients enough to
-// fail test_learner_fused_bn_statistics_track_separate_passes (min cosine 0.93 < 0.98, a noise bound
-// between two bf16 realisations), so the Cout 128 convs keep the three loops
-template <int COUT> constexpr bool band_one = BAND_ONEPASS && COUT == 256;
+
+// the one pass runs every conv (B = 4096 isolated: 256->256 1202 -> 1131 us, 128->256 675 -> 639 us;
+// 128->128 with the 3-entry ring 368 -> 355 us). The Cout 128 convs kept the three loops in round 2
+// because their one pass moved the bf16 learner's gradients past a noise bound between two bf16
+// realisations; that bound was a lucky seed (tools/learner_bn_calib.py: 0.86 - 0.9998 over 6 seeds on
+// either build) and the learner test now checks each realisation against the f32 path instead
+template <int COUT> constexpr bool band_one = BAND_ONEPASS && (COUT == 256 || BAND_ONEPASS128);
 
 // pack step of one-pass ring entry e = 3 (dyi * NC + c) + d (d = dx + 1)
 template <int NC>
@@ -240,6 +263,8 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
   __shared__ __attribute__((aligned(16))) uint8_t lds[G::BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / NB, x0 = (blockIdx.x % NB) * XT;
+  BSTAMP_REAL(6);
+  BSTAMP(0);
   // stage the band: NSRC*16 rows x NCH chunks, then the zero block. Every load of the band is in
   // flight at once (one memory round trip; batches of 4 per thread behind a `#pragma unroll 1` waited
   // once per batch)
@@ -270,6 +295,7 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
     for (int i = tid; i < G::RB; i += BNT) *reinterpret_cast<uint4*>(lds + G::LZ + i * 16) = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
+  BSTAMP(1);
   // this wave's column tiles of the weight pack through a wave-uniform buffer resource (one VGPR for
   // the lane offset; the (tile, step) offset in an SGPR)
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -293,6 +319,7 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
     band_dx<CIN, COUT, XT, 0>(lds, wrs, bq, acc, lane);
     band_dx<CIN, COUT, XT, 1>(lds, wrs, bq, acc, lane);
   }
+  BSTAMP(2);
   __syncthreads();  // the band is no longer read
   // output tile in LDS: row 16 t + y, 16-B chunks swizzled by KEY[y]
   constexpr int ONCH = COUT / 8;
@@ -315,6 +342,7 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
     }
     __syncthreads();
   }
+  BSTAMP(3);
   {
     const int q = lane >> 4, ys = nib(SIG, lane & 15), ky = nib(KEY, ys);
     float4 bias4[CTW];  // every bias load in flight before the first use
@@ -342,16 +370,19 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
     }
   }
   __syncthreads();
+  BSTAMP(4);
   for (int i = tid; i < XT * 16 * ONCH; i += BNT) {
     const int row = i / ONCH, ch = i % ONCH, t = row >> 4, y = row & 15;
     *reinterpret_cast<uint4*>(gout + (size_t)(y * BW + x0 + t) * COUT + ch * 8) =
         *reinterpret_cast<const uint4*>(lds + row * G::OB + ((ch ^ nib(KEY, y)) << 4));
   }
+  BSTAMP(5);
+  BSTAMP_REAL(7);
 }
 
 }  // namespace
 
-static int g_band_xt = 5;  // output columns per workgroup (mzba_conv_band_set_xt)
+static thread_local int g_band_xt = 5;  // output columns per workgroup (mzba_conv_band_set_xt; per thread)
 
 extern "C" {
 
@@ -363,6 +394,12 @@ int mzba_conv_band_set_xt(int xt) {
   g_band_xt = xt;
   return 0;
 }
+
+#ifdef BAND_STAMPS
+int mzba_band_stamps_read(unsigned long long* host, int nrows) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mz_band_stamps), sizeof(unsigned long long) * BST_N * nrows);
+}
+#endif
 
 int mzba_conv_band_supported(int H, int W, int Cin, int Cout, int ks) {
   return H == BH && W == BW && ks == 3 && ((Cin == 64 && Cout == 128) || ((Cin == 128 || Cin == 256) &&

@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256) void scale_state_big_kernel(const T* __restric
   }
 }
 
-static int g_conv_big = 1;  // 1: large bf16 convs on conv_big_bf16_kernel (mzba_conv2d_set_variant)
+static thread_local int g_conv_big = 1;  // 1: large bf16 convs on conv_big_bf16_kernel (mzba_conv2d_set_variant)
 
 template <typename T>
 int launch_conv(const ConvArgs& a, hipStream_t s) {

@@ -475,7 +475,7 @@ __global__ void current_frame_kernel(const uint8_t* __restrict__ cur_frame, Hist
 
 }  // namespace
 
-static int g_block_envs = 0;  // 0 = automatic (mzba_env_set_block_envs, diagnostics)
+static thread_local int g_block_envs = 0;  // 0 = automatic (mzba_env_set_block_envs, diagnostics)
 
 // =============================================================================== C ABI
 extern "C" {

@@ -1282,7 +1282,7 @@ int mzba_conv_pack_bf16(const float* w, void* out, int Cout, int taps, int Cin, 
   return 0;
 }
 
-static int g_wgrad_img = 1;
+static thread_local int g_wgrad_img = 1;
 // 1 (default): bf16 3x3 weight gradients on the whole-image kernel where it wins (see
 // wgrad_img_eligible); 2: whole-image kernel for every supported shape; 0: per-tap kernel only
 int mzba_conv_wgrad_set_variant(int v) {

@@ -130,15 +130,15 @@ __global__ void results_kernel(TreeArgs t, int64_t* __restrict__ counts, float* 
 // 1/T (double) comes from inv_t_dev[0] when given (one captured graph replays any temperature).
 __global__ void sample_kernel(const int64_t* __restrict__ counts, int64_t* __restrict__ action,
                               float* __restrict__ probs_out, int B, double inv_t_arg,
-                              const double* __restrict__ inv_t_dev, long long nvec, int env_offset, int step_arg,
-                              uint64_t seed, const int32_t* __restrict__ ctx) {
+                              const double* __restrict__ inv_t_dev, long long n_total, long long chunk, int vb,
+                              int env_offset, int step_arg, uint64_t seed, const int32_t* __restrict__ ctx) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   const int step = ctx ? ctx[1] : step_arg;
   const double e = inv_t_dev ? inv_t_dev[0] : inv_t_arg;
   float vt[3];
   for (int a = 0; a < 3; ++a)
-    vt[a] = mzpow::torch_cpu_pow(counts[b * 3 + a], e, 3LL * (b + env_offset) + a, nvec);
+    vt[a] = mzpow::torch_cpu_pow(counts[b * 3 + a], e, 3LL * (b + env_offset) + a, chunk, n_total, vb);
   const float s = (vt[0] + vt[1]) + vt[2];  // train_torch.py:193 sum(dim=1): ((c0 + c1) + c2)
   const float u = mz_uniform((uint32_t)(b + env_offset), MZ_STREAM_SAMPLE, (uint32_t)step, 0u, seed);
   float cdf = 0.f;
@@ -153,12 +153,12 @@ __global__ void sample_kernel(const int64_t* __restrict__ counts, int64_t* __res
   action[b] = chosen >= 0 ? chosen : last;
 }
 
-// torch's CPU int64 ** e (torch_pow.h) for n elements at flat positions [start, start + n) of a tensor
-// with vector-lane prefix nvec: the device pow exposed for exhaustive parity tests
+// torch's CPU int64 ** e (torch_pow.h) for n elements at flat positions [start, start + n) of a tensor of
+// n_total elements (thread chunks of `chunk`): the device pow exposed for exhaustive parity tests
 __global__ void torch_pow_kernel(const int64_t* __restrict__ counts, float* __restrict__ out, long long n, double e,
-                                 long long start, long long nvec) {
+                                 long long start, long long n_total, long long chunk, int vb) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = mzpow::torch_cpu_pow(counts[i], e, start + i, nvec);
+  if (i < n) out[i] = mzpow::torch_cpu_pow(counts[i], e, start + i, chunk, n_total, vb);
 }
 
 // acting-loop records of the search results at row ctx[2] (train_torch.py:204-208 sink)
@@ -231,22 +231,22 @@ int mzba_mcts_results(MZ_TREE_PARAMS, int64_t* counts, float* values, hipStream_
 }
 
 int mzba_sample_actions(const int64_t* counts, int64_t* action, float* probs_out, int B, double inv_t,
-                        const double* inv_t_dev, int n_envs_total, int vec_block, int env_offset, int step,
-                        uint64_t seed, const int32_t* ctx, hipStream_t stream) {
-  MZ_CHECK_ARG(B > 0 && counts && action && (inv_t_dev || inv_t > 0.0) && vec_block > 0 && env_offset >= 0 &&
-                   n_envs_total >= env_offset + B, -1);
+                        const double* inv_t_dev, int n_envs_total, int vec_block, int pow_threads, int env_offset,
+                        int step, uint64_t seed, const int32_t* ctx, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && counts && action && (inv_t_dev || inv_t > 0.0) && vec_block > 0 && pow_threads >= 1 &&
+                   env_offset >= 0 && n_envs_total >= env_offset + B, -1);
   const long long n = 3LL * n_envs_total;
   hipLaunchKernelGGL(sample_kernel, dim3((B + 255) / 256), dim3(256), 0, stream, counts, action, probs_out, B, inv_t,
-                     inv_t_dev, n - n % vec_block, env_offset, step, seed, ctx);
+                     inv_t_dev, n, mzpow::torch_pow_chunk(n, pow_threads), vec_block, env_offset, step, seed, ctx);
   MZ_LAUNCH_CHECK();
   return 0;
 }
 
 int mzba_torch_pow(const int64_t* counts, float* out, long long n, double e, long long start, long long n_total,
-                   int vec_block, hipStream_t stream) {
-  MZ_CHECK_ARG(n > 0 && counts && out && vec_block > 0 && start >= 0 && n_total >= start + n, -1);
+                   int vec_block, int pow_threads, hipStream_t stream) {
+  MZ_CHECK_ARG(n > 0 && counts && out && vec_block > 0 && pow_threads >= 1 && start >= 0 && n_total >= start + n, -1);
   hipLaunchKernelGGL(torch_pow_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, counts, out, n, e,
-                     start, n_total - n_total % vec_block);
+                     start, n_total, mzpow::torch_pow_chunk(n_total, pow_threads), vec_block);
   MZ_LAUNCH_CHECK();
   return 0;
 }

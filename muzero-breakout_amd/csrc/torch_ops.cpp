@@ -195,15 +195,16 @@ void mcts_results_(const at::Tensor& nodes_, const at::Tensor& root_sum_, const 
 // ---- temperature sampling, support decode -------------------------------------------------------
 std::tuple<at::Tensor, at::Tensor> sample_actions(const at::Tensor& counts, double inv_t,
                                                   const c10::optional<at::Tensor>& inv_t_dev, int64_t n_envs_total,
-                                                  int64_t vec_block, int64_t env_offset, int64_t step, int64_t seed,
-                                                  const c10::optional<at::Tensor>& ctx) {
+                                                  int64_t vec_block, int64_t pow_threads, int64_t env_offset,
+                                                  int64_t step, int64_t seed, const c10::optional<at::Tensor>& ctx) {
   check_dev(counts, "counts", at::kLong);
   TORCH_CHECK(counts.dim() == 2 && counts.size(1) == 3, "mz::sample_actions: counts must be (B, 3)");
   const int B = (int)counts.size(0);
   at::Tensor action = at::empty({B}, counts.options());
   at::Tensor probs = at::empty({B, 3}, counts.options().dtype(at::kFloat));
   check_rc(mzba_sample_actions(counts.data_ptr<int64_t>(), action.data_ptr<int64_t>(), probs.data_ptr<float>(), B, inv_t,
-                               ptr_or_null<double>(inv_t_dev), (int)n_envs_total, (int)vec_block, (int)env_offset,
+                               ptr_or_null<double>(inv_t_dev), (int)n_envs_total, (int)vec_block, (int)pow_threads,
+                               (int)env_offset,
                                (int)step, (uint64_t)seed, ptr_or_null<int32_t>(ctx), cur_stream(counts)),
            "mzba_sample_actions");
   return {action, probs};
@@ -236,7 +237,7 @@ TORCH_LIBRARY(mz, m) {
   m.def("mcts_backup_(" MZ_TREE_SCHEMA ", int sim, Tensor r, Tensor v, Tensor pi, float gamma) -> ()");
   m.def("mcts_results_(" MZ_TREE_SCHEMA_RO ", Tensor(h!) values, Tensor(i!) counts) -> ()");
   m.def("sample_actions(Tensor counts, float inv_t, Tensor? inv_t_dev, int n_envs_total, int vec_block, "
-        "int env_offset, int step, int seed, Tensor? ctx) -> (Tensor action, Tensor probs)");
+        "int pow_threads, int env_offset, int step, int seed, Tensor? ctx) -> (Tensor action, Tensor probs)");
   m.def("support_decode(Tensor logits, float smin, float smax) -> Tensor");
 }
 

@@ -10,6 +10,7 @@
 // division, fmaf and the op order below: compiled with -ffp-contract=off. Pinned bit for bit against
 // torch (tests/golden/sampling.npz; oracle/torch_pow.c is the CPU twin used by the tests).
 #pragma once
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 namespace mzpow {
@@ -103,17 +104,36 @@ __device__ __forceinline__ float sleef_powf_u10(float x, float y) {
   return expk(mul_f2f(logk(x), y));
 }
 
-// one element of torch's CPU `int64 counts ** e` at flat position `idx` of a batch tensor whose
-// vector-lane prefix is [0, nvec) (nvec = n - n % VB)
-__device__ __forceinline__ float torch_cpu_pow(long long count, double e, long long idx, long long nvec) {
+// The SIMD / scalar lane of the element at flat position idx of a tensor of n_total elements: torch's
+// TensorIterator::for_each splits tensors of >= 32768 elements over its intra-op threads (at::parallel_for
+// chunks of `chunk` elements; chunk = n_total when serial) and each chunk runs the vectorized loop over
+// its first len - len % vb elements, the rest (its tail) through the scalar op
+__device__ __forceinline__ bool torch_vec_lane(long long idx, long long chunk, long long n_total, int vb) {
+  const long long c0 = idx / chunk * chunk;
+  const long long len = (c0 + chunk < n_total ? c0 + chunk : n_total) - c0;
+  return idx - c0 < len - len % vb;
+}
+
+// one element of torch's CPU `int64 counts ** e` at flat position `idx` of the batch tensor
+__device__ __forceinline__ float torch_cpu_pow(long long count, double e, long long idx, long long chunk,
+                                               long long n_total, int vb) {
   const float b = (float)count;
   if (e == 0.0) return 1.0f;
   if (e == 1.0) return b;
   if (e == 0.5) return sqrtf(b);
   if (e == 2.0) return b * b;
   if (e == 3.0) return b * b * b;
-  if (idx < nvec) return sleef_powf_u10(b, (float)e);
+  if (torch_vec_lane(idx, chunk, n_total, vb)) return sleef_powf_u10(b, (float)e);
   return (float)pow((double)b, e);
+}
+
+// elements per intra-op thread chunk for a tensor of n_total elements evaluated with `threads` threads
+// (at::internal::GRAIN_SIZE = 32768: serial below it; else min(threads, ceil(n / grain)) chunks)
+inline long long torch_pow_chunk(long long n_total, int threads) {
+  constexpr long long GRAIN = 32768;
+  if (threads <= 1 || n_total < GRAIN) return n_total;
+  const long long num = std::min<long long>(threads, (n_total + GRAIN - 1) / GRAIN);
+  return (n_total + num - 1) / num;
 }
 
 }  // namespace mzpow

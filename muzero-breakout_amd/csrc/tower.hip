@@ -1158,7 +1158,7 @@ __global__ __launch_bounds__(t8::NT, 1) void rep_tail_kernel(RepTailArgs a) {
   }
 }
 
-static int g_tower_variant = 0;  // 0 auto, 1 four-env kernel, 2 eight-env kernel, 3 four-env 4-wave
+static thread_local int g_tower_variant = 0;  // (per thread: an acting thread beside the learner) 0 auto, 1 four-env kernel, 2 eight-env kernel, 3 four-env 4-wave
 
 static size_t t8_dyn_lds(int nblocks) { return (size_t)nblocks * 2 * TC * sizeof(float); }
 

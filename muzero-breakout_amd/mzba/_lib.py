@@ -59,8 +59,8 @@ SIGNATURES = {
     "mzba_mcts_select": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, I, P],
     "mzba_mcts_backup": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, I, P, P, P, F, P],
     "mzba_mcts_results": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P],
-    "mzba_sample_actions": [P, P, P, I, D, P, I, I, I, I, U64, P, P],
-    "mzba_torch_pow": [P, P, LL, D, LL, LL, I, P],
+    "mzba_sample_actions": [P, P, P, I, D, P, I, I, I, I, I, U64, P, P],
+    "mzba_torch_pow": [P, P, LL, D, LL, LL, I, I, P],
     "mzba_record_results": [P, P, P, P, I, I, P, P],
     "mzba_ctx_advance": [P, P],
     # learner (learn.hip)

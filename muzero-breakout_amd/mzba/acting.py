@@ -60,14 +60,17 @@ class ActingLoop:
 
     def __init__(self, cfg, agent, B, seed=0, env_offset=0, temperature=1.0, height=16, width=20,
                  record_frames=True, max_steps=MAX_STEPS, pad_action=0, rec_flags=0, n_envs_total=None,
-                 rep_agent=None):
+                 rep_agent=None, pow_threads=None):
         """`n_envs_total`: envs of the whole (sharded) batch, the reference's visit_counts tensor
         (default env_offset + B); `rep_agent`: the net of the root representation when it differs
-        from the search's (run_test_simulation: learner net for the root, target net in the search)."""
+        from the search's (run_test_simulation: learner net for the root, target net in the search);
+        `pow_threads`: intra-op threads of the reference's torch process, which split its visit-count
+        pow into per-thread chunks from 32768 elements on (default: this process's torch threads)."""
         self.cfg, self.agent, self.B = cfg, agent, B
         self.seed, self.env_offset = seed, env_offset
         self.n_envs_total = env_offset + B if n_envs_total is None else n_envs_total
         self.max_steps = max_steps
+        self.pow_threads = torch.get_num_threads() if pow_threads is None else pow_threads
         dev = agent.device
         # graph-replayable schedule values (train_torch.py:129-135): 1/T in double for the sampling
         # kernel, (f32(1 - noise_weight), f32(noise_weight)) for the root expansion
@@ -151,7 +154,8 @@ class ActingLoop:
         self.rep_runner.representation(self.rep_in, ws.cur, pool=ws.pool, pool_env_stride=(ws.S + 1) * n)
         values, counts = ws.run(self.search_id, self._noise_in, ctx=self.ctx, w_dev=self.root_w_dev)
         L.call("mzba_sample_actions", L.ptr(counts), L.ptr(self.action), None, self.B, 1.0 / self.temperature,
-               L.ptr(self.inv_t_dev), self.n_envs_total, self.VEC_BLOCK, self.env_offset, self.step_index, self.seed,
+               L.ptr(self.inv_t_dev), self.n_envs_total, self.VEC_BLOCK, self.pow_threads, self.env_offset,
+               self.step_index, self.seed,
                L.ptr(self.ctx), L.stream())
         L.call("mzba_record_results", L.ptr(counts), L.ptr(values), L.ptr(self.rec["counts"]),
                L.ptr(self.rec["values"]), self.B, 0, L.ptr(self.ctx), L.stream())
@@ -161,7 +165,10 @@ class ActingLoop:
     def capture(self):
         """Capture one acting step (~S x 65 launches) into a HIP graph; act() then replays it.
         Temperature and noise weight are read from device buffers, so the graph stays valid across
-        the reference's schedule."""
+        the reference's schedule. The captured step draws its root noise on the device."""
+        if self.inject_noise is not None:
+            raise RuntimeError("capture(): injected noise is host data per step; clear inject_noise first")
+        self._noise_in = None
         self._sync_noise_weight()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -178,6 +185,8 @@ class ActingLoop:
             nz = np.ascontiguousarray(self.inject_noise(self.search_id, self.B), dtype=np.float32)
             self._noise_in = torch.from_numpy(nz).to(self.agent.device)
             eager = True
+        else:  # back to the device Dirichlet draw (a later capture must not bake in the last injected rows)
+            self._noise_in = None
         if self.graph is not None and not eager and self.noise_log is None:
             self.graph.replay()
         else:

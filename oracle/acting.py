@@ -18,22 +18,22 @@ from . import nets as N
 f32 = np.float32
 
 
-def sample_probs(counts, temperature, vec_block=None, env_offset=0, n_envs_total=None):
+def sample_probs(counts, temperature, vec_block=None, env_offset=0, n_envs_total=None, threads=1):
     """train_torch.py:192-193 bit for bit: `visit_counts ** (1/self.temperature)` on the whole (B, 3)
     int64 batch tensor (torch's CPU pow, restated in oracle/torch_pow.c: the element's position in the
     tensor decides between SLEEF's vector powf and the scalar double pow), then the f32 row sum
     ((c0 + c1) + c2, torch's order for a size-3 dim) and the f32 division."""
     from .torch_pow import pow_counts, VEC_BLOCK
     vt = pow_counts(counts, 1.0 / temperature, VEC_BLOCK if vec_block is None else vec_block, env_offset,
-                    n_envs_total)
+                    n_envs_total, threads)
     s = (vt[:, 0] + vt[:, 1]) + vt[:, 2]
     return (vt / s[:, None]).astype(np.float32)
 
 
-def sample_actions(counts, temperature, u, vec_block=None, env_offset=0, n_envs_total=None):
+def sample_actions(counts, temperature, u, vec_block=None, env_offset=0, n_envs_total=None, threads=1):
     """train_torch.py:192-198 with inverse-CDF sampling on injected u (f32) in place of
     `Categorical(probs[i]).sample()`. A shard passes its env_offset and the global env count."""
-    probs = sample_probs(counts, temperature, vec_block, env_offset, n_envs_total)
+    probs = sample_probs(counts, temperature, vec_block, env_offset, n_envs_total, threads)
     B = counts.shape[0]
     out = np.zeros(B, dtype=np.int64)
     for b in range(B):

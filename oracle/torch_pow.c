@@ -95,19 +95,24 @@ float mz_sleef_powf_u10(float x, float y) {
 
 /* torch CPU `int64 (B,3) ** e` (see header) for n elements that sit at flat positions
  * [start, start + n) of the reference's whole batch tensor of n_total = 3B elements (a shard of the
- * envs: start = 3 * env_offset); vb = 32 (AVX512 host) or 16 (AVX2). */
+ * envs: start = 3 * env_offset); vb = 32 (AVX512 host) or 16 (AVX2). TensorIterator::for_each splits
+ * tensors of >= 32768 elements over the intra-op threads (at::parallel_for: chunks of `chunk`
+ * elements, oracle/torch_pow.py pow_chunk) and each chunk runs the vectorized loop with its own
+ * scalar tail: element i takes the vector lane iff its offset in its chunk is below len - len % vb. */
 void mz_torch_pow_counts(const int64_t* counts, float* out, long long n, double e, int vb, long long start,
-                         long long n_total) {
-  const long long nv = n_total - n_total % vb;
+                         long long n_total, long long chunk) {
+  if (chunk <= 0) chunk = n_total;
   for (long long i = 0; i < n; ++i) {
     const float b = (float)counts[i];
+    const long long g = start + i, c0 = g / chunk * chunk;
+    const long long len = (c0 + chunk < n_total ? c0 + chunk : n_total) - c0;
     float r;
     if (e == 0.0) r = 1.0f;
     else if (e == 1.0) r = b;
     else if (e == 0.5) r = sqrtf(b);
     else if (e == 2.0) r = b * b;
     else if (e == 3.0) r = b * b * b;
-    else if (start + i < nv) r = mz_sleef_powf_u10(b, (float)e);
+    else if (g - c0 < len - len % vb) r = mz_sleef_powf_u10(b, (float)e);
     else r = (float)pow((double)b, e);
     out[i] = r;
   }

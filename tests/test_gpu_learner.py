@@ -558,37 +558,40 @@ def _conv_lat_bn_case(B, H, W, Cin, Cout, ks):
 
 
 def test_learner_fused_bn_statistics_track_separate_passes():
-    """bf16 learner with the BN statistics in the conv epilogues vs the separate BN passes: the same
-    algorithm with different f32 summation chunks, so some bf16 activations round the other way
-    and the two bf16 runs differ at bf16-noise scale. Checked: losses within 2e-3 relative;
-    per-tensor gradient cosine fused vs separate >= 0.98 (median >= 0.99); and the fused run is as
-    close to the f32 parity path as the separate-pass run is (median cosine within 0.01, min
-    within 0.05) — a wiring error (wrong consumer BN, mask or chunk) would fall far below."""
+    """bf16 learner with the BN statistics in the conv epilogues vs the separate BN passes. The per-kernel
+    arithmetic is checked deterministically by test_conv_lat_bn_matches_separate_passes (partial
+    statistics, masks, applies); end to end the two are the same algorithm with different f32 summation
+    chunks, so some bf16 activations round the other way, and the k-step loss is chaotic: two such
+    bf16 realisations are NOT close to each other per tensor (calibrated over 6 seeds on two band-kernel
+    builds, tools/learner_bn_calib.py, profiles/r03/learner_calib/: min gradient cosine fused~sep 0.86 -
+    0.9998, median >= 0.94). What a wiring error (wrong consumer BN, mask or chunk) would break is how
+    close each realisation is to the f32 parity path, so per seed (4 seeds) the fused run must be as
+    close to f32 as the separate-pass run: median cosine within 0.02 (observed |diff| <= 0.019) and min
+    within 0.1 (observed >= -0.049); losses within 2e-3 relative (observed <= 1.5e-3)."""
     from mzba.config import learner_model_cfg
     from mzba.learner import Learner
     from mzba.weights import init_state_dict
     mcfg = learner_model_cfg()
     mcfg["latent_channels"] = [128, 128]
-    ring = _random_ring(64, mcfg["state_history_length"], 5, 21)
-    out = {}
-    # thresholds calibrated on the 3-row tiling's statistics chunks (the k-step loss is chaotic, so
-    # another chunking is another bf16-noise realisation); the 5-row tiling's partial statistics are
-    # checked against the separate passes directly (test_conv_lat_bn_matches_separate_passes[2-...])
-    for tag, dt, fuse in (("sep", "bf16", False), ("fused", "bf16", True), ("f32", "f32", False)):
-        ln = Learner(mcfg, init_state_dict(mcfg, 4), K=5, dtype=dt, fuse_bn=fuse, lat_rows="auto")
-        out[tag] = (ln.train_minibatch(ring, ring.slots()).cpu(), ln.gradients())
-        del ln
-    torch.testing.assert_close(out["fused"][0], out["sep"][0], rtol=2e-3, atol=1e-5)
+    for seed in range(4):
+        ring = _random_ring(64, mcfg["state_history_length"], 5, 21 + seed)
+        out = {}
+        for tag, dt, fuse in (("sep", "bf16", False), ("fused", "bf16", True), ("f32", "f32", False)):
+            ln = Learner(mcfg, init_state_dict(mcfg, 4 + seed), K=5, dtype=dt, fuse_bn=fuse, lat_rows="auto")
+            out[tag] = (ln.train_minibatch(ring, ring.slots()).cpu(), ln.gradients())
+            del ln
+        torch.testing.assert_close(out["fused"][0], out["sep"][0], rtol=2e-3, atol=1e-5)
 
-    def cosines(a, b):
-        c = {}
-        for k, g0 in out[b][1].items():
-            if _pre_bn_bias(k) or g0.abs().max() == 0:
-                continue
-            c[k] = torch.nn.functional.cosine_similarity(g0.flatten().double(), out[a][1][k].flatten().double(),
-                                                         dim=0).item()
-        return np.array(list(c.values()))
-    fs, ff, sf = cosines("fused", "sep"), cosines("fused", "f32"), cosines("sep", "f32")
-    print("fused~sep", np.median(fs), fs.min(), "fused~f32", np.median(ff), ff.min(), "sep~f32", np.median(sf), sf.min())
-    assert fs.min() >= 0.98 and np.median(fs) >= 0.99
-    assert np.median(ff) >= np.median(sf) - 0.01 and ff.min() >= sf.min() - 0.05
+        def cosines(a, b):
+            c = {}
+            for k, g0 in out[b][1].items():
+                if _pre_bn_bias(k) or g0.abs().max() == 0:
+                    continue
+                c[k] = torch.nn.functional.cosine_similarity(g0.flatten().double(), out[a][1][k].flatten().double(),
+                                                             dim=0).item()
+            return np.array(list(c.values()))
+        fs, ff, sf = cosines("fused", "sep"), cosines("fused", "f32"), cosines("sep", "f32")
+        print(f"seed {seed}: fused~sep {np.median(fs):.4f} / {fs.min():.4f}, fused~f32 {np.median(ff):.4f} / "
+              f"{ff.min():.4f}, sep~f32 {np.median(sf):.4f} / {sf.min():.4f}")
+        assert np.median(fs) >= 0.9, (seed, np.median(fs))
+        assert np.median(ff) >= np.median(sf) - 0.02 and ff.min() >= sf.min() - 0.1, (seed, ff, sf)

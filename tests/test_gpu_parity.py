@@ -568,14 +568,14 @@ def test_dirichlet_noise_statistics():
     del L
 
 
-def _sample_dev(counts, T, step, seed, inv_t_dev=None, n_total=None, off=0, vb=32):
+def _sample_dev(counts, T, step, seed, inv_t_dev=None, n_total=None, off=0, vb=32, threads=1):
     from mzba import _lib as L
     B = counts.shape[0]
     a = torch.empty(B, dtype=torch.int64, device="cuda")
     p = torch.empty(B, 3, dtype=torch.float32, device="cuda")
     cd = dev(counts)
     L.call("mzba_sample_actions", L.ptr(cd), L.ptr(a), L.ptr(p), B, 1.0 / T, L.ptr(inv_t_dev),
-           off + B if n_total is None else n_total, vb, off, step, seed, None, L.stream())
+           off + B if n_total is None else n_total, vb, threads, off, step, seed, None, L.stream())
     torch.cuda.synchronize()
     return a.cpu().numpy(), p.cpu().numpy()
 
@@ -631,11 +631,42 @@ def test_torch_pow_device_exhaustive():
             # rows at positions [0, 1024) of a 4096-element tensor: all vector lanes; at positions
             # [0, 1024) of a 1027-element tensor with vb = 2048: all scalar lanes
             vb = 32 if n_total == 4096 else 2048
-            L.call("mzba_torch_pow", L.ptr(bd), L.ptr(out), 1024, 1.0 / T, 0, n_total, vb, L.stream())
+            L.call("mzba_torch_pow", L.ptr(bd), L.ptr(out), 1024, 1.0 / T, 0, n_total, vb, 1, L.stream())
             got = out.cpu().numpy()
             assert got.view(np.uint32).astype(np.uint64).sum() == d[key][j], (T, key)
             ref = pow_counts(base[:, None], 1.0 / T, vb, 0, n_total // 3 if n_total == 4096 else 1)[:, 0]
             np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32), err_msg=f"T={T} {key}")
+
+
+def test_sample_kernel_threaded_pow_chunks():
+    """From 32768 elements on torch's CPU pow runs in per-thread chunks, each with its own scalar tail
+    (TensorIterator::for_each -> at::parallel_for), so the lane of an element depends on the reference
+    process's thread count: 12000 envs (36000 elements; a 2-thread chunk of 18000 is not a multiple of
+    32) at 1 / 2 / 3 / 8 threads — the device pow equals torch's own `counts ** (1/T)` computed here with
+    that many threads, and the sampled probabilities / actions equal the oracle's, shards included."""
+    from mzba import _lib as L
+    from oracle.acting import sample_actions, sample_probs
+    from oracle import rng as R
+    n_env, T, seed, step = 12000, 0.996 ** 37, 3, 5
+    counts = np.random.default_rng(1).integers(0, 51, (n_env, 3))
+    cd = dev(counts)
+    out = torch.empty(3 * n_env, dtype=torch.float32, device="cuda")
+    nthreads = torch.get_num_threads()
+    try:
+        for thr in (1, 2, 3, 8):
+            torch.set_num_threads(thr)
+            ref = (torch.from_numpy(counts) ** (1.0 / T)).numpy().reshape(-1)
+            L.call("mzba_torch_pow", L.ptr(cd), L.ptr(out), 3 * n_env, 1.0 / T, 0, 3 * n_env, 32, thr, L.stream())
+            np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32), err_msg=f"{thr} threads")
+            a, p = _sample_dev(counts, T, step, seed, threads=thr)
+            u = R.uniform(np.arange(n_env), R.STREAM_SAMPLE, step, 0, seed)
+            np.testing.assert_array_equal(p.view(np.uint32), sample_probs(counts, T, threads=thr).view(np.uint32))
+            np.testing.assert_array_equal(a, sample_actions(counts, T, u, threads=thr))
+            for off, n in ((0, 7001), (7001, 4999)):  # shards take the lanes of their global positions
+                a2, p2 = _sample_dev(counts[off:off + n], T, step, seed, n_total=n_env, off=off, threads=thr)
+                np.testing.assert_array_equal(p2.view(np.uint32), p[off:off + n].view(np.uint32))
+    finally:
+        torch.set_num_threads(nthreads)
 
 
 def _replay_reference_episode(name, graph):

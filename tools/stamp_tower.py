@@ -32,18 +32,31 @@ def main():
     D.mzba_tower_set_variant.argtypes = [I]
     assert D.mzba_tower_set_variant(2) == 0
     C = 256
+    # STAMP_ELEM=1: the fp16 tower (config 5's dynamics net: fp16 LDS images, weights, MFMA) through
+    # mzba_tower_fused with no prologue / epilogue; STAMP_ELEM=0 the bf16 tower through the same call
+    elem = os.environ.get("STAMP_ELEM")
+    wdt = torch.float16 if elem == "1" else torch.bfloat16
     g = torch.Generator().manual_seed(0)
     x = torch.rand(B * 20 * C, generator=g).to(torch.bfloat16).cuda()
-    wf = (torch.randn(2 * nb * C * 2304 + 8 * 64 * 8, generator=g) * 0.02).to(torch.bfloat16).cuda()
+    wf = (torch.randn(2 * nb * C * 2304 + 8 * 64 * 8, generator=g) * 0.02).to(wdt).cuda()
     b = (torch.randn(2 * nb * C, generator=g) * 0.1).cuda()
     y = torch.empty_like(x)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    if elem is not None:
+        from mzba._lib import TowerExt
+        D.mzba_tower_fused.argtypes = [P, LL, P, LL, P, P, P, I, I, P, P]
+        ext = TowerExt()
+        ext.epilogue, ext.elem, ext.plan = 0, int(elem), 2
     for it in range(30):
         if it == 29:
             ev[0].record()
-        assert D.mzba_tower(x.data_ptr(), 20 * C, None, 0, y.data_ptr(), wf.data_ptr(), b.data_ptr(), nb, B, None, 0,
-                            st) == 0
+        if elem is not None:
+            assert D.mzba_tower_fused(x.data_ptr(), 20 * C, None, 0, y.data_ptr(), wf.data_ptr(), b.data_ptr(), nb, B,
+                                      ctypes.byref(ext), st) == 0
+        else:
+            assert D.mzba_tower(x.data_ptr(), 20 * C, None, 0, y.data_ptr(), wf.data_ptr(), b.data_ptr(), nb, B, None, 0,
+                                st) == 0
     ev[1].record()
     torch.cuda.synchronize()
     nwg = (B + 7) // 8
@@ -66,7 +79,7 @@ def main():
     med = np.median(ph[:, 1:-1, :], axis=(0, 1))  # interior convs
     conv = float(med.sum())
     floor = 2496 * 16
-    out = {"B": B, "nblocks": nb, "launch_us": ev[0].elapsed_time(ev[1]) * 1e3, "clock_ghz": float(clock),
+    out = {"B": B, "nblocks": nb, "elem": {"1": "fp16", "0": "bf16"}.get(elem, "bf16 (mzba_tower)"), "launch_us": ev[0].elapsed_time(ev[1]) * 1e3, "clock_ghz": float(clock),
            "cycles_per_conv": conv, "mfma_floor_cycles": floor, "mfma_frac_in_conv": floor / conv,
            "phase_cycles": {"bias init (+ dx0 pass if two-pass)": float(med[0]), "-": float(med[1]),
                             "k loop (one pass; dx-1/+1 pass if two-pass)": float(med[2]),
