@@ -145,6 +145,15 @@ int mzba_conv_band_set_xt(int xt);
 int mzba_conv_band(const void* in, const void* wf16, const float* bias, const void* res, void* out, int B, int H,
                    int W, int Cin, int Cout, int relu, hipStream_t stream);
 
+/* ResidualBlock(C) of the representation net at 16x20 in ONE launch (networks.py:19-35, 46-92):
+ * out = relu(conv2(relu(conv1(in) + b1)) + b2 + in), BN folded, both weights in the tower packing
+ * (agent.pack_tower_conv, + 8 KB pad). A workgroup owns one env's 10-column band and keeps it in LDS
+ * across both convs (conv1 over the band + 1 halo column each side); the outputs equal two
+ * mzba_conv_band launches bit for bit. NHWC bf16; C in {128, 256}; out must not alias in. */
+int mzba_conv_band_res_supported(int H, int W, int C);
+int mzba_conv_band_res(const void* in, const void* w1, const float* b1, const void* w2, const float* b2, void* out,
+                       int B, int H, int W, int C, hipStream_t stream);
+
 /* Replay ingest on the device (replay_buffer.py:96-165, train_torch.py:223-225). Records of one episode
  * batch as the acting loop's sink holds them: action u8 [T][B], reward f32 [T][B], mask u8 [T][B]
  * (recorded = not prev_done, a prefix), counts i64 [T][B][3], value f32 [T][B], frame u8 [T][B][HW]

@@ -177,18 +177,21 @@ MZ_DEV int band_step(int e) { return (e % 3) * 3 * NC + e / 3; }
 // XT + 2 source columns are read from LDS once; output column t takes dx = -1 from source t, dx = 0
 // from t + 1, dx = +1 from t + 2. Column-tile major: a column tile's 3 x XT MFMAs, then its three
 // ring slots reloaded RDB / 3 steps ahead (free registers once the MFMAs have issued: no copies)
-template <int CIN, int COUT, int XT>
+// (the residual-block kernel runs it on a wider staged band: source columns from byte offset CB of the
+// LDS image, the zero block after LZC staged columns)
+template <int CIN, int COUT, int XT, int LZC = XT + 2, int CB = 0, int ACC = XT, int RDB = BandGeo<CIN, COUT, XT>::RDB>
 __device__ __forceinline__ void band_all(const uint8_t* __restrict__ lds, __amdgpu_buffer_rsrc_t wrs,
-                                         uint4 (&bq)[COUT / 64][BandGeo<CIN, COUT, XT>::RDB], f32x4 (&acc)[XT][COUT / 64],
-                                         int lane) {
+                                         uint4 (&bq)[COUT / 64][RDB], f32x4 (&acc)[ACC][COUT / 64], int lane) {
+  static_assert(ACC >= XT, "accumulator rows");
   using G = BandGeo<CIN, COUT, XT>;
-  constexpr int CTW = G::CTW, NC = G::NC, NS = XT + 2, RDB = G::RDB;
+  constexpr int CTW = G::CTW, NC = G::NC, NS = XT + 2;
+  constexpr int LZ = LZC * 16 * G::RB;
   static_assert((3 * NC) % RDB == 0 && 3 * XT >= NS, "ring slot restarts at every dy; schedule groups");
   const int q = lane >> 4, ys = nib(SIG, lane & 15);
   auto rows = [&](int dy, int& base, int& tst, int& sw) {
     const int yy = ys + dy;
     const bool ok = (unsigned)yy < (unsigned)BH;
-    base = ok ? yy * G::RB : G::LZ + (yy & 15) * G::RB;
+    base = ok ? CB + yy * G::RB : LZ + (yy & 15) * G::RB;
     tst = ok ? 16 * G::RB : 0;
     sw = nib(KEY, yy & 15) << 4;
   };
@@ -348,6 +351,19 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
     float4 bias4[CTW];  // every bias load in flight before the first use
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) bias4[ct] = *reinterpret_cast<const float4*>(a.bias + (wave * CTW + ct) * 16 + 4 * q);
+    // every residual element of this lane read from LDS before any result is written back: a read
+    // after the previous element's write (same array) was one serialised LDS round trip per element
+    // (stamps: 13.4 k cycles of epilogue at 256 -> 256)
+    uint2 rr[CTW][XT];
+    if (a.res) {
+#pragma unroll
+      for (int ct = 0; ct < CTW; ++ct) {
+        const int n = (wave * CTW + ct) * 16 + 4 * q;
+#pragma unroll
+        for (int t = 0; t < XT; ++t)
+          rr[ct][t] = *reinterpret_cast<const uint2*>(lds + (t * 16 + ys) * G::OB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1));
+      }
+    }
 #pragma unroll
     for (int ct = 0; ct < CTW; ++ct) {
       const int n = (wave * CTW + ct) * 16 + 4 * q;  // D[channel n + i][column j = lane & 15]
@@ -357,7 +373,7 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
         uint2* p = reinterpret_cast<uint2*>(lds + (t * 16 + ys) * G::OB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1));
         float v0 = acc[t][ct][0] + b4.x, v1 = acc[t][ct][1] + b4.y, v2 = acc[t][ct][2] + b4.z, v3 = acc[t][ct][3] + b4.w;
         if (a.res) {
-          const uint2 r = *p;
+          const uint2 r = rr[ct][t];
           v0 += __uint_as_float(r.x << 16); v1 += __uint_as_float(r.x & 0xffff0000u);
           v2 += __uint_as_float(r.y << 16); v3 += __uint_as_float(r.y & 0xffff0000u);
         }
@@ -380,6 +396,179 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
   BSTAMP_REAL(7);
 }
 
+// ResidualBlock(C) at 16x20 (networks.py:19-35; RepresentationNetwork's blocks, :46-92) in ONE launch:
+// out = relu(conv2(relu(conv1(x) + b1)) + b2 + x), BN folded. A workgroup owns one env and the 10 output
+// columns x0..x0+9 (x0 = 0 or 10): it stages the 14 source columns x0-2..x0+11 once; conv1 computes the
+// 12 columns x0-1..x0+10 (the band and the halo conv2 needs; a column outside the image is written as
+// zeros, conv2's padding) and writes them back in place as bf16 — what the two-launch sequence stores —
+// then conv2 computes the band from them, + bias + the residual (re-read from global), ReLU. The same
+// k loop as band_conv_kernel, so the outputs equal two band launches bit for bit; every weight fragment
+// feeds 12 (conv1) / 10 (conv2) MFMAs instead of 5, at 10 % recomputed halo columns.
+#ifndef BAND_RES_RDB
+#define BAND_RES_RDB 3
+#endif
+struct BandResArgs {
+  const bf16_t* in;   // [B][320][C]
+  const bf16_t* w1;   // tower packing (+ pad)
+  const float* b1;
+  const bf16_t* w2;
+  const float* b2;
+  bf16_t* out;        // [B][320][C]; must not alias in (neighbouring bands read its halo columns)
+  int B;
+};
+
+template <int C>
+__global__ __launch_bounds__(BNT, 1) void band_res_kernel(BandResArgs a) {
+  using G1 = BandGeo<C, C, 12>;  // conv1: 12 output tiles over the 14 staged columns
+  using G2 = BandGeo<C, C, 10>;  // conv2: 10 output tiles over staged columns 1..12
+  // weight ring: 3 entries (one k step) per column tile; the 12 accumulator tiles take 192 of the 256
+  // AGPRs at C = 256, the A fragments of two k steps 112 VGPRs
+  constexpr int NSRC = 14, CTW = G1::CTW, RB = G1::RB, NC = G1::NC, TNS = G1::TNS, RDB = BAND_RES_RDB;
+  static_assert(G2::RB == RB && RB == 2 * C, "one row layout for both convs");
+  constexpr int LZ = NSRC * 16 * RB;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LZ + 16 * RB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x >> 1, x0 = (blockIdx.x & 1) * 10;
+  BSTAMP_REAL(6);
+  BSTAMP(0);
+  const bf16_t* src = a.in + (size_t)b * BH * BW * C;
+  {  // stage source columns x0-2 .. x0+11 (zero outside the image), every load in flight at once
+    constexpr int NCH = C / 8, N = NSRC * 16 * NCH, UB = N / BNT;
+    static_assert(N % BNT == 0, "whole batches");
+    uint4 v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int i = u * BNT + tid;
+      const int row = i / NCH, ch = i % NCH;
+      const int x = x0 - 2 + (row >> 4), y = row & 15;
+      const bool ok = (unsigned)x < (unsigned)BW;
+      v[u] = *reinterpret_cast<const uint4*>(src + ((size_t)(y * BW + (ok ? x : 0)) * C + ch * 8));
+      if (!ok) v[u] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int i = u * BNT + tid;
+      const int row = i / NCH, ch = i % NCH;
+      *reinterpret_cast<uint4*>(lds + row * RB + ((ch ^ nib(KEY, row & 15)) << 4)) = v[u];
+    }
+    for (int i = tid; i < RB; i += BNT) *reinterpret_cast<uint4*>(lds + LZ + i * 16) = make_uint4(0, 0, 0, 0);
+  }
+  const int wt = __builtin_amdgcn_readfirstlane(wave * CTW);
+  const __amdgpu_buffer_rsrc_t wrs1 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint4*>(reinterpret_cast<const uint4*>(a.w1) + (size_t)wt * TNS * 64), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs2 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint4*>(reinterpret_cast<const uint4*>(a.w2) + (size_t)wt * TNS * 64), 0, 0x7fffffff, 0x00020000);
+  uint4 bq[CTW][RDB];
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct)
+#pragma unroll
+    for (int i = 0; i < RDB; ++i) bq[ct][i] = wld<TNS>(wrs1, ct, band_step<NC>(i), lane);
+  f32x4 acc[12][CTW];
+#pragma unroll
+  for (int t = 0; t < 12; ++t)
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  BSTAMP(1);
+#pragma unroll
+  for (int t = 0; t < 12; ++t)  // accumulators in the AGPR half (tower.hip: no per-step copies)
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) asm volatile("" : "+a"(acc[t][ct]));
+  band_all<C, C, 12, NSRC, 0, 12, RDB>(lds, wrs1, bq, acc, lane);
+  const int q = lane >> 4, ys = nib(SIG, lane & 15), ky = nib(KEY, ys);
+  float4 bias1[CTW];
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) bias1[ct] = *reinterpret_cast<const float4*>(a.b1 + (wt + ct) * 16 + 4 * q);
+  __syncthreads();  // every wave is done reading x
+  // conv1's output in place: relu(acc + b1) as bf16 at source column t + 1 (image column x0 - 1 + t)
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) {
+    const int n = (wt + ct) * 16 + 4 * q;
+    const float4 b4 = bias1[ct];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) {
+      const bool img = (unsigned)(x0 - 1 + t) < (unsigned)BW;
+      const float v0 = fmaxf(acc[t][ct][0] + b4.x, 0.f), v1 = fmaxf(acc[t][ct][1] + b4.y, 0.f);
+      const float v2 = fmaxf(acc[t][ct][2] + b4.z, 0.f), v3 = fmaxf(acc[t][ct][3] + b4.w, 0.f);
+      uint2 o;
+      o.x = img ? ((uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16)) : 0u;
+      o.y = img ? ((uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16)) : 0u;
+      *reinterpret_cast<uint2*>(lds + (16 * (t + 1) + ys) * RB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1)) = o;
+      acc[t][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  // conv2's ring fills while the barrier waits
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct)
+#pragma unroll
+    for (int i = 0; i < RDB; ++i) bq[ct][i] = wld<TNS>(wrs2, ct, band_step<NC>(i), lane);
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < 12; ++t)
+#pragma unroll
+    for (int ct = 0; ct < CTW; ++ct) asm volatile("" : "+a"(acc[t][ct]));
+  band_all<C, C, 10, NSRC, 16 * RB, 12, RDB>(lds, wrs2, bq, acc, lane);
+  BSTAMP(2);
+  // epilogue (band_conv_kernel's): the residual tile x (band columns) from global, coalesced, into LDS
+  // rows 16 t + y; + b2 + residual, ReLU, bf16; 16-B stores
+  constexpr int ONCH = C / 8, NR = 10 * 16 * ONCH, UR = (NR + BNT - 1) / BNT;
+  uint4 rv[UR];
+#pragma unroll
+  for (int u = 0; u < UR; ++u) {
+    const int i = min(u * BNT + tid, NR - 1);
+    const int row = i / ONCH, ch = i % ONCH, t = row >> 4, y = row & 15;
+    rv[u] = *reinterpret_cast<const uint4*>(src + (size_t)(y * BW + x0 + t) * C + ch * 8);
+  }
+  float4 bias2[CTW];
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) bias2[ct] = *reinterpret_cast<const float4*>(a.b2 + (wt + ct) * 16 + 4 * q);
+  __syncthreads();  // conv1's output is no longer read
+#pragma unroll
+  for (int u = 0; u < UR; ++u) {
+    const int i = u * BNT + tid;
+    const int row = i / ONCH, ch = i % ONCH, y = row & 15;
+    if (NR % BNT == 0 || i < NR) *reinterpret_cast<uint4*>(lds + row * RB + ((ch ^ nib(KEY, y)) << 4)) = rv[u];
+  }
+  __syncthreads();
+  BSTAMP(3);
+  uint2 rr[CTW][10];  // every residual read before the first write (one LDS round trip)
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) {
+    const int n = (wt + ct) * 16 + 4 * q;
+#pragma unroll
+    for (int t = 0; t < 10; ++t)
+      rr[ct][t] = *reinterpret_cast<const uint2*>(lds + (t * 16 + ys) * RB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1));
+  }
+#pragma unroll
+  for (int ct = 0; ct < CTW; ++ct) {
+    const int n = (wt + ct) * 16 + 4 * q;
+    const float4 b4 = bias2[ct];
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      uint2* p = reinterpret_cast<uint2*>(lds + (t * 16 + ys) * RB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1));
+      const uint2 r = rr[ct][t];
+      float v0 = acc[t][ct][0] + b4.x, v1 = acc[t][ct][1] + b4.y, v2 = acc[t][ct][2] + b4.z, v3 = acc[t][ct][3] + b4.w;
+      v0 += __uint_as_float(r.x << 16); v1 += __uint_as_float(r.x & 0xffff0000u);
+      v2 += __uint_as_float(r.y << 16); v3 += __uint_as_float(r.y & 0xffff0000u);
+      v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      uint2 o;
+      o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+      o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
+      *p = o;
+    }
+  }
+  __syncthreads();
+  BSTAMP(4);
+  bf16_t* gout = a.out + (size_t)b * BH * BW * C;
+  for (int i = tid; i < NR; i += BNT) {
+    const int row = i / ONCH, ch = i % ONCH, t = row >> 4, y = row & 15;
+    *reinterpret_cast<uint4*>(gout + (size_t)(y * BW + x0 + t) * C + ch * 8) =
+        *reinterpret_cast<const uint4*>(lds + row * RB + ((ch ^ nib(KEY, y)) << 4));
+  }
+  BSTAMP(5);
+  BSTAMP_REAL(7);
+}
+
 }  // namespace
 
 static thread_local int g_band_xt = 5;  // output columns per workgroup (mzba_conv_band_set_xt; per thread)
@@ -392,6 +581,19 @@ extern "C" {
 int mzba_conv_band_set_xt(int xt) {
   if (xt != 5 && xt != 10) return -1;
   g_band_xt = xt;
+  return 0;
+}
+
+// ResidualBlock(C) at 16x20 in one launch (band_res_kernel), C in {128, 256}
+int mzba_conv_band_res_supported(int H, int W, int C) { return H == BH && W == BW && (C == 256 || C == 128); }
+
+int mzba_conv_band_res(const void* in, const void* w1, const float* b1, const void* w2, const float* b2, void* out,
+                       int B, int H, int W, int C, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && in && w1 && b1 && w2 && b2 && out && in != out && mzba_conv_band_res_supported(H, W, C), -1);
+  BandResArgs a{(const bf16_t*)in, (const bf16_t*)w1, b1, (const bf16_t*)w2, b2, (bf16_t*)out, B};
+  if (C == 256) hipLaunchKernelGGL(band_res_kernel<256>, dim3(2 * B), dim3(BNT), 0, stream, a);
+  else hipLaunchKernelGGL(band_res_kernel<128>, dim3(2 * B), dim3(BNT), 0, stream, a);
+  MZ_LAUNCH_CHECK();
   return 0;
 }
 

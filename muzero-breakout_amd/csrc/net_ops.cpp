@@ -130,7 +130,7 @@ struct NetPack : torch::CustomClassHolder {
 struct NetRunner : torch::CustomClassHolder {
   NetPack* p;  // the pack that owns this runner (NetPack::runners); the Python wrapper keeps both alive
   int64_t B, H, W, lhw, HW, plan = 0;
-  bool use_lat = true, use_tower = true, use_fused = true, use_band = true, use_rep_tail = true;
+  bool use_lat = true, use_tower = true, use_fused = true, use_band = true, use_rep_tail = true, use_band_res = true;
   at::Tensor r_a, r_t, r_b, x, tt, rc, pc, vc;  // scratch, allocated on first use
   // live probe: HIP events around every tower launch / latent residual conv (eager launches only)
   bool probe_on = false;
@@ -270,7 +270,18 @@ struct NetRunner : torch::CustomClassHolder {
         cur = bufs[which];
         which ^= 1;
       } else if (kind == "res") {
-        resblock(a.substr(0, a.size() - 2), cur, r_t.data_ptr(), const_cast<void*>(cur), h, w, s);
+        const Conv &c1 = p->conv(a), &c2 = p->conv(b);
+        if (use_band_res && use_band && c1.wt.defined() && c2.wt.defined() && c1.cin == c1.cout &&
+            c2.cin == c2.cout && c1.cout == c2.cout && mzba_conv_band_res_supported((int)h, (int)w, (int)c1.cout)) {
+          // both convs of the block in one launch, the band LDS-resident across them (out != in)
+          check_rc(mzba_conv_band_res(cur, vp(c1.wt), vp<float>(c1.b), vp(c2.wt), vp<float>(c2.b), bufs[which], (int)B,
+                                      (int)h, (int)w, (int)c1.cout, s),
+                   "mzba_conv_band_res");
+          cur = bufs[which];
+          which ^= 1;
+        } else {
+          resblock(a.substr(0, a.size() - 2), cur, r_t.data_ptr(), const_cast<void*>(cur), h, w, s);
+        }
       } else {
         check_rc(mzba_avgpool2((int)p->dtype, cur, bufs[which], (int)B, (int)h, (int)w, (int)p->c1, s), "mzba_avgpool2");
         h /= 2, w /= 2;
@@ -547,6 +558,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              else if (k == "use_fused") r->use_fused = v;
              else if (k == "use_band") r->use_band = v;
              else if (k == "use_rep_tail") r->use_rep_tail = v;
+             else if (k == "use_band_res") r->use_band_res = v;
              else TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
            })
       .def("get_flag",
@@ -556,6 +568,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              if (k == "use_fused") return r->use_fused;
              if (k == "use_band") return r->use_band;
              if (k == "use_rep_tail") return r->use_rep_tail;
+             if (k == "use_band_res") return r->use_band_res;
              TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
              return false;
            })

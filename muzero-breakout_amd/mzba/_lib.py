@@ -48,6 +48,8 @@ SIGNATURES = {
     "mzba_replay_write": [P, P, P, P, P, P, P, I, I, I, P, P, P, I, P, P, P, P, P, P, P, P, I, I, I, I, P, P],
     "mzba_replay_states": [P, P, I, P, P, I, I, P],
     "mzba_conv_band": [P, P, P, P, P, I, I, I, I, I, I, P],
+    "mzba_conv_band_res_supported": [I, I, I],
+    "mzba_conv_band_res": [P, P, P, P, P, P, I, I, I, I, P],
     "mzba_tower_set_variant": [I],
     "mzba_avgpool2": [I, P, P, I, I, I, I, P],
     "mzba_scale_state": [I, P, P, P, LL, P, I, LL, I, I, P],

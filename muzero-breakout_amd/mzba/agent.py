@@ -348,7 +348,7 @@ class NetRunner:
     `mz.NetRunner` (csrc/net_ops.cpp), whose torch custom ops run every launch on torch's current
     stream — representation_ / dynamics_ / prediction_ / prediction_tree_ (`torch.ops.mz`)."""
 
-    FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail")
+    FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail", "use_band_res")
 
     def __init__(self, packed, B, H, W):
         self.p = packed
@@ -359,7 +359,8 @@ class NetRunner:
         self.tower_plan = self.native.plan() or None  # the kernel this runner launches (fixed at creation)
         self._probe = None
 
-    # kernel switches (tests / A-B runs): use_lat, use_tower, use_fused, use_band, use_rep_tail
+    # kernel switches (tests / A-B runs): use_lat, use_tower, use_fused, use_band, use_rep_tail,
+    # use_band_res (the representation's 16x20 residual blocks as one launch each)
     def __getattr__(self, k):
         if k in NetRunner.FLAGS:
             return self.native.get_flag(k)

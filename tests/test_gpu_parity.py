@@ -478,6 +478,52 @@ def test_band_conv_vs_torch_fp32(Cin, Cout, resid, relu, xt):
     assert err < 1e-2, err
 
 
+@pytest.mark.parametrize("C,B", [(256, 5), (128, 3), (256, 130)])
+def test_band_res_block_equals_two_band_convs(C, B):
+    """mzba_conv_band_res (a representation ResidualBlock at 16x20 in one launch: the 10-column band
+    LDS-resident across both convs, conv1 recomputing one halo column each side) against the two
+    mzba_conv_band launches it replaces, bit for bit (same k loop, same bf16 store of conv1's output),
+    and against a plain torch fp32 block of the bf16-rounded operands; and the representation net
+    with the fused blocks against the per-conv launches, bit for bit."""
+    from mzba import _lib as L
+    from mzba.agent import MuZeroAgent, pack_tower_conv, LAT_PAD_ELEMS
+    g = torch.Generator().manual_seed(C + B)
+    bf = lambda t: t.to(torch.bfloat16).float()  # noqa: E731
+    x = bf(torch.rand(B, C, 16, 20, generator=g))
+    w1, w2 = (bf(torch.randn(C, C, 3, 3, generator=g) / (C * 9) ** 0.5) for _ in range(2))
+    b1, b2 = torch.randn(C, generator=g) * 0.1, torch.randn(C, generator=g) * 0.1
+    pk = lambda w: torch.from_numpy(np.concatenate([pack_tower_conv(w.numpy()), np.zeros(LAT_PAD_ELEMS, np.float32)])).to(torch.bfloat16).cuda()  # noqa: E731
+    d = dict(x=x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda(), w1=pk(w1), w2=pk(w2), b1=b1.cuda(),
+             b2=b2.cuda())
+    t = torch.empty(B, 16, 20, C, dtype=torch.bfloat16, device="cuda")
+    two = torch.empty_like(t)
+    one = torch.full_like(t, float("nan"))
+    assert L.lib().mzba_conv_band_res_supported(16, 20, C)
+    L.call("mzba_conv_band", L.ptr(d["x"]), L.ptr(d["w1"]), L.ptr(d["b1"]), None, L.ptr(t), B, 16, 20, C, C, 1, L.stream())
+    L.call("mzba_conv_band", L.ptr(t), L.ptr(d["w2"]), L.ptr(d["b2"]), L.ptr(d["x"]), L.ptr(two), B, 16, 20, C, C, 1,
+           L.stream())
+    L.call("mzba_conv_band_res", L.ptr(d["x"]), L.ptr(d["w1"]), L.ptr(d["b1"]), L.ptr(d["w2"]), L.ptr(d["b2"]),
+           L.ptr(one), B, 16, 20, C, L.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(one, two)
+    ref = torch.relu(torch.nn.functional.conv2d(bf(torch.relu(torch.nn.functional.conv2d(x, w1, b1, padding=1))), w2, b2,
+                                                padding=1) + x)
+    err = (one.float().cpu().permute(0, 3, 1, 2) - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+    assert err < 2e-2, err
+    if C == 256 and B == 5:  # the whole representation net: fused blocks == per-conv launches
+        mcfg = default_config()["model"]
+        ag = MuZeroAgent(mcfg, dtype="bf16")
+        ag.load_state_dict(init_state_dict(mcfg, 12))
+        rn = ag.runner(B, 16, 20)
+        xs = torch.rand(B, 64, 16, 20, generator=g).cuda()
+        lat = {}
+        for fused in (True, False):
+            rn.use_band_res = fused
+            lat[fused] = ag.create_hidden_state_root(xs).cpu()
+        rn.use_band_res = True
+        assert torch.equal(lat[True], lat[False])
+
+
 def test_conv_kernel_vs_torch_fp32_random():
     """Raw conv op vs a plain torch fp32 conv, ragged M (B*HW not a tile multiple), 1x1 and 3x3."""
     from mzba import _lib as L

@@ -1,7 +1,7 @@
 """Phase breakdown of band_conv_kernel (representation convs at 16x20) from in-kernel s_memtime stamps
 (diagnostic build only: make -C muzero-breakout_amd/csrc band-stamps -> libmzba_bstamp.so).
 
-  python tools/stamp_band.py [B] [XT] [JSON_OUT]
+  python tools/stamp_band.py [B] [XT] [JSON_OUT]     (XT = 0: the residual-block kernel, mzba_conv_band_res)
 
 Per (Cin, Cout) of the representation: runs the conv 20 times (random bf16 weights / inputs, residual
 when Cin == Cout), reads the stamps of the last launch and prints median cycles per phase (band staging,
@@ -27,9 +27,12 @@ def main():
     D.mzba_conv_band.argtypes = [P, P, P, P, P, I, I, I, I, I, I, P]
     D.mzba_band_stamps_read.argtypes = [P, I]
     D.mzba_conv_band_set_xt.argtypes = [I]
-    assert D.mzba_conv_band_set_xt(xt) == 0
+    D.mzba_conv_band_res.argtypes = [P, P, P, P, P, P, I, I, I, I, P]
+    blocks = xt == 0  # XT = 0: the residual-block kernel (mzba_conv_band_res: both convs, 10-column bands)
+    if not blocks:
+        assert D.mzba_conv_band_set_xt(xt) == 0
     res = []
-    for cin, cout in ((64, 128), (128, 128), (128, 256), (256, 256)):
+    for cin, cout in (((128, 128), (256, 256)) if blocks else ((64, 128), (128, 128), (128, 256), (256, 256))):
         g = torch.Generator().manual_seed(cin + cout)
         x = torch.rand(B * 320 * cin, generator=g).to(torch.bfloat16).cuda()
         wf = (torch.randn(cout * 9 * cin + 8 * 64 * 8, generator=g) * 0.02).to(torch.bfloat16).cuda()
@@ -41,11 +44,15 @@ def main():
         for it in range(20):
             if it == 19:
                 ev[0].record()
-            assert D.mzba_conv_band(x.data_ptr(), wf.data_ptr(), b.data_ptr(), r.data_ptr() if r is not None else None,
-                                    y.data_ptr(), B, 16, 20, cin, cout, 1, st) == 0
+            if blocks:
+                assert D.mzba_conv_band_res(x.data_ptr(), wf.data_ptr(), b.data_ptr(), wf.data_ptr(), b.data_ptr(),
+                                            y.data_ptr(), B, 16, 20, cin, st) == 0
+            else:
+                assert D.mzba_conv_band(x.data_ptr(), wf.data_ptr(), b.data_ptr(), r.data_ptr() if r is not None else None,
+                                        y.data_ptr(), B, 16, 20, cin, cout, 1, st) == 0
         ev[1].record()
         torch.cuda.synchronize()
-        nwg = (20 // xt) * B
+        nwg = (2 if blocks else 20 // xt) * B
         rows = min(nwg, BST_WG) * 4
         buf = (ctypes.c_ulonglong * (BST_N * rows))()
         assert D.mzba_band_stamps_read(buf, rows) == 0
@@ -53,11 +60,12 @@ def main():
         clock = np.median((a[:, 5] - a[:, 0]) / (a[:, 7] - a[:, 6]) * 0.1)
         ph = {"staging": a[:, 1] - a[:, 0], "k_loop": a[:, 2] - a[:, 1], "residual_staging": a[:, 3] - a[:, 2],
               "epilogue_lds": a[:, 4] - a[:, 3], "stores": a[:, 5] - a[:, 4], "total": a[:, 5] - a[:, 0]}
-        mfma = (xt * (cout // 64) * 9 * (cin // 32)) if True else 0
-        # zero-pad column taps are computed (the band kernel does not skip them)
+        # zero-pad column taps are computed (the band kernels do not skip them); a block runs conv1 over
+        # 12 and conv2 over 10 column tiles
+        mfma = ((12 + 10) if blocks else xt) * (cout // 64) * 9 * (cin // 32)
         floor = mfma * 16
         ms = ev[0].elapsed_time(ev[1])
-        fl = 2.0 * B * 320 * cout * 9 * cin
+        fl = (2 if blocks else 1) * 2.0 * B * 320 * cout * 9 * cin
         out = {"B": B, "xt": xt, "cin": cin, "cout": cout, "launch_us": ms * 1e3, "tflops": fl / (ms * 1e-3) / 1e12,
                "frac_of_2500": fl / (ms * 1e-3) / 1e12 / 2500, "clock_ghz": float(clock),
                "median_cycles": {k: float(np.median(v)) for k, v in ph.items()},
