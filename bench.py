@@ -41,8 +41,8 @@ def parse():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--dyn-dtype", default=None, choices=[None, "fp16"], help="fp16 dynamics net (config 5)")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--cpu-envs", type=int, default=256,
-                    help="bounded CPU sample (cpu_baseline + match rate): ~10 s of the CPU port on 16 host cores")
+    ap.add_argument("--cpu-envs", type=int, default=768,
+                    help="bounded CPU sample (cpu_baseline + match rate): ~20 s of the CPU port on 16 host cores")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of HIP-graph replay")
     ap.add_argument("--no-parity", action="store_true",

@@ -407,6 +407,7 @@ __global__ __launch_bounds__(BNT, XT == 10 ? 1 : 2) void band_conv_kernel(BandAr
 #ifndef BAND_RES_RDB
 #define BAND_RES_RDB 3
 #endif
+
 struct BandResArgs {
   const bf16_t* in;   // [B][320][C]
   const bf16_t* w1;   // tower packing (+ pad)
@@ -509,43 +510,29 @@ __global__ __launch_bounds__(BNT, 1) void band_res_kernel(BandResArgs a) {
     for (int ct = 0; ct < CTW; ++ct) asm volatile("" : "+a"(acc[t][ct]));
   band_all<C, C, 10, NSRC, 16 * RB, 12, RDB>(lds, wrs2, bq, acc, lane);
   BSTAMP(2);
-  // epilogue (band_conv_kernel's): the residual tile x (band columns) from global, coalesced, into LDS
-  // rows 16 t + y; + b2 + residual, ReLU, bf16; 16-B stores
-  constexpr int ONCH = C / 8, NR = 10 * 16 * ONCH, UR = (NR + BNT - 1) / BNT;
-  uint4 rv[UR];
+  // epilogue: the residual straight into registers in the accumulator layout (this lane's image row
+  // ys, 4 channels, every band column): all loads in flight before the barrier that waits for the other
+  // waves' conv2, so their latency hides behind it (staged through LDS after the barrier it was a
+  // serialised 32 k-cycle phase in the stamps); + b2 + residual, ReLU, bf16 to LDS, 16-B stores
+  uint2 rr[CTW][10];
 #pragma unroll
-  for (int u = 0; u < UR; ++u) {
-    const int i = min(u * BNT + tid, NR - 1);
-    const int row = i / ONCH, ch = i % ONCH, t = row >> 4, y = row & 15;
-    rv[u] = *reinterpret_cast<const uint4*>(src + (size_t)(y * BW + x0 + t) * C + ch * 8);
+  for (int ct = 0; ct < CTW; ++ct) {
+    const int n = (wt + ct) * 16 + 4 * q;
+#pragma unroll
+    for (int t = 0; t < 10; ++t) rr[ct][t] = *reinterpret_cast<const uint2*>(src + (size_t)(ys * BW + x0 + t) * C + n);
   }
   float4 bias2[CTW];
 #pragma unroll
   for (int ct = 0; ct < CTW; ++ct) bias2[ct] = *reinterpret_cast<const float4*>(a.b2 + (wt + ct) * 16 + 4 * q);
   __syncthreads();  // conv1's output is no longer read
-#pragma unroll
-  for (int u = 0; u < UR; ++u) {
-    const int i = u * BNT + tid;
-    const int row = i / ONCH, ch = i % ONCH, y = row & 15;
-    if (NR % BNT == 0 || i < NR) *reinterpret_cast<uint4*>(lds + row * RB + ((ch ^ nib(KEY, y)) << 4)) = rv[u];
-  }
-  __syncthreads();
   BSTAMP(3);
-  uint2 rr[CTW][10];  // every residual read before the first write (one LDS round trip)
-#pragma unroll
-  for (int ct = 0; ct < CTW; ++ct) {
-    const int n = (wt + ct) * 16 + 4 * q;
-#pragma unroll
-    for (int t = 0; t < 10; ++t)
-      rr[ct][t] = *reinterpret_cast<const uint2*>(lds + (t * 16 + ys) * RB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1));
-  }
+  constexpr int ONCH = C / 8, NR = 10 * 16 * ONCH;
 #pragma unroll
   for (int ct = 0; ct < CTW; ++ct) {
     const int n = (wt + ct) * 16 + 4 * q;
     const float4 b4 = bias2[ct];
 #pragma unroll
     for (int t = 0; t < 10; ++t) {
-      uint2* p = reinterpret_cast<uint2*>(lds + (t * 16 + ys) * RB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1));
       const uint2 r = rr[ct][t];
       float v0 = acc[t][ct][0] + b4.x, v1 = acc[t][ct][1] + b4.y, v2 = acc[t][ct][2] + b4.z, v3 = acc[t][ct][3] + b4.w;
       v0 += __uint_as_float(r.x << 16); v1 += __uint_as_float(r.x & 0xffff0000u);
@@ -554,7 +541,7 @@ __global__ __launch_bounds__(BNT, 1) void band_res_kernel(BandResArgs a) {
       uint2 o;
       o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
       o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
-      *p = o;
+      *reinterpret_cast<uint2*>(lds + (t * 16 + ys) * RB + (((n >> 3) ^ ky) << 4) + ((n & 7) << 1)) = o;
     }
   }
   __syncthreads();
