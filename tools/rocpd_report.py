@@ -1,6 +1,8 @@
 """Read rocprofv3's rocpd SQLite output (run_results.db) without the rocpd CLI.
   rocpd_report.py stats DB OUT.csv         per-kernel stats (calls, total/avg/min/max ns, %)
-  rocpd_report.py counter DB NAME KERNEL   print per-dispatch values of counter NAME for kernels matching KERNEL"""
+  rocpd_report.py counter DB NAME KERNEL   print per-dispatch values of counter NAME for kernels matching KERNEL
+  rocpd_report.py gaps DB OUT.json         per acting step (kernels between two ctx_advance_kernel launches): span,
+                                           busy time (sum of kernel durations), idle gaps between consecutive kernels"""
 import csv
 import glob
 import os
@@ -32,7 +34,39 @@ def counter_values(db, name, kernel):
                                     "kernel_name like ? order by dispatch_id", (name, f"%{kernel}%"))]
 
 
+def step_gaps(db):
+    c = sqlite3.connect(find_db(db))
+    cur = c.execute("select * from kernels limit 1")
+    cols = [d[0] for d in cur.description]
+    ks = "start" if "start" in cols else [x for x in cols if "start" in x][0]
+    ke = "end" if "end" in cols else [x for x in cols if x.endswith("end")][0]
+    rows = c.execute(f"select name, {ks}, {ke} from kernels order by {ks}").fetchall()
+    steps, cur_step = [], []
+    for name, t0, t1 in rows:
+        cur_step.append((name, t0, t1))
+        if "ctx_advance_kernel" in name:
+            steps.append(cur_step)
+            cur_step = []
+    out = []
+    for st in steps:
+        span = st[-1][2] - st[0][1]
+        busy = sum(t1 - t0 for _, t0, t1 in st)
+        gaps = [max(0, st[i][1] - st[i - 1][2]) for i in range(1, len(st))]
+        tg = [max(0, st[i][1] - st[i - 1][2]) for i in range(1, len(st)) if "tower8" in st[i][0]]
+        out.append({"kernels": len(st), "span_us": span / 1e3, "busy_us": busy / 1e3, "idle_us": sum(gaps) / 1e3,
+                    "gap_median_us": sorted(gaps)[len(gaps) // 2] / 1e3 if gaps else None,
+                    "gap_before_tower_median_us": sorted(tg)[len(tg) // 2] / 1e3 if tg else None})
+    return out
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "gaps":
+        import json
+        res = step_gaps(sys.argv[2])
+        json.dump(res, open(sys.argv[3], "w"), indent=1)
+        for r in res:
+            print(json.dumps(r))
+        sys.exit(0)
     if sys.argv[1] == "stats":
         st = kernel_stats(sys.argv[2])
         with open(sys.argv[3], "w", newline="") as f:
