@@ -672,10 +672,14 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
         for (int j = 0; j < NA; ++j) {
           acc[j][ct] = Elt<EL>::mfma(w[1], afc[j], acc[j][ct]);
           if (ct == 0) {
+#if TOWER_ABLATE == 6  // diagnostic: no LDS A reads in the k loop (the fragments are reused)
+            afn[j] = afc[j];
+#else
             if (c + 1 < NC)
               afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
             else
               afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+#endif
           }
         }
 #pragma unroll
@@ -695,6 +699,10 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
             so = last ? ct * nxt.tstride + t8_first(nxt, nn) * 1024 : so;
             rs = last ? nxt.rs : cur.rs;
           }
+#if TOWER_ABLATE == 5  // diagnostic: every ring load re-reads 8 KB per column tile (L1-resident weights)
+          so = ct * (TNS * 1024) + ((3 * c + d) % 8) * 1024;
+          rs = cur.rs;
+#endif
           bq[ct][(3 * c + d) % RD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
         }
         if (ct == 0) {
