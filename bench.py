@@ -300,7 +300,8 @@ def tower_traffic(B, fused_tower):
 def tower_kernel_name(B):
     """The kernel mzba_tower_plan picks for batch B (tower.hip)."""
     from mzba import _lib as L
-    return {2: "tower8_kernel<0, 2>", 3: "tower8_kernel<0, 1>"}.get(L.lib().mzba_tower_plan(B), "tower_kernel<0>")
+    return {2: "tower8_kernel<0, 2>", 3: "tower8_kernel<0, 1>", 4: "towerp_kernel"}.get(L.lib().mzba_tower_plan(B),
+                                                                                      "tower_kernel<0>")
 
 
 def conv_flops(B, hw, C):

@@ -215,6 +215,8 @@ typedef struct mzba_tree_step {
   const float* r;         /* decoded rewards of this simulation's dynamics step [B] */
 } mzba_tree_step;
 
+/* Pixel-tiled tower (csrc/towerp.hip): the same math as mzba_tower on 16 envs per workgroup with one
+ * 16-row MFMA tile per latent pixel (no padding taps issued); same weight packing and I/O layout. */
 typedef struct mzba_tower_ext {
   /* prologue: dynamics ConvBlock 259->256 = 3x3 conv (tower packing) + bias + per-(position,
    * action) bias table [20][A][256] f32 (the action planes folded in), ReLU; w0 = NULL: none */
@@ -245,12 +247,23 @@ typedef struct mzba_tower_ext {
   const mzba_tree_step* tree;  /* epilogue 2 only, may be NULL */
   int elem;                    /* LDS image / weight element type: 0 bf16, 1 fp16 (weights w0, we1, we3, lw and
                                   the tower packs in fp16; latents in / out stay bf16) */
-  int plan;                    /* tower kernel: 0 = mzba_tower_plan(B) at launch; 1 / 2 / 3 = that kernel (the
+  int plan;                    /* tower kernel: 0 = mzba_tower_plan(B) at launch; 1 / 2 / 3 / 4 = that kernel (the
                                   runner records the plan it packed for and launches exactly that one) */
 } mzba_tower_ext;
 int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                      void* out, const void* wf16, const float* bias, int nblocks, int B,
                      const mzba_tower_ext* ext, hipStream_t stream);
+
+/* Pixel-tiled tower kernel (csrc/towerp.hip; plan 4 of mzba_tower / mzba_tower_fused): 16 envs per
+ * workgroup, one 16-row MFMA tile per latent pixel, so the 3x3 taps that fall on the 4x5 latent's
+ * zero padding are never issued; bit-identical to plans 2/3 on the same weight packing and I/O
+ * layout. mzba_towerp_fused takes mzba_tower_fused's arguments (bf16 only: ext->elem == 0);
+ * mzba_towerp is the plain tower (mzba_tower's arguments without the workspace). */
+int mzba_towerp_fused(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
+                      void* out, const void* wf16, const float* bias, int nblocks, int B,
+                      const mzba_tower_ext* ext, hipStream_t stream);
+int mzba_towerp(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride, void* out,
+                const void* wf16, const float* bias, int nblocks, int B, hipStream_t stream);
 
 /* Representation tail in one launch (networks.py:86-99, 271-280, 314-328): AvgPool2d of the 16x20
  * activations after the last full-resolution block (in [B][320][256] bf16), nblocks ResidualBlock(256)

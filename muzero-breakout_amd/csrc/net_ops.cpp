@@ -243,7 +243,7 @@ struct NetRunner : torch::CustomClassHolder {
     conv(t, p->conv(pre + ".2"), out, H_, W_, in, true, s);
   }
 
-  bool fused_ok() const { return use_fused && use_tower && p->fused_ok() && plan >= 1 && plan <= 3; }
+  bool fused_ok() const { return use_fused && use_tower && p->fused_ok() && plan >= 1 && plan <= 4; }
 
   // nets -------------------------------------------------------------------------------------------
   // RepresentationNetwork + _scale_state (networks.py:94-99, 271-280); x [B][HW][Cin_pad] NHWC

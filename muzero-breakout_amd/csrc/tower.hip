@@ -1193,7 +1193,7 @@ int mzba_tower_stamps_read(unsigned long long* host, int nrows) {
 // 0: pick by batch (default), 1: force the 4-env kernel, 2: force the 8-env kernel, 3: the 4-env
 // 4-wave kernel (the 8-env kernel's structure on one env quad)
 int mzba_tower_set_variant(int v) {
-  if (v < 0 || v > 3) return -1;
+  if (v < 0 || v > 4) return -1;
   g_tower_variant = v;
   return 0;
 }
@@ -1204,10 +1204,15 @@ int mzba_tower_set_variant(int v) {
 // default below 8 x CUs until the 4-wave kernels got the cross-conv weight ring and front-loaded A
 // reads (B = 1024 acting loop, same box: 20.2k env-steps/s on kernel 1, 20.9k on kernel 3,
 // profiles/r02/plan3_1024/). All take agent.pack_tower_conv weights.
+//
+// Plan 4 (towerp.hip, round 3): 16 envs per workgroup, one MFMA tile per latent pixel — the padding
+// taps the column tiles of plans 1-3 run on zero rows are not issued (130 of 180 tile-taps per env
+// instead of 156), bit-identical outputs. It needs 16 envs per CU to fill the chip: from B >= 16 x CUs.
 int mzba_tower_plan(int B) {
   if (B <= 0) return -1;
   if (g_tower_variant) return g_tower_variant;
-  return B >= 8 * tower_ncu() ? 2 : 3;
+  const int ncu = tower_ncu();
+  return B >= 16 * ncu ? 4 : (B >= 8 * ncu ? 2 : 3);
 }
 
 // device workspace bytes mzba_tower needs for batch B (0 for both current kernels)
@@ -1228,6 +1233,7 @@ int mzba_tower(const void* in, long long in_env_stride, const int32_t* slot, lon
               nblocks, B, mzba_tower_ext{}, TreeArgs{}, 0, 0, 0.f, nullptr};
   (void)ws;
   (void)ws_bytes;
+  if (plan == 4) return mzba_towerp(in, in_env_stride, slot, in_slot_stride, out, wf16, bias, nblocks, B, stream);
   if (plan == 2) {
     hipLaunchKernelGGL((tower8_kernel<0, 2>), dim3((B + 7) / 8), dim3(t8::NT), t8_dyn_lds(nblocks), stream, a);
   } else if (plan == 3) {
@@ -1254,8 +1260,11 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
                      void* out, const void* wf16, const float* bias, int nblocks, int B, const mzba_tower_ext* ext,
                      hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && wf16 && bias && ext, -1);
-  const int plan = ext->plan ? ext->plan : mzba_tower_plan(B);
-  MZ_CHECK_ARG(plan >= 1 && plan <= 3, -4);
+  int plan = ext->plan ? ext->plan : mzba_tower_plan(B);
+  MZ_CHECK_ARG(plan >= 1 && plan <= 4, -4);
+  if (plan == 4 && ext->elem == 0)
+    return mzba_towerp_fused(in, in_env_stride, slot, in_slot_stride, out, wf16, bias, nblocks, B, ext, stream);
+  if (plan == 4) plan = 2;  // the fp16 dynamics net (config 5) runs on the 8-env kernel (same packing)
   MZ_CHECK_ARG(plan == 1 || nblocks <= T8_MAX_BLOCKS, -5);  // tower8: bias table in LDS
   const mzba_tower_ext& x = *ext;
   MZ_CHECK_ARG(x.epilogue >= 0 && x.epilogue <= 2 && (x.elem == 0 || x.elem == 1), -2);

@@ -38,6 +38,8 @@ SIGNATURES = {
     "mzba_conv_lat_get_variant": [],
     "mzba_conv_lat": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
     "mzba_tower": [P, LL, P, LL, P, P, P, I, I, P, LL, P],
+    "mzba_towerp": [P, LL, P, LL, P, P, P, I, I, P],
+    "mzba_towerp_fused": [P, LL, P, LL, P, P, P, I, I, P, P],
     "mzba_tower_plan": [I],
     "mzba_tower_ws_bytes": [I],
     "mzba_tower_fused": [P, LL, P, LL, P, P, P, I, I, P, P],

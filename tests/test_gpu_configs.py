@@ -72,11 +72,13 @@ def test_config3_env_84x84_at_4096_envs_matches_oracle():
 
 # ------------------------------------------------------------------------------ config 4
 def test_config4_bf16_fused_shards_equal_global_loop():
-    """Config 4's partitioning on the benchmarked kernels: the bf16 fused path (tower8_kernel<0,2>,
-    tree step in the prediction launch, HIP-graph replay) as two shards of 2048 envs (env_offset 0 and
-    2048, n_envs_total 4096) reproduces one 4096-env loop record for record, bit for bit, over 4 acting
+    """Config 4's partitioning on the benchmarked kernels: the bf16 fused path (tree step in the
+    prediction launch, HIP-graph replay) as two shards of 2048 envs (env_offset 0 and 2048,
+    n_envs_total 4096) reproduces one 4096-env loop record for record, bit for bit, over 4 acting
     steps at T < 1 (the sampling's torch-pow lanes follow the global env position). Every RNG draw is
-    keyed on the global env id, so the records do not depend on the GPU count."""
+    keyed on the global env id, so the records do not depend on the GPU count. The global loop runs
+    the kernel the headline uses at 4096 envs (plan 4, the pixel-tiled towerp_kernel on 256 CUs), the
+    shards the 8-env tower8_kernel<0, 2> (plan 2): the two kernels agree bit for bit as well."""
     from mzba import _lib as L
     from mzba.agent import MuZeroAgent
     from mzba.acting import ActingLoop
@@ -89,7 +91,7 @@ def test_config4_bf16_fused_shards_equal_global_loop():
 
     def run(B, off):
         loop = ActingLoop(cfg, ag, B, seed=23, env_offset=off, max_steps=T, n_envs_total=4096, temperature=0.9)
-        assert loop.ws.runner.fused_ok() and loop.ws.runner.tower_plan == 2  # the 8-env kernel at both sizes
+        assert loop.ws.runner.fused_ok() and loop.ws.runner.tower_plan == L.lib().mzba_tower_plan(B)
         loop.reset(0)
         loop.act(eager=True)
         loop.capture()

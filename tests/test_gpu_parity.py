@@ -243,7 +243,7 @@ def test_nets_bf16_close():
     assert np.abs(rl.cpu().numpy() - d["r1"]).max() < 0.05
 
 
-@pytest.mark.parametrize("B,variant", [(13, 1), (1024, 1), (13, 2), (2048, 0), (13, 3), (1024, 3)])
+@pytest.mark.parametrize("B,variant", [(13, 1), (1024, 1), (13, 2), (2048, 0), (13, 3), (1024, 3), (13, 4), (40, 4)])
 def test_fused_steps_match_unfused(B, variant):
     """mzba_tower_fused (dynamics ConvBlock + tower + reward head + scale in one launch; tower +
     policy/value heads in one launch) vs the per-layer launch sequence, both bf16, same inputs;
@@ -347,7 +347,7 @@ class _Bf16StepRef:
         return self._lin(p, "pred_net.policy_head.2"), self._lin(v, "pred_net.value_head.2")
 
 
-@pytest.mark.parametrize("B,variant", [(13, 1), (64, 2), (13, 3), (64, 0)])
+@pytest.mark.parametrize("B,variant", [(13, 1), (64, 2), (13, 3), (64, 0), (13, 4), (64, 4)])
 def test_fused_bf16_steps_vs_torch_fp32(B, variant):
     """The fused bf16 dynamics and prediction launches (ConvBlock + 14 residual blocks + heads +
     min-max scale in one launch each) against a plain torch fp32 evaluation of the same folded,
@@ -1109,7 +1109,7 @@ def test_dropin_modules_resolve_via_get_class():
     assert tuple(s.shape) == e.state_shape
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4])
 @pytest.mark.parametrize("B,nblocks,gather", [(4, 1, False), (13, 3, True), (1024, 2, False)])
 def test_tower_matches_conv_chain(B, nblocks, gather, variant):
     """Fused tower (activations LDS-resident across blocks) vs torch fp32 residual blocks with
@@ -1272,7 +1272,7 @@ def test_checkpoint_reference_format_roundtrip(tmp_path):
     assert buf.get_reward_sums() == buf2.get_reward_sums()
 
 
-@pytest.mark.parametrize("variant,S", [(1, 12), (2, 12), (3, 12), (2, 200), (3, 200)])
+@pytest.mark.parametrize("variant,S", [(1, 12), (2, 12), (3, 12), (2, 200), (3, 200), (4, 12), (4, 200)])
 def test_tree_step_fused_into_prediction_is_identical(variant, S):
     """backup(sim) + select(sim + 1) inside the fused prediction launch == the separate tree
     kernels: same visit counts, values and tie-break draws, bit for bit (bf16 nets), at 12 and at

@@ -22,7 +22,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 
 python3 tools/rocpd_report.py stats $O/prof $O/kernel_stats_4096.csv
 rm -rf $O/prof
 for B in 4096 1024; do
-  K=$(python3 -c "import sys; sys.path.insert(0,'muzero-breakout_amd'); from mzba import _lib as L; print({2: 'tower8_kernel<0, 2>', 3: 'tower8_kernel<0, 1>'}.get(L.lib().mzba_tower_plan($B), 'tower_kernel<0>'))")
+  K=$(python3 -c "import sys; sys.path.insert(0,'muzero-breakout_amd'); from mzba import _lib as L; print({2: 'tower8_kernel<0, 2>', 3: 'tower8_kernel<0, 1>', 4: 'towerp_kernel'}.get(L.lib().mzba_tower_plan($B), 'tower_kernel<0>'))")
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 bench.py --envs $B --steps 1 --warmup 1 --no-graph --no-cpu --no-parity > $O/pmc_f_$B.log 2>&1
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 bench.py --envs $B --steps 1 --warmup 1 --no-graph --no-cpu --no-parity > $O/pmc_w_$B.log 2>&1
   python3 tools/pmc_tower_bench.py $O/pmc_fetch $O/pmc_write $B "$K" $O/tower_hbm_traffic.json
