@@ -32,6 +32,10 @@
 #include "common.h"
 #include "tree_dev.h"
 
+#ifndef TP_ABLATE
+#define TP_ABLATE 0  // diagnostic builds only (make towerp-ablate): 1 no LDS B reads in the k loop, 2 L1-resident weights
+#endif
+
 namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -61,6 +65,25 @@ MZ_DEV uint32_t relu_pk(uint32_t u) {
   return r;
 }
 }  // namespace tp
+
+#ifdef TOWERP_STAMPS
+// diagnostic build only (make towerp-stamps -> libmzba_pstamp.so, tools/stamp_towerp.py): s_memtime at
+// the phase boundaries, per workgroup and wave. 0 entry, 1 after staging; conv ci (0-based, the
+// dynamics prologue conv included): 2 + 5 ci + {0 start, 1 pass 0 k loop done, 2 pass 1 k loop done,
+// 3 after the first barrier, 4 after the write-back barrier}; 160.. epilogue phases; PST_N - 3 / - 2
+// s_memrealtime at entry / exit, PST_N - 1 s_memtime at exit
+constexpr int PST_N = 192, PST_WG = 256;
+__device__ unsigned long long mz_towerp_stamps[PST_WG * 4][PST_N];
+MZ_DEV void pstamp(int k, bool real = false) {
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < PST_WG && k < PST_N)
+    mz_towerp_stamps[blockIdx.x * 4 + (threadIdx.x >> 6)][k] = real ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime();
+}
+#define PSTAMP(k) pstamp(k)
+#else
+#define PSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
 
 // A wave's view of a 3x3 weight pack: buffer resource at the wave's first column tile; a fragment
 // load takes the lane's offset in one VGPR and the (column tile, pack step) offset in an SGPR
@@ -137,7 +160,11 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
 #pragma unroll
             for (int xp = 0; xp < 5; ++xp) {
               acc[(yp - DY) * 5 + xp][ct] = tp::mfma(w1, f[xp], acc[(yp - DY) * 5 + xp][ct]);
+#if TP_ABLATE == 1  // diagnostic only: no LDS B reads in the k loop (the fragments are reused)
+              if (ct == 0) fn[xp] = f[xp];
+#else
               if (ct == 0) fn[xp] = *reinterpret_cast<const bf16x8*>(lds + nb + xp * tp::PIX);
+#endif
             }
 #pragma unroll
             for (int xp = 0; xp < 4; ++xp) acc[(yp - DY) * 5 + xp + 1][ct] = tp::mfma(w0, f[xp], acc[(yp - DY) * 5 + xp + 1][ct]);
@@ -146,8 +173,13 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
             if (last) {
 #pragma unroll
               for (int d = 0; d < 3; ++d)
+#if TP_ABLATE == 2  // diagnostic only: every ring load re-reads an 8 KB L1-resident slice of the pack
+                bq[cc][d][ct] = __builtin_bit_cast(
+                    uint4, __builtin_amdgcn_raw_buffer_load_b128(cur.rs, lane * 16, ct * tp::CTB + ((3 * cc + d) & 3) * 1024, 0));
+#else
                 bq[cc][d][ct] = __builtin_bit_cast(
                     uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, ct * tp::CTB + (24 * d + st) * 1024, 0));
+#endif
             }
             if (ct == 0) {
 #pragma unroll
@@ -189,36 +221,47 @@ struct TPArgs {
   const float* tree_r;
 };
 
-// Accumulator init of one pass; its channels are chb + 16 ct + 4q + i of the lane's row (pixel p,
-// env n). MODE 0: bias; 1: bias + res (bf16 residual in registers); 2: bias + the dynamics action
-// bias table act_bias[pixel][act][256] (the one-hot action planes folded, tower.hip MODE 2).
+// Accumulator init of one pixel of a pass; its channels are chb + 16 ct + 4q + i of the lane's row
+// (pixel p, env n). MODE 0: bias; 1: bias + res (bf16 residual in registers); 2: bias + the dynamics
+// action bias table act_bias[pixel][act][256] (the one-hot action planes folded, tower.hip MODE 2).
 template <int MODE>
-MZ_DEV void tp_init(f32x4 (&acc)[tp::P][2], const float* __restrict__ bias, int chb, const uint2 (&res)[tp::P][2],
-                    const float* __restrict__ actb, int act, int A, int q) {
+MZ_DEV void tp_init1(f32x4 (&acc)[2], const float4 (&bias)[2], int chb, const uint2 (&res)[2],
+                     const float* __restrict__ actb, int act, int A, int q, int p) {
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
     const int ch = chb + 16 * ct + 4 * q;
-    const float4 b4 = *reinterpret_cast<const float4*>(bias + ch);
-#pragma unroll
-    for (int p = 0; p < tp::P; ++p) {
-      f32x4 v = {b4.x, b4.y, b4.z, b4.w};
-      if (MODE == 1) {
-        const uint2 r = res[p][ct];
-        v[0] += tp::lo(r.x); v[1] += tp::hi(r.x);
-        v[2] += tp::lo(r.y); v[3] += tp::hi(r.y);
-      } else if (MODE == 2) {
-        const float4 t = *reinterpret_cast<const float4*>(actb + ((size_t)p * A + act) * tp::C + ch);
-        v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
-      }
-      acc[p][ct] = v;
+    const float4 b4 = bias[ct];
+    f32x4 v = {b4.x, b4.y, b4.z, b4.w};
+    if (MODE == 1) {
+      const uint2 r = res[ct];
+      v[0] += tp::lo(r.x); v[1] += tp::hi(r.x);
+      v[2] += tp::lo(r.y); v[3] += tp::hi(r.y);
+    } else if (MODE == 2) {
+      const float4 t = *reinterpret_cast<const float4*>(actb + ((size_t)p * A + act) * tp::C + ch);
+      v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
     }
+    acc[ct] = v;
   }
-  // pinned to AGPRs before the k loop (left to the allocator the loop-carried accumulators move
-  // between the register files on every iteration)
+}
+template <int MODE>
+MZ_DEV void tp_init(f32x4 (&acc)[tp::P][2], const float4 (&bias)[2], int chb, const uint2 (&res)[tp::P][2],
+                    const float* __restrict__ actb, int act, int A, int q) {
+#pragma unroll
+  for (int p = 0; p < tp::P; ++p) tp_init1<MODE>(acc[p], bias, chb, res[p], actb, act, A, q, p);
+}
+// the initialised accumulators pinned to AGPRs before a k loop (left to the allocator the loop-carried
+// accumulators move between the register files on every iteration)
+MZ_DEV void tp_pin(f32x4 (&acc)[tp::P][2]) {
 #pragma unroll
   for (int p = 0; p < tp::P; ++p)
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct) asm volatile("" : "+a"(acc[p][ct]));
+}
+
+// the lane's bias values of a pass whose first channel is chb
+MZ_DEV void tp_bias(float4 (&b)[2], const float* __restrict__ bias, int chb, int q) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) b[ct] = *reinterpret_cast<const float4*>(bias + chb + 16 * ct + 4 * q);
 }
 
 // k loop of a 3x3 pass (weights in the ring, fa = its first fragments)
@@ -271,35 +314,52 @@ MZ_DEV void tp_first_frags(const uint8_t* __restrict__ lds, int lb, int q, int n
 // One 3x3 256 -> 256 conv, in place: two passes (the wave's column tiles 0-1, then 2-3), barrier,
 // write-back (ReLU, bf16), barrier. MODE as tp_init; SAVE (conv1 of a block): the write-back first
 // lifts the block input at the wave's output positions into res (conv2's residual).
-// w: this conv's pack; wn: where the ring goes after it (the next conv's first pass).
+// w: this conv's pack; wn: where the ring goes after it (the next conv's first pass). bc holds this
+// conv's pass-0 bias on entry and the next conv's (nbias) on exit; every bias is loaded one pass
+// ahead, so no pass starts with a global round trip.
 template <int MODE, bool SAVE>
 __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* w, const TPW& wn,
-                                        const float* __restrict__ bias, uint2 (&res)[2][tp::P][2],
+                                        const float* __restrict__ bias, float4 (&bc)[2], const float* __restrict__ nbias,
+                                        uint2 (&res)[2][tp::P][2],
                                         const float* __restrict__ actb, int act, int A, uint4 (&bq)[2][3][2], int lane,
-                                        int wave) {
+                                        int wave, int ci) {
   const int q = lane >> 4, n = lane & 15;
   const int lb = n * tp::ROWB;
   const int ct0 = tp::CT * wave;
   const TPW w0 = tpw(w, ct0), w1 = tpw(w, ct0 + 2);
+  PSTAMP(2 + 5 * ci);
   bf16x8 fa[5], fb[5];
   tp_first_frags(lds, lb, q, n, fa);
   uint2 out0[tp::P][2];
-  {
-    f32x4 acc[tp::P][2];
-    tp_init<MODE>(acc, bias, 64 * wave, res[0], actb, act, A, q);
-    tp_k3(lds, lb, q, n, w0, w1, bq, fa, fb, acc, lane);
-#pragma unroll
-    for (int p = 0; p < tp::P; ++p)
-#pragma unroll
-      for (int ct = 0; ct < 2; ++ct) out0[p][ct] = tp_pack(acc[p][ct]);
-  }
   f32x4 acc[tp::P][2];
-  tp_init<MODE>(acc, bias, 64 * wave + 32, res[1], actb, act, A, q);
+  tp_init<MODE>(acc, bc, 64 * wave, res[0], actb, act, A, q);
+  tp_pin(acc);
+  float4 b1[2];  // pass 1's bias, loaded ahead of pass 0's k loop
+  tp_bias(b1, bias, 64 * wave + 32, q);
+  tp_k3(lds, lb, q, n, w0, w1, bq, fa, fb, acc, lane);
+  PSTAMP(3 + 5 * ci);
+  // pass 0's accumulators out (ReLU, bf16, held in registers until the write-back) and pass 1's in,
+  // pixel by pixel: each pixel's residual registers are freed as its packed output appears, so the
+  // live register count stays flat through the transition (packing all, then initialising all,
+  // spilled part of the packed output)
+#pragma unroll
+  for (int p = 0; p < tp::P; ++p) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) out0[p][ct] = tp_pack(acc[p][ct]);
+    tp_init1<MODE>(acc[p], b1, 64 * wave + 32, res[1][p], actb, act, A, q, p);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  tp_pin(acc);
+  tp_bias(bc, nbias, 64 * wave, q);  // the next conv's pass-0 bias, ahead of pass 1's k loop
   tp_k3(lds, lb, q, n, w1, wn, bq, fa, fb, acc, lane);
+  PSTAMP(4 + 5 * ci);
   __syncthreads();  // every wave has read the whole image
+  PSTAMP(5 + 5 * ci);
   int cofs[tp::CT];
 #pragma unroll
   for (int ct = 0; ct < tp::CT; ++ct) cofs[ct] = tp_cofs(64 * wave + 16 * ct + 4 * q, n);
+  // one pixel at a time (a scheduling barrier per pixel: hoisting every accumulator read ahead of the
+  // stores spilled the packed first-pass output)
 #pragma unroll
   for (int p = 0; p < tp::P; ++p) {
 #pragma unroll
@@ -308,8 +368,10 @@ __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* 
       if (SAVE) res[ct >> 1][p][ct & 1] = *ptr;
       *ptr = ct < 2 ? out0[p][ct] : tp_pack(acc[p][ct - 2]);
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
+  PSTAMP(6 + 5 * ci);
 }
 
 // Linear heads over the image (networks.py:147, 207, 221): head h reads image channels
@@ -319,33 +381,30 @@ __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* 
 // sums, logits and decoded outputs go to LDS over it (scratch floats: part [2][4][16][16], lg
 // [2][16][16], dec [2][16][4]). Then softmax (kind 0) or support decode (1), as tower_heads.
 constexpr int TPH_PART = 0, TPH_LG = 2048, TPH_DEC = 2560, TPH_TAB = 2688;  // float offsets in the scratch
-MZ_DEV void tp_heads(const TPArgs& a, uint8_t* __restrict__ lds, int nh, const int (&hc0)[2], const int (&hC)[2],
-                     const int (&kind)[2], int env0, int nenv, int tid) {
+// NH heads over channel widths C0 / C1: every weight fragment of the wave (its k steps wave + 4u of
+// each head, 40 in all) is loaded in one batch before the first MFMA — one L2 round trip instead of
+// one per 10-step batch; the MFMAs run in tower_heads' order (k steps ascending per head)
+template <int NH, int C0, int C1>
+MZ_DEV void tp_heads(const TPArgs& a, uint8_t* __restrict__ lds, const int (&hc0)[2], const int (&kind)[2], int env0,
+                     int nenv, int tid) {
+  constexpr int NU0 = 20 * C0 / 32 / 4, NU1 = NH > 1 ? 20 * C1 / 32 / 4 : 0, NU = NU0 + NU1;
+  static_assert(NU <= 40, "head weight batch");
+  const int nh = NH;
   const int lane = tid & 63, wave = tid >> 6, q = lane >> 4, el = lane & 15;
   f32x4 hacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  bf16x8 bv[NU];
 #pragma unroll
-  for (int hd = 0; hd < 2; ++hd) {
-    if (hd >= nh) break;
-    const int C = hC[hd], K = 20 * C, nk = K / 32;
-    const bf16_t* wr = reinterpret_cast<const bf16_t*>(a.x.lw[hd]) + (size_t)el * K;
-    constexpr int HU = 10;
-    for (int s0 = wave; s0 < nk; s0 += 4 * HU) {
-      bf16x8 bv[HU];
+  for (int u = 0; u < NU; ++u) {
+    const int hd = u < NU0 ? 0 : 1, K = 20 * (hd ? C1 : C0), s = wave + 4 * (hd ? u - NU0 : u);
+    bv[u] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.x.lw[hd]) + (size_t)el * K + s * 32 + q * 8);
+  }
 #pragma unroll
-      for (int u = 0; u < HU; ++u) {
-        const int s = min(s0 + u * 4, nk - 1);
-        bv[u] = *reinterpret_cast<const bf16x8*>(wr + s * 32 + q * 8);
-      }
-#pragma unroll
-      for (int u = 0; u < HU; ++u) {
-        if (s0 + u * 4 < nk) {
-          const int k = (s0 + u * 4) * 32 + q * 8;
-          const int pos = k / C, c = hc0[hd] + (k - pos * C);
-          const bf16x8 av = *reinterpret_cast<const bf16x8*>(lds + tp::off(pos * tp::E + el, c >> 3));
-          hacc[hd] = tp::mfma(av, bv[u], hacc[hd]);
-        }
-      }
-    }
+  for (int u = 0; u < NU; ++u) {
+    const int hd = u < NU0 ? 0 : 1, C = hd ? C1 : C0, s = wave + 4 * (hd ? u - NU0 : u);
+    const int k = s * 32 + q * 8;
+    const int pos = k / C, c = hc0[hd] + (k - pos * C);
+    const bf16x8 av = *reinterpret_cast<const bf16x8*>(lds + tp::off(pos * tp::E + el, c >> 3));
+    hacc[hd] = tp::mfma(av, bv[u], hacc[hd]);
   }
   __syncthreads();  // the image is dead: LDS becomes head scratch
   float* sc = reinterpret_cast<float*>(lds);
@@ -412,6 +471,13 @@ MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0,
   for (int o = 8; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
   if (e >= nenv) return;
   const float den = (mx - mn) + 1e-8f;
+  // x / den correctly rounded as f32((double)x * R), R = f64(1 / den): the product is within 2^-52
+  // (relative) of the exact quotient, while a quotient of two f32 lies at least 2^-49 from any f32
+  // rounding midpoint (a = mu den would need a 25-bit odd significand times a 24-bit one to fit in
+  // 24 bits), so the rounding is the IEEE division's, bit for bit, at 3 instructions per element
+  // instead of the ~10 of the f32 division sequence
+  const double rden = 1.0 / (double)den;
+  auto dv = [&](float x) { return (float)((double)(x - mn) * rden); };
   const int b = env0 + e;
   bf16_t* o1 = a.out + (size_t)b * 20 * tp::C;
   bf16_t* o2 = a.x.pool ? reinterpret_cast<bf16_t*>(a.x.pool) + (size_t)b * a.x.pool_env_stride +
@@ -421,8 +487,8 @@ MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0,
     const int i = u * 16 + t, p = i >> 5, c = i & 31;
     const uint4 v = *reinterpret_cast<const uint4*>(lds + tp::off(p * tp::E + e, c));
     float f[8] = {tp::lo(v.x), tp::hi(v.x), tp::lo(v.y), tp::hi(v.y), tp::lo(v.z), tp::hi(v.z), tp::lo(v.w), tp::hi(v.w)};
-    const uint4 r = make_uint4(pack_bf16x2((f[0] - mn) / den, (f[1] - mn) / den), pack_bf16x2((f[2] - mn) / den, (f[3] - mn) / den),
-                               pack_bf16x2((f[4] - mn) / den, (f[5] - mn) / den), pack_bf16x2((f[6] - mn) / den, (f[7] - mn) / den));
+    const uint4 r = make_uint4(pack_bf16x2(dv(f[0]), dv(f[1])), pack_bf16x2(dv(f[2]), dv(f[3])),
+                               pack_bf16x2(dv(f[4]), dv(f[5])), pack_bf16x2(dv(f[6]), dv(f[7])));
     *reinterpret_cast<uint4*>(o1 + p * tp::C + c * 8) = r;
     if (o2) *reinterpret_cast<uint4*>(o2 + p * tp::C + c * 8) = r;
   }
@@ -439,6 +505,10 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
   constexpr size_t WCONV = (size_t)16 * tp::TNS * 64;  // uint4 per conv pack
   const bool pro = a.x.w0 != nullptr;
   const int ct0 = tp::CT * wave;
+  PSTAMP(0);
+#ifdef TOWERP_STAMPS
+  pstamp(PST_N - 3, true);
+#endif
   uint4 bq[2][3][2];
   tp_preload(bq, tpw(pro ? a.x.w0 : a.wf, ct0), lane);
   // the lane's env (row n of every pixel tile): its action for the dynamics ConvBlock's bias table
@@ -470,26 +540,34 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
     }
   }
   __syncthreads();
+  PSTAMP(1);
   uint2 res[2][tp::P][2];
   const int nconv = 2 * a.nblocks;
   // where the ring goes after the last tower conv: the prediction epilogue's policy conv, else
   // anything in bounds (the first tower conv)
   const TPW after = a.x.epilogue == 2 ? tpw(a.x.we3, 2 * wave) : tpw(wf, ct0);
+  float4 bc[2];
+  tp_bias(bc, pro ? a.x.b0 : a.bias, 64 * wave, q);
   if (pro)  // dynamics ConvBlock 259 -> 256 (in place)
-    tp_conv<2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), tpw(wf, ct0), a.x.b0, res, a.x.act_bias, act, a.x.A,
-                      bq, lane, wave);
+    tp_conv<2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), tpw(wf, ct0), a.x.b0, bc, a.bias, res, a.x.act_bias,
+                      act, a.x.A, bq, lane, wave, 0);
+  const int ci0 = pro ? 1 : 0;
   for (int blk = 0; blk < a.nblocks; ++blk) {
     const int k1 = 2 * blk, k2 = k1 + 1;
     const TPW w3 = k2 + 1 < nconv ? tpw(wf + (k2 + 1) * WCONV, ct0) : after;
-    tp_conv<0, true>(lds, wf + k1 * WCONV, tpw(wf + k2 * WCONV, ct0), a.bias + k1 * tp::C, res, nullptr, 0, 0, bq, lane,
-                     wave);
-    tp_conv<1, false>(lds, wf + k2 * WCONV, w3, a.bias + k2 * tp::C, res, nullptr, 0, 0, bq, lane, wave);
+    tp_conv<0, true>(lds, wf + k1 * WCONV, tpw(wf + k2 * WCONV, ct0), a.bias + k1 * tp::C, bc, a.bias + k2 * tp::C, res,
+                     nullptr, 0, 0, bq, lane, wave, ci0 + k1);
+    tp_conv<1, false>(lds, wf + k2 * WCONV, w3, a.bias + k2 * tp::C, bc, a.bias + (k2 + 1 < nconv ? k2 + 1 : k2) * tp::C,
+                      res, nullptr, 0, 0, bq, lane, wave, ci0 + k2);
   }
   if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1, the scaled latent from X, then Linear + decode
     uint2 out0[tp::P][2];
     {
       f32x4 acc[tp::P][2];
-      tp_init<0>(acc, a.x.be1, 64 * wave, res[0], nullptr, 0, 0, q);
+      float4 b4[2];
+      tp_bias(b4, a.x.be1, 64 * wave, q);
+      tp_init<0>(acc, b4, 64 * wave, res[0], nullptr, 0, 0, q);
+      tp_pin(acc);
       tp_k1(lds, lb, q, n, tpw1(a.x.we1, ct0), acc, lane);
 #pragma unroll
       for (int p = 0; p < tp::P; ++p)
@@ -497,11 +575,16 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
         for (int ct = 0; ct < 2; ++ct) out0[p][ct] = tp_pack(acc[p][ct]);
     }
     f32x4 acc[tp::P][2];
-    tp_init<0>(acc, a.x.be1, 64 * wave + 32, res[0], nullptr, 0, 0, q);
+    float4 b4[2];
+    tp_bias(b4, a.x.be1, 64 * wave + 32, q);
+    tp_init<0>(acc, b4, 64 * wave + 32, res[0], nullptr, 0, 0, q);
+    tp_pin(acc);
     tp_k1(lds, lb, q, n, tpw1(a.x.we1, ct0 + 2), acc, lane);
+    PSTAMP(160);
     __syncthreads();
     tp_scale(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
     __syncthreads();
+    PSTAMP(161);
 #pragma unroll
     for (int p = 0; p < tp::P; ++p)
 #pragma unroll
@@ -509,8 +592,14 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
         *reinterpret_cast<uint2*>(lds + p * tp::PIX + tp_cofs(64 * wave + 16 * ct + 4 * q, n)) =
             ct < 2 ? out0[p][ct] : tp_pack(acc[p][ct - 2]);
     __syncthreads();
-    const int hc0[2] = {0, 0}, hC[2] = {tp::C, 0}, kind[2] = {1, 0};
-    tp_heads(a, lds, 1, hc0, hC, kind, env0, nenv, tid);
+    const int hc0[2] = {0, 0}, kind[2] = {1, 0};
+    PSTAMP(162);
+    tp_heads<1, tp::C, 0>(a, lds, hc0, kind, env0, nenv, tid);
+    PSTAMP(163);
+#ifdef TOWERP_STAMPS
+    pstamp(PST_N - 2, true);
+    pstamp(PST_N - 1);
+#endif
     return;
   }
   if (a.x.epilogue == 2) {  // prediction: policy 3x3 256->128 -> [0,128), value 1x1 256->128 -> [128,256):
@@ -520,17 +609,25 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
       f32x4 acc[tp::P][2];
       bf16x8 fa[5], fb[5];
       tp_first_frags(lds, lb, q, n, fa);
-      tp_init<0>(acc, a.x.be3, 32 * wave, res[0], nullptr, 0, 0, q);
+      float4 b4[2];
+      tp_bias(b4, a.x.be3, 32 * wave, q);
+      tp_init<0>(acc, b4, 32 * wave, res[0], nullptr, 0, 0, q);
+      tp_pin(acc);
       const TPW wp = tpw(a.x.we3, 2 * wave);
       tp_k3(lds, lb, q, n, wp, wp, bq, fa, fb, acc, lane);
+      PSTAMP(160);
 #pragma unroll
       for (int p = 0; p < tp::P; ++p)
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct) pol[p][ct] = tp_pack(acc[p][ct]);
     }
     f32x4 acc[tp::P][2];
-    tp_init<0>(acc, a.x.be1, 32 * wave, res[0], nullptr, 0, 0, q);
+    float4 b4[2];
+    tp_bias(b4, a.x.be1, 32 * wave, q);
+    tp_init<0>(acc, b4, 32 * wave, res[0], nullptr, 0, 0, q);
+    tp_pin(acc);
     tp_k1(lds, lb, q, n, tpw1(a.x.we1, 2 * wave), acc, lane);
+    PSTAMP(161);
     __syncthreads();
 #pragma unroll
     for (int p = 0; p < tp::P; ++p)
@@ -544,8 +641,10 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
     const bool tab_lds = a.tree_on && ntab <= tp::NT;
     float tsq = 0.f, tct = 0.f;
     if (tab_lds && tid < ntab) { tsq = a.tree.sqrt_tab[tid]; tct = a.tree.c_tab[tid]; }
-    const int hc0[2] = {0, 128}, hC[2] = {128, 128}, kind[2] = {0, 1};
-    tp_heads(a, lds, 2, hc0, hC, kind, env0, nenv, tid);
+    const int hc0[2] = {0, 128}, kind[2] = {0, 1};
+    PSTAMP(162);
+    tp_heads<2, 128, 128>(a, lds, hc0, kind, env0, nenv, tid);
+    PSTAMP(163);
     if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
       float* sc = reinterpret_cast<float*>(lds);
       float* tab = sc + TPH_TAB;
@@ -559,6 +658,11 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
           tree_select_env(a.tree, a.tree_sim + 1, b, tab_lds ? tab : nullptr, tab_lds ? tab + ntab : nullptr);
       }
     }
+    PSTAMP(164);
+#ifdef TOWERP_STAMPS
+    pstamp(PST_N - 2, true);
+    pstamp(PST_N - 1);
+#endif
     return;
   }
   // the tower output, env-contiguous
@@ -574,11 +678,21 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
       }
     }
   }
+#ifdef TOWERP_STAMPS
+  pstamp(PST_N - 2, true);
+  pstamp(PST_N - 1);
+#endif
 }
 
 }  // namespace
 
 extern "C" {
+
+#ifdef TOWERP_STAMPS
+int mzba_towerp_stamps_read(unsigned long long* host, int nrows) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mz_towerp_stamps), sizeof(unsigned long long) * PST_N * nrows);
+}
+#endif
 
 // Dynamics / prediction step (or the plain tower, epilogue 0) on the pixel-tiled kernel: the
 // arguments of mzba_tower_fused (include/mzba.h); bf16 only (x.elem 0). Called by mzba_tower /
