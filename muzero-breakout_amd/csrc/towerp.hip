@@ -32,6 +32,9 @@
 #include "common.h"
 #include "tree_dev.h"
 
+#ifndef TP_SCHED
+#define TP_SCHED 1  // k-loop schedule (make towerp-sched builds the others): 1 the current fragments' MFMAs first, then the next reads
+#endif
 #ifndef TP_ABLATE
 #define TP_ABLATE 0  // diagnostic builds only (make towerp-ablate): 1 no LDS B reads in the k loop, 2 L1-resident weights
 #endif
@@ -181,6 +184,7 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
                     uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, ct * tp::CTB + (24 * d + st) * 1024, 0));
 #endif
             }
+#if TP_SCHED == 0
             if (ct == 0) {
 #pragma unroll
               for (int j = 0; j < 5; ++j) {
@@ -192,6 +196,32 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
               __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
             }
             if (last) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
+#elif TP_SCHED == 1  // the current fragments' MFMAs first (one wait), the next row's reads after them
+            if (ct == 0) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
+#pragma unroll
+              for (int j = 0; j < 5; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              }
+              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+            } else {
+              __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
+            }
+            if (last) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
+#elif TP_SCHED == 3  // reads spread over ct 0's MFMAs (one per two slots)
+            if (ct == 0) {
+#pragma unroll
+              for (int j = 0; j < 5; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              }
+              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+            } else {
+              __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
+            }
+            if (last) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
+#endif  // TP_SCHED 2: the compiler's own order
           }
           __builtin_amdgcn_sched_barrier(0);
         };
