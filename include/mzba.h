@@ -273,6 +273,14 @@ int mzba_towerp(const void* in, long long in_env_stride, const int32_t* slot, lo
 int mzba_rep_tail(const void* in, void* out, void* pool, long long pool_env_stride, const void* wf16,
                   const float* bias, int nblocks, int B, hipStream_t stream);
 
+/* nblocks ResidualBlock(256) at 16x20 in one launch (networks.py:73-82; csrc/repblocks.hip): one env per
+ * workgroup, its whole 16x20x256 image LDS-resident across the blocks; the same arithmetic as
+ * mzba_conv_band_res per block (bit-identical). in / out [B][320][256] bf16 NHWC (distinct), wf16 the
+ * 2 nblocks convs BN-folded in the tower packing back to back (+ 8 KB pad), bias [2 nblocks][256] f32.
+ * nblocks <= 24. */
+int mzba_rep_blocks(const void* in, void* out, const void* wf16, const float* bias, int nblocks, int B,
+                    hipStream_t stream);
+
 /* nn.AvgPool2d(2, 2) (networks.py:44), NHWC. */
 int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream);
 

@@ -130,7 +130,8 @@ struct NetPack : torch::CustomClassHolder {
 struct NetRunner : torch::CustomClassHolder {
   NetPack* p;  // the pack that owns this runner (NetPack::runners); the Python wrapper keeps both alive
   int64_t B, H, W, lhw, HW, plan = 0;
-  bool use_lat = true, use_tower = true, use_fused = true, use_band = true, use_rep_tail = true, use_band_res = true;
+  bool use_lat = true, use_tower = true, use_fused = true, use_band = true, use_rep_tail = true, use_band_res = true,
+       use_rep_blocks = true;
   at::Tensor r_a, r_t, r_b, x, tt, rc, pc, vc;  // scratch, allocated on first use
   // live probe: HIP events around every tower launch / latent residual conv (eager launches only)
   bool probe_on = false;
@@ -257,8 +258,20 @@ struct NetRunner : torch::CustomClassHolder {
     int64_t h = H, w = W;
     const bool tail = use_rep_tail && H == 16 && W == 20 && p->has("rep_tail.wf");
     const int64_t first = tail ? p->i("rep_tail.first") : -1;
+    // the 256-channel 16x20 residual blocks: one launch, whole images LDS-resident (mzba_rep_blocks)
+    const bool blocks = use_rep_blocks && H == 16 && W == 20 && p->has("rep_blocks.wf");
+    const int64_t bfirst = blocks ? p->i("rep_blocks.first") : -1;
     for (size_t li = 0; li < p->rep.size(); ++li) {
       const auto& [kind, a, b] = p->rep[li];
+      if ((int64_t)li == bfirst) {
+        check_rc(mzba_rep_blocks(cur, bufs[which], vp(p->t("rep_blocks.wf")), vp<float>(p->t("rep_blocks.b")),
+                                 (int)p->i("rep_blocks.n"), (int)B, s),
+                 "mzba_rep_blocks");
+        cur = bufs[which];
+        which ^= 1;
+        li += p->i("rep_blocks.n") - 1;
+        continue;
+      }
       if ((int64_t)li == first) {  // pool + 8x10 blocks + pool + scale: one launch
         check_rc(mzba_rep_tail(cur, out.data_ptr(), vp(pool), pool_env_stride, vp(p->t("rep_tail.wf")),
                                vp<float>(p->t("rep_tail.b")), (int)p->i("rep_tail.n"), (int)B, s),
@@ -559,6 +572,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              else if (k == "use_band") r->use_band = v;
              else if (k == "use_rep_tail") r->use_rep_tail = v;
              else if (k == "use_band_res") r->use_band_res = v;
+             else if (k == "use_rep_blocks") r->use_rep_blocks = v;
              else TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
            })
       .def("get_flag",
@@ -569,6 +583,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              if (k == "use_band") return r->use_band;
              if (k == "use_rep_tail") return r->use_rep_tail;
              if (k == "use_band_res") return r->use_band_res;
+             if (k == "use_rep_blocks") return r->use_rep_blocks;
              TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
              return false;
            })

@@ -106,6 +106,7 @@ class PackedNets:
         self.val_lin = self._linear(sd["pred_net.value_head.2.weight"], sd["pred_net.value_head.2.bias"], self.c1 // 2)
         self.fused = self._fused(sd, w[:, :cmain])
         self.rep_tail = self._rep_tail(sd)
+        self.rep_blocks = self._rep_blocks(sd)
         self.native = self._native()
 
     def _native(self):
@@ -156,6 +157,11 @@ class PackedNets:
             n.set_int("fused.A", self.fused["A"])
             for k, t in self.fused.get("dyn16", {}).items():
                 n.set_tensor("fused16." + k, t)
+        if self.rep_blocks is not None:
+            n.set_tensor("rep_blocks.wf", self.rep_blocks["wf"])
+            n.set_tensor("rep_blocks.b", self.rep_blocks["b"])
+            n.set_int("rep_blocks.n", self.rep_blocks["n"])
+            n.set_int("rep_blocks.first", self.rep_blocks["first"])
         if self.rep_tail is not None:
             n.set_tensor("rep_tail.wf", self.rep_tail["wf"])
             n.set_tensor("rep_tail.b", self.rep_tail["b"])
@@ -261,6 +267,37 @@ class PackedNets:
                 "wf": torch.tensor(wf, dtype=torch.float32).to(self.tdt).to(self.device),
                 "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device)}
 
+    def _rep_blocks(self, sd):
+        """Weights of mzba_rep_blocks: the run of 256-channel residual blocks at full resolution that
+        ends at the first AvgPool2d of rep_layout (bf16, 16x20 input), BN folded, in the tower packing
+        back to back. first: the rep_layout index of the run's first block."""
+        lay = rep_layout(self.mcfg)
+        if not (self.dtype == "bf16" and self.c1 == 256):
+            return None
+        pool = next((i for i, (k, _) in enumerate(lay) if k == "pool"), None)
+        if pool is None:
+            return None
+        i, blocks = pool - 1, []
+        while i >= 0 and lay[i][0] == "res":
+            blocks.insert(0, lay[i][1])
+            i -= 1
+        # 256-channel blocks only: the run starts after the conv that widens to c1
+        if not blocks or i < 0 or lay[i][0] != "conv" or len(blocks) > 24:
+            return None
+        ws, bs = [], []
+        for j in blocks:
+            for k in (1, 2):
+                p = f"rep_net.blocks.{j}"
+                alpha, beta = self._bn(sd, f"{p}.bn{k}")
+                ws.append(sd[f"{p}.conv{k}.weight"] * alpha[:, None, None, None])
+                bs.append(sd[f"{p}.conv{k}.bias"] * alpha + beta)
+        if any(w.shape[:2] != (256, 256) for w in ws):
+            return None
+        wf = np.concatenate([pack_tower_conv(w) for w in ws] + [np.zeros(LAT_PAD_ELEMS)])
+        return {"n": len(blocks), "first": i + 1,
+                "wf": torch.tensor(wf, dtype=torch.float32).to(self.tdt).to(self.device),
+                "b": torch.tensor(np.concatenate(bs), dtype=torch.float32, device=self.device)}
+
     # -- packing helpers ---------------------------------------------------------------
     @staticmethod
     def _bn(sd, p):
@@ -348,7 +385,7 @@ class NetRunner:
     `mz.NetRunner` (csrc/net_ops.cpp), whose torch custom ops run every launch on torch's current
     stream — representation_ / dynamics_ / prediction_ / prediction_tree_ (`torch.ops.mz`)."""
 
-    FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail", "use_band_res")
+    FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail", "use_band_res", "use_rep_blocks")
 
     def __init__(self, packed, B, H, W):
         self.p = packed
@@ -360,7 +397,8 @@ class NetRunner:
         self._probe = None
 
     # kernel switches (tests / A-B runs): use_lat, use_tower, use_fused, use_band, use_rep_tail,
-    # use_band_res (the representation's 16x20 residual blocks as one launch each)
+    # use_band_res (the representation's 16x20 residual blocks as one launch each), use_rep_blocks (the
+    # 256-channel 16x20 blocks as one launch, whole images LDS-resident)
     def __getattr__(self, k):
         if k in NetRunner.FLAGS:
             return self.native.get_flag(k)
