@@ -184,7 +184,7 @@ class PackedNets:
                     walk(y)
 
         for nm in ("rep", "dyn0", "dyn", "rew_conv", "rew_lin", "pred", "dyn_tower", "pred_tower", "pol_conv",
-                   "pol_lin", "val_conv", "val_lin", "fused", "rep_tail"):
+                   "pol_lin", "val_conv", "val_lin", "fused", "rep_tail", "rep_blocks"):
             walk(getattr(self, nm))
         return out
 
