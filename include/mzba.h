@@ -274,12 +274,23 @@ int mzba_rep_tail(const void* in, void* out, void* pool, long long pool_env_stri
                   const float* bias, int nblocks, int B, hipStream_t stream);
 
 /* nblocks ResidualBlock(256) at 16x20 in one launch (networks.py:73-82; csrc/repblocks.hip): one env per
- * workgroup, its whole 16x20x256 image LDS-resident across the blocks; the same arithmetic as
- * mzba_conv_band_res per block (bit-identical). in / out [B][320][256] bf16 NHWC (distinct), wf16 the
- * 2 nblocks convs BN-folded in the tower packing back to back (+ 8 KB pad), bias [2 nblocks][256] f32.
- * nblocks <= 24. */
+ * workgroup, its whole 16x20x256 image LDS-resident across the blocks; mzba_conv_band_res's tap order per
+ * accumulator, with bias + residual added first (equal to the band path within f32 rounding).
+ * in / out [B][320][256] bf16 NHWC (distinct), wf16 the 2 nblocks convs BN-folded in the tower packing
+ * back to back (+ 8 KB pad), bias [2 nblocks][256] f32. nblocks <= 24. */
 int mzba_rep_blocks(const void* in, void* out, const void* wf16, const float* bias, int nblocks, int B,
                     hipStream_t stream);
+
+/* The representation trunk at 16x20 in one launch (RepresentationNetwork, networks.py:46-82: Conv2d
+ * 2L -> c0, n0 ResidualBlock(c0), Conv2d c0 -> c1, n1 ResidualBlock(c1); everything before the first
+ * AvgPool2d; csrc/repblocks.hip): one env per workgroup, its image LDS-resident throughout, replacing the
+ * band launches and mzba_rep_blocks. 2L = 64, c0 = 128, c1 = 256. in [B][320][64] bf16 NHWC (the
+ * representation input), out [B][320][256] bf16 NHWC (distinct). w / b: HOST arrays of the
+ * 2 n0 + 2 + 2 n1 convs' device pointers in network order (stem, each c0 block's conv1 / conv2, widening
+ * conv, each c1 block's conv1 / conv2): weights in the tower packing (the last followed by 8 KB of
+ * padding), biases [Cout] f32 (BN folded into the block convs). 2 n0 + 2 + 2 n1 <= 56. */
+int mzba_rep_trunk(const void* in, void* out, const void* const* w, const float* const* b, int n0, int n1, int B,
+                   hipStream_t stream);
 
 /* nn.AvgPool2d(2, 2) (networks.py:44), NHWC. */
 int mzba_avgpool2(int dtype, const void* in, void* out, int B, int H, int W, int C, hipStream_t stream);

@@ -131,7 +131,7 @@ struct NetRunner : torch::CustomClassHolder {
   NetPack* p;  // the pack that owns this runner (NetPack::runners); the Python wrapper keeps both alive
   int64_t B, H, W, lhw, HW, plan = 0;
   bool use_lat = true, use_tower = true, use_fused = true, use_band = true, use_rep_tail = true, use_band_res = true,
-       use_rep_blocks = true;
+       use_rep_blocks = true, use_rep_trunk = true;
   at::Tensor r_a, r_t, r_b, x, tt, rc, pc, vc;  // scratch, allocated on first use
   // live probe: HIP events around every tower launch / latent residual conv (eager launches only)
   bool probe_on = false;
@@ -247,6 +247,31 @@ struct NetRunner : torch::CustomClassHolder {
   bool fused_ok() const { return use_fused && use_tower && p->fused_ok() && plan >= 1 && plan <= 4; }
 
   // nets -------------------------------------------------------------------------------------------
+  // The representation trunk as one mzba_rep_trunk launch (networks.py:46-82): when rep_layout opens
+  // with the reference's conv 2L=64 -> 128, n0 ResidualBlock(128), conv 128 -> 256, n1 ResidualBlock(256),
+  // AvgPool2d at 16x20 in bf16, fills the kernel's pointer tables (network order) and returns the index
+  // of the trunk's last layer in p->rep; else -1
+  int64_t trunk(std::vector<const void*>& w, std::vector<const float*>& b, int& n0, int& n1) const {
+    if (!use_rep_trunk || !use_band || p->dtype != 1 || H != 16 || W != 20 || p->rep.empty()) return -1;
+    w.clear(), b.clear();
+    n0 = n1 = 0;
+    auto add = [&](const Conv& c, int64_t cin, int64_t cout) {
+      if (!c.wt.defined() || c.cin != cin || c.cout != cout || c.ks != 3) return false;
+      w.push_back(c.wt.data_ptr()), b.push_back(static_cast<const float*>(c.b.data_ptr()));
+      return true;
+    };
+    size_t li = 0;
+    const auto& r = p->rep;
+    if (std::get<0>(r[li]) != "conv" || !add(p->conv(std::get<1>(r[li])), 64, 128)) return -1;
+    for (++li; li < r.size() && std::get<0>(r[li]) == "res"; ++li, ++n0)
+      if (!add(p->conv(std::get<1>(r[li])), 128, 128) || !add(p->conv(std::get<2>(r[li])), 128, 128)) return -1;
+    if (li >= r.size() || std::get<0>(r[li]) != "conv" || !add(p->conv(std::get<1>(r[li])), 128, 256)) return -1;
+    for (++li; li < r.size() && std::get<0>(r[li]) == "res"; ++li, ++n1)
+      if (!add(p->conv(std::get<1>(r[li])), 256, 256) || !add(p->conv(std::get<2>(r[li])), 256, 256)) return -1;
+    if (li >= r.size() || std::get<0>(r[li]) != "pool" || w.size() > 56) return -1;
+    return (int64_t)li - 1;
+  }
+
   // RepresentationNetwork + _scale_state (networks.py:94-99, 271-280); x [B][HW][Cin_pad] NHWC
   void representation(const at::Tensor& xin, const at::Tensor& out, const c10::optional<at::Tensor>& pool,
                       int64_t pool_env_stride) {
@@ -261,8 +286,21 @@ struct NetRunner : torch::CustomClassHolder {
     // the 256-channel 16x20 residual blocks: one launch, whole images LDS-resident (mzba_rep_blocks)
     const bool blocks = use_rep_blocks && H == 16 && W == 20 && p->has("rep_blocks.wf");
     const int64_t bfirst = blocks ? p->i("rep_blocks.first") : -1;
+    // stem, 128-channel blocks, widening conv and 256-channel blocks: one launch, whole images
+    // LDS-resident (mzba_rep_trunk)
+    std::vector<const void*> tw;
+    std::vector<const float*> tb;
+    int n0 = 0, n1 = 0;
+    const int64_t tlast = trunk(tw, tb, n0, n1);
     for (size_t li = 0; li < p->rep.size(); ++li) {
       const auto& [kind, a, b] = p->rep[li];
+      if (li == 0 && tlast >= 0) {
+        check_rc(mzba_rep_trunk(cur, bufs[which], tw.data(), tb.data(), n0, n1, (int)B, s), "mzba_rep_trunk");
+        cur = bufs[which];
+        which ^= 1;
+        li = (size_t)tlast;
+        continue;
+      }
       if ((int64_t)li == bfirst) {
         check_rc(mzba_rep_blocks(cur, bufs[which], vp(p->t("rep_blocks.wf")), vp<float>(p->t("rep_blocks.b")),
                                  (int)p->i("rep_blocks.n"), (int)B, s),
@@ -573,6 +611,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              else if (k == "use_rep_tail") r->use_rep_tail = v;
              else if (k == "use_band_res") r->use_band_res = v;
              else if (k == "use_rep_blocks") r->use_rep_blocks = v;
+             else if (k == "use_rep_trunk") r->use_rep_trunk = v;
              else TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
            })
       .def("get_flag",
@@ -584,6 +623,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              if (k == "use_rep_tail") return r->use_rep_tail;
              if (k == "use_band_res") return r->use_band_res;
              if (k == "use_rep_blocks") return r->use_rep_blocks;
+             if (k == "use_rep_trunk") return r->use_rep_trunk;
              TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
              return false;
            })

@@ -1,27 +1,32 @@
-// The representation's residual blocks at 16x20 x 256 channels (networks.py:73-82, ResidualBlock
-// :19-35; the trunk's last stage before the first AvgPool2d) in ONE launch, bf16, gfx950 MFMA. The
-// stem, the 128-channel blocks and the widening conv before them stay on the band kernels (band.hip), the
-// tail (pool, 8x10 blocks, pool, _scale_state) on rep_tail_kernel.
+// The representation's trunk at 16x20 (networks.py:46-82: the stem Conv2d(2L -> c0), the c0-channel
+// ResidualBlocks, the widening Conv2d(c0 -> c1), the c1-channel ResidualBlocks; ResidualBlock :19-35)
+// in ONE launch, bf16, gfx950 MFMA — everything before the first AvgPool2d. The tail (pool, 8x10 blocks,
+// pool, _scale_state) runs on rep_tail_kernel. The same kernel without its stem stage is
+// mzba_rep_blocks (the c1 = 256-channel blocks alone).
 //
-// One workgroup (4 waves, one per SIMD) owns ONE env: its 16 x 20 x 256 activation image is 160 KiB,
-// the CU's whole LDS, so it stays resident across every conv of the blocks (band_res_kernel re-stages a
-// 10-column band with its halo per block and recomputes the halo columns of conv1). A 16-row MFMA tile
-// is one image column x (rows = y): a tap (dy, dx) maps tile x onto tile x + dx whole (the 2 tile-taps
-// that leave the image are not issued) and shifts rows by dy inside the tile; the one row a shift
-// pushes out of the image is zeroed in the B fragment (v_cndmask on the lane that reads it: LDS has no
-// room for zero rows). LDS row of (x, y) = 16 x + y (512 B), 16-B chunks XOR-swizzled by y: every B
-// fragment read is conflict-free for every shift.
+// One workgroup (4 waves, one per SIMD) owns ONE env: its 16 x 20 activation image (64, 128 or 256
+// channels: 40 / 80 / 160 KiB, the last the CU's whole LDS) stays resident from the staged input to the
+// last block (the band kernels re-stage a 10-column band with its halo per conv or block and recompute the
+// halo columns). A 16-row MFMA tile is one image column x (rows = y): a tap (dy, dx) maps tile x onto tile
+// x + dx whole (the 2 tile-taps that leave the image are not issued) and shifts rows by dy inside the tile;
+// the one row a shift pushes out of the image is zeroed in the B fragment (v_cndmask on the lane that
+// reads it: LDS has no room for zero rows). LDS row of (x, y) = 16 x + y (2C bytes), 16-B chunks
+// XOR-swizzled by a key of y (y for 256- and 512-B rows, y >> 1 for the stem input's 128-B rows, whose
+// pairs of rows share a bank set): every B fragment read is conflict-free for every shift.
 //
-// Each conv runs towerp_kernel's structure: the wave's 4 output column tiles in two passes of two (32
-// channels x all 20 column tiles = 160 accumulators), the first pass's output held packed in registers,
-// weights (the tower packing, agent.pack_tower_conv) through a two-step ring that runs across passes
-// and convs, in place (k loops, barrier, write-back, barrier); conv1 lifts the block input at its output
-// positions into registers for conv2. Per accumulator the taps are added in the band kernels' order (dy,
-// channel step, then dx = 0, -1, +1; their padding taps add exact zeros, skipped or zeroed here); the
-// accumulators start at bias (+ residual) as in towerp_kernel, where band_res_kernel adds them after the
-// taps (with its epilogue order this kernel equals band_res_kernel bit for bit, but the residual of
-// conv2's second pass then stays live through both passes and spills: 8 % slower). Parity: a plain torch
-// fp32 evaluation of the bf16-rounded operands, as the band kernels (tests/test_gpu_repblocks.py).
+// Each conv runs towerp_kernel's structure: a wave owns a quarter of the output channels (32 at Cout 128:
+// one pass of two column tiles; 64 at Cout 256: two passes, the first pass's output held packed in
+// registers), all 20 column tiles (40 accumulators a pass); weights (the tower packing,
+// agent.pack_tower_conv) through a two-step ring that runs across passes and convs, whatever their
+// widths; in place (k loops, barrier, write-back in the output's row width, barrier — every input read
+// precedes every output write, so a conv may widen the image); conv1 of a block lifts the block input
+// at its output positions into registers for conv2. Per accumulator the taps are added in the band
+// kernels' order (dy, channel step, then dx = 0, -1, +1; their padding taps add exact zeros, skipped or
+// zeroed here); the accumulators start at bias (+ residual) as in towerp_kernel, where band_res_kernel
+// adds them after the taps (with its epilogue order this kernel equals band_res_kernel bit for bit, but
+// the residual of conv2's second pass then stays live through both passes and spills: 8 % slower).
+// Parity: a plain torch fp32 evaluation of the bf16-rounded operands, as the band kernels
+// (tests/test_gpu_repblocks.py).
 #include "common.h"
 
 namespace {
@@ -33,6 +38,7 @@ namespace rf {
 constexpr int H = 16, W = 20;          // image rows (a column tile) x columns (tiles)
 constexpr int NT = 256;                // 4 waves
 constexpr int IMG = 163840;            // 320 rows x 512 B: the CU's LDS
+constexpr int MAXC = 56;               // convs per launch (kernel-argument pointer tables)
 MZ_DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 MZ_DEV float lo(uint32_t u) { return __uint_as_float(u << 16); }
 MZ_DEV float hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
@@ -45,17 +51,26 @@ MZ_DEV uint2 pack(const f32x4& a, bool relu) {
   const uint32_t x = pack_bf16x2(a[0], a[1]), y = pack_bf16x2(a[2], a[3]);
   return relu ? make_uint2(relu_pk(x), relu_pk(y)) : make_uint2(x, y);
 }
+// swizzle key of image row y for rows of 1 << RBL bytes. A B-fragment read of 16 lanes (rows y = 0..15,
+// one 16-B chunk each) is conflict-free when the lanes' (bank set of the row start, chunk ^ key) pairs
+// differ: 256- and 512-B rows all start in bank set 0, so key = y; 128-B rows alternate two bank sets
+// by y & 1, so key = y >> 1 (8 chunks a row, 8 keys per set)
+template <int RBL> MZ_DEV int key(int y) { return RBL == 7 ? (y >> 1) : y; }
+template <int C> constexpr int rbl() { return C == 64 ? 7 : (C == 128 ? 8 : 9); }
 }  // namespace rf
 
 struct RFArgs {
-  const bf16_t* in;  // [B][320][256] NHWC, the blocks' input
-  bf16_t* out;       // [B][320][256] NHWC
-  const uint4* wf;   // 2 nblocks convs in the tower packing back to back (+ the ring's 8 KB overrun)
-  const float* bias; // [2 nblocks][256], BN folded
-  int B, nblocks;
+  const bf16_t* in;               // [B][320][Cin] NHWC: 2L = 64 channels with the stem, else 256
+  bf16_t* out;                    // [B][320][256] NHWC
+  const uint4* w[rf::MAXC];       // per conv: its tower packing (+ the ring's 8 KB overrun after the last)
+  const float* b[rf::MAXC];       // per conv: [Cout] f32, BN folded
+  int n0, n1, B;                  // c0- / c1-channel blocks; n0 < 0: no stem stage (mzba_rep_blocks)
 };
-constexpr int RF_CIN = 256, RF_TNS = 72;                     // every conv 256 -> 256, 3x3
-constexpr size_t RF_WCONV = (size_t)16 * RF_TNS * 64;        // uint4 per conv pack
+// conv k's widths: with the stem, k = 0 stem (64 -> 128), 1 .. 2 n0 the 128-channel blocks, 2 n0 + 1 the
+// widening conv (128 -> 256), then the 256-channel blocks; without it, every conv 256 -> 256
+MZ_DEV int rf_cin(const RFArgs& a, int k) { return a.n0 < 0 ? 256 : (k == 0 ? 64 : (k <= 2 * a.n0 + 1 ? 128 : 256)); }
+MZ_DEV int rf_cout(const RFArgs& a, int k) { return a.n0 < 0 ? 256 : (k <= 2 * a.n0 ? 128 : 256); }
+MZ_DEV int rf_nconv(const RFArgs& a) { return a.n0 < 0 ? 2 * a.n1 : 2 * a.n0 + 2 + 2 * a.n1; }
 
 // A wave's view of one pass of a conv: the pack at the pass's first column tile, bytes per column tile,
 // channel steps per tap (k step s of the pass, column shift index d = dx + 1: pack step 3 nc d + s)
@@ -63,53 +78,55 @@ struct RFW {
   __amdgpu_buffer_rsrc_t rs;
   int ts, nc;
 };
-MZ_DEV RFW rfw(const uint4* pack, int ct) {
-  const uint4* p = pack + (size_t)ct * RF_TNS * 64;
-  return RFW{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(p), 0, 0x7fffffff, 0x00020000), RF_TNS * 1024,
-             RF_CIN / 32};
+// pass h of conv k for wave `wave`: its column tiles (Cout / 64) wave + 2 h, + 1
+MZ_DEV RFW rfw(const RFArgs& a, int k, int wave, int h) {
+  const int nc = rf_cin(a, k) / 32, ct = (rf_cout(a, k) / 64) * wave + 2 * h;
+  const uint4* p = a.w[k] + (size_t)ct * 9 * nc * 64;
+  return RFW{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(p), 0, 0x7fffffff, 0x00020000), 9 * nc * 1024, nc};
 }
 
-// B-fragment addressing of lane (q, n) for row shift dy over an image at src with row bytes 1 << rbl:
-// byte offset of its row in column 0 (the clamped row for the lane a shift pushes out) and the
-// swizzle key; ok = the row is inside the image
-MZ_DEV void rf_rows(int src, int rbl, int n, int dy, int& base, int& key, bool& ok) {
+// B-fragment addressing of lane (q, n) for row shift dy over an image at src with rows of 1 << RBL bytes:
+// byte offset of its row in column 0 (the clamped row for the lane a shift pushes out) and the swizzle
+// key; ok = the row is inside the image
+template <int RBL>
+MZ_DEV void rf_rows(int src, int n, int dy, int& base, int& key, bool& ok) {
   const int yy = n + dy;
   ok = (unsigned)yy < (unsigned)rf::H;
   const int yc = ok ? yy : n;
-  base = src + (yc << rbl);
-  key = yc;
+  base = src + (yc << RBL);
+  key = rf::key<RBL>(yc);
 }
 
-// the 3 nc k steps of one pass with row shift dy = DYI - 1: per (dy, channel step c) the 20 columns in
+// the 3 NC k steps of one pass with row shift dy = DYI - 1: per (dy, channel step c) the 20 columns in
 // 4 groups of 5; a group's 5 B fragments (read during the previous group's first MFMAs) feed dx = 0
 // (output x'), dx = -1 (x' + 1) and dx = +1 (x' - 1) of both column tiles. fa holds the first group's
 // fragments on entry and the next dy's first on exit.
-template <int DYI>
-__device__ __forceinline__ void rf_dy(const uint8_t* __restrict__ lds, int src, int rbl, int q, int n, const RFW& cur,
+template <int DYI, int RBL, int NC>
+__device__ __forceinline__ void rf_dy(const uint8_t* __restrict__ lds, int src, int q, int n, const RFW& cur,
                                       const RFW& nxt, uint4 (&bq)[2][3][2], f32x4 (&acc)[rf::W][2], bf16x8 (&fa)[5],
                                       bf16x8 (&fb)[5], int lane) {
   constexpr int DY = DYI - 1, DYN = DYI == 2 ? -1 : DY + 1;  // the next dy loop's (after dy = +1: the next pass's)
-  const int nc = cur.nc, ncp = nc >> 1, cstr = 16 << rbl;
+  constexpr int ncp = NC >> 1, cstr = 16 << RBL;
   int base, key, nbase, nkey;
   bool ok, nok;
-  rf_rows(src, rbl, n, DY, base, key, ok);
-  rf_rows(src, rbl, n, DYN, nbase, nkey, nok);
+  rf_rows<RBL>(src, n, DY, base, key, ok);
+  rf_rows<RBL>(src, n, DYN, nbase, nkey, nok);
   (void)nok;
 #pragma unroll 1
   for (int cp = 0; cp < ncp; ++cp) {
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc) {
-      const int c = 2 * cp + cc, s = nc * DYI + c;
+      const int c = 2 * cp + cc, s = NC * DYI + c;
       const bool wrap = cc == 1 && cp == ncp - 1;  // the next k step opens the next dy loop
       const int xc = base + (((4 * c + q) ^ key) << 4);
       const int xn = wrap ? nbase + ((q ^ nkey) << 4) : base + (((4 * (c + 1) + q) ^ key) << 4);
-      // ring slots of this step reload k step s + 2 (past the pass: the next pass's s + 2 - 3 nc)
-      int st = s + 2, ts = cur.ts, sn = 3 * nc;
+      // ring slots of this step reload k step s + 2 (past the pass: the next pass's s + 2 - 3 NC)
+      int st = s + 2, ts = cur.ts, sn = 3 * NC;
       __amdgpu_buffer_rsrc_t rs = cur.rs;
       if (DYI == 2) {
-        const bool past = st >= 3 * nc;
+        const bool past = st >= 3 * NC;
         rs = past ? nxt.rs : cur.rs;
-        st = past ? st - 3 * nc : st;
+        st = past ? st - 3 * NC : st;
         ts = past ? nxt.ts : cur.ts;
         sn = past ? 3 * nxt.nc : sn;
       }
@@ -172,11 +189,12 @@ __device__ __forceinline__ void rf_dy(const uint8_t* __restrict__ lds, int src, 
   }
 }
 
-MZ_DEV void rf_first_frags(const uint8_t* __restrict__ lds, int src, int rbl, int q, int n, bf16x8 (&fa)[5]) {
+template <int RBL>
+MZ_DEV void rf_first_frags(const uint8_t* __restrict__ lds, int src, int q, int n, bf16x8 (&fa)[5]) {
   int base, key;
   bool ok;
-  rf_rows(src, rbl, n, -1, base, key, ok);
-  const int x0 = base + ((q ^ key) << 4), cstr = 16 << rbl;
+  rf_rows<RBL>(src, n, -1, base, key, ok);
+  const int x0 = base + ((q ^ key) << 4), cstr = 16 << RBL;
 #pragma unroll
   for (int j = 0; j < 5; ++j) fa[j] = *reinterpret_cast<const bf16x8*>(lds + x0 + j * cstr);
 }
@@ -203,85 +221,96 @@ MZ_DEV void rf_pin(f32x4 (&acc)[rf::W][2]) {
     for (int ct = 0; ct < 2; ++ct) asm volatile("" : "+a"(acc[x][ct]));
 }
 
-// the lane's bias values of pass h of conv k (its column tiles 4 wave + 2h, + 1)
-MZ_DEV void rf_bias(float4 (&b)[2], const float* bias, int k, int wave, int h, int q) {
-  const int ct0 = 4 * wave + 2 * h;
+// the lane's bias values of pass h of conv k (its column tiles (Cout / 64) wave + 2h, + 1)
+MZ_DEV void rf_bias(float4 (&b)[2], const RFArgs& a, int k, int wave, int h, int q) {
+  const int ct0 = (rf_cout(a, k) / 64) * wave + 2 * h;
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct) b[ct] = *reinterpret_cast<const float4*>(bias + k * 256 + 16 * (ct0 + ct) + 4 * q);
+  for (int ct = 0; ct < 2; ++ct) b[ct] = *reinterpret_cast<const float4*>(a.b[k] + 16 * (ct0 + ct) + 4 * q);
 }
 
 // One pass (h) of conv k: k loops over the pass's two column tiles (acc initialised and pinned by the
-// caller), the ring's continuation pointed at the next pass's weights
+// caller), the ring's continuation pointed at the next pass's weights: this conv's second, the next
+// conv's first, or (after the last) this one again (loads in range, never used)
+template <int RBL, int NC, int NP>
 __device__ __forceinline__ void rf_pass(const RFArgs& a, const uint8_t* __restrict__ lds, int k, int h,
-                                        float4 (&bc)[2], uint4 (&bq)[2][3][2], f32x4 (&acc)[rf::W][2],
-                                        bf16x8 (&fa)[5], bf16x8 (&fb)[5], int lane, int wave) {
+                                        uint4 (&bq)[2][3][2], f32x4 (&acc)[rf::W][2], bf16x8 (&fa)[5],
+                                        bf16x8 (&fb)[5], int lane, int wave) {
   const int q = lane >> 4, n = lane & 15;
-  // the next pass: this conv's second, the next conv's first, or (after the last) this one again
-  // (loads in range, never used); its bias now, its weights by the ring
-  const int nconv = 2 * a.nblocks;
-  const bool more = h == 0, nextk = !more && k + 1 < nconv;
-  const int nk = more ? k : (nextk ? k + 1 : k), nh = more ? 1 : 0;
-  (void)bc;
-  const RFW cur = rfw(a.wf + k * RF_WCONV, 4 * wave + 2 * h);
-  const RFW nxt = (more || nextk) ? rfw(a.wf + nk * RF_WCONV, 4 * wave + 2 * nh) : cur;
-  rf_dy<0>(lds, 0, 9, q, n, cur, nxt, bq, acc, fa, fb, lane);
-  rf_dy<1>(lds, 0, 9, q, n, cur, nxt, bq, acc, fa, fb, lane);
-  rf_dy<2>(lds, 0, 9, q, n, cur, nxt, bq, acc, fa, fb, lane);
+  const bool more = h + 1 < NP, nextk = !more && k + 1 < rf_nconv(a);
+  const RFW cur = rfw(a, k, wave, h);
+  const RFW nxt = more ? rfw(a, k, wave, h + 1) : (nextk ? rfw(a, k + 1, wave, 0) : cur);
+  rf_dy<0, RBL, NC>(lds, 0, q, n, cur, nxt, bq, acc, fa, fb, lane);
+  rf_dy<1, RBL, NC>(lds, 0, q, n, cur, nxt, bq, acc, fa, fb, lane);
+  rf_dy<2, RBL, NC>(lds, 0, q, n, cur, nxt, bq, acc, fa, fb, lane);
 }
 
-// One conv of a block, k loops then an in-place write-back. RES false: conv1 (the write-back first
-// lifts the block input at the wave's output positions into res); true: conv2 (acc starts at bias +
-// res). ReLU on both. bc: this conv's pass-0 bias on entry, the next conv's on exit (every bias loaded
-// a pass ahead of its use).
-template <bool RES>
+// One conv (Cin -> Cout, 3x3), k loops then an in-place write-back. RES 0: plain (the stem and the
+// widening conv: no activation, networks.py:47-55, 64-72); 1: conv1 of a block (ReLU; the write-back
+// first lifts the block input at the wave's output positions into res); 2: conv2 (acc starts at bias +
+// res, ReLU after the sum). bc: this conv's pass-0 bias on entry, the next conv's on exit (every bias
+// loaded a pass ahead of its use).
+template <int CIN, int COUT, int RES>
 __device__ __forceinline__ void rf_conv(const RFArgs& a, uint8_t* __restrict__ lds, int k, float4 (&bc)[2],
-                                        uint2 (&res)[2][rf::W][2], uint4 (&bq)[2][3][2], int lane, int wave) {
+                                        uint2 (&res)[COUT / 128][rf::W][2], uint4 (&bq)[2][3][2], int lane,
+                                        int wave) {
+  constexpr int RBI = rf::rbl<CIN>(), RBO = rf::rbl<COUT>(), NC = CIN / 32, NP = COUT / 128, CTW = COUT / 64;
+  constexpr bool RELU = RES != 0;
+  static_assert(RES == 0 || CIN == COUT, "residual blocks keep their width");
   const int q = lane >> 4, n = lane & 15;
+  const int kn = k + 1 < rf_nconv(a) ? k + 1 : k;
   bf16x8 fa[5], fb[5];
-  rf_first_frags(lds, 0, 9, q, n, fa);
-  uint2 out0[rf::W][2];
+  rf_first_frags<RBI>(lds, 0, q, n, fa);
+  uint2 out0[rf::W][2];  // pass 0's output (two passes only)
   f32x4 acc[rf::W][2];
 #pragma unroll
-  for (int x = 0; x < rf::W; ++x) rf_init1(acc[x], bc, res[0][x], RES);
+  for (int x = 0; x < rf::W; ++x) rf_init1(acc[x], bc, res[0][x], RES == 2);
   rf_pin(acc);
-  rf_bias(bc, a.bias, k, wave, 1, q);  // pass 1's bias, ahead of pass 0's k loop
-  rf_pass(a, lds, k, 0, bc, bq, acc, fa, fb, lane, wave);
+  if (NP > 1)
+    rf_bias(bc, a, k, wave, 1, q);  // pass 1's bias, ahead of pass 0's k loop
+  else
+    rf_bias(bc, a, kn, wave, 0, q);  // the next conv's pass-0 bias
+  rf_pass<RBI, NC, NP>(a, lds, k, 0, bq, acc, fa, fb, lane, wave);
+  if constexpr (NP > 1) {
 #pragma unroll
-  for (int x = 0; x < rf::W; ++x) {  // pass 0 out (ReLU, bf16, held), pass 1 in, column by column
+    for (int x = 0; x < rf::W; ++x) {  // pass 0 out (bf16, held), pass 1 in, column by column
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) out0[x][ct] = rf::pack(acc[x][ct], true);
-    rf_init1(acc[x], bc, res[1][x], RES);
-    __builtin_amdgcn_sched_barrier(0);
+      for (int ct = 0; ct < 2; ++ct) out0[x][ct] = rf::pack(acc[x][ct], RELU);
+      rf_init1(acc[x], bc, res[NP - 1][x], RES == 2);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    rf_pin(acc);
+    rf_bias(bc, a, kn, wave, 0, q);  // the next conv's pass-0 bias
+    rf_pass<RBI, NC, NP>(a, lds, k, 1, bq, acc, fa, fb, lane, wave);
   }
-  rf_pin(acc);
-  rf_bias(bc, a.bias, k + 1 < 2 * a.nblocks ? k + 1 : k, wave, 0, q);  // the next conv's pass-0 bias
-  rf_pass(a, lds, k, 1, bc, bq, acc, fa, fb, lane, wave);
   __syncthreads();  // every wave has read the whole image
-  // write-back column by column: row 16 x + n (swizzle key n), the wave's 64 channels. The lane's
-  // offsets are recomputed per conv from an opaque copy of n: left CSE'd across the block's convs, the
-  // 80 addresses stayed live through conv2 and were spilled, each reload waiting on the weight ring
+  // write-back column by column: row 16 x + n (swizzle key of n), the wave's Cout / 4 channels. The
+  // lane's offsets are recomputed per conv from an opaque copy of n: left CSE'd across the block's convs,
+  // the 80 addresses stayed live through conv2 and were spilled, each reload waiting on the weight ring
   int no = n;
   asm volatile("" : "+v"(no));
-  int cofs[4];
+  int cofs[CTW];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int ch = 16 * (4 * wave + ct) + 4 * q;
-    cofs[ct] = (no << 9) + (((ch >> 3) ^ no) << 4) + ((ch & 7) << 1);
+  for (int ct = 0; ct < CTW; ++ct) {
+    const int ch = 16 * (CTW * wave + ct) + 4 * q;
+    cofs[ct] = (no << RBO) + (((ch >> 3) ^ rf::key<RBO>(no)) << 4) + ((ch & 7) << 1);
   }
 #pragma unroll
   for (int x = 0; x < rf::W; ++x) {
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      uint2* p = reinterpret_cast<uint2*>(lds + (x << 13) + cofs[ct]);
-      if (!RES) res[ct >> 1][x][ct & 1] = *p;
-      *p = ct < 2 ? out0[x][ct] : rf::pack(acc[x][ct - 2], true);
+    for (int ct = 0; ct < CTW; ++ct) {
+      uint2* p = reinterpret_cast<uint2*>(lds + (x << (RBO + 4)) + cofs[ct]);
+      if (RES == 1) res[ct >> 1][x][ct & 1] = *p;
+      *p = (NP > 1 && ct < 2) ? out0[x][ct] : rf::pack(acc[x][ct - (NP > 1 ? 2 : 0)], RELU);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   __syncthreads();
 }
 
-__global__ __launch_bounds__(rf::NT, 1) void rep_blocks_kernel(RFArgs a) {
+// STEM: the input is the 64-channel representation input and the launch runs the whole trunk; else the
+// input is the 256-channel image and the launch runs the n1 blocks alone (mzba_rep_blocks)
+template <bool STEM>
+__global__ __launch_bounds__(rf::NT, 1) void rep_trunk_kernel(RFArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[rf::IMG];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -289,7 +318,7 @@ __global__ __launch_bounds__(rf::NT, 1) void rep_blocks_kernel(RFArgs a) {
   const int b = blockIdx.x;
   uint4 bq[2][3][2];
   {  // the ring's first two k steps (conv 0, pass 0)
-    const RFW w0 = rfw(a.wf, 4 * wave);
+    const RFW w0 = rfw(a, 0, wave, 0);
 #pragma unroll
     for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
@@ -300,8 +329,18 @@ __global__ __launch_bounds__(rf::NT, 1) void rep_blocks_kernel(RFArgs a) {
               uint4, __builtin_amdgcn_raw_buffer_load_b128(w0.rs, lane * 16, ct * w0.ts + (3 * w0.nc * d + cc) * 1024, 0));
   }
   float4 bc[2];
-  rf_bias(bc, a.bias, 0, wave, 0, q);
-  {  // stage: pixel p = 20 y + x -> LDS row 16 x + y, two batches of 20 chunks per thread
+  rf_bias(bc, a, 0, wave, 0, q);
+  if constexpr (STEM) {  // stage: pixel p = 20 y + x -> LDS row 16 x + y (128 B, key y >> 1), 10 chunks per thread
+    const bf16_t* src = a.in + (size_t)b * rf::H * rf::W * 64;
+    uint4 v[10];
+#pragma unroll
+    for (int u = 0; u < 10; ++u) v[u] = *reinterpret_cast<const uint4*>(src + (size_t)(u * rf::NT + tid) * 8);
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const int i = u * rf::NT + tid, p = i >> 3, c = i & 7, y = p / rf::W, x = p % rf::W;
+      *reinterpret_cast<uint4*>(lds + ((x * 16 + y) << 7) + ((c ^ rf::key<7>(y)) << 4)) = v[u];
+    }
+  } else {  // stage: pixel p = 20 y + x -> LDS row 16 x + y, two batches of 20 chunks per thread
     const bf16_t* src = a.in + (size_t)b * rf::H * rf::W * 256;
 #pragma unroll
     for (int hb = 0; hb < 2; ++hb) {
@@ -316,10 +355,26 @@ __global__ __launch_bounds__(rf::NT, 1) void rep_blocks_kernel(RFArgs a) {
     }
   }
   __syncthreads();
-  for (int blk = 0; blk < a.nblocks; ++blk) {
+  int k = 0;
+  if constexpr (STEM) {
+    {
+      uint2 none[1][rf::W][2];
+      rf_conv<64, 128, 0>(a, lds, k++, bc, none, bq, lane, wave);
+    }
+    for (int blk = 0; blk < a.n0; ++blk) {
+      uint2 res[1][rf::W][2];  // lives from conv1's write-back to conv2's inits
+      rf_conv<128, 128, 1>(a, lds, k++, bc, res, bq, lane, wave);
+      rf_conv<128, 128, 2>(a, lds, k++, bc, res, bq, lane, wave);
+    }
+    {
+      uint2 none[2][rf::W][2];
+      rf_conv<128, 256, 0>(a, lds, k++, bc, none, bq, lane, wave);
+    }
+  }
+  for (int blk = 0; blk < a.n1; ++blk) {
     uint2 res[2][rf::W][2];  // lives from conv1's write-back to conv2's inits
-    rf_conv<false>(a, lds, 2 * blk, bc, res, bq, lane, wave);
-    rf_conv<true>(a, lds, 2 * blk + 1, bc, res, bq, lane, wave);
+    rf_conv<256, 256, 1>(a, lds, k++, bc, res, bq, lane, wave);
+    rf_conv<256, 256, 2>(a, lds, k++, bc, res, bq, lane, wave);
   }
   // the output, NHWC: pixel p = 20 y + x from LDS row 16 x + y
   bf16_t* dst = a.out + (size_t)b * rf::H * rf::W * 256;
@@ -331,18 +386,45 @@ __global__ __launch_bounds__(rf::NT, 1) void rep_blocks_kernel(RFArgs a) {
   }
 }
 
+constexpr size_t RF_WCONV = (size_t)16 * 72 * 64;  // uint4 per 256 -> 256 conv pack
+
 }  // namespace
 
 extern "C" {
 
-// nblocks ResidualBlock(256) at 16x20 in one launch (see above): in / out [B][320][256] bf16 NHWC
-// (distinct buffers), wf16: the 2 nblocks convs in the tower packing back to back + 8 KB, bias
-// [2 nblocks][256] f32 (BN folded)
+// nblocks ResidualBlock(256) at 16x20 in one launch (the trunk kernel without its stem stage): in / out
+// [B][320][256] bf16 NHWC (distinct buffers), wf16: the 2 nblocks convs in the tower packing back to
+// back + 8 KB, bias [2 nblocks][256] f32 (BN folded)
 int mzba_rep_blocks(const void* in, void* out, const void* wf16, const float* bias, int nblocks, int B,
                     hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && nblocks <= 24 && in && out && wf16 && bias && in != out, -1);
-  RFArgs a{(const bf16_t*)in, (bf16_t*)out, (const uint4*)wf16, bias, B, nblocks};
-  hipLaunchKernelGGL(rep_blocks_kernel, dim3(B), dim3(rf::NT), 0, stream, a);
+  RFArgs a{};
+  a.in = (const bf16_t*)in, a.out = (bf16_t*)out, a.n0 = -1, a.n1 = nblocks, a.B = B;
+  for (int k = 0; k < 2 * nblocks; ++k) {
+    a.w[k] = (const uint4*)wf16 + k * RF_WCONV;
+    a.b[k] = bias + k * 256;
+  }
+  hipLaunchKernelGGL(rep_trunk_kernel<false>, dim3(B), dim3(rf::NT), 0, stream, a);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+// the representation trunk at 16x20 in one launch (see above): in [B][320][64] bf16 NHWC (the
+// representation input, 2L = 64 channels), out [B][320][256] bf16 NHWC (distinct); w / b: host arrays of
+// the 2 n0 + 2 + 2 n1 convs' device pointers in network order (stem 64 -> 128, the n0 blocks' conv1 /
+// conv2 at 128, the widening conv 128 -> 256, the n1 blocks' at 256): each weight in the tower packing,
+// the last followed by the ring's 8 KB overrun; each bias [Cout] f32 (BN folded into the block convs)
+int mzba_rep_trunk(const void* in, void* out, const void* const* w, const float* const* b, int n0, int n1, int B,
+                   hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && n0 >= 0 && n1 >= 0 && 2 * n0 + 2 + 2 * n1 <= rf::MAXC && in && out && w && b && in != out, -1);
+  RFArgs a{};
+  a.in = (const bf16_t*)in, a.out = (bf16_t*)out, a.n0 = n0, a.n1 = n1, a.B = B;
+  for (int k = 0; k < 2 * n0 + 2 + 2 * n1; ++k) {
+    MZ_CHECK_ARG(w[k] && b[k], -1);
+    a.w[k] = (const uint4*)w[k];
+    a.b[k] = b[k];
+  }
+  hipLaunchKernelGGL(rep_trunk_kernel<true>, dim3(B), dim3(rf::NT), 0, stream, a);
   MZ_LAUNCH_CHECK();
   return 0;
 }

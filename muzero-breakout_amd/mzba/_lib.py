@@ -45,6 +45,7 @@ SIGNATURES = {
     "mzba_tower_fused": [P, LL, P, LL, P, P, P, I, I, P, P],
     "mzba_rep_tail": [P, P, P, LL, P, P, I, I, P],
     "mzba_rep_blocks": [P, P, P, P, I, I, P],
+    "mzba_rep_trunk": [P, P, P, P, I, I, I, P],
     "mzba_conv_band_supported": [I, I, I, I, I],
     "mzba_conv_band_set_xt": [I],
     "mzba_replay_plan": [P, P, P, P, P, P, P, I, I, I, I, I, P, P, P, P],

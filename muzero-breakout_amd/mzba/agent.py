@@ -385,7 +385,8 @@ class NetRunner:
     `mz.NetRunner` (csrc/net_ops.cpp), whose torch custom ops run every launch on torch's current
     stream — representation_ / dynamics_ / prediction_ / prediction_tree_ (`torch.ops.mz`)."""
 
-    FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail", "use_band_res", "use_rep_blocks")
+    FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail", "use_band_res", "use_rep_blocks",
+             "use_rep_trunk")
 
     def __init__(self, packed, B, H, W):
         self.p = packed
@@ -398,7 +399,8 @@ class NetRunner:
 
     # kernel switches (tests / A-B runs): use_lat, use_tower, use_fused, use_band, use_rep_tail,
     # use_band_res (the representation's 16x20 residual blocks as one launch each), use_rep_blocks (the
-    # 256-channel 16x20 blocks as one launch, whole images LDS-resident)
+    # 256-channel 16x20 blocks as one launch, whole images LDS-resident), use_rep_trunk (everything
+    # before the first pool as one launch: stem, 128-channel blocks, widening conv, 256-channel blocks)
     def __getattr__(self, k):
         if k in NetRunner.FLAGS:
             return self.native.get_flag(k)

@@ -62,14 +62,17 @@ def main():
             launch = lambda: rn.prediction(src, pi, v, plg, vlg)  # noqa: E731
         pro = mode == "dyn"
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    nrow = PST_WG * 4
+    prev = np.zeros((nrow, PST_N), dtype=np.uint64)
     for it in range(30):
         if it == 29:
+            torch.cuda.synchronize()
+            assert D.mzba_towerp_stamps_read(prev.ctypes.data, nrow) == 0  # launch 28's stamps
             ev[0].record()
         launch()
     ev[1].record()
     torch.cuda.synchronize()
     wall_us = ev[0].elapsed_time(ev[1]) * 1e3
-    nrow = PST_WG * 4
     st = np.zeros((nrow, PST_N), dtype=np.uint64)
     assert D.mzba_towerp_stamps_read(st.ctypes.data, nrow) == 0
     st = st.astype(np.int64)
@@ -99,6 +102,21 @@ def main():
            "kernel_cycles": med(0, PST_N - 1), "clock_ghz_median": float(np.median(clk)),
            "launch_wall_us": wall_us,
            "realtime_span_us": float((st[:, PST_N - 2].max() - st[:, PST_N - 3].min()) / 100.0)}
+    # per-workgroup spread (s_memrealtime, 100 MHz): dispatch skew of the entries, each workgroup's
+    # duration, the tail of the exits; and whether the slow workgroups are the same in two launches (a
+    # systematic tail — slower CUs or XCDs — survives a persistent kernel, a random one averages out)
+    def wg(stamps):
+        s_ = stamps.astype(np.int64).reshape(PST_WG, 4, PST_N)
+        ent, ext = s_[:, :, PST_N - 3].min(1), s_[:, :, PST_N - 2].max(1)
+        return (ent - ent.min()) / 100.0, (ext - ent.min()) / 100.0, (ext - ent) / 100.0
+    ent, ext, dur = wg(st)
+    _, _, dur0 = wg(prev)
+    pc = lambda a: {f"p{q}": float(np.percentile(a, q)) for q in (0, 50, 90, 99, 100)}  # noqa: E731
+    xcd = [float(np.mean(dur[i::8])) for i in range(8)]
+    res["workgroups"] = {"entry_skew_us": pc(ent), "duration_us": pc(dur), "exit_us": pc(ext),
+                         "duration_by_xcd_us": xcd,
+                         "duration_corr_with_previous_launch": float(np.corrcoef(dur, dur0)[0, 1]),
+                         "previous_launch_duration_us": pc(dur0)}
     if mode != "plain":
         e = [160, 161, 162, 163, 164]
         last = 2 + 5 * (nconv - 1) + 4
