@@ -113,8 +113,13 @@ def main():
     _, _, dur0 = wg(prev)
     pc = lambda a: {f"p{q}": float(np.percentile(a, q)) for q in (0, 50, 90, 99, 100)}  # noqa: E731
     xcd = [float(np.mean(dur[i::8])) for i in range(8)]
+    # the same per XCD in core cycles (s_memtime, wave 0) and the clock they imply: equal cycles at
+    # different durations = the XCDs' clocks differ; different cycles = memory-side differences
+    cyc = (st.astype(np.int64).reshape(PST_WG, 4, PST_N)[:, 0, PST_N - 1] - st.astype(np.int64).reshape(PST_WG, 4, PST_N)[:, 0, 0])
+    xcd_cyc = [float(np.mean(cyc[i::8])) for i in range(8)]
+    xcd_clk = [c / d / 1e3 for c, d in zip(xcd_cyc, xcd)]
     res["workgroups"] = {"entry_skew_us": pc(ent), "duration_us": pc(dur), "exit_us": pc(ext),
-                         "duration_by_xcd_us": xcd,
+                         "duration_by_xcd_us": xcd, "cycles_by_xcd": xcd_cyc, "clock_ghz_by_xcd": xcd_clk,
                          "duration_corr_with_previous_launch": float(np.corrcoef(dur, dur0)[0, 1]),
                          "previous_launch_duration_us": pc(dur0)}
     if mode != "plain":
