@@ -257,7 +257,7 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
 /* Pixel-tiled tower kernel (csrc/towerp.hip; plan 4 of mzba_tower / mzba_tower_fused): 16 envs per
  * workgroup, one 16-row MFMA tile per latent pixel, so the 3x3 taps that fall on the 4x5 latent's
  * zero padding are never issued; bit-identical to plans 2/3 on the same weight packing and I/O
- * layout. mzba_towerp_fused takes mzba_tower_fused's arguments (bf16 only: ext->elem == 0);
+ * layout. mzba_towerp_fused takes mzba_tower_fused's arguments (bf16, or ext->elem == 1: the fp16 dynamics net);
  * mzba_towerp is the plain tower (mzba_tower's arguments without the workspace). */
 int mzba_towerp_fused(const void* in, long long in_env_stride, const int32_t* slot, long long in_slot_stride,
                       void* out, const void* wf16, const float* bias, int nblocks, int B,

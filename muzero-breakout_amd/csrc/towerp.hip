@@ -28,9 +28,12 @@
 //     accumulator layout and parks it in a per-wave global scratch (40 x 1 KB per wave,
 //     L2 / Infinity-Cache resident), and the same lanes load it back before the barrier that
 //     ends conv1, so it lands while conv2's accumulators are initialised.
-// The kernel fills one CU per workgroup: B = 4096 is exactly one round on 256 CUs.
+// The kernel fills one CU per workgroup: B = 4096 is exactly one round on 256 CUs. EL (elt.h): bf16, or fp16
+// for the fp16 dynamics net of config 5 (fp16 image, weights and MFMAs; latents in and out of HBM stay bf16,
+// converted on staging and in the epilogues, as tower8_kernel<1, NQ>, bit for bit).
 #include "common.h"
 #include "tree_dev.h"
+#include "elt.h"  // Elt<EL>: bf16 (EL 0) / fp16 (EL 1, the fp16 dynamics net of config 5) images and weights
 
 #ifndef TP_SCHED
 #define TP_SCHED 1  // k-loop schedule (make towerp-sched builds the others): 1 the current fragments' MFMAs first, then the next reads
@@ -40,9 +43,6 @@
 #endif
 
 namespace {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 namespace tp {
 constexpr int E = 16;                  // envs per workgroup
@@ -57,11 +57,9 @@ constexpr int CT = 4;                  // column tiles per wave (64 output chann
 constexpr int TNS = 72;                // pack k steps per column tile of a 3x3 conv
 constexpr int CTB = TNS * 1024;        // bytes per column tile of a 3x3 pack
 MZ_DEV int off(int row, int chunk) { return row * ROWB + ((chunk ^ (row & 15)) << 4); }
-MZ_DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
-MZ_DEV float lo(uint32_t u) { return __uint_as_float(u << 16); }
-MZ_DEV float hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
-// ReLU on two packed bf16 (signed 16-bit max with 0 clears negatives and -0): relu(round(x)) ==
-// round(relu(x)) for round-to-nearest, so this is the f32 ReLU before the conversion, bit for bit
+// ReLU on two packed bf16 / fp16 (the sign bit is the int16 sign: a signed 16-bit max with 0 clears
+// negatives and -0): relu(round(x)) == round(relu(x)) for round-to-nearest, so this is the f32 ReLU
+// before the conversion, bit for bit
 MZ_DEV uint32_t relu_pk(uint32_t u) {
   uint32_t r;
   asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(u));
@@ -124,10 +122,11 @@ MZ_DEV void tp_preload(uint4 (&bq)[2][3][2], const TPW& w, int lane) {
 // row y' at lds + lb + xo(c) + (5 y' + x') PIX with xo(c) = ((4c + q) ^ n) << 4 (lane row n, k
 // quarter q). fa holds the first row step's fragments on entry and the next dy's first on exit
 // (after dy = +1: the pass's own first ones again, i.e. the next pass's if the image is unchanged).
-template <int DYI>
+template <int EL, int DYI>
 __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, int q, int n, const TPW& cur,
                                       const TPW& nxt, uint4 (&bq)[2][3][2], f32x4 (&acc)[tp::P][2],
-                                      bf16x8 (&fa)[5], bf16x8 (&fb)[5], int lane) {
+                                      typename Elt<EL>::v8 (&fa)[5], typename Elt<EL>::v8 (&fb)[5], int lane) {
+  typedef typename Elt<EL>::v8 V8;
   constexpr int DY = DYI - 1;
   constexpr int YLO = DY < 0 ? 0 : DY, YHI = DY > 0 ? 3 : 3 + DY, NY = YHI - YLO + 1;
   constexpr int NYLO = DYI == 0 ? 0 : (DYI == 1 ? 1 : 0);  // first input row of the next dy loop
@@ -152,27 +151,27 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
         const int yp = YLO + yi;
         const int nb = yi + 1 < NY ? xc + 5 * (yp + 1) * tp::PIX : xn + 5 * ynext * tp::PIX;
         const bool last = yi == NY - 1;
-        auto row = [&](const bf16x8(&f)[5], bf16x8(&fn)[5]) {
+        auto row = [&](const V8(&f)[5], V8(&fn)[5]) {
 #pragma unroll
           for (int ct = 0; ct < 2; ++ct) {
-            const bf16x8 w0 = __builtin_bit_cast(bf16x8, bq[cc][0][ct]);
-            const bf16x8 w1 = __builtin_bit_cast(bf16x8, bq[cc][1][ct]);
-            const bf16x8 w2 = __builtin_bit_cast(bf16x8, bq[cc][2][ct]);
+            const V8 w0 = __builtin_bit_cast(V8, bq[cc][0][ct]);
+            const V8 w1 = __builtin_bit_cast(V8, bq[cc][1][ct]);
+            const V8 w2 = __builtin_bit_cast(V8, bq[cc][2][ct]);
             // dx = 0 first (its 5 MFMA slots carry the next row step's 5 reads), then dx = -1
             // (input x' feeds output x' + 1) and dx = +1 (output x' - 1)
 #pragma unroll
             for (int xp = 0; xp < 5; ++xp) {
-              acc[(yp - DY) * 5 + xp][ct] = tp::mfma(w1, f[xp], acc[(yp - DY) * 5 + xp][ct]);
+              acc[(yp - DY) * 5 + xp][ct] = Elt<EL>::mfma(w1, f[xp], acc[(yp - DY) * 5 + xp][ct]);
 #if TP_ABLATE == 1  // diagnostic only: no LDS B reads in the k loop (the fragments are reused)
               if (ct == 0) fn[xp] = f[xp];
 #else
-              if (ct == 0) fn[xp] = *reinterpret_cast<const bf16x8*>(lds + nb + xp * tp::PIX);
+              if (ct == 0) fn[xp] = *reinterpret_cast<const V8*>(lds + nb + xp * tp::PIX);
 #endif
             }
 #pragma unroll
-            for (int xp = 0; xp < 4; ++xp) acc[(yp - DY) * 5 + xp + 1][ct] = tp::mfma(w0, f[xp], acc[(yp - DY) * 5 + xp + 1][ct]);
+            for (int xp = 0; xp < 4; ++xp) acc[(yp - DY) * 5 + xp + 1][ct] = Elt<EL>::mfma(w0, f[xp], acc[(yp - DY) * 5 + xp + 1][ct]);
 #pragma unroll
-            for (int xp = 1; xp < 5; ++xp) acc[(yp - DY) * 5 + xp - 1][ct] = tp::mfma(w2, f[xp], acc[(yp - DY) * 5 + xp - 1][ct]);
+            for (int xp = 1; xp < 5; ++xp) acc[(yp - DY) * 5 + xp - 1][ct] = Elt<EL>::mfma(w2, f[xp], acc[(yp - DY) * 5 + xp - 1][ct]);
             if (last) {
 #pragma unroll
               for (int d = 0; d < 3; ++d)
@@ -254,7 +253,7 @@ struct TPArgs {
 // Accumulator init of one pixel of a pass; its channels are chb + 16 ct + 4q + i of the lane's row
 // (pixel p, env n). MODE 0: bias; 1: bias + res (bf16 residual in registers); 2: bias + the dynamics
 // action bias table act_bias[pixel][act][256] (the one-hot action planes folded, tower.hip MODE 2).
-template <int MODE>
+template <int EL, int MODE>
 MZ_DEV void tp_init1(f32x4 (&acc)[2], const float4 (&bias)[2], int chb, const uint2 (&res)[2],
                      const float* __restrict__ actb, int act, int A, int q, int p) {
 #pragma unroll
@@ -264,8 +263,8 @@ MZ_DEV void tp_init1(f32x4 (&acc)[2], const float4 (&bias)[2], int chb, const ui
     f32x4 v = {b4.x, b4.y, b4.z, b4.w};
     if (MODE == 1) {
       const uint2 r = res[ct];
-      v[0] += tp::lo(r.x); v[1] += tp::hi(r.x);
-      v[2] += tp::lo(r.y); v[3] += tp::hi(r.y);
+      v[0] += Elt<EL>::lo(r.x); v[1] += Elt<EL>::hi(r.x);
+      v[2] += Elt<EL>::lo(r.y); v[3] += Elt<EL>::hi(r.y);
     } else if (MODE == 2) {
       const float4 t = *reinterpret_cast<const float4*>(actb + ((size_t)p * A + act) * tp::C + ch);
       v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
@@ -273,11 +272,11 @@ MZ_DEV void tp_init1(f32x4 (&acc)[2], const float4 (&bias)[2], int chb, const ui
     acc[ct] = v;
   }
 }
-template <int MODE>
+template <int EL, int MODE>
 MZ_DEV void tp_init(f32x4 (&acc)[tp::P][2], const float4 (&bias)[2], int chb, const uint2 (&res)[tp::P][2],
                     const float* __restrict__ actb, int act, int A, int q) {
 #pragma unroll
-  for (int p = 0; p < tp::P; ++p) tp_init1<MODE>(acc[p], bias, chb, res[p], actb, act, A, q, p);
+  for (int p = 0; p < tp::P; ++p) tp_init1<EL, MODE>(acc[p], bias, chb, res[p], actb, act, A, q, p);
 }
 // the initialised accumulators pinned to AGPRs before a k loop (left to the allocator the loop-carried
 // accumulators move between the register files on every iteration)
@@ -295,17 +294,21 @@ MZ_DEV void tp_bias(float4 (&b)[2], const float* __restrict__ bias, int chb, int
 }
 
 // k loop of a 3x3 pass (weights in the ring, fa = its first fragments)
+template <int EL>
 MZ_DEV void tp_k3(const uint8_t* __restrict__ lds, int lb, int q, int n, const TPW& cur, const TPW& nxt,
-                  uint4 (&bq)[2][3][2], bf16x8 (&fa)[5], bf16x8 (&fb)[5], f32x4 (&acc)[tp::P][2], int lane) {
-  tp_dy<0>(lds, lb, q, n, cur, nxt, bq, acc, fa, fb, lane);
-  tp_dy<1>(lds, lb, q, n, cur, nxt, bq, acc, fa, fb, lane);
-  tp_dy<2>(lds, lb, q, n, cur, nxt, bq, acc, fa, fb, lane);
+                  uint4 (&bq)[2][3][2], typename Elt<EL>::v8 (&fa)[5], typename Elt<EL>::v8 (&fb)[5],
+                  f32x4 (&acc)[tp::P][2], int lane) {
+  tp_dy<EL, 0>(lds, lb, q, n, cur, nxt, bq, acc, fa, fb, lane);
+  tp_dy<EL, 1>(lds, lb, q, n, cur, nxt, bq, acc, fa, fb, lane);
+  tp_dy<EL, 2>(lds, lb, q, n, cur, nxt, bq, acc, fa, fb, lane);
 }
 
 // k loop of a 1x1 pass (centre tap: every pixel tile, 8 channel steps); the pack has 8 k steps per
 // column tile, the pass's two tiles at w (loaded here: an epilogue conv, once per launch)
+template <int EL>
 MZ_DEV void tp_k1(const uint8_t* __restrict__ lds, int lb, int q, int n, const TPW& w, f32x4 (&acc)[tp::P][2],
                   int lane) {
+  typedef typename Elt<EL>::v8 V8;
   uint4 wq[8][2];
 #pragma unroll
   for (int c = 0; c < 8; ++c)
@@ -317,28 +320,30 @@ MZ_DEV void tp_k1(const uint8_t* __restrict__ lds, int lb, int q, int n, const T
     const int xc = lb + (((4 * c + q) ^ n) << 4);
 #pragma unroll
     for (int yp = 0; yp < 4; ++yp) {
-      bf16x8 f[5];
+      V8 f[5];
 #pragma unroll
-      for (int xp = 0; xp < 5; ++xp) f[xp] = *reinterpret_cast<const bf16x8*>(lds + xc + (5 * yp + xp) * tp::PIX);
+      for (int xp = 0; xp < 5; ++xp) f[xp] = *reinterpret_cast<const V8*>(lds + xc + (5 * yp + xp) * tp::PIX);
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
         for (int xp = 0; xp < 5; ++xp)
-          acc[5 * yp + xp][ct] = tp::mfma(__builtin_bit_cast(bf16x8, wq[c][ct]), f[xp], acc[5 * yp + xp][ct]);
+          acc[5 * yp + xp][ct] = Elt<EL>::mfma(__builtin_bit_cast(V8, wq[c][ct]), f[xp], acc[5 * yp + xp][ct]);
     }
   }
 }
 
+template <int EL>
 MZ_DEV uint2 tp_pack(const f32x4& a) {
-  return make_uint2(tp::relu_pk(pack_bf16x2(a[0], a[1])), tp::relu_pk(pack_bf16x2(a[2], a[3])));
+  return make_uint2(tp::relu_pk(Elt<EL>::pack2(a[0], a[1])), tp::relu_pk(Elt<EL>::pack2(a[2], a[3])));
 }
 // byte offset (in the image) of the lane's 4 channels ch..ch+3 of pixel 0, row n
 MZ_DEV int tp_cofs(int ch, int n) { return n * tp::ROWB + (((ch >> 3) ^ n) << 4) + ((ch & 7) << 1); }
 
-MZ_DEV void tp_first_frags(const uint8_t* __restrict__ lds, int lb, int q, int n, bf16x8 (&fa)[5]) {
+template <int EL>
+MZ_DEV void tp_first_frags(const uint8_t* __restrict__ lds, int lb, int q, int n, typename Elt<EL>::v8 (&fa)[5]) {
   const int x0 = lb + ((q ^ n) << 4);  // dy = -1: first input row y' = 0, channel step 0
 #pragma unroll
-  for (int xp = 0; xp < 5; ++xp) fa[xp] = *reinterpret_cast<const bf16x8*>(lds + x0 + xp * tp::PIX);
+  for (int xp = 0; xp < 5; ++xp) fa[xp] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + x0 + xp * tp::PIX);
 }
 
 // One 3x3 256 -> 256 conv, in place: two passes (the wave's column tiles 0-1, then 2-3), barrier,
@@ -347,7 +352,7 @@ MZ_DEV void tp_first_frags(const uint8_t* __restrict__ lds, int lb, int q, int n
 // w: this conv's pack; wn: where the ring goes after it (the next conv's first pass). bc holds this
 // conv's pass-0 bias on entry and the next conv's (nbias) on exit; every bias is loaded one pass
 // ahead, so no pass starts with a global round trip.
-template <int MODE, bool SAVE>
+template <int EL, int MODE, bool SAVE>
 __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* w, const TPW& wn,
                                         const float* __restrict__ bias, float4 (&bc)[2], const float* __restrict__ nbias,
                                         uint2 (&res)[2][tp::P][2],
@@ -358,15 +363,15 @@ __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* 
   const int ct0 = tp::CT * wave;
   const TPW w0 = tpw(w, ct0), w1 = tpw(w, ct0 + 2);
   PSTAMP(2 + 5 * ci);
-  bf16x8 fa[5], fb[5];
-  tp_first_frags(lds, lb, q, n, fa);
+  typename Elt<EL>::v8 fa[5], fb[5];
+  tp_first_frags<EL>(lds, lb, q, n, fa);
   uint2 out0[tp::P][2];
   f32x4 acc[tp::P][2];
-  tp_init<MODE>(acc, bc, 64 * wave, res[0], actb, act, A, q);
+  tp_init<EL, MODE>(acc, bc, 64 * wave, res[0], actb, act, A, q);
   tp_pin(acc);
   float4 b1[2];  // pass 1's bias, loaded ahead of pass 0's k loop
   tp_bias(b1, bias, 64 * wave + 32, q);
-  tp_k3(lds, lb, q, n, w0, w1, bq, fa, fb, acc, lane);
+  tp_k3<EL>(lds, lb, q, n, w0, w1, bq, fa, fb, acc, lane);
   PSTAMP(3 + 5 * ci);
   // pass 0's accumulators out (ReLU, bf16, held in registers until the write-back) and pass 1's in,
   // pixel by pixel: each pixel's residual registers are freed as its packed output appears, so the
@@ -375,13 +380,13 @@ __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* 
 #pragma unroll
   for (int p = 0; p < tp::P; ++p) {
 #pragma unroll
-    for (int ct = 0; ct < 2; ++ct) out0[p][ct] = tp_pack(acc[p][ct]);
-    tp_init1<MODE>(acc[p], b1, 64 * wave + 32, res[1][p], actb, act, A, q, p);
+    for (int ct = 0; ct < 2; ++ct) out0[p][ct] = tp_pack<EL>(acc[p][ct]);
+    tp_init1<EL, MODE>(acc[p], b1, 64 * wave + 32, res[1][p], actb, act, A, q, p);
     __builtin_amdgcn_sched_barrier(0);
   }
   tp_pin(acc);
   tp_bias(bc, nbias, 64 * wave, q);  // the next conv's pass-0 bias, ahead of pass 1's k loop
-  tp_k3(lds, lb, q, n, w1, wn, bq, fa, fb, acc, lane);
+  tp_k3<EL>(lds, lb, q, n, w1, wn, bq, fa, fb, acc, lane);
   PSTAMP(4 + 5 * ci);
   __syncthreads();  // every wave has read the whole image
   PSTAMP(5 + 5 * ci);
@@ -396,7 +401,7 @@ __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* 
     for (int ct = 0; ct < tp::CT; ++ct) {
       uint2* ptr = reinterpret_cast<uint2*>(lds + p * tp::PIX + cofs[ct]);
       if (SAVE) res[ct >> 1][p][ct & 1] = *ptr;
-      *ptr = ct < 2 ? out0[p][ct] : tp_pack(acc[p][ct - 2]);
+      *ptr = ct < 2 ? out0[p][ct] : tp_pack<EL>(acc[p][ct - 2]);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -414,27 +419,28 @@ constexpr int TPH_PART = 0, TPH_LG = 2048, TPH_DEC = 2560, TPH_TAB = 2688;  // f
 // NH heads over channel widths C0 / C1: every weight fragment of the wave (its k steps wave + 4u of
 // each head, 40 in all) is loaded in one batch before the first MFMA — one L2 round trip instead of
 // one per 10-step batch; the MFMAs run in tower_heads' order (k steps ascending per head)
-template <int NH, int C0, int C1>
+template <int EL, int NH, int C0, int C1>
 MZ_DEV void tp_heads(const TPArgs& a, uint8_t* __restrict__ lds, const int (&hc0)[2], const int (&kind)[2], int env0,
                      int nenv, int tid) {
   constexpr int NU0 = 20 * C0 / 32 / 4, NU1 = NH > 1 ? 20 * C1 / 32 / 4 : 0, NU = NU0 + NU1;
   static_assert(NU <= 40, "head weight batch");
   const int nh = NH;
   const int lane = tid & 63, wave = tid >> 6, q = lane >> 4, el = lane & 15;
+  typedef typename Elt<EL>::v8 V8;
   f32x4 hacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  bf16x8 bv[NU];
+  V8 bv[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int hd = u < NU0 ? 0 : 1, K = 20 * (hd ? C1 : C0), s = wave + 4 * (hd ? u - NU0 : u);
-    bv[u] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(a.x.lw[hd]) + (size_t)el * K + s * 32 + q * 8);
+    bv[u] = *reinterpret_cast<const V8*>(reinterpret_cast<const bf16_t*>(a.x.lw[hd]) + (size_t)el * K + s * 32 + q * 8);
   }
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int hd = u < NU0 ? 0 : 1, C = hd ? C1 : C0, s = wave + 4 * (hd ? u - NU0 : u);
     const int k = s * 32 + q * 8;
     const int pos = k / C, c = hc0[hd] + (k - pos * C);
-    const bf16x8 av = *reinterpret_cast<const bf16x8*>(lds + tp::off(pos * tp::E + el, c >> 3));
-    hacc[hd] = tp::mfma(av, bv[u], hacc[hd]);
+    const V8 av = *reinterpret_cast<const V8*>(lds + tp::off(pos * tp::E + el, c >> 3));
+    hacc[hd] = Elt<EL>::mfma(av, bv[u], hacc[hd]);
   }
   __syncthreads();  // the image is dead: LDS becomes head scratch
   float* sc = reinterpret_cast<float*>(lds);
@@ -485,6 +491,7 @@ MZ_DEV void tp_heads(const TPArgs& a, uint8_t* __restrict__ lds, const int (&hc0
 
 // _scale_state (networks.py:314-328) of the image: per env (h - min) / (max - min + 1e-8) in f32,
 // bf16 to out (and the node-pool slot); 16 threads per env, 40 chunks each
+template <int EL>
 MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0, int nenv, int tid) {
   const int e = tid >> 4, t = tid & 15;
   float mn = INFINITY, mx = -INFINITY;
@@ -494,8 +501,8 @@ MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0,
     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      mn = fminf(mn, tp::lo(w4[j])); mx = fmaxf(mx, tp::lo(w4[j]));
-      mn = fminf(mn, tp::hi(w4[j])); mx = fmaxf(mx, tp::hi(w4[j]));
+      mn = fminf(mn, Elt<EL>::lo(w4[j])); mx = fmaxf(mx, Elt<EL>::lo(w4[j]));
+      mn = fminf(mn, Elt<EL>::hi(w4[j])); mx = fmaxf(mx, Elt<EL>::hi(w4[j]));
     }
   }
   for (int o = 8; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
@@ -516,7 +523,8 @@ MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0,
   for (int u = 0; u < 40; ++u) {
     const int i = u * 16 + t, p = i >> 5, c = i & 31;
     const uint4 v = *reinterpret_cast<const uint4*>(lds + tp::off(p * tp::E + e, c));
-    float f[8] = {tp::lo(v.x), tp::hi(v.x), tp::lo(v.y), tp::hi(v.y), tp::lo(v.z), tp::hi(v.z), tp::lo(v.w), tp::hi(v.w)};
+    float f[8];
+    unpack8<EL>(v, f);
     const uint4 r = make_uint4(pack_bf16x2(dv(f[0]), dv(f[1])), pack_bf16x2(dv(f[2]), dv(f[3])),
                                pack_bf16x2(dv(f[4]), dv(f[5])), pack_bf16x2(dv(f[6]), dv(f[7])));
     *reinterpret_cast<uint4*>(o1 + p * tp::C + c * 8) = r;
@@ -524,6 +532,7 @@ MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0,
   }
 }
 
+template <int EL>
 __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[tp::IMG];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -555,7 +564,7 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
       const long long eo = (long long)b * a.in_env_stride + (a.slot ? (long long)a.slot[b] * a.in_slot_stride : 0);
 #pragma unroll
       for (int u = 0; u < 10; ++u) {
-        v[bb * 10 + u] = *reinterpret_cast<const uint4*>(a.in + eo + (long long)(u * 64 + lane) * 8);
+        v[bb * 10 + u] = Elt<EL>::from_bf16(*reinterpret_cast<const uint4*>(a.in + eo + (long long)(u * 64 + lane) * 8));
         if (!ok) v[bb * 10 + u] = make_uint4(0, 0, 0, 0);
       }
     }
@@ -579,15 +588,15 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
   float4 bc[2];
   tp_bias(bc, pro ? a.x.b0 : a.bias, 64 * wave, q);
   if (pro)  // dynamics ConvBlock 259 -> 256 (in place)
-    tp_conv<2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), tpw(wf, ct0), a.x.b0, bc, a.bias, res, a.x.act_bias,
+    tp_conv<EL, 2, false>(lds, reinterpret_cast<const uint4*>(a.x.w0), tpw(wf, ct0), a.x.b0, bc, a.bias, res, a.x.act_bias,
                       act, a.x.A, bq, lane, wave, 0);
   const int ci0 = pro ? 1 : 0;
   for (int blk = 0; blk < a.nblocks; ++blk) {
     const int k1 = 2 * blk, k2 = k1 + 1;
     const TPW w3 = k2 + 1 < nconv ? tpw(wf + (k2 + 1) * WCONV, ct0) : after;
-    tp_conv<0, true>(lds, wf + k1 * WCONV, tpw(wf + k2 * WCONV, ct0), a.bias + k1 * tp::C, bc, a.bias + k2 * tp::C, res,
+    tp_conv<EL, 0, true>(lds, wf + k1 * WCONV, tpw(wf + k2 * WCONV, ct0), a.bias + k1 * tp::C, bc, a.bias + k2 * tp::C, res,
                      nullptr, 0, 0, bq, lane, wave, ci0 + k1);
-    tp_conv<1, false>(lds, wf + k2 * WCONV, w3, a.bias + k2 * tp::C, bc, a.bias + (k2 + 1 < nconv ? k2 + 1 : k2) * tp::C,
+    tp_conv<EL, 1, false>(lds, wf + k2 * WCONV, w3, a.bias + k2 * tp::C, bc, a.bias + (k2 + 1 < nconv ? k2 + 1 : k2) * tp::C,
                       res, nullptr, 0, 0, bq, lane, wave, ci0 + k2);
   }
   if (a.x.epilogue == 1) {  // dynamics: reward ConvBlock1x1, the scaled latent from X, then Linear + decode
@@ -596,23 +605,23 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
       f32x4 acc[tp::P][2];
       float4 b4[2];
       tp_bias(b4, a.x.be1, 64 * wave, q);
-      tp_init<0>(acc, b4, 64 * wave, res[0], nullptr, 0, 0, q);
+      tp_init<EL, 0>(acc, b4, 64 * wave, res[0], nullptr, 0, 0, q);
       tp_pin(acc);
-      tp_k1(lds, lb, q, n, tpw1(a.x.we1, ct0), acc, lane);
+      tp_k1<EL>(lds, lb, q, n, tpw1(a.x.we1, ct0), acc, lane);
 #pragma unroll
       for (int p = 0; p < tp::P; ++p)
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct) out0[p][ct] = tp_pack(acc[p][ct]);
+        for (int ct = 0; ct < 2; ++ct) out0[p][ct] = tp_pack<EL>(acc[p][ct]);
     }
     f32x4 acc[tp::P][2];
     float4 b4[2];
     tp_bias(b4, a.x.be1, 64 * wave + 32, q);
-    tp_init<0>(acc, b4, 64 * wave + 32, res[0], nullptr, 0, 0, q);
+    tp_init<EL, 0>(acc, b4, 64 * wave + 32, res[0], nullptr, 0, 0, q);
     tp_pin(acc);
-    tp_k1(lds, lb, q, n, tpw1(a.x.we1, ct0 + 2), acc, lane);
+    tp_k1<EL>(lds, lb, q, n, tpw1(a.x.we1, ct0 + 2), acc, lane);
     PSTAMP(160);
     __syncthreads();
-    tp_scale(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
+    tp_scale<EL>(a, lds, env0, nenv, tid);  // reads X before the reward conv output replaces it
     __syncthreads();
     PSTAMP(161);
 #pragma unroll
@@ -620,11 +629,11 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
 #pragma unroll
       for (int ct = 0; ct < tp::CT; ++ct)
         *reinterpret_cast<uint2*>(lds + p * tp::PIX + tp_cofs(64 * wave + 16 * ct + 4 * q, n)) =
-            ct < 2 ? out0[p][ct] : tp_pack(acc[p][ct - 2]);
+            ct < 2 ? out0[p][ct] : tp_pack<EL>(acc[p][ct - 2]);
     __syncthreads();
     const int hc0[2] = {0, 0}, kind[2] = {1, 0};
     PSTAMP(162);
-    tp_heads<1, tp::C, 0>(a, lds, hc0, kind, env0, nenv, tid);
+    tp_heads<EL, 1, tp::C, 0>(a, lds, hc0, kind, env0, nenv, tid);
     PSTAMP(163);
 #ifdef TOWERP_STAMPS
     pstamp(PST_N - 2, true);
@@ -637,26 +646,26 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
     uint2 pol[tp::P][2];
     {
       f32x4 acc[tp::P][2];
-      bf16x8 fa[5], fb[5];
-      tp_first_frags(lds, lb, q, n, fa);
+      typename Elt<EL>::v8 fa[5], fb[5];
+      tp_first_frags<EL>(lds, lb, q, n, fa);
       float4 b4[2];
       tp_bias(b4, a.x.be3, 32 * wave, q);
-      tp_init<0>(acc, b4, 32 * wave, res[0], nullptr, 0, 0, q);
+      tp_init<EL, 0>(acc, b4, 32 * wave, res[0], nullptr, 0, 0, q);
       tp_pin(acc);
       const TPW wp = tpw(a.x.we3, 2 * wave);
-      tp_k3(lds, lb, q, n, wp, wp, bq, fa, fb, acc, lane);
+      tp_k3<EL>(lds, lb, q, n, wp, wp, bq, fa, fb, acc, lane);
       PSTAMP(160);
 #pragma unroll
       for (int p = 0; p < tp::P; ++p)
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct) pol[p][ct] = tp_pack(acc[p][ct]);
+        for (int ct = 0; ct < 2; ++ct) pol[p][ct] = tp_pack<EL>(acc[p][ct]);
     }
     f32x4 acc[tp::P][2];
     float4 b4[2];
     tp_bias(b4, a.x.be1, 32 * wave, q);
-    tp_init<0>(acc, b4, 32 * wave, res[0], nullptr, 0, 0, q);
+    tp_init<EL, 0>(acc, b4, 32 * wave, res[0], nullptr, 0, 0, q);
     tp_pin(acc);
-    tp_k1(lds, lb, q, n, tpw1(a.x.we1, 2 * wave), acc, lane);
+    tp_k1<EL>(lds, lb, q, n, tpw1(a.x.we1, 2 * wave), acc, lane);
     PSTAMP(161);
     __syncthreads();
 #pragma unroll
@@ -664,7 +673,7 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
         *reinterpret_cast<uint2*>(lds + p * tp::PIX + tp_cofs(32 * wave + 16 * ct + 4 * q, n)) = pol[p][ct];
-        *reinterpret_cast<uint2*>(lds + p * tp::PIX + tp_cofs(128 + 32 * wave + 16 * ct + 4 * q, n)) = tp_pack(acc[p][ct]);
+        *reinterpret_cast<uint2*>(lds + p * tp::PIX + tp_cofs(128 + 32 * wave + 16 * ct + 4 * q, n)) = tp_pack<EL>(acc[p][ct]);
       }
     __syncthreads();
     const int ntab = a.tree.S + 1;
@@ -673,7 +682,7 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
     if (tab_lds && tid < ntab) { tsq = a.tree.sqrt_tab[tid]; tct = a.tree.c_tab[tid]; }
     const int hc0[2] = {0, 128}, kind[2] = {0, 1};
     PSTAMP(162);
-    tp_heads<2, 128, 128>(a, lds, hc0, kind, env0, nenv, tid);
+    tp_heads<EL, 2, 128, 128>(a, lds, hc0, kind, env0, nenv, tid);
     PSTAMP(163);
     if (a.tree_on) {  // this simulation's backup and the next selection (mcts.py:136-234), per env
       float* sc = reinterpret_cast<float*>(lds);
@@ -704,7 +713,7 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
       for (int u = 0; u < 10; ++u) {
         const int cj = u * 64 + lane;
         *reinterpret_cast<uint4*>(a.out + (long long)(env0 + e) * tp::P * tp::C + (long long)cj * 8) =
-            *reinterpret_cast<const uint4*>(lds + tp::off((cj >> 5) * tp::E + e, cj & 31));
+            Elt<EL>::to_bf16(*reinterpret_cast<const uint4*>(lds + tp::off((cj >> 5) * tp::E + e, cj & 31)));
       }
     }
   }
@@ -732,7 +741,7 @@ int mzba_towerp_fused(const void* in, long long in_env_stride, const int32_t* sl
                       hipStream_t stream) {
   MZ_CHECK_ARG(B > 0 && nblocks >= 1 && in && wf16 && bias && ext, -1);
   const mzba_tower_ext& x = *ext;
-  MZ_CHECK_ARG(x.elem == 0 && x.epilogue >= 0 && x.epilogue <= 2, -2);
+  MZ_CHECK_ARG((x.elem == 0 || x.elem == 1) && x.epilogue >= 0 && x.epilogue <= 2, -2);
   MZ_CHECK_ARG(!x.w0 || (x.b0 && x.act_bias && x.act && x.A > 0), -3);
   MZ_CHECK_ARG(x.epilogue != 0 || out, -3);
   MZ_CHECK_ARG(x.epilogue != 1 || (out && x.we1 && x.be1 && x.lw[0] && x.lb[0] && x.dec[0] && x.lO[0] > 1 &&
@@ -752,7 +761,10 @@ int mzba_towerp_fused(const void* in, long long in_env_stride, const int32_t* sl
     a.tree_gamma = t.gamma;
     a.tree_r = t.r;
   }
-  hipLaunchKernelGGL(towerp_kernel, dim3((B + tp::E - 1) / tp::E), dim3(tp::NT), 0, stream, a);
+  if (x.elem == 1)
+    hipLaunchKernelGGL(towerp_kernel<1>, dim3((B + tp::E - 1) / tp::E), dim3(tp::NT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(towerp_kernel<0>, dim3((B + tp::E - 1) / tp::E), dim3(tp::NT), 0, stream, a);
   MZ_LAUNCH_CHECK();
   return 0;
 }

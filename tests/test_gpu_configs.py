@@ -148,7 +148,7 @@ def test_config5_search_s200_f32_matches_oracle():
 
 def test_config5_acting_step_4096x200_fp16_and_bf16_vs_f32_path():
     """Config 5 end to end: one acting step of 4096 envs x 200 sims with the full-width nets, the
-    dynamics net in fp16 (the config's precision, tower8_kernel<1,2>) and in bf16, each against the
+    dynamics net in fp16 (the config's precision, towerp_kernel<1>) and in bf16, each against the
     same step on the f32 parity path (same state, same keyed noise and tie-breaks). Every count row
     sums to 200.
     Stated bound: reduced-precision rounding in the 2 x 14-block towers moves PUCT decisions that are

@@ -1333,7 +1333,7 @@ def test_test_simulation_matches_oracle():
             np.testing.assert_array_equal(np.stack([f.numpy() for f in frames[b]]), np.stack(oframes[b]))
 
 
-@pytest.mark.parametrize("B,variant", [(64, 1), (64, 3), (2048, 0)])
+@pytest.mark.parametrize("B,variant", [(64, 1), (64, 3), (2048, 0), (4096, 4)])
 def test_fp16_dynamics_step(B, variant):
     """BASELINE config 5's fp16 dynamics net: the fused dynamics step with fp16 LDS images / weights
     / MFMA (latents in and out bf16) against the f32 path of the same weights; its error must not

@@ -52,19 +52,19 @@ def test_towerp_plain_tower_bit_identical_to_tower8(B, nb):
     np.testing.assert_array_equal(a, b)
 
 
-def _agent(seed, cfg=None):
+def _agent(seed, cfg=None, dyn_dtype=None):
     """A fresh agent per kernel: runners (and the plan each fixes at creation) are cached per batch in
     the agent's native pack."""
     from mzba.agent import MuZeroAgent
     mcfg = (cfg or default_config())["model"]
-    ag = MuZeroAgent(mcfg, dtype="bf16")
+    ag = MuZeroAgent(mcfg, dtype="bf16", dyn_dtype=dyn_dtype)
     ag.load_state_dict(init_state_dict(mcfg, seed))
     return ag
 
 
-def _fused(B, variant):
+def _fused(B, variant, dyn_dtype=None):
     from mzba import _lib as L
-    ag = _agent(7)
+    ag = _agent(7, dyn_dtype=dyn_dtype)
     L.call("mzba_tower_set_variant", variant)
     try:
         rn = ag.runner(B, 16, 20)
@@ -149,3 +149,14 @@ def test_towerp_is_the_default_plan_at_16_envs_per_cu():
     assert L.lib().mzba_tower_plan(16 * ncu - 1) == 2
     assert L.lib().mzba_tower_plan(8 * ncu) == 2
     assert L.lib().mzba_tower_plan(8 * ncu - 1) == 3
+
+
+@pytest.mark.parametrize("B", [4096, 13])
+def test_towerp_fp16_dynamics_step_bit_identical_to_tower8(B):
+    """BASELINE config 5's fp16 dynamics net (fp16 LDS image, weights and MFMAs; latents in and out
+    bf16) on the pixel-tiled kernel (towerp_kernel<1>) against tower8_kernel<1, 2>: the fused dynamics
+    step (and the bf16 prediction step after it) equal bit for bit."""
+    a, b = _fused(B, 2, "fp16"), _fused(B, 4, "fp16")
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert np.isfinite(b["r"].view(np.float32)).all()
