@@ -227,7 +227,8 @@ typedef struct mzba_tower_ext {
   int A;
   /* epilogue: 0 none (out = tower output); 1 dynamics: reward ConvBlock1x1 256->256 (we1/be1) +
    * Linear lw[0] -> lO[0] logits -> decode to dec[0][B], then the per-env min-max scaled latent
-   * to out and to pool slot pool_slot; 2 prediction: policy ConvBlock3x3 256->128 (we3/be3) and
+   * to out (may be NULL when pool is set: the node-pool slot is the only copy, as in the search) and
+   * to pool slot pool_slot; 2 prediction: policy ConvBlock3x3 256->128 (we3/be3) and
    * value ConvBlock1x1 256->128 (we1/be1), Linear lw[0] -> softmax dec[0][B][lO[0]],
    * Linear lw[1] -> decode dec[1][B] */
   int epilogue;

@@ -347,10 +347,15 @@ struct NetRunner : torch::CustomClassHolder {
 
   // DynamicsNetwork + _scale_state (networks.py:151-167, 282-298) on NHWC latents
   void dynamics(const at::Tensor& src, int64_t env_stride, const c10::optional<at::Tensor>& slot, int64_t slot_stride,
-                const at::Tensor& act, const at::Tensor& out, const at::Tensor& r_dec,
+                const at::Tensor& act, const c10::optional<at::Tensor>& out_, const at::Tensor& r_dec,
                 const c10::optional<at::Tensor>& r_logits, const c10::optional<at::Tensor>& pool, int64_t pool_env_stride,
                 int64_t pool_slot) {
     hipStream_t s = cur_stream(src);
+    // out absent: the fused step writes the scaled latent to the node-pool slot only (the search reads
+    // it from there)
+    const bool has_out = out_.has_value() && out_->defined();
+    TORCH_CHECK(has_out || (fused_ok() && vp(pool)), "mz::dynamics_: out may be omitted only on the fused step with a pool");
+    const at::Tensor out = has_out ? *out_ : at::Tensor();
     const int64_t n = lhw * p->c1;
     if (env_stride <= 0) env_stride = n;
     if (fused_ok()) {  // one launch: ConvBlock + 14 blocks + reward head + scale
@@ -374,7 +379,7 @@ struct NetRunner : torch::CustomClassHolder {
       e.pool = vp(pool);
       e.pool_env_stride = pool_env_stride;
       e.pool_slot = (int)pool_slot;
-      tower_call("dyn_tower", src.data_ptr(), env_stride, vp<int32_t>(slot), slot_stride, out.data_ptr(), e, s,
+      tower_call("dyn_tower", src.data_ptr(), env_stride, vp<int32_t>(slot), slot_stride, vp(out), e, s,
                  2 * p->i("dyn_tower.n") + 1);
       return;
     }
@@ -407,9 +412,14 @@ struct NetRunner : torch::CustomClassHolder {
 
   // PredictionNetwork (networks.py:225-241) + decode (mcts.py:97-100, 197-199); with `tree` the fused
   // launch also runs this simulation's backup and the next selection (mcts.py:136-234)
-  void prediction(const at::Tensor& h, const at::Tensor& pi, const at::Tensor& v, const c10::optional<at::Tensor>& pl,
-                  const c10::optional<at::Tensor>& vl, const mzba_tree_step* tree = nullptr) {
-    hipStream_t s = cur_stream(h);
+  // h: B latents, env b at h + b * h_stride elements (h_stride 0: contiguous)
+  void prediction(const at::Tensor& h_, const at::Tensor& pi, const at::Tensor& v, const c10::optional<at::Tensor>& pl,
+                  const c10::optional<at::Tensor>& vl, const mzba_tree_step* tree = nullptr, int64_t h_stride = 0) {
+    hipStream_t s = cur_stream(h_);
+    const int64_t n = lhw * p->c1;
+    if (h_stride <= 0) h_stride = n;
+    // the unfused launches read contiguous latents
+    const at::Tensor h = (fused_ok() || h_stride == n) ? h_ : h_.as_strided({B, n}, {h_stride, 1}).contiguous();
     if (fused_ok()) {  // one launch: 14 blocks + policy / value heads (+ tree step)
       mzba_tower_ext e = ext0();
       e.epilogue = 2;
@@ -421,7 +431,7 @@ struct NetRunner : torch::CustomClassHolder {
       e.logits[0] = vp<float>(pl), e.dec[0] = vp<float>(pi);
       e.logits[1] = vp<float>(vl), e.dec[1] = vp<float>(v);
       e.tree = tree;
-      tower_call("pred_tower", h.data_ptr(), lhw * p->c1, nullptr, 0, nullptr, e, s, 2 * p->i("pred_tower.n"));
+      tower_call("pred_tower", h.data_ptr(), h_stride, nullptr, 0, nullptr, e, s, 2 * p->i("pred_tower.n"));
       return;
     }
     TORCH_CHECK(!tree, "mz: the tree step rides on the fused prediction launch only");
@@ -489,14 +499,16 @@ void representation_(const RunPtr& rn, const at::Tensor& x, at::Tensor& out, con
 }
 
 void dynamics_(const RunPtr& rn, const at::Tensor& src, int64_t env_stride, const c10::optional<at::Tensor>& slot,
-               int64_t slot_stride, const at::Tensor& act, at::Tensor& out, at::Tensor& r_dec,
+               int64_t slot_stride, const at::Tensor& act, c10::optional<at::Tensor> out, at::Tensor& r_dec,
                const c10::optional<at::Tensor>& r_logits, const c10::optional<at::Tensor>& pool, int64_t pool_env_stride,
                int64_t pool_slot) {
   const NetPack* p = rn->p;
   check_act_dtype(rn, src, "src");
-  check_act_dtype(rn, out, "out");
   check_dev(src, "src");
-  check_batch(rn, out, rn->lhw * p->c1, "out");
+  if (out.has_value() && out->defined()) {
+    check_act_dtype(rn, *out, "out");
+    check_batch(rn, *out, rn->lhw * p->c1, "out");
+  }
   check_batch(rn, r_dec, 1, "r_dec");
   check_batch(rn, act, 1, "act");
   TORCH_CHECK(act.scalar_type() == at::kInt, "mz::dynamics_: act must be int32");
@@ -508,14 +520,27 @@ void dynamics_(const RunPtr& rn, const at::Tensor& src, int64_t env_stride, cons
   rn->dynamics(src, env_stride, slot, slot_stride, act, out, r_dec, r_logits, pool, pool_env_stride, pool_slot);
 }
 
+// latents for a prediction step: a contiguous buffer of >= B latents, or a [>= B, n] view whose rows are
+// contiguous (e.g. one node-pool slot of every env); returns the env stride in elements
+int64_t latent_rows(const RunPtr& rn, const at::Tensor& h) {
+  const int64_t n = rn->lhw * rn->p->c1;
+  check_act_dtype(rn, h, "h");
+  TORCH_CHECK(h.is_cuda(), "mz: h must be a device tensor");
+  if (h.is_contiguous()) {
+    check_batch(rn, h, n, "h");
+    return n;
+  }
+  TORCH_CHECK(h.dim() == 2 && h.size(0) >= rn->B && h.size(1) == n && h.stride(1) == 1 && h.stride(0) >= n,
+              "mz: h must be contiguous or a [B, ", n, "] view with contiguous rows");
+  return h.stride(0);
+}
+
 void prediction_(const RunPtr& rn, const at::Tensor& h, at::Tensor& pi, at::Tensor& v,
                  const c10::optional<at::Tensor>& pl, const c10::optional<at::Tensor>& vl) {
-  const NetPack* p = rn->p;
-  check_act_dtype(rn, h, "h");
-  check_batch(rn, h, rn->lhw * p->c1, "h");
+  const int64_t hs = latent_rows(rn, h);
   check_batch(rn, pi, 3, "pi");
   check_batch(rn, v, 1, "v");
-  rn->prediction(h, pi, v, pl, vl);
+  rn->prediction(h, pi, v, pl, vl, nullptr, hs);
 }
 
 void prediction_tree_(const RunPtr& rn, const at::Tensor& h, at::Tensor& pi, at::Tensor& v, at::Tensor& nodes,
@@ -523,9 +548,7 @@ void prediction_tree_(const RunPtr& rn, const at::Tensor& h, at::Tensor& pi, at:
                       at::Tensor& depth, at::Tensor& path, const at::Tensor& sqrt_tab, const at::Tensor& c_tab, int64_t S,
                       int64_t env_offset, int64_t search_id, int64_t seed, const c10::optional<at::Tensor>& ctx,
                       int64_t sim, double gamma, const at::Tensor& r) {
-  const NetPack* p = rn->p;
-  check_act_dtype(rn, h, "h");
-  check_batch(rn, h, rn->lhw * p->c1, "h");
+  const int64_t hs = latent_rows(rn, h);
   check_batch(rn, pi, 3, "pi");
   check_batch(rn, v, 1, "v");
   check_batch(rn, r, 1, "r");
@@ -541,7 +564,7 @@ void prediction_tree_(const RunPtr& rn, const at::Tensor& h, at::Tensor& pi, at:
                    vp<int32_t>(leaf_action), vp<int32_t>(depth), vp<int32_t>(path), vp<float>(sqrt_tab),
                    vp<float>(c_tab), (int)B, (int)S, (int)env_offset, (int)search_id, (uint64_t)seed,
                    vp<int32_t>(ctx), (int)sim, (float)gamma, vp<float>(r)};
-  rn->prediction(h, pi, v, c10::nullopt, c10::nullopt, &t);
+  rn->prediction(h, pi, v, c10::nullopt, c10::nullopt, &t, hs);
 }
 
 // ---- reference surface (NCHW f32 in / out) --------------------------------------------------------
@@ -656,7 +679,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
   m.def("representation_(__torch__.torch.classes.mz.NetRunner rn, Tensor x, Tensor(a!) out, Tensor(b!)? pool, "
         "int pool_env_stride) -> ()");
   m.def("dynamics_(__torch__.torch.classes.mz.NetRunner rn, Tensor src, int env_stride, Tensor? slot, int slot_stride, "
-        "Tensor act, Tensor(a!) out, Tensor(b!) r_dec, Tensor(c!)? r_logits, Tensor(d!)? pool, int pool_env_stride, "
+        "Tensor act, Tensor(a!)? out, Tensor(b!) r_dec, Tensor(c!)? r_logits, Tensor(d!)? pool, int pool_env_stride, "
         "int pool_slot) -> ()");
   m.def("prediction_(__torch__.torch.classes.mz.NetRunner rn, Tensor h, Tensor(a!) pi, Tensor(b!) v, "
         "Tensor(c!)? p_logits, Tensor(d!)? v_logits) -> ()");

@@ -411,7 +411,7 @@ __device__ __forceinline__ void tower_scale(const TowerArgs& a, const uint8_t* _
   if (e >= nenv) return;
   const float den = (mx - mn) + 1e-8f;
   const int b = env0 + e;
-  bf16_t* o1 = a.out + (size_t)b * 20 * TC;
+  bf16_t* o1 = a.out ? a.out + (size_t)b * 20 * TC : nullptr;  // null: the node-pool slot only
   bf16_t* o2 = a.x.pool ? reinterpret_cast<bf16_t*>(a.x.pool) + (size_t)b * a.x.pool_env_stride +
                               (size_t)a.x.pool_slot * 20 * TC
                         : nullptr;
@@ -422,7 +422,7 @@ __device__ __forceinline__ void tower_scale(const TowerArgs& a, const uint8_t* _
     unpack8<EL>(v[u], f);
     const uint4 r = make_uint4(pack_bf16x2((f[0] - mn) / den, (f[1] - mn) / den), pack_bf16x2((f[2] - mn) / den, (f[3] - mn) / den),
                                pack_bf16x2((f[4] - mn) / den, (f[5] - mn) / den), pack_bf16x2((f[6] - mn) / den, (f[7] - mn) / den));
-    *reinterpret_cast<uint4*>(o1 + p * TC + c * 8) = r;
+    if (o1) *reinterpret_cast<uint4*>(o1 + p * TC + c * 8) = r;
     if (o2) *reinterpret_cast<uint4*>(o2 + p * TC + c * 8) = r;
   }
 }
@@ -822,7 +822,7 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
   if (e >= nenv) return;
   const float den = (mx - mn) + 1e-8f;
   const int b = env0 + e;
-  bf16_t* o1 = a.out + (size_t)b * 20 * TC;
+  bf16_t* o1 = a.out ? a.out + (size_t)b * 20 * TC : nullptr;  // null: the node-pool slot only
   bf16_t* o2 = a.x.pool ? reinterpret_cast<bf16_t*>(a.x.pool) + (size_t)b * a.x.pool_env_stride +
                               (size_t)a.x.pool_slot * 20 * TC
                         : nullptr;
@@ -832,7 +832,7 @@ __device__ __forceinline__ void tower8_scale(const TowerArgs& a, const uint8_t* 
     unpack8<EL>(*reinterpret_cast<const uint4*>(lds + toff(t8::row8(e, p), c)), f);
     const uint4 r = make_uint4(pack_bf16x2((f[0] - mn) / den, (f[1] - mn) / den), pack_bf16x2((f[2] - mn) / den, (f[3] - mn) / den),
                                pack_bf16x2((f[4] - mn) / den, (f[5] - mn) / den), pack_bf16x2((f[6] - mn) / den, (f[7] - mn) / den));
-    *reinterpret_cast<uint4*>(o1 + p * TC + c * 8) = r;
+    if (o1) *reinterpret_cast<uint4*>(o1 + p * TC + c * 8) = r;
     if (o2) *reinterpret_cast<uint4*>(o2 + p * TC + c * 8) = r;
   }
 }
@@ -1228,7 +1228,7 @@ int mzba_tower_fused(const void* in, long long in_env_stride, const int32_t* slo
   MZ_CHECK_ARG(x.epilogue >= 0 && x.epilogue <= 2 && (x.elem == 0 || x.elem == 1), -2);
   MZ_CHECK_ARG(!x.w0 || (x.b0 && x.act_bias && x.act && x.A > 0), -3);
   MZ_CHECK_ARG(x.epilogue != 0 || out, -3);
-  MZ_CHECK_ARG(x.epilogue != 1 || (out && x.we1 && x.be1 && x.lw[0] && x.lb[0] && x.dec[0] && x.lO[0] > 1 &&
+  MZ_CHECK_ARG(x.epilogue != 1 || ((out || x.pool) && x.we1 && x.be1 && x.lw[0] && x.lb[0] && x.dec[0] && x.lO[0] > 1 &&
                                    x.lO[0] <= 16), -3);
   MZ_CHECK_ARG(x.epilogue != 2 || (x.we3 && x.be3 && x.we1 && x.be1 && x.lw[0] && x.lw[1] && x.lb[0] && x.lb[1] &&
                                    x.dec[0] && x.dec[1] && x.lO[0] >= 1 && x.lO[0] <= 16 && x.lO[1] > 1 &&

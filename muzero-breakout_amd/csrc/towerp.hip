@@ -516,7 +516,7 @@ MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0,
   const double rden = 1.0 / (double)den;
   auto dv = [&](float x) { return (float)((double)(x - mn) * rden); };
   const int b = env0 + e;
-  bf16_t* o1 = a.out + (size_t)b * 20 * tp::C;
+  bf16_t* o1 = a.out ? a.out + (size_t)b * 20 * tp::C : nullptr;  // null: the node-pool slot only
   bf16_t* o2 = a.x.pool ? reinterpret_cast<bf16_t*>(a.x.pool) + (size_t)b * a.x.pool_env_stride +
                               (size_t)a.x.pool_slot * 20 * tp::C
                         : nullptr;
@@ -527,7 +527,7 @@ MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0,
     unpack8<EL>(v, f);
     const uint4 r = make_uint4(pack_bf16x2(dv(f[0]), dv(f[1])), pack_bf16x2(dv(f[2]), dv(f[3])),
                                pack_bf16x2(dv(f[4]), dv(f[5])), pack_bf16x2(dv(f[6]), dv(f[7])));
-    *reinterpret_cast<uint4*>(o1 + p * tp::C + c * 8) = r;
+    if (o1) *reinterpret_cast<uint4*>(o1 + p * tp::C + c * 8) = r;
     if (o2) *reinterpret_cast<uint4*>(o2 + p * tp::C + c * 8) = r;
   }
 }
@@ -744,7 +744,7 @@ int mzba_towerp_fused(const void* in, long long in_env_stride, const int32_t* sl
   MZ_CHECK_ARG((x.elem == 0 || x.elem == 1) && x.epilogue >= 0 && x.epilogue <= 2, -2);
   MZ_CHECK_ARG(!x.w0 || (x.b0 && x.act_bias && x.act && x.A > 0), -3);
   MZ_CHECK_ARG(x.epilogue != 0 || out, -3);
-  MZ_CHECK_ARG(x.epilogue != 1 || (out && x.we1 && x.be1 && x.lw[0] && x.lb[0] && x.dec[0] && x.lO[0] > 1 &&
+  MZ_CHECK_ARG(x.epilogue != 1 || ((out || x.pool) && x.we1 && x.be1 && x.lw[0] && x.lb[0] && x.dec[0] && x.lO[0] > 1 &&
                                    x.lO[0] <= 16), -3);
   MZ_CHECK_ARG(x.epilogue != 2 || (x.we3 && x.be3 && x.we1 && x.be1 && x.lw[0] && x.lw[1] && x.lb[0] && x.lb[1] &&
                                    x.dec[0] && x.dec[1] && x.lO[0] >= 1 && x.lO[0] <= 16 && x.lO[1] > 1 &&

@@ -446,12 +446,14 @@ class NetRunner:
     def dynamics(self, parent_src, act, out_latent, r_dec, r_logits=None, slot=None, env_stride=None, slot_stride=0,
                  pool=None, pool_env_stride=0, pool_slot=0):
         """DynamicsNetwork + _scale_state (networks.py:151-167, 282-298) on NHWC latents.
-        parent_src (+ slot gather) -> out_latent (scaled), r_dec (decoded reward)."""
+        parent_src (+ slot gather) -> out_latent (scaled), r_dec (decoded reward). out_latent None: the
+        fused step writes the scaled latent to pool slot pool_slot only."""
         L.ops().dynamics_(self.native, parent_src, 0 if env_stride is None else env_stride, slot, slot_stride, act,
                           out_latent, r_dec, r_logits, pool, pool_env_stride, pool_slot)
 
     def prediction(self, h, pi, v, p_logits=None, v_logits=None, tree=None):
-        """PredictionNetwork (networks.py:225-241) + decode (mcts.py:97-100, 197-199).
+        """PredictionNetwork (networks.py:225-241) + decode (mcts.py:97-100, 197-199). h: contiguous
+        latents, or a [B, n] view with contiguous rows (one node-pool slot of every env).
         tree: optional (tree_args, sim, gamma, r) — the same launch then runs this simulation's backup
         and the next selection (mcts.py:136-234; fused path only, mz::prediction_tree_)."""
         if tree is None:

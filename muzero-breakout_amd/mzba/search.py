@@ -131,6 +131,9 @@ class SearchWorkspace:
         self.runner = agent.runner(B, p.lh * 4, p.lw * 4)
         # backup + next select ride on the fused prediction launch (MZBA_TREE_FUSION=0: separate kernels)
         self.use_tree_fusion = os.environ.get("MZBA_TREE_FUSION", "1") != "0"
+        # fused steps: latents straight from / to their node-pool slots (MZBA_POOL_SLOTS=0: through `cur`,
+        # the round-3 second-session form, for A/B runs)
+        self.use_pool_slots = os.environ.get("MZBA_POOL_SLOTS", "1") != "0"
 
     def load_root(self, hidden_state):
         """NCHW (B,C,h,w) latent -> pool slot 0 (NHWC)."""
@@ -150,28 +153,35 @@ class SearchWorkspace:
         B, S, n = self.B, self.S, self.n
         ta = self.tree.args(s.env_offset, search_id, s.seed, ctx)
         rn = self.runner
-        root = self.pool.view(B, S + 1, n)[:, 0]
-        self.cur.view(B, n).copy_(root)
-        rn.prediction(self.cur, self.pi, self.v)  # _expand_root_nodes mcts.py:95-100
+        slots = self.pool.view(B, S + 1, n)  # node pool: slot 0 the root, slot s + 1 the node of simulation s
+        fused = rn.fused_ok() and self.use_tree_fusion
+        direct = fused and self.use_pool_slots
+        # the fused steps read each latent from its node-pool slot and the dynamics step writes the new
+        # latent there only (no copy into `cur`: one latent write per env and simulation, not two)
+        rn.prediction(slots[:, 0] if direct else self._root_copy(slots), self.pi, self.v)  # _expand_root_nodes mcts.py:95-100
         w_pol = float(np.float32(1 - s.noise_weight))
         w_noise = float(np.float32(s.noise_weight))
         self.tree.root(ta, self.v, self.pi, noise, w_pol, w_noise, s.dirchlet_alpha, w_dev)
         gamma = float(np.float32(s.discount))
         env_stride = (S + 1) * n
-        fused = rn.fused_ok() and self.use_tree_fusion
         for sim in range(S):
             if sim > 0 and not fused:
                 self.tree.select(ta, sim)
-            rn.dynamics(self.pool, self.tree.leaf_action, self.cur, self.r, slot=self.tree.leaf_parent,
-                        env_stride=env_stride, slot_stride=n, pool=self.pool, pool_env_stride=env_stride,
-                        pool_slot=sim + 1)
+            rn.dynamics(self.pool, self.tree.leaf_action, None if direct else self.cur, self.r,
+                        slot=self.tree.leaf_parent, env_stride=env_stride, slot_stride=n, pool=self.pool,
+                        pool_env_stride=env_stride, pool_slot=sim + 1)
             if fused:  # prediction + backup(sim) + select(sim + 1) in one launch
-                rn.prediction(self.cur, self.pi, self.v, tree=(ta, sim, gamma, self.r))
+                rn.prediction(slots[:, sim + 1] if direct else self.cur, self.pi, self.v, tree=(ta, sim, gamma, self.r))
             else:
                 rn.prediction(self.cur, self.pi, self.v)
                 self.tree.backup(ta, sim, self.r, self.v, self.pi, gamma)
         self.tree.results(ta)
         return self.tree.values, self.tree.counts
+
+    def _root_copy(self, slots):
+        """The root latents contiguous in `cur` (the unfused launches read contiguous latents)."""
+        self.cur.view(self.B, self.n).copy_(slots[:, 0])
+        return self.cur
 
 
 def replay_search(B, S, cfg, v_root, pi_root, noise, r, v, pi, seed, search_id, env_offset=0, device="cuda"):

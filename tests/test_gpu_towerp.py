@@ -160,3 +160,37 @@ def test_towerp_fp16_dynamics_step_bit_identical_to_tower8(B):
     for k in a:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     assert np.isfinite(b["r"].view(np.float32)).all()
+
+
+@pytest.mark.parametrize("B", [4096, 40])
+def test_pool_only_dynamics_and_prediction_from_pool_slots(B):
+    """The search's form of the fused steps: the dynamics step without `out` writes the scaled latent to
+    its node-pool slot only, and the prediction step reads a [B, n] view of one slot of every env
+    (env stride (S + 1) n). Against the contiguous forms (out + pool, prediction on out): every output
+    equal bit for bit."""
+    ag = _agent(8)
+    rn = ag.runner(B, 16, 20)
+    assert rn.fused_ok()
+    S1, n = 3, 20 * C
+    g = torch.Generator().manual_seed(B + 5)
+    pool0 = torch.rand(B, S1 + 1, n, generator=g).to(torch.bfloat16).cuda()
+    slot = torch.randint(0, S1, (B,), generator=g, dtype=torch.int32).cuda()
+    act = torch.randint(0, 3, (B,), generator=g, dtype=torch.int32).cuda()
+    res = {}
+    for pool_only in (False, True):
+        pool = pool0.clone()
+        o = None if pool_only else torch.empty(B, n, dtype=torch.bfloat16, device="cuda")
+        r = torch.full((B,), float("nan"), device="cuda")
+        pi, v = torch.full((B, 3), float("nan"), device="cuda"), torch.full((B,), float("nan"), device="cuda")
+        rn.dynamics(pool, act, o, r, slot=slot, env_stride=(S1 + 1) * n, slot_stride=n, pool=pool,
+                    pool_env_stride=(S1 + 1) * n, pool_slot=S1)
+        h = pool[:, S1] if pool_only else o
+        assert h.is_contiguous() != pool_only
+        rn.prediction(h, pi, v)
+        torch.cuda.synchronize()
+        res[pool_only] = [t.view(torch.int16 if t.dtype == torch.bfloat16 else torch.int32).cpu().numpy()
+                          for t in (pool, r, pi, v)]
+        if not pool_only:
+            np.testing.assert_array_equal(o.view(torch.int16).cpu().numpy(), res[False][0][:, S1])
+    for a, b in zip(res[False], res[True]):
+        np.testing.assert_array_equal(a, b)
