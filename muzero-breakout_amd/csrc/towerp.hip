@@ -36,7 +36,13 @@
 #include "elt.h"  // Elt<EL>: bf16 (EL 0) / fp16 (EL 1, the fp16 dynamics net of config 5) images and weights
 
 #ifndef TP_SCHED
-#define TP_SCHED 1  // k-loop schedule (make towerp-sched builds the others): 1 the current fragments' MFMAs first, then the next reads
+// k-loop schedule (make towerp-sched / towerp-prod build the others): 6 the two column tiles' MFMAs
+// interleaved — each B fragment feeds two MFMAs back to back, the next row's reads after the 10 dx = 0
+// MFMAs; the same cycles within 0.4 % as 1 but the chip holds a 1-2 % higher clock under it (bench A/B
+// +1.0-1.2 %, profiles/r03/tp_sched); 1 per column tile, the current fragments' MFMAs first, then the next
+// reads; 5 as 1 without the fence between row steps; 7 as 6 without it; 8 as 6 with the reads among the
+// first dx = 0 pairs
+#define TP_SCHED 6
 #endif
 #ifndef TP_ABLATE
 #define TP_ABLATE 0  // diagnostic builds only (make towerp-ablate): 1 no LDS B reads in the k loop, 2 L1-resident weights
@@ -151,6 +157,60 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
         const int yp = YLO + yi;
         const int nb = yi + 1 < NY ? xc + 5 * (yp + 1) * tp::PIX : xn + 5 * ynext * tp::PIX;
         const bool last = yi == NY - 1;
+#if TP_SCHED >= 6  // the two column tiles' MFMAs interleaved (per accumulator the same order)
+        auto row = [&](const V8(&f)[5], V8(&fn)[5]) {
+          V8 w[3][2];
+#pragma unroll
+          for (int d = 0; d < 3; ++d)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) w[d][ct] = __builtin_bit_cast(V8, bq[cc][d][ct]);
+#pragma unroll
+          for (int xp = 0; xp < 5; ++xp)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+              acc[(yp - DY) * 5 + xp][ct] = Elt<EL>::mfma(w[1][ct], f[xp], acc[(yp - DY) * 5 + xp][ct]);
+#pragma unroll
+          for (int xp = 0; xp < 5; ++xp) fn[xp] = *reinterpret_cast<const V8*>(lds + nb + xp * tp::PIX);
+#pragma unroll
+          for (int xp = 0; xp < 4; ++xp)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+              acc[(yp - DY) * 5 + xp + 1][ct] = Elt<EL>::mfma(w[0][ct], f[xp], acc[(yp - DY) * 5 + xp + 1][ct]);
+#pragma unroll
+          for (int xp = 1; xp < 5; ++xp)
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+              acc[(yp - DY) * 5 + xp - 1][ct] = Elt<EL>::mfma(w[2][ct], f[xp], acc[(yp - DY) * 5 + xp - 1][ct]);
+          if (last) {
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+              for (int d = 0; d < 3; ++d)
+                bq[cc][d][ct] = __builtin_bit_cast(
+                    uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, ct * tp::CTB + (24 * d + st) * 1024, 0));
+          }
+#if TP_SCHED == 8  // the next row's reads among the first dx = 0 pairs
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+#else  // 6, 7: after 8 of the 10 dx = 0 MFMAs, the reads ride in the next 5 slots
+          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+#pragma unroll
+          for (int j = 0; j < 5; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
+#endif
+          if (last) __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);
+#if TP_SCHED != 7  // 7: no scheduling fence between row steps
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+        };
+#else
         auto row = [&](const V8(&f)[5], V8(&fn)[5]) {
 #pragma unroll
           for (int ct = 0; ct < 2; ++ct) {
@@ -195,7 +255,7 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
               __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
             }
             if (last) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
-#elif TP_SCHED == 1  // the current fragments' MFMAs first (one wait), the next row's reads after them
+#elif TP_SCHED == 1 || TP_SCHED == 5  // the current fragments' MFMAs first (one wait), the next row's reads after them
             if (ct == 0) {
               __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
 #pragma unroll
@@ -222,8 +282,11 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
             if (last) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
 #endif  // TP_SCHED 2: the compiler's own order
           }
+#if TP_SCHED != 5  // 5 (diagnostic): no scheduling fence between row steps
           __builtin_amdgcn_sched_barrier(0);
+#endif
         };
+#endif
         if (((cc * NY + yi) & 1) == 0)
           row(fa, fb);
         else
