@@ -41,7 +41,7 @@
 // MFMAs; the same cycles within 0.4 % as 1 but the chip holds a 1-2 % higher clock under it (bench A/B
 // +1.0-1.2 %, profiles/r03/tp_sched); 1 per column tile, the current fragments' MFMAs first, then the next
 // reads; 5 as 1 without the fence between row steps; 7 as 6 without it; 8 as 6 with the reads among the
-// first dx = 0 pairs
+// first dx = 0 pairs; 9 as 6 in snake order (no headline change)
 #define TP_SCHED 6
 #endif
 #ifndef TP_ABLATE
@@ -164,23 +164,31 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
           for (int d = 0; d < 3; ++d)
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) w[d][ct] = __builtin_bit_cast(V8, bq[cc][d][ct]);
+          // TP_SCHED 9: snake order — the column tile alternates direction per source pixel, so every
+          // MFMA shares its A or its B operand with the one before it
 #pragma unroll
           for (int xp = 0; xp < 5; ++xp)
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
+            for (int k = 0; k < 2; ++k) {
+              const int ct = TP_SCHED == 9 && (xp & 1) ? 1 - k : k;
               acc[(yp - DY) * 5 + xp][ct] = Elt<EL>::mfma(w[1][ct], f[xp], acc[(yp - DY) * 5 + xp][ct]);
+            }
 #pragma unroll
           for (int xp = 0; xp < 5; ++xp) fn[xp] = *reinterpret_cast<const V8*>(lds + nb + xp * tp::PIX);
 #pragma unroll
           for (int xp = 0; xp < 4; ++xp)
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
+            for (int k = 0; k < 2; ++k) {
+              const int ct = TP_SCHED == 9 && !(xp & 1) ? 1 - k : k;
               acc[(yp - DY) * 5 + xp + 1][ct] = Elt<EL>::mfma(w[0][ct], f[xp], acc[(yp - DY) * 5 + xp + 1][ct]);
+            }
 #pragma unroll
           for (int xp = 1; xp < 5; ++xp)
 #pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
+            for (int k = 0; k < 2; ++k) {
+              const int ct = TP_SCHED == 9 && (xp & 1) ? 1 - k : k;
               acc[(yp - DY) * 5 + xp - 1][ct] = Elt<EL>::mfma(w[2][ct], f[xp], acc[(yp - DY) * 5 + xp - 1][ct]);
+            }
           if (last) {
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct)
