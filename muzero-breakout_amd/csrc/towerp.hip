@@ -565,17 +565,23 @@ MZ_DEV void tp_heads(const TPArgs& a, uint8_t* __restrict__ lds, const int (&hc0
 template <int EL>
 MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0, int nenv, int tid) {
   const int e = tid >> 4, t = tid & 15;
-  float mn = INFINITY, mx = -INFINITY;
+  // min / max on the packed 16-bit words: X is a ReLU output (relu_pk: +0 for every non-positive), and
+  // non-negative bf16 / fp16 values order as their unsigned bit patterns, so v_pk_min_u16 /
+  // v_pk_max_u16 over two values at a time give the f32 min / max of the unpacked values exactly
+  uint32_t mn2 = 0xffffffffu, mx2 = 0u;
+#pragma unroll 8
   for (int u = 0; u < 40; ++u) {
     const int i = u * 16 + t, p = i >> 5, c = i & 31;
     const uint4 v = *reinterpret_cast<const uint4*>(lds + tp::off(p * tp::E + e, c));
     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      mn = fminf(mn, Elt<EL>::lo(w4[j])); mx = fmaxf(mx, Elt<EL>::lo(w4[j]));
-      mn = fminf(mn, Elt<EL>::hi(w4[j])); mx = fmaxf(mx, Elt<EL>::hi(w4[j]));
+      asm("v_pk_min_u16 %0, %1, %2" : "=v"(mn2) : "v"(mn2), "v"(w4[j]));
+      asm("v_pk_max_u16 %0, %1, %2" : "=v"(mx2) : "v"(mx2), "v"(w4[j]));
     }
   }
+  const uint32_t mnh = min(mn2 & 0xffffu, mn2 >> 16), mxh = max(mx2 & 0xffffu, mx2 >> 16);
+  float mn = Elt<EL>::lo(mnh), mx = Elt<EL>::lo(mxh);
   for (int o = 8; o > 0; o >>= 1) { mn = fminf(mn, __shfl_xor(mn, o)); mx = fmaxf(mx, __shfl_xor(mx, o)); }
   if (e >= nenv) return;
   const float den = (mx - mn) + 1e-8f;
@@ -591,6 +597,7 @@ MZ_DEV void tp_scale(const TPArgs& a, const uint8_t* __restrict__ lds, int env0,
   bf16_t* o2 = a.x.pool ? reinterpret_cast<bf16_t*>(a.x.pool) + (size_t)b * a.x.pool_env_stride +
                               (size_t)a.x.pool_slot * 20 * tp::C
                         : nullptr;
+#pragma unroll 4
   for (int u = 0; u < 40; ++u) {
     const int i = u * 16 + t, p = i >> 5, c = i & 31;
     const uint4 v = *reinterpret_cast<const uint4*>(lds + tp::off(p * tp::E + e, c));
