@@ -386,20 +386,41 @@ MZ_DEV void tp_k1(const uint8_t* __restrict__ lds, int lb, int q, int n, const T
 #pragma unroll
     for (int ct = 0; ct < 2; ++ct)
       wq[c][ct] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(w.rs, lane * 16, ct * 8192 + c * 1024, 0));
+  // 32 steps (channel step c, pixel row yp), each 5 B fragments -> 10 MFMAs; the next step's fragments
+  // are read during the current step's MFMAs (double-buffered: a read per step waited on its own LDS
+  // round trip, 20 k cycles for the reward conv's two passes against a 10 k MFMA floor). Per accumulator
+  // the channel steps stay in ascending order.
+  V8 fa[5], fb[5];
+  auto rd = [&](int k, V8(&f)[5]) {
+    const int xc = lb + (((4 * (k >> 2) + q) ^ n) << 4), yp = k & 3;
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int xc = lb + (((4 * c + q) ^ n) << 4);
+    for (int xp = 0; xp < 5; ++xp) f[xp] = *reinterpret_cast<const V8*>(lds + xc + (5 * yp + xp) * tp::PIX);
+  };
+  rd(0, fa);
 #pragma unroll
-    for (int yp = 0; yp < 4; ++yp) {
-      V8 f[5];
-#pragma unroll
-      for (int xp = 0; xp < 5; ++xp) f[xp] = *reinterpret_cast<const V8*>(lds + xc + (5 * yp + xp) * tp::PIX);
+  for (int k = 0; k < 32; ++k) {
+    auto step = [&](const V8(&f)[5], V8(&fn)[5]) {
+      const int c = k >> 2, yp = k & 3;
+      if (k + 1 < 32) rd(k + 1, fn);
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
         for (int xp = 0; xp < 5; ++xp)
           acc[5 * yp + xp][ct] = Elt<EL>::mfma(__builtin_bit_cast(V8, wq[c][ct]), f[xp], acc[5 * yp + xp][ct]);
-    }
+      if (k + 1 < 32) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    if (k & 1)
+      step(fb, fa);
+    else
+      step(fa, fb);
   }
 }
 
