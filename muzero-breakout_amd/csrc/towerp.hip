@@ -44,6 +44,9 @@
 // first dx = 0 pairs; 9 as 6 in snake order (no headline change)
 #define TP_SCHED 6
 #endif
+#ifndef TP_STAGE
+#define TP_STAGE 2  // staging batches per wave (2: two envs' 20 loads in flight at a time; 1: all four)
+#endif
 #ifndef TP_ABLATE
 #define TP_ABLATE 0  // diagnostic builds only (make towerp-ablate): 1 no LDS B reads in the k loop, 2 L1-resident weights
 #endif
@@ -651,13 +654,15 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
   tp_preload(bq, tpw(pro ? a.x.w0 : a.wf, ct0), lane);
   // the lane's env (row n of every pixel tile): its action for the dynamics ConvBlock's bias table
   const int act = pro ? a.x.act[env0 + (n < nenv ? n : 0)] : 0;
-  // stage: wave w owns envs 4w .. 4w + 3, one env (640 contiguous 16-B chunks) per batch of 10 loads
+  // stage: wave w owns envs 4w .. 4w + 3, one env (640 contiguous 16-B chunks) per batch of 10 loads;
+  // TP_STAGE batches of 4 / TP_STAGE envs in flight at once
+  constexpr int SB = 4 / TP_STAGE;
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    uint4 v[20];
+  for (int h = 0; h < TP_STAGE; ++h) {
+    uint4 v[10 * SB];
 #pragma unroll
-    for (int bb = 0; bb < 2; ++bb) {
-      const int e = 4 * wave + 2 * h + bb;
+    for (int bb = 0; bb < SB; ++bb) {
+      const int e = 4 * wave + SB * h + bb;
       const bool ok = e < nenv;
       const int b = env0 + (ok ? e : 0);
       const long long eo = (long long)b * a.in_env_stride + (a.slot ? (long long)a.slot[b] * a.in_slot_stride : 0);
@@ -668,8 +673,8 @@ __global__ __launch_bounds__(tp::NT, 1) void towerp_kernel(TPArgs a) {
       }
     }
 #pragma unroll
-    for (int bb = 0; bb < 2; ++bb) {
-      const int e = 4 * wave + 2 * h + bb;
+    for (int bb = 0; bb < SB; ++bb) {
+      const int e = 4 * wave + SB * h + bb;
 #pragma unroll
       for (int u = 0; u < 10; ++u) {
         const int cj = u * 64 + lane;
