@@ -52,6 +52,9 @@ static_assert(8 % TD == 0, "ring index restarts at every tap");
 // tower8 weight ring depth in entries (one entry = one 1 KB fragment per column tile): two k steps of
 // the one-pass k loop (3 column shifts each); a ring entry count must divide the 24 of a dy
 template <int NQ> constexpr int t8d = 6;
+#ifndef T8_SCHED
+#define T8_SCHED 1  // tower8 one-pass k loop: 1 column-tile major; 6 the column tiles' MFMAs interleaved
+#endif
 #ifndef TOWER_ABLATE
 #define TOWER_ABLATE 0  // diagnostic builds of the 4-env 8-wave kernel only (make tower-variants): 1 hot
                         // weights, 2 no LDS A reads, 3 duplicate weight streams (waves w, w+4), 4 = 3 with
@@ -622,6 +625,56 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
       // then that tile's three ring slots are reloaded with the entries of the step after next (their
       // registers are free once its MFMAs have issued: no copies, a ring of two steps in the same
       // registers); the next step's A reads ride in the first column tile's MFMA slots
+#if T8_SCHED == 6
+      // the column tiles' MFMAs interleaved: every A fragment feeds its CT MFMAs back to back (per
+      // accumulator the same order; towerp_kernel's schedule 6), then every tile's ring slots reloaded
+      {
+        typename Elt<EL>::v8 w[3][CT];
+#pragma unroll
+        for (int d = 0; d < 3; ++d)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) w[d][ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][(3 * c + d) % RD]);
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) acc[j][ct] = Elt<EL>::mfma(w[1][ct], afc[j], acc[j][ct]);
+          if (c + 1 < NC)
+            afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
+          else
+            afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
+        }
+#pragma unroll
+        for (int j = 0; j < NA; ++j)
+          if (j % TX + 1 < TX)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[j + 1][ct] = Elt<EL>::mfma(w[0][ct], afc[j], acc[j + 1][ct]);
+#pragma unroll
+        for (int j = 0; j < NA; ++j)
+          if (j % TX >= 1)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct) acc[j - 1][ct] = Elt<EL>::mfma(w[2][ct], afc[j], acc[j - 1][ct]);
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+          for (int d = 0; d < 3; ++d) {
+            int so = ct * (TNS * 1024) + (24 * d + dyi * NC + c + RD / 3) * 1024;
+            __amdgpu_buffer_rsrc_t rs = cur.rs;
+            if (3 * c + d + RD >= 3 * NC) {
+              const int nn = 3 * c + d + RD - 3 * NC;
+              so = last ? ct * nxt.tstride + t8_first(nxt, nn) * 1024 : so;
+              rs = last ? nxt.rs : cur.rs;
+            }
+            bq[ct][(3 * c + d) % RD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
+          }
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, CT, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM - CT * NA, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 3 * CT, 0);
+      }
+#else
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         typename Elt<EL>::v8 w[3];
@@ -676,6 +729,7 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
         }
         __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
       }
+#endif
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NA; ++j) afc[j] = afn[j];
