@@ -147,3 +147,23 @@ def test_scale_division_by_double_reciprocal_is_ieee():
     q_ieee = a / d
     q_dbl = (a.astype(np.float64) * (1.0 / d.astype(np.float64))).astype(np.float32)
     np.testing.assert_array_equal(q_ieee.view(np.uint32), q_dbl.view(np.uint32))
+
+
+def test_rep_trunk_rejects_bad_arguments_without_gpu():
+    """mzba_rep_trunk checks its arguments before any HIP call: null buffers or pointer tables, negative
+    block counts, more convs than its kernel-argument tables hold (2 n0 + 2 + 2 n1 <= 56), in == out."""
+    import ctypes
+    from mzba import _lib
+    L = _lib.lib()
+    nc = 2 * 2 + 2 + 2 * 3
+    w = (ctypes.c_void_p * nc)(*([1] * nc))
+    b = (ctypes.c_void_p * nc)(*([1] * nc))
+    x, y = ctypes.c_void_p(16), ctypes.c_void_p(32)
+    assert L.mzba_rep_trunk(None, y, w, b, 2, 3, 4, None) == -1
+    assert L.mzba_rep_trunk(x, y, None, b, 2, 3, 4, None) == -1
+    assert L.mzba_rep_trunk(x, y, w, b, -1, 3, 4, None) == -1
+    assert L.mzba_rep_trunk(x, y, w, b, 2, 3, 0, None) == -1
+    assert L.mzba_rep_trunk(x, x, w, b, 2, 3, 4, None) == -1
+    assert L.mzba_rep_trunk(x, y, w, b, 20, 8, 4, None) == -1  # 58 convs
+    wn = (ctypes.c_void_p * nc)(*([1] * (nc - 1) + [0]))
+    assert L.mzba_rep_trunk(x, y, wn, b, 2, 3, 4, None) == -1
