@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--width", type=int, default=None, help="env workload frame width (default 84)")
     ap.add_argument("--hist", type=int, default=4, help="env workload frame-stack length")
     ap.add_argument("--minibatch", type=int, default=512, help="learner workload minibatch (config.yaml:7)")
+    ap.add_argument("--pow-threads", type=int, default=1,
+                    help="intra-op threads of the reference process whose temperature pow the sampling reproduces "
+                         "(splits torch's pow into per-thread chunks from 3 x global envs >= 32768 on)")
     return ap.parse_args()
 
 
@@ -297,6 +300,26 @@ def tower_traffic(B, fused_tower):
     return None, None
 
 
+def tower_counters(B, kname):
+    """Measured SQ counters of the dominant kernel at this batch (profiles/tower_sq_counters.json, from the
+    two rocprofv3 --pmc passes of tools/pmc_towerp_sq.sh inside this bench): MFMA-pipe busy fraction of the
+    SIMD cycles at the clock the chip held, LDS bank-conflict share, and the executed MFMA count."""
+    tpath = os.path.join(ROOT, "profiles", "tower_sq_counters.json")
+    if not os.path.exists(tpath):
+        return None
+    for rec in json.load(open(tpath))["records"]:
+        if rec.get("envs") == B and rec.get("kernel_name") == kname:
+            return rec
+    return None
+
+
+# Fraction of a launch's algorithmic 3x3-conv FLOPs the kernel issues to the MFMA pipe: the reference's
+# Conv2d(padding=1) on the 4x5 latent evaluates 50 of its 180 taps per env on zero padding. The pixel-tiled
+# kernel (plan 4) skips them all (130 / 180); the column-tiled tower8 (plans 2 / 3) skips the dx ones only
+# (39 of 45 tile-taps, 86.7 %, DESIGN.md §3.0).
+EXECUTED_FRACTION = {"towerp_kernel": 130.0 / 180.0, "tower8_kernel<0, 2>": 39.0 / 45.0, "tower8_kernel<0, 1>": 39.0 / 45.0}
+
+
 def tower_kernel_name(B):
     """The kernel mzba_tower_plan picks for batch B (tower.hip)."""
     from mzba import _lib as L
@@ -347,7 +370,7 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
     ag32 = MuZeroAgent(mcfg, dtype="f32", device=loop.agent.device)
     ag32.load_state_dict(sd)
     l32 = ActingLoop(cfg, ag32, B, seed=args.seed, env_offset=loop.env_offset, height=H, width=W,
-                     n_envs_total=loop.n_envs_total)
+                     n_envs_total=loop.n_envs_total, pow_threads=loop.pow_threads)
     l32.temperature = loop.temperature
     l32.search.noise_weight = loop.search.noise_weight
     l32.reset(0)
@@ -426,7 +449,8 @@ def main():
     else:
         sd = init_state_dict(mcfg, args.seed)
     agent.load_state_dict(sd)
-    loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B, height=H, width=W, n_envs_total=world * B)
+    loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B, height=H, width=W, n_envs_total=world * B,
+                      pow_threads=args.pow_threads)
     gather = TrajectoryGather(world, rank, RECORD_K, B, H * W, f"cuda:{local}")
     loop.reset(0)
     last_flush = [0]
@@ -532,6 +556,9 @@ def main():
     fl = conv_flops(B, p.lh * p.lw, p.c1)
     achieved = fl / (conv_ms * 1e-3) / 1e12 if conv_ms else None
     traffic, traffic_rec = tower_traffic(B, any(n > 1 for _, n in probe))
+    kname = tower_kernel_name(B) if tower_launch_ms else None
+    ex_frac = EXECUTED_FRACTION.get(kname)
+    sq = tower_counters(B, kname) if kname else None
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -551,6 +578,7 @@ def main():
                                    (f"config 3 acting geometry: {B} envs/GPU x {args.sims} MCTS sims, {H}x{W} Breakout, "
                                     f"{args.hist}-frame stack, latent {H // 4}x{W // 4} (generic conv kernels)"),
                        "envs_per_gpu": B, "global_envs": world * B, "sims": args.sims,
+                       "pow_threads": args.pow_threads,
                        "parallelism": f"env-sharded x{world}, RCCL gather of trajectory records to rank 0, target-net broadcast"},
             "roofline": {"bound": "mfma",
                          "kernel": (f"{tower_kernel_name(B)} (fused dynamics / prediction step: 14-block residual "
@@ -566,7 +594,16 @@ def main():
                              traffic_rec.get("algorithmic_bytes") + 7 * (2 * 14 * 256 * 2304 * 2)),
                          "traffic_source": traffic_rec and "profiles/tower_hbm_traffic.json",
                          "flop_per_conv": fl, "avg_ms_per_conv": conv_ms, "avg_launch_ms": tower_launch_ms or conv_ms,
-                         "launches_timed": len(probe)},
+                         "launches_timed": len(probe),
+                         # what the MFMA pipe actually issues: the algorithmic rate x the kernel's padding-free
+                         # fraction of the 3x3 taps, against the same dense peak (live, this run)
+                         "executed_fraction_of_algorithmic": ex_frac,
+                         "executed_frac": (achieved * ex_frac / PEAK_BF16_TFLOPS) if (achieved and ex_frac) else None,
+                         # measured PMC of the same kernel in this bench (profiled run, not this one)
+                         "mfma_busy": sq and sq.get("mfma_busy"),
+                         "mfma_busy_clock_ghz": sq and sq.get("clock_ghz"),
+                         "lds_bank_conflict_frac": sq and sq.get("lds_bank_conflict_frac"),
+                         "counters_source": sq and sq.get("source")},
             "cpu_baseline": cpu_info,
             "visit_count_match": match,
             "visit_count_match_sample": (f"{min(args.cpu_envs, B)} envs, bf16 HIP path vs the f32 CPU port (same keyed "

@@ -26,6 +26,7 @@
 #include <torch/library.h>
 
 #include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -71,7 +72,11 @@ struct NetPack : torch::CustomClassHolder {
   std::map<std::string, at::Tensor> tens;  // tower packs / biases, fused-step weights, rep tail
   std::map<std::string, int64_t> ints;
   std::vector<std::tuple<std::string, std::string, std::string>> rep;  // (kind, conv1, conv2)
+  // one runner per (B, H, W), shared by every caller of that batch shape (the acting loop, the search and the
+  // reference-surface ops): its scratch is single-stream — launches through one runner must be
+  // stream-ordered (the reference's caller is single-threaded Python); the map is locked
   std::map<std::tuple<int64_t, int64_t, int64_t>, c10::intrusive_ptr<struct NetRunner>> runners;
+  std::mutex runners_mu;
 
   void set_meta(int64_t dt, int64_t c0_, int64_t c1_, int64_t L_, int64_t lh_, int64_t lw_, int64_t ns_, double smin_,
                 double smax_, bool dyn16) {
@@ -128,7 +133,11 @@ struct NetPack : torch::CustomClassHolder {
 
 // ---- launch sequences per batch ----------------------------------------------------------------
 struct NetRunner : torch::CustomClassHolder {
-  NetPack* p;  // the pack that owns this runner (NetPack::runners); the Python wrapper keeps both alive
+  // the pack that owns this runner (NetPack::runners holds it strongly): a weak back-reference, so a runner
+  // handle that outlives its pack raises (pin()) instead of dangling; `p` is valid while a pin is held,
+  // and every op holds one for its whole duration
+  c10::weak_intrusive_ptr<NetPack> pack_ref;
+  NetPack* p;
   int64_t B, H, W, lhw, HW, plan = 0;
   bool use_lat = true, use_tower = true, use_fused = true, use_band = true, use_rep_tail = true, use_band_res = true,
        use_rep_blocks = true, use_rep_trunk = true;
@@ -137,13 +146,19 @@ struct NetRunner : torch::CustomClassHolder {
   bool probe_on = false;
   std::vector<std::tuple<hipEvent_t, hipEvent_t, int64_t>> probe;
 
-  NetRunner(NetPack* pack, int64_t B_, int64_t H_, int64_t W_) : p(pack), B(B_), H(H_), W(W_) {
+  NetRunner(const c10::intrusive_ptr<NetPack>& pack, int64_t B_, int64_t H_, int64_t W_)
+      : pack_ref(pack), p(pack.get()), B(B_), H(H_), W(W_) {
     TORCH_CHECK(B > 0 && H > 0 && W > 0, "mz.NetRunner: empty batch or image");
     lhw = p->lh * p->lw;
     HW = H * W;
     if (p->tower_ok()) plan = mzba_tower_plan((int)B);  // the kernel this runner launches, fixed here
   }
   ~NetRunner() override { clear_probe(); }
+  c10::intrusive_ptr<NetPack> pin() const {
+    auto k = pack_ref.lock();
+    TORCH_CHECK(k, "mz.NetRunner: its NetPack has been destroyed");
+    return k;
+  }
 
   at::TensorOptions opt(const at::Tensor& like) const { return like.options().dtype(p->tdt()); }
   void scratch(const at::Tensor& like) {
@@ -463,10 +478,11 @@ struct NetRunner : torch::CustomClassHolder {
 };
 
 c10::intrusive_ptr<NetRunner> NetPack::runner(int64_t B, int64_t H, int64_t W) {
+  std::lock_guard<std::mutex> lk(runners_mu);
   auto key = std::make_tuple(B, H, W);
   auto it = runners.find(key);
   if (it != runners.end()) return it->second;
-  auto r = c10::make_intrusive<NetRunner>(this, B, H, W);
+  auto r = c10::make_intrusive<NetRunner>(c10::intrusive_ptr<NetPack>::unsafe_reclaim_from_nonowning(this), B, H, W);
   runners[key] = r;
   return r;
 }
@@ -488,13 +504,29 @@ void check_act_dtype(const RunPtr& rn, const at::Tensor& t, const char* name) {
 }
 
 // ---- NHWC acting-loop ops -------------------------------------------------------------------------
+// an optional node pool written at slot `slot` of every env: same dtype and device as the nets' activations,
+// and large enough for env B - 1's slot
+void check_pool(const RunPtr& rn, const c10::optional<at::Tensor>& pool, int64_t env_stride, int64_t slot) {
+  if (!(pool.has_value() && pool->defined())) return;
+  const int64_t n = rn->lhw * rn->p->c1;
+  check_act_dtype(rn, *pool, "pool");
+  check_dev(*pool, "pool");
+  TORCH_CHECK(pool->is_contiguous(), "mz: pool must be contiguous");
+  TORCH_CHECK(slot >= 0 && env_stride >= (slot + 1) * n, "mz: pool_env_stride ", env_stride, " cannot hold slot ", slot,
+              " of ", n, " elements");
+  TORCH_CHECK(pool->numel() >= (rn->B - 1) * env_stride + (slot + 1) * n, "mz: pool holds ", pool->numel(),
+              " elements, the runner's batch needs ", (rn->B - 1) * env_stride + (slot + 1) * n);
+}
+
 void representation_(const RunPtr& rn, const at::Tensor& x, at::Tensor& out, const c10::optional<at::Tensor>& pool,
                      int64_t pool_env_stride) {
+  const auto hold = rn->pin();
   const NetPack* p = rn->p;
   check_act_dtype(rn, x, "x");
   check_act_dtype(rn, out, "out");
   check_batch(rn, x, rn->HW * round64(2 * p->L), "x");
   check_batch(rn, out, rn->lhw * p->c1, "out");
+  check_pool(rn, pool, pool_env_stride, 0);
   rn->representation(x, out, pool, pool_env_stride);
 }
 
@@ -502,9 +534,17 @@ void dynamics_(const RunPtr& rn, const at::Tensor& src, int64_t env_stride, cons
                int64_t slot_stride, const at::Tensor& act, c10::optional<at::Tensor> out, at::Tensor& r_dec,
                const c10::optional<at::Tensor>& r_logits, const c10::optional<at::Tensor>& pool, int64_t pool_env_stride,
                int64_t pool_slot) {
+  const auto hold = rn->pin();
   const NetPack* p = rn->p;
+  const int64_t n = rn->lhw * p->c1;
   check_act_dtype(rn, src, "src");
   check_dev(src, "src");
+  // env b's latent starts at b * env_stride (+ slot[b] * slot_stride: slot values are device data, the
+  // caller's node-pool contract bounds them, as the reference's node dicts bound its parent lookups)
+  const int64_t es = env_stride <= 0 ? n : env_stride;  // 0: contiguous latents
+  TORCH_CHECK(es >= n && slot_stride >= 0 && src.is_contiguous() && src.numel() >= (rn->B - 1) * es + n,
+              "mz::dynamics_: src holds ", src.numel(), " elements, env_stride ", es, " needs ", (rn->B - 1) * es + n);
+  check_pool(rn, pool, pool_env_stride, pool_slot);
   if (out.has_value() && out->defined()) {
     check_act_dtype(rn, *out, "out");
     check_batch(rn, *out, rn->lhw * p->c1, "out");
@@ -523,6 +563,7 @@ void dynamics_(const RunPtr& rn, const at::Tensor& src, int64_t env_stride, cons
 // latents for a prediction step: a contiguous buffer of >= B latents, or a [>= B, n] view whose rows are
 // contiguous (e.g. one node-pool slot of every env); returns the env stride in elements
 int64_t latent_rows(const RunPtr& rn, const at::Tensor& h) {
+  rn->pin();  // raises if the pack is gone (the op's caller holds its own pin below)
   const int64_t n = rn->lhw * rn->p->c1;
   check_act_dtype(rn, h, "h");
   TORCH_CHECK(h.is_cuda(), "mz: h must be a device tensor");
@@ -537,6 +578,7 @@ int64_t latent_rows(const RunPtr& rn, const at::Tensor& h) {
 
 void prediction_(const RunPtr& rn, const at::Tensor& h, at::Tensor& pi, at::Tensor& v,
                  const c10::optional<at::Tensor>& pl, const c10::optional<at::Tensor>& vl) {
+  const auto hold = rn->pin();
   const int64_t hs = latent_rows(rn, h);
   check_batch(rn, pi, 3, "pi");
   check_batch(rn, v, 1, "v");
@@ -548,6 +590,7 @@ void prediction_tree_(const RunPtr& rn, const at::Tensor& h, at::Tensor& pi, at:
                       at::Tensor& depth, at::Tensor& path, const at::Tensor& sqrt_tab, const at::Tensor& c_tab, int64_t S,
                       int64_t env_offset, int64_t search_id, int64_t seed, const c10::optional<at::Tensor>& ctx,
                       int64_t sim, double gamma, const at::Tensor& r) {
+  const auto hold = rn->pin();
   const int64_t hs = latent_rows(rn, h);
   check_batch(rn, pi, 3, "pi");
   check_batch(rn, v, 1, "v");

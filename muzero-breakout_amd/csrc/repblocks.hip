@@ -29,10 +29,6 @@
 // (tests/test_gpu_repblocks.py).
 #include "common.h"
 
-#ifndef RF_SCHED
-#define RF_SCHED 1  // k-loop schedule: 1 per column tile (reads in column tile 0's MFMA slots 5-9); 6 the two
-                    // column tiles' MFMAs interleaved (towerp's TP_SCHED 6)
-#endif
 
 namespace {
 
@@ -139,57 +135,6 @@ __device__ __forceinline__ void rf_dy(const uint8_t* __restrict__ lds, int src, 
       for (int g = 0; g < 4; ++g) {
         const int nb = g < 3 ? xc + 5 * (g + 1) * cstr : xn;
         const bool last = g == 3;
-#if RF_SCHED == 6  // the two column tiles' MFMAs interleaved (per accumulator the same order)
-        auto grp = [&](const bf16x8(&f0)[5], bf16x8(&fn)[5]) {
-          bf16x8 f[5], fp;
-#pragma unroll
-          for (int j = 0; j < 5; ++j) f[j] = (DY == 0 || ok) ? f0[j] : bf16x8{};
-          fp = (DY == 0 || ok) ? fn[4] : bf16x8{};
-          bf16x8 w[3][2];
-#pragma unroll
-          for (int d = 0; d < 3; ++d)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) w[d][ct] = __builtin_bit_cast(bf16x8, bq[cc][d][ct]);
-#pragma unroll
-          for (int j = 0; j < 5; ++j)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) acc[5 * g + j][ct] = rf::mfma(w[1][ct], f[j], acc[5 * g + j][ct]);
-#pragma unroll
-          for (int j = 0; j < 5; ++j) fn[j] = *reinterpret_cast<const bf16x8*>(lds + nb + j * cstr);
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct)
-            if (g > 0) acc[5 * g][ct] = rf::mfma(w[0][ct], fp, acc[5 * g][ct]);
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) acc[5 * g + j + 1][ct] = rf::mfma(w[0][ct], f[j], acc[5 * g + j + 1][ct]);
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct)
-            if (g > 0) acc[5 * g - 1][ct] = rf::mfma(w[2][ct], f[0], acc[5 * g - 1][ct]);
-#pragma unroll
-          for (int j = 1; j < 5; ++j)
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct) acc[5 * g + j - 1][ct] = rf::mfma(w[2][ct], f[j], acc[5 * g + j - 1][ct]);
-          if (last) {
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-              for (int d = 0; d < 3; ++d)
-                bq[cc][d][ct] = __builtin_bit_cast(
-                    uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, ct * ts + (sn * d + st) * 1024, 0));
-          }
-          // the next group's 5 reads after 8 of the 10 dx = 0 MFMAs (fp is a copy of the previous group's
-          // last fragment taken before its register is reloaded)
-          __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-#pragma unroll
-          for (int j = 0; j < 5; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
-          if (last) __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);
-          __builtin_amdgcn_sched_barrier(0);
-        };
-#else
         auto grp = [&](const bf16x8(&f0)[5], bf16x8(&fn)[5]) {
           // every accumulator takes its taps in the band kernels' order dx = 0, -1, +1 within a (dy,
           // channel step): so column 5g's dx = -1 tap (source 5g - 1, the previous group's last
@@ -236,7 +181,6 @@ __device__ __forceinline__ void rf_dy(const uint8_t* __restrict__ lds, int src, 
           }
           __builtin_amdgcn_sched_barrier(0);
         };
-#endif
         if (((cc * 4 + g) & 1) == 0)
           grp(fa, fb);
         else

@@ -44,27 +44,11 @@ constexpr int TC = 256;            // channels
 constexpr int TROWB = TC * 2;      // 512 B per LDS row
 constexpr int TR = 5;              // 16-row tiles = latent columns x
 constexpr int TNS = 9 * TC / 32;   // 72 k steps per 3x3 conv
-#ifndef TOWER_TD
-#define TOWER_TD 4
-#endif
-constexpr int TD = TOWER_TD;       // 4-env 8-wave kernel's weight ring depth (k steps); divides a tap's 8
+constexpr int TD = 4;              // 4-env 8-wave kernel's weight ring depth (k steps); divides a tap's 8
 static_assert(8 % TD == 0, "ring index restarts at every tap");
 // tower8 weight ring depth in entries (one entry = one 1 KB fragment per column tile): two k steps of
 // the one-pass k loop (3 column shifts each); a ring entry count must divide the 24 of a dy
 template <int NQ> constexpr int t8d = 6;
-#ifndef T8_SCHED
-#define T8_SCHED 1  // tower8 one-pass k loop: 1 column-tile major; 6 the column tiles' MFMAs interleaved
-#endif
-#ifndef TOWER_ABLATE
-#define TOWER_ABLATE 0  // diagnostic builds of the 4-env 8-wave kernel only (make tower-variants): 1 hot
-                        // weights, 2 no LDS A reads, 3 duplicate weight streams (waves w, w+4), 4 = 3 with
-                        // waves 4-7 started late (tower8's own ablations went with its three-pass loop)
-#endif
-#if TOWER_ABLATE == 3 || TOWER_ABLATE == 4
-#define TOWER_CT0(wave) (2 * ((wave) & 3))
-#else
-#define TOWER_CT0(wave) (2 * (wave))
-#endif
 constexpr int TNT = 512;
 constexpr int IMG = TROWS * TROWB;         // one activation image (40 KB)
 constexpr int LDS_X = 0, LDS_T = IMG, LDS_Z = 2 * IMG, LDS_BYTES = 2 * IMG + 16 * TROWB;
@@ -175,20 +159,13 @@ __device__ __forceinline__ void tower_dx(const uint8_t* __restrict__ lds, int sr
       const int s = SB + dyi * NC + c;
       const typename Elt<EL>::v8 w0 = __builtin_bit_cast(typename Elt<EL>::v8, b0q[c % TD]);
       const typename Elt<EL>::v8 w1 = __builtin_bit_cast(typename Elt<EL>::v8, b1q[c % TD]);
-#if TOWER_ABLATE == 1  // diagnostic only: weights from one L1-resident k step
-      b0q[c % TD] = wp0[(size_t)((s + TD) & 1) * 64];
-      b1q[c % TD] = wp1[(size_t)((s + TD) & 1) * 64];
-#else
       b0q[c % TD] = wp0[(size_t)(s + TD) * 64];
       b1q[c % TD] = wp1[(size_t)(s + TD) * 64];
-#endif
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         acc0[A0 + j] = Elt<EL>::mfma(w0, afc[j], acc0[A0 + j]);
         acc1[A0 + j] = Elt<EL>::mfma(w1, afc[j], acc1[A0 + j]);
-        if (TOWER_ABLATE == 2)  // diagnostic only: no LDS A reads inside the loop
-          afn[j] = afc[j];
-        else if (c + 1 < NC)
+        if (c + 1 < NC)
           afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
         else
           afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
@@ -482,16 +459,10 @@ __global__ __launch_bounds__(TNT, 2) void tower_kernel(TowerArgs a) {
   const uint4* wf = reinterpret_cast<const uint4*>(a.wf);
   constexpr size_t WCONV = (size_t)16 * TNS * 64;  // uint4 per conv
   for (int blk = 0; blk < a.nblocks; ++blk) {
-#if TOWER_ABLATE == 4  // diagnostic: the duplicate-stream waves trail by ~1 k step so their loads hit L1
-    if (wave >= 4) __builtin_amdgcn_s_sleep(6);
-#endif
-    tower_conv<EL, 0, false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, TNS, TOWER_CT0(wave), a.bias + (2 * blk) * TC, 0,
+    tower_conv<EL, 0, false>(lds, LDS_X, LDS_T, wf + (2 * blk) * WCONV, TNS, 2 * wave, a.bias + (2 * blk) * TC, 0,
                          nullptr, nullptr, 0, lane);
     __syncthreads();
-#if TOWER_ABLATE == 4
-    if (wave >= 4) __builtin_amdgcn_s_sleep(6);
-#endif
-    tower_conv<EL, 1, false>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, TNS, TOWER_CT0(wave),
+    tower_conv<EL, 1, false>(lds, LDS_T, LDS_X, wf + (2 * blk + 1) * WCONV, TNS, 2 * wave,
                          a.bias + (2 * blk + 1) * TC, 0, nullptr, nullptr, 0, lane);
     __syncthreads();
   }
@@ -625,56 +596,6 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
       // then that tile's three ring slots are reloaded with the entries of the step after next (their
       // registers are free once its MFMAs have issued: no copies, a ring of two steps in the same
       // registers); the next step's A reads ride in the first column tile's MFMA slots
-#if T8_SCHED == 6
-      // the column tiles' MFMAs interleaved: every A fragment feeds its CT MFMAs back to back (per
-      // accumulator the same order; towerp_kernel's schedule 6), then every tile's ring slots reloaded
-      {
-        typename Elt<EL>::v8 w[3][CT];
-#pragma unroll
-        for (int d = 0; d < 3; ++d)
-#pragma unroll
-          for (int ct = 0; ct < CT; ++ct) w[d][ct] = __builtin_bit_cast(typename Elt<EL>::v8, bq[ct][(3 * c + d) % RD]);
-#pragma unroll
-        for (int j = 0; j < NA; ++j) {
-#pragma unroll
-          for (int ct = 0; ct < CT; ++ct) acc[j][ct] = Elt<EL>::mfma(w[1][ct], afc[j], acc[j][ct]);
-          if (c + 1 < NC)
-            afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
-          else
-            afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
-        }
-#pragma unroll
-        for (int j = 0; j < NA; ++j)
-          if (j % TX + 1 < TX)
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[j + 1][ct] = Elt<EL>::mfma(w[0][ct], afc[j], acc[j + 1][ct]);
-#pragma unroll
-        for (int j = 0; j < NA; ++j)
-          if (j % TX >= 1)
-#pragma unroll
-            for (int ct = 0; ct < CT; ++ct) acc[j - 1][ct] = Elt<EL>::mfma(w[2][ct], afc[j], acc[j - 1][ct]);
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-#pragma unroll
-          for (int d = 0; d < 3; ++d) {
-            int so = ct * (TNS * 1024) + (24 * d + dyi * NC + c + RD / 3) * 1024;
-            __amdgpu_buffer_rsrc_t rs = cur.rs;
-            if (3 * c + d + RD >= 3 * NC) {
-              const int nn = 3 * c + d + RD - 3 * NC;
-              so = last ? ct * nxt.tstride + t8_first(nxt, nn) * 1024 : so;
-              rs = last ? nxt.rs : cur.rs;
-            }
-            bq[ct][(3 * c + d) % RD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
-          }
-#pragma unroll
-        for (int j = 0; j < NA; ++j) {
-          __builtin_amdgcn_sched_group_barrier(0x008, CT, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, NM - CT * NA, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 3 * CT, 0);
-      }
-#else
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) {
         typename Elt<EL>::v8 w[3];
@@ -684,14 +605,10 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
         for (int j = 0; j < NA; ++j) {
           acc[j][ct] = Elt<EL>::mfma(w[1], afc[j], acc[j][ct]);
           if (ct == 0) {
-#if TOWER_ABLATE == 6  // diagnostic: no LDS A reads in the k loop (the fragments are reused)
-            afn[j] = afc[j];
-#else
             if (c + 1 < NC)
               afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + base + j * tst + (((4 * (c + 1) + q) << 4) ^ sw));
             else
               afn[j] = *reinterpret_cast<const typename Elt<EL>::v8*>(lds + nbase + j * ntst + ((q << 4) ^ nsw));
-#endif
           }
         }
 #pragma unroll
@@ -711,10 +628,6 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
             so = last ? ct * nxt.tstride + t8_first(nxt, nn) * 1024 : so;
             rs = last ? nxt.rs : cur.rs;
           }
-#if TOWER_ABLATE == 5  // diagnostic: every ring load re-reads 8 KB per column tile (L1-resident weights)
-          so = ct * (TNS * 1024) + ((3 * c + d) % 8) * 1024;
-          rs = cur.rs;
-#endif
           bq[ct][(3 * c + d) % RD] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, so, 0));
         }
         if (ct == 0) {
@@ -729,7 +642,6 @@ __device__ __forceinline__ void tower8_dall(const uint8_t* __restrict__ lds, con
         }
         __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
       }
-#endif
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < NA; ++j) afc[j] = afn[j];

@@ -22,12 +22,12 @@
 //   * weights: the tower packing ([col tile][pack step 24 (dx+1) + 8 (dy+1) + c][lane][8], 1 KB per
 //     fragment, agent.pack_tower_conv) through a two-k-step ring of 24 fragments in registers, each
 //     slot reloaded right after its last MFMA of the step; the ring runs across conv boundaries;
-//   * in place: k loop, barrier, write-back (ReLU, bf16), barrier. The block input that conv2
-//     adds back (the residual) cannot stay in LDS (no room beside the image) nor in registers (80
-//     accumulators leave no 160 VGPRs): conv1's write-back lifts it out of the image in the
-//     accumulator layout and parks it in a per-wave global scratch (40 x 1 KB per wave,
-//     L2 / Infinity-Cache resident), and the same lanes load it back before the barrier that
-//     ends conv1, so it lands while conv2's accumulators are initialised.
+//   * two 32-channel passes per conv (a wave's column tiles 0-1, then 2-3: 40 accumulators each);
+//     pass 0's result waits packed (ReLU, bf16) in registers for the write-back;
+//   * in place: k loops, barrier, write-back (ReLU, bf16), barrier. The block input that conv2
+//     adds back (the residual) cannot stay in LDS (no room beside the image): conv1's write-back
+//     lifts it out of the image at the wave's own output positions, in the accumulator layout, into
+//     registers (80 VGPRs), where conv2's accumulator init adds it.
 // The kernel fills one CU per workgroup: B = 4096 is exactly one round on 256 CUs. EL (elt.h): bf16, or fp16
 // for the fp16 dynamics net of config 5 (fp16 image, weights and MFMAs; latents in and out of HBM stay bf16,
 // converted on staging and in the epilogues, as tower8_kernel<1, NQ>, bit for bit).
@@ -35,20 +35,8 @@
 #include "tree_dev.h"
 #include "elt.h"  // Elt<EL>: bf16 (EL 0) / fp16 (EL 1, the fp16 dynamics net of config 5) images and weights
 
-#ifndef TP_SCHED
-// k-loop schedule (make towerp-sched / towerp-prod build the others): 6 the two column tiles' MFMAs
-// interleaved — each B fragment feeds two MFMAs back to back, the next row's reads after the 10 dx = 0
-// MFMAs; the same cycles within 0.4 % as 1 but the chip holds a 1-2 % higher clock under it (bench A/B
-// +1.0-1.2 %, profiles/r03/tp_sched); 1 per column tile, the current fragments' MFMAs first, then the next
-// reads; 5 as 1 without the fence between row steps; 7 as 6 without it; 8 as 6 with the reads among the
-// first dx = 0 pairs; 9 as 6 in snake order (no headline change)
-#define TP_SCHED 6
-#endif
 #ifndef TP_STAGE
 #define TP_STAGE 2  // staging batches per wave (2: two envs' 20 loads in flight at a time; 1: all four)
-#endif
-#ifndef TP_ABLATE
-#define TP_ABLATE 0  // diagnostic builds only (make towerp-ablate): 1 no LDS B reads in the k loop, 2 L1-resident weights
 #endif
 
 namespace {
@@ -160,38 +148,29 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
         const int yp = YLO + yi;
         const int nb = yi + 1 < NY ? xc + 5 * (yp + 1) * tp::PIX : xn + 5 * ynext * tp::PIX;
         const bool last = yi == NY - 1;
-#if TP_SCHED >= 6  // the two column tiles' MFMAs interleaved (per accumulator the same order)
         auto row = [&](const V8(&f)[5], V8(&fn)[5]) {
           V8 w[3][2];
 #pragma unroll
           for (int d = 0; d < 3; ++d)
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) w[d][ct] = __builtin_bit_cast(V8, bq[cc][d][ct]);
-          // TP_SCHED 9: snake order — the column tile alternates direction per source pixel, so every
-          // MFMA shares its A or its B operand with the one before it
 #pragma unroll
           for (int xp = 0; xp < 5; ++xp)
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              const int ct = TP_SCHED == 9 && (xp & 1) ? 1 - k : k;
+            for (int ct = 0; ct < 2; ++ct)
               acc[(yp - DY) * 5 + xp][ct] = Elt<EL>::mfma(w[1][ct], f[xp], acc[(yp - DY) * 5 + xp][ct]);
-            }
 #pragma unroll
           for (int xp = 0; xp < 5; ++xp) fn[xp] = *reinterpret_cast<const V8*>(lds + nb + xp * tp::PIX);
 #pragma unroll
           for (int xp = 0; xp < 4; ++xp)
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              const int ct = TP_SCHED == 9 && !(xp & 1) ? 1 - k : k;
+            for (int ct = 0; ct < 2; ++ct)
               acc[(yp - DY) * 5 + xp + 1][ct] = Elt<EL>::mfma(w[0][ct], f[xp], acc[(yp - DY) * 5 + xp + 1][ct]);
-            }
 #pragma unroll
           for (int xp = 1; xp < 5; ++xp)
 #pragma unroll
-            for (int k = 0; k < 2; ++k) {
-              const int ct = TP_SCHED == 9 && (xp & 1) ? 1 - k : k;
+            for (int ct = 0; ct < 2; ++ct)
               acc[(yp - DY) * 5 + xp - 1][ct] = Elt<EL>::mfma(w[2][ct], f[xp], acc[(yp - DY) * 5 + xp - 1][ct]);
-            }
           if (last) {
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct)
@@ -200,14 +179,7 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
                 bq[cc][d][ct] = __builtin_bit_cast(
                     uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, ct * tp::CTB + (24 * d + st) * 1024, 0));
           }
-#if TP_SCHED == 8  // the next row's reads among the first dx = 0 pairs
-#pragma unroll
-          for (int j = 0; j < 5; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
-#else  // 6, 7: after 8 of the 10 dx = 0 MFMAs, the reads ride in the next 5 slots
+          // after 8 of the 10 dx = 0 MFMAs, the next row's 5 reads ride in the next 5 MFMA slots
           __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
 #pragma unroll
           for (int j = 0; j < 5; ++j) {
@@ -215,89 +187,9 @@ __device__ __forceinline__ void tp_dy(const uint8_t* __restrict__ lds, int lb, i
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           }
           __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
-#endif
           if (last) __builtin_amdgcn_sched_group_barrier(0x020, 6, 0);
-#if TP_SCHED != 7  // 7: no scheduling fence between row steps
           __builtin_amdgcn_sched_barrier(0);
-#endif
         };
-#else
-        auto row = [&](const V8(&f)[5], V8(&fn)[5]) {
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) {
-            const V8 w0 = __builtin_bit_cast(V8, bq[cc][0][ct]);
-            const V8 w1 = __builtin_bit_cast(V8, bq[cc][1][ct]);
-            const V8 w2 = __builtin_bit_cast(V8, bq[cc][2][ct]);
-            // dx = 0 first (its 5 MFMA slots carry the next row step's 5 reads), then dx = -1
-            // (input x' feeds output x' + 1) and dx = +1 (output x' - 1)
-#pragma unroll
-            for (int xp = 0; xp < 5; ++xp) {
-              acc[(yp - DY) * 5 + xp][ct] = Elt<EL>::mfma(w1, f[xp], acc[(yp - DY) * 5 + xp][ct]);
-#if TP_ABLATE == 1  // diagnostic only: no LDS B reads in the k loop (the fragments are reused)
-              if (ct == 0) fn[xp] = f[xp];
-#else
-              if (ct == 0) fn[xp] = *reinterpret_cast<const V8*>(lds + nb + xp * tp::PIX);
-#endif
-            }
-#pragma unroll
-            for (int xp = 0; xp < 4; ++xp) acc[(yp - DY) * 5 + xp + 1][ct] = Elt<EL>::mfma(w0, f[xp], acc[(yp - DY) * 5 + xp + 1][ct]);
-#pragma unroll
-            for (int xp = 1; xp < 5; ++xp) acc[(yp - DY) * 5 + xp - 1][ct] = Elt<EL>::mfma(w2, f[xp], acc[(yp - DY) * 5 + xp - 1][ct]);
-            if (last) {
-#pragma unroll
-              for (int d = 0; d < 3; ++d)
-#if TP_ABLATE == 2  // diagnostic only: every ring load re-reads an 8 KB L1-resident slice of the pack
-                bq[cc][d][ct] = __builtin_bit_cast(
-                    uint4, __builtin_amdgcn_raw_buffer_load_b128(cur.rs, lane * 16, ct * tp::CTB + ((3 * cc + d) & 3) * 1024, 0));
-#else
-                bq[cc][d][ct] = __builtin_bit_cast(
-                    uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, ct * tp::CTB + (24 * d + st) * 1024, 0));
-#endif
-            }
-#if TP_SCHED == 0
-            if (ct == 0) {
-#pragma unroll
-              for (int j = 0; j < 5; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-              }
-              __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-            } else {
-              __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
-            }
-            if (last) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
-#elif TP_SCHED == 1 || TP_SCHED == 5  // the current fragments' MFMAs first (one wait), the next row's reads after them
-            if (ct == 0) {
-              __builtin_amdgcn_sched_group_barrier(0x008, 5, 0);
-#pragma unroll
-              for (int j = 0; j < 5; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-              }
-              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-            } else {
-              __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
-            }
-            if (last) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
-#elif TP_SCHED == 3  // reads spread over ct 0's MFMAs (one per two slots)
-            if (ct == 0) {
-#pragma unroll
-              for (int j = 0; j < 5; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-              }
-              __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-            } else {
-              __builtin_amdgcn_sched_group_barrier(0x008, 13, 0);
-            }
-            if (last) __builtin_amdgcn_sched_group_barrier(0x020, 3, 0);
-#endif  // TP_SCHED 2: the compiler's own order
-          }
-#if TP_SCHED != 5  // 5 (diagnostic): no scheduling fence between row steps
-          __builtin_amdgcn_sched_barrier(0);
-#endif
-        };
-#endif
         if (((cc * NY + yi) & 1) == 0)
           row(fa, fb);
         else
@@ -485,18 +377,46 @@ __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* 
   PSTAMP(4 + 5 * ci);
   __syncthreads();  // every wave has read the whole image
   PSTAMP(5 + 5 * ci);
+  // Write-back in whole 16-B chunks: lanes of k quarters q and q ^ 1 (rows 2j, 2j + 1 of the wave)
+  // hold the two 8-B halves of the same chunk (channels ch and ch + 4 of row n). For a pixel pair
+  // (p, p + 1) one v_permlane16_swap per dword hands q-odd lanes' pixel-p half to the q-even lane and
+  // the q-even lanes' pixel-(p + 1) half to the q-odd lane: the q-even lane then stores pixel p's chunk,
+  // the q-odd lane pixel p + 1's — 40 ds_write_b128 per wave instead of 80 ds_write_b64, each lane
+  // group of 16 covering the 16 distinct swizzled chunks of its rows (every bank once). conv1's read of
+  // the residual loads the same chunks and swaps back into the accumulator layout (the swap is an
+  // involution). Data movement only: the image is bit-identical.
   int cofs[tp::CT];
 #pragma unroll
-  for (int ct = 0; ct < tp::CT; ++ct) cofs[ct] = tp_cofs(64 * wave + 16 * ct + 4 * q, n);
-  // one pixel at a time (a scheduling barrier per pixel: hoisting every accumulator read ahead of the
+  for (int ct = 0; ct < tp::CT; ++ct)
+    cofs[ct] = n * tp::ROWB + ((((64 * wave + 16 * ct + 4 * q) >> 3) ^ n) << 4) + (q & 1) * tp::PIX;
+  // opaque per conv: left loop-invariant, the compiler hoists the 40 pixel-pair addresses out of the block
+  // loop and spills them across the k loops
+#pragma unroll
+  for (int ct = 0; ct < tp::CT; ++ct) asm volatile("" : "+v"(cofs[ct]));
+  auto swap2 = [](uint2& a, uint2& b) {
+    const auto x = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+    const auto y = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+    a = make_uint2(x[0], y[0]);
+    b = make_uint2(x[1], y[1]);
+  };
+  // one pixel pair at a time (a scheduling barrier per pair: hoisting every accumulator read ahead of the
   // stores spilled the packed first-pass output)
 #pragma unroll
-  for (int p = 0; p < tp::P; ++p) {
+  for (int p = 0; p < tp::P; p += 2) {
 #pragma unroll
     for (int ct = 0; ct < tp::CT; ++ct) {
-      uint2* ptr = reinterpret_cast<uint2*>(lds + p * tp::PIX + cofs[ct]);
-      if (SAVE) res[ct >> 1][p][ct & 1] = *ptr;
-      *ptr = ct < 2 ? out0[p][ct] : tp_pack<EL>(acc[p][ct - 2]);
+      uint4* ptr = reinterpret_cast<uint4*>(lds + p * tp::PIX + cofs[ct]);
+      if (SAVE) {
+        const uint4 r = *ptr;
+        uint2 r0 = make_uint2(r.x, r.y), r1 = make_uint2(r.z, r.w);
+        swap2(r0, r1);
+        res[ct >> 1][p][ct & 1] = r0;
+        res[ct >> 1][p + 1][ct & 1] = r1;
+      }
+      uint2 a = ct < 2 ? out0[p][ct] : tp_pack<EL>(acc[p][ct - 2]);
+      uint2 b = ct < 2 ? out0[p + 1][ct] : tp_pack<EL>(acc[p + 1][ct - 2]);
+      swap2(a, b);
+      *ptr = make_uint4(a.x, a.y, b.x, b.y);
     }
     __builtin_amdgcn_sched_barrier(0);
   }

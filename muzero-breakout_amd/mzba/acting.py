@@ -65,12 +65,15 @@ class ActingLoop:
         (default env_offset + B); `rep_agent`: the net of the root representation when it differs
         from the search's (run_test_simulation: learner net for the root, target net in the search);
         `pow_threads`: intra-op threads of the reference's torch process, which split its visit-count
-        pow into per-thread chunks from 32768 elements on (default: this process's torch threads)."""
+        pow into per-thread chunks from 32768 elements on (3 x n_envs_total >= 32768); default
+        cfg["pow_threads"], else 1."""
         self.cfg, self.agent, self.B = cfg, agent, B
         self.seed, self.env_offset = seed, env_offset
         self.n_envs_total = env_offset + B if n_envs_total is None else n_envs_total
         self.max_steps = max_steps
-        self.pow_threads = torch.get_num_threads() if pow_threads is None else pow_threads
+        # the reference process's intra-op thread count is a property of ITS launch, not of this one:
+        # explicit (argument, else cfg["pow_threads"], else 1 — what the oracle assumes), never inferred
+        self.pow_threads = int(cfg.get("pow_threads", 1) if pow_threads is None else pow_threads)
         dev = agent.device
         # graph-replayable schedule values (train_torch.py:129-135): 1/T in double for the sampling
         # kernel, (f32(1 - noise_weight), f32(noise_weight)) for the root expansion
@@ -212,28 +215,33 @@ class ActingLoop:
     def trajectories(self):
         """Per-env ObservationTrajectory exactly as _pad_initial_state + add_observation
         build them (31 padding frames of g(s0), 32 padding actions 0, then the records)."""
-        T = self.t
-        B, L_ = self.B, self.Lh
-        H, W = self.H, self.W
-        rec = {k: (v[:T].cpu().numpy() if v is not None else None) for k, v in self.rec.items()}
-        lut = gray_lut()
-        f0 = self.frame0.view(B, H * W).cpu().numpy()
-        out = []
-        for b in range(B):
-            m = rec["mask"][:, b].astype(bool)
-            acts = [self.env.pad_action] * L_ + [int(a) for a in rec["action"][m, b]]
-            pad = torch.from_numpy(lut[f0[b] & 7].reshape(1, H, W))
-            states = [pad] * (L_ - 1)
-            if rec["frame"] is not None:
-                states += [torch.from_numpy(lut[f & 7].reshape(1, H, W)) for f in rec["frame"][m, b]]
-            rews = [0] * L_ + [float(r) for r in rec["reward"][m, b]]
-            vc = [torch.zeros(3)] * L_ + [torch.from_numpy(c) for c in rec["counts"][m, b]]
-            vals = [0.0] * L_ + [float(v) for v in rec["values"][m, b]]
-            rs = np.float32(0)
-            for r in rec["reward"][m, b]:
-                rs = np.float32(rs + r)
-            out.append(ObservationTrajectory(acts, states, rews, vc, vals, int(m.sum()), float(rs)))
-        return out
+        return trajectories_from_records(self.rec, self.frame0, self.t, self.Lh, self.H, self.W, self.env.pad_action)
+
+
+def trajectories_from_records(rec, frame0, T, L_, H, W, pad_action=0):
+    """The sink's first T rows (dict of (T_max, B, ...) tensors) + the u8 g(s0) codes (B*H*W) ->
+    one ObservationTrajectory per env, as _pad_initial_state (train_torch.py:313-332) and the
+    recording loop (:204-209) build them."""
+    rec = {k: (v[:T].cpu().numpy() if v is not None else None) for k, v in rec.items()}
+    B = rec["action"].shape[1]
+    lut = gray_lut()
+    f0 = frame0.reshape(B, H * W).cpu().numpy()
+    out = []
+    for b in range(B):
+        m = rec["mask"][:, b].astype(bool)
+        acts = [pad_action] * L_ + [int(a) for a in rec["action"][m, b]]
+        pad = torch.from_numpy(lut[f0[b] & 7].reshape(1, H, W))
+        states = [pad] * (L_ - 1)
+        if rec.get("frame") is not None:
+            states += [torch.from_numpy(lut[f & 7].reshape(1, H, W)) for f in rec["frame"][m, b]]
+        rews = [0] * L_ + [float(r) for r in rec["reward"][m, b]]
+        vc = [torch.zeros(3)] * L_ + [torch.from_numpy(c) for c in rec["counts"][m, b]]
+        vals = [0.0] * L_ + [float(v) for v in rec["values"][m, b]]
+        rs = np.float32(0)
+        for r in rec["reward"][m, b]:
+            rs = np.float32(rs + r)
+        out.append(ObservationTrajectory(acts, states, rews, vc, vals, int(m.sum()), float(rs)))
+    return out
 
 
 def run_test_simulation(cfg, agent, batch=2, seed=0, episode=0, max_steps_test=200, temperature=0.1,
@@ -268,16 +276,38 @@ def run_test_simulation(cfg, agent, batch=2, seed=0, episode=0, max_steps_test=2
 
 
 class ActingStage:
-    """Mirror of RLSystem._acting_stage (train_torch.py:160-169): `num_episodes` episodes of
-    `n_parallel` envs with the target agent, returning the per-env ObservationTrajectory
-    lists (what the reference hands to ReplayBuffer.save_observation_trajectory).
+    """Mirror of RLSystem._acting_stage (train_torch.py:160-169): `num_episodes` episodes of the
+    `n_parallel` envs of cfg with the target agent, each run until every env is done or after 261 steps
+    (:184-187), the records going where the reference sends them (:222-225).
+
+    Sharded: with `world_size` > 1 (one process per GPU, torch.distributed initialised —
+    backend "nccl" = RCCL over xGMI) rank r runs the global envs [r*B, (r+1)*B), B = n_parallel /
+    world_size, every random draw keyed on the global env id and the temperature pow on the envs'
+    global positions (n_envs_total = n_parallel); the ranks step in lockstep until the whole global batch
+    is done (one all-reduce of a live flag per step), and every `record_k` steps their record rows are
+    gathered to rank 0 (`mzba.shard.ShardedSink`). Rank 0 then holds the episode as one loop over the
+    global batch would have recorded it, bit for bit, and saves it into `replay_buffer`
+    (`DeviceReplayBuffer.ingest_records`: windows + n-step targets of every trajectory longer than K + 1,
+    in global env order) and/or returns the per-env ObservationTrajectory lists.
     `temperature` / `noise_weight` follow the caller's schedule (train_torch.py:129-135)."""
 
-    def __init__(self, cfg, agent, seed=0, env_offset=0, use_graph=True):
+    def __init__(self, cfg, agent, seed=0, env_offset=0, use_graph=True, world_size=1, rank=0, record_k=16,
+                 pow_threads=None, max_steps=ActingLoop.MAX_STEPS, height=16, width=20):
+        n = cfg["n_parallel"]
+        if world_size < 1 or not 0 <= rank < world_size or n % world_size:
+            raise ValueError(f"ActingStage: n_parallel {n} must split evenly over world_size {world_size}")
         self.cfg = cfg
-        self.loop = ActingLoop(cfg, agent, cfg["n_parallel"], seed=seed, env_offset=env_offset)
+        self.world, self.rank = world_size, rank
+        B = n // world_size
+        self.loop = ActingLoop(cfg, agent, B, seed=seed, env_offset=env_offset + rank * B,
+                               n_envs_total=env_offset + n, pow_threads=pow_threads, max_steps=max_steps,
+                               height=height, width=width)
         self.use_graph = use_graph
         self.num_episodes = cfg["num_episodes"]
+        self.sink = None
+        if world_size > 1:
+            from .shard import ShardedSink
+            self.sink = ShardedSink(world_size, rank, record_k, B, height * width, max_steps, agent.device)
 
     @property
     def temperature(self):
@@ -290,14 +320,40 @@ class ActingStage:
     def set_noise_weight(self, w):
         self.loop.search.noise_weight = w  # copied to the device before the next step
 
-    def run(self):
-        out = []
-        for _ in range(self.num_episodes):
-            loop = self.loop
-            loop.reset()
-            while not loop.all_done() and loop.t < loop.max_steps:
-                loop.act()
-                if self.use_graph and loop.graph is None:
-                    loop.capture()
-            out.append(loop.trajectories())
-        return out
+    def _all_done(self):
+        if self.sink is None:
+            return self.loop.all_done()
+        from .shard import all_ranks_done
+        return all_ranks_done(self.loop.env.done)
+
+    def run_episode(self, replay_buffer=None, trajectories=True):
+        """One episode (_acting_stage :166-167 + _run_episode :171-233). Returns the per-env
+        ObservationTrajectory list of the global batch on rank 0 (None elsewhere, or when not
+        `trajectories`); rank 0 saves the episode into `replay_buffer` when one is given."""
+        loop, sink = self.loop, self.sink
+        if sink is not None:
+            sink.gather.fence()
+        loop.reset()
+        if sink is not None:
+            sink.begin(loop.frame0)
+        while not self._all_done() and loop.t < loop.max_steps:
+            loop.act()
+            if self.use_graph and loop.graph is None:
+                loop.capture()
+            if sink is not None:
+                sink.push(loop.rec, loop.t)
+        if sink is not None:
+            rec, frame0 = sink.finish(loop.rec, loop.t)
+        else:
+            rec, frame0 = loop.rec, loop.frame0
+        if self.rank != 0:
+            return None
+        if replay_buffer is not None:
+            replay_buffer.ingest_records(rec, frame0.reshape(-1, loop.H * loop.W), loop.t)
+        if trajectories:
+            return trajectories_from_records(rec, frame0, loop.t, loop.Lh, loop.H, loop.W, loop.env.pad_action)
+        return None
+
+    def run(self, replay_buffer=None, trajectories=True):
+        """`num_episodes` episodes -> a list of run_episode results."""
+        return [self.run_episode(replay_buffer, trajectories) for _ in range(self.num_episodes)]

@@ -8,12 +8,13 @@ flatten order to the NHWC (h,w,c) order. Activations are NHWC on the device in b
 (throughput path) or f32 (parity path), computed by the HIP kernels in libmzba.so.
 """
 import math
+from collections import OrderedDict
 
 import numpy as np
 import torch
 
 from . import _lib as L
-from .weights import rep_layout, state_dict_spec
+from .weights import rep_layout, state_dict_spec, torch_init_state_dict
 
 BN_EPS = 1e-5
 DT_CODE = {"f32": 0, "bf16": 1}
@@ -470,6 +471,16 @@ class MuZeroAgent:
 
     cfg: the reference's `model` config dict. Extra key `dtype` ("bf16" | "f32",
     default "bf16") selects the device precision; "f32" is the parity mode.
+
+    Like the reference agent (networks.py:245-266) it holds weights from construction on: the
+    reference's own default initialisation drawn from torch's global CPU generator in module order
+    (`weights.torch_init_state_dict`, bit-identical under the same seed), so RLSystem.__init__'s
+    `target.load_state_dict(learner.state_dict())` and `for p in target.parameters():
+    p.requires_grad = False` (train_torch.py:86-98) work unchanged. The host copy (`state_dict()`,
+    `parameters()`: CPU tensors in the reference's keys and order) is the source of truth; the device
+    pack (`packed`: BN folded, kernel layouts) is built from it on first use and refreshed in place by
+    every `load_state_dict`. Training (`optimizer`, `train_mode`, train_torch.py:369-452) is served by
+    `mzba.learner.Learner`, not by this class.
     """
 
     def __init__(self, cfg, dtype=None, device="cuda", dyn_dtype=None):
@@ -478,13 +489,40 @@ class MuZeroAgent:
         self.device = torch.device(device)
         self.dtype = dtype or cfg.get("dtype", "bf16")
         self.dyn_dtype = dyn_dtype or cfg.get("dyn_dtype")  # "fp16": fp16 dynamics net (BASELINE config 5)
-        self.packed = None
+        self._packed = None
         self._runners = {}
         self._sd = None
+        self._set_host(torch_init_state_dict(cfg))
 
     # reference API ---------------------------------------------------------------------
+    def _set_host(self, sd):
+        """The host copy in the reference's key order: float entries as nn.Parameter (trainable
+        ones) / plain tensors (BN running statistics), the BN counters as int64."""
+        spec = state_dict_spec(self.cfg)
+        out = OrderedDict()
+        for k, _ in spec:
+            t = torch.as_tensor(_np(sd[k]).copy())
+            if k.endswith("num_batches_tracked"):
+                out[k] = t.to(torch.int64)
+            elif k.endswith(("running_mean", "running_var")):
+                out[k] = t.to(torch.float32)
+            else:
+                out[k] = torch.nn.Parameter(t.to(torch.float32))
+        self._sd = out
+
     def state_dict(self):
-        return self._sd
+        """OrderedDict of the reference's keys (networks.py's module order), detached CPU tensors."""
+        return OrderedDict((k, v.detach()) for k, v in self._sd.items())
+
+    def named_parameters(self):
+        return ((k, v) for k, v in self._sd.items() if isinstance(v, torch.nn.Parameter))
+
+    def parameters(self):
+        """The trainable tensors in nn.Module.parameters() order (the state_dict minus the BN buffers)."""
+        return (v for _, v in self.named_parameters())
+
+    def buffers(self):
+        return (v for k, v in self._sd.items() if not isinstance(v, torch.nn.Parameter))
 
     def load_state_dict(self, sd):
         spec = state_dict_spec(self.cfg)
@@ -494,15 +532,26 @@ class MuZeroAgent:
         for k, shape in spec:
             if tuple(np.shape(_np(sd[k]))) != tuple(shape):
                 raise ValueError(f"shape mismatch for {k}: {np.shape(_np(sd[k]))} vs {shape}")
-        self._sd = {k: _np(sd[k]).copy() for k, _ in spec}
-        packed = PackedNets(self._sd, self.cfg, self.dtype, self.device, self.dyn_dtype)
-        if self.packed is None:
-            self.packed = packed
-        else:  # a refresh: new weights into the existing buffers, live loops and graphs keep working
-            self.packed.refresh_from(packed)
+        self._set_host(sd)
+        if self._packed is not None:  # a refresh: new weights into the existing buffers, live loops and
+            self._packed.refresh_from(self._pack())  # captured graphs run them from their next launch
+
+    def _pack(self):
+        return PackedNets({k: _np(v) for k, v in self._sd.items()}, self.cfg, self.dtype, self.device, self.dyn_dtype)
+
+    @property
+    def packed(self):
+        """The device pack of the current weights (built on first use)."""
+        if self._packed is None:
+            self._packed = self._pack()
+        return self._packed
 
     def eval_mode(self):
         pass  # BN always uses running stats on this path (networks.py:336-342)
+
+    def train_mode(self):
+        raise NotImplementedError("training runs on mzba.learner.Learner (train_torch.py:369-452); the acting "
+                                  "agent is eval-only")
 
     def runner(self, B, H, W):
         key = (B, H, W)

@@ -20,8 +20,14 @@ from . import _lib as L
 
 
 class BreakoutEnvironment:
-    def __init__(self, cfg, width=10, height=15, paddle_width=6, brick_rows=3, device="cuda", seed=0, env_offset=0):
+    def __init__(self, cfg, width=10, height=15, paddle_width=6, brick_rows=3, device="cuda", seed=0, env_offset=0,
+                 state_device="cpu"):
+        """`device`: where the kernels run; `state_device`: where reset() returns the state — the CPU,
+        like the reference's env (parallel_breakout.py:80 `self.device = "cpu"`), so the reference's
+        `_prepare_mcts_input` can concatenate it with its CPU action planes (train_torch.py:271-276).
+        step() returns its outputs on the device of the state it is given."""
         L.require_gpu()
+        self.state_device = torch.device(state_device)
         self.height = 16  # parallel_breakout.py:76-79 (hard-coded by the reference)
         self.width = 20
         self.paddle_width = paddle_width
@@ -61,7 +67,7 @@ class BreakoutEnvironment:
         L.ops().env_reset_(state, self.ball_dx, self.ball_dy, self.paddle_width, self.brick_rows, self.seed,
                            self.episode, self.env_offset, pr)
         self.episode += 1
-        return state, 0
+        return state.to(self.state_device), 0
 
     def get_valid_actions(self, state, paddle_pos_new):
         """parallel_breakout.py:141-155."""

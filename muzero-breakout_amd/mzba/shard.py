@@ -84,11 +84,18 @@ class TrajectoryGather:
             self.host = torch.zeros(world_size, k_steps, B, rec_bytes(hw), dtype=torch.uint8,
                                     pin_memory=pin and self.device.type == "cuda")
 
-    def exchange(self, rec, t0, t1):
+    def exchange(self, rec, t0, t1, into=None, to_host=True):
         """Records of steps [t0, t1) (t1 - t0 <= k) of every rank -> rank 0. Every rank calls it.
         With torch.distributed initialised the collective runs at any world size (RCCL on the
-        device with backend "nccl"; gloo moves host copies)."""
+        device with backend "nccl"; gloo moves host copies). Rank 0 then unpacks the rows into
+        `into` (a dict of (T, world*B, ...) device tensors in global env order, rows [t0, t1)) and/or
+        copies them to its pinned host buffer (`to_host`), on the same side stream."""
         n = t1 - t0
+        if not 0 < n <= self.k:
+            raise ValueError(f"exchange: {n} rows, the slab holds 1..{self.k}")
+        distributed = dist.is_available() and dist.is_initialized()
+        if self.ws > 1 and not distributed:
+            raise RuntimeError("TrajectoryGather: world_size > 1 needs torch.distributed initialised")
         cuda = self.device.type == "cuda"
         if cuda:
             if self.side is None:
@@ -104,7 +111,7 @@ class TrajectoryGather:
             if cuda:
                 self.packed = torch.cuda.Event()
                 self.packed.record()
-            if dist.is_available() and dist.is_initialized():
+            if distributed:
                 if dist.get_backend() == "gloo" and cuda:
                     # gloo gathers host tensors only (CPU tests, and bench.py's one-GPU rehearsal)
                     gl = [torch.empty_like(self.slab, device="cpu") for _ in range(self.ws)] if self.rank == 0 else None
@@ -116,12 +123,25 @@ class TrajectoryGather:
                     dist.gather(self.slab, gl, dst=0)
             elif self.rank == 0:
                 self.gathered[0].copy_(self.slab)
-            if self.rank == 0:
+            if self.rank == 0 and into is not None:
+                g = self.gathered[:, :n].permute(1, 0, 2, 3).reshape(n, self.ws * self.B, -1)
+                for k, v in unpack_records(g).items():
+                    if into.get(k) is not None:
+                        into[k][t0:t1].copy_(v)
+            if self.rank == 0 and to_host:
                 self.host.copy_(self.gathered, non_blocking=True)
                 if cuda:  # host_records() waits for exactly this copy
                     self.copied = torch.cuda.Event()
                     self.copied.record()
+            if cuda:
+                self.landed = torch.cuda.Event()
+                self.landed.record()
         return n
+
+    def wait_landed(self):
+        """The current stream waits for the last exchange's unpack into `into` (rank 0)."""
+        if getattr(self, "landed", None) is not None:
+            torch.cuda.current_stream(self.device).wait_event(self.landed)
 
     def fence(self):
         """The acting stream waits until the last exchange has packed its rows (call before the
@@ -135,6 +155,78 @@ class TrajectoryGather:
             self.copied.synchronize()
         h = self.host[:, :n].permute(1, 0, 2, 3).reshape(n, self.ws * self.B, -1)
         return unpack_records(h)
+
+
+def gather_rows(x, world_size, rank):
+    """Rank 0 <- every rank's (B, ...) tensor, concatenated in rank order (global env order); the other
+    ranks get None. Used once per episode for the g(s0) frames the padded trajectories start from
+    (train_torch.py:167, _pad_initial_state :313-332)."""
+    if world_size == 1:
+        return x
+    gloo_cuda = dist.get_backend() == "gloo" and x.device.type == "cuda"
+    src = x.cpu() if gloo_cuda else x.contiguous()
+    gl = [torch.empty_like(src) for _ in range(world_size)] if rank == 0 else None
+    dist.gather(src, gl, dst=0)
+    return torch.cat(gl).to(x.device) if rank == 0 else None
+
+
+def all_ranks_done(local_done):
+    """True when every env of every rank is done (`torch.all(done_mask == True)` over the global batch,
+    train_torch.py:184): the ranks keep stepping in lockstep until then, so the step index, the search
+    id and every keyed draw stay those of the one global loop. local_done: this rank's done flags."""
+    live = (local_done != 0).logical_not().any().to(torch.int32).reshape(1)
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if dist.get_backend() == "gloo" and live.device.type == "cuda":
+            live = live.cpu()
+        dist.all_reduce(live, op=dist.ReduceOp.MAX)
+    return int(live.item()) == 0
+
+
+class ShardedSink:
+    """Rank 0's device copy of one episode's records of ALL ranks, in global env order: every k steps the
+    ranks' record rows go through a TrajectoryGather straight into (T, world*B, ...) tensors, which the
+    replay ingest (replay_buffer.py:96-165 via DeviceReplayBuffer.ingest_records) and the trajectory
+    lists read as if one loop had run the global batch. Every rank calls begin / push / finish."""
+
+    KEYS = ("action", "reward", "mask", "frame", "counts", "values")
+
+    def __init__(self, world_size, rank, k_steps, B, hw, max_steps, device):
+        self.ws, self.rank, self.k, self.B, self.hw = world_size, rank, k_steps, B, hw
+        self.device = torch.device(device)
+        self.gather = TrajectoryGather(world_size, rank, k_steps, B, hw, device, pin=False)
+        self.rec = self.frame0 = None
+        if rank == 0:
+            n, T, dev = world_size * B, max_steps, self.device
+            self.rec = {"action": torch.zeros(T, n, dtype=torch.uint8, device=dev),
+                        "reward": torch.zeros(T, n, dtype=torch.float32, device=dev),
+                        "mask": torch.zeros(T, n, dtype=torch.uint8, device=dev),
+                        "frame": torch.zeros(T, n, hw, dtype=torch.uint8, device=dev),
+                        "counts": torch.zeros(T, n, 3, dtype=torch.int64, device=dev),
+                        "values": torch.zeros(T, n, dtype=torch.float32, device=dev)}
+        self.t0 = 0
+
+    def begin(self, frame0):
+        """A new episode: frame0 = this rank's u8 g(s0) codes (B, H*W)."""
+        self.gather.fence()  # the loop's record rows restart at 0: after the last pack read them
+        self.frame0 = gather_rows(frame0.reshape(self.B, self.hw), self.ws, self.rank)
+        self.t0 = 0
+
+    def push(self, rec, t, final=False):
+        """The loop has written rows [0, t): exchange the rows since the last push every k steps (and
+        at the end of the episode)."""
+        if t - self.t0 >= self.k or (final and t > self.t0):
+            while self.t0 < t:
+                t1 = min(t, self.t0 + self.k)
+                self.gather.exchange(rec, self.t0, t1, into=self.rec, to_host=False)
+                self.t0 = t1
+
+    def finish(self, rec, t):
+        """End of episode (t rows): rank 0 gets (records, frame0) in global env order, ready on its
+        current stream; the other ranks get (None, None)."""
+        self.push(rec, t, final=True)
+        if self.device.type == "cuda":
+            self.gather.wait_landed()
+        return (self.rec, self.frame0) if self.rank == 0 else (None, None)
 
 
 def broadcast_state_dict(mcfg, state_dict, device, src=0):

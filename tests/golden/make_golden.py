@@ -759,10 +759,33 @@ def make_learner(cfg):
         np.savez_compressed(os.path.join(HERE, f"learner_{tag}.npz"), **out)
 
 
+# --------------------------------------------------------------------------------------
+def make_agent_init(cfg):
+    """The reference agent's own random initialisation (networks.py:245-266, MuZeroAgent(cfg) as
+    RLSystem.__init__ builds it twice, train_torch.py:86-88) under torch.manual_seed(s): the small
+    and the full-width model's state_dicts as per-tensor checksums (f64 sum, sum of |x|, first 4 and
+    last elements), for the learner agent and the target agent built right after it."""
+    reference_modules()
+    from src.networks import MuZeroAgent
+    out = {}
+    for tag, mcfg in (("small", small_model_cfg(cfg)), ("full", {**cfg["model"], "device": "cpu"})):
+        for seed in (42, 7):
+            torch.manual_seed(seed)
+            agents = [MuZeroAgent(mcfg), MuZeroAgent(mcfg)]  # self.mu_zero, self.mu_zero_target
+            for ai, ag in enumerate(agents):
+                for k, v in ag.state_dict().items():
+                    a = v.detach().cpu().numpy()
+                    key = f"{tag}/s{seed}/a{ai}/{k}"
+                    f = a.astype(np.float64).reshape(-1)
+                    out[key] = np.concatenate([[f.sum(), np.abs(f).sum()], f[:4], f[-1:]])
+            print("agent_init", tag, seed, len(agents[0].state_dict()), "tensors")
+    np.savez_compressed(os.path.join(HERE, "agent_init.npz"), **out)
+
+
 if __name__ == "__main__":
     cfg = ref_harness.load_config()
     which = sys.argv[1:] or ["env", "fuzz", "nets", "mcts", "acting", "replay", "learner", "sampling", "acting_t",
-                             "test_sim"]
+                             "test_sim", "agent_init"]
     if "env" in which:
         make_env(cfg)
     if "fuzz" in which:
@@ -783,3 +806,5 @@ if __name__ == "__main__":
         make_acting_temperature(cfg)
     if "test_sim" in which:
         make_test_sim(cfg)
+    if "agent_init" in which:
+        make_agent_init(cfg)

@@ -167,3 +167,25 @@ def test_rep_trunk_rejects_bad_arguments_without_gpu():
     assert L.mzba_rep_trunk(x, y, w, b, 20, 8, 4, None) == -1  # 58 convs
     wn = (ctypes.c_void_p * nc)(*([1] * (nc - 1) + [0]))
     assert L.mzba_rep_trunk(x, y, wn, b, 2, 3, 4, None) == -1
+
+
+@pytest.mark.parametrize("tag", ["small", "full"])
+def test_agent_random_init_equals_reference_construction(tag):
+    """MuZeroAgent(cfg)'s starting weights (networks.py:245-266) are the reference agent's bit for
+    bit under the same torch seed: tests/golden/agent_init.npz holds per-tensor checksums of the
+    reference's own `MuZeroAgent(cfg)` built twice in a row (RLSystem's learner and target agents,
+    train_torch.py:86-88) after torch.manual_seed(42) (train_torch.py set_seed) and (7)."""
+    import torch
+    from conftest import GOLDEN
+    from mzba.weights import torch_init_state_dict
+    d = np.load(os.path.join(GOLDEN, "agent_init.npz"))
+    mcfg = small_model_cfg() if tag == "small" else default_config()["model"]
+    for seed in (42, 7):
+        torch.manual_seed(seed)
+        for ai in range(2):
+            sd = torch_init_state_dict(mcfg)
+            assert list(sd) == [k for k, _ in state_dict_spec(mcfg)]
+            for k, v in sd.items():
+                f = v.numpy().astype(np.float64).reshape(-1)
+                got = np.concatenate([[f.sum(), np.abs(f).sum()], f[:4], f[-1:]])
+                np.testing.assert_array_equal(got, d[f"{tag}/s{seed}/a{ai}/{k}"], err_msg=f"s{seed} a{ai} {k}")

@@ -110,6 +110,98 @@ def test_config4_bf16_fused_shards_equal_global_loop():
     assert (full["counts"].sum(-1) == 50).all()
 
 
+def _stage_cfg():
+    cfg = default_config()
+    cfg["model"] = small_model_cfg(cfg)
+    cfg["num_simulations"] = 8
+    cfg["n_parallel"] = 10924  # 3 x 10924 >= 32768: torch's pow splits the (n, 3) tensor over its threads
+    cfg["num_episodes"] = 1
+    cfg["pow_threads"] = 4
+    return cfg
+
+
+STAGE_SEED, STAGE_T, STAGE_STEPS = 29, 0.9, 9
+
+
+def _stage_run(world, rank):
+    """One ActingStage episode (global batch of _stage_cfg) -> rank 0: the replay buffer's windows and
+    the episode's records, as numpy."""
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingStage
+    from mzba.replay import DeviceReplayBuffer
+    cfg = _stage_cfg()
+    mcfg = cfg["model"]
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(init_state_dict(mcfg, 9))
+    st = ActingStage(cfg, ag, seed=STAGE_SEED, world_size=world, rank=rank, record_k=3, max_steps=STAGE_STEPS)
+    st.temperature = STAGE_T
+    rb = DeviceReplayBuffer(mcfg["state_history_length"], cfg["num_unroll_steps"], 60000, cfg["discount_factor"],
+                            cfg["n_parallel"]) if rank == 0 else None
+    st.run_episode(rb, trajectories=False)
+    torch.cuda.synchronize()
+    if rank != 0:
+        return None
+    rec = st.sink.rec if st.sink is not None else st.loop.rec
+    out = {"T": st.loop.t, "length": rb.length}
+    out.update({f"rec/{k}": v[:st.loop.t].cpu().numpy() for k, v in rec.items() if v is not None})
+    out.update({f"ring/{k}": v[:rb.length].cpu().numpy() for k, v in rb._ring.items()})
+    return out
+
+
+def _stage_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _stage_run(world, rank)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config4_sharded_acting_stages_fill_the_replay_buffer_like_one_global_stage():
+    """Config 4's sink end to end (train_torch.py:160-233 -> replay_buffer.py:96-165): two ActingStage
+    ranks (two processes sharing cuda:0, gloo collectives: bench.py's rehearsal path minus RCCL) over a
+    10 924-env global batch at T = 0.9, each acting on its 5 462 envs, gathering its record rows to rank 0
+    every 3 steps, stepping until the GLOBAL batch is done; rank 0 ingests the episode into a
+    DeviceReplayBuffer. Against one 10 924-env stage in this process: the episode's records (sampled
+    actions, rewards, masks, frames, visit counts, values) and every replay window (past / future actions,
+    frames, rewards, visit counts, values, n-step value targets, reward sums) bit for bit. 3 x 10 924
+    elements cross torch's 32 768-element threaded-pow boundary (pow_threads = 4, explicit): the sampled
+    actions equal the oracle's sampling of the same counts with 4 threads."""
+    import socket
+    import torch.multiprocessing as mp
+    from oracle import rng as R
+    from oracle.acting import sample_actions
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_stage_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=300) for _ in range(2))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    full = _stage_run(1, 0)
+    shard = got[0]
+    assert got[1] is None
+    assert shard["T"] == full["T"] and shard["length"] == full["length"] > 0
+    for k in full:
+        if k.startswith(("rec/", "ring/")):
+            np.testing.assert_array_equal(shard[k], full[k], err_msg=k)
+    n, T = _stage_cfg()["n_parallel"], full["T"]
+    counts, act, mask = full["rec/counts"], full["rec/action"], full["rec/mask"].astype(bool)
+    for t in range(T):
+        u = R.uniform(np.arange(n), R.STREAM_SAMPLE, t, 0, STAGE_SEED)
+        want = sample_actions(counts[t], STAGE_T, u, threads=4)
+        np.testing.assert_array_equal(act[t][mask[t]], want[mask[t]], err_msg=f"t={t}")
+
+
 # ------------------------------------------------------------------------------ config 5
 def test_config5_search_s200_f32_matches_oracle():
     """200-sim searches (config 5's tree size: 201 nodes per env) with networks: the f32 path against

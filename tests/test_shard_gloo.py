@@ -6,6 +6,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -108,3 +109,64 @@ def test_sharded_sampling_oracle_equals_global():
     for off, n in ((0, 515), (515, 514)):
         np.testing.assert_array_equal(sample_probs(c[off:off + n], 0.7, env_offset=off, n_envs_total=1029)
                                       .view(np.uint32), full[off:off + n].view(np.uint32))
+
+
+def _sink_worker(rank, world, port, out):
+    """One rank of a sharded episode through mzba.shard.ShardedSink: its records are written row by row
+    (as ActingLoop.act does), pushed every k = 4 rows, and the ranks stop together when every env of
+    every rank is done (all_ranks_done). Rank 0 returns the global records."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mzba.shard import ShardedSink, all_ranks_done
+    B, hw, Tmax = 5, 320, 20
+    rec = _rec(Tmax, B, hw, rank)
+    done_at = [6, 11][rank]  # rank 0's envs finish first: it keeps stepping until rank 1's do too
+    frame0 = torch.randint(0, 8, (B * hw,), generator=torch.Generator().manual_seed(7 + rank), dtype=torch.uint8)
+    sink = ShardedSink(world, rank, 4, B, hw, Tmax, "cpu")
+    sink.begin(frame0)
+    t = 0
+    while not all_ranks_done(torch.full((B,), int(t >= done_at), dtype=torch.uint8)) and t < Tmax:
+        t += 1  # the loop wrote row t - 1
+        sink.push(rec, t)
+    g, f0 = sink.finish(rec, t)
+    res = {"t": t}
+    if rank == 0:
+        res["rec"] = {k: v[:t].numpy() for k, v in g.items()}
+        res["frame0"] = f0.numpy()
+    else:
+        assert g is None and f0 is None
+    out.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_sink_assembles_the_global_episode_world2():
+    """ActingStage's N > 1 sink on CPU collectives: two ranks' record rows, gathered every 4 steps,
+    land in rank 0's (T, 2B, ...) episode tensors in global env order, the frames g(s0) of both
+    ranks with them; the ranks stop on the same step (the global batch's all-done)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_sink_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(2))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got[0]["t"] == got[1]["t"] == 11
+    ref = [_rec(20, 5, 320, r) for r in range(2)]
+    for k in ("action", "mask", "reward", "values", "counts", "frame"):
+        want = np.concatenate([ref[r][k][:11].numpy() for r in range(2)], axis=1)
+        np.testing.assert_array_equal(got[0]["rec"][k], want, err_msg=k)
+    f0 = [torch.randint(0, 8, (5 * 320,), generator=torch.Generator().manual_seed(7 + r), dtype=torch.uint8)
+          for r in range(2)]
+    np.testing.assert_array_equal(got[0]["frame0"], torch.cat(f0).view(10, 320).numpy())
+
+
+def test_exchange_refuses_world_gt1_without_process_group():
+    g = TrajectoryGather(2, 0, 4, 3, 320, "cpu", pin=False)
+    with pytest.raises(RuntimeError):
+        g.exchange(_rec(4, 3, 320, 0), 0, 4)
