@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--width", type=int, default=None, help="env workload frame width (default 84)")
     ap.add_argument("--hist", type=int, default=4, help="env workload frame-stack length")
     ap.add_argument("--minibatch", type=int, default=512, help="learner workload minibatch (config.yaml:7)")
+    ap.add_argument("--no-halo", action="store_true",
+                    help="A/B: large-image 3x3 convs on conv_big_bf16_kernel instead of the halo-tiled conv_halo_kernel")
     ap.add_argument("--pow-threads", type=int, default=1,
                     help="intra-op threads of the reference process whose temperature pow the sampling reproduces "
                          "(splits torch's pow into per-thread chunks from 3 x global envs >= 32768 on)")
@@ -260,6 +262,16 @@ def run_learner(args, world, rank, local):
         dist.destroy_process_group()
 
 
+def big_conv_kernel(args, B, p):
+    """The kernel the latent residual convs run on when the fused tower does not apply (config 3)."""
+    from mzba import _lib as L
+    if p.lh * p.lw <= 160:
+        return "conv_lat"
+    if args.dtype == "bf16" and not args.no_halo and L.lib().mzba_conv_halo_supported(p.lh, p.lw, p.c1, p.c1, 3):
+        return "conv_halo"
+    return "conv_big_bf16" if B * p.lh * p.lw >= 65536 and args.dtype == "bf16" else "conv_igemm"
+
+
 def cfg_name(B, S, dyn=None):
     """Which BASELINE config an acting-loop run is (per-GPU batch, sims, dynamics precision)."""
     if (B, S) == (4096, 200):
@@ -451,6 +463,9 @@ def main():
     agent.load_state_dict(sd)
     loop = ActingLoop(cfg, agent, B, seed=args.seed, env_offset=rank * B, height=H, width=W, n_envs_total=world * B,
                       pow_threads=args.pow_threads)
+    if args.no_halo:
+        loop.ws.runner.use_halo = False
+        loop.rep_runner.use_halo = False
     gather = TrajectoryGather(world, rank, RECORD_K, B, H * W, f"cuda:{local}")
     loop.reset(0)
     last_flush = [0]
@@ -584,7 +599,7 @@ def main():
                          "kernel": (f"{tower_kernel_name(B)} (fused dynamics / prediction step: 14-block residual "
                                     "tower, bf16 3x3 256->256 convs, M=B*20, N=256, K=2304 each)") if tower_launch_ms else
                                    (f"latent residual conv bf16 3x3 256->256 (M=B*{p.lh * p.lw},N=256,K=2304; "
-                                    f"{'conv_lat' if p.lh * p.lw <= 160 else ('conv_big_bf16' if B * p.lh * p.lw >= 65536 and args.dtype == 'bf16' else 'conv_igemm')} kernel)"),
+                                    f"{big_conv_kernel(args, B, p)} kernel)"),
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None, "traffic": traffic,
                          "traffic_algorithmic_bytes": traffic_rec and traffic_rec.get("algorithmic_bytes"),

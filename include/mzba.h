@@ -98,6 +98,17 @@ int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_
                 const void* w, const float* bias, const float* act_bias, const int32_t* act, int A, const void* res,
                 void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream);
 
+/* Halo-tiled 3x3 conv (bf16, config 3's large images: the 21x21 latent towers, the 42x42 / 84x84
+ * representation convs; networks.py:19-35): out = act(conv3x3(in) + bias (+ res)) on contiguous NHWC images
+ * of B envs, zero padding. A workgroup stages 256 consecutive output pixels plus W + 1 halo rows on each side
+ * into LDS once per channel block and runs all 9 taps from it. wh = pack_lat16 of the BN-folded
+ * [Cout][3][3][Cin] weights: wh[Cout/16][9*Cin/32][64][8], wh[ct][s][l][j] = W[16 ct + l % 16][32 s + 8 (l / 16) + j]
+ * with the K index tap * Cin + channel. Supported: Cin % 128 == 0, Cout % 256 == 0, the staged halo within the
+ * LDS (mzba_conv_halo_supported). Replaces networks.py:19-35 ResidualBlock convs (the second with res). */
+int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks);
+int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
+                   int Cin, int Cout, int relu, hipStream_t stream);
+
 /* Latent-resolution conv (bf16): same contract as mzba_conv2d for H*W <= 160, Cin in {64,128,256},
  * Cout % 32 == 0, but the weights are in fragment-major order wf[Cout/32][2][ks*ks][Cin/32][64][8]
  * followed by 8*64*8 padding elements (the weight ring prefetches 8 k steps past the end; see

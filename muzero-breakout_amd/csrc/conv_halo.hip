@@ -1,0 +1,288 @@
+// Halo-tiled 3x3 convolution for large images (gfx950, bf16 MFMA): config 3's 21x21 latent towers and its
+// 42x42 / 84x84 representation convs (networks.py:19-35, 38-241 at the 84x84 / 4-frame geometry).
+//
+// out[m][n] = act(sum_{tap, c} in[m + dy W + dx][c] W[n][tap][c] + bias[n] (+ res[m][n])), m = (env, y, x)
+// flattened over the batch, NHWC bf16, zero padding (taps leaving the image read zeros).
+//
+// A workgroup (8 waves) owns TM = 256 consecutive output pixels x 256 output
+// channels. A 3x3 tap shifts the flattened pixel index by dy W + dx, so every tap of the tile reads rows of ONE
+// staged range: the tile's pixels plus a halo of W + 1 rows on each side (HR = 256 + 2 W + 2 pixel rows). That
+// range is staged into LDS once, all Cin (128 or 256) channels (supported while HR x 2 Cin B fits the 160 KiB:
+// W <= 30 at Cin 256, W <= 156 at Cin 128) with LDS-DMA (global_load_lds_dwordx4, no VGPR round trip), and the 9 taps
+// x the block's channel steps run from it — the activation operand is fetched from L2 once per tile, not once
+// per tap as an im2col GEMM tile fetches it (conv_big_bf16_kernel: 9 x the activation traffic and its LDS
+// writes every K step).
+//   * LDS row r = pixel m0 - (W + 1) + r, 16-B chunks XOR-swizzled by (r & 15): a B fragment (16
+//     consecutive rows = 16 pixels of a tile shifted by any tap, 8 channels per lane) hits 16 distinct bank
+//     slots for every shift; LDS-DMA writes lane-linear 1-KiB blocks, so the swizzle is applied on the
+//     source addresses. One extra zero row: a tap that leaves the image (y + dy or x + dx outside, which the
+//     flattened shift would wrap into the neighbouring row or env) reads it instead.
+//   * 8 waves (two per SIMD), each 128 pixels (8 tiles) x 64 output channels (4 column tiles): 32
+//     accumulators (128 AGPRs); weights = MFMA A operand from a two-k-step register ring (buffer_load_dwordx4
+//     off a wave-uniform resource, the fragment-major packing pack_lat16 of [Cout][tap][Cin]), activations =
+//     B operand from LDS (v_mfma_f32_16x16x32_bf16): per 32-channel k step 8 B reads + 4 weight loads feed 32
+//     MFMAs, pixel-tile major (each B fragment feeds its 4 MFMAs back to back).
+//   * epilogue: + bias (+ residual), ReLU, bf16; a lane holds 4 consecutive channels of one pixel.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace hl {
+constexpr int TM = 256;            // output pixels per workgroup
+constexpr int TN = 256;            // output channels per workgroup
+constexpr int NT = 512;            // 8 waves, two per SIMD
+constexpr int LDS_MAX = 160 * 1024;
+}  // namespace hl
+
+struct HaloArgs {
+  const bf16_t* in;    // [M][Cin]
+  const bf16_t* wh;    // pack_lat16: [Cout / 16][9 Cin / 32][64][8]
+  const float* bias;   // [Cout]
+  const bf16_t* res;   // optional [M][Cout]
+  bf16_t* out;         // [M][Cout]
+  int M, H, W, Cin, Cout, relu;
+  int HALO, HR, CB;    // halo rows each side, staged rows, channels per staged block
+  int NI, ZOFF;        // LDS-DMA 1-KiB blocks per staging, byte offset of the zero row
+};
+
+// + bias (+ residual), ReLU, bf16: (acc + bias) + res in f32, as conv_big_bf16_kernel; a lane stores 4
+// consecutive channels (8 B) of one pixel per (pixel tile, column tile); every residual load of a pixel tile
+// is issued before its first use
+template <bool RES>
+MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[8][4], int m0, int nb, int wm, int q, int n) {
+  float4 bb[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
+  const float lo = a.relu ? 0.f : -__builtin_inff();  // ReLU as max(v, 0); max(v, -inf) = v
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = m0 + wm * 128 + mi * 16 + n;
+    const int mc = m < a.M ? m : a.M - 1;
+    uint2 rv[4];
+    if (RES) {
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) rv[ct] = *reinterpret_cast<const uint2*>(a.res + (size_t)mc * a.Cout + nb + ct * 16 + 4 * q);
+    }
+    uint2 o[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[mi][ct][i] + (&bb[ct].x)[i];
+      if (RES) {
+        v[0] = v[0] + bf16_to_f32((bf16_t)(rv[ct].x & 0xffffu));
+        v[1] = v[1] + bf16_to_f32((bf16_t)(rv[ct].x >> 16));
+        v[2] = v[2] + bf16_to_f32((bf16_t)(rv[ct].y & 0xffffu));
+        v[3] = v[3] + bf16_to_f32((bf16_t)(rv[ct].y >> 16));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = fmaxf(v[i], lo);
+      o[ct] = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+    if (m < a.M) {
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) *reinterpret_cast<uint2*>(a.out + (size_t)m * a.Cout + nb + ct * 16 + 4 * q) = o[ct];
+    }
+  }
+}
+
+template <int CB, int NBLK>
+__global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
+  constexpr int RB = CB * 2;        // bytes per staged row
+  constexpr int NC = CB / 8;        // 16-B chunks per row
+  constexpr int NCS = CB / 32;      // 32-channel k steps per tap and block
+  static_assert(NCS % 2 == 0, "ring slot = channel step parity");
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // pixel half (128), channel quarter (64)
+  const int q = lane >> 4, n = lane & 15;
+  const int m0 = blockIdx.x * hl::TM, n0 = blockIdx.y * hl::TN;
+  const int HW = a.H * a.W;
+  const int KS = 9 * a.Cin / 32;            // k steps of the whole conv (pack stride per column tile)
+  constexpr int nsteps = NBLK * 9 * NCS;  // NBLK = Cin / CB
+
+  // the zero row (never overwritten by staging)
+  if (tid < RB / 16) *reinterpret_cast<uint4*>(lds + a.ZOFF + tid * 16) = make_uint4(0, 0, 0, 0);
+
+  // per pixel tile mi of the wave: the lane's pixel is staged row prow0 + 16 mi at tap (0, 0); byte mi of
+  // okw[mi / 4] says which taps stay in the image (bit 0: y > 0, 1: y < H - 1, 2: x > 0, 3: x < W - 1,
+  // 4: the pixel exists — rows past M read only the zero row)
+  const int prow0 = wm * 128 + n + a.HALO;
+  uint32_t okw[2] = {0u, 0u};
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+    const int m = m0 + wm * 128 + mi * 16 + n;
+    if (m < a.M) {
+      const int p = m % HW, y = p / a.W, x = p - y * a.W;
+      const uint32_t b = 16u | (y > 0 ? 1u : 0u) | (y < a.H - 1 ? 2u : 0u) | (x > 0 ? 4u : 0u) | (x < a.W - 1 ? 8u : 0u);
+      okw[mi >> 2] |= b << (8 * (mi & 3));
+    }
+  }
+
+  // weight ring: k step j (loop order block, tap, channel step) -> pack k step
+  auto kstep = [&](int j) {
+    j = j < nsteps ? j : nsteps - 1;  // the ring's prefetch past the end re-reads the last step
+    const int blk = j / (9 * NCS), r = j - blk * 9 * NCS, t = r / NCS, c = r - t * NCS;
+    return t * (a.Cin / 32) + blk * NCS + c;
+  };
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint4*>(reinterpret_cast<const uint4*>(a.wh) + (size_t)(n0 / 16 + wn * 4) * KS * 64), 0, 0x7fffffff,
+      0x00020000);
+  auto wload = [&](int ct, int s) {
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (ct * KS + s) * 1024, 0));
+  };
+  bf16x8 bq[2][4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    bq[0][ct] = wload(ct, kstep(0));
+    bq[1][ct] = wload(ct, kstep(1));
+  }
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      acc[mi][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+
+  // a tap's fragment addresses: per pixel tile, the byte offset of its staged row (the zero row for a tap that
+  // leaves the image); the row's swizzle key (row & 15) is recovered from the offset
+  auto tap_set = [&](int t, int (&rb)[8]) {
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    const uint32_t need = 16u | (dy < 0 ? 1u : 0u) | (dy > 0 ? 2u : 0u) | (dx < 0 ? 4u : 0u) | (dx > 0 ? 8u : 0u);
+    const int shift = dy * a.W + dx;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
+      const int r = prow0 + 16 * mi + shift;
+      rb[mi] = ok ? r * RB : a.ZOFF;  // the zero row reads zeros under any key
+    }
+  };
+  // B fragment of pixel tile mi, channel step c (32 channels: chunk 4c + q of the row)
+  auto frag = [&](const int (&rb)[8], int c, int mi) {
+    const int key = ((unsigned)rb[mi] / RB) & 15;
+    return *reinterpret_cast<const bf16x8*>(lds + rb[mi] + (((4 * c + q) ^ key) << 4));
+  };
+  constexpr int NF = 8 * NCS;  // fragments per tap, in (channel step, pixel tile) order; a multiple of 4
+
+  int j = 0;  // k step
+#pragma unroll
+  for (int blk = 0; blk < NBLK; ++blk) {
+    if (blk > 0) __syncthreads();  // every wave is done with the previous block's rows
+    // stage rows [m0 - HALO, m0 - HALO + HR) x channels [blk CB, (blk + 1) CB): block i of 1 KiB holds
+    // chunks 64 i .. 64 i + 63 (row g / NC, physical chunk g % NC = logical chunk ^ (row & 15))
+    for (int i = wave; i < a.NI; i += 8) {
+      const int g = i * 64 + lane, r = g / NC, s = g - r * NC;
+      int m = m0 - a.HALO + r;
+      m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);  // rows outside [0, M) are only read by masked taps
+      const bf16_t* src = a.in + (size_t)m * a.Cin + blk * CB + ((s ^ (r & 15)) << 3);
+      __builtin_amdgcn_global_load_lds(src, lds + i * 1024, 16, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int rbc[8], rbn[8];  // this tap's row offsets, the next tap's
+    tap_set(0, rbc);
+    bf16x8 fr[4];  // rolling fragment buffer, two reads ahead
+    fr[0] = frag(rbc, 0, 0);
+    fr[1] = frag(rbc, 0, 1);
+    // the taps unrolled: loop-carried accumulators in a rolled loop were renamed and copied between the
+    // register files on every iteration
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      tap_set(t < 8 ? t + 1 : t, rbn);
+#pragma unroll
+      for (int c = 0; c < NCS; ++c) {
+        const int sl = c & 1;  // = j & 1: the steps per tap (NCS) are even
+        const int sn = kstep(j + 2);
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+          const int idx = c * 8 + mi, nx = idx + 2;
+          if (nx < NF)
+            fr[nx & 3] = frag(rbc, nx >> 3, nx & 7);
+          else if (t < 8)  // the next tap's first fragments (not across a restaging)
+            fr[nx & 3] = frag(rbn, (nx - NF) >> 3, (nx - NF) & 7);
+          const bf16x8 f = fr[idx & 3];
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct) acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][ct], f, acc[mi][ct], 0, 0, 0);
+        }
+        // this step's ring slots are free once its MFMAs have issued: the step after next
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) bq[sl][ct] = wload(ct, sn);
+        // per pixel tile: its fragment read two tiles ahead, then its 4 MFMAs; the ring loads after the step's
+        // MFMAs (their slots are free then; issued earlier they would need fresh registers)
+#pragma unroll
+        for (int mi = 0; mi < 8; ++mi) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        ++j;
+      }
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) rbc[mi] = rbn[mi];
+    }
+  }
+
+  // epilogue: acc[mi][ct] = D[channel n0 + 128 wn + 16 ct + 4q + i][pixel m0 + 128 wm + 16 mi + n]
+  if (a.res)
+    halo_epilogue<true>(a, acc, m0, n0 + wn * 64, wm, q, n);
+  else
+    halo_epilogue<false>(a, acc, m0, n0 + wn * 64, wm, q, n);
+}
+
+// staging geometry for a (W, Cin) pair: the whole Cin staged at once (one block; a rolled loop over channel
+// blocks would carry the accumulators across its back edge, which the compiler renames and copies), 0 if the
+// halo does not fit the LDS
+int halo_geometry(int W, int Cin, HaloArgs& g) {
+  const int cb = Cin, halo = W + 1, hr = hl::TM + 2 * halo, rb = cb * 2;
+  const int ni = (hr * rb + 1023) / 1024;
+  const int zoff = ni * 1024;
+  if ((cb != 128 && cb != 256) || zoff + rb > hl::LDS_MAX) return 0;
+  g.HALO = halo, g.HR = hr, g.CB = cb, g.NI = ni, g.ZOFF = zoff;
+  return zoff + rb;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks) {
+  HaloArgs g{};
+  return ks == 3 && H >= 2 && W >= 2 && (Cin == 128 || Cin == 256) && Cout % 256 == 0 && halo_geometry(W, Cin, g) > 0 ? 1
+                                                                                                               : 0;
+}
+
+// out = act(conv3x3(in, W) + bias (+ res)) on contiguous NHWC bf16 images (B envs of H x W x Cin); wh = the
+// pack_lat16 packing of the BN-folded [Cout][3][3][Cin] weights (agent.py PackedNets._conv "wh").
+int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
+                   int Cin, int Cout, int relu, hipStream_t stream) {
+  MZ_CHECK_ARG(in && wh && bias && out && B > 0, -1);
+  MZ_CHECK_ARG(mzba_conv_halo_supported(H, W, Cin, Cout, 3), -2);
+  const long long M = (long long)B * H * W;
+  MZ_CHECK_ARG(M < (1LL << 31) / 512, -3);  // 32-bit row offsets
+  HaloArgs a{(const bf16_t*)in, (const bf16_t*)wh, bias, (const bf16_t*)res, (bf16_t*)out, (int)M, H, W, Cin, Cout, relu};
+  const int lds = halo_geometry(W, Cin, a);
+  const dim3 grid((unsigned)((M + hl::TM - 1) / hl::TM), (unsigned)(Cout / hl::TN));
+  auto launch = [&](auto kern) {
+    static bool attr = false;  // per instance: the 160 KiB of dynamic LDS
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, hl::LDS_MAX);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(hl::NT), lds, stream, a);
+  };
+  if (a.CB == 256)
+    launch(conv_halo_kernel<256, 1>);
+  else
+    launch(conv_halo_kernel<128, 1>);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

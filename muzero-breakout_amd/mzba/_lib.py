@@ -33,6 +33,8 @@ SIGNATURES = {
     "mzba_env_set_block_envs": [I],
     "mzba_conv2d": [I, P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
     "mzba_conv2d_set_variant": [I],
+    "mzba_conv_halo_supported": [I, I, I, I, I],
+    "mzba_conv_halo": [P, P, P, P, P, I, I, I, I, I, I, P],
     "mzba_conv_lat_supported": [I, I, I, I, I],
     "mzba_conv_lat_set_variant": [I],
     "mzba_conv_lat_get_variant": [],

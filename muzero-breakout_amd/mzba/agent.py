@@ -72,28 +72,33 @@ class PackedNets:
         self.rep = []
         cin = 2 * self.L
         nconv = 0
+        hw = (4 * self.lh, 4 * self.lw)  # the representation's input resolution; halved by each pool
         for kind, i in rep_layout(mcfg):
             p = f"rep_net.blocks.{i}"
             if kind == "conv":
                 cout = self.c0 if nconv == 0 else self.c1
-                self.rep.append(("conv", self._conv(sd[p + ".weight"], sd[p + ".bias"], None, band=True)))
+                self.rep.append(("conv", self._conv(sd[p + ".weight"], sd[p + ".bias"], None, band=True, hw=hw)))
                 nconv += 1
                 cin = cout
             elif kind == "res":
-                self.rep.append(("res", self._res(sd, p, band=True)))
+                self.rep.append(("res", self._res(sd, p, band=True, hw=hw)))
             else:
                 self.rep.append(("pool", None))
+                hw = (hw[0] // 2, hw[1] // 2)
         # dynamics (networks.py:117-149)
         w = sd["dyn_net.conv_block.conv.weight"]
         cmain = self.c1
         self.dyn0 = self._conv(w[:, :cmain], sd["dyn_net.conv_block.conv.bias"], self._bn(sd, "dyn_net.conv_block.bn"),
                                act_w=w[:, cmain:])
-        self.dyn = [self._res(sd, f"dyn_net.res_blocks.{i}") for i in range(mcfg["dynamics_network"]["num_res_blocks"])]
+        lat = (self.lh, self.lw)
+        self.dyn = [self._res(sd, f"dyn_net.res_blocks.{i}", hw=lat)
+                    for i in range(mcfg["dynamics_network"]["num_res_blocks"])]
         self.rew_conv = self._conv(sd["dyn_net.reward_head.0.conv.weight"], sd["dyn_net.reward_head.0.conv.bias"],
                                    self._bn(sd, "dyn_net.reward_head.0.bn"))
         self.rew_lin = self._linear(sd["dyn_net.reward_head.2.weight"], sd["dyn_net.reward_head.2.bias"], self.c1)
         # prediction (networks.py:190-223)
-        self.pred = [self._res(sd, f"pred_net.res_blocks.{i}") for i in range(mcfg["prediction_network"]["num_res_blocks"])]
+        self.pred = [self._res(sd, f"pred_net.res_blocks.{i}", hw=lat)
+                     for i in range(mcfg["prediction_network"]["num_res_blocks"])]
         # fused-tower packing (bf16, 256 channels, 4x5 latent): every residual conv of a tower
         # back to back in the 16-column fragment-major order + 8 padding k steps
         self.tower_ok = (self.dtype == "bf16" and self.c1 == 256 and (self.lh, self.lw) == (4, 5))
@@ -120,7 +125,7 @@ class PackedNets:
 
         def conv(name, c):
             n.add_conv(name, c["w"], c["b"], c.get("wf"), c.get("wt"), c.get("act_bias"), c["cin"], c["cout"], c["ks"],
-                       c.get("A", 0))
+                       c.get("A", 0), c.get("wh"))
 
         for i, (kind, layer) in enumerate(self.rep):
             if kind == "conv":
@@ -306,7 +311,8 @@ class PackedNets:
         alpha = g / np.sqrt(v + BN_EPS)
         return alpha, b - m * alpha
 
-    def _conv(self, w, bias, bn, act_w=None, band=False):
+    def _conv(self, w, bias, bn, act_w=None, band=False, hw=None):
+        """hw: the (H, W) the conv runs at, when known: large images get the halo-tiled kernel's packing."""
         cout, cin, k, _ = w.shape
         if bn is not None:
             alpha, beta = bn
@@ -339,15 +345,20 @@ class PackedNets:
         if self.dtype == "bf16" and cout % 32 == 0 and cin_p in (64, 128, 256):
             layer["wf"] = torch.tensor(pack_lat(wp.reshape(cout, -1), cout, k, cin_p),
                                        dtype=torch.float32).to(self.tdt).to(self.device)
+        if (hw is not None and self.dtype == "bf16" and act_w is None and hw[0] * hw[1] > 320
+                and L.lib().mzba_conv_halo_supported(hw[0], hw[1], cin_p, cout, k)):
+            # config 3's large images (mzba_conv_halo): pack_lat16 of [Cout][tap][Cin]
+            layer["wh"] = torch.tensor(pack_lat16(wp.reshape(cout, -1), cout, k, cin_p),
+                                       dtype=torch.float32).to(self.tdt).to(self.device)
         if band and self.dtype == "bf16" and k == 3 and L.lib().mzba_conv_band_supported(16, 20, cin, cout, 3):
             # representation convs at full resolution: the band kernel's packing (tower order)
             layer["wt"] = torch.tensor(np.concatenate([pack_tower_conv(w), np.zeros(LAT_PAD_ELEMS)]),
                                        dtype=torch.float32).to(self.tdt).to(self.device)
         return layer
 
-    def _res(self, sd, p, band=False):
-        return (self._conv(sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], self._bn(sd, p + ".bn1"), band=band),
-                self._conv(sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], self._bn(sd, p + ".bn2"), band=band))
+    def _res(self, sd, p, band=False, hw=None):
+        return (self._conv(sd[p + ".conv1.weight"], sd[p + ".conv1.bias"], self._bn(sd, p + ".bn1"), band=band, hw=hw),
+                self._conv(sd[p + ".conv2.weight"], sd[p + ".conv2.bias"], self._bn(sd, p + ".bn2"), band=band, hw=hw))
 
     def _tower(self, sd, prefix, n):
         if not self.tower_ok or n == 0:
@@ -387,7 +398,7 @@ class NetRunner:
     stream — representation_ / dynamics_ / prediction_ / prediction_tree_ (`torch.ops.mz`)."""
 
     FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail", "use_band_res", "use_rep_blocks",
-             "use_rep_trunk")
+             "use_rep_trunk", "use_halo")
 
     def __init__(self, packed, B, H, W):
         self.p = packed

@@ -581,6 +581,44 @@ def test_conv_big_kernel_vs_torch_fp32(B, H, W, Cin, Cout, ks, relu):
     assert (outs[0] - outs[1]).abs().max().item() <= 1e-2 * scale
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout,relu,with_res", [(150, 21, 21, 256, 256, 1, True), (37, 21, 21, 256, 256, 0, False),
+                                                          (12, 84, 84, 128, 256, 0, True), (9, 16, 20, 256, 256, 1, True),
+                                                          (3, 21, 21, 256, 512, 1, True)])
+def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res):
+    """The halo-tiled 3x3 conv (mzba_conv_halo: config 3's 21x21 latent convs and 84x84 128 -> 256 conv; 256
+    output pixels + W + 1 halo rows staged once per workgroup, every tap read from LDS, taps leaving the image
+    redirected to a zero row) vs a torch fp32 conv of the same bf16 operands (+ bias, residual, ReLU), ragged
+    pixel counts (the last tile partial), tiles crossing env boundaries; and close to conv_big_bf16_kernel."""
+    from mzba import _lib as L
+    from mzba.agent import pack_lat16
+    assert L.lib().mzba_conv_halo_supported(H, W, Cin, Cout, 3)
+    g = torch.Generator(device="cuda").manual_seed(B + Cin + W)
+    dev = torch.device("cuda")
+    x = torch.randn(B, H, W, Cin, generator=g, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Cout, 3, 3, Cin, generator=g, device=dev) / (Cin * 9) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g, device=dev)
+    res = torch.randn(B, H, W, Cout, generator=g, device=dev).to(torch.bfloat16) if with_res else None
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1)
+    ref = ref.permute(0, 2, 3, 1) + (res.float() if with_res else 0)
+    if relu:
+        ref = torch.relu(ref)
+    wh = torch.tensor(pack_lat16(w.float().cpu().numpy().reshape(Cout, -1), Cout, 3, Cin)).to(torch.bfloat16).cuda()
+    out = torch.full((B, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu, L.stream())
+    big = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    L.call("mzba_conv2d", 1, L.ptr(x), H * W * Cin, None, 0, L.ptr(w), L.ptr(b), None, None, 0, L.ptr(res), L.ptr(big),
+           B, H, W, Cin, Cout, 3, relu, L.stream())
+    torch.cuda.synchronize()
+    got = out.float()
+    assert torch.isfinite(got).all()
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    print(f"conv_halo {B}x{H}x{W} {Cin}->{Cout}: max err {err / scale:.2e} of the magnitude, vs conv_big "
+          f"{(got - big.float()).abs().max().item() / scale:.2e}")
+    assert err <= 1e-2 * scale  # bf16 output rounding
+    assert (got - big.float()).abs().max().item() <= 1e-2 * scale
+
+
 # ------------------------------------------------------------------------------ MCTS
 @pytest.mark.parametrize("tag", ["b16_s50", "b4_s200"])
 def test_mcts_replay_bit_exact(tag):
