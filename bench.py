@@ -325,6 +325,25 @@ def tower_counters(B, kname):
     return None
 
 
+def l2_weight_stream(conv_ms, C=256):
+    """The per-CU weight-stream bound of a tower conv: every workgroup (one per CU)
+    streams each conv's whole weight pack (C x 9C bf16 = 1.18 MB) from L2 into its registers, whatever its
+    env count, so a conv takes at least those bytes / the per-CU rate that rate the L2 weight-stream probe
+    measured for the tower's access form (tools/probes/l2_stream_probe.hip: all 256 CUs streaming the 33 MB
+    tower pack with 6 fragments in flight per wave, profiles/l2_stream.json)."""
+    tpath = os.path.join(ROOT, "profiles", "l2_stream.json")
+    if not (conv_ms and os.path.exists(tpath)):
+        return None
+    rec = json.load(open(tpath))
+    rate = rec.get("per_cu_GBps")
+    if not rate:
+        return None
+    nbytes = C * 9 * C * 2
+    floor_ms = nbytes / (rate * 1e9) * 1e3
+    return {"bytes_per_cu_per_conv": nbytes, "per_cu_GBps": rate, "floor_ms_per_conv": floor_ms,
+            "measured_ms_per_conv": conv_ms, "frac": floor_ms / conv_ms, "source": "profiles/l2_stream.json"}
+
+
 # Fraction of a launch's algorithmic 3x3-conv FLOPs the kernel issues to the MFMA pipe: the reference's
 # Conv2d(padding=1) on the 4x5 latent evaluates 50 of its 180 taps per env on zero padding. The pixel-tiled
 # kernel (plan 4) skips them all (130 / 180); the column-tiled tower8 (plans 2 / 3) skips the dx ones only
@@ -374,9 +393,12 @@ def restore_loop(loop, snap):
 
 def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
     """The first timed step replayed on the f32 parity path (networks within 1e-5 of the reference,
-    bit-exact trees): the same env state, search id and keyed randomness as the benchmarked step.
-    Returns the fraction of all B envs whose visit counts equal the benchmarked step's, and the parity
-    path's own throughput (second replay, timed with HIP events) against the dense f32 MFMA peak."""
+    bit-exact trees): the same env state, search id and keyed randomness as the benchmarked step. The parity
+    path's latent convs run as f32-faithful split-bf16 products (conv_x6: six bf16 MFMAs per f32 product,
+    each conv as close to exact as an f32 one); the same step is also replayed with those convs on the
+    f32-input MFMA (conv_igemm, the parity path of rounds 1-3). Returns the fraction of all B envs whose visit
+    counts equal the benchmarked step's, the agreement of the two parity paths, and their throughputs (second
+    replays, HIP events) against the dense f32 MFMA peak."""
     from mzba.agent import MuZeroAgent
     from mzba.acting import ActingLoop
     ag32 = MuZeroAgent(mcfg, dtype="f32", device=loop.agent.device)
@@ -386,29 +408,49 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
     l32.temperature = loop.temperature
     l32.search.noise_weight = loop.search.noise_weight
     l32.reset(0)
-    counts, ms = [], []
-    for _ in range(2):  # the first replay also warms the f32 path (scratch, code objects)
-        restore_loop(l32, snap)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        l32.act(eager=True)
-        e1.record()
-        torch.cuda.synchronize()
-        ms.append(e0.elapsed_time(e1))
-        counts.append(l32.rec["counts"][t0].cpu().numpy())
+    fl = step_flops(ag32.packed, H, W, args.sims)
+    runs = {}
+    for x6 in (True, False):
+        for rn in (l32.ws.runner, l32.rep_runner):
+            rn.use_x6 = x6
+        counts, ms = [], []
+        for _ in range(2):  # the first replay also warms the path (scratch, code objects)
+            restore_loop(l32, snap)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            l32.act(eager=True)
+            e1.record()
+            torch.cuda.synchronize()
+            ms.append(e0.elapsed_time(e1))
+            counts.append(l32.rec["counts"][t0].cpu().numpy())
+        runs[x6] = (counts, ms, l32.rec["values"][t0].cpu().numpy())
+    counts, ms, v32 = runs[True]
     c16 = loop.rec["counts"][t0].cpu().numpy()
     same = (counts[-1] == c16).all(1)
-    v16, v32 = loop.rec["values"][t0].cpu().numpy(), l32.rec["values"][t0].cpu().numpy()
+    l1 = np.abs(counts[-1].astype(np.int64) - c16.astype(np.int64)).sum(1)
+    v16 = loop.rec["values"][t0].cpu().numpy()
     eps = B / (ms[-1] * 1e-3)
-    fl = step_flops(ag32.packed, H, W, args.sims)
+    cf, msf, vf = runs[False]
+    same_f = (cf[-1] == counts[-1]).all(1)
+    eps_f = B / (msf[-1] * 1e-3)
     out = {"match": float(same.mean()),
-           "path": {"dtype": "f32", "value": eps, "unit": "env-steps/s", "ms_per_step": ms[-1],
-                    "achieved_tflops": eps * fl / 1e12, "peak": PEAK_F32_TFLOPS,
+           # beside the exact-match fraction: how far the count rows are apart, and whether the most visited
+           # action (what temperature sampling mostly picks at low T) agrees
+           "l1_mean": float(l1.mean()), "l1_max": int(l1.max()),
+           "top_action_agreement": float((counts[-1].argmax(1) == c16.argmax(1)).mean()),
+           "path": {"dtype": "f32 (latent convs as split-bf16 x6 products)", "value": eps, "unit": "env-steps/s",
+                    "ms_per_step": ms[-1], "achieved_tflops": eps * fl / 1e12, "peak": PEAK_F32_TFLOPS,
                     "frac": eps * fl / 1e12 / PEAK_F32_TFLOPS,
                     "deterministic": bool((counts[0] == counts[1]).all()),
                     "value_max_abs_diff_where_counts_agree": float(np.abs(v16 - v32)[same].max()) if same.any() else None,
-                    "what": "one acting step of the same envs on the f32 parity path (f32 MFMA convs, separate "
-                            "launches per layer), eager, HIP events around the step"}}
+                    "vs_f32_mfma_path": {"value": eps_f, "ms_per_step": msf[-1], "speedup": eps / eps_f,
+                                         "frac": eps_f * fl / 1e12 / PEAK_F32_TFLOPS,
+                                         "visit_count_match": float(same_f.mean()),
+                                         "value_max_abs_diff": float(np.abs(vf - v32).max()),
+                                         "deterministic": bool((cf[0] == cf[1]).all())},
+                    "what": "one acting step of the same envs on the f32 parity path (separate launches per layer, "
+                            "the latent 3x3 convs on conv_x6), eager, HIP events around the step; vs_f32_mfma_path: "
+                            "the same with those convs on the f32-input MFMA"}}
     del l32, ag32
     torch.cuda.empty_cache()
     return out
@@ -618,7 +660,9 @@ def main():
                          "mfma_busy": sq and sq.get("mfma_busy"),
                          "mfma_busy_clock_ghz": sq and sq.get("clock_ghz"),
                          "lds_bank_conflict_frac": sq and sq.get("lds_bank_conflict_frac"),
-                         "counters_source": sq and sq.get("source")},
+                         "counters_source": sq and sq.get("source"),
+                         # below 16 x CUs envs a CU holds too few envs to hide its weight stream: the bound there
+                         "l2_weight_stream": l2_weight_stream(conv_ms) if tower_launch_ms else None},
             "cpu_baseline": cpu_info,
             "visit_count_match": match,
             "visit_count_match_sample": (f"{min(args.cpu_envs, B)} envs, bf16 HIP path vs the f32 CPU port (same keyed "
@@ -627,6 +671,8 @@ def main():
             # every env of the first timed step: the benchmarked bf16 path against this build's f32
             # parity path (1e-5 nets, bit-exact trees) replaying that step from the same state
             "visit_count_match_full": parity and parity["match"],
+            "visit_count_l1_full": parity and {"mean": parity["l1_mean"], "max": parity["l1_max"], "sims": args.sims},
+            "top_action_agreement_full": parity and parity["top_action_agreement"],
             "visit_count_match_full_sample": parity and (
                 f"all {B} envs of the first timed step: {args.dtype} HIP path vs the f32 HIP parity path from the "
                 "same env state, search id and keyed noise / tie-breaks"),

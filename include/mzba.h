@@ -106,6 +106,15 @@ int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_
  * with the K index tap * Cin + channel. Supported: Cin % 128 == 0, Cout % 256 == 0, the staged halo within the
  * LDS (mzba_conv_halo_supported). Replaces networks.py:19-35 ResidualBlock convs (the second with res). */
 int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks);
+/* f32-faithful 3x3 conv on bf16 MFMAs (the f32 parity path's latent towers, networks.py:19-35): f32 NHWC in /
+ * out, out = act(conv3x3(in) + bias (+ res)); every f32 operand split into three bf16 parts and each product
+ * taken as the six terms down to 2^-18 (csrc/conv_x6.hip), as close to exact as an f32 conv. wx = the three
+ * parts of the f32 [Cout][3][3][Cin] weights (hi = bf16(w), mid = bf16(w - hi), lo = bf16(w - hi - mid)), each
+ * in mzba_conv_halo's pack_lat16 packing, back to back. Supported: Cin 128 / 256, Cout % 256 == 0, the staged
+ * halo within the LDS (mzba_conv_x6_supported). */
+int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks);
+int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
+                 int Cin, int Cout, int relu, hipStream_t stream);
 int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
                    int Cin, int Cout, int relu, hipStream_t stream);
 

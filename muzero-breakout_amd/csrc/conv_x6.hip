@@ -1,0 +1,273 @@
+// f32-faithful 3x3 convolution on bf16 MFMAs ("x6": split-bf16 products), for the f32 parity path's
+// latent towers (networks.py:19-35, 103-241): the parity path runs the reference's f32 arithmetic, whose
+// ceiling on the f32-input MFMA (v_mfma_f32_16x16x4_f32, 157 TF) is 1/16 of the bf16 one.
+//
+// Every f32 operand is split exactly-rounded into three bf16 parts, x = xh + xm + xl (xh = bf16(x),
+// xm = bf16(x - xh), xl = bf16(x - xh - xm); |xm| <= 2^-9 |x|, |xl| <= 2^-18 |x|), and a product is taken
+// as the six terms down to the 2^-18 order, xh wh + xh wm + xm wh + xh wl + xm wm + xl wh, each a bf16 x bf16
+// MFMA accumulating in f32: the dropped terms (xm wl, xl wm, xl wl) are below 2^-26 of the product and the
+// parts' own rounding below 2^-26, so a conv is as close to the exact result as an f32 one (a 14-block tower
+// simulated on the CPU: 2.5e-7 of the magnitude from f64, the f32 chain 4.1e-7). Six bf16 MFMAs cost 6/16 of
+// one f32 MFMA's issue.
+//
+// Structure: conv_halo_kernel's (csrc/conv_halo.hip) — a workgroup stages TM consecutive output pixels plus
+// W + 1 halo rows on each side once (here the f32 activations: Cin x 4 B per row, 16-B chunks XOR-swizzled
+// by row), runs all 9 taps from LDS (taps leaving the image read a zero row), 8 waves = 2 pixel halves x 4
+// output-channel quarters; weights = MFMA A operand, their three bf16 parts pre-split on the host
+// (agent.py "wx": three pack_lat16 packs back to back) through a two-k-step register ring; activations = B
+// operand, read as f32 from LDS and split in registers per fragment (each split feeds 4 column tiles x 6
+// MFMAs). Epilogue in f32: + bias (+ residual), ReLU.
+#include "common.h"
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace x6 {
+constexpr int TN = 256;            // output channels per workgroup
+constexpr int NT = 512;            // 8 waves, two per SIMD
+constexpr int LDS_MAX = 160 * 1024;
+}  // namespace x6
+
+struct X6Args {
+  const float* in;     // [M][Cin] f32
+  const bf16_t* wx;    // [3 parts][Cout / 16][9 Cin / 32][64][8]
+  const float* bias;   // [Cout]
+  const float* res;    // optional [M][Cout] f32
+  float* out;          // [M][Cout] f32
+  int M, H, W, Cin, Cout, relu;
+  int HALO, NI, ZOFF;  // halo rows each side, LDS-DMA 1-KiB blocks of the staging, byte offset of the zero row
+  long long part;      // elements per weight part
+};
+
+// bf16 split of 8 f32 (two 16-B halves): hi, mid, lo with x == hi + mid + lo up to the lo part's rounding
+MZ_DEV void split8(const uint4& u0, const uint4& u1, bf16x8& h, bf16x8& m, bf16x8& l) {
+  const float x[8] = {__uint_as_float(u0.x), __uint_as_float(u0.y), __uint_as_float(u0.z), __uint_as_float(u0.w),
+                      __uint_as_float(u1.x), __uint_as_float(u1.y), __uint_as_float(u1.z), __uint_as_float(u1.w)};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const __bf16 hb = (__bf16)x[i];
+    const float r = x[i] - (float)hb;
+    const __bf16 mb = (__bf16)r;
+    const float r2 = r - (float)mb;
+    h[i] = hb;
+    m[i] = mb;
+    l[i] = (__bf16)r2;
+  }
+}
+
+template <int CIN, int TM>
+__global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
+  constexpr int RB = CIN * 4;        // bytes per staged row (f32)
+  constexpr int NC = RB / 16;        // 16-B chunks per row
+  constexpr int NCS = CIN / 32;      // 32-channel k steps per tap
+  constexpr int MT = TM / 32;        // 16-pixel tiles per wave (two pixel halves)
+  static_assert(NCS % 2 == 0 && TM % 32 == 0, "ring slot = step parity; whole pixel tiles per half");
+  constexpr int nsteps = 9 * NCS;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // pixel half, channel quarter (64)
+  const int q = lane >> 4, n = lane & 15;
+  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * x6::TN;
+  const int HW = a.H * a.W;
+
+  if (tid < RB / 16) *reinterpret_cast<uint4*>(lds + a.ZOFF + tid * 16) = make_uint4(0, 0, 0, 0);
+
+  // the lane's pixel in tile mi: staged row prow0 + 16 mi at tap (0, 0); byte mi of okw: its taps in the image
+  const int prow0 = wm * (TM / 2) + n + a.HALO;
+  uint32_t okw[2] = {0u, 0u};
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = m0 + wm * (TM / 2) + mi * 16 + n;
+    if (m < a.M) {
+      const int p = m % HW, y = p / a.W, x = p - y * a.W;
+      const uint32_t b = 16u | (y > 0 ? 1u : 0u) | (y < a.H - 1 ? 2u : 0u) | (x > 0 ? 4u : 0u) | (x < a.W - 1 ? 8u : 0u);
+      okw[mi >> 2] |= b << (8 * (mi & 3));
+    }
+  }
+
+  // weight ring: k step j = tap * NCS + channel step (the pack's own order); three parts per fragment
+  const int KS = 9 * CIN / 32;
+  const uint4* wbase = reinterpret_cast<const uint4*>(a.wx) + (size_t)(n0 / 16 + wn * 4) * KS * 64;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wbase), 0, 0x7fffffff, 0x00020000);
+  const int pstride = (int)(a.part * 2);  // bytes per part
+  auto wload = [&](int ct, int part, int s) {
+    s = s < nsteps ? s : nsteps - 1;
+    return __builtin_bit_cast(bf16x8,
+                              __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + (ct * KS + s) * 1024, 0));
+  };
+  bf16x8 bq[2][3][4];  // [step parity][part][column tile]
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) bq[cc][pt][ct] = wload(ct, pt, cc);
+
+  f32x4 acc[MT][4];
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[mi][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // stage rows [m0 - HALO, m0 - HALO + TM + 2 HALO) x all Cin channels (f32): 1-KiB block i holds chunks
+  // 64 i .. 64 i + 63 (row g / NC, physical chunk g % NC = logical chunk ^ (row & 15))
+  for (int i = wave; i < a.NI; i += 8) {
+    const int g = i * 64 + lane, r = g / NC, s = g - r * NC;
+    int m = m0 - a.HALO + r;
+    m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);
+    const float* src = a.in + (size_t)m * CIN + ((s ^ (r & 15)) << 2);
+    __builtin_amdgcn_global_load_lds(src, lds + i * 1024, 16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // a tap's row offsets per pixel tile (the zero row for a tap leaving the image; any key reads it as 0)
+  auto tap_set = [&](int t, int (&rb)[MT]) {
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    const uint32_t need = 16u | (dy < 0 ? 1u : 0u) | (dy > 0 ? 2u : 0u) | (dx < 0 ? 4u : 0u) | (dx > 0 ? 8u : 0u);
+    const int shift = dy * a.W + dx;
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) {
+      const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
+      rb[mi] = ok ? (prow0 + 16 * mi + shift) * RB : a.ZOFF;
+    }
+  };
+  // the 8 f32 channels 32 c + 8 q .. of the lane's row: chunks 8c + 2q, 8c + 2q + 1 (swizzled by row & 15)
+  auto frag = [&](const int (&rb)[MT], int c, int mi, uint4& u0, uint4& u1) {
+    const int key = ((unsigned)rb[mi] / RB) & 15, ch = 8 * c + 2 * q;
+    u0 = *reinterpret_cast<const uint4*>(lds + rb[mi] + ((ch ^ key) << 4));
+    u1 = *reinterpret_cast<const uint4*>(lds + rb[mi] + (((ch + 1) ^ key) << 4));
+  };
+  constexpr int NF = MT * NCS;  // fragments per tap in (channel step, pixel tile) order
+  static_assert(NF % 2 == 0, "rolling buffer");
+
+  int rbc[MT], rbn[MT];
+  tap_set(0, rbc);
+  uint4 f0[2], f1[2];  // rolling raw buffer, one fragment ahead
+  frag(rbc, 0, 0, f0[0], f1[0]);
+  int j = 0;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    tap_set(t < 8 ? t + 1 : t, rbn);
+#pragma unroll
+    for (int c = 0; c < NCS; ++c) {
+      const int sl = c & 1;
+      const int sn = j + 2;
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int idx = c * MT + mi, nx = idx + 1;
+        const uint4 u0 = f0[idx & 1], u1 = f1[idx & 1];
+        if (nx < NF)
+          frag(rbc, nx / MT, nx % MT, f0[nx & 1], f1[nx & 1]);
+        else if (t < 8)
+          frag(rbn, (nx - NF) / MT, (nx - NF) % MT, f0[nx & 1], f1[nx & 1]);
+        bf16x8 xh, xm, xl;
+        split8(u0, u1, xh, xm, xl);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          f32x4 v = acc[mi][ct];
+          // the small terms first, then the large ones (each an f32-accumulating bf16 MFMA)
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][2][ct], xh, v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][1][ct], xm, v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][0][ct], xl, v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][1][ct], xh, v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][0][ct], xm, v, 0, 0, 0);
+          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][0][ct], xh, v, 0, 0, 0);
+          acc[mi][ct] = v;
+        }
+      }
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) bq[sl][pt][ct] = wload(ct, pt, sn);
+      __builtin_amdgcn_sched_barrier(0);
+      ++j;
+    }
+#pragma unroll
+    for (int mi = 0; mi < MT; ++mi) rbc[mi] = rbn[mi];
+  }
+
+  // epilogue (f32): acc[mi][ct] = D[channel n0 + 64 wn + 16 ct + 4q + i][pixel m0 + TM/2 wm + 16 mi + n]
+  const int nb = n0 + wn * 64;
+  float4 bb[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
+  const float lo = a.relu ? 0.f : -__builtin_inff();
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = m0 + wm * (TM / 2) + mi * 16 + n;
+    const int mc = m < a.M ? m : a.M - 1;
+    float4 rv[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+      rv[ct] = a.res ? *reinterpret_cast<const float4*>(a.res + (size_t)mc * a.Cout + nb + ct * 16 + 4 * q)
+                     : make_float4(-0.f, -0.f, -0.f, -0.f);  // (acc + bias) + -0 is acc + bias
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      float4 o;
+      o.x = fmaxf((acc[mi][ct][0] + bb[ct].x) + rv[ct].x, lo);
+      o.y = fmaxf((acc[mi][ct][1] + bb[ct].y) + rv[ct].y, lo);
+      o.z = fmaxf((acc[mi][ct][2] + bb[ct].z) + rv[ct].z, lo);
+      o.w = fmaxf((acc[mi][ct][3] + bb[ct].w) + rv[ct].w, lo);
+      if (m < a.M) *reinterpret_cast<float4*>(a.out + (size_t)m * a.Cout + nb + ct * 16 + 4 * q) = o;
+    }
+  }
+}
+
+// the pixel tile for (W, Cin): 96, or 64 when that halo does not fit the LDS; 0 if neither fits
+int x6_geometry(int W, int Cin, X6Args& g) {
+  if (Cin != 128 && Cin != 256) return 0;
+  for (int tm : {96, 64}) {  // 128: the ring, 64 accumulators and the split fragments spill
+    const int halo = W + 1, hr = tm + 2 * halo, rb = Cin * 4;
+    const int ni = (hr * rb + 1023) / 1024, zoff = ni * 1024;
+    if (zoff + rb <= x6::LDS_MAX) {
+      g.HALO = halo, g.NI = ni, g.ZOFF = zoff;
+      return tm;
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks) {
+  X6Args g{};
+  return ks == 3 && H >= 2 && W >= 2 && Cout % 256 == 0 && x6_geometry(W, Cin, g) > 0 ? 1 : 0;
+}
+
+// out = act(conv3x3(in) + bias (+ res)) in f32 on contiguous NHWC images of B envs, every product as the
+// six split-bf16 terms (above); wx = the three bf16 parts of the f32 [Cout][3][3][Cin] weights, each in the
+// pack_lat16 packing, back to back (agent.py PackedNets._conv "wx").
+int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
+                 int Cin, int Cout, int relu, hipStream_t stream) {
+  MZ_CHECK_ARG(in && wx && bias && out && B > 0, -1);
+  MZ_CHECK_ARG(mzba_conv_x6_supported(H, W, Cin, Cout, 3), -2);
+  const long long M = (long long)B * H * W;
+  MZ_CHECK_ARG(M * Cin < (1LL << 31), -3);
+  X6Args a{(const float*)in, (const bf16_t*)wx, bias, (const float*)res, (float*)out, (int)M, H, W, Cin, Cout, relu};
+  const int tm = x6_geometry(W, Cin, a);
+  a.part = (long long)Cout * 9 * Cin;
+  const int lds = a.ZOFF + Cin * 4;
+  const dim3 grid((unsigned)((M + tm - 1) / tm), (unsigned)(Cout / x6::TN));
+  auto launch = [&](auto kern) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, x6::LDS_MAX);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kern, grid, dim3(x6::NT), lds, stream, a);
+  };
+  if (Cin == 256)
+    tm == 96 ? launch(conv_x6_kernel<256, 96>) : launch(conv_x6_kernel<256, 64>);
+  else
+    tm == 96 ? launch(conv_x6_kernel<128, 96>) : launch(conv_x6_kernel<128, 64>);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

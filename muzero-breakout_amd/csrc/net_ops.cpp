@@ -51,7 +51,7 @@ void check_dev(const at::Tensor& t, const char* name) {
 int64_t round64(int64_t c) { return (c + 63) / 64 * 64; }
 
 struct Conv {  // one conv (+ folded BN); PackedNets._conv
-  at::Tensor w, b, wf, wt, act_bias, wh;
+  at::Tensor w, b, wf, wt, act_bias, wh, wx;
   int64_t cin = 0, cout = 0, ks = 0, A = 0;
 };
 struct Lin {  // Linear head in NHWC flatten order; PackedNets._linear
@@ -85,13 +85,14 @@ struct NetPack : torch::CustomClassHolder {
   }
   void add_conv(const std::string& name, const at::Tensor& w, const at::Tensor& b, const c10::optional<at::Tensor>& wf,
                 const c10::optional<at::Tensor>& wt, const c10::optional<at::Tensor>& act_bias, int64_t cin, int64_t cout,
-                int64_t ks, int64_t A, const c10::optional<at::Tensor>& wh) {
+                int64_t ks, int64_t A, const c10::optional<at::Tensor>& wh, const c10::optional<at::Tensor>& wx) {
     Conv c;
     c.w = w, c.b = b, c.cin = cin, c.cout = cout, c.ks = ks, c.A = A;
     if (wf.has_value()) c.wf = *wf;
     if (wt.has_value()) c.wt = *wt;
     if (act_bias.has_value()) c.act_bias = *act_bias;
     if (wh.has_value()) c.wh = *wh;
+    if (wx.has_value()) c.wx = *wx;
     convs[name] = c;
   }
   void add_linear(const std::string& name, const at::Tensor& w, const at::Tensor& b, const c10::optional<at::Tensor>& wb,
@@ -141,7 +142,7 @@ struct NetRunner : torch::CustomClassHolder {
   NetPack* p;
   int64_t B, H, W, lhw, HW, plan = 0;
   bool use_lat = true, use_tower = true, use_fused = true, use_band = true, use_rep_tail = true, use_band_res = true,
-       use_rep_blocks = true, use_rep_trunk = true, use_halo = true;
+       use_rep_blocks = true, use_rep_trunk = true, use_halo = true, use_x6 = true;
   at::Tensor r_a, r_t, r_b, x, tt, rc, pc, vc;  // scratch, allocated on first use
   // live probe: HIP events around every tower launch / latent residual conv (eager launches only)
   bool probe_on = false;
@@ -209,6 +210,14 @@ struct NetRunner : torch::CustomClassHolder {
             const int32_t* act = nullptr) {
     env_stride = env_stride < 0 ? H_ * W_ * l.cin : env_stride;
     const bool ab = l.act_bias.defined();
+    // the f32 parity path's 3x3 convs: f32-faithful split-bf16 products (conv_x6)
+    if (l.wx.defined() && use_x6 && p->dtype == 0 && !slot && env_stride == H_ * W_ * l.cin && !ab &&
+        mzba_conv_x6_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks)) {
+      check_rc(mzba_conv_x6(in, vp(l.wx), vp<float>(l.b), res, out, (int)B, (int)H_, (int)W_, (int)l.cin, (int)l.cout,
+                            relu, s),
+               "mzba_conv_x6");
+      return;
+    }
     // large images (config 3: 21x21 latents, the 84x84 128 -> 256 conv): the halo-tiled kernel
     if (l.wh.defined() && use_halo && !slot && env_stride == H_ * W_ * l.cin && !ab &&
         mzba_conv_halo_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks)) {
@@ -688,6 +697,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              else if (k == "use_rep_blocks") r->use_rep_blocks = v;
              else if (k == "use_rep_trunk") r->use_rep_trunk = v;
              else if (k == "use_halo") r->use_halo = v;
+             else if (k == "use_x6") r->use_x6 = v;
              else TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
            })
       .def("get_flag",
@@ -701,6 +711,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              if (k == "use_rep_blocks") return r->use_rep_blocks;
              if (k == "use_rep_trunk") return r->use_rep_trunk;
              if (k == "use_halo") return r->use_halo;
+             if (k == "use_x6") return r->use_x6;
              TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
              return false;
            })

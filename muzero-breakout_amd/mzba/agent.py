@@ -44,6 +44,19 @@ def pack_lat16(wp, cout, ks, cin):
     return wp.reshape(cout // 16, 16, K // 32, 4, 8).transpose(0, 2, 3, 1, 4).reshape(-1)
 
 
+def split_pack_x6(wp, cout, ks, cin):
+    """mzba_conv_x6's weights: the f32 weights [Cout][tap][Cin] split into three bf16 parts hi = bf16(w),
+    mid = bf16(w - hi), lo = bf16(w - hi - mid) (round to nearest even), each in the pack_lat16 packing, back to
+    back, as one bf16 tensor."""
+    w = torch.tensor(np.asarray(wp, dtype=np.float64).astype(np.float32).reshape(cout, -1))
+    hi = w.to(torch.bfloat16)
+    r = w - hi.float()
+    mid = r.to(torch.bfloat16)
+    lo = (r - mid.float()).to(torch.bfloat16)
+    return torch.cat([torch.tensor(pack_lat16(part.float().numpy(), cout, ks, cin)).to(torch.bfloat16)
+                      for part in (hi, mid, lo)])
+
+
 def pack_tower_conv(w):
     """3x3 conv weight (OIHW, BN folded) -> the fused tower's packing: pack_lat16 with the taps
     ordered (dx, dy) (tower.hip walks column shifts outermost)."""
@@ -125,7 +138,7 @@ class PackedNets:
 
         def conv(name, c):
             n.add_conv(name, c["w"], c["b"], c.get("wf"), c.get("wt"), c.get("act_bias"), c["cin"], c["cout"], c["ks"],
-                       c.get("A", 0), c.get("wh"))
+                       c.get("A", 0), c.get("wh"), c.get("wx"))
 
         for i, (kind, layer) in enumerate(self.rep):
             if kind == "conv":
@@ -350,6 +363,9 @@ class PackedNets:
             # config 3's large images (mzba_conv_halo): pack_lat16 of [Cout][tap][Cin]
             layer["wh"] = torch.tensor(pack_lat16(wp.reshape(cout, -1), cout, k, cin_p),
                                        dtype=torch.float32).to(self.tdt).to(self.device)
+        if (hw is not None and self.dtype == "f32" and act_w is None
+                and L.lib().mzba_conv_x6_supported(hw[0], hw[1], cin_p, cout, k)):
+            layer["wx"] = split_pack_x6(wp, cout, k, cin_p).to(self.device)
         if band and self.dtype == "bf16" and k == 3 and L.lib().mzba_conv_band_supported(16, 20, cin, cout, 3):
             # representation convs at full resolution: the band kernel's packing (tower order)
             layer["wt"] = torch.tensor(np.concatenate([pack_tower_conv(w), np.zeros(LAT_PAD_ELEMS)]),
@@ -398,7 +414,7 @@ class NetRunner:
     stream — representation_ / dynamics_ / prediction_ / prediction_tree_ (`torch.ops.mz`)."""
 
     FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail", "use_band_res", "use_rep_blocks",
-             "use_rep_trunk", "use_halo")
+             "use_rep_trunk", "use_halo", "use_x6")
 
     def __init__(self, packed, B, H, W):
         self.p = packed

@@ -595,3 +595,13 @@ def test_learner_fused_bn_statistics_track_separate_passes():
               f"{ff.min():.4f}, sep~f32 {np.median(sf):.4f} / {sf.min():.4f}")
         assert np.median(fs) >= 0.9, (seed, np.median(fs))
         assert np.median(ff) >= np.median(sf) - 0.02 and ff.min() >= sf.min() - 0.1, (seed, ff, sf)
+        # per tensor where a wiring error shows and the chaos does not: the three Linear heads' weight
+        # gradients (activation x logit gradient of the last layer, each a single consumer)
+        heads = [k for k in out["sep"][1] if k.endswith(("reward_head.2.weight", "policy_head.2.weight",
+                                                          "value_head.2.weight"))]
+        assert len(heads) == 3
+        for k in heads:
+            a, b = out["fused"][1][k].flatten().double(), out["sep"][1][k].flatten().double()
+            cs = torch.nn.functional.cosine_similarity(a, b, dim=0).item()
+            print(f"seed {seed}: {k} fused~sep cosine {cs:.5f}")
+            assert cs >= 0.95, (seed, k, cs)

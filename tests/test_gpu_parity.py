@@ -619,6 +619,44 @@ def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res):
     assert (got - big.float()).abs().max().item() <= 1e-2 * scale
 
 
+@pytest.mark.parametrize("B,H,W,Cin,relu,with_res", [(1000, 4, 5, 256, 1, True), (37, 4, 5, 256, 0, False),
+                                                     (7, 16, 20, 128, 1, True), (3, 21, 21, 256, 1, True)])
+def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, relu, with_res):
+    """mzba_conv_x6 (the f32 parity path's latent convs as six split-bf16 MFMA products each) against an f64
+    conv of the same f32 operands: at least as close as the f32-input MFMA conv of the f32 path (mzba_conv2d
+    dtype 0) — within 2x its error + 1e-7 of the magnitude — and within 2e-6 of the magnitude absolutely
+    (ragged tiles, tiles crossing envs, every tap that leaves the image)."""
+    from mzba import _lib as L
+    from mzba.agent import split_pack_x6
+    Cout = 256
+    assert L.lib().mzba_conv_x6_supported(H, W, Cin, Cout, 3)
+    g = torch.Generator(device="cuda").manual_seed(B + Cin + W)
+    dev = torch.device("cuda")
+    x = torch.rand(B, H, W, Cin, generator=g, device=dev)
+    w = torch.randn(Cout, 3, 3, Cin, generator=g, device=dev) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=g, device=dev) * 0.1
+    res = torch.rand(B, H, W, Cout, generator=g, device=dev) if with_res else None
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), b.double(),
+                                     padding=1).permute(0, 2, 3, 1)
+    if with_res:
+        ref = ref + res.double()
+    if relu:
+        ref = torch.relu(ref)
+    wx = split_pack_x6(w.cpu().numpy().reshape(Cout, -1), Cout, 3, Cin).cuda()
+    out = torch.full((B, H, W, Cout), float("nan"), device=dev)
+    L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu, L.stream())
+    f32 = torch.empty(B, H, W, Cout, device=dev)
+    wd = w.reshape(Cout, -1).contiguous()
+    L.call("mzba_conv2d", 0, L.ptr(x), H * W * Cin, None, 0, L.ptr(wd), L.ptr(b), None, None, 0, L.ptr(res), L.ptr(f32),
+           B, H, W, Cin, Cout, 3, relu, L.stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    scale = ref.abs().max().item()
+    e6, e32 = (out.double() - ref).abs().max().item(), (f32.double() - ref).abs().max().item()
+    print(f"conv_x6 {B}x{H}x{W} {Cin}: max err vs f64 {e6 / scale:.2e} of the magnitude, f32 MFMA conv {e32 / scale:.2e}")
+    assert e6 <= 2 * e32 + 1e-7 * scale and e6 <= 2e-6 * scale, (e6 / scale, e32 / scale)
+
+
 # ------------------------------------------------------------------------------ MCTS
 @pytest.mark.parametrize("tag", ["b16_s50", "b4_s200"])
 def test_mcts_replay_bit_exact(tag):

@@ -5,14 +5,14 @@
 # passes of the dominant kernel. Every GPU step has its own time limit; any failure ends the script.
 # usage (repo root on the box): bash tools/gpu_r4.sh TAG [skip-tests]
 set -euo pipefail
-export TMPDIR=/tmp
+export TMPDIR=/tmp MZBA_LIB_PARTIAL=1
 O=gpurun_out/$1
 M=$PWD/muzero-breakout_amd/mzba
 mkdir -p $O
 if [ "${2:-}" != skip-tests ]; then
-  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "halo" -x -v -s --timeout 200 --timeout-method thread \
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "halo or x6 or nets_f32" -x -v -s --timeout 200 --timeout-method thread \
     > $O/pytest_halo.txt 2>&1 || { tail -60 $O/pytest_halo.txt; exit 1; }
-  grep -E "conv_halo|passed|failed" $O/pytest_halo.txt | tail -8
+  grep -E "conv_halo|conv_x6|passed|failed" $O/pytest_halo.txt | tail -12
   timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread \
     > $O/pytest.txt 2>&1 || { tail -60 $O/pytest.txt; exit 1; }
   tail -3 $O/pytest.txt
@@ -33,6 +33,8 @@ for v in halo no-halo; do
     > $O/bench_c3_$v.json 2> $O/bench_c3_$v.err
   python3 -c "import json; d=json.load(open('$O/bench_c3_$v.json')); r=d['roofline']; print('config 3 $v', round(d['value'],1), round(r['avg_ms_per_conv'],4), round(r['frac'],4), r['kernel'])"
 done
+timeout -k 10 600 python bench.py --steps 8 --warmup 2 > $O/bench_full.json 2> $O/bench_full.err
+python3 -c "import json; d=json.load(open('$O/bench_full.json')); p=d['parity_path']; print('headline', round(d['value'],1), 'match_full', d['visit_count_match_full'], 'parity x6', round(p['value'],1), 'f32mfma', round(p['vs_f32_mfma_path']['value'],1), 'x6~f32', p['vs_f32_mfma_path']['visit_count_match'], 'cpu', d['cpu_baseline']['value'])"
 bash tools/pmc_towerp_sq.sh $1/sq_new
 python3 tools/sq_record.py $O/sq_new/sq1.json $O/sq_new/sq2.json 4096 towerp_kernel gpurun_out/$1/sq_new $O/tower_sq_counters.json
 echo r4 done
