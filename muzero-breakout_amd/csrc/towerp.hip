@@ -377,46 +377,18 @@ __device__ __forceinline__ void tp_conv(uint8_t* __restrict__ lds, const uint4* 
   PSTAMP(4 + 5 * ci);
   __syncthreads();  // every wave has read the whole image
   PSTAMP(5 + 5 * ci);
-  // Write-back in whole 16-B chunks: lanes of k quarters q and q ^ 1 (rows 2j, 2j + 1 of the wave)
-  // hold the two 8-B halves of the same chunk (channels ch and ch + 4 of row n). For a pixel pair
-  // (p, p + 1) one v_permlane16_swap per dword hands q-odd lanes' pixel-p half to the q-even lane and
-  // the q-even lanes' pixel-(p + 1) half to the q-odd lane: the q-even lane then stores pixel p's chunk,
-  // the q-odd lane pixel p + 1's — 40 ds_write_b128 per wave instead of 80 ds_write_b64, each lane
-  // group of 16 covering the 16 distinct swizzled chunks of its rows (every bank once). conv1's read of
-  // the residual loads the same chunks and swaps back into the accumulator layout (the swap is an
-  // involution). Data movement only: the image is bit-identical.
   int cofs[tp::CT];
 #pragma unroll
-  for (int ct = 0; ct < tp::CT; ++ct)
-    cofs[ct] = n * tp::ROWB + ((((64 * wave + 16 * ct + 4 * q) >> 3) ^ n) << 4) + (q & 1) * tp::PIX;
-  // opaque per conv: left loop-invariant, the compiler hoists the 40 pixel-pair addresses out of the block
-  // loop and spills them across the k loops
-#pragma unroll
-  for (int ct = 0; ct < tp::CT; ++ct) asm volatile("" : "+v"(cofs[ct]));
-  auto swap2 = [](uint2& a, uint2& b) {
-    const auto x = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
-    const auto y = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
-    a = make_uint2(x[0], y[0]);
-    b = make_uint2(x[1], y[1]);
-  };
-  // one pixel pair at a time (a scheduling barrier per pair: hoisting every accumulator read ahead of the
+  for (int ct = 0; ct < tp::CT; ++ct) cofs[ct] = tp_cofs(64 * wave + 16 * ct + 4 * q, n);
+  // one pixel at a time (a scheduling barrier per pixel: hoisting every accumulator read ahead of the
   // stores spilled the packed first-pass output)
 #pragma unroll
-  for (int p = 0; p < tp::P; p += 2) {
+  for (int p = 0; p < tp::P; ++p) {
 #pragma unroll
     for (int ct = 0; ct < tp::CT; ++ct) {
-      uint4* ptr = reinterpret_cast<uint4*>(lds + p * tp::PIX + cofs[ct]);
-      if (SAVE) {
-        const uint4 r = *ptr;
-        uint2 r0 = make_uint2(r.x, r.y), r1 = make_uint2(r.z, r.w);
-        swap2(r0, r1);
-        res[ct >> 1][p][ct & 1] = r0;
-        res[ct >> 1][p + 1][ct & 1] = r1;
-      }
-      uint2 a = ct < 2 ? out0[p][ct] : tp_pack<EL>(acc[p][ct - 2]);
-      uint2 b = ct < 2 ? out0[p + 1][ct] : tp_pack<EL>(acc[p + 1][ct - 2]);
-      swap2(a, b);
-      *ptr = make_uint4(a.x, a.y, b.x, b.y);
+      uint2* ptr = reinterpret_cast<uint2*>(lds + p * tp::PIX + cofs[ct]);
+      if (SAVE) res[ct >> 1][p][ct & 1] = *ptr;
+      *ptr = ct < 2 ? out0[p][ct] : tp_pack<EL>(acc[p][ct - 2]);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
