@@ -57,6 +57,13 @@ MZ_DEV void split8(const uint4& u0, const uint4& u1, bf16x8& h, bf16x8& m, bf16x
   }
 }
 
+// swizzle key of staged row r. A fragment read puts rows n = 0-3, 12-15 of k quarter q and rows 4-11 of
+// quarter q ^ 1 in one ds_read_b128 lane group (MI355X_MICROARCH.md LDS table); a lane's chunks are 8c + 2q
+// (+ 1), so the groups' chunks differ in bit 1: with this key (conv_halo.hip's hkey with bits 0 and 1
+// swapped) the 16 chunks of ANY 16 consecutive rows differ in every group (tools/swizzle_search.py; key
+// r & 15 was 2-way conflicted at every shift)
+MZ_DEV int xkey(int r) { return (r & 1) | (((r >> 2) & 1) * 10) | (((r >> 1) & 1) << 2); }
+
 template <int CIN, int TM>
 __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
   constexpr int RB = CIN * 4;        // bytes per staged row (f32)
@@ -113,18 +120,19 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
     for (int ct = 0; ct < 4; ++ct) acc[mi][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // stage rows [m0 - HALO, m0 - HALO + TM + 2 HALO) x all Cin channels (f32): 1-KiB block i holds chunks
-  // 64 i .. 64 i + 63 (row g / NC, physical chunk g % NC = logical chunk ^ (row & 15))
+  // 64 i .. 64 i + 63 (row g / NC, physical chunk g % NC = logical chunk ^ xkey(row))
   for (int i = wave; i < a.NI; i += 8) {
     const int g = i * 64 + lane, r = g / NC, s = g - r * NC;
     int m = m0 - a.HALO + r;
     m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);
-    const float* src = a.in + (size_t)m * CIN + ((s ^ (r & 15)) << 2);
+    const float* src = a.in + (size_t)m * CIN + ((s ^ xkey(r)) << 2);
     __builtin_amdgcn_global_load_lds(src, lds + i * 1024, 16, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // a tap's row offsets per pixel tile (the zero row for a tap leaving the image; any key reads it as 0)
+  // a tap's row offsets per pixel tile (the zero row for a tap leaving the image; any key reads it as 0); the
+  // row's key is recomputed from the offset at each read (kept beside the offsets, the keys spilled)
   auto tap_set = [&](int t, int (&rb)[MT]) {
     const int dy = t / 3 - 1, dx = t % 3 - 1;
     const uint32_t need = 16u | (dy < 0 ? 1u : 0u) | (dy > 0 ? 2u : 0u) | (dx < 0 ? 4u : 0u) | (dx > 0 ? 8u : 0u);
@@ -135,9 +143,10 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
       rb[mi] = ok ? (prow0 + 16 * mi + shift) * RB : a.ZOFF;
     }
   };
-  // the 8 f32 channels 32 c + 8 q .. of the lane's row: chunks 8c + 2q, 8c + 2q + 1 (swizzled by row & 15)
+  // the 8 f32 channels 32 c + 8 q .. of the lane's row: chunks 8c + 2q, 8c + 2q + 1 (swizzled by xkey(row))
   auto frag = [&](const int (&rb)[MT], int c, int mi, uint4& u0, uint4& u1) {
-    const int key = ((unsigned)rb[mi] / RB) & 15, ch = 8 * c + 2 * q;
+    const int ch = 8 * c + 2 * q;
+    const int key = xkey(((unsigned)rb[mi] / RB) & 15);
     u0 = *reinterpret_cast<const uint4*>(lds + rb[mi] + ((ch ^ key) << 4));
     u1 = *reinterpret_cast<const uint4*>(lds + rb[mi] + (((ch + 1) ^ key) << 4));
   };
@@ -248,7 +257,7 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
   MZ_CHECK_ARG(in && wx && bias && out && B > 0, -1);
   MZ_CHECK_ARG(mzba_conv_x6_supported(H, W, Cin, Cout, 3), -2);
   const long long M = (long long)B * H * W;
-  MZ_CHECK_ARG(M * Cin < (1LL << 31), -3);
+  MZ_CHECK_ARG(M + 256 < (1LL << 31), -3);  // pixel indices in int (global offsets are size_t)
   X6Args a{(const float*)in, (const bf16_t*)wx, bias, (const float*)res, (float*)out, (int)M, H, W, Cin, Cout, relu};
   const int tm = x6_geometry(W, Cin, a);
   a.part = (long long)Cout * 9 * Cin;
