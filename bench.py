@@ -59,8 +59,6 @@ def parse():
     ap.add_argument("--minibatch", type=int, default=512, help="learner workload minibatch (config.yaml:7)")
     ap.add_argument("--no-halo", action="store_true",
                     help="A/B: large-image 3x3 convs on conv_big_bf16_kernel instead of the halo-tiled conv_halo_kernel")
-    ap.add_argument("--halo-single", action="store_true",
-                    help="A/B: the single-stage halo conv instead of its pipelined form (21x21 latent, Cin = Cout = 256)")
     ap.add_argument("--pow-threads", type=int, default=1,
                     help="intra-op threads of the reference process whose temperature pow the sampling reproduces "
                          "(splits torch's pow into per-thread chunks from 3 x global envs >= 32768 on)")
@@ -270,8 +268,7 @@ def big_conv_kernel(args, B, p):
     if p.lh * p.lw <= 160:
         return "conv_lat"
     if args.dtype == "bf16" and not args.no_halo and L.lib().mzba_conv_halo_supported(p.lh, p.lw, p.c1, p.c1, 3):
-        # the pipelined form where its two 128-channel buffers fit (include/mzba.h mzba_conv_halo_set_variant)
-        return "conv_halo_pipe" if p.c1 == 256 and p.lw <= 22 and not args.halo_single else "conv_halo"
+        return "conv_halo"
     return "conv_big_bf16" if B * p.lh * p.lw >= 65536 and args.dtype == "bf16" else "conv_igemm"
 
 
@@ -511,8 +508,6 @@ def main():
     if args.no_halo:
         loop.ws.runner.use_halo = False
         loop.rep_runner.use_halo = False
-    if args.halo_single:
-        L.call("mzba_conv_halo_set_variant", 1)
     gather = TrajectoryGather(world, rank, RECORD_K, B, H * W, f"cuda:{local}")
     loop.reset(0)
     last_flush = [0]

@@ -117,11 +117,6 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
                  int Cin, int Cout, int relu, hipStream_t stream);
 int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
                    int Cin, int Cout, int relu, hipStream_t stream);
-/* Cin = Cout = 256 with W <= 22 (the 21x21 latent) runs a pipelined form by default: one persistent workgroup
- * per CU, two 128-channel halo buffers, the next stage staged by LDS-DMA while the current one computes (sums in
- * channel-block order; within bf16 rounding of the single-stage kernel). v = 1 forces the single-stage kernel
- * (A/B runs), 0 restores the default. */
-int mzba_conv_halo_set_variant(int v);
 
 /* Latent-resolution conv (bf16): same contract as mzba_conv2d for H*W <= 160, Cin in {64,128,256},
  * Cout % 32 == 0, but the weights are in fragment-major order wf[Cout/32][2][ks*ks][Cin/32][64][8]

@@ -15,8 +15,9 @@
 //   * LDS row r = pixel m0 - (W + 1) + r, 16-B chunks XOR-swizzled by hkey(r): a B fragment (16
 //     consecutive rows = 16 pixels of a tile shifted by any tap, 8 channels per lane) is conflict-free in each
 //     of ds_read_b128's four 16-lane groups for every shift (key r & 15, round 3, was 2-way conflicted at odd
-//     shifts); LDS-DMA writes lane-linear 1-KiB blocks, so the swizzle is applied on the source addresses. One extra zero row: a tap that leaves the image (y + dy or x + dx outside, which the
-//     flattened shift would wrap into the neighbouring row or env) reads it instead.
+//     shifts); LDS-DMA writes lane-linear 1-KiB blocks, so the swizzle is applied on the source addresses.
+//     A tap that leaves the image (y + dy or x + dx outside, which the flattened shift wraps into the
+//     neighbouring row or env) reads a 16-row zero block instead, at its own row's bank slot.
 //   * 8 waves (two per SIMD), each 128 pixels (8 tiles) x 64 output channels (4 column tiles): 32
 //     accumulators (128 AGPRs); weights = MFMA A operand from a two-k-step register ring (buffer_load_dwordx4
 //     off a wave-uniform resource, the fragment-major packing pack_lat16 of [Cout][tap][Cin]), activations =
@@ -24,8 +25,6 @@
 //     MFMAs, pixel-tile major (each B fragment feeds its 4 MFMAs back to back).
 //   * epilogue: + bias (+ residual), ReLU, bf16; a lane holds 4 consecutive channels of one pixel.
 #include "common.h"
-
-#include <algorithm>
 
 namespace {
 
@@ -47,7 +46,7 @@ struct HaloArgs {
   bf16_t* out;         // [M][Cout]
   int M, H, W, Cin, Cout, relu;
   int HALO, HR, CB;    // halo rows each side, staged rows, channels per staged block
-  int NI, ZOFF;        // LDS-DMA 1-KiB blocks per staging, byte offset of the zero row
+  int NI, ZOFF;        // LDS-DMA 1-KiB blocks per staging, byte offset of the zero block (pipelined: row)
 };
 
 // swizzle key of staged row r: ds_read_b128 serves a wave in lane groups {0-3, 12-15, 20-27}, ... (rows
@@ -113,12 +112,12 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   const int KS = 9 * a.Cin / 32;            // k steps of the whole conv (pack stride per column tile)
   constexpr int nsteps = NBLK * 9 * NCS;  // NBLK = Cin / CB
 
-  // the zero row (never overwritten by staging)
-  if (tid < RB / 16) *reinterpret_cast<uint4*>(lds + a.ZOFF + tid * 16) = make_uint4(0, 0, 0, 0);
+  // the zero block: 16 rows (never overwritten by staging)
+  for (int i = tid; i < RB; i += hl::NT) *reinterpret_cast<uint4*>(lds + a.ZOFF + i * 16) = make_uint4(0, 0, 0, 0);
 
   // per pixel tile mi of the wave: the lane's pixel is staged row prow0 + 16 mi at tap (0, 0); byte mi of
   // okw[mi / 4] says which taps stay in the image (bit 0: y > 0, 1: y < H - 1, 2: x > 0, 3: x < W - 1,
-  // 4: the pixel exists — rows past M read only the zero row)
+  // 4: the pixel exists — rows past M read only the zero block)
   const int prow0 = wm * 128 + n + a.HALO;
   uint32_t okw[2] = {0u, 0u};
 #pragma unroll
@@ -158,8 +157,8 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
       acc[mi][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
-  // a tap's fragment addresses: per pixel tile, the byte offset of its staged row (the zero row for a tap that
-  // leaves the image); the row's swizzle key is recomputed from the offset at each read (kept beside the
+  // a tap's fragment addresses: per pixel tile, the byte offset of its staged row (of the zero block for a tap
+  // that leaves the image); the row's swizzle key is recomputed from the offset at each read (kept beside the
   // offsets, the keys' registers made the loop spill)
   auto tap_set = [&](int t, int (&rb)[8]) {
     const int dy = t / 3 - 1, dx = t % 3 - 1;
@@ -169,10 +168,13 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
     for (int mi = 0; mi < 8; ++mi) {
       const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
       const int r = prow0 + 16 * mi + shift;
-      rb[mi] = ok ? r * RB : a.ZOFF;  // the zero row reads zeros under any key
+      rb[mi] = ok ? r * RB : a.ZOFF + (r & 15) * RB;  // the zero block's row with this row's key
     }
   };
-  // B fragment of pixel tile mi, channel step c (32 channels: chunk 4c + q of the row)
+  // B fragment of pixel tile mi, channel step c (32 channels: chunk 4c + q of the row). A lane whose tap leaves
+  // the image reads row (r & 15) of a 16-row zero block at ZOFF (16-row aligned): the bank slot its own row
+  // would take. One shared zero row put that lane on a slot one of the 15 others held in ~7/8 of such
+  // fragments (SQ_LDS_BANK_CONFLICT 0.31 of LDS-active cycles in config 3, profiles/r04/r4f)
   auto frag = [&](const int (&rb)[8], int c, int mi) {
     const int key = hkey(((unsigned)rb[mi] / RB) & 15);
     return *reinterpret_cast<const bf16x8*>(lds + rb[mi] + (((4 * c + q) ^ key) << 4));
@@ -245,203 +247,16 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
     halo_epilogue<false>(a, acc, m0, n0 + wn * 64, wm, q, n);
 }
 
-// Pipelined form (Cin = Cout = 256: NB = 2 channel blocks of 128 per tile): a persistent workgroup per CU walks its tiles (tile, channel
-// block of 128) as STAGES through two LDS buffers of 128-channel halo rows: while the waves run stage s's 9
-// taps x 4 channel steps from one buffer, LDS-DMA fills the other with stage s + 1 (this tile's next block or
-// the next tile's first). The single-stage kernel stages all of Cin and then waits for it with nothing else
-// on the CU (one workgroup per CU: 150 KiB of LDS), ~5 us of ~60 per 21x21 tile. Both buffers fit while
-// 2 x (256 + 2 W + 2) rows x 256 B <= 160 KiB: W <= 22. Every wave issues the same NPW DMA blocks per stage
-// (the surplus re-writes its buffer's last block with the same bytes), so the wait for stage s is one
-// s_waitcnt vmcnt(NPW) issued after stage s + 1's DMA (VMEM ops retire in order; it also retires the
-// weight ring's loads and the previous tile's epilogue stores). The accumulation order differs from the
-// single-stage kernel's (all taps of channels 0-127, then of 128-255, instead of tap-major): both are within
-// the f32 tolerance of a plain torch evaluation, not bit-equal. (NB = 1, Cin 128, spilled 33 registers and has
-// no 21x21 user: Cin 128 convs run at 84x84 in config 3, where two buffers do not fit.)
-namespace hp {
-constexpr int NPW = 10;  // DMA blocks per wave per stage: NI <= 80 1-KiB blocks
-}
-
-template <int NB>
-__global__ __launch_bounds__(hl::NT, 1) void conv_halo_pipe_kernel(HaloArgs a) {
-  constexpr int CB = 128, RB = 256, NC = 16, NCS = 4, NPW = hp::NPW;
-  constexpr int KS = 9 * NB * NCS;  // k steps per tile = 9 Cin / 32
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int q = lane >> 4, n = lane & 15;
-  const int HW = a.H * a.W;
-  const int ntiles = (a.M + hl::TM - 1) / hl::TM;
-  const int BUF = a.ZOFF >> 1;  // buffer stride: a multiple of 16 rows, so a row's key is hkey(offset / RB)
-
-  if (tid < RB / 16) *reinterpret_cast<uint4*>(lds + a.ZOFF + tid * 16) = make_uint4(0, 0, 0, 0);
-
-  // stage (tile, block b) into buffer k: rows [m0 - HALO, m0 - HALO + HR) x channels [128 b, 128 b + 128)
-  auto dma = [&](int tile, int b, int k) {
-    const int m0 = tile * hl::TM;
-    // the block / row indices recomputed per call from opaque copies: common to every stage, they were kept
-    // live across the tile loop (and spilled)
-    int wv = wave, ln = lane;
-    asm volatile("" : "+s"(wv), "+v"(ln));
-#pragma unroll
-    for (int u = 0; u < NPW; ++u) {
-      const int i = min(wv + 8 * u, a.NI - 1);
-      const int g = i * 64 + ln, r = g / NC, s = g - r * NC;
-      int m = m0 - a.HALO + r;
-      m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);
-      const bf16_t* src = a.in + (size_t)m * a.Cin + b * CB + ((s ^ hkey(r)) << 3);
-      __builtin_amdgcn_global_load_lds(src, lds + k * BUF + i * 1024, 16, 0, 0);
-    }
-  };
-  // k step j of a tile (block, tap, channel step) -> pack k step; past the tile's last: the next tile's first
-  auto kstep = [&](int j) {
-    j = j >= KS ? j - KS : j;
-    const int blk = j / (9 * NCS), r = j - blk * 9 * NCS, t = r / NCS, c = r - t * NCS;
-    return t * (NB * NCS) + blk * NCS + c;
-  };
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint4*>(reinterpret_cast<const uint4*>(a.wh) + (size_t)(wn * 4) * KS * 64), 0, 0x7fffffff, 0x00020000);
-  int sbase = 0;  // the stage's block offset (opaque: the constant weight offsets are not hoisted out of the loop)
-  auto wload = [&](int ct, int off) {  // off: byte offset of the k step in the column tile's pack
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, ct * KS * 1024 + off, 0));
-  };
-
-  bf16x8 bq[2][4];
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    bq[0][ct] = wload(ct, kstep(0) * 1024);
-    bq[1][ct] = wload(ct, kstep(1) * 1024);
-  }
-  if ((int)blockIdx.x < ntiles) dma(blockIdx.x, 0, 0);
-  const int prow0 = wm * 128 + n + a.HALO;
-  uint32_t okw[2] = {0u, 0u};
-  f32x4 acc[8][4];
-  // one stage per iteration (tile = the WG's st / NB-th, block b = st % NB): one copy of the 36-step body with
-  // the block's weight offset in an SGPR; the accumulators carry across a tile's NB stages
-#pragma unroll 1
-  for (int st = 0;; ++st) {
-    const int tile = (int)blockIdx.x + (st / NB) * (int)gridDim.x, b = st % NB, kbuf = st & 1;
-    if (tile >= ntiles) break;
-    const int m0 = tile * hl::TM;
-    if (b == 0) {
-      okw[0] = okw[1] = 0u;  // as conv_halo_kernel
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) {
-        const int m = m0 + wm * 128 + mi * 16 + n;
-        if (m < a.M) {
-          const int p = m % HW, y = p / a.W, x = p - y * a.W;
-          const uint32_t bits = 16u | (y > 0 ? 1u : 0u) | (y < a.H - 1 ? 2u : 0u) | (x > 0 ? 4u : 0u) | (x < a.W - 1 ? 8u : 0u);
-          okw[mi >> 2] |= bits << (8 * (mi & 3));
-        }
-      }
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[mi][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    const int ntile = b + 1 < NB ? tile : tile + (int)gridDim.x;
-    __syncthreads();  // every wave is done with the other buffer (the previous stage)
-    if (ntile < ntiles) {
-      dma(ntile, b + 1 < NB ? b + 1 : 0, kbuf ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPW) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();  // this stage's rows have landed from every wave
-    // this block's k steps t (NB NCS) + b NCS + c; the ring's prefetch two steps ahead crosses into the next
-    // block (b + 1) or the next tile's block 0 at the stage's last two steps
-    sbase = b * NCS * 1024;
-    const int snext = (b + 1 < NB ? b + 1 : 0) * NCS * 1024;
-    asm volatile("" : "+s"(sbase));
-    auto sstep = [&](int t, int c) {  // pack byte offset of (tap t, channel step c) of this block (t 9: the next block's tap 0)
-      return t < 9 ? sbase + (t * NB * NCS + c) * 1024 : snext + c * 1024;
-    };
-    const int vrow = kbuf * BUF + prow0 * RB;
-    // a fragment's address from scratch at each read (the tap's shift is wave-uniform; per-tap offset arrays
-    // for this tap and the next cost the registers the pipeline's loop state needs)
-    auto frag = [&](int t, int c, int mi) {
-      const int dy = t / 3 - 1, dx = t % 3 - 1;
-      const uint32_t need = 16u | (dy < 0 ? 1u : 0u) | (dy > 0 ? 2u : 0u) | (dx < 0 ? 4u : 0u) | (dx > 0 ? 8u : 0u);
-      const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
-      const int rb = ok ? vrow + (16 * mi + dy * a.W + dx) * RB : a.ZOFF;
-      const int key = hkey(((unsigned)rb / RB) & 15);  // buffers start on 16-row boundaries
-      return *reinterpret_cast<const bf16x8*>(lds + rb + (((4 * c + q) ^ key) << 4));
-    };
-    constexpr int NF = 8 * NCS;
-    bf16x8 fr[4];
-    fr[0] = frag(0, 0, 0);
-    fr[1] = frag(0, 0, 1);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-#pragma unroll
-      for (int c = 0; c < NCS; ++c) {
-        const int sl = c & 1;
-        const int tn = c + 2 < NCS ? t : t + 1, cn = c + 2 < NCS ? c + 2 : c + 2 - NCS;
-        const int sn = sstep(tn, cn);
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          const int idx = c * 8 + mi, nx = idx + 2;
-          if (nx < NF)
-            fr[nx & 3] = frag(t, nx >> 3, nx & 7);
-          else if (t < 8)
-            fr[nx & 3] = frag(t + 1, (nx - NF) >> 3, (nx - NF) & 7);
-          const bf16x8 f = fr[idx & 3];
-#pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][ct], f, acc[mi][ct], 0, 0, 0);
-        }
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) bq[sl][ct] = wload(ct, sn);
-#pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (b == NB - 1) {
-      if (a.res)
-        halo_epilogue<true>(a, acc, m0, wn * 64, wm, q, n);
-      else
-        halo_epilogue<false>(a, acc, m0, wn * 64, wm, q, n);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outstanding at exit
-}
-
-// pipelined geometry: two 128-channel buffers + the zero row; 0 if they do not fit
-int halo_pipe_geometry(int W, int Cin, int Cout, HaloArgs& g) {
-  const int halo = W + 1, hr = hl::TM + 2 * halo, rb = 256;
-  const int ni = (hr * rb + 1023) / 1024;
-  const int buf = (ni * 1024 + 4095) / 4096 * 4096;  // 16-row multiple: the swizzle key of a row is its offset's
-  if (Cin != 256 || Cout != 256 || ni > 8 * hp::NPW || 2 * buf + rb > hl::LDS_MAX) return 0;
-  g.HALO = halo, g.HR = hr, g.CB = 128, g.NI = ni, g.ZOFF = 2 * buf;
-  return g.ZOFF + rb;
-}
-
-static int g_halo_variant = 0;  // 0: pipelined where it fits, 1: single-stage only
-
-int halo_ncu() {
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
-  return ncu;
-}
-
 // staging geometry for a (W, Cin) pair: the whole Cin staged at once (one block; a rolled loop over channel
 // blocks would carry the accumulators across its back edge, which the compiler renames and copies), 0 if the
 // halo does not fit the LDS
 int halo_geometry(int W, int Cin, HaloArgs& g) {
   const int cb = Cin, halo = W + 1, hr = hl::TM + 2 * halo, rb = cb * 2;
   const int ni = (hr * rb + 1023) / 1024;
-  const int zoff = ni * 1024;
-  if ((cb != 128 && cb != 256) || zoff + rb > hl::LDS_MAX) return 0;
+  const int zoff = (ni * 1024 + 16 * rb - 1) / (16 * rb) * (16 * rb);  // the 16-row zero block, 16-row aligned
+  if ((cb != 128 && cb != 256) || zoff + 16 * rb > hl::LDS_MAX) return 0;
   g.HALO = halo, g.HR = hr, g.CB = cb, g.NI = ni, g.ZOFF = zoff;
-  return zoff + rb;
+  return zoff + 16 * rb;
 }
 
 }  // namespace
@@ -473,33 +288,11 @@ int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void
     }
     hipLaunchKernelGGL(kern, grid, dim3(hl::NT), lds, stream, a);
   };
-  HaloArgs pa = a;
-  const int plds = g_halo_variant == 0 ? halo_pipe_geometry(W, Cin, Cout, pa) : 0;
-  if (plds > 0) {  // persistent: one workgroup per CU (or per tile)
-    const long long ntiles = (M + hl::TM - 1) / hl::TM;
-    const dim3 pgrid((unsigned)std::min<long long>(ntiles, halo_ncu()));
-    auto plaunch = [&](auto kern) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, hl::LDS_MAX);
-        attr = true;
-      }
-      hipLaunchKernelGGL(kern, pgrid, dim3(hl::NT), plds, stream, pa);
-    };
-    plaunch(conv_halo_pipe_kernel<2>);
-  } else if (a.CB == 256) {
+  if (a.CB == 256)
     launch(conv_halo_kernel<256, 1>);
-  } else {
+  else
     launch(conv_halo_kernel<128, 1>);
-  }
   MZ_LAUNCH_CHECK();
-  return 0;
-}
-
-// 0: the pipelined kernel where its two buffers fit (default), 1: the single-stage kernel only (A/B)
-int mzba_conv_halo_set_variant(int v) {
-  if (v < 0 || v > 1) return -1;
-  g_halo_variant = v;
   return 0;
 }
 

@@ -35,7 +35,6 @@ SIGNATURES = {
     "mzba_conv2d_set_variant": [I],
     "mzba_conv_halo_supported": [I, I, I, I, I],
     "mzba_conv_halo": [P, P, P, P, P, I, I, I, I, I, I, P],
-    "mzba_conv_halo_set_variant": [I],
     "mzba_conv_x6_supported": [I, I, I, I, I],
     "mzba_conv_x6": [P, P, P, P, P, I, I, I, I, I, I, P],
     "mzba_conv_lat_supported": [I, I, I, I, I],

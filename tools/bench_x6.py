@@ -1,0 +1,76 @@
+"""Same-box A/B of the f32-faithful split-bf16 conv (mzba_conv_x6) wave splits and of the halo conv forms, at the
+acting loop's shapes: x6 at the 4x5 latent (B = 4096, the parity path's towers) and 8x10 (the representation
+tail), halo at config 3's 21x21 latent (B = 4096). HIP events around 20 launches after 3 warm-up launches,
+alternated twice. Prints one JSON line per (kernel, shape, variant). The variant setters
+(mzba_conv_x6_set_variant, mzba_conv_halo_set_variant) exist only in the A/B builds of round 4 (the rejected
+channel-slice x6 split; profiles/r04/halo_pipe/conv_halo_pipelined.patch); without them the default runs once per
+variant slot (variant None).
+  python tools/bench_x6.py"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "muzero-breakout_amd"))
+from mzba import _lib as L  # noqa: E402
+
+
+def timeit(fn, n=20, warm=3):
+    for _ in range(warm):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+def set_variant(name, v):
+    """variant setters a library may predate (A/B against an older build, MZBA_LIB_PARTIAL=1)"""
+    if hasattr(L.lib(), name):
+        L.call(name, v)
+        return v
+    return None
+
+
+def main():
+    tag = os.environ.get("MZBA_LIB", "libmzba.so").rsplit("/", 1)[-1]
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    C = 256
+    for (B, H, W) in ((4096, 4, 5), (4096, 8, 10)):
+        x = torch.rand(B, H, W, C, generator=g, device=dev)
+        wx = torch.randn(3 * C * 9 * C, generator=g, device=dev).to(torch.bfloat16)
+        b = torch.randn(C, generator=g, device=dev)
+        out = torch.empty(B, H, W, C, device=dev)
+        fl = 2.0 * B * H * W * C * 9 * C * 6
+        for rep in range(2):
+            for v in (0, 1):
+                v = set_variant("mzba_conv_x6_set_variant", v)
+                ms = timeit(lambda: L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), None, L.ptr(out), B, H, W, C, C, 1,
+                                           L.stream()))
+                print(json.dumps({"lib": tag, "kernel": "conv_x6", "shape": [B, H, W, C], "variant": v, "rep": rep, "ms": ms,
+                                  "bf16_tflops": fl / ms / 1e9, "frac_bf16_peak": fl / ms / 1e9 / 2500}), flush=True)
+        set_variant("mzba_conv_x6_set_variant", 0)
+        del x, wx, out
+    B, H, W = 4096, 21, 21
+    x = torch.randn(B, H, W, C, generator=g, device=dev).to(torch.bfloat16)
+    wh = torch.randn(C * 9 * C, generator=g, device=dev).to(torch.bfloat16)
+    b = torch.randn(C, generator=g, device=dev)
+    out = torch.empty(B, H, W, C, dtype=torch.bfloat16, device=dev)
+    fl = 2.0 * B * H * W * C * 9 * C
+    for rep in range(2):
+        for v in (0, 1):
+            v = set_variant("mzba_conv_halo_set_variant", v)
+            ms = timeit(lambda: L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(x), L.ptr(out), B, H, W, C, C, 1,
+                                       L.stream()), n=10)
+            print(json.dumps({"lib": tag, "kernel": "conv_halo", "shape": [B, H, W, C], "variant": v, "rep": rep, "ms": ms,
+                              "tflops": fl / ms / 1e9, "frac": fl / ms / 1e9 / 2500}), flush=True)
+    set_variant("mzba_conv_halo_set_variant", 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -7,6 +7,13 @@ set -euo pipefail
 export TMPDIR=/tmp
 O=gpurun_out/$1
 mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "x6 or nets_f32 or halo" -x -v --timeout 200 --timeout-method thread \
+  > $O/pytest_x6.txt 2>&1 || { tail -60 $O/pytest_x6.txt; exit 1; }
+grep -E "conv_x6|passed|failed" $O/pytest_x6.txt | tail -8
+for v in "" "--x6-split2"; do
+  timeout -k 10 600 python bench.py --steps 4 --warmup 1 --no-cpu $v > $O/bench_par$v.json 2> $O/bench_par$v.err
+  python3 -c "import json; d=json.load(open('$O/bench_par$v.json')); p=d['parity_path']; print('x6 $v', round(p['value'],1), 'f32mfma', round(p['vs_f32_mfma_path']['value'],1), 'x6~f32', p['vs_f32_mfma_path']['visit_count_match'], 'head', round(d['value'],1))"
+done
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $O/prof.log 2>&1
 python3 tools/rocpd_report.py stats $O/prof $O/kernel_stats_full.csv
 rm -rf $O/prof
