@@ -58,24 +58,24 @@ MZ_DEV int hkey(int r) { return ((r << 1) & 6) | (((r >> 2) & 1) * 9); }
 // + bias (+ residual), ReLU, bf16: (acc + bias) + res in f32, as conv_big_bf16_kernel; a lane stores 4
 // consecutive channels (8 B) of one pixel per (pixel tile, column tile); every residual load of a pixel tile
 // is issued before its first use
-template <bool RES>
-MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[8][4], int m0, int nb, int wm, int q, int n) {
-  float4 bb[4];
+template <bool RES, int MT, int CT>
+MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb, int nb, int q, int n) {
+  float4 bb[CT];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
+  for (int ct = 0; ct < CT; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
   const float lo = a.relu ? 0.f : -__builtin_inff();  // ReLU as max(v, 0); max(v, -inf) = v
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    const int m = m0 + wm * 128 + mi * 16 + n;
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = mb + mi * 16 + n;
     const int mc = m < a.M ? m : a.M - 1;
-    uint2 rv[4];
+    uint2 rv[CT];
     if (RES) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) rv[ct] = *reinterpret_cast<const uint2*>(a.res + (size_t)mc * a.Cout + nb + ct * 16 + 4 * q);
+      for (int ct = 0; ct < CT; ++ct) rv[ct] = *reinterpret_cast<const uint2*>(a.res + (size_t)mc * a.Cout + nb + ct * 16 + 4 * q);
     }
-    uint2 o[4];
+    uint2 o[CT];
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
+    for (int ct = 0; ct < CT; ++ct) {
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc[mi][ct][i] + (&bb[ct].x)[i];
@@ -91,21 +91,27 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[8][4], int m0, i
     }
     if (m < a.M) {
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) *reinterpret_cast<uint2*>(a.out + (size_t)m * a.Cout + nb + ct * 16 + 4 * q) = o[ct];
+      for (int ct = 0; ct < CT; ++ct) *reinterpret_cast<uint2*>(a.out + (size_t)m * a.Cout + nb + ct * 16 + 4 * q) = o[ct];
     }
   }
 }
 
-template <int CB, int NBLK>
+// WM = 2 pixel halves x 4 quarters of 64 channels. Measured and dropped (profiles/r04/halo_wm/, same box, B = 4096,
+// 21x21): WM = 1 (8 slices of 32 channels over all 256 pixels: no weight fragment loaded twice per workgroup,
+// half the per-CU L2 weight stream, twice the B reads) 1.76-1.85 ms vs 1.75-1.83; B fragments read 16 MFMAs
+// ahead instead of 8: 1.82-1.83 ms. Neither the weight stream nor the LDS read latency bounds this kernel.
+template <int CB, int NBLK, int WM = 2, int PFM = 1>
 __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   constexpr int RB = CB * 2;        // bytes per staged row
   constexpr int NC = CB / 8;        // 16-B chunks per row
   constexpr int NCS = CB / 32;      // 32-channel k steps per tap and block
+  constexpr int WN = 8 / WM, CT = 16 / WN, MT = 16 / WM;  // channel slices, column tiles / pixel tiles per wave
+  constexpr int PF = PFM * 8 / CT;  // fragment reads ahead: 8 PFM MFMAs
   static_assert(NCS % 2 == 0, "ring slot = channel step parity");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;  // pixel half (128), channel quarter (64)
+  const int wm = wave / WN, wn = wave % WN;  // pixel part (TM / WM), channel slice (16 CT)
   const int q = lane >> 4, n = lane & 15;
   const int m0 = blockIdx.x * hl::TM, n0 = blockIdx.y * hl::TN;
   const int HW = a.H * a.W;
@@ -118,11 +124,11 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   // per pixel tile mi of the wave: the lane's pixel is staged row prow0 + 16 mi at tap (0, 0); byte mi of
   // okw[mi / 4] says which taps stay in the image (bit 0: y > 0, 1: y < H - 1, 2: x > 0, 3: x < W - 1,
   // 4: the pixel exists — rows past M read only the zero block)
-  const int prow0 = wm * 128 + n + a.HALO;
-  uint32_t okw[2] = {0u, 0u};
+  const int prow0 = wm * (hl::TM / WM) + n + a.HALO;
+  uint32_t okw[MT / 4] = {};
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-    const int m = m0 + wm * 128 + mi * 16 + n;
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = m0 + wm * (hl::TM / WM) + mi * 16 + n;
     if (m < a.M) {
       const int p = m % HW, y = p / a.W, x = p - y * a.W;
       const uint32_t b = 16u | (y > 0 ? 1u : 0u) | (y < a.H - 1 ? 2u : 0u) | (x > 0 ? 4u : 0u) | (x < a.W - 1 ? 8u : 0u);
@@ -137,49 +143,41 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
     return t * (a.Cin / 32) + blk * NCS + c;
   };
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint4*>(reinterpret_cast<const uint4*>(a.wh) + (size_t)(n0 / 16 + wn * 4) * KS * 64), 0, 0x7fffffff,
+      const_cast<uint4*>(reinterpret_cast<const uint4*>(a.wh) + (size_t)(n0 / 16 + wn * CT) * KS * 64), 0, 0x7fffffff,
       0x00020000);
   auto wload = [&](int ct, int s) {
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (ct * KS + s) * 1024, 0));
   };
-  bf16x8 bq[2][4];
+  bf16x8 bq[2][CT];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
+  for (int ct = 0; ct < CT; ++ct) {
     bq[0][ct] = wload(ct, kstep(0));
     bq[1][ct] = wload(ct, kstep(1));
   }
 
-  f32x4 acc[8][4];
+  f32x4 acc[MT][CT];
 #pragma unroll
-  for (int mi = 0; mi < 8; ++mi)
+  for (int mi = 0; mi < MT; ++mi)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
+    for (int ct = 0; ct < CT; ++ct) {
       acc[mi][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
-  // a tap's fragment addresses: per pixel tile, the byte offset of its staged row (of the zero block for a tap
-  // that leaves the image); the row's swizzle key is recomputed from the offset at each read (kept beside the
-  // offsets, the keys' registers made the loop spill)
-  auto tap_set = [&](int t, int (&rb)[8]) {
+  // B fragment of pixel tile mi, channel step c (32 channels: chunk 4c + q of the row) of tap t, its address
+  // computed at the read (the tap's shift is wave-uniform; per-tap offset arrays cost 2 MT registers). A lane
+  // whose tap leaves the image reads row (r & 15) of a 16-row zero block at ZOFF (16-row aligned): the bank slot
+  // its own row would take. One shared zero row put that lane on a slot one of the 15 others held in ~7/8 of
+  // such fragments (SQ_LDS_BANK_CONFLICT 0.31 of LDS-active cycles in config 3, profiles/r04/r4f)
+  auto frag = [&](int t, int c, int mi) {
     const int dy = t / 3 - 1, dx = t % 3 - 1;
     const uint32_t need = 16u | (dy < 0 ? 1u : 0u) | (dy > 0 ? 2u : 0u) | (dx < 0 ? 4u : 0u) | (dx > 0 ? 8u : 0u);
-    const int shift = dy * a.W + dx;
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) {
-      const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
-      const int r = prow0 + 16 * mi + shift;
-      rb[mi] = ok ? r * RB : a.ZOFF + (r & 15) * RB;  // the zero block's row with this row's key
-    }
+    const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
+    const int r = prow0 + 16 * mi + dy * a.W + dx;
+    const int rb = ok ? r * RB : a.ZOFF + (r & 15) * RB;  // the zero block's row with this row's key
+    const int key = hkey(r & 15);
+    return *reinterpret_cast<const bf16x8*>(lds + rb + (((4 * c + q) ^ key) << 4));
   };
-  // B fragment of pixel tile mi, channel step c (32 channels: chunk 4c + q of the row). A lane whose tap leaves
-  // the image reads row (r & 15) of a 16-row zero block at ZOFF (16-row aligned): the bank slot its own row
-  // would take. One shared zero row put that lane on a slot one of the 15 others held in ~7/8 of such
-  // fragments (SQ_LDS_BANK_CONFLICT 0.31 of LDS-active cycles in config 3, profiles/r04/r4f)
-  auto frag = [&](const int (&rb)[8], int c, int mi) {
-    const int key = hkey(((unsigned)rb[mi] / RB) & 15);
-    return *reinterpret_cast<const bf16x8*>(lds + rb[mi] + (((4 * c + q) ^ key) << 4));
-  };
-  constexpr int NF = 8 * NCS;  // fragments per tap, in (channel step, pixel tile) order; a multiple of 4
+  constexpr int NF = MT * NCS;  // fragments per tap, in (channel step, pixel tile) order
 
   int j = 0;  // k step
 #pragma unroll
@@ -196,55 +194,50 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int rbc[8], rbn[8];  // this tap's row offsets, the next tap's
-    tap_set(0, rbc);
-    bf16x8 fr[4];  // rolling fragment buffer, two reads ahead
-    fr[0] = frag(rbc, 0, 0);
-    fr[1] = frag(rbc, 0, 1);
+    bf16x8 fr[2 * PF];  // rolling fragment buffer, PF reads ahead
+#pragma unroll
+    for (int i = 0; i < PF; ++i) fr[i] = frag(0, 0, i);
     // the taps unrolled: loop-carried accumulators in a rolled loop were renamed and copied between the
     // register files on every iteration
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      tap_set(t < 8 ? t + 1 : t, rbn);
 #pragma unroll
       for (int c = 0; c < NCS; ++c) {
         const int sl = c & 1;  // = j & 1: the steps per tap (NCS) are even
         const int sn = kstep(j + 2);
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
-          const int idx = c * 8 + mi, nx = idx + 2;
+        for (int mi = 0; mi < MT; ++mi) {
+          const int idx = c * MT + mi, nx = idx + PF;
           if (nx < NF)
-            fr[nx & 3] = frag(rbc, nx >> 3, nx & 7);
+            fr[nx % (2 * PF)] = frag(t, nx / MT, nx % MT);
           else if (t < 8)  // the next tap's first fragments (not across a restaging)
-            fr[nx & 3] = frag(rbn, (nx - NF) >> 3, (nx - NF) & 7);
-          const bf16x8 f = fr[idx & 3];
+            fr[nx % (2 * PF)] = frag(t + 1, (nx - NF) / MT, (nx - NF) % MT);
+          const bf16x8 f = fr[idx % (2 * PF)];
 #pragma unroll
-          for (int ct = 0; ct < 4; ++ct) acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][ct], f, acc[mi][ct], 0, 0, 0);
+          for (int ct = 0; ct < CT; ++ct) acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][ct], f, acc[mi][ct], 0, 0, 0);
         }
         // this step's ring slots are free once its MFMAs have issued: the step after next
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) bq[sl][ct] = wload(ct, sn);
-        // per pixel tile: its fragment read two tiles ahead, then its 4 MFMAs; the ring loads after the step's
+        for (int ct = 0; ct < CT; ++ct) bq[sl][ct] = wload(ct, sn);
+        // per pixel tile: its fragment read PF tiles ahead, then its CT MFMAs; the ring loads after the step's
         // MFMAs (their slots are free then; issued earlier they would need fresh registers)
 #pragma unroll
-        for (int mi = 0; mi < 8; ++mi) {
+        for (int mi = 0; mi < MT; ++mi) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, CT, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, CT, 0);
         __builtin_amdgcn_sched_barrier(0);
         ++j;
       }
-#pragma unroll
-      for (int mi = 0; mi < 8; ++mi) rbc[mi] = rbn[mi];
     }
   }
 
-  // epilogue: acc[mi][ct] = D[channel n0 + 128 wn + 16 ct + 4q + i][pixel m0 + 128 wm + 16 mi + n]
+  // epilogue: acc[mi][ct] = D[channel n0 + 16 CT wn + 16 ct + 4q + i][pixel m0 + TM / WM wm + 16 mi + n]
   if (a.res)
-    halo_epilogue<true>(a, acc, m0, n0 + wn * 64, wm, q, n);
+    halo_epilogue<true>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
   else
-    halo_epilogue<false>(a, acc, m0, n0 + wn * 64, wm, q, n);
+    halo_epilogue<false>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
 }
 
 // staging geometry for a (W, Cin) pair: the whole Cin staged at once (one block; a rolled loop over channel

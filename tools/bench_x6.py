@@ -2,9 +2,8 @@
 acting loop's shapes: x6 at the 4x5 latent (B = 4096, the parity path's towers) and 8x10 (the representation
 tail), halo at config 3's 21x21 latent (B = 4096). HIP events around 20 launches after 3 warm-up launches,
 alternated twice. Prints one JSON line per (kernel, shape, variant). The variant setters
-(mzba_conv_x6_set_variant, mzba_conv_halo_set_variant) exist only in the A/B builds of round 4 (the rejected
-channel-slice x6 split; profiles/r04/halo_pipe/conv_halo_pipelined.patch); without them the default runs once per
-variant slot (variant None).
+(mzba_conv_x6_set_variant: the rejected channel-slice x6 split of round 4; mzba_conv_halo_set_wm: the halo conv's
+wave split) may be missing from a build; the default then runs once per variant slot (variant None).
   python tools/bench_x6.py"""
 import json
 import os
@@ -63,13 +62,13 @@ def main():
     out = torch.empty(B, H, W, C, dtype=torch.bfloat16, device=dev)
     fl = 2.0 * B * H * W * C * 9 * C
     for rep in range(2):
-        for v in (0, 1):
-            v = set_variant("mzba_conv_halo_set_variant", v)
+        for v in (1, 2, 3):
+            v = set_variant("mzba_conv_halo_set_wm", v)
             ms = timeit(lambda: L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(x), L.ptr(out), B, H, W, C, C, 1,
                                        L.stream()), n=10)
             print(json.dumps({"lib": tag, "kernel": "conv_halo", "shape": [B, H, W, C], "variant": v, "rep": rep, "ms": ms,
                               "tflops": fl / ms / 1e9, "frac": fl / ms / 1e9 / 2500}), flush=True)
-    set_variant("mzba_conv_halo_set_variant", 0)
+    set_variant("mzba_conv_halo_set_wm", 1)
 
 
 if __name__ == "__main__":
