@@ -155,8 +155,15 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
 
   int rbc[MT], rbn[MT];
   tap_set(0, rbc);
-  uint4 f0[2], f1[2];  // rolling raw buffer, one fragment ahead
+  // software pipeline over the flat fragment sequence (tap, channel step, pixel tile): fragment i's 24 MFMAs
+  // run while fragment i + 1 is split into its bf16 parts (VALU, interleaved below) and fragment i + 2 is read
+  // from LDS. Split in place just before its own MFMAs, the ~50 VALU of a split stalled the wave between
+  // fragments.
+  uint4 f0[2], f1[2];  // raw f32 fragments, slot = index parity (NF is even)
+  bf16x8 sp[2][3];     // split parts (hi, mid, lo), slot = index parity
   frag(rbc, 0, 0, f0[0], f1[0]);
+  frag(rbc, NF > 1 ? 1 / MT : 0, 1 % MT, f0[1], f1[1]);
+  split8(f0[0], f1[0], sp[0][0], sp[0][1], sp[0][2]);
   int j = 0;
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
@@ -167,26 +174,29 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
       const int sn = j + 2;
 #pragma unroll
       for (int mi = 0; mi < MT; ++mi) {
-        const int idx = c * MT + mi, nx = idx + 1;
-        const uint4 u0 = f0[idx & 1], u1 = f1[idx & 1];
-        if (nx < NF)
-          frag(rbc, nx / MT, nx % MT, f0[nx & 1], f1[nx & 1]);
+        const int idx = c * MT + mi, n1 = idx + 1, n2 = idx + 2;
+        if (n2 < NF)
+          frag(rbc, n2 / MT, n2 % MT, f0[n2 & 1], f1[n2 & 1]);
         else if (t < 8)
-          frag(rbn, (nx - NF) / MT, (nx - NF) % MT, f0[nx & 1], f1[nx & 1]);
-        bf16x8 xh, xm, xl;
-        split8(u0, u1, xh, xm, xl);
+          frag(rbn, (n2 - NF) / MT, (n2 - NF) % MT, f0[n2 & 1], f1[n2 & 1]);
+        if (n1 < NF || t < 8) split8(f0[n1 & 1], f1[n1 & 1], sp[n1 & 1][0], sp[n1 & 1][1], sp[n1 & 1][2]);
+        const bf16x8 &xh = sp[idx & 1][0], &xm = sp[idx & 1][1], &xl = sp[idx & 1][2];
+        // per accumulator the small terms first, then the large ones (each an f32-accumulating bf16 MFMA);
+        // issued term-major across the column tiles, so consecutive MFMAs are independent
+        const bf16x8* xs[6] = {&xh, &xm, &xl, &xh, &xm, &xh};
+        constexpr int wp[6] = {2, 1, 0, 1, 0, 0};
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          f32x4 v = acc[mi][ct];
-          // the small terms first, then the large ones (each an f32-accumulating bf16 MFMA)
-          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][2][ct], xh, v, 0, 0, 0);
-          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][1][ct], xm, v, 0, 0, 0);
-          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][0][ct], xl, v, 0, 0, 0);
-          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][1][ct], xh, v, 0, 0, 0);
-          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][0][ct], xm, v, 0, 0, 0);
-          v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][0][ct], xh, v, 0, 0, 0);
-          acc[mi][ct] = v;
+        for (int k = 0; k < 6; ++k)
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct)
+            acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][wp[k]][ct], *xs[k], acc[mi][ct], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // the LDS reads of fragment i + 2 first
+#pragma unroll
+        for (int k = 0; k < 24; ++k) {  // then each MFMA with two VALU of the next split in its shadow
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int pt = 0; pt < 3; ++pt)
