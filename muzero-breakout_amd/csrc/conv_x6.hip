@@ -12,7 +12,7 @@
 //
 // Structure: conv_halo_kernel's (csrc/conv_halo.hip) — a workgroup stages TM consecutive output pixels plus
 // W + 1 halo rows on each side once (here the f32 activations: Cin x 4 B per row, 16-B chunks XOR-swizzled
-// by row), runs all 9 taps from LDS (taps leaving the image read a zero row), 8 waves = 2 pixel halves x 4
+// by row), runs all 9 taps from LDS (taps leaving the image read a 16-row zero block), 8 waves = 2 pixel halves x 4
 // output-channel quarters; weights = MFMA A operand, their three bf16 parts pre-split on the host
 // (agent.py "wx": three pack_lat16 packs back to back) through a two-k-step register ring; activations = B
 // operand, read as f32 from LDS and split in registers per fragment (each split feeds 4 column tiles x 6
@@ -37,7 +37,7 @@ struct X6Args {
   const float* res;    // optional [M][Cout] f32
   float* out;          // [M][Cout] f32
   int M, H, W, Cin, Cout, relu;
-  int HALO, NI, ZOFF;  // halo rows each side, LDS-DMA 1-KiB blocks of the staging, byte offset of the zero row
+  int HALO, NI, ZOFF;  // halo rows each side, LDS-DMA 1-KiB blocks of the staging, byte offset of the zero block
   long long part;      // elements per weight part
 };
 
@@ -80,7 +80,8 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
   const int m0 = blockIdx.x * TM, n0 = blockIdx.y * x6::TN;
   const int HW = a.H * a.W;
 
-  if (tid < RB / 16) *reinterpret_cast<uint4*>(lds + a.ZOFF + tid * 16) = make_uint4(0, 0, 0, 0);
+  // the zero block: 16 rows at ZOFF (16-row aligned), never overwritten by staging
+  for (int i = tid; i < RB; i += x6::NT) *reinterpret_cast<uint4*>(lds + a.ZOFF + i * 16) = make_uint4(0, 0, 0, 0);
 
   // the lane's pixel in tile mi: staged row prow0 + 16 mi at tap (0, 0); byte mi of okw: its taps in the image
   const int prow0 = wm * (TM / 2) + n + a.HALO;
@@ -131,8 +132,10 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  // a tap's row offsets per pixel tile (the zero row for a tap leaving the image; any key reads it as 0); the
-  // row's key is recomputed from the offset at each read (kept beside the offsets, the keys spilled)
+  // a tap's row offsets per pixel tile; a tap that leaves the image reads row (r & 15) of the zero block, the
+  // bank slot its own row would take (one shared zero row cost 0.44 of the LDS-active cycles in bank conflicts
+  // at the 4x5 latent, where 14 of 20 pixels are on the border: profiles/r04/r4f/psq2_x6.json). The row's key is
+  // recomputed from the offset at each read (kept beside the offsets, the keys spilled)
   auto tap_set = [&](int t, int (&rb)[MT]) {
     const int dy = t / 3 - 1, dx = t % 3 - 1;
     const uint32_t need = 16u | (dy < 0 ? 1u : 0u) | (dy > 0 ? 2u : 0u) | (dx < 0 ? 4u : 0u) | (dx > 0 ? 8u : 0u);
@@ -140,7 +143,8 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
 #pragma unroll
     for (int mi = 0; mi < MT; ++mi) {
       const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
-      rb[mi] = ok ? (prow0 + 16 * mi + shift) * RB : a.ZOFF;
+      const int r = prow0 + 16 * mi + shift;
+      rb[mi] = ok ? r * RB : a.ZOFF + (r & 15) * RB;
     }
   };
   // the 8 f32 channels 32 c + 8 q .. of the lane's row: chunks 8c + 2q, 8c + 2q + 1 (swizzled by xkey(row))
@@ -241,8 +245,8 @@ int x6_geometry(int W, int Cin, X6Args& g) {
   if (Cin != 128 && Cin != 256) return 0;
   for (int tm : {96, 64}) {  // 128: the ring, 64 accumulators and the split fragments spill
     const int halo = W + 1, hr = tm + 2 * halo, rb = Cin * 4;
-    const int ni = (hr * rb + 1023) / 1024, zoff = ni * 1024;
-    if (zoff + rb <= x6::LDS_MAX) {
+    const int ni = (hr * rb + 1023) / 1024, zoff = (ni * 1024 + 16 * rb - 1) / (16 * rb) * (16 * rb);
+    if (zoff + 16 * rb <= x6::LDS_MAX) {
       g.HALO = halo, g.NI = ni, g.ZOFF = zoff;
       return tm;
     }
@@ -271,7 +275,7 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
   X6Args a{(const float*)in, (const bf16_t*)wx, bias, (const float*)res, (float*)out, (int)M, H, W, Cin, Cout, relu};
   const int tm = x6_geometry(W, Cin, a);
   a.part = (long long)Cout * 9 * Cin;
-  const int lds = a.ZOFF + Cin * 4;
+  const int lds = a.ZOFF + 16 * Cin * 4;
   const dim3 grid((unsigned)((M + tm - 1) / tm), (unsigned)(Cout / x6::TN));
   auto launch = [&](auto kern) {
     static bool attr = false;
