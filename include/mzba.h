@@ -115,6 +115,10 @@ int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks);
 int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks);
 int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
                  int Cin, int Cout, int relu, hipStream_t stream);
+/* 1 (default): the pre-split form where its staged rows fit (the f32 activations split once into bf16 hi / mid /
+ * lo planes while staging, 1.5x the f32 row; 8 waves x 32 channels); 0: the per-read-split kernel only (A/B; it
+ * remains the form for halos too large for the planes). Same sums in the same order: bit-identical outputs. */
+int mzba_conv_x6_set_variant(int v);
 int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
                    int Cin, int Cout, int relu, hipStream_t stream);
 

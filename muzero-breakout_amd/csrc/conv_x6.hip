@@ -240,6 +240,208 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
   }
 }
 
+// Pre-split form (default where it fits): the staging goes through registers and splits every f32 value ONCE
+// into its hi / mid / lo bf16 parts, stored as three planes per staged row (row = hi[Cin] | mid[Cin] | lo[Cin],
+// 16-B chunks XOR-swizzled by hkey(row) within each plane, conv_halo.hip's key: bf16 chunks 4c + q); the k loop
+// then reads MFMA-ready operands (three ds_read_b128 per fragment, no VALU). conv_x6_kernel splits per fragment
+// read, i.e. each staged value 9 taps x 4 channel-quarter waves = 36 times, and that split was 24 % of its time
+// by ablation (profiles/r04/x6_abl/). The 8 waves own 32 output channels each over all TM pixels (no weight
+// fragment streamed twice per workgroup); a row is 1.5x the f32 row, so TM is 80 at the 4x5 latent (1 024
+// tiles at B = 4 096: four rounds of 256 CUs exactly). Same products, same order per accumulator: bit-identical
+// to conv_x6_kernel.
+MZ_DEV int pkey(int r) { return ((r << 1) & 6) | (((r >> 2) & 1) * 9); }  // = conv_halo.hip hkey
+
+template <int CIN, int TM>
+__global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
+  constexpr int PB = CIN * 2;        // bytes per plane row (bf16)
+  constexpr int RB = 3 * PB;         // bytes per staged row: hi | mid | lo
+  constexpr int NC8 = CIN / 8;       // 8-channel chunks per row
+  constexpr int NCS = CIN / 32;      // 32-channel k steps per tap
+  constexpr int CT = 2;              // column tiles per wave (32 channels)
+  constexpr int MT = TM / 16;        // pixel tiles per wave: all of the workgroup's
+  static_assert(NCS % 2 == 0 && TM % 16 == 0 && MT <= 8, "ring slot = step parity; whole pixel tiles");
+  constexpr int nsteps = 9 * NCS;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, n = lane & 15;
+  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * x6::TN;
+  const int HW = a.H * a.W;
+  const int HR = TM + 2 * a.HALO;
+
+  for (int i = tid; i < RB / 16; i += x6::NT) *reinterpret_cast<uint4*>(lds + a.ZOFF + i * 16) = make_uint4(0, 0, 0, 0);
+
+  const int prow0 = n + a.HALO;
+  uint32_t okw[(MT + 3) / 4] = {};
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = m0 + mi * 16 + n;
+    if (m < a.M) {
+      const int p = m % HW, y = p / a.W, x = p - y * a.W;
+      const uint32_t b = 16u | (y > 0 ? 1u : 0u) | (y < a.H - 1 ? 2u : 0u) | (x > 0 ? 4u : 0u) | (x < a.W - 1 ? 8u : 0u);
+      okw[mi >> 2] |= b << (8 * (mi & 3));
+    }
+  }
+
+  const int KS = 9 * CIN / 32;
+  const uint4* wbase = reinterpret_cast<const uint4*>(a.wx) + (size_t)(n0 / 16 + wave * CT) * KS * 64;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wbase), 0, 0x7fffffff, 0x00020000);
+  const int pstride = (int)(a.part * 2);
+  auto wload = [&](int ct, int part, int s) {
+    s = s < nsteps ? s : nsteps - 1;
+    return __builtin_bit_cast(bf16x8,
+                              __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + (ct * KS + s) * 1024, 0));
+  };
+  bf16x8 bq[2][3][CT];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) bq[cc][pt][ct] = wload(ct, pt, cc);
+
+  f32x4 acc[MT][CT];
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[mi][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // staging: item g = (row, 8-channel chunk); 8 f32 loaded, split, written as one chunk per plane. Loads of a
+  // batch of 8 items are all issued before its first split.
+  const int items = HR * NC8;
+  for (int g0 = 0; g0 < items; g0 += 8 * x6::NT) {
+    uint4 v[8][2];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int g = min(g0 + u * x6::NT + tid, items - 1), r = g / NC8, s8 = g - r * NC8;
+      int m = m0 - a.HALO + r;
+      m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);
+      const float* src = a.in + (size_t)m * CIN + s8 * 8;
+      v[u][0] = *reinterpret_cast<const uint4*>(src);
+      v[u][1] = *reinterpret_cast<const uint4*>(src + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int g = g0 + u * x6::NT + tid;
+      if (g < items) {
+        const int r = g / NC8, s8 = g - r * NC8;
+        bf16x8 h, mm, l;
+        split8(v[u][0], v[u][1], h, mm, l);
+        uint8_t* row = lds + r * RB + ((s8 ^ pkey(r)) << 4);
+        *reinterpret_cast<bf16x8*>(row) = h;
+        *reinterpret_cast<bf16x8*>(row + PB) = mm;
+        *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+      }
+    }
+  }
+  __syncthreads();
+
+  // fragment of pixel tile mi, channel step c at tap t: chunk 4c + q of the three planes of its row (the zero row
+  // for a tap leaving the image; its bank slots collide with at most a few lanes', measured neutral for conv_x6)
+  auto frag = [&](int t, int c, int mi, bf16x8 (&f)[3]) {
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    const uint32_t need = 16u | (dy < 0 ? 1u : 0u) | (dy > 0 ? 2u : 0u) | (dx < 0 ? 4u : 0u) | (dx > 0 ? 8u : 0u);
+    const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
+    const int r = prow0 + 16 * mi + dy * a.W + dx;
+    const int base = ok ? r * RB + (((4 * c + q) ^ pkey(r)) << 4) : a.ZOFF;
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt) f[pt] = *reinterpret_cast<const bf16x8*>(lds + base + pt * PB);
+  };
+  constexpr int NF = MT * NCS;
+  bf16x8 fr[2][3];  // rolling: fragment i + 1 read during fragment i's MFMAs
+  frag(0, 0, 0, fr[0]);
+  int j = 0;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+#pragma unroll
+    for (int c = 0; c < NCS; ++c) {
+      const int sl = c & 1;
+      const int sn = j + 2;
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) {
+        const int idx = c * MT + mi, nx = idx + 1;
+        // the flat fragment index parity picks the buffer: NF may be odd, so count across taps
+        const int cur = (t * NF + idx) & 1, nxt = cur ^ 1;
+        if (nx < NF)
+          frag(t, nx / MT, nx % MT, fr[nxt]);
+        else if (t < 8)
+          frag(t + 1, 0, 0, fr[nxt]);
+        const bf16x8* xs[6] = {&fr[cur][0], &fr[cur][1], &fr[cur][2], &fr[cur][0], &fr[cur][1], &fr[cur][0]};
+        constexpr int wp[6] = {2, 1, 0, 1, 0, 0};  // per accumulator the small terms first, as conv_x6_kernel
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+            acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][wp[k]][ct], *xs[k], acc[mi][ct], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 6 * CT, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) bq[sl][pt][ct] = wload(ct, pt, sn);
+      __builtin_amdgcn_sched_barrier(0);
+      ++j;
+    }
+  }
+
+  // epilogue (f32): acc[mi][ct] = D[channel n0 + 32 wave + 16 ct + 4q + i][pixel m0 + 16 mi + n]
+  const int nb = n0 + wave * 16 * CT;
+  float4 bb[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
+  const float lo = a.relu ? 0.f : -__builtin_inff();
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = m0 + mi * 16 + n;
+    const int mc = m < a.M ? m : a.M - 1;
+    float4 rv[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+      rv[ct] = a.res ? *reinterpret_cast<const float4*>(a.res + (size_t)mc * a.Cout + nb + ct * 16 + 4 * q)
+                     : make_float4(-0.f, -0.f, -0.f, -0.f);
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      float4 o;
+      o.x = fmaxf((acc[mi][ct][0] + bb[ct].x) + rv[ct].x, lo);
+      o.y = fmaxf((acc[mi][ct][1] + bb[ct].y) + rv[ct].y, lo);
+      o.z = fmaxf((acc[mi][ct][2] + bb[ct].z) + rv[ct].z, lo);
+      o.w = fmaxf((acc[mi][ct][3] + bb[ct].w) + rv[ct].w, lo);
+      if (m < a.M) *reinterpret_cast<float4*>(a.out + (size_t)m * a.Cout + nb + ct * 16 + 4 * q) = o;
+    }
+  }
+}
+
+static int g_x6_presplit = 1;  // A/B: 1 the pre-split form where it fits, 0 conv_x6_kernel only
+
+int x6p_ncu() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  return ncu;
+}
+
+// pre-split geometry for (W, Cin, M pixels): among the tiles whose 1.5x rows fit the LDS, the one that loads the
+// busiest CU least (ceil(tiles / CUs) x TM; the larger tile on a tie); 0 if none fits
+int x6p_geometry(int W, int Cin, long long M, X6Args& g) {
+  if (Cin != 128 && Cin != 256) return 0;
+  int best = 0;
+  long long best_load = 0;
+  for (int tm : {128, 112, 96, 80, 64, 48}) {
+    const int halo = W + 1, hr = tm + 2 * halo, rb = 3 * Cin * 2;
+    if ((long long)(hr + 1) * rb > x6::LDS_MAX) continue;
+    const long long load = ((M + tm - 1) / tm + x6p_ncu() - 1) / x6p_ncu() * tm;
+    if (!best || load < best_load) best = tm, best_load = load;
+  }
+  if (!best) return 0;
+  g.HALO = W + 1, g.NI = 0, g.ZOFF = (best + 2 * (W + 1)) * 3 * Cin * 2;
+  return best;
+}
+
 // the pixel tile for (W, Cin): 96, or 64 when that halo does not fit the LDS; 0 if neither fits
 int x6_geometry(int W, int Cin, X6Args& g) {
   if (Cin != 128 && Cin != 256) return 0;
@@ -273,8 +475,43 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
   const long long M = (long long)B * H * W;
   MZ_CHECK_ARG(M + 256 < (1LL << 31), -3);  // pixel indices in int (global offsets are size_t)
   X6Args a{(const float*)in, (const bf16_t*)wx, bias, (const float*)res, (float*)out, (int)M, H, W, Cin, Cout, relu};
-  const int tm = x6_geometry(W, Cin, a);
   a.part = (long long)Cout * 9 * Cin;
+  X6Args ap = a;
+  const int tmp = g_x6_presplit ? x6p_geometry(W, Cin, M, ap) : 0;
+  if (tmp == 128 || tmp == 112 || tmp == 96 || tmp == 80 || tmp == 64 || tmp == 48) {
+    const int ldsp = ap.ZOFF + 3 * Cin * 2;
+    const dim3 gridp((unsigned)((M + tmp - 1) / tmp), (unsigned)(Cout / x6::TN));
+    auto launchp = [&](auto kern) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, x6::LDS_MAX);
+        attr = true;
+      }
+      hipLaunchKernelGGL(kern, gridp, dim3(x6::NT), ldsp, stream, ap);
+    };
+    if (Cin == 256) {
+      switch (tmp) {
+        case 128: launchp(conv_x6p_kernel<256, 128>); break;
+        case 112: launchp(conv_x6p_kernel<256, 112>); break;
+        case 96: launchp(conv_x6p_kernel<256, 96>); break;
+        case 80: launchp(conv_x6p_kernel<256, 80>); break;
+        case 64: launchp(conv_x6p_kernel<256, 64>); break;
+        default: launchp(conv_x6p_kernel<256, 48>); break;
+      }
+    } else {
+      switch (tmp) {
+        case 128: launchp(conv_x6p_kernel<128, 128>); break;
+        case 112: launchp(conv_x6p_kernel<128, 112>); break;
+        case 96: launchp(conv_x6p_kernel<128, 96>); break;
+        case 80: launchp(conv_x6p_kernel<128, 80>); break;
+        case 64: launchp(conv_x6p_kernel<128, 64>); break;
+        default: launchp(conv_x6p_kernel<128, 48>); break;
+      }
+    }
+    MZ_LAUNCH_CHECK();
+    return 0;
+  }
+  const int tm = x6_geometry(W, Cin, a);
   const int lds = a.ZOFF + 16 * Cin * 4;
   const dim3 grid((unsigned)((M + tm - 1) / tm), (unsigned)(Cout / x6::TN));
   auto launch = [&](auto kern) {
@@ -290,6 +527,12 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
   else
     tm == 96 ? launch(conv_x6_kernel<128, 96>) : launch(conv_x6_kernel<128, 64>);
   MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+int mzba_conv_x6_set_variant(int v) {
+  if (v != 0 && v != 1) return -1;
+  g_x6_presplit = v;
   return 0;
 }
 

@@ -37,6 +37,7 @@ SIGNATURES = {
     "mzba_conv_halo": [P, P, P, P, P, I, I, I, I, I, I, P],
     "mzba_conv_x6_supported": [I, I, I, I, I],
     "mzba_conv_x6": [P, P, P, P, P, I, I, I, I, I, I, P],
+    "mzba_conv_x6_set_variant": [I],
     "mzba_conv_lat_supported": [I, I, I, I, I],
     "mzba_conv_lat_set_variant": [I],
     "mzba_conv_lat_get_variant": [],

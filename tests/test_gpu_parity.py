@@ -625,7 +625,8 @@ def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, relu, with_res):
     """mzba_conv_x6 (the f32 parity path's latent convs as six split-bf16 MFMA products each) against an f64
     conv of the same f32 operands: at least as close as the f32-input MFMA conv of the f32 path (mzba_conv2d
     dtype 0) — within 2x its error + 1e-7 of the magnitude — and within 2e-6 of the magnitude absolutely
-    (ragged tiles, tiles crossing envs, every tap that leaves the image)."""
+    (ragged tiles, tiles crossing envs, every tap that leaves the image); the pre-split form (default) and the
+    per-read-split kernel bit-identical."""
     from mzba import _lib as L
     from mzba.agent import split_pack_x6
     Cout = 256
@@ -645,12 +646,20 @@ def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, relu, with_res):
     wx = split_pack_x6(w.cpu().numpy().reshape(Cout, -1), Cout, 3, Cin).cuda()
     out = torch.full((B, H, W, Cout), float("nan"), device=dev)
     L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu, L.stream())
+    # the per-read-split kernel (the fallback where the pre-split form's rows do not fit): the same sums in the same order
+    out2 = torch.full((B, H, W, Cout), float("nan"), device=dev)
+    try:
+        assert L.lib().mzba_conv_x6_set_variant(0) == 0
+        L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), L.ptr(res), L.ptr(out2), B, H, W, Cin, Cout, relu, L.stream())
+    finally:
+        L.lib().mzba_conv_x6_set_variant(1)
     f32 = torch.empty(B, H, W, Cout, device=dev)
     wd = w.reshape(Cout, -1).contiguous()
     L.call("mzba_conv2d", 0, L.ptr(x), H * W * Cin, None, 0, L.ptr(wd), L.ptr(b), None, None, 0, L.ptr(res), L.ptr(f32),
            B, H, W, Cin, Cout, 3, relu, L.stream())
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
+    assert torch.equal(out, out2)
     scale = ref.abs().max().item()
     e6, e32 = (out.double() - ref).abs().max().item(), (f32.double() - ref).abs().max().item()
     print(f"conv_x6 {B}x{H}x{W} {Cin}: max err vs f64 {e6 / scale:.2e} of the magnitude, f32 MFMA conv {e32 / scale:.2e}")

@@ -2,8 +2,9 @@
 acting loop's shapes: x6 at the 4x5 latent (B = 4096, the parity path's towers) and 8x10 (the representation
 tail), halo at config 3's 21x21 latent (B = 4096). HIP events around 20 launches after 3 warm-up launches,
 alternated twice. Prints one JSON line per (kernel, shape, variant). The variant setters
-(mzba_conv_x6_set_variant: the rejected channel-slice x6 split of round 4; mzba_conv_halo_set_wm: the halo conv's
-wave split) may be missing from a build; the default then runs once per variant slot (variant None).
+(mzba_conv_x6_set_variant: 1 the pre-split x6 form, 0 the per-read-split kernel; mzba_conv_halo_set_wm: the halo
+conv's wave split, round-4 A/B builds only) may be missing from a build; the default then runs once per variant
+slot (variant None).
   python tools/bench_x6.py"""
 import json
 import os
@@ -47,13 +48,13 @@ def main():
         out = torch.empty(B, H, W, C, device=dev)
         fl = 2.0 * B * H * W * C * 9 * C * 6
         for rep in range(2):
-            for v in (0, 1):
+            for v in (1, 0):
                 v = set_variant("mzba_conv_x6_set_variant", v)
                 ms = timeit(lambda: L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), None, L.ptr(out), B, H, W, C, C, 1,
                                            L.stream()))
                 print(json.dumps({"lib": tag, "kernel": "conv_x6", "shape": [B, H, W, C], "variant": v, "rep": rep, "ms": ms,
                                   "bf16_tflops": fl / ms / 1e9, "frac_bf16_peak": fl / ms / 1e9 / 2500}), flush=True)
-        set_variant("mzba_conv_x6_set_variant", 0)
+        set_variant("mzba_conv_x6_set_variant", 1)
         del x, wx, out
     B, H, W = 4096, 21, 21
     x = torch.randn(B, H, W, C, generator=g, device=dev).to(torch.bfloat16)
