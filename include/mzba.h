@@ -103,9 +103,20 @@ int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_
  * of B envs, zero padding. A workgroup stages 256 consecutive output pixels plus W + 1 halo rows on each side
  * into LDS once per channel block and runs all 9 taps from it. wh = pack_lat16 of the BN-folded
  * [Cout][3][3][Cin] weights: wh[Cout/16][9*Cin/32][64][8], wh[ct][s][l][j] = W[16 ct + l % 16][32 s + 8 (l / 16) + j]
- * with the K index tap * Cin + channel. Supported: Cin % 128 == 0, Cout % 256 == 0, the staged halo within the
- * LDS (mzba_conv_halo_supported). Replaces networks.py:19-35 ResidualBlock convs (the second with res). */
+ * with the K index tap * Cin + channel. Supported: Cin 128 / 256, Cout % 256 == 0 or Cout 128 at Cin 256 (the
+ * policy head's conv, networks.py:200-206), the staged halo within the LDS (mzba_conv_halo_supported). Replaces
+ * networks.py:19-35 ResidualBlock convs (the second with res). */
 int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks);
+/* mzba_conv_halo with a gathered input and the action planes folded into a bias table (the dynamics' first conv,
+ * networks.py:117-122, 160; the same contract as mzba_conv2d's slot / act_bias arguments): env b's image at
+ * in + b env_stride + slot[b] slot_stride elements (slot optional), out = act(conv3x3 + act_bias[p][act[b]][n] +
+ * bias[n] (+ res)), ((acc + act_bias) + bias) in f32 as conv_igemm; act_bias [H W][A][Cout] f32 excludes res.
+ * gather = 1 in the support check: a strided / gathered input or an action-bias table (Cin 256, Cout % 256 == 0,
+ * 256 + 2 (W + 1) <= H W: a workgroup's staged rows within two envs). */
+int mzba_conv_halo_ex_supported(int H, int W, int Cin, int Cout, int ks, int gather);
+int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wh,
+                      const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,
+                      int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream);
 /* f32-faithful 3x3 conv on bf16 MFMAs (the f32 parity path's latent towers, networks.py:19-35): f32 NHWC in /
  * out, out = act(conv3x3(in) + bias (+ res)); every f32 operand split into three bf16 parts and each product
  * taken as the six terms down to 2^-18 (csrc/conv_x6.hip), as close to exact as an f32 conv. wx = the three

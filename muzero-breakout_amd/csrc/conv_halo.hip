@@ -24,6 +24,11 @@
 //     B operand from LDS (v_mfma_f32_16x16x32_bf16): per 32-channel k step 8 B reads + 4 weight loads feed 32
 //     MFMAs, pixel-tile major (each B fragment feeds its 4 MFMAs back to back).
 //   * epilogue: + bias (+ residual), ReLU, bf16; a lane holds 4 consecutive channels of one pixel.
+//   * Cout 128 (the prediction's 3x3 policy-head conv, networks.py:200-206): TN = 128, 4 pixel quarters x 2
+//     channel halves of 64. GA instances (the dynamics' first conv, networks.py:117-122 / agent.py dyn0): the
+//     input gathered per env from the latent pool (in + b env_stride + slot[b] slot_stride) and the action
+//     planes' contribution added from their folded [HW][A][Cout] table, as conv_igemm ((acc + act_bias) + bias);
+//     a staged range then spans at most two envs (HR <= H W), whose offsets are read once per workgroup.
 #include "common.h"
 
 namespace {
@@ -47,6 +52,12 @@ struct HaloArgs {
   int M, H, W, Cin, Cout, relu;
   int HALO, HR, CB;    // halo rows each side, staged rows, channels per staged block
   int NI, ZOFF;        // LDS-DMA 1-KiB blocks per staging, byte offset of the zero block (pipelined: row)
+  // GA instances only
+  const int32_t* slot;                // optional [B]: env b's input at in + b env_stride + slot[b] slot_stride
+  long long env_stride, slot_stride;  // elements
+  const float* act_bias;              // optional [H W][A][Cout] f32
+  const int32_t* act;                 // [B] (with act_bias)
+  int A;
 };
 
 // swizzle key of staged row r: ds_read_b128 serves a wave in lane groups {0-3, 12-15, 20-27}, ... (rows
@@ -58,8 +69,17 @@ MZ_DEV int hkey(int r) { return ((r << 1) & 6) | (((r >> 2) & 1) * 9); }
 // + bias (+ residual), ReLU, bf16: (acc + bias) + res in f32, as conv_big_bf16_kernel; a lane stores 4
 // consecutive channels (8 B) of one pixel per (pixel tile, column tile); every residual load of a pixel tile
 // is issued before its first use
-template <bool RES, int MT, int CT>
+template <bool RES, bool AB, int MT, int CT>
 MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb, int nb, int q, int n) {
+  const int HW = a.H * a.W;
+  // AB: the tile's pixels span at most two envs (TM <= H W): their action indices read once
+  int tb0 = 0, tb1 = 0, av0 = 0, av1 = 0;
+  if (AB) {
+    tb0 = __builtin_amdgcn_readfirstlane(mb / HW);
+    tb1 = (tb0 + 1) * HW;
+    av0 = a.act[tb0];
+    av1 = a.act[min(tb0 + 1, a.M / HW - 1)];
+  }
   float4 bb[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
@@ -69,6 +89,14 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
     const int m = mb + mi * 16 + n;
     const int mc = m < a.M ? m : a.M - 1;
     uint2 rv[CT];
+    float4 ab[CT];
+    if (AB) {
+      const bool hi = mc >= tb1;
+      const int p = mc - (hi ? tb1 : tb1 - HW), av = hi ? av1 : av0;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        ab[ct] = *reinterpret_cast<const float4*>(a.act_bias + ((size_t)p * a.A + av) * a.Cout + nb + ct * 16 + 4 * q);
+    }
     if (RES) {
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) rv[ct] = *reinterpret_cast<const uint2*>(a.res + (size_t)mc * a.Cout + nb + ct * 16 + 4 * q);
@@ -78,7 +106,7 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
     for (int ct = 0; ct < CT; ++ct) {
       float v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = acc[mi][ct][i] + (&bb[ct].x)[i];
+      for (int i = 0; i < 4; ++i) v[i] = AB ? (acc[mi][ct][i] + (&ab[ct].x)[i]) + (&bb[ct].x)[i] : acc[mi][ct][i] + (&bb[ct].x)[i];
       if (RES) {
         v[0] = v[0] + bf16_to_f32((bf16_t)(rv[ct].x & 0xffffu));
         v[1] = v[1] + bf16_to_f32((bf16_t)(rv[ct].x >> 16));
@@ -100,12 +128,12 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
 // 21x21): WM = 1 (8 slices of 32 channels over all 256 pixels: no weight fragment loaded twice per workgroup,
 // half the per-CU L2 weight stream, twice the B reads) 1.76-1.85 ms vs 1.75-1.83; B fragments read 16 MFMAs
 // ahead instead of 8: 1.82-1.83 ms. Neither the weight stream nor the LDS read latency bounds this kernel.
-template <int CB, int NBLK, int WM = 2, int PFM = 1>
+template <int CB, int NBLK, int WM = 2, int PFM = 1, int TN = hl::TN, bool GA = false>
 __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   constexpr int RB = CB * 2;        // bytes per staged row
   constexpr int NC = CB / 8;        // 16-B chunks per row
   constexpr int NCS = CB / 32;      // 32-channel k steps per tap and block
-  constexpr int WN = 8 / WM, CT = 16 / WN, MT = 16 / WM;  // channel slices, column tiles / pixel tiles per wave
+  constexpr int WN = 8 / WM, CT = TN / 16 / WN, MT = 16 / WM;  // channel slices, column tiles / pixel tiles per wave
   constexpr int PF = PFM * 8 / CT;  // fragment reads ahead: 8 PFM MFMAs
   static_assert(NCS % 2 == 0, "ring slot = channel step parity");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -113,8 +141,18 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;  // pixel part (TM / WM), channel slice (16 CT)
   const int q = lane >> 4, n = lane & 15;
-  const int m0 = blockIdx.x * hl::TM, n0 = blockIdx.y * hl::TN;
+  const int m0 = blockIdx.x * hl::TM, n0 = blockIdx.y * TN;
   const int HW = a.H * a.W;
+  // GA: element offset of staged row m = eoff[m >= sb1] + m Cin (the range's two envs, b env_stride + slot[b]
+  // slot_stride - b H W Cin)
+  long long eoff0 = 0, eoff1 = 0;
+  int sb1 = 0;
+  if (GA) {
+    const int sb0 = __builtin_amdgcn_readfirstlane(max(m0 - a.HALO, 0) / HW), sbn = min(sb0 + 1, a.M / HW - 1);
+    sb1 = (sb0 + 1) * HW;
+    eoff0 = (long long)sb0 * a.env_stride + (a.slot ? (long long)a.slot[sb0] * a.slot_stride : 0) - (long long)sb0 * HW * a.Cin;
+    eoff1 = (long long)sbn * a.env_stride + (a.slot ? (long long)a.slot[sbn] * a.slot_stride : 0) - (long long)sbn * HW * a.Cin;
+  }
   const int KS = 9 * a.Cin / 32;            // k steps of the whole conv (pack stride per column tile)
   constexpr int nsteps = NBLK * 9 * NCS;  // NBLK = Cin / CB
 
@@ -189,7 +227,8 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
       const int g = i * 64 + lane, r = g / NC, s = g - r * NC;
       int m = m0 - a.HALO + r;
       m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);  // rows outside [0, M) are only read by masked taps
-      const bf16_t* src = a.in + (size_t)m * a.Cin + blk * CB + ((s ^ hkey(r)) << 3);
+      const long long eo = GA ? (m >= sb1 ? eoff1 : eoff0) : 0;
+      const bf16_t* src = a.in + (eo + (long long)m * a.Cin) + blk * CB + ((s ^ hkey(r)) << 3);
       __builtin_amdgcn_global_load_lds(src, lds + i * 1024, 16, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -234,10 +273,12 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   }
 
   // epilogue: acc[mi][ct] = D[channel n0 + 16 CT wn + 16 ct + 4q + i][pixel m0 + TM / WM wm + 16 mi + n]
-  if (a.res)
-    halo_epilogue<true>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
+  if (GA && a.act_bias)
+    halo_epilogue<false, GA>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
+  else if (a.res)
+    halo_epilogue<true, false>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
   else
-    halo_epilogue<false>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
+    halo_epilogue<false, false>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
 }
 
 // staging geometry for a (W, Cin) pair: the whole Cin staged at once (one block; a rolled loop over channel
@@ -258,35 +299,59 @@ extern "C" {
 
 int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks) {
   HaloArgs g{};
-  return ks == 3 && H >= 2 && W >= 2 && (Cin == 128 || Cin == 256) && Cout % 256 == 0 && halo_geometry(W, Cin, g) > 0 ? 1
-                                                                                                               : 0;
+  return ks == 3 && H >= 2 && W >= 2 && (Cin == 128 || Cin == 256) && (Cout % 256 == 0 || (Cout == 128 && Cin == 256)) &&
+                 halo_geometry(W, Cin, g) > 0
+             ? 1
+             : 0;
 }
 
-// out = act(conv3x3(in, W) + bias (+ res)) on contiguous NHWC bf16 images (B envs of H x W x Cin); wh = the
+// gather = 1: a slot-gathered / strided input and / or an action-bias table (the GA instance: Cin 256, Cout % 256
+// == 0, the staged range within two envs)
+int mzba_conv_halo_ex_supported(int H, int W, int Cin, int Cout, int ks, int gather) {
+  if (!mzba_conv_halo_supported(H, W, Cin, Cout, ks)) return 0;
+  if (!gather) return 1;
+  HaloArgs g{};
+  halo_geometry(W, Cin, g);
+  return Cin == 256 && Cout % 256 == 0 && g.HR <= H * W ? 1 : 0;
+}
+
+// out = act(conv3x3(in, W) (+ act_bias[p][act[b]]) + bias (+ res)); env b's input image at in + b env_stride +
+// slot[b] slot_stride (slot optional; env_stride = H W Cin with neither slot nor act_bias: contiguous); wh = the
 // pack_lat16 packing of the BN-folded [Cout][3][3][Cin] weights (agent.py PackedNets._conv "wh").
-int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
-                   int Cin, int Cout, int relu, hipStream_t stream) {
+int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wh,
+                      const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,
+                      int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream) {
   MZ_CHECK_ARG(in && wh && bias && out && B > 0, -1);
-  MZ_CHECK_ARG(mzba_conv_halo_supported(H, W, Cin, Cout, 3), -2);
+  MZ_CHECK_ARG(!act_bias || (act && A > 0 && !res), -1);
+  const bool ga = slot || act_bias || env_stride != (long long)H * W * Cin;
+  MZ_CHECK_ARG(mzba_conv_halo_ex_supported(H, W, Cin, Cout, 3, ga ? 1 : 0), -2);
   const long long M = (long long)B * H * W;
   MZ_CHECK_ARG(M + 2 * hl::TM < (1LL << 31), -3);  // pixel indices in int (global offsets are size_t)
   HaloArgs a{(const bf16_t*)in, (const bf16_t*)wh, bias, (const bf16_t*)res, (bf16_t*)out, (int)M, H, W, Cin, Cout, relu};
+  a.slot = slot, a.env_stride = env_stride, a.slot_stride = slot_stride, a.act_bias = act_bias, a.act = act, a.A = A;
   const int lds = halo_geometry(W, Cin, a);
-  const dim3 grid((unsigned)((M + hl::TM - 1) / hl::TM), (unsigned)(Cout / hl::TN));
-  auto launch = [&](auto kern) {
-    static bool attr = false;  // per instance: the 160 KiB of dynamic LDS
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, hl::LDS_MAX);
-      attr = true;
-    }
-    hipLaunchKernelGGL(kern, grid, dim3(hl::NT), lds, stream, a);
-  };
-  if (a.CB == 256)
-    launch(conv_halo_kernel<256, 1>);
-  else
-    launch(conv_halo_kernel<128, 1>);
+  const int tn = Cout % 256 == 0 ? 256 : 128;
+  const dim3 grid((unsigned)((M + hl::TM - 1) / hl::TM), (unsigned)(Cout / tn));
+  typedef void (*Kern)(HaloArgs);
+  static const Kern kerns[4] = {conv_halo_kernel<256, 1, 2, 1, 256, true>, conv_halo_kernel<256, 1, 4, 1, 128>,
+                                conv_halo_kernel<256, 1>, conv_halo_kernel<128, 1>};
+  static const bool attrs = [] {  // every instance: the 160 KiB of dynamic LDS
+    for (Kern k : kerns)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, hl::LDS_MAX);
+    return true;
+  }();
+  (void)attrs;
+  const Kern kern = ga ? kerns[0] : (tn == 128 ? kerns[1] : (a.CB == 256 ? kerns[2] : kerns[3]));
+  hipLaunchKernelGGL(kern, grid, dim3(hl::NT), lds, stream, a);
   MZ_LAUNCH_CHECK();
   return 0;
+}
+
+// the contiguous form (no gather, no action bias)
+int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
+                   int Cin, int Cout, int relu, hipStream_t stream) {
+  return mzba_conv_halo_ex(in, (long long)H * W * Cin, nullptr, 0, wh, bias, nullptr, nullptr, 0, res, out, B, H, W, Cin,
+                           Cout, relu, stream);
 }
 
 }  // extern "C"

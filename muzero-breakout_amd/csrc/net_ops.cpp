@@ -218,12 +218,15 @@ struct NetRunner : torch::CustomClassHolder {
                "mzba_conv_x6");
       return;
     }
-    // large images (config 3: 21x21 latents, the 84x84 128 -> 256 conv): the halo-tiled kernel
-    if (l.wh.defined() && use_halo && !slot && env_stride == H_ * W_ * l.cin && !ab &&
-        mzba_conv_halo_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks)) {
-      check_rc(mzba_conv_halo(in, vp(l.wh), vp<float>(l.b), res, out, (int)B, (int)H_, (int)W_, (int)l.cin, (int)l.cout,
-                              relu, s),
-               "mzba_conv_halo");
+    // large images (config 3: 21x21 latents, the 84x84 128 -> 256 conv; with gather the dynamics' first conv off
+    // the latent pool + its action-bias table): the halo-tiled kernel
+    const int gather = (slot || ab || env_stride != H_ * W_ * l.cin) ? 1 : 0;
+    if (l.wh.defined() && use_halo && !(ab && res) &&
+        mzba_conv_halo_ex_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks, gather)) {
+      check_rc(mzba_conv_halo_ex(in, env_stride, slot, slot_stride, vp(l.wh), vp<float>(l.b),
+                                 ab ? vp<float>(l.act_bias) : nullptr, ab ? act : nullptr, (int)l.A, res, out, (int)B,
+                                 (int)H_, (int)W_, (int)l.cin, (int)l.cout, relu, s),
+               "mzba_conv_halo_ex");
       return;
     }
     if (l.wt.defined() && use_band && !slot && env_stride == H_ * W_ * l.cin && !ab &&

@@ -35,6 +35,8 @@ SIGNATURES = {
     "mzba_conv2d_set_variant": [I],
     "mzba_conv_halo_supported": [I, I, I, I, I],
     "mzba_conv_halo": [P, P, P, P, P, I, I, I, I, I, I, P],
+    "mzba_conv_halo_ex_supported": [I, I, I, I, I, I],
+    "mzba_conv_halo_ex": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, P],
     "mzba_conv_x6_supported": [I, I, I, I, I],
     "mzba_conv_x6": [P, P, P, P, P, I, I, I, I, I, I, P],
     "mzba_conv_x6_set_variant": [I],

@@ -101,9 +101,9 @@ class PackedNets:
         # dynamics (networks.py:117-149)
         w = sd["dyn_net.conv_block.conv.weight"]
         cmain = self.c1
-        self.dyn0 = self._conv(w[:, :cmain], sd["dyn_net.conv_block.conv.bias"], self._bn(sd, "dyn_net.conv_block.bn"),
-                               act_w=w[:, cmain:])
         lat = (self.lh, self.lw)
+        self.dyn0 = self._conv(w[:, :cmain], sd["dyn_net.conv_block.conv.bias"], self._bn(sd, "dyn_net.conv_block.bn"),
+                               act_w=w[:, cmain:], hw=lat)
         self.dyn = [self._res(sd, f"dyn_net.res_blocks.{i}", hw=lat)
                     for i in range(mcfg["dynamics_network"]["num_res_blocks"])]
         self.rew_conv = self._conv(sd["dyn_net.reward_head.0.conv.weight"], sd["dyn_net.reward_head.0.conv.bias"],
@@ -118,7 +118,7 @@ class PackedNets:
         self.dyn_tower = self._tower(sd, "dyn_net.res_blocks", mcfg["dynamics_network"]["num_res_blocks"])
         self.pred_tower = self._tower(sd, "pred_net.res_blocks", mcfg["prediction_network"]["num_res_blocks"])
         self.pol_conv = self._conv(sd["pred_net.policy_head.0.conv.weight"], sd["pred_net.policy_head.0.conv.bias"],
-                                   self._bn(sd, "pred_net.policy_head.0.bn"))
+                                   self._bn(sd, "pred_net.policy_head.0.bn"), hw=lat)
         self.pol_lin = self._linear(sd["pred_net.policy_head.2.weight"], sd["pred_net.policy_head.2.bias"], self.c1 // 2)
         self.val_conv = self._conv(sd["pred_net.value_head.0.conv.weight"], sd["pred_net.value_head.0.conv.bias"],
                                    self._bn(sd, "pred_net.value_head.0.bn"))
@@ -358,9 +358,10 @@ class PackedNets:
         if self.dtype == "bf16" and cout % 32 == 0 and cin_p in (64, 128, 256):
             layer["wf"] = torch.tensor(pack_lat(wp.reshape(cout, -1), cout, k, cin_p),
                                        dtype=torch.float32).to(self.tdt).to(self.device)
-        if (hw is not None and self.dtype == "bf16" and act_w is None and hw[0] * hw[1] > 320
-                and L.lib().mzba_conv_halo_supported(hw[0], hw[1], cin_p, cout, k)):
-            # config 3's large images (mzba_conv_halo): pack_lat16 of [Cout][tap][Cin]
+        if (hw is not None and self.dtype == "bf16" and hw[0] * hw[1] > 320
+                and L.lib().mzba_conv_halo_ex_supported(hw[0], hw[1], cin_p, cout, k, int(act_w is not None))):
+            # config 3's large images (mzba_conv_halo / _ex with the dynamics' gather + action bias): pack_lat16
+            # of [Cout][tap][Cin]
             layer["wh"] = torch.tensor(pack_lat16(wp.reshape(cout, -1), cout, k, cin_p),
                                        dtype=torch.float32).to(self.tdt).to(self.device)
         if (hw is not None and self.dtype == "f32" and act_w is None

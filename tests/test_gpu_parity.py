@@ -583,7 +583,8 @@ def test_conv_big_kernel_vs_torch_fp32(B, H, W, Cin, Cout, ks, relu):
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout,relu,with_res", [(150, 21, 21, 256, 256, 1, True), (37, 21, 21, 256, 256, 0, False),
                                                           (12, 84, 84, 128, 256, 0, True), (9, 16, 20, 256, 256, 1, True),
-                                                          (3, 21, 21, 256, 512, 1, True)])
+                                                          (3, 21, 21, 256, 512, 1, True), (37, 21, 21, 256, 128, 1, False),
+                                                          (20, 21, 21, 256, 128, 0, True)])
 def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res):
     """The halo-tiled 3x3 conv (mzba_conv_halo: config 3's 21x21 latent convs and 84x84 128 -> 256 conv; 256
     output pixels + W + 1 halo rows staged once per workgroup, every tap read from LDS, taps leaving the image
@@ -617,6 +618,53 @@ def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res):
           f"{(got - big.float()).abs().max().item() / scale:.2e}")
     assert err <= 1e-2 * scale  # bf16 output rounding
     assert (got - big.float()).abs().max().item() <= 1e-2 * scale
+
+
+@pytest.mark.parametrize("B,S,A", [(37, 5, 3), (150, 1, 3), (9, 50, 4)])
+def test_conv_halo_gather_action_bias_vs_torch_fp32(B, S, A):
+    """mzba_conv_halo_ex as config 3's dynamics first conv (networks.py:117-122, 160): every env's input
+    gathered from its slot of a latent pool ((S + 1) latents per env), the action planes folded into a
+    [HW][A][Cout] bias table (agent.py _conv act_w), ReLU — vs a torch fp32 conv of the gathered bf16 operands
+    + the table row of the env's action + bias, and vs conv_igemm (mzba_conv2d) on the same arguments."""
+    from mzba import _lib as L
+    from mzba.agent import pack_lat16
+    H = W = 21
+    Cin = Cout = 256
+    HW = H * W
+    assert L.lib().mzba_conv_halo_ex_supported(H, W, Cin, Cout, 3, 1)
+    g = torch.Generator(device="cuda").manual_seed(B + S)
+    dev = torch.device("cuda")
+    pool = torch.randn(B, S + 1, H, W, Cin, generator=g, device=dev).to(torch.bfloat16)
+    slot = torch.randint(0, S + 1, (B,), generator=g, device=dev, dtype=torch.int32)
+    act = torch.randint(0, A, (B,), generator=g, device=dev, dtype=torch.int32)
+    w = (torch.randn(Cout, 3, 3, Cin, generator=g, device=dev) / (Cin * 9) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g, device=dev)
+    tab = torch.randn(HW, A, Cout, generator=g, device=dev)
+    x = pool[torch.arange(B, device=dev), slot.long()]
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1)
+    ref = ref.permute(0, 2, 3, 1) + tab[:, act.long()].permute(1, 0, 2).reshape(B, H, W, Cout)
+    ref = torch.relu(ref)
+    wh = torch.tensor(pack_lat16(w.float().cpu().numpy().reshape(Cout, -1), Cout, 3, Cin)).to(torch.bfloat16).cuda()
+    out = torch.full((B, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    L.call("mzba_conv_halo_ex", L.ptr(pool), (S + 1) * HW * Cin, L.ptr(slot), HW * Cin, L.ptr(wh), L.ptr(b), L.ptr(tab),
+           L.ptr(act), A, None, L.ptr(out), B, H, W, Cin, Cout, 1, L.stream())
+    ig = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=dev)
+    L.call("mzba_conv2d", 1, L.ptr(pool), (S + 1) * HW * Cin, L.ptr(slot), HW * Cin, L.ptr(w), L.ptr(b), L.ptr(tab),
+           L.ptr(act), A, None, L.ptr(ig), B, H, W, Cin, Cout, 3, 1, L.stream())
+    torch.cuda.synchronize()
+    got = out.float()
+    assert torch.isfinite(got).all()
+    scale = ref.abs().max().item()
+    err = (got - ref).abs().max().item()
+    print(f"conv_halo_ex B={B} S={S}: max err {err / scale:.2e} of the magnitude, vs conv_igemm "
+          f"{(got - ig.float()).abs().max().item() / scale:.2e}")
+    assert err <= 1e-2 * scale  # bf16 output rounding
+    assert (got - ig.float()).abs().max().item() <= 1e-2 * scale
+    # the contract's refusals: an action-bias table with a residual, an unsupported geometry
+    assert L.lib().mzba_conv_halo_ex(L.ptr(pool), (S + 1) * HW * Cin, L.ptr(slot), HW * Cin, L.ptr(wh), L.ptr(b),
+                                     L.ptr(tab), L.ptr(act), A, L.ptr(out), L.ptr(out), B, H, W, Cin, Cout, 1,
+                                     L.stream()) == -1
+    assert not L.lib().mzba_conv_halo_ex_supported(4, 5, Cin, Cout, 3, 1)
 
 
 @pytest.mark.parametrize("B,H,W,Cin,relu,with_res", [(1000, 4, 5, 256, 1, True), (37, 4, 5, 256, 0, False),
