@@ -103,8 +103,10 @@ int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_
  * of B envs, zero padding. A workgroup stages 256 consecutive output pixels plus W + 1 halo rows on each side
  * into LDS once per channel block and runs all 9 taps from it. wh = pack_lat16 of the BN-folded
  * [Cout][3][3][Cin] weights: wh[Cout/16][9*Cin/32][64][8], wh[ct][s][l][j] = W[16 ct + l % 16][32 s + 8 (l / 16) + j]
- * with the K index tap * Cin + channel. Supported: Cin 128 / 256, Cout % 256 == 0 or Cout 128 at Cin 256 (the
- * policy head's conv, networks.py:200-206), the staged halo within the LDS (mzba_conv_halo_supported). Replaces
+ * with the K index tap * Cin + channel. Supported: Cin 128 / 256, Cout % 256 == 0, or Cout 128 with all Cin channels
+ * staged at once (the policy head's conv, networks.py:200-206; the 84x84 128-channel blocks), the staged halo within
+ * the LDS in one block or, at Cin 256, two 128-channel blocks (W <= 30 / 156: one block at Cin 256 / 128; two
+ * blocks up to W = 156) (mzba_conv_halo_supported). Replaces
  * networks.py:19-35 ResidualBlock convs (the second with res). */
 int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks);
 /* mzba_conv_halo with a gathered input and the action planes folded into a bias table (the dynamics' first conv,

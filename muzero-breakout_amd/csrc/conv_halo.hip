@@ -8,7 +8,7 @@
 // channels. A 3x3 tap shifts the flattened pixel index by dy W + dx, so every tap of the tile reads rows of ONE
 // staged range: the tile's pixels plus a halo of W + 1 rows on each side (HR = 256 + 2 W + 2 pixel rows). That
 // range is staged into LDS once, all Cin (128 or 256) channels (supported while HR x 2 Cin B fits the 160 KiB:
-// W <= 30 at Cin 256, W <= 156 at Cin 128) with LDS-DMA (global_load_lds_dwordx4, no VGPR round trip), and the 9 taps
+// W <= 30 at Cin 256, W <= 156 at Cin 128; past W = 30 at Cin 256 in two 128-channel blocks) with LDS-DMA (global_load_lds_dwordx4, no VGPR round trip), and the 9 taps
 // x the block's channel steps run from it — the activation operand is fetched from L2 once per tile, not once
 // per tap as an im2col GEMM tile fetches it (conv_big_bf16_kernel: 9 x the activation traffic and its LDS
 // writes every K step).
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   // per pixel tile mi of the wave: the lane's pixel is staged row prow0 + 16 mi at tap (0, 0); byte mi of
   // okw[mi / 4] says which taps stay in the image (bit 0: y > 0, 1: y < H - 1, 2: x > 0, 3: x < W - 1,
   // 4: the pixel exists — rows past M read only the zero block)
-  const int prow0 = wm * (hl::TM / WM) + n + a.HALO;
+  int prow0 = wm * (hl::TM / WM) + n + a.HALO;
   uint32_t okw[MT / 4] = {};
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
@@ -221,6 +221,11 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
 #pragma unroll
   for (int blk = 0; blk < NBLK; ++blk) {
     if (blk > 0) __syncthreads();  // every wave is done with the previous block's rows
+    if (NBLK > 1) {  // opaque per block: the fragment addresses CSE'd across the unrolled blocks spilled 322 VGPRs
+      asm volatile("" : "+v"(prow0));
+#pragma unroll
+      for (int i = 0; i < MT / 4; ++i) asm volatile("" : "+v"(okw[i]));
+    }
     // stage rows [m0 - HALO, m0 - HALO + HR) x channels [blk CB, (blk + 1) CB): block i of 1 KiB holds
     // chunks 64 i .. 64 i + 63 (row g / NC, physical chunk g % NC = logical chunk ^ hkey(row))
     for (int i = wave; i < a.NI; i += 8) {
@@ -281,16 +286,19 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
     halo_epilogue<false, false>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
 }
 
-// staging geometry for a (W, Cin) pair: the whole Cin staged at once (one block; a rolled loop over channel
-// blocks would carry the accumulators across its back edge, which the compiler renames and copies), 0 if the
-// halo does not fit the LDS
+// staging geometry for a (W, Cin) pair: the whole Cin staged at once where it fits (one block), else Cin 256 in two
+// 128-channel blocks (the blocks unrolled: a rolled loop would carry the accumulators across its back edge, which
+// the compiler renames and copies); 0 if the halo does not fit the LDS
 int halo_geometry(int W, int Cin, HaloArgs& g) {
-  const int cb = Cin, halo = W + 1, hr = hl::TM + 2 * halo, rb = cb * 2;
-  const int ni = (hr * rb + 1023) / 1024;
-  const int zoff = (ni * 1024 + 16 * rb - 1) / (16 * rb) * (16 * rb);  // the 16-row zero block, 16-row aligned
-  if ((cb != 128 && cb != 256) || zoff + 16 * rb > hl::LDS_MAX) return 0;
-  g.HALO = halo, g.HR = hr, g.CB = cb, g.NI = ni, g.ZOFF = zoff;
-  return zoff + 16 * rb;
+  for (int cb = Cin; cb >= 128; cb /= 2) {
+    const int halo = W + 1, hr = hl::TM + 2 * halo, rb = cb * 2;
+    const int ni = (hr * rb + 1023) / 1024;
+    const int zoff = (ni * 1024 + 16 * rb - 1) / (16 * rb) * (16 * rb);  // the 16-row zero block, 16-row aligned
+    if ((Cin != 128 && Cin != 256) || zoff + 16 * rb > hl::LDS_MAX) continue;
+    g.HALO = halo, g.HR = hr, g.CB = cb, g.NI = ni, g.ZOFF = zoff;
+    return zoff + 16 * rb;
+  }
+  return 0;
 }
 
 }  // namespace
@@ -299,10 +307,8 @@ extern "C" {
 
 int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks) {
   HaloArgs g{};
-  return ks == 3 && H >= 2 && W >= 2 && (Cin == 128 || Cin == 256) && (Cout % 256 == 0 || (Cout == 128 && Cin == 256)) &&
-                 halo_geometry(W, Cin, g) > 0
-             ? 1
-             : 0;
+  if (ks != 3 || H < 2 || W < 2 || (Cin != 128 && Cin != 256) || halo_geometry(W, Cin, g) == 0) return 0;
+  return Cout % 256 == 0 || (Cout == 128 && g.CB == Cin) ? 1 : 0;  // Cout 128: one staged block
 }
 
 // gather = 1: a slot-gathered / strided input and / or an action-bias table (the GA instance: Cin 256, Cout % 256
@@ -312,7 +318,7 @@ int mzba_conv_halo_ex_supported(int H, int W, int Cin, int Cout, int ks, int gat
   if (!gather) return 1;
   HaloArgs g{};
   halo_geometry(W, Cin, g);
-  return Cin == 256 && Cout % 256 == 0 && g.HR <= H * W ? 1 : 0;
+  return Cin == 256 && g.CB == 256 && Cout % 256 == 0 && g.HR <= H * W ? 1 : 0;
 }
 
 // out = act(conv3x3(in, W) (+ act_bias[p][act[b]]) + bias (+ res)); env b's input image at in + b env_stride +
@@ -333,15 +339,18 @@ int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot,
   const int tn = Cout % 256 == 0 ? 256 : 128;
   const dim3 grid((unsigned)((M + hl::TM - 1) / hl::TM), (unsigned)(Cout / tn));
   typedef void (*Kern)(HaloArgs);
-  static const Kern kerns[4] = {conv_halo_kernel<256, 1, 2, 1, 256, true>, conv_halo_kernel<256, 1, 4, 1, 128>,
-                                conv_halo_kernel<256, 1>, conv_halo_kernel<128, 1>};
+  static const Kern kerns[6] = {conv_halo_kernel<256, 1, 2, 1, 256, true>, conv_halo_kernel<256, 1, 4, 1, 128>,
+                                conv_halo_kernel<256, 1>, conv_halo_kernel<128, 1>, conv_halo_kernel<128, 2>,
+                                conv_halo_kernel<128, 1, 4, 1, 128>};
   static const bool attrs = [] {  // every instance: the 160 KiB of dynamic LDS
     for (Kern k : kerns)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, hl::LDS_MAX);
     return true;
   }();
   (void)attrs;
-  const Kern kern = ga ? kerns[0] : (tn == 128 ? kerns[1] : (a.CB == 256 ? kerns[2] : kerns[3]));
+  const Kern kern = ga ? kerns[0]
+                       : tn == 128 ? (Cin == 256 ? kerns[1] : kerns[5])
+                                   : (a.CB == 256 ? kerns[2] : (Cin == 128 ? kerns[3] : kerns[4]));
   hipLaunchKernelGGL(kern, grid, dim3(hl::NT), lds, stream, a);
   MZ_LAUNCH_CHECK();
   return 0;

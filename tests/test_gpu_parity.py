@@ -584,7 +584,8 @@ def test_conv_big_kernel_vs_torch_fp32(B, H, W, Cin, Cout, ks, relu):
 @pytest.mark.parametrize("B,H,W,Cin,Cout,relu,with_res", [(150, 21, 21, 256, 256, 1, True), (37, 21, 21, 256, 256, 0, False),
                                                           (12, 84, 84, 128, 256, 0, True), (9, 16, 20, 256, 256, 1, True),
                                                           (3, 21, 21, 256, 512, 1, True), (37, 21, 21, 256, 128, 1, False),
-                                                          (20, 21, 21, 256, 128, 0, True)])
+                                                          (20, 21, 21, 256, 128, 0, True), (5, 84, 84, 256, 256, 1, True),
+                                                          (9, 42, 42, 256, 256, 0, False), (6, 84, 84, 128, 128, 1, True)])
 def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res):
     """The halo-tiled 3x3 conv (mzba_conv_halo: config 3's 21x21 latent convs and 84x84 128 -> 256 conv; 256
     output pixels + W + 1 halo rows staged once per workgroup, every tap read from LDS, taps leaving the image
