@@ -189,3 +189,34 @@ def test_agent_random_init_equals_reference_construction(tag):
                 f = v.numpy().astype(np.float64).reshape(-1)
                 got = np.concatenate([[f.sum(), np.abs(f).sum()], f[:4], f[-1:]])
                 np.testing.assert_array_equal(got, d[f"{tag}/s{seed}/a{ai}/{k}"], err_msg=f"s{seed} a{ai} {k}")
+
+
+def test_conv_halo_support_matrix_and_bad_arguments_without_gpu():
+    """mzba_conv_halo(_ex)'s support checks and argument checks run before any HIP call: the 21x21 latent
+    convs (gathered / action-bias form too), the 84x84 and 42x42 representation convs (two-block staging past
+    W = 30 at Cin 256), Cout 128 only with all Cin channels staged at once, no gather past two envs per staged
+    range (4x5), no action-bias table with a residual, null buffers."""
+    import ctypes
+    from mzba import _lib
+    L = _lib.lib()
+    sup = {(H, W, ci, co): (L.mzba_conv_halo_supported(H, W, ci, co, 3), L.mzba_conv_halo_ex_supported(H, W, ci, co, 3, 1))
+           for H, W, ci, co in [(21, 21, 256, 256), (21, 21, 256, 128), (42, 42, 256, 256), (84, 84, 256, 256),
+                                (84, 84, 128, 128), (84, 84, 128, 256), (42, 42, 256, 128), (84, 84, 64, 128),
+                                (4, 5, 256, 256)]}
+    assert sup == {(21, 21, 256, 256): (1, 1), (21, 21, 256, 128): (1, 0), (42, 42, 256, 256): (1, 0),
+                   (84, 84, 256, 256): (1, 0), (84, 84, 128, 128): (1, 0), (84, 84, 128, 256): (1, 0),
+                   (42, 42, 256, 128): (0, 0), (84, 84, 64, 128): (0, 0), (4, 5, 256, 256): (1, 0)}
+    assert L.mzba_conv_halo_supported(21, 21, 256, 256, 1) == 0
+    p = ctypes.c_void_p(64)
+    n = 21 * 21 * 256
+    # null input / weights / bias / output
+    assert L.mzba_conv_halo_ex(None, n, None, 0, p, p, None, None, 0, None, p, 4, 21, 21, 256, 256, 1, None) == -1
+    assert L.mzba_conv_halo_ex(p, n, None, 0, p, None, None, None, 0, None, p, 4, 21, 21, 256, 256, 1, None) == -1
+    # action-bias table without actions, with a residual
+    assert L.mzba_conv_halo_ex(p, n, None, 0, p, p, p, None, 3, None, p, 4, 21, 21, 256, 256, 1, None) == -1
+    assert L.mzba_conv_halo_ex(p, n, None, 0, p, p, p, p, 3, p, p, 4, 21, 21, 256, 256, 1, None) == -1
+    # gather where a staged range spans more than two envs; unsupported widths
+    assert L.mzba_conv_halo_ex(p, 2 * 20 * 256, p, 20 * 256, p, p, None, None, 0, None, p, 4, 4, 5, 256, 256, 1,
+                               None) == -2
+    assert L.mzba_conv_halo_ex(p, 21 * 21 * 64, None, 0, p, p, None, None, 0, None, p, 4, 21, 21, 64, 256, 1, None) == -2
+    assert L.mzba_conv_halo(p, p, p, None, p, 4, 42, 42, 256, 128, 1, None) == -2
