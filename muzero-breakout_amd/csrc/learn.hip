@@ -798,12 +798,18 @@ static bool wgrad_img_plan(int B, int Bseg, int H, int W, int Cin, int Cout, WgP
   return true;
 }
 
-// acc[i] += sum_s part[s][i] (split order)
-__global__ void sum_partials_kernel(const float* __restrict__ part, int nsplit, size_t n, float* __restrict__ acc) {
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    float s = part[i];
-    for (int k = 1; k < nsplit; ++k) s += part[(size_t)k * n + i];
-    acc[i] += s;
+// the weight and bias partials of one split weight-gradient launch, summed in one launch: acc[i] += sum_s
+// part[s][i] for i < n, bacc[j] += sum_s bpart[s][j] for j < nb, each element in split order (round 4: one launch
+// instead of one per buffer, the same sums)
+__global__ void sum_partials2_kernel(const float* __restrict__ part, const float* __restrict__ bpart, int nsplit,
+                                     size_t n, size_t nb, float* __restrict__ acc, float* __restrict__ bacc) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + nb; i += (size_t)gridDim.x * blockDim.x) {
+    const bool w = i < n;
+    const float* p = w ? part + i : bpart + (i - n);
+    const size_t st = w ? n : nb;
+    float s = p[0];
+    for (int k = 1; k < nsplit; ++k) s += p[(size_t)k * st];
+    (w ? acc[i] : bacc[i - n]) += s;
   }
 }
 
@@ -1344,11 +1350,9 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
       hipLaunchKernelGGL(conv_wgrad_img_kernel<true>, grid, dim3(WI_NT), ip.lds, stream, ip.a, ipart, ibpart);
     else
       hipLaunchKernelGGL(conv_wgrad_img_kernel<false>, grid, dim3(WI_NT), ip.lds, stream, ip.a, ipart, ibpart);
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(nwi)), dim3(256), 0, stream, (const float*)ipart, ip.nsplit,
-                       nwi, dw);
-    if (db)
-      hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(Cout)), dim3(256), 0, stream, (const float*)ibpart,
-                         ip.nsplit, (size_t)Cout, db);
+    const size_t nbi = db ? (size_t)Cout : 0;
+    hipLaunchKernelGGL(sum_partials2_kernel, dim3(grid_for(nwi + nbi)), dim3(256), 0, stream, (const float*)ipart,
+                       (const float*)ibpart, ip.nsplit, nwi, nbi, dw, db);
     MZ_LAUNCH_CHECK();
     return 0;
   }
@@ -1368,11 +1372,9 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
     else
       hipLaunchKernelGGL(conv_wgrad_kernel<float>, dim3((unsigned)tiles, (unsigned)nsplit), dim3(256), 0, stream,
                          (const float*)xs[i], (const float*)dys[i], B, H, W, Cin, Cout, ks, rps, part, bpart);
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(nw)), dim3(256), 0, stream, (const float*)part,
-                       (int)nsplit, nw, dw);
-    if (db)
-      hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for(Cout)), dim3(256), 0, stream, (const float*)bpart,
-                         (int)nsplit, (size_t)Cout, db);
+    const size_t nb = db ? (size_t)Cout : 0;
+    hipLaunchKernelGGL(sum_partials2_kernel, dim3(grid_for(nw + nb)), dim3(256), 0, stream, (const float*)part,
+                       (const float*)bpart, (int)nsplit, nw, nb, dw, db);
   }
   MZ_LAUNCH_CHECK();
   return 0;
@@ -1466,9 +1468,8 @@ int mzba_linear_backward(int dtype, const void* x, const float* w, const float* 
                          K, O, accumulate);
     hipLaunchKernelGGL(linear_bwd_w_kernel<T>, dim3((K + 255) / 256, nsplit), dim3(256), 0, stream, dy, (const T*)x,
                        B, K, O, rps, part, bpart);
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(grid_for((size_t)O * K)), dim3(256), 0, stream, (const float*)part,
-                       nsplit, (size_t)O * K, dw);
-    hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(64), 0, stream, (const float*)bpart, nsplit, (size_t)O, db);
+    hipLaunchKernelGGL(sum_partials2_kernel, dim3(grid_for((size_t)O * K + O)), dim3(256), 0, stream,
+                       (const float*)part, (const float*)bpart, nsplit, (size_t)O * K, (size_t)O, dw, db);
     MZ_LAUNCH_CHECK();
     return 0;
   });
