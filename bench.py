@@ -142,7 +142,7 @@ def run_env(args, world, rank, local):
                "sample": f"oracle numpy env (batched like parallel_breakout.py) + grayscale, {nb} envs x {n} steps "
                          f"at {H}x{W} ({cs:.1f} s)"}
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": "env-steps/sec, env step + render + frame stack only (SURVEY configs 1/3)",
             "value": world * B * args.steps / dt, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
@@ -154,7 +154,9 @@ def run_env(args, world, rank, local):
                          "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
                          "traffic": traffic, "bytes_per_env_step": env_bytes(H, W), "avg_launch_ms": kms},
             "cpu_baseline": cpu,
-        }))
+        }
+        check_fracs(line)
+        print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
 
@@ -241,7 +243,7 @@ def run_learner(args, world, rank, local):
                "sample": f"oracle/learner.py (torch-CPU f32, the reference's ops) on {n} minibatches of {nb} "
                          f"windows ({cs:.1f} s)"}
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": "learner windows/sec (RLSystem._training_stage minibatch: K=5 rollout, train-mode BN, "
                       "backward, Adam)",
             "value": world * B * args.steps / dtt, "unit": "windows/s", "n_gpus": world, "steps": args.steps,
@@ -257,7 +259,9 @@ def run_learner(args, world, rank, local):
             "launch": "eager" if args.no_graph else "hip-graph replay of the whole minibatch",
             "streams": args.learner_streams,
             "cpu_baseline": cpu,
-        }))
+        }
+        check_fracs(line)
+        print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
 
@@ -299,63 +303,107 @@ def step_flops(p, H, W, S):
     return fl + pred + S * (dyn + pred)
 
 
-def tower_traffic(B, fused_tower):
+def tower_traffic(B, fused_tower, kname):
     """PMC HBM bytes per launch of the dominant kernel at this batch (profiles/tower_hbm_traffic.json,
     written by tools/pmc_summarize.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)."""
     tpath = os.path.join(ROOT, "profiles", "tower_hbm_traffic.json")
     if not (fused_tower and os.path.exists(tpath)):
         return None, None
-    kname = tower_kernel_name(B)
     for rec in json.load(open(tpath))["records"]:
         if rec.get("envs") == B and rec.get("kernel_name") == kname:
             return rec.get("bytes_per_launch"), rec
     return None, None
 
 
-def tower_counters(B, kname):
-    """Measured SQ counters of the dominant kernel at this batch (profiles/tower_sq_counters.json, from the
-    two rocprofv3 --pmc passes of tools/pmc_towerp_sq.sh inside this bench): MFMA-pipe busy fraction of the
-    SIMD cycles at the clock the chip held, LDS bank-conflict share, and the executed MFMA count."""
+def tower_counters(B, kname, sims, dyn):
+    """Measured SQ counters of one template instance of the dominant kernel in the bench run with this batch,
+    simulation count and dynamics precision (profiles/tower_sq_counters.json, from the two rocprofv3 --pmc passes
+    of tools/gpu_run.sh 'sq' inside this bench): MFMA-pipe busy fraction of the SIMD cycles at the clock the
+    chip held, LDS bank-conflict share, and the executed MFMA count. Keyed on the instance (towerp_kernel<1> is
+    the fp16 dynamics step of config 5, towerp_kernel<0> every bf16 step), so a record is never quoted for
+    launches it did not count."""
     tpath = os.path.join(ROOT, "profiles", "tower_sq_counters.json")
     if not os.path.exists(tpath):
         return None
     for rec in json.load(open(tpath))["records"]:
-        if rec.get("envs") == B and rec.get("kernel_name") == kname:
+        if (rec.get("envs"), rec.get("kernel_name"), rec.get("sims", 50), rec.get("dyn_dtype")) == (B, kname, sims, dyn):
             return rec
     return None
 
 
-def l2_weight_stream(conv_ms, C=256):
-    """The per-CU weight-stream bound of a tower conv: every workgroup (one per CU)
-    streams each conv's whole weight pack (C x 9C bf16 = 1.18 MB) from L2 into its registers, whatever its
-    env count, so a conv takes at least those bytes / the per-CU rate that rate the L2 weight-stream probe
-    measured for the tower's access form (tools/probes/l2_stream_probe.hip: all 256 CUs streaming the 33 MB
-    tower pack with 6 fragments in flight per wave, profiles/l2_stream.json)."""
-    tpath = os.path.join(ROOT, "profiles", "l2_stream.json")
-    if not (conv_ms and os.path.exists(tpath)):
-        return None
-    rec = json.load(open(tpath))
-    rate = rec.get("per_cu_GBps")
-    if not rate:
+L2_PEAK_TBPS = 34.5  # MI355X L2 (8 XCDs x 4 MiB) aggregate read rate, MI355X_MICROARCH.md 'L2 (per XCD)'
+
+
+def l2_weight_stream(conv_ms, C=256, n_cu=256):
+    """The per-CU weight stream of a tower conv: every workgroup streams each conv's whole
+    weight pack (C x 9C bf16 = 1.18 MB) from L2 into its registers whatever its env count, so a CU moves those
+    bytes per conv. `frac` = that per-CU rate / the L2 peak per CU (34.5 TB/s / 256 CUs, the guide's chip figure).
+    Beside it, not a bound: the rate tools/probes/l2_stream_probe.hip sustained with the tower's own access form
+    (all 256 CUs streaming the 33 MB tower pack, profiles/l2_stream.json) — the kernel may exceed what that
+    probe sustains, so it is reported as a ratio, never as a roofline fraction."""
+    if not conv_ms:
         return None
     nbytes = C * 9 * C * 2
-    floor_ms = nbytes / (rate * 1e9) * 1e3
-    return {"bytes_per_cu_per_conv": nbytes, "per_cu_GBps": rate, "floor_ms_per_conv": floor_ms,
-            "measured_ms_per_conv": conv_ms, "frac": floor_ms / conv_ms, "source": "profiles/l2_stream.json"}
+    rate = nbytes / (conv_ms * 1e-3) / 1e9
+    peak = L2_PEAK_TBPS * 1e3 / n_cu
+    out = {"bytes_per_cu_per_conv": nbytes, "measured_ms_per_conv": conv_ms, "achieved_per_cu_GBps": rate,
+           "peak_per_cu_GBps": peak, "frac": rate / peak, "peak_source": "MI355X_MICROARCH.md L2 aggregate / 256 CUs"}
+    tpath = os.path.join(ROOT, "profiles", "l2_stream.json")
+    if os.path.exists(tpath):
+        probe = json.load(open(tpath)).get("per_cu_GBps")
+        if probe:
+            out.update({"probe_per_cu_GBps": probe, "ratio_to_probe": rate / probe,
+                        "probe_source": "profiles/l2_stream.json"})
+    return out
 
 
 # Fraction of a launch's algorithmic 3x3-conv FLOPs the kernel issues to the MFMA pipe: the reference's
 # Conv2d(padding=1) on the 4x5 latent evaluates 50 of its 180 taps per env on zero padding. The pixel-tiled
 # kernel (plan 4) skips them all (130 / 180); the column-tiled tower8 (plans 2 / 3) skips the dx ones only
 # (39 of 45 tile-taps, 86.7 %, DESIGN.md §3.0).
-EXECUTED_FRACTION = {"towerp_kernel": 130.0 / 180.0, "tower8_kernel<0, 2>": 39.0 / 45.0, "tower8_kernel<0, 1>": 39.0 / 45.0}
+EXECUTED_FRACTION = {"towerp_kernel<0>": 130.0 / 180.0, "towerp_kernel<1>": 130.0 / 180.0,
+                     "tower8_kernel<0, 2>": 39.0 / 45.0, "tower8_kernel<0, 1>": 39.0 / 45.0}
 
 
-def tower_kernel_name(B):
-    """The kernel mzba_tower_plan picks for batch B (tower.hip)."""
+def tower_kernel_name(B, fp16=False):
+    """The kernel mzba_tower_plan picks for batch B (tower.hip), as rocprofv3 names the template instance
+    (<1>: the fp16 element type of config 5's dynamics step)."""
     from mzba import _lib as L
-    return {2: "tower8_kernel<0, 2>", 3: "tower8_kernel<0, 1>", 4: "towerp_kernel"}.get(L.lib().mzba_tower_plan(B),
-                                                                                      "tower_kernel<0>")
+    e = int(bool(fp16))
+    return {2: f"tower8_kernel<{e}, 2>", 3: f"tower8_kernel<{e}, 1>", 4: f"towerp_kernel<{e}>"}.get(
+        L.lib().mzba_tower_plan(B), f"tower_kernel<{e}>")
+
+
+def x6_flops(p, H, W, S):
+    """Per env-step FLOPs of the f32 parity path's convs that run as split-bf16 x6 products (conv_x6: the
+    layers PackedNets gave x6 weights, 'wx' — the representation's Cout-256 3x3 convs, the latent towers'
+    residual convs) and of the rest (f32-input MFMA convs and heads), at this geometry."""
+    conv = lambda c, hw: 2.0 * hw * c["cout"] * c["ks"] ** 2 * c["cin"]  # noqa: E731
+    x6, hh, ww = 0.0, H, W
+    for kind, layer in p.rep:
+        if kind == "pool":
+            hh, ww = hh // 2, ww // 2
+            continue
+        for c in ([layer] if kind == "conv" else list(layer)):
+            if c.get("wx") is not None:
+                x6 += conv(c, hh * ww)
+    hw = p.lh * p.lw
+    tower = lambda blocks: sum(conv(c, hw) for blk in blocks for c in blk if c.get("wx") is not None)  # noqa: E731
+    x6 += tower(p.pred) + S * (tower(p.dyn) + tower(p.pred))
+    return x6, step_flops(p, H, W, S) - x6
+
+
+X6_PEAK_TFLOPS = 2500.0 / 6  # six bf16 MFMAs per f32-faithful product
+
+
+def parity_roofline(p, H, W, S, ms_per_step, B):
+    """Roofline of the f32 parity path's step: its x6 convs against the dense bf16 peak / 6, the rest against
+    the dense f32 MFMA peak; frac = the time both would take at their peaks / the measured time."""
+    fx6, frest = x6_flops(p, H, W, S)
+    ideal_ms = B * (fx6 / (X6_PEAK_TFLOPS * 1e12) + frest / (PEAK_F32_TFLOPS * 1e12)) * 1e3
+    return {"flop_x6_per_env_step": fx6, "flop_f32_per_env_step": frest, "peak_x6": X6_PEAK_TFLOPS,
+            "peak_f32": PEAK_F32_TFLOPS, "peak": B * (fx6 + frest) / (ideal_ms * 1e-3) / 1e12,
+            "ideal_ms_per_step": ideal_ms, "frac": ideal_ms / ms_per_step}
 
 
 def conv_flops(B, hw, C):
@@ -409,6 +457,7 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
     l32.search.noise_weight = loop.search.noise_weight
     l32.reset(0)
     fl = step_flops(ag32.packed, H, W, args.sims)
+    p32 = ag32.packed
     runs = {}
     for x6 in (True, False):
         for rn in (l32.ws.runner, l32.rep_runner):
@@ -433,14 +482,16 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
     cf, msf, vf = runs[False]
     same_f = (cf[-1] == counts[-1]).all(1)
     eps_f = B / (msf[-1] * 1e-3)
+    rl = parity_roofline(p32, H, W, args.sims, ms[-1], B)
     out = {"match": float(same.mean()),
            # beside the exact-match fraction: how far the count rows are apart, and whether the most visited
            # action (what temperature sampling mostly picks at low T) agrees
            "l1_mean": float(l1.mean()), "l1_max": int(l1.max()),
            "top_action_agreement": float((counts[-1].argmax(1) == c16.argmax(1)).mean()),
            "path": {"dtype": "f32 (latent convs as split-bf16 x6 products)", "value": eps, "unit": "env-steps/s",
-                    "ms_per_step": ms[-1], "achieved_tflops": eps * fl / 1e12, "peak": PEAK_F32_TFLOPS,
-                    "frac": eps * fl / 1e12 / PEAK_F32_TFLOPS,
+                    "ms_per_step": ms[-1], "achieved_tflops": eps * fl / 1e12,
+                    # the x6 convs against 2500 / 6 TF, the rest against 157.3 TF; `peak` = the blended ceiling
+                    "peak": rl["peak"], "frac": rl["frac"], "roofline": rl,
                     "deterministic": bool((counts[0] == counts[1]).all()),
                     "value_max_abs_diff_where_counts_agree": float(np.abs(v16 - v32)[same].max()) if same.any() else None,
                     "vs_f32_mfma_path": {"value": eps_f, "ms_per_step": msf[-1], "speedup": eps / eps_f,
@@ -612,10 +663,13 @@ def main():
     p = agent.packed
     fl = conv_flops(B, p.lh * p.lw, p.c1)
     achieved = fl / (conv_ms * 1e-3) / 1e12 if conv_ms else None
-    traffic, traffic_rec = tower_traffic(B, any(n > 1 for _, n in probe))
     kname = tower_kernel_name(B) if tower_launch_ms else None
+    traffic, traffic_rec = tower_traffic(B, any(n > 1 for _, n in probe), kname)
     ex_frac = EXECUTED_FRACTION.get(kname)
-    sq = tower_counters(B, kname) if kname else None
+    sq = tower_counters(B, kname, args.sims, args.dyn_dtype) if kname else None
+    # config 5: the fp16 dynamics step is its own instance (towerp_kernel<1>), counted separately
+    kname16 = tower_kernel_name(B, fp16=True) if (kname and args.dyn_dtype == "fp16") else None
+    sq16 = tower_counters(B, kname16, args.sims, args.dyn_dtype) if kname16 else None
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -638,8 +692,10 @@ def main():
                        "pow_threads": args.pow_threads,
                        "parallelism": f"env-sharded x{world}, RCCL gather of trajectory records to rank 0, target-net broadcast"},
             "roofline": {"bound": "mfma",
-                         "kernel": (f"{tower_kernel_name(B)} (fused dynamics / prediction step: 14-block residual "
-                                    "tower, bf16 3x3 256->256 convs, M=B*20, N=256, K=2304 each)") if tower_launch_ms else
+                         "kernel": (f"{kname} (fused dynamics / prediction step: 14-block residual "
+                                    "tower, bf16 3x3 256->256 convs, M=B*20, N=256, K=2304 each)"
+                                    + (f"; the dynamics step on {kname16} (fp16)" if kname16 else ""))
+                                   if tower_launch_ms else
                                    (f"latent residual conv bf16 3x3 256->256 (M=B*{p.lh * p.lw},N=256,K=2304; "
                                     f"{big_conv_kernel(args, B, p)} kernel)"),
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -661,6 +717,11 @@ def main():
                          "mfma_busy_clock_ghz": sq and sq.get("clock_ghz"),
                          "lds_bank_conflict_frac": sq and sq.get("lds_bank_conflict_frac"),
                          "counters_source": sq and sq.get("source"),
+                         "counters_kernel": sq and sq.get("kernel_name"),
+                         # config 5: the fp16 dynamics instance's own counters (not the bf16 record reused)
+                         "counters_dynamics_fp16": sq16 and {k: sq16.get(k) for k in (
+                             "kernel_name", "mfma_busy", "clock_ghz", "wait_inst", "duration_ns",
+                             "lds_bank_conflict_frac", "source")},
                          # below 16 x CUs envs a CU holds too few envs to hide its weight stream: the bound there
                          "l2_weight_stream": l2_weight_stream(conv_ms) if tower_launch_ms else None},
             "cpu_baseline": cpu_info,
@@ -682,9 +743,21 @@ def main():
                                     / (PEAK_BF16_TFLOPS * world),
             "flop_per_env_step": step_flops(agent.packed, H, W, args.sims),
         }
+        check_fracs(out)
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def check_fracs(out, path="bench"):
+    """Every roofline fraction in the line is measured against a true ceiling, so none may exceed 1: a value above
+    it means a wrong denominator, and the bench fails instead of printing it."""
+    if isinstance(out, dict):
+        for k, v in out.items():
+            if (k == "frac" or k.endswith("_frac")) and isinstance(v, (int, float)) and v > 1.0:
+                raise SystemExit(f"bench.py: {path}.{k} = {v:.4f} > 1 — a fraction of a peak above the peak is a "
+                                 "wrong denominator, not a result")
+            check_fracs(v, f"{path}.{k}")
 
 
 if __name__ == "__main__":

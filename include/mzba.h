@@ -105,8 +105,8 @@ int mzba_conv2d(int dtype, const void* in, long long in_env_stride, const int32_
  * [Cout][3][3][Cin] weights: wh[Cout/16][9*Cin/32][64][8], wh[ct][s][l][j] = W[16 ct + l % 16][32 s + 8 (l / 16) + j]
  * with the K index tap * Cin + channel. Supported: Cin 128 / 256, Cout % 256 == 0, or Cout 128 with all Cin channels
  * staged at once (the policy head's conv, networks.py:200-206; the 84x84 128-channel blocks), the staged halo within
- * the LDS in one block or, at Cin 256, two 128-channel blocks (W <= 30 / 156: one block at Cin 256 / 128; two
- * blocks up to W = 156) (mzba_conv_halo_supported). Replaces
+ * the LDS (with its 16-row zero block) in one block or, at Cin 256, two 128-channel blocks (W <= 23 / 183: one
+ * block at Cin 256 / 128; two blocks up to W = 183) (mzba_conv_halo_supported). Replaces
  * networks.py:19-35 ResidualBlock convs (the second with res). */
 int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks);
 /* mzba_conv_halo with a gathered input and the action planes folded into a bias table (the dynamics' first conv,
@@ -114,7 +114,7 @@ int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks);
  * in + b env_stride + slot[b] slot_stride elements (slot optional), out = act(conv3x3 + act_bias[p][act[b]][n] +
  * bias[n] (+ res)), ((acc + act_bias) + bias) in f32 as conv_igemm; act_bias [H W][A][Cout] f32 excludes res.
  * gather = 1 in the support check: a strided / gathered input or an action-bias table (Cin 256, Cout % 256 == 0,
- * 256 + 2 (W + 1) <= H W: a workgroup's staged rows within two envs). */
+ * one staged 256-channel block, i.e. W <= 23; 256 + 2 (W + 1) <= H W: a workgroup's staged rows within two envs). */
 int mzba_conv_halo_ex_supported(int H, int W, int Cin, int Cout, int ks, int gather);
 int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wh,
                       const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,

@@ -8,6 +8,17 @@
 
 #define MZ_DEV __device__ __forceinline__
 
+// hipFuncAttributeMaxDynamicSharedMemorySize for a kernel, set once per kernel pointer (a launch helper
+// shared by several template instances must not key the one-time flag on the helper: ADVICE r4)
+#include <mutex>
+#include <set>
+inline void mz_set_lds_max_once(const void* kern, int bytes) {
+  static std::mutex mu;
+  static std::set<const void*> done;
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.insert(kern).second) (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
 // ------------------------------------------------------------------ error plumbing
 // Every C-ABI entry point returns 0 on success, a negative code on a bad argument,
 // or the positive hipError_t of the failing launch.

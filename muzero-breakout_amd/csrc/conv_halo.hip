@@ -7,8 +7,9 @@
 // A workgroup (8 waves) owns TM = 256 consecutive output pixels x 256 output
 // channels. A 3x3 tap shifts the flattened pixel index by dy W + dx, so every tap of the tile reads rows of ONE
 // staged range: the tile's pixels plus a halo of W + 1 rows on each side (HR = 256 + 2 W + 2 pixel rows). That
-// range is staged into LDS once, all Cin (128 or 256) channels (supported while HR x 2 Cin B fits the 160 KiB:
-// W <= 30 at Cin 256, W <= 156 at Cin 128; past W = 30 at Cin 256 in two 128-channel blocks) with LDS-DMA (global_load_lds_dwordx4, no VGPR round trip), and the 9 taps
+// range is staged into LDS once, all Cin (128 or 256) channels (supported while HR x 2 Cin B plus the 16-row zero
+// block fits the 160 KiB: W <= 23 at Cin 256, W <= 183 at Cin 128; past W = 23 at Cin 256 in two 128-channel
+// blocks, up to W = 183; halo_geometry) with LDS-DMA (global_load_lds_dwordx4, no VGPR round trip), and the 9 taps
 // x the block's channel steps run from it — the activation operand is fetched from L2 once per tile, not once
 // per tap as an im2col GEMM tile fetches it (conv_big_bf16_kernel: 9 x the activation traffic and its LDS
 // writes every K step).

@@ -482,11 +482,7 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
     const int ldsp = ap.ZOFF + 3 * Cin * 2;
     const dim3 gridp((unsigned)((M + tmp - 1) / tmp), (unsigned)(Cout / x6::TN));
     auto launchp = [&](auto kern) {
-      static bool attr = false;
-      if (!attr) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, x6::LDS_MAX);
-        attr = true;
-      }
+      mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
       hipLaunchKernelGGL(kern, gridp, dim3(x6::NT), ldsp, stream, ap);
     };
     if (Cin == 256) {
@@ -515,11 +511,7 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
   const int lds = a.ZOFF + 16 * Cin * 4;
   const dim3 grid((unsigned)((M + tm - 1) / tm), (unsigned)(Cout / x6::TN));
   auto launch = [&](auto kern) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, x6::LDS_MAX);
-      attr = true;
-    }
+    mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
     hipLaunchKernelGGL(kern, grid, dim3(x6::NT), lds, stream, a);
   };
   if (Cin == 256)

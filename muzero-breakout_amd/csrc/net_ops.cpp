@@ -131,6 +131,22 @@ struct NetPack : torch::CustomClassHolder {
   bool fused_ok() const { return tower_ok() && has("fused.w0"); }
 
   c10::intrusive_ptr<struct NetRunner> runner(int64_t B, int64_t H, int64_t W);
+
+  // the last strong reference is gone: drop the runners (each holds a weak reference back to this pack, so
+  // keeping them would keep the weak count above zero and the pack, its device weights and every runner's
+  // batch-sized scratch alive forever) and the weight tensors (a runner handle still held by Python keeps
+  // only this emptied object alive; its ops raise through pin())
+  void release_resources() override {
+    std::map<std::tuple<int64_t, int64_t, int64_t>, c10::intrusive_ptr<struct NetRunner>> dead;
+    {
+      std::lock_guard<std::mutex> lk(runners_mu);
+      dead.swap(runners);
+    }
+    dead.clear();
+    convs.clear();
+    lins.clear();
+    tens.clear();
+  }
 };
 
 // ---- launch sequences per batch ----------------------------------------------------------------

@@ -37,7 +37,8 @@ def save_checkpoint(path, agent, replay=None, training_iteration=0, acting_step=
                     optimizer_state=None, learner=None):
     """train_torch.py:612-637. The optimizer state is, in order of preference: `optimizer_state`,
     `learner.optimizer_state_dict()`, a fresh Adam state for the agent's parameters."""
-    sd = {k: torch.from_numpy(np.array(v, copy=True)) for k, v in agent.state_dict().items()}  # keeps 0-d shapes
+    sd = {k: (v.detach().clone() if torch.is_tensor(v) else torch.from_numpy(np.array(v, copy=True)))
+          for k, v in agent.state_dict().items()}  # own copies; keeps 0-d shapes
     if optimizer_state is None:
         optimizer_state = learner.optimizer_state_dict() if learner is not None else fresh_optimizer_state(agent.cfg)
     torch.save({

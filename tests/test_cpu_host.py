@@ -220,3 +220,14 @@ def test_conv_halo_support_matrix_and_bad_arguments_without_gpu():
                                None) == -2
     assert L.mzba_conv_halo_ex(p, 21 * 21 * 64, None, 0, p, p, None, None, 0, None, p, 4, 21, 21, 64, 256, 1, None) == -2
     assert L.mzba_conv_halo(p, p, p, None, p, 4, 42, 42, 256, 128, 1, None) == -2
+    # the one-block bounds halo_geometry computes with the 16-row zero block: at Cin 256 one
+    # 256-channel block up to W = 23 (so the gathered GA instance, which needs it, up to W = 23; past it the
+    # plain conv stages two 128-channel blocks); at Cin 128 one block up to W = 183, and nothing past it
+    assert L.mzba_conv_halo_ex_supported(23, 23, 256, 256, 3, 1) == 1
+    assert L.mzba_conv_halo_ex_supported(24, 24, 256, 256, 3, 1) == 0
+    assert L.mzba_conv_halo_supported(24, 24, 256, 256, 3) == 1
+    assert L.mzba_conv_halo_supported(24, 24, 256, 128, 3) == 0  # Cout 128 needs one staged block
+    assert L.mzba_conv_halo_supported(8, 183, 128, 128, 3) == 1
+    assert L.mzba_conv_halo_supported(8, 184, 128, 128, 3) == 0
+    assert L.mzba_conv_halo_supported(8, 183, 256, 256, 3) == 1
+    assert L.mzba_conv_halo_supported(8, 184, 256, 256, 3) == 0

@@ -110,6 +110,50 @@ def test_config4_bf16_fused_shards_equal_global_loop():
     assert (full["counts"].sum(-1) == 50).all()
 
 
+def test_config4_32768_global_loop_equals_eight_4096_shards():
+    """BASELINE config 4's own workload on one GPU (train_torch.py:160-233 as each of its 8 ranks runs it):
+    one 32 768-env acting loop on the full-width bf16 fused path (towerp_kernel, HIP-graph replay, T = 0.9,
+    pow_threads = 4) against the same steps as 8 shards x 4 096 envs (env_offset = r * 4096, n_envs_total =
+    32 768, each the headline's per-GPU loop), run one after the other on cuda:0. Every record — sampled
+    actions, visit counts, root values, rewards, masks, frames — is equal bit for bit. At this size the
+    sampling's 3 x 32 768 = 98 304 flat counts cross torch's threaded-pow split (>= 32 768 elements with 4
+    intra-op threads): each shard's pow lanes follow its envs' global positions. The global loop's node pool
+    alone is 17 GB (32 768 x 51 latents), its representation activations 16 GB: 64-bit offsets everywhere."""
+    from mzba import _lib as L
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingLoop
+    cfg = default_config()
+    cfg["num_simulations"] = 50
+    sd = init_state_dict(cfg["model"], 12)
+    ag = MuZeroAgent(cfg["model"], dtype="bf16")
+    ag.load_state_dict(sd)
+    T, NT, G = 3, 32768, 8
+
+    def run(B, off):
+        loop = ActingLoop(cfg, ag, B, seed=41, env_offset=off, max_steps=T, n_envs_total=NT, temperature=0.9,
+                          pow_threads=4)
+        assert loop.ws.runner.fused_ok() and loop.ws.runner.tower_plan == 4 == L.lib().mzba_tower_plan(B)
+        loop.reset(0)
+        loop.act(eager=True)
+        loop.capture()
+        for _ in range(T - 1):
+            loop.act()
+        out = _records(loop, T)
+        del loop
+        torch.cuda.empty_cache()
+        return out
+
+    full = run(NT, 0)
+    B = NT // G
+    for r in range(G):
+        part = run(B, r * B)
+        for k in full:
+            np.testing.assert_array_equal(part[k], full[k][:, r * B:(r + 1) * B], err_msg=f"shard {r}: {k}")
+    assert (full["counts"].sum(-1) == 50).all()
+    # the episode is live (not all done) and the sampling saw T < 1 over both pow lane kinds
+    assert full["mask"].any()
+
+
 def _stage_cfg():
     cfg = default_config()
     cfg["model"] = small_model_cfg(cfg)
