@@ -124,13 +124,27 @@ int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot,
  * taken as the six terms down to 2^-18 (csrc/conv_x6.hip), as close to exact as an f32 conv. wx = the three
  * parts of the f32 [Cout][3][3][Cin] weights (hi = bf16(w), mid = bf16(w - hi), lo = bf16(w - hi - mid)), each
  * in mzba_conv_halo's pack_lat16 packing, back to back. Supported: Cin 128 / 256, Cout % 256 == 0, the staged
- * halo within the LDS (mzba_conv_x6_supported). */
+ * halo within the LDS; and the 4x5 latent at Cin 256 with Cout 256 or 128 (the pixel-tiled form, round 5: 16 envs
+ * x 20 pixels per workgroup, the zero-padding taps not issued) (mzba_conv_x6_supported). */
 int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks);
 int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
                  int Cin, int Cout, int relu, hipStream_t stream);
-/* 1 (default): the pre-split form where its staged rows fit (the f32 activations split once into bf16 hi / mid /
- * lo planes while staging, 1.5x the f32 row; 8 waves x 32 channels); 0: the per-read-split kernel only (A/B; it
- * remains the form for halos too large for the planes). Same sums in the same order: bit-identical outputs. */
+/* mzba_conv_x6 with a gathered input and the action planes folded into a bias table (the f32 dynamics' first conv,
+ * networks.py:117-122, 160; the contract of mzba_conv_halo_ex): env b's image at in + b env_stride + slot[b]
+ * slot_stride elements (slot optional), out = act(conv3x3 + act_bias[p][act[b]][n] + bias[n] (+ res)),
+ * ((acc + act_bias) + bias) in f32 as conv_igemm; act_bias [H W][A][Cout] f32 excludes res. gather = 1 in the
+ * support check: a strided / gathered input or an action-bias table (the pixel-tiled form only: the 4x5 latent,
+ * Cin 256, Cout 256 / 128). */
+int mzba_conv_x6_ex_supported(int H, int W, int Cin, int Cout, int ks, int gather);
+int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx,
+                    const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,
+                    int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream);
+/* 2 (default): the pixel-tiled form at the 4x5 latent where its 16-env workgroups load the busiest CU less than the
+ * pre-split tiles (the gathered / Cout 128 convs always), else the pre-split form where its staged rows fit (the f32
+ * activations split once into bf16 hi / mid / lo planes while staging, 1.5x the f32 row; 8 waves x 32 channels),
+ * else the per-read-split kernel; 3: the pixel-tiled form wherever it applies; 1: no pixel-tiled form (A/B);
+ * 0: the per-read-split kernel only (A/B). The pre-split and per-read-split forms are bit-identical (same sums in
+ * the same order); the pixel-tiled form sums the same products in another order (channel block, tap). */
 int mzba_conv_x6_set_variant(int v);
 int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
                    int Cin, int Cout, int relu, hipStream_t stream);

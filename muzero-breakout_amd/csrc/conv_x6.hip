@@ -18,6 +18,7 @@
 // operand, read as f32 from LDS and split in registers per fragment (each split feeds 4 column tiles x 6
 // MFMAs). Epilogue in f32: + bias (+ residual), ReLU.
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
@@ -413,7 +414,247 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
   }
 }
 
-static int g_x6_presplit = 1;  // A/B: 1 the pre-split form where it fits, 0 conv_x6_kernel only
+// Pixel-tiled form for the 4x5 latent at full batches (round 5; conv_x6t): a workgroup owns 16 whole envs, all
+// 20 pixels, and an MFMA column tile is ONE pixel of those 16 envs (towerp.hip's tiling), so a 3x3 tap maps pixel
+// tile p onto pixel tile p + dy W + dx whole and the 50 of 180 tile-taps that fall on the zero padding
+// (Conv2d(padding=1) on the 4x5 latent) are not issued: 0.72 of conv_x6p's MFMAs, where every 16-pixel tile
+// runs all 9 taps (the zero block for the out-of-image rows). 16 envs x 20 pixels x 256 channels as three bf16
+// planes are 480 KiB, so the input channels are staged in 8 blocks of 32: the next block's f32 rows come in by
+// LDS-DMA (40 KiB, issued when the previous split ends) while the current block's k steps run; at a block end
+// the raw rows are split once into the hi / mid / lo planes (3 x 20 KiB; row (pixel p, env e) = 16 p + e,
+// 64 B per plane row, chunk q ^ key(e): any 16 rows of a tile conflict-free, tools/swizzle search). 8 waves, each
+// 16 output channels x all 20 pixel tiles (acc 20, pinned to AGPRs), so a workgroup owns 128 output channels
+// (grid.y = Cout / 128; 32 channels per wave need 160 accumulators beside the ring: 300 VGPRs spilled at two waves
+// per SIMD, and one wave per SIMD would need 320 accumulators for all 256); weights from the 'wx' pack through
+// a two-step register ring, k step j = (block b, tap t) -> pack step 8 t + b. Per accumulator the order is
+// (channel block, tap, the six terms small first): the same products as conv_x6p in another order, so the two
+// agree to f32 rounding (both as close to exact as an f32 conv), not bit for bit.
+// GA: the input gathered per env from the latent pool (in + b env_stride + slot[b] slot_stride) and the
+// action-bias table added ((acc + act_bias) + bias, conv_igemm's order): the f32 dynamics' first conv.
+namespace x6t {
+constexpr int E = 16, HW = 20, H = 4, W = 5, CIN = 256, NCS = 8, KS = 72;
+constexpr int ROWS = HW * E;          // 320 staged rows (pixel, env)
+constexpr int PB = ROWS * 64;         // bytes per bf16 plane of a 32-channel block
+constexpr int RAW = 3 * PB;           // f32 rows of the next block: 320 x 128 B
+constexpr int LDS = RAW + ROWS * 128;  // 100 KiB
+}  // namespace x6t
+
+// the (tap, output pixel) pairs of a 3x3 conv on the 4x5 latent whose source pixel is in the image: 130 of 180
+struct X6TPairs {
+  int n = 0;
+  int tap[180] = {}, out[180] = {}, src[180] = {};
+  bool last[180] = {};  // the tap's last pair
+};
+constexpr X6TPairs make_x6t_pairs() {
+  X6TPairs r{};
+  for (int t = 0; t < 9; ++t) {
+    const int dy = t / 3 - 1, dx = t % 3 - 1;
+    for (int p = 0; p < x6t::HW; ++p) {
+      const int y = p / x6t::W + dy, x = p % x6t::W + dx;
+      if (y < 0 || y >= x6t::H || x < 0 || x >= x6t::W) continue;
+      r.tap[r.n] = t, r.out[r.n] = p, r.src[r.n] = y * x6t::W + x;
+      ++r.n;
+    }
+    r.last[r.n - 1] = true;
+  }
+  return r;
+}
+constexpr X6TPairs kPairs = make_x6t_pairs();
+static_assert(kPairs.n == 130, "130 of the 180 tile-taps of a 4x5 latent are in the image");
+
+struct X6TArgs {
+  const float* in;
+  long long env_stride;   // elements between envs (contiguous: 20 x 256)
+  const int32_t* slot;    // optional: env b's image at in + b env_stride + slot[b] slot_stride
+  long long slot_stride;
+  const bf16_t* wx;       // [3 parts][Cout / 16][72][64][8]
+  const float* bias;      // [Cout]
+  const float* act_bias;  // optional [20][A][Cout] (GA)
+  const int32_t* act;     // [B] (GA)
+  int A;
+  const float* res;       // optional [B][20][Cout]
+  float* out;             // [B][20][Cout]
+  int B, Cout, relu;
+  long long part;         // elements per weight part
+};
+
+MZ_DEV int tkey(int e) { return (e >> 2) & 2; }  // chunk swizzle of row 16 p + e (64-B plane rows)
+
+template <bool GA>
+__global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
+  using namespace x6t;
+  constexpr int CT = 1;  // 16 output channels per wave, 128 per workgroup (CT 2 needs 160 accumulators: spilled)
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, n = lane & 15;
+  const int e0 = blockIdx.x * E;
+  const int nb = blockIdx.y * 128 + wave * 16 * CT;  // the wave's first output channel
+
+  // LDS-DMA of block cb's f32 rows: 1-KiB piece i = rows 8 i .. 8 i + 7 = pixel i >> 1, envs 8 (i & 1) + 0..7; the
+  // waves take pieces wave + 8 k, so a lane's env (8 (wave & 1) + lane / 8) is fixed: its offset is read once
+  const int se = min(e0 + 8 * (wave & 1) + (lane >> 3), a.B - 1);
+  long long eoff = (long long)se * a.env_stride;
+  if (GA && a.slot) eoff += (long long)a.slot[se] * a.slot_stride;
+  const float* src0 = a.in + eoff + (lane & 7) * 4;
+  auto stage = [&](int cb) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int i = wave + 8 * k;
+      __builtin_amdgcn_global_load_lds(src0 + (size_t)(i >> 1) * CIN + cb * 32, lds + RAW + i * 1024, 16, 0, 0);
+    }
+  };
+  // split of the raw block into the three planes: item g = (row, 8-channel chunk)
+  auto split = [&]() {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int g = tid + u * x6::NT;
+      if (g < ROWS * 4) {
+        const int r = g >> 2, k8 = g & 3;
+        const uint4 u0 = *reinterpret_cast<const uint4*>(lds + RAW + r * 128 + k8 * 32);
+        const uint4 u1 = *reinterpret_cast<const uint4*>(lds + RAW + r * 128 + k8 * 32 + 16);
+        bf16x8 h, m, l;
+        split8(u0, u1, h, m, l);
+        uint8_t* row = lds + r * 64 + ((k8 ^ tkey(r & 15)) << 4);
+        *reinterpret_cast<bf16x8*>(row) = h;
+        *reinterpret_cast<bf16x8*>(row + PB) = m;
+        *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+      }
+    }
+  };
+
+  // weight ring: step j = 9 b + t reads pack step 8 t + b; slot j & 1
+  const uint4* wbase = reinterpret_cast<const uint4*>(a.wx) + (size_t)(nb / 16) * KS * 64;
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wbase), 0, 0x7fffffff, 0x00020000);
+  const int pstride = (int)(a.part * 2);
+  auto wload = [&](int ct, int part, int j) {
+    j = j < KS ? j : KS - 1;
+    const int s = (j % 9) * 8 + j / 9;
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + (ct * KS + s) * 1024, 0));
+  };
+  bf16x8 bq[2][3][CT];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) bq[cc][pt][ct] = wload(ct, pt, cc);
+
+  f32x4 acc[HW][CT];
+#pragma unroll
+  for (int p = 0; p < HW; ++p)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      acc[p][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "+a"(acc[p][ct]));
+    }
+
+  stage(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  split();
+  __syncthreads();
+  stage(1);
+
+  // the lane's B fragment of source pixel ps: row 16 ps + n, chunk q of each plane
+  const int lrow = n * 64 + ((q ^ tkey(n)) << 4);
+  auto frag = [&](int ps, bf16x8 (&f)[3]) {
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt) f[pt] = *reinterpret_cast<const bf16x8*>(lds + pt * PB + ps * 1024 + lrow);
+  };
+
+  // one 32-channel block: the (tap, output pixel) pairs whose source pixel is in the image (x6t::PAIRS, tap-major),
+  // fragment i + 1 read during pair i's MFMAs; after a tap's last pair its ring slot is reloaded (step j + 2)
+  auto block = [&](int b, auto par) {
+    constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (9 b + t)
+    bf16x8 fr[2][3];
+    frag(kPairs.src[0], fr[0]);
+#pragma unroll
+    for (int i = 0; i < kPairs.n; ++i) {
+      const int t = kPairs.tap[i], p = kPairs.out[i], sl = (P0 + t) & 1, cur = i & 1;
+      if (i + 1 < kPairs.n) frag(kPairs.src[i + 1], fr[cur ^ 1]);
+      const bf16x8* xs[6] = {&fr[cur][0], &fr[cur][1], &fr[cur][2], &fr[cur][0], &fr[cur][1], &fr[cur][0]};
+      constexpr int wp[6] = {2, 1, 0, 1, 0, 0};  // per accumulator the small terms first (conv_x6p's order)
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct)
+          acc[p][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][wp[k]][ct], *xs[k], acc[p][ct], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 6 * CT, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kPairs.last[i]) {
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) bq[sl][pt][ct] = wload(ct, pt, 9 * b + t + 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  for (int b = 0; b < NCS; b += 2) {
+    block(b, std::integral_constant<int, 0>());  // 9 b even
+    // block b + 1's raw rows: wait for this wave's LDS-DMA (older than every ring load of block b: all but the
+    // youngest 2 steps of ring loads may be waited on), then every wave's, then split
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * CT) : "memory");
+    __syncthreads();
+    split();
+    __syncthreads();
+    if (b + 2 < NCS) stage(b + 2);
+    block(b + 1, std::integral_constant<int, 1>());  // 9 (b + 1) odd
+    if (b + 2 < NCS) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * CT) : "memory");
+      __syncthreads();
+      split();
+      __syncthreads();
+      if (b + 3 < NCS) stage(b + 3);
+    }
+  }
+
+  // epilogue (f32): acc[p][ct] = D[channel nb + 16 ct + 4 q + i][env e0 + n at pixel p]
+  const int env = e0 + n;
+  if (env >= a.B) return;
+  const float lo = a.relu ? 0.f : -__builtin_inff();
+  float4 bb[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
+  const int act = GA && a.act_bias ? a.act[env] : 0;
+  const size_t ob = (size_t)env * HW * a.Cout;
+#pragma unroll
+  for (int p = 0; p < HW; ++p) {
+    float4 rv[CT];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int ch = nb + ct * 16 + 4 * q;
+      if (GA && a.act_bias)
+        rv[ct] = *reinterpret_cast<const float4*>(a.act_bias + ((size_t)p * a.A + act) * a.Cout + ch);
+      else
+        rv[ct] = a.res ? *reinterpret_cast<const float4*>(a.res + ob + (size_t)p * a.Cout + ch)
+                       : make_float4(-0.f, -0.f, -0.f, -0.f);
+    }
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      float4 o;
+      if (GA && a.act_bias) {  // (acc + act_bias) + bias
+        o.x = fmaxf((acc[p][ct][0] + rv[ct].x) + bb[ct].x, lo);
+        o.y = fmaxf((acc[p][ct][1] + rv[ct].y) + bb[ct].y, lo);
+        o.z = fmaxf((acc[p][ct][2] + rv[ct].z) + bb[ct].z, lo);
+        o.w = fmaxf((acc[p][ct][3] + rv[ct].w) + bb[ct].w, lo);
+      } else {  // (acc + bias) + res
+        o.x = fmaxf((acc[p][ct][0] + bb[ct].x) + rv[ct].x, lo);
+        o.y = fmaxf((acc[p][ct][1] + bb[ct].y) + rv[ct].y, lo);
+        o.z = fmaxf((acc[p][ct][2] + bb[ct].z) + rv[ct].z, lo);
+        o.w = fmaxf((acc[p][ct][3] + bb[ct].w) + rv[ct].w, lo);
+      }
+      *reinterpret_cast<float4*>(a.out + ob + (size_t)p * a.Cout + nb + ct * 16 + 4 * q) = o;
+    }
+  }
+}
+
+// A/B: 0 conv_x6_kernel only, 1 + the pre-split form where it fits, 2 (default) + the pixel-tiled form where it
+// loads the busiest CU less than the pre-split one, 3 the pixel-tiled form wherever it applies
+static int g_x6_variant = 2;
 
 int x6p_ncu() {
   static int ncu = 0;
@@ -456,13 +697,58 @@ int x6_geometry(int W, int Cin, X6Args& g) {
   return 0;
 }
 
+int x6_halo_launch(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
+                   int Cin, int Cout, int relu, hipStream_t stream);
+
 }  // namespace
 
 extern "C" {
 
 int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks) {
   X6Args g{};
+  if (ks == 3 && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128)) return 1;  // conv_x6t
   return ks == 3 && H >= 2 && W >= 2 && Cout % 256 == 0 && x6_geometry(W, Cin, g) > 0 ? 1 : 0;
+}
+
+// gather = 1: a slot-gathered / strided input and / or an action-bias table (conv_x6t's GA instance: the 4x5
+// latent, Cin 256, Cout 256 / 128)
+int mzba_conv_x6_ex_supported(int H, int W, int Cin, int Cout, int ks, int gather) {
+  if (ks == 3 && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128)) return 1;
+  return gather ? 0 : mzba_conv_x6_supported(H, W, Cin, Cout, ks);
+}
+
+int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx,
+                    const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,
+                    int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream) {
+  MZ_CHECK_ARG(in && wx && bias && out && B > 0, -1);
+  MZ_CHECK_ARG(!act_bias || (act && A > 0 && !res), -1);
+  const bool ga = slot || act_bias || env_stride != (long long)H * W * Cin;
+  MZ_CHECK_ARG(mzba_conv_x6_ex_supported(H, W, Cin, Cout, 3, ga ? 1 : 0), -2);
+  const long long M = (long long)B * H * W;
+  MZ_CHECK_ARG(M + 256 < (1LL << 31), -3);
+  bool tiled = H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128);
+  if (tiled && !ga && Cout % 256 == 0 && g_x6_variant < 3) {
+    // the pixel tiles where they load the busiest CU less (pixel-taps issued per CU) than conv_x6p's tiles
+    X6Args ap{};
+    const int tmp = g_x6_variant >= 1 ? x6p_geometry(W, Cin, M, ap) : 0;
+    const long long ncu = x6p_ncu(), t16 = (B + x6t::E - 1) / x6t::E;
+    const long long load_t = (2 * t16 + ncu - 1) / ncu * x6t::E * kPairs.n / 2;  // two 128-channel halves
+    const long long load_p = tmp ? ((M + tmp - 1) / tmp + ncu - 1) / ncu * tmp * 9 : load_t + 1;
+    tiled = g_x6_variant == 2 && load_t < load_p;
+  }
+  if (tiled) {
+    X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx, bias, act_bias, act, A,
+              (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * 9 * Cin};
+    const dim3 grid((unsigned)((B + x6t::E - 1) / x6t::E), (unsigned)(Cout / 128));
+    auto launch = [&](auto kern) {
+      mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
+      hipLaunchKernelGGL(kern, grid, dim3(x6::NT), x6t::LDS, stream, t);
+    };
+    ga ? launch(conv_x6t_kernel<true>) : launch(conv_x6t_kernel<false>);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  }
+  return x6_halo_launch(in, wx, bias, res, out, B, H, W, Cin, Cout, relu, stream);
 }
 
 // out = act(conv3x3(in) + bias (+ res)) in f32 on contiguous NHWC images of B envs, every product as the
@@ -470,14 +756,24 @@ int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks) {
 // pack_lat16 packing, back to back (agent.py PackedNets._conv "wx").
 int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
                  int Cin, int Cout, int relu, hipStream_t stream) {
-  MZ_CHECK_ARG(in && wx && bias && out && B > 0, -1);
-  MZ_CHECK_ARG(mzba_conv_x6_supported(H, W, Cin, Cout, 3), -2);
+  return mzba_conv_x6_ex(in, (long long)H * W * Cin, nullptr, 0, wx, bias, nullptr, nullptr, 0, res, out, B, H, W, Cin,
+                         Cout, relu, stream);
+}
+
+}  // extern "C"
+
+namespace {
+// the halo-staged forms (conv_x6p_kernel, else conv_x6_kernel) on contiguous images, Cout % 256 == 0
+int x6_halo_launch(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
+                   int Cin, int Cout, int relu, hipStream_t stream) {
+  X6Args g0{};
+  MZ_CHECK_ARG(Cout % 256 == 0 && H >= 2 && W >= 2 && x6_geometry(W, Cin, g0) > 0, -2);
   const long long M = (long long)B * H * W;
   MZ_CHECK_ARG(M + 256 < (1LL << 31), -3);  // pixel indices in int (global offsets are size_t)
   X6Args a{(const float*)in, (const bf16_t*)wx, bias, (const float*)res, (float*)out, (int)M, H, W, Cin, Cout, relu};
   a.part = (long long)Cout * 9 * Cin;
   X6Args ap = a;
-  const int tmp = g_x6_presplit ? x6p_geometry(W, Cin, M, ap) : 0;
+  const int tmp = g_x6_variant >= 1 ? x6p_geometry(W, Cin, M, ap) : 0;
   if (tmp == 128 || tmp == 112 || tmp == 96 || tmp == 80 || tmp == 64 || tmp == 48) {
     const int ldsp = ap.ZOFF + 3 * Cin * 2;
     const dim3 gridp((unsigned)((M + tmp - 1) / tmp), (unsigned)(Cout / x6::TN));
@@ -521,10 +817,13 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
   MZ_LAUNCH_CHECK();
   return 0;
 }
+}  // namespace
+
+extern "C" {
 
 int mzba_conv_x6_set_variant(int v) {
-  if (v != 0 && v != 1) return -1;
-  g_x6_presplit = v;
+  if (v < 0 || v > 3) return -1;
+  g_x6_variant = v;
   return 0;
 }
 

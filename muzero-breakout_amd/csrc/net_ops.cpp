@@ -226,17 +226,19 @@ struct NetRunner : torch::CustomClassHolder {
             const int32_t* act = nullptr) {
     env_stride = env_stride < 0 ? H_ * W_ * l.cin : env_stride;
     const bool ab = l.act_bias.defined();
-    // the f32 parity path's 3x3 convs: f32-faithful split-bf16 products (conv_x6)
-    if (l.wx.defined() && use_x6 && p->dtype == 0 && !slot && env_stride == H_ * W_ * l.cin && !ab &&
-        mzba_conv_x6_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks)) {
-      check_rc(mzba_conv_x6(in, vp(l.wx), vp<float>(l.b), res, out, (int)B, (int)H_, (int)W_, (int)l.cin, (int)l.cout,
-                            relu, s),
-               "mzba_conv_x6");
+    const int gather = (slot || ab || env_stride != H_ * W_ * l.cin) ? 1 : 0;
+    // the f32 parity path's 3x3 convs: f32-faithful split-bf16 products (conv_x6; at the 4x5 latent the pixel-tiled
+    // form, which also takes the dynamics' first conv off the latent pool + its action-bias table)
+    if (l.wx.defined() && use_x6 && p->dtype == 0 && !(ab && res) &&
+        mzba_conv_x6_ex_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks, gather)) {
+      check_rc(mzba_conv_x6_ex(in, env_stride, slot, slot_stride, vp(l.wx), vp<float>(l.b),
+                               ab ? vp<float>(l.act_bias) : nullptr, ab ? act : nullptr, (int)l.A, res, out, (int)B,
+                               (int)H_, (int)W_, (int)l.cin, (int)l.cout, relu, s),
+               "mzba_conv_x6_ex");
       return;
     }
     // large images (config 3: 21x21 latents, the 84x84 128 -> 256 conv; with gather the dynamics' first conv off
     // the latent pool + its action-bias table): the halo-tiled kernel
-    const int gather = (slot || ab || env_stride != H_ * W_ * l.cin) ? 1 : 0;
     if (l.wh.defined() && use_halo && !(ab && res) &&
         mzba_conv_halo_ex_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks, gather)) {
       check_rc(mzba_conv_halo_ex(in, env_stride, slot, slot_stride, vp(l.wh), vp<float>(l.b),

@@ -364,8 +364,10 @@ class PackedNets:
             # of [Cout][tap][Cin]
             layer["wh"] = torch.tensor(pack_lat16(wp.reshape(cout, -1), cout, k, cin_p),
                                        dtype=torch.float32).to(self.tdt).to(self.device)
-        if (hw is not None and self.dtype == "f32" and act_w is None
-                and L.lib().mzba_conv_x6_supported(hw[0], hw[1], cin_p, cout, k)):
+        if (hw is not None and self.dtype == "f32"
+                and L.lib().mzba_conv_x6_ex_supported(hw[0], hw[1], cin_p, cout, k, int(act_w is not None))):
+            # the f32 parity path's 3x3 convs as split-bf16 x6 products (round 5: the 4x5 latent's dynamics first
+            # conv with its slot gather + action-bias table, and the policy head's 256 -> 128 conv, too)
             layer["wx"] = split_pack_x6(wp, cout, k, cin_p).to(self.device)
         if band and self.dtype == "bf16" and k == 3 and L.lib().mzba_conv_band_supported(16, 20, cin, cout, 3):
             # representation convs at full resolution: the band kernel's packing (tower order)

@@ -206,8 +206,12 @@ def test_rep_input_builder(L, steps, single_write):
 
 
 # ------------------------------------------------------------------------------ nets
-@pytest.mark.parametrize("tag", ["small", "full"])
-def test_nets_f32_match_reference(tag):
+@pytest.mark.parametrize("tag,x6", [("small", 2), ("full", 2), ("full", 3)])
+def test_nets_f32_match_reference(tag, x6):
+    """The f32 parity path's nets on the reference's own outputs (nets_*.npz) within 1e-5. x6 = 3: every 4x5 latent
+    3x3 conv on the pixel-tiled x6 form (the form the 4096-env parity path runs: the towers, the dynamics' first
+    conv with its gather + action bias, the policy head's conv); 2: the form chosen by batch (pre-split here)."""
+    from mzba import _lib as L
     from mzba.agent import MuZeroAgent
     d = np.load(os.path.join(GOLDEN, f"nets_{tag}.npz"))
     cfg = default_config()
@@ -215,15 +219,23 @@ def test_nets_f32_match_reference(tag):
     ag = MuZeroAgent(mcfg, dtype="f32")
     ag.load_state_dict(init_state_dict(mcfg, int(d["weight_seed"])))
     tol = dict(rtol=1e-5, atol=1e-5)  # north_star: within 1e-5 for network logits/values
-    h = ag.create_hidden_state_root(dev(d["x"])).cpu().numpy()
-    np.testing.assert_allclose(h, d["h"], **tol)
-    pl, vl = ag.evaluate_state(dev(d["h"]))
-    np.testing.assert_allclose(pl.cpu().numpy(), d["p0"], **tol)
-    np.testing.assert_allclose(vl.cpu().numpy(), d["v0"], **tol)
-    planes = N.encode_action_planes(d["action"], mcfg["latent_resolution"])
-    h1, rl = ag.hidden_state_transition(dev(d["h"]), dev(planes))
-    np.testing.assert_allclose(h1.cpu().numpy(), d["h1"], **tol)
-    np.testing.assert_allclose(rl.cpu().numpy(), d["r1"], **tol)
+    try:
+        assert L.lib().mzba_conv_x6_set_variant(x6) == 0
+        h = ag.create_hidden_state_root(dev(d["x"])).cpu().numpy()
+        np.testing.assert_allclose(h, d["h"], **tol)
+        pl, vl = ag.evaluate_state(dev(d["h"]))
+        np.testing.assert_allclose(pl.cpu().numpy(), d["p0"], **tol)
+        np.testing.assert_allclose(vl.cpu().numpy(), d["v0"], **tol)
+        planes = N.encode_action_planes(d["action"], mcfg["latent_resolution"])
+        h1, rl = ag.hidden_state_transition(dev(d["h"]), dev(planes))
+        np.testing.assert_allclose(h1.cpu().numpy(), d["h1"], **tol)
+        np.testing.assert_allclose(rl.cpu().numpy(), d["r1"], **tol)
+    finally:
+        L.lib().mzba_conv_x6_set_variant(2)
+    if tag == "full":  # the 4x5 latent's 3x3 convs all carry x6 weights (round 5: dyn0 and the policy conv too)
+        p = ag.packed
+        assert p.dyn0.get("wx") is not None and p.pol_conv.get("wx") is not None
+        assert all(c.get("wx") is not None for blk in p.dyn + p.pred for c in blk)
 
 
 def test_nets_bf16_close():
@@ -701,7 +713,7 @@ def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, relu, with_res):
         assert L.lib().mzba_conv_x6_set_variant(0) == 0
         L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), L.ptr(res), L.ptr(out2), B, H, W, Cin, Cout, relu, L.stream())
     finally:
-        L.lib().mzba_conv_x6_set_variant(1)
+        L.lib().mzba_conv_x6_set_variant(2)
     f32 = torch.empty(B, H, W, Cout, device=dev)
     wd = w.reshape(Cout, -1).contiguous()
     L.call("mzba_conv2d", 0, L.ptr(x), H * W * Cin, None, 0, L.ptr(wd), L.ptr(b), None, None, 0, L.ptr(res), L.ptr(f32),
@@ -713,6 +725,79 @@ def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, relu, with_res):
     e6, e32 = (out.double() - ref).abs().max().item(), (f32.double() - ref).abs().max().item()
     print(f"conv_x6 {B}x{H}x{W} {Cin}: max err vs f64 {e6 / scale:.2e} of the magnitude, f32 MFMA conv {e32 / scale:.2e}")
     assert e6 <= 2 * e32 + 1e-7 * scale and e6 <= 2e-6 * scale, (e6 / scale, e32 / scale)
+
+
+@pytest.mark.parametrize("B,Cout,mode", [(4100, 256, "res"), (37, 256, "plain"), (4096, 128, "plain"),
+                                         (1000, 256, "gather"), (21, 128, "gather")])
+def test_conv_x6_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode):
+    """The pixel-tiled x6 conv at the 4x5 latent (conv_x6t: 16 envs x 20 pixels per workgroup, the zero-padding
+    taps not issued, the input staged in 32-channel blocks by LDS-DMA) against an f64 conv of the same f32
+    operands: within 2x the f32-input MFMA conv's error + 1e-7 and within 2e-6 of the magnitude, and within 2e-6
+    of the pre-split form (the same products summed in another order). Ragged batches (B % 16 != 0), Cout 128
+    (the policy head's conv), and the gathered form: each env's image read from a slot of a latent pool with the
+    action planes' folded [HW][A][Cout] bias table ((acc + act_bias) + bias, the f32 dynamics' first conv)."""
+    from mzba import _lib as L
+    from mzba.agent import split_pack_x6
+    H, W, Cin, A, S = 4, 5, 256, 3, 6
+    g = torch.Generator(device="cuda").manual_seed(B + Cout)
+    dev = torch.device("cuda")
+    w = torch.randn(Cout, 3, 3, Cin, generator=g, device=dev) / (Cin * 9) ** 0.5
+    b = torch.randn(Cout, generator=g, device=dev) * 0.1
+    wx = split_pack_x6(w.cpu().numpy().reshape(Cout, -1), Cout, 3, Cin).cuda()
+    relu = 1 if mode != "plain" else 0
+    res = tab = act = slot = None
+    if mode == "gather":
+        pool = torch.rand(B, S + 1, H, W, Cin, generator=g, device=dev)
+        slot = torch.randint(0, S + 1, (B,), generator=g, device=dev, dtype=torch.int32)
+        act = torch.randint(0, A, (B,), generator=g, device=dev, dtype=torch.int32)
+        tab = torch.randn(H * W, A, Cout, generator=g, device=dev) * 0.1
+        x = pool[torch.arange(B, device=dev), slot.long()].contiguous()
+        src, env_stride, slot_stride = pool, (S + 1) * H * W * Cin, H * W * Cin
+    else:
+        x = torch.rand(B, H, W, Cin, generator=g, device=dev)
+        src, env_stride, slot_stride = x, H * W * Cin, 0
+        if mode == "res":
+            res = torch.rand(B, H, W, Cout, generator=g, device=dev)
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), b.double(),
+                                     padding=1).permute(0, 2, 3, 1)
+    if res is not None:
+        ref = ref + res.double()
+    if tab is not None:
+        ref = ref + tab.double()[:, act.long()].permute(1, 0, 2).reshape(B, H, W, Cout)
+    if relu:
+        ref = torch.relu(ref)
+    assert L.lib().mzba_conv_x6_ex_supported(H, W, Cin, Cout, 3, int(mode == "gather"))
+    out = torch.full((B, H, W, Cout), float("nan"), device=dev)
+    try:
+        assert L.lib().mzba_conv_x6_set_variant(3) == 0
+        L.call("mzba_conv_x6_ex", L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(wx), L.ptr(b), L.ptr(tab),
+               L.ptr(act), A if tab is not None else 0, L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu, L.stream())
+    finally:
+        L.lib().mzba_conv_x6_set_variant(2)
+    # the f32-input MFMA conv (conv_igemm, the f32 path's form before x6) on the same gathered operands
+    f32 = torch.empty(B, H, W, Cout, device=dev)
+    wd = w.reshape(Cout, -1).contiguous()
+    L.call("mzba_conv2d", 0, L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(wd), L.ptr(b), L.ptr(tab), L.ptr(act),
+           A if tab is not None else 0, L.ptr(res), L.ptr(f32), B, H, W, Cin, Cout, 3, relu, L.stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    scale = ref.abs().max().item()
+    et, e32 = (out.double() - ref).abs().max().item(), (f32.double() - ref).abs().max().item()
+    msg = f"conv_x6t B={B} Cout={Cout} {mode}: max err vs f64 {et / scale:.2e} of the magnitude, f32 MFMA conv {e32 / scale:.2e}"
+    if mode != "gather" and Cout == 256:  # the pre-split halo form on the same contiguous operands
+        try:
+            assert L.lib().mzba_conv_x6_set_variant(1) == 0
+            outp = torch.full_like(out, float("nan"))
+            L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), L.ptr(res), L.ptr(outp), B, H, W, Cin, Cout, relu,
+                   L.stream())
+        finally:
+            L.lib().mzba_conv_x6_set_variant(2)
+        torch.cuda.synchronize()
+        ep = (out - outp).abs().max().item()
+        msg += f", vs the pre-split form {ep / scale:.2e}"
+        assert ep <= 2e-6 * scale, msg
+    print(msg)
+    assert et <= 2 * e32 + 1e-7 * scale and et <= 2e-6 * scale, msg
 
 
 # ------------------------------------------------------------------------------ MCTS
