@@ -1,4 +1,5 @@
-"""MuZero networks on the MI355X path (mirror of src/networks.py:MuZeroAgent, eval only).
+"""MuZero networks on the MI355X path (mirror of src/networks.py:MuZeroAgent: eval-mode inference on the packed
+HIP nets; train mode = the device learner's kernels behind torch.autograd, for RLSystem._training_stage).
 
 Weights are taken in the reference's `state_dict` format and packed once on the host:
 BatchNorm (eval, running stats) folded into the conv weights/bias, convs packed
@@ -496,6 +497,124 @@ class NetRunner:
         L.ops().prediction_tree_(self.native, h, pi, v, *tree_args, sim, gamma, r)
 
 
+def _rows(x):
+    """NCHW -> the learner's NHWC rows [B * H * W][C] (contiguous f32)."""
+    B, C, H, W = x.shape
+    return x.detach().permute(0, 2, 3, 1).reshape(B * H * W, C).contiguous().float()
+
+
+def _nchw(rows, B, H, W):
+    return rows.view(B, H, W, -1).permute(0, 3, 1, 2).contiguous()
+
+
+class _RepFn(torch.autograd.Function):
+    """create_hidden_state_root in train mode (networks.py:271-280, BatchNorm on batch statistics)."""
+
+    @staticmethod
+    def forward(ctx, anchor, x, ln):
+        B, C, H, W = x.shape
+        xin = torch.zeros(B * H * W, ln.rep[0][1].cin_p, device=ln.device)
+        xin[:, :C] = _rows(x)
+        h, saved = ln.rep_forward(xin, B)
+        ctx.ln, ctx.saved, ctx.B = ln, saved, B
+        return _nchw(h, B, *ln.lat)
+
+    @staticmethod
+    def backward(ctx, gh):
+        ctx.ln.rep_backward(ctx.saved, _rows(gh), ctx.B)
+        ctx.saved = None
+        return None, None, None
+
+
+class _PredFn(torch.autograd.Function):
+    """evaluate_state in train mode (networks.py:300-312) -> (policy logits, value logits)."""
+
+    @staticmethod
+    def forward(ctx, anchor, h, ln):
+        B = h.shape[0]
+        lp, lv, u = ln.pred_forward(_rows(h), B)
+        ctx.ln, ctx.u, ctx.B = ln, u, B
+        return lp, lv
+
+    @staticmethod
+    def backward(ctx, dlp, dlv):
+        ln, B = ctx.ln, ctx.B
+        dlp = dlp if dlp is not None else torch.zeros(B, ln.na, device=ln.device)
+        dlv = dlv if dlv is not None else torch.zeros(B, ln.ns, device=ln.device)
+        gh = ln.pred_backward(ctx.u, dlp.float(), dlv.float(), B)
+        ctx.u = None
+        return None, _nchw(gh, B, *ln.lat), None
+
+
+class _DynFn(torch.autograd.Function):
+    """hidden_state_transition in train mode (networks.py:282-298) -> (next scaled latent, reward logits); the
+    action planes carry no gradient (the reference builds them from replay actions)."""
+
+    @staticmethod
+    def forward(ctx, anchor, h, planes, ln):
+        B = h.shape[0]
+        hn, lr, u = ln.dyn_forward(_rows(h), _rows(planes.to(ln.device)), B)
+        ctx.ln, ctx.u, ctx.B = ln, u, B
+        return _nchw(hn, B, *ln.lat), lr
+
+    @staticmethod
+    def backward(ctx, ghn, dlr):
+        ln, B = ctx.ln, ctx.B
+        dlr = dlr if dlr is not None else torch.zeros(B, ln.ns, device=ln.device)
+        gh = ln.dyn_backward(ctx.u, _rows(ghn) if ghn is not None else None, dlr.float(), B)
+        ctx.u = None
+        return None, _nchw(gh, B, *ln.lat), None, None
+
+
+class LearnerOptimizer:
+    """`mu_zero.optimizer` of the drop-in agent (networks.py:268: Adam(lr, weight_decay=1e-4) over the agent's
+    parameters): zero_grad / step / state_dict / load_state_dict as torch.optim.Adam, on the device learner's flat
+    f32 master weights, gradients and moments (mzba_adam: torch's single-tensor order). The state_dict is
+    torch.optim.Adam's (params in MuZeroAgent.parameters() order), so the reference's checkpoints round-trip."""
+
+    def __init__(self, agent):
+        self.agent = agent
+        self._pending = None  # an optimizer state loaded before the first train_mode()
+
+    @property
+    def param_groups(self):
+        ln = self.agent._learner
+        lr = ln.lr if ln is not None else float(self.agent.cfg["learning_rate"])
+        return [{"params": list(self.agent.parameters()), "lr": lr, "betas": (0.9, 0.999), "eps": 1e-8,
+                 "weight_decay": 1e-4}]
+
+    def zero_grad(self, set_to_none=True):
+        ln = self.agent._learner
+        if ln is not None:
+            ln.G.zero_()
+            ln.begin_calls()  # the input-gradient packs of the current weights
+
+    def step(self, closure=None):
+        ln = self.agent._learner
+        if ln is None:
+            raise RuntimeError("optimizer.step() before train_mode(): no gradients")
+        ln.adam_step()
+        ln.begin_calls()
+        self.agent._host_stale = True
+        return None
+
+    def state_dict(self):
+        ln = self.agent._learner
+        if ln is not None:
+            return ln.optimizer_state_dict()
+        if self._pending is not None:
+            return self._pending
+        from .checkpoint import fresh_optimizer_state
+        return fresh_optimizer_state(self.agent.cfg)
+
+    def load_state_dict(self, d):
+        ln = self.agent._learner
+        if ln is not None:
+            ln.load_optimizer_state_dict(d)
+        else:
+            self._pending = d
+
+
 class MuZeroAgent:
     """Drop-in for src/networks.py:MuZeroAgent inference (eval mode).
 
@@ -509,8 +628,11 @@ class MuZeroAgent:
     p.requires_grad = False` (train_torch.py:86-98) work unchanged. The host copy (`state_dict()`,
     `parameters()`: CPU tensors in the reference's keys and order) is the source of truth; the device
     pack (`packed`: BN folded, kernel layouts) is built from it on first use and refreshed in place by
-    every `load_state_dict`. Training (`optimizer`, `train_mode`, train_torch.py:369-452) is served by
-    `mzba.learner.Learner`, not by this class.
+    every `load_state_dict`. Training (train_torch.py:369-452): `train_mode()` hands the three nets to a
+    device learner (`mzba.learner.Learner`, f32, BatchNorm on batch statistics) behind torch.autograd
+    Functions, so the reference's `_k_step_rollout` + `loss_fn` + `loss.backward()` run unchanged on the HIP
+    kernels, and `optimizer` (zero_grad / step / state_dict / load_state_dict) is Adam on the learner's master
+    weights; `eval_mode()` copies the trained weights back into the host copy and the packed inference nets.
     """
 
     def __init__(self, cfg, dtype=None, device="cuda", dyn_dtype=None):
@@ -522,6 +644,10 @@ class MuZeroAgent:
         self._packed = None
         self._runners = {}
         self._sd = None
+        self._learner = None      # train mode: the device learner (created by the first train_mode())
+        self._training = False
+        self._host_stale = False  # the learner's weights moved since the host copy was taken
+        self._optimizer = LearnerOptimizer(self)
         self._set_host(torch_init_state_dict(cfg))
 
     # reference API ---------------------------------------------------------------------
@@ -540,11 +666,18 @@ class MuZeroAgent:
                 out[k] = torch.nn.Parameter(t.to(torch.float32))
         self._sd = out
 
+    def _sync_host(self):
+        if self._learner is not None and self._host_stale:
+            self._set_host(self._learner.state_dict())
+            self._host_stale = False
+
     def state_dict(self):
         """OrderedDict of the reference's keys (networks.py's module order), detached CPU tensors."""
+        self._sync_host()
         return OrderedDict((k, v.detach()) for k, v in self._sd.items())
 
     def named_parameters(self):
+        self._sync_host()
         return ((k, v) for k, v in self._sd.items() if isinstance(v, torch.nn.Parameter))
 
     def parameters(self):
@@ -563,6 +696,10 @@ class MuZeroAgent:
             if tuple(np.shape(_np(sd[k]))) != tuple(shape):
                 raise ValueError(f"shape mismatch for {k}: {np.shape(_np(sd[k]))} vs {shape}")
         self._set_host(sd)
+        self._host_stale = False
+        if self._learner is not None:  # train_torch.py:645-652: the model first, then the optimizer state
+            self._learner.load_state_dict({k: _np(v) for k, v in self._sd.items()})
+            self._learner.begin_calls()
         if self._packed is not None:  # a refresh: new weights into the existing buffers, live loops and
             self._packed.refresh_from(self._pack())  # captured graphs run them from their next launch
 
@@ -577,11 +714,33 @@ class MuZeroAgent:
         return self._packed
 
     def eval_mode(self):
-        pass  # BN always uses running stats on this path (networks.py:336-342)
+        """networks.py:336-342: BatchNorm on running statistics. After training, the learner's weights and
+        running statistics become the host copy and the packed inference nets (refreshed in place)."""
+        if self._training:
+            self._training = False
+            self._host_stale = True
+            self._sync_host()
+            if self._packed is not None:
+                self._packed.refresh_from(self._pack())
 
     def train_mode(self):
-        raise NotImplementedError("training runs on mzba.learner.Learner (train_torch.py:369-452); the acting "
-                                  "agent is eval-only")
+        """networks.py:344-350: BatchNorm on batch statistics (running statistics updated, momentum 0.1). The
+        three nets then run on the device learner's kernels and back-propagate through torch.autograd."""
+        if self._learner is None:
+            from .learner import Learner
+            self._learner = Learner(self.cfg, {k: _np(v) for k, v in self._sd.items()}, dtype="f32",
+                                    device=self.device, streams=1, defer_wgrad=False, fuse_bn=False)
+            self._anchor = torch.zeros(1, device=self.device, requires_grad=True)
+            if self._optimizer._pending is not None:
+                self._learner.load_optimizer_state_dict(self._optimizer._pending)
+                self._optimizer._pending = None
+        self._learner.begin_calls()
+        self._training = True
+
+    @property
+    def optimizer(self):
+        """networks.py:268 `self.optimizer` (Adam, lr, weight_decay 1e-4): LearnerOptimizer."""
+        return self._optimizer
 
     def runner(self, B, H, W):
         key = (B, H, W)
@@ -592,14 +751,21 @@ class MuZeroAgent:
     # reference API on NCHW tensors: the torch.ops.mz net ops (csrc/net_ops.cpp) -----------------
     def create_hidden_state_root(self, state):
         """networks.py:271-280: (B, 2L, H, W) -> scaled latent (B, C, h, w)."""
+        if self._training:
+            return _RepFn.apply(self._anchor, state.to(self.device).float(), self._learner)
         return L.ops().representation(self.packed.native, state.to(self.device))
 
     def hidden_state_transition(self, prev_hidden_state, action):
         """networks.py:282-298: action = one-hot planes (B, A, h, w) -> (h', reward logits)."""
+        if self._training:
+            return _DynFn.apply(self._anchor, prev_hidden_state.to(self.device).float(), action.to(self.device).float(),
+                                self._learner)
         return L.ops().dynamics(self.packed.native, prev_hidden_state.to(self.device), action.to(self.device))
 
     def evaluate_state(self, hidden_state):
         """networks.py:300-312 -> (policy logits (B,3), value logits (B,11))."""
+        if self._training:
+            return _PredFn.apply(self._anchor, hidden_state.to(self.device).float(), self._learner)
         return L.ops().prediction(self.packed.native, hidden_state.to(self.device))
 
     def _rep_hw(self):

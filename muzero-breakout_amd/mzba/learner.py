@@ -863,6 +863,121 @@ class Learner:
                    *self._adam_scalars(self.step_count), s)
         return loss
 
+    # -- the three nets one call at a time (the drop-in agent's train mode: RLSystem._training_stage calls
+    # create_hidden_state_root / evaluate_state / hidden_state_transition itself, train_torch.py:487-528, and
+    # back-propagates its own loss_fn through them). The same launches as _minibatch_body's forward and backward
+    # pieces, on one stream with immediate weight gradients; gradients accumulate into G until zero_grad().
+    # Activations NHWC rows [B * H * W][C] of this learner's dtype; each forward returns what its backward needs.
+    def begin_calls(self):
+        """Per-call mode: one stream, no deferred weight gradients, per-step packs from the current weights."""
+        if self.streams != 1 or self.defer_wgrad or self.fuse_bn and self.dt == 1:
+            raise RuntimeError("per-call nets need a Learner(streams=1, defer_wgrad=False, fuse_bn=False)")
+        self._pending = None
+        self._scale_idx = []
+        self._prepare_packs()
+
+    def rep_forward(self, x, B):
+        """RepresentationNetwork + _scale_state (networks.py:38-99, 314-328) in train mode; x [B*H*W][cin_p]."""
+        s = L.stream()
+        tape, h, hh, ww = [], x, 16, 20
+        for kind, mod in self.rep:
+            if kind == "conv":
+                y, _ = self._conv(mod, h, B, hh, ww)
+                tape.append(("conv", mod, (h, hh, ww)))
+                h = y
+            elif kind == "res":
+                h, sv = self._res_fwd(mod, h, B, hh, ww)
+                tape.append(("res", mod, (sv, hh, ww)))
+            else:
+                y = self._act(B * (hh // 2) * (ww // 2), h.shape[1])
+                L.call("mzba_avgpool2", self.dt, L.ptr(h), L.ptr(y), B, hh, ww, h.shape[1], s)
+                tape.append(("pool", None, (hh, ww, h.shape[1])))
+                h, hh, ww = y, hh // 2, ww // 2
+        h, sc = self._scale_fwd(h, B)
+        return h, (tape, sc)
+
+    def rep_backward(self, saved, gh, B):
+        """Weight gradients of the representation from d(scaled root latent) gh."""
+        tape, sc = saved
+        s = L.stream()
+        gx = self._scale_bwd(sc, gh, B)
+        for ti in reversed(range(len(tape))):
+            kind, mod, sv = tape[ti]
+            if kind == "pool":
+                hh2, ww2, C = sv
+                dx = self._act(B * hh2 * ww2, C)
+                L.call("mzba_avgpool2_backward", self.dt, L.ptr(gx), L.ptr(dx), B, hh2, ww2, C, s)
+                gx = dx
+            elif kind == "res":
+                svr, hh2, ww2 = sv
+                gx = self._res_bwd(mod, svr, gx, None, B, hh2, ww2)
+            else:
+                xin, hh2, ww2 = sv
+                self._wgrad(mod, xin, gx, B, hh2, ww2)
+                gx = self._dgrad(mod, gx, B, hh2, ww2) if mod is not self.rep[0][1] else None
+
+    def pred_forward(self, h, B):
+        """PredictionNetwork (networks.py:170-241) in train mode -> (policy logits [B][na], value logits [B][ns])."""
+        hl, wl = self.lat
+        xp, psv = h, []
+        for r in self.pred_res:
+            xp, sv = self._res_fwd(r, xp, B, hl, wl)
+            psv.append(sv)
+        lp = torch.empty(B, self.na, device=self.device)
+        lv = torch.empty(B, self.ns, device=self.device)
+        yp, spol = self._block_fwd(self.pred_pconv, xp, B, hl, wl)
+        self._linear(self.pred_plin[0], yp, B, self.pred_plin[1], self.na, lp)
+        yv, sval = self._block_fwd(self.pred_vconv, xp, B, hl, wl)
+        self._linear(self.pred_vlin[0], yv, B, self.pred_vlin[1], self.ns, lv)
+        return lp, lv, dict(psv=psv, spol=spol, sval=sval, yp=yp, yv=yv)
+
+    def pred_backward(self, u, dlp, dlv, B):
+        """-> d h from the policy / value logit gradients (each [B][n] f32)."""
+        hl, wl = self.lat
+        dyv = self._linear_bwd(self.pred_vlin[0], u["yv"], dlv.contiguous(), B, self.pred_vlin[1], self.ns)
+        gp = self._block_bwd(self.pred_vconv, u["sval"], dyv, B, hl, wl)
+        dyp = self._linear_bwd(self.pred_plin[0], u["yp"], dlp.contiguous(), B, self.pred_plin[1], self.na)
+        self._block_bwd(self.pred_pconv, u["spol"], dyp, B, hl, wl, acc=gp)
+        for i in reversed(range(len(self.pred_res))):
+            gp = self._res_bwd(self.pred_res[i], u["psv"][i], gp, None, B, hl, wl)
+        return gp
+
+    def dyn_forward(self, h, planes, B):
+        """DynamicsNetwork + _scale_state (networks.py:103-167, 282-298) in train mode on concat(h, action planes);
+        planes [B][hw][A] (NHWC one-hot planes) -> (next scaled latent, reward logits [B][ns])."""
+        hl, wl = self.lat
+        cdyn = self.dyn_block.cin_p
+        xin = torch.zeros(B * hl * wl, cdyn, dtype=self.tdtype, device=self.device)
+        xin[:, :self.c1] = h
+        xin[:, self.c1:self.c1 + self.A] = planes.reshape(B * hl * wl, self.A).to(self.tdtype)
+        xd, sblk = self._block_fwd(self.dyn_block, xin, B, hl, wl)
+        dsv = []
+        for r in self.dyn_res:
+            xd, sv = self._res_fwd(r, xd, B, hl, wl)
+            dsv.append(sv)
+        lr = torch.empty(B, self.ns, device=self.device)
+        yr, srew = self._block_fwd(self.dyn_rconv, xd, B, hl, wl)
+        self._linear(self.dyn_rlin[0], yr, B, self.dyn_rlin[1], self.ns, lr)
+        h_next, ssc = self._scale_fwd(xd, B)
+        return h_next, lr, dict(sblk=sblk, dsv=dsv, yr=yr, srew=srew, ssc=ssc)
+
+    def dyn_backward(self, u, gh_next, dlr, B):
+        """-> d h (the latent part of the dynamics input) from d(next scaled latent) (or None) and d(reward logits)."""
+        hl, wl = self.lat
+        gx = self._scale_bwd(u["ssc"], gh_next, B) if gh_next is not None else None
+        dyr = self._linear_bwd(self.dyn_rlin[0], u["yr"], dlr.contiguous(), B, self.dyn_rlin[1], self.ns)
+        gx = self._block_bwd(self.dyn_rconv, u["srew"], dyr, B, hl, wl, acc=gx)
+        for i in reversed(range(len(self.dyn_res))):
+            gx = self._res_bwd(self.dyn_res[i], u["dsv"][i], gx, None, B, hl, wl)
+        return self._block_bwd(self.dyn_block, u["sblk"], gx, B, hl, wl)
+
+    def adam_step(self):
+        """Adam(lr, weight_decay=1e-4) on the accumulated gradients (networks.py:268, torch's single-tensor
+        order, the kernel of train_minibatch)."""
+        self.step_count += 1
+        L.call("mzba_adam", L.ptr(self.P), L.ptr(self.G), L.ptr(self.M1), L.ptr(self.M2), self.n_flat,
+               *self._adam_scalars(self.step_count), L.stream())
+
     def flops_per_minibatch(self, B):
         """Algorithmic conv + linear FLOPs of one minibatch: forward, input gradients (all convs
         but the first) and weight gradients, 2 * M * Cout * Cin * taps each (Cin unpadded)."""

@@ -158,3 +158,134 @@ def test_rlsystem_constructs_and_acts_on_this_build():
             windows += t.length - K + 1
     assert rl.replay_buffer.length == windows
     assert len(reward_sums) == min(B, windows)
+
+
+def _loss_fn(observed_reward, predicted_reward, bootstrapped_reward, predicted_value, visit_counts, predicted_policy,
+             target_transformation, K):
+    """train_torch.py:33-66 (loss_fn), restated."""
+    import torch.nn.functional as F
+    reward_loss = F.kl_div(F.log_softmax(predicted_reward.view(-1, predicted_reward.shape[-1]), dim=-1),
+                           target_transformation(observed_reward).view(-1, predicted_reward.shape[-1]),
+                           reduction="batchmean")
+    value_loss = F.kl_div(F.log_softmax(predicted_value.view(-1, predicted_value.shape[-1]), dim=-1),
+                          target_transformation(bootstrapped_reward).view(-1, predicted_value.shape[-1]),
+                          reduction="batchmean")
+    vcn = visit_counts / visit_counts.sum(dim=-1, keepdim=True)
+    policy_loss = F.kl_div(F.log_softmax(predicted_policy.view(-1, predicted_policy.shape[-1]), dim=-1),
+                           vcn.view(-1, vcn.shape[-1]), reduction="batchmean")
+    return (1 / K) * (reward_loss + value_loss + policy_loss), reward_loss, value_loss, policy_loss
+
+
+def _training_iteration(mu_zero, scalar_transforms, mb, K, L, latent_resolution, n_actions=3):
+    """One iteration of RLSystem._training_stage's loop body (train_torch.py:385-411) on a minibatch already
+    drawn from the replay buffer (_prepare_minibatch :454-485): _encode_actions (:279-293), _k_step_rollout
+    (:487-528, with _encode_action_dynamics :295-311), loss_fn, loss.backward(), optimizer.step()."""
+    import torch.nn.functional as F
+    dev = "cuda"
+    mu_zero.optimizer.zero_grad()
+    with torch.no_grad():
+        states = torch.as_tensor(mb["states"], dtype=torch.float32, device=dev)
+        B = states.shape[0]
+        acts = torch.as_tensor(mb["past_actions"], device=dev)
+        ex = (acts / n_actions)[:, :, None, None].expand(-1, -1, 16, 20)
+        input_actions_encoded = torch.ones((B, L, 16, 20), device=dev) * ex
+    repnet_input = torch.cat((states.view(B, L, 16, 20), input_actions_encoded), dim=1)
+    hidden_state = mu_zero.create_hidden_state_root(repnet_input)
+    k_step_actions = torch.as_tensor(mb["future_actions"], device=dev)
+    pols, vals, rews = [], [], []
+    for k in range(K):
+        p, v = mu_zero.evaluate_state(hidden_state)
+        pols.append(p)
+        vals.append(v)
+        one_hot = F.one_hot(k_step_actions[:, k], num_classes=n_actions).float()
+        a_enc = one_hot.view(B, n_actions, 1, 1).expand(-1, -1, latent_resolution[0], latent_resolution[1])
+        hidden_state, r = mu_zero.hidden_state_transition(hidden_state, a_enc)
+        rews.append(r)
+    pr, pv, pp = torch.stack(rews, 1), torch.stack(vals, 1), torch.stack(pols, 1)
+    tt = lambda x: scalar_transforms.supports_representation(torch.as_tensor(x, dtype=torch.float32)).to(dev)  # noqa: E731
+    loss, rl, vl, pl = _loss_fn(torch.as_tensor(mb["rewards"]), pr, torch.as_tensor(mb["targets"]), pv,
+                                torch.as_tensor(mb["counts"], dtype=torch.float32, device=dev), pp, tt, K)
+    loss.backward()
+    mu_zero.optimizer.step()
+    return np.array([float(loss), float(rl), float(vl), float(pl)]), (pr.detach(), pv.detach(), pp.detach())
+
+
+def test_training_stage_runs_on_the_dropin_agent():
+    """RLSystem._training_stage on this build's MuZeroAgent (train_torch.py:373-411): train_mode(), then the
+    reference's own minibatch loop body — zero_grad, _k_step_rollout through create_hidden_state_root /
+    evaluate_state / hidden_state_transition, loss_fn, loss.backward(), optimizer.step() — on the reference's two
+    training minibatches (tests/golden/learner_small.npz, narrow nets). The three nets run on the device learner's
+    HIP kernels behind torch.autograd. Against the reference: both steps' losses and logits within rtol 2e-4, the
+    parameters after each Adam step within 2 lr (first-step updates are ~lr sign(g)), BN running statistics rtol
+    1e-4. Against mzba.learner.Learner.train_minibatch on the same minibatch (same kernels, its fused loss kernel):
+    gradients within 1e-4 of each tensor's magnitude. Then eval_mode() puts the trained weights into the packed
+    inference nets (the target-net copy, train_torch.py:361-367, reads them through state_dict()), and the
+    optimizer's state_dict is torch.optim.Adam's (train_torch.py:622, 652) and round-trips."""
+    import os
+    from conftest import GOLDEN
+    from mzba.config import learner_model_cfg
+    from mzba.learner import Learner, MinibatchRing
+    from mzba.weights import init_state_dict
+    from src.networks import MuZeroAgent
+    from utils import ScalarTransforms
+    z = np.load(os.path.join(GOLDEN, "learner_small.npz"))
+    mcfg, K, lr = learner_model_cfg(), int(z["K"]), float(z["lr"])
+    mcfg = dict(mcfg, learning_rate=lr, device="cuda")
+    start = init_state_dict(mcfg, int(z["seed"]))
+    ag = MuZeroAgent(mcfg)
+    ag.load_state_dict(start)
+    st = ScalarTransforms(mcfg)
+    ref_ln = Learner(mcfg, start, K=K, streams=1, defer_wgrad=False)
+    ag.train_mode()
+    for s in (1, 2):
+        mb = {k.split("/")[-1]: z[k] for k in z.files if k.startswith(f"s{s}/in/")}
+        loss, logits = _training_iteration(ag, st, mb, K, mcfg["state_history_length"], mcfg["latent_resolution"])
+        ref = np.array([float(z[f"s{s}/{k}"]) for k in ("loss", "rl", "vl", "pl")])
+        np.testing.assert_allclose(loss, ref, rtol=2e-4, atol=2e-5, err_msg=f"step {s} losses")
+        for got, key in zip(logits, ("pr", "pv", "pp")):
+            np.testing.assert_allclose(got.cpu().numpy(), z[f"s{s}/{key}"], rtol=2e-4, atol=5e-5, err_msg=f"step {s} {key}")
+        # the same minibatch through the learner's own fused minibatch (its loss kernel), from the same state
+        ring = MinibatchRing(mb)
+        ref_ln.train_minibatch(ring, ring.slots())
+        g_ref, g_got = ref_ln.gradients(), ag._learner.gradients()
+        for k, g in g_ref.items():
+            a, b = g.numpy().astype(np.float64), g_got[k].numpy().astype(np.float64)
+            scale = max(np.abs(a).max(), 1e-30)
+            if k.endswith((".conv1.bias", ".conv2.bias", ".conv.bias")):  # pre-BN biases: exactly 0 up to rounding
+                continue
+            assert np.abs(a - b).max() <= 1e-4 * scale + 1e-9, (s, k, np.abs(a - b).max() / scale)
+        sd = ag.state_dict()
+        for k, v in sd.items():
+            want = z[f"s{s}/param/{k}"].astype(np.float64)
+            got = v.numpy().astype(np.float64)
+            if k.endswith(("running_mean", "running_var")):
+                np.testing.assert_allclose(got, want, rtol=1e-4, atol=1e-6, err_msg=k)
+            elif k.endswith("num_batches_tracked"):
+                assert int(got) == int(want), k
+            else:
+                assert np.abs(got - want).max() <= 2.0 * lr * 1.001, (s, k, np.abs(got - want).max() / lr)
+        # teacher forcing for step 2, as the learner test: the reference's post-step-1 state
+        if s == 1:
+            nxt = {k[len("s1/param/"):]: z[k] for k in z.files if k.startswith("s1/param/")}
+            opt = {"state": {i: {"step": torch.tensor(1.0), "exp_avg": torch.as_tensor(z[f"s1/opt/exp_avg/{k}"]),
+                                 "exp_avg_sq": torch.as_tensor(z[f"s1/opt/exp_avg_sq/{k}"])}
+                             for i, k in enumerate(ref_ln.params)},
+                   "param_groups": ag.optimizer.state_dict()["param_groups"]}
+            ag.load_state_dict(nxt)          # train_torch.py:645-652: model, then optimizer
+            ag.optimizer.load_state_dict(opt)
+            ref_ln.load_state_dict(nxt)
+            ref_ln.load_optimizer_state_dict(opt)
+    # the optimizer state round-trips in torch.optim.Adam's format
+    osd = ag.optimizer.state_dict()
+    assert len(osd["state"]) == len(list(ag.parameters())) and float(osd["state"][0]["step"]) == 2.0
+    adam = torch.optim.Adam([torch.zeros_like(p) for p in ag.parameters()], lr=lr, weight_decay=1e-4)
+    adam.load_state_dict(osd)
+    # eval_mode: the trained weights reach the inference nets (BN folded from the trained running stats)
+    trained = {k: v.clone() for k, v in ag.state_dict().items()}
+    ag.eval_mode()
+    ref_ag = MuZeroAgent(mcfg)
+    ref_ag.load_state_dict(trained)
+    x = torch.rand(3, 2 * mcfg["state_history_length"], 16, 20, device="cuda")
+    assert torch.equal(ag.create_hidden_state_root(x), ref_ag.create_hidden_state_root(x))
+    for k, v in ag.state_dict().items():
+        assert torch.equal(v, trained[k]), k
