@@ -79,6 +79,10 @@ class PackedNets:
         self.dyn_fp16 = dyn_dtype == "fp16"  # BASELINE config 5: fp16 dynamics net (fused step only)
         self.tdt = TORCH_DT[dtype]
         self.c0, self.c1 = mcfg["latent_channels"]
+        if self.c0 % 64 or self.c1 % 64:
+            # every inference kernel's channel stride is the layer's width padded to 64 (cin_p); a narrower net
+            # would read its activations at the wrong stride. Training narrow nets (Learner) is unaffected.
+            raise ValueError(f"PackedNets: latent_channels {mcfg['latent_channels']} must be multiples of 64")
         self.L = mcfg["state_history_length"]
         self.lh, self.lw = mcfg["latent_resolution"]
         self.ns = mcfg["num_supports"]

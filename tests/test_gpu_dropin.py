@@ -207,7 +207,7 @@ def _training_iteration(mu_zero, scalar_transforms, mb, K, L, latent_resolution,
                                 torch.as_tensor(mb["counts"], dtype=torch.float32, device=dev), pp, tt, K)
     loss.backward()
     mu_zero.optimizer.step()
-    return np.array([float(loss), float(rl), float(vl), float(pl)]), (pr.detach(), pv.detach(), pp.detach())
+    return (np.array([float(x.detach()) for x in (loss, rl, vl, pl)]), (pr.detach(), pv.detach(), pp.detach()))
 
 
 def test_training_stage_runs_on_the_dropin_agent():
@@ -230,7 +230,7 @@ def test_training_stage_runs_on_the_dropin_agent():
     from utils import ScalarTransforms
     z = np.load(os.path.join(GOLDEN, "learner_small.npz"))
     mcfg, K, lr = learner_model_cfg(), int(z["K"]), float(z["lr"])
-    mcfg = dict(mcfg, learning_rate=lr, device="cuda")
+    mcfg = dict(mcfg, learning_rate=lr, device="cuda", dtype="f32")  # narrow nets: the f32 inference path
     start = init_state_dict(mcfg, int(z["seed"]))
     ag = MuZeroAgent(mcfg)
     ag.load_state_dict(start)
@@ -280,12 +280,47 @@ def test_training_stage_runs_on_the_dropin_agent():
     assert len(osd["state"]) == len(list(ag.parameters())) and float(osd["state"][0]["step"]) == 2.0
     adam = torch.optim.Adam([torch.zeros_like(p) for p in ag.parameters()], lr=lr, weight_decay=1e-4)
     adam.load_state_dict(osd)
-    # eval_mode: the trained weights reach the inference nets (BN folded from the trained running stats)
+    # eval_mode: the host copy holds the trained weights and running statistics (what the target-net copy,
+    # train_torch.py:361-367, reads through state_dict()); these 32-channel nets have no packed inference form
+    # (PackedNets needs multiples of 64 channels), so the pack refresh is checked on the 64-channel nets below
     trained = {k: v.clone() for k, v in ag.state_dict().items()}
     ag.eval_mode()
-    ref_ag = MuZeroAgent(mcfg)
-    ref_ag.load_state_dict(trained)
-    x = torch.rand(3, 2 * mcfg["state_history_length"], 16, 20, device="cuda")
-    assert torch.equal(ag.create_hidden_state_root(x), ref_ag.create_hidden_state_root(x))
     for k, v in ag.state_dict().items():
         assert torch.equal(v, trained[k]), k
+
+
+def test_dropin_agent_eval_after_training_refreshes_the_packed_nets():
+    """A 64-channel agent whose packed inference nets exist (acting) trains one reference minibatch body in
+    train_mode() (synthetic replay windows), then eval_mode(): its packed nets equal, tensor for tensor, a fresh
+    agent's built from the trained state_dict (BN folded from the trained running statistics), and its inference
+    matches the numpy oracle of those weights within 1e-5 (f32 path)."""
+    from mzba.config import small_model_cfg
+    from mzba.weights import init_state_dict
+    from oracle import nets as N
+    from src.networks import MuZeroAgent
+    from utils import ScalarTransforms
+    mcfg = dict(small_model_cfg(default_config()), device="cuda", dtype="f32")
+    ag = MuZeroAgent(mcfg)
+    ag.load_state_dict(init_state_dict(mcfg, 3))
+    x = torch.rand(5, 2 * mcfg["state_history_length"], 16, 20, device="cuda")
+    h0 = ag.create_hidden_state_root(x)  # the packed nets exist before training
+    g = np.random.default_rng(4)
+    B, K, Lh = 6, 5, mcfg["state_history_length"]
+    lut = np.array([0, 0.3, 0.6, 1.0], np.float32)
+    mb = dict(states=lut[g.integers(0, 4, (B, Lh, 16, 20))], past_actions=g.integers(0, 3, (B, Lh)),
+              future_actions=g.integers(0, 3, (B, K)), rewards=g.choice(np.array([-1, 0, 1], np.float32), (B, K)),
+              targets=(g.normal(size=(B, K)) * 2).astype(np.float32),
+              counts=g.multinomial(50, [0.3, 0.3, 0.4], (B, K)).astype(np.float32) + 1)
+    ag.train_mode()
+    loss, _ = _training_iteration(ag, ScalarTransforms(mcfg), mb, K, Lh, mcfg["latent_resolution"])
+    assert np.isfinite(loss).all()
+    ag.eval_mode()
+    trained = ag.state_dict()
+    ref = MuZeroAgent(mcfg)
+    ref.load_state_dict(trained)
+    for a, b in zip(ag.packed.device_tensors(), ref.packed.device_tensors()):
+        assert torch.equal(a, b)
+    got = ag.create_hidden_state_root(x)
+    assert not torch.equal(got, h0)  # the weights moved
+    want = N.create_hidden_state_root(x.cpu().numpy(), {k: v.numpy() for k, v in trained.items()}, mcfg)
+    np.testing.assert_allclose(got.cpu().numpy(), want, rtol=1e-5, atol=1e-5)
