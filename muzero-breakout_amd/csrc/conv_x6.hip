@@ -19,6 +19,7 @@
 // MFMAs). Epilogue in f32: + bias (+ residual), ReLU.
 #include "common.h"
 #include <type_traits>
+#include <utility>
 
 namespace {
 
@@ -462,6 +463,50 @@ constexpr X6TPairs make_x6t_pairs() {
 constexpr X6TPairs kPairs = make_x6t_pairs();
 static_assert(kPairs.n == 130, "130 of the 180 tile-taps of a 4x5 latent are in the image");
 
+// the same pairs grouped by (dy, source pixel), dy-major, sources ascending: one B fragment read feeds the group's
+// 1-3 output pixels (dx = -1, 0, +1 ascending), so per accumulator the taps still come dy-major, dx ascending
+struct X6TGroups {
+  int n = 0;
+  int dy[60] = {}, src[60] = {}, cnt[60] = {}, out[60][3] = {}, dx[60][3] = {};
+  bool last[60] = {};  // the dy row's last group
+};
+constexpr X6TGroups make_x6t_groups() {
+  X6TGroups r{};
+  int pairs = 0;
+  for (int dy = -1; dy <= 1; ++dy) {
+    for (int ps = 0; ps < x6t::HW; ++ps) {
+      const int ys = ps / x6t::W, xs = ps % x6t::W, y = ys - dy;
+      if (y < 0 || y >= x6t::H) continue;
+      int c = 0;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int x = xs - dx;
+        if (x < 0 || x >= x6t::W) continue;
+        r.out[r.n][c] = y * x6t::W + x, r.dx[r.n][c] = dx + 1;
+        ++c;
+      }
+      r.dy[r.n] = dy + 1, r.src[r.n] = ps, r.cnt[r.n] = c;
+      pairs += c;
+      ++r.n;
+    }
+    r.last[r.n - 1] = true;
+  }
+  r.n = pairs == 130 ? r.n : -1;
+  return r;
+}
+constexpr X6TGroups kGroups = make_x6t_groups();
+
+// f(std::integral_constant<int, i>) for i = 0 .. N - 1, each a compile-time index (the group tables index
+// sched_group_barrier counts, which must be constants)
+template <typename F, size_t... Is>
+MZ_DEV void x6t_static_for_impl(F&& f, std::index_sequence<Is...>) {
+  (f(std::integral_constant<int, (int)Is>()), ...);
+}
+template <int N, typename F>
+MZ_DEV void x6t_static_for(F&& f) {
+  x6t_static_for_impl(f, std::make_index_sequence<N>());
+}
+static_assert(kGroups.n == 50, "15 + 20 + 15 source pixels, 130 (tap, pixel) pairs");
+
 struct X6TArgs {
   const float* in;
   long long env_stride;   // elements between envs (contiguous: 20 x 256)
@@ -483,13 +528,12 @@ MZ_DEV int tkey(int e) { return (e >> 2) & 2; }  // chunk swizzle of row 16 p + 
 template <bool GA>
 __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
   using namespace x6t;
-  constexpr int CT = 1;  // 16 output channels per wave, 128 per workgroup (CT 2 needs 160 accumulators: spilled)
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, n = lane & 15;
   const int e0 = blockIdx.x * E;
-  const int nb = blockIdx.y * 128 + wave * 16 * CT;  // the wave's first output channel
+  const int nb = blockIdx.y * 128 + wave * 16;  // the wave's first output channel
 
   // LDS-DMA of block cb's f32 rows: 1-KiB piece i = rows 8 i .. 8 i + 7 = pixel i >> 1, envs 8 (i & 1) + 0..7; the
   // waves take pieces wave + 8 k, so a lane's env (8 (wave & 1) + lane / 8) is fixed: its offset is read once
@@ -523,31 +567,30 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
     }
   };
 
-  // weight ring: step j = 9 b + t reads pack step 8 t + b; slot j & 1
+  // weight ring: step j = 3 b + d (block b, dy = d - 1) holds the three dx taps t = 3 d + i (pack step 8 t + b) x
+  // the three parts; slot j & 1
   const uint4* wbase = reinterpret_cast<const uint4*>(a.wx) + (size_t)(nb / 16) * KS * 64;
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wbase), 0, 0x7fffffff, 0x00020000);
   const int pstride = (int)(a.part * 2);
-  auto wload = [&](int ct, int part, int j) {
-    j = j < KS ? j : KS - 1;
-    const int s = (j % 9) * 8 + j / 9;
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + (ct * KS + s) * 1024, 0));
+  auto wload = [&](int ti, int part, int j) {
+    j = j < 3 * NCS ? j : 3 * NCS - 1;
+    const int s = (3 * (j % 3) + ti) * 8 + j / 3;
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + s * 1024, 0));
   };
-  bf16x8 bq[2][3][CT];
+  bf16x8 bq[2][3][3];  // [step parity][dx tap][part]
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
-    for (int pt = 0; pt < 3; ++pt)
+    for (int ti = 0; ti < 3; ++ti)
 #pragma unroll
-      for (int ct = 0; ct < CT; ++ct) bq[cc][pt][ct] = wload(ct, pt, cc);
+      for (int pt = 0; pt < 3; ++pt) bq[cc][ti][pt] = wload(ti, pt, cc);
 
-  f32x4 acc[HW][CT];
+  f32x4 acc[HW];
 #pragma unroll
-  for (int p = 0; p < HW; ++p)
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      acc[p][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-      asm volatile("" : "+a"(acc[p][ct]));
-    }
+  for (int p = 0; p < HW; ++p) {
+    acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("" : "+a"(acc[p]));
+  }
 
   stage(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -563,48 +606,49 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
     for (int pt = 0; pt < 3; ++pt) f[pt] = *reinterpret_cast<const bf16x8*>(lds + pt * PB + ps * 1024 + lrow);
   };
 
-  // one 32-channel block: the (tap, output pixel) pairs whose source pixel is in the image (x6t::PAIRS, tap-major),
-  // fragment i + 1 read during pair i's MFMAs; after a tap's last pair its ring slot is reloaded (step j + 2)
+  // one 32-channel block: the (dy, source pixel) groups (x6t::kGroups), the next group's fragment read during the
+  // current group's MFMAs; after a dy row's last group its ring slot is reloaded (step j + 2)
   auto block = [&](int b, auto par) {
-    constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (9 b + t)
+    constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (3 b + d)
     bf16x8 fr[2][3];
-    frag(kPairs.src[0], fr[0]);
-#pragma unroll
-    for (int i = 0; i < kPairs.n; ++i) {
-      const int t = kPairs.tap[i], p = kPairs.out[i], sl = (P0 + t) & 1, cur = i & 1;
-      if (i + 1 < kPairs.n) frag(kPairs.src[i + 1], fr[cur ^ 1]);
+    frag(kGroups.src[0], fr[0]);
+    x6t_static_for<kGroups.n>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int d = kGroups.dy[i], sl = (P0 + d) & 1, cur = i & 1, cnt = kGroups.cnt[i];
+      if (i + 1 < kGroups.n) frag(kGroups.src[i + 1], fr[cur ^ 1]);
       const bf16x8* xs[6] = {&fr[cur][0], &fr[cur][1], &fr[cur][2], &fr[cur][0], &fr[cur][1], &fr[cur][0]};
       constexpr int wp[6] = {2, 1, 0, 1, 0, 0};  // per accumulator the small terms first (conv_x6p's order)
 #pragma unroll
       for (int k = 0; k < 6; ++k)
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-          acc[p][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][wp[k]][ct], *xs[k], acc[p][ct], 0, 0, 0);
+        for (int o = 0; o < cnt; ++o)
+          acc[kGroups.out[i][o]] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][kGroups.dx[i][o]][wp[k]], *xs[k],
+                                                                           acc[kGroups.out[i][o]], 0, 0, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 6 * CT, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 6 * cnt, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (kPairs.last[i]) {
+      if (kGroups.last[i]) {
 #pragma unroll
-        for (int pt = 0; pt < 3; ++pt)
+        for (int ti = 0; ti < 3; ++ti)
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct) bq[sl][pt][ct] = wload(ct, pt, 9 * b + t + 2);
+          for (int pt = 0; pt < 3; ++pt) bq[sl][ti][pt] = wload(ti, pt, 3 * b + d + 2);
         __builtin_amdgcn_sched_barrier(0);
       }
-    }
+    });
   };
 
   for (int b = 0; b < NCS; b += 2) {
     block(b, std::integral_constant<int, 0>());  // 9 b even
     // block b + 1's raw rows: wait for this wave's LDS-DMA (older than every ring load of block b: all but the
     // youngest 2 steps of ring loads may be waited on), then every wave's, then split
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * CT) : "memory");
+    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
     __syncthreads();
     split();
     __syncthreads();
     if (b + 2 < NCS) stage(b + 2);
     block(b + 1, std::integral_constant<int, 1>());  // 9 (b + 1) odd
     if (b + 2 < NCS) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * CT) : "memory");
+      asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
       __syncthreads();
       split();
       __syncthreads();
@@ -612,43 +656,35 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
     }
   }
 
-  // epilogue (f32): acc[p][ct] = D[channel nb + 16 ct + 4 q + i][env e0 + n at pixel p]
+  // epilogue (f32): acc[p] = D[channel nb + 4 q + i][env e0 + n at pixel p]
   const int env = e0 + n;
   if (env >= a.B) return;
   const float lo = a.relu ? 0.f : -__builtin_inff();
-  float4 bb[CT];
-#pragma unroll
-  for (int ct = 0; ct < CT; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
+  const int ch = nb + 4 * q;
+  const float4 bb = *reinterpret_cast<const float4*>(a.bias + ch);
   const int act = GA && a.act_bias ? a.act[env] : 0;
   const size_t ob = (size_t)env * HW * a.Cout;
+  float4 rv[HW];
+#pragma unroll
+  for (int p = 0; p < HW; ++p)  // every residual / action-bias load before the first use
+    rv[p] = GA && a.act_bias ? *reinterpret_cast<const float4*>(a.act_bias + ((size_t)p * a.A + act) * a.Cout + ch)
+          : a.res            ? *reinterpret_cast<const float4*>(a.res + ob + (size_t)p * a.Cout + ch)
+                             : make_float4(-0.f, -0.f, -0.f, -0.f);  // (acc + bias) + -0 is acc + bias
 #pragma unroll
   for (int p = 0; p < HW; ++p) {
-    float4 rv[CT];
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int ch = nb + ct * 16 + 4 * q;
-      if (GA && a.act_bias)
-        rv[ct] = *reinterpret_cast<const float4*>(a.act_bias + ((size_t)p * a.A + act) * a.Cout + ch);
-      else
-        rv[ct] = a.res ? *reinterpret_cast<const float4*>(a.res + ob + (size_t)p * a.Cout + ch)
-                       : make_float4(-0.f, -0.f, -0.f, -0.f);
+    float4 o;
+    if (GA && a.act_bias) {  // (acc + act_bias) + bias
+      o.x = fmaxf((acc[p][0] + rv[p].x) + bb.x, lo);
+      o.y = fmaxf((acc[p][1] + rv[p].y) + bb.y, lo);
+      o.z = fmaxf((acc[p][2] + rv[p].z) + bb.z, lo);
+      o.w = fmaxf((acc[p][3] + rv[p].w) + bb.w, lo);
+    } else {  // (acc + bias) + res
+      o.x = fmaxf((acc[p][0] + bb.x) + rv[p].x, lo);
+      o.y = fmaxf((acc[p][1] + bb.y) + rv[p].y, lo);
+      o.z = fmaxf((acc[p][2] + bb.z) + rv[p].z, lo);
+      o.w = fmaxf((acc[p][3] + bb.w) + rv[p].w, lo);
     }
-#pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      float4 o;
-      if (GA && a.act_bias) {  // (acc + act_bias) + bias
-        o.x = fmaxf((acc[p][ct][0] + rv[ct].x) + bb[ct].x, lo);
-        o.y = fmaxf((acc[p][ct][1] + rv[ct].y) + bb[ct].y, lo);
-        o.z = fmaxf((acc[p][ct][2] + rv[ct].z) + bb[ct].z, lo);
-        o.w = fmaxf((acc[p][ct][3] + rv[ct].w) + bb[ct].w, lo);
-      } else {  // (acc + bias) + res
-        o.x = fmaxf((acc[p][ct][0] + bb[ct].x) + rv[ct].x, lo);
-        o.y = fmaxf((acc[p][ct][1] + bb[ct].y) + rv[ct].y, lo);
-        o.z = fmaxf((acc[p][ct][2] + bb[ct].z) + rv[ct].z, lo);
-        o.w = fmaxf((acc[p][ct][3] + bb[ct].w) + rv[ct].w, lo);
-      }
-      *reinterpret_cast<float4*>(a.out + ob + (size_t)p * a.Cout + nb + ct * 16 + 4 * q) = o;
-    }
+    *reinterpret_cast<float4*>(a.out + ob + (size_t)p * a.Cout + ch) = o;
   }
 }
 
