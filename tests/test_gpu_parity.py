@@ -733,7 +733,7 @@ def test_conv_x6_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode):
     """The pixel-tiled x6 conv at the 4x5 latent (conv_x6t: 16 envs x 20 pixels per workgroup, the zero-padding
     taps not issued, the input staged in 32-channel blocks by LDS-DMA) against an f64 conv of the same f32
     operands: within 2x the f32-input MFMA conv's error + 1e-7 and within 2e-6 of the magnitude, and within 2e-6
-    of the pre-split form (the same products summed in another order). Ragged batches (B % 16 != 0), Cout 128
+    of the pre-split form (the same products summed in another order: 4e-6, the sum of two such errors). Ragged batches (B % 16 != 0), Cout 128
     (the policy head's conv), and the gathered form: each env's image read from a slot of a latent pool with the
     action planes' folded [HW][A][Cout] bias table ((acc + act_bias) + bias, the f32 dynamics' first conv)."""
     from mzba import _lib as L
@@ -795,7 +795,7 @@ def test_conv_x6_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode):
         torch.cuda.synchronize()
         ep = (out - outp).abs().max().item()
         msg += f", vs the pre-split form {ep / scale:.2e}"
-        assert ep <= 2e-6 * scale, msg
+        assert ep <= 4e-6 * scale, msg  # each within ~2e-6 of f64: apart by up to the sum
     print(msg)
     assert et <= 2 * e32 + 1e-7 * scale and et <= 2e-6 * scale, msg
 
