@@ -134,11 +134,12 @@ int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* 
  * slot_stride elements (slot optional), out = act(conv3x3 + act_bias[p][act[b]][n] + bias[n] (+ res)),
  * ((acc + act_bias) + bias) in f32 as conv_igemm; act_bias [H W][A][Cout] f32 excludes res. gather = 1 in the
  * support check: a strided / gathered input or an action-bias table (the pixel-tiled form only: the 4x5 latent,
- * Cin 256, Cout 256 / 128). */
+ * Cin 256, Cout 256 / 128). ks 3, or 1 at the 4x5 latent (the reward / value heads' 1x1 ConvBlocks, wx then the
+ * three parts of [Cout][1][1][Cin]). */
 int mzba_conv_x6_ex_supported(int H, int W, int Cin, int Cout, int ks, int gather);
 int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx,
                     const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,
-                    int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream);
+                    int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream);
 /* 2 (default): the pixel-tiled form at the 4x5 latent where its 16-env workgroups load the busiest CU less than the
  * pre-split tiles (the gathered / Cout 128 convs always), else the pre-split form where its staged rows fit (the f32
  * activations split once into bf16 hi / mid / lo planes while staging, 1.5x the f32 row; 8 waves x 32 channels),

@@ -433,7 +433,7 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
 // GA: the input gathered per env from the latent pool (in + b env_stride + slot[b] slot_stride) and the
 // action-bias table added ((acc + act_bias) + bias, conv_igemm's order): the f32 dynamics' first conv.
 namespace x6t {
-constexpr int E = 16, HW = 20, H = 4, W = 5, CIN = 256, NCS = 8, KS = 72;
+constexpr int E = 16, HW = 20, H = 4, W = 5, CIN = 256, NCS = 8;
 constexpr int ROWS = HW * E;          // 320 staged rows (pixel, env)
 constexpr int PB = ROWS * 64;         // bytes per bf16 plane of a 32-channel block
 constexpr int RAW = 3 * PB;           // f32 rows of the next block: 320 x 128 B
@@ -470,30 +470,34 @@ struct X6TGroups {
   int dy[60] = {}, src[60] = {}, cnt[60] = {}, out[60][3] = {}, dx[60][3] = {};
   bool last[60] = {};  // the dy row's last group
 };
-constexpr X6TGroups make_x6t_groups() {
+// ks = 3: the 3x3 conv's groups; ks = 1: the centre tap only (a 1x1 conv: 20 groups of one pixel each)
+constexpr X6TGroups make_x6t_groups(int ks) {
   X6TGroups r{};
   int pairs = 0;
   for (int dy = -1; dy <= 1; ++dy) {
+    if (ks == 1 && dy != 0) continue;
     for (int ps = 0; ps < x6t::HW; ++ps) {
       const int ys = ps / x6t::W, xs = ps % x6t::W, y = ys - dy;
       if (y < 0 || y >= x6t::H) continue;
       int c = 0;
       for (int dx = -1; dx <= 1; ++dx) {
+        if (ks == 1 && dx != 0) continue;
         const int x = xs - dx;
         if (x < 0 || x >= x6t::W) continue;
         r.out[r.n][c] = y * x6t::W + x, r.dx[r.n][c] = dx + 1;
         ++c;
       }
-      r.dy[r.n] = dy + 1, r.src[r.n] = ps, r.cnt[r.n] = c;
+      r.dy[r.n] = ks == 3 ? dy + 1 : 0, r.src[r.n] = ps, r.cnt[r.n] = c;  // dy: the ring step within a block
       pairs += c;
       ++r.n;
     }
     r.last[r.n - 1] = true;
   }
-  r.n = pairs == 130 ? r.n : -1;
+  r.n = pairs == (ks == 3 ? 130 : 20) ? r.n : -1;
   return r;
 }
-constexpr X6TGroups kGroups = make_x6t_groups();
+constexpr X6TGroups kGroups = make_x6t_groups(3);
+constexpr X6TGroups kGroups1 = make_x6t_groups(1);
 
 // f(std::integral_constant<int, i>) for i = 0 .. N - 1, each a compile-time index (the group tables index
 // sched_group_barrier counts, which must be constants)
@@ -506,13 +510,14 @@ MZ_DEV void x6t_static_for(F&& f) {
   x6t_static_for_impl(f, std::make_index_sequence<N>());
 }
 static_assert(kGroups.n == 50, "15 + 20 + 15 source pixels, 130 (tap, pixel) pairs");
+static_assert(kGroups1.n == 20, "a 1x1 conv: 20 (centre tap, pixel) pairs");
 
 struct X6TArgs {
   const float* in;
   long long env_stride;   // elements between envs (contiguous: 20 x 256)
   const int32_t* slot;    // optional: env b's image at in + b env_stride + slot[b] slot_stride
   long long slot_stride;
-  const bf16_t* wx;       // [3 parts][Cout / 16][72][64][8]
+  const bf16_t* wx;       // [3 parts][Cout / 16][9 or 1 taps x 8][64][8]
   const float* bias;      // [Cout]
   const float* act_bias;  // optional [20][A][Cout] (GA)
   const int32_t* act;     // [B] (GA)
@@ -525,9 +530,12 @@ struct X6TArgs {
 
 MZ_DEV int tkey(int e) { return (e >> 2) & 2; }  // chunk swizzle of row 16 p + e (64-B plane rows)
 
-template <bool GA>
+template <bool GA, int KSZ = 3>
 __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
   using namespace x6t;
+  constexpr const X6TGroups& G = KSZ == 3 ? kGroups : kGroups1;
+  constexpr int SPB = KSZ == 3 ? 3 : 1;     // ring steps per channel block (the dy rows)
+  constexpr int KST = KSZ * KSZ * NCS;      // pack k steps per column tile
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -568,20 +576,21 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
   };
 
   // weight ring: step j = 3 b + d (block b, dy = d - 1) holds the three dx taps t = 3 d + i (pack step 8 t + b) x
-  // the three parts; slot j & 1
-  const uint4* wbase = reinterpret_cast<const uint4*>(a.wx) + (size_t)(nb / 16) * KS * 64;
+  // the three parts; slot j & 1. A 1x1 conv: step j = b, the centre tap only (pack step b).
+  const uint4* wbase = reinterpret_cast<const uint4*>(a.wx) + (size_t)(nb / 16) * KST * 64;
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wbase), 0, 0x7fffffff, 0x00020000);
   const int pstride = (int)(a.part * 2);
   auto wload = [&](int ti, int part, int j) {
-    j = j < 3 * NCS ? j : 3 * NCS - 1;
-    const int s = (3 * (j % 3) + ti) * 8 + j / 3;
+    j = j < SPB * NCS ? j : SPB * NCS - 1;
+    const int s = KSZ == 3 ? (3 * (j % 3) + ti) * 8 + j / 3 : j;
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + s * 1024, 0));
   };
+  constexpr int T0 = KSZ == 3 ? 0 : 1, T1 = KSZ == 3 ? 3 : 2;  // the dx taps the ring holds
   bf16x8 bq[2][3][3];  // [step parity][dx tap][part]
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
-    for (int ti = 0; ti < 3; ++ti)
+    for (int ti = T0; ti < T1; ++ti)
 #pragma unroll
       for (int pt = 0; pt < 3; ++pt) bq[cc][ti][pt] = wload(ti, pt, cc);
 
@@ -609,46 +618,52 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
   // one 32-channel block: the (dy, source pixel) groups (x6t::kGroups), the next group's fragment read during the
   // current group's MFMAs; after a dy row's last group its ring slot is reloaded (step j + 2)
   auto block = [&](int b, auto par) {
-    constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (3 b + d)
+    constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (SPB b)
     bf16x8 fr[2][3];
-    frag(kGroups.src[0], fr[0]);
-    x6t_static_for<kGroups.n>([&](auto I) {
+    frag(G.src[0], fr[0]);
+    x6t_static_for<G.n>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      constexpr int d = kGroups.dy[i], sl = (P0 + d) & 1, cur = i & 1, cnt = kGroups.cnt[i];
-      if (i + 1 < kGroups.n) frag(kGroups.src[i + 1], fr[cur ^ 1]);
+      constexpr int d = G.dy[i], sl = (P0 + d) & 1, cur = i & 1, cnt = G.cnt[i];
+      if (i + 1 < G.n) frag(G.src[i + 1], fr[cur ^ 1]);
       const bf16x8* xs[6] = {&fr[cur][0], &fr[cur][1], &fr[cur][2], &fr[cur][0], &fr[cur][1], &fr[cur][0]};
       constexpr int wp[6] = {2, 1, 0, 1, 0, 0};  // per accumulator the small terms first (conv_x6p's order)
 #pragma unroll
       for (int k = 0; k < 6; ++k)
 #pragma unroll
         for (int o = 0; o < cnt; ++o)
-          acc[kGroups.out[i][o]] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][kGroups.dx[i][o]][wp[k]], *xs[k],
-                                                                           acc[kGroups.out[i][o]], 0, 0, 0);
+          acc[G.out[i][o]] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][G.dx[i][o]][wp[k]], *xs[k],
+                                                                     acc[G.out[i][o]], 0, 0, 0);
       __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 6 * cnt, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (kGroups.last[i]) {
+      if (G.last[i]) {
 #pragma unroll
-        for (int ti = 0; ti < 3; ++ti)
+        for (int ti = T0; ti < T1; ++ti)
 #pragma unroll
-          for (int pt = 0; pt < 3; ++pt) bq[sl][ti][pt] = wload(ti, pt, 3 * b + d + 2);
+          for (int pt = 0; pt < 3; ++pt) bq[sl][ti][pt] = wload(ti, pt, SPB * b + d + 2);
         __builtin_amdgcn_sched_barrier(0);
       }
     });
   };
 
   for (int b = 0; b < NCS; b += 2) {
-    block(b, std::integral_constant<int, 0>());  // 9 b even
+    block(b, std::integral_constant<int, 0>());  // SPB b even
     // block b + 1's raw rows: wait for this wave's LDS-DMA (older than every ring load of block b: all but the
-    // youngest 2 steps of ring loads may be waited on), then every wave's, then split
-    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    // youngest 2 steps of ring loads, 2 x 9 or 2 x 3, may be waited on), then every wave's, then split
+    if (KSZ == 3)
+      asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     __syncthreads();
     split();
     __syncthreads();
     if (b + 2 < NCS) stage(b + 2);
-    block(b + 1, std::integral_constant<int, 1>());  // 9 (b + 1) odd
+    block(b + 1, std::integral_constant<int, 1>());  // SPB (b + 1) odd (SPB = 3 or 1)
     if (b + 2 < NCS) {
-      asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+      if (KSZ == 3)
+        asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       __syncthreads();
       split();
       __syncthreads();
@@ -742,28 +757,29 @@ extern "C" {
 
 int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks) {
   X6Args g{};
-  if (ks == 3 && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128)) return 1;  // conv_x6t
+  if ((ks == 3 || ks == 1) && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128))
+    return 1;  // conv_x6t (the 4x5 latent; 3x3 and 1x1)
   return ks == 3 && H >= 2 && W >= 2 && Cout % 256 == 0 && x6_geometry(W, Cin, g) > 0 ? 1 : 0;
 }
 
 // gather = 1: a slot-gathered / strided input and / or an action-bias table (conv_x6t's GA instance: the 4x5
 // latent, Cin 256, Cout 256 / 128)
 int mzba_conv_x6_ex_supported(int H, int W, int Cin, int Cout, int ks, int gather) {
-  if (ks == 3 && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128)) return 1;
+  if ((ks == 3 || ks == 1) && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128)) return 1;
   return gather ? 0 : mzba_conv_x6_supported(H, W, Cin, Cout, ks);
 }
 
 int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx,
                     const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,
-                    int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream) {
+                    int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream) {
   MZ_CHECK_ARG(in && wx && bias && out && B > 0, -1);
   MZ_CHECK_ARG(!act_bias || (act && A > 0 && !res), -1);
   const bool ga = slot || act_bias || env_stride != (long long)H * W * Cin;
-  MZ_CHECK_ARG(mzba_conv_x6_ex_supported(H, W, Cin, Cout, 3, ga ? 1 : 0), -2);
+  MZ_CHECK_ARG(mzba_conv_x6_ex_supported(H, W, Cin, Cout, ks, ga ? 1 : 0), -2);
   const long long M = (long long)B * H * W;
   MZ_CHECK_ARG(M + 256 < (1LL << 31), -3);
   bool tiled = H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128);
-  if (tiled && !ga && Cout % 256 == 0 && g_x6_variant < 3) {
+  if (tiled && ks == 3 && !ga && Cout % 256 == 0 && g_x6_variant < 3) {
     // the pixel tiles where they load the busiest CU less (pixel-taps issued per CU) than conv_x6p's tiles
     X6Args ap{};
     const int tmp = g_x6_variant >= 1 ? x6p_geometry(W, Cin, M, ap) : 0;
@@ -774,13 +790,16 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
   }
   if (tiled) {
     X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx, bias, act_bias, act, A,
-              (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * 9 * Cin};
+              (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin};
     const dim3 grid((unsigned)((B + x6t::E - 1) / x6t::E), (unsigned)(Cout / 128));
     auto launch = [&](auto kern) {
       mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
       hipLaunchKernelGGL(kern, grid, dim3(x6::NT), x6t::LDS, stream, t);
     };
-    ga ? launch(conv_x6t_kernel<true>) : launch(conv_x6t_kernel<false>);
+    if (ks == 1)
+      launch(conv_x6t_kernel<false, 1>);  // the reward / value heads' 1x1 ConvBlocks (never gathered)
+    else
+      ga ? launch(conv_x6t_kernel<true, 3>) : launch(conv_x6t_kernel<false, 3>);
     MZ_LAUNCH_CHECK();
     return 0;
   }
@@ -793,7 +812,7 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
 int mzba_conv_x6(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
                  int Cin, int Cout, int relu, hipStream_t stream) {
   return mzba_conv_x6_ex(in, (long long)H * W * Cin, nullptr, 0, wx, bias, nullptr, nullptr, 0, res, out, B, H, W, Cin,
-                         Cout, relu, stream);
+                         Cout, 3, relu, stream);
 }
 
 }  // extern "C"

@@ -233,7 +233,7 @@ struct NetRunner : torch::CustomClassHolder {
         mzba_conv_x6_ex_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks, gather)) {
       check_rc(mzba_conv_x6_ex(in, env_stride, slot, slot_stride, vp(l.wx), vp<float>(l.b),
                                ab ? vp<float>(l.act_bias) : nullptr, ab ? act : nullptr, (int)l.A, res, out, (int)B,
-                               (int)H_, (int)W_, (int)l.cin, (int)l.cout, relu, s),
+                               (int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks, relu, s),
                "mzba_conv_x6_ex");
       return;
     }

@@ -112,7 +112,7 @@ class PackedNets:
         self.dyn = [self._res(sd, f"dyn_net.res_blocks.{i}", hw=lat)
                     for i in range(mcfg["dynamics_network"]["num_res_blocks"])]
         self.rew_conv = self._conv(sd["dyn_net.reward_head.0.conv.weight"], sd["dyn_net.reward_head.0.conv.bias"],
-                                   self._bn(sd, "dyn_net.reward_head.0.bn"))
+                                   self._bn(sd, "dyn_net.reward_head.0.bn"), hw=lat)
         self.rew_lin = self._linear(sd["dyn_net.reward_head.2.weight"], sd["dyn_net.reward_head.2.bias"], self.c1)
         # prediction (networks.py:190-223)
         self.pred = [self._res(sd, f"pred_net.res_blocks.{i}", hw=lat)
@@ -126,7 +126,7 @@ class PackedNets:
                                    self._bn(sd, "pred_net.policy_head.0.bn"), hw=lat)
         self.pol_lin = self._linear(sd["pred_net.policy_head.2.weight"], sd["pred_net.policy_head.2.bias"], self.c1 // 2)
         self.val_conv = self._conv(sd["pred_net.value_head.0.conv.weight"], sd["pred_net.value_head.0.conv.bias"],
-                                   self._bn(sd, "pred_net.value_head.0.bn"))
+                                   self._bn(sd, "pred_net.value_head.0.bn"), hw=lat)
         self.val_lin = self._linear(sd["pred_net.value_head.2.weight"], sd["pred_net.value_head.2.bias"], self.c1 // 2)
         self.fused = self._fused(sd, w[:, :cmain])
         self.rep_tail = self._rep_tail(sd)

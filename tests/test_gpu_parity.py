@@ -727,23 +727,25 @@ def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, relu, with_res):
     assert e6 <= 2 * e32 + 1e-7 * scale and e6 <= 2e-6 * scale, (e6 / scale, e32 / scale)
 
 
-@pytest.mark.parametrize("B,Cout,mode", [(4100, 256, "res"), (37, 256, "plain"), (4096, 128, "plain"),
-                                         (1000, 256, "gather"), (21, 128, "gather")])
-def test_conv_x6_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode):
+@pytest.mark.parametrize("B,Cout,mode,ks", [(4100, 256, "res", 3), (37, 256, "plain", 3), (4096, 128, "plain", 3),
+                                            (1000, 256, "gather", 3), (21, 128, "gather", 3), (4096, 256, "plain", 1),
+                                            (45, 128, "plain", 1)])
+def test_conv_x6_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks):
     """The pixel-tiled x6 conv at the 4x5 latent (conv_x6t: 16 envs x 20 pixels per workgroup, the zero-padding
     taps not issued, the input staged in 32-channel blocks by LDS-DMA) against an f64 conv of the same f32
-    operands: within 2x the f32-input MFMA conv's error + 1e-7 and within 2e-6 of the magnitude, and within 2e-6
-    of the pre-split form (the same products summed in another order: 4e-6, the sum of two such errors). Ragged batches (B % 16 != 0), Cout 128
-    (the policy head's conv), and the gathered form: each env's image read from a slot of a latent pool with the
-    action planes' folded [HW][A][Cout] bias table ((acc + act_bias) + bias, the f32 dynamics' first conv)."""
+    operands: within 2x the f32-input MFMA conv's error + 1e-7 and within 2e-6 of the magnitude, and within 4e-6
+    of the pre-split form (the same products summed in another order: the sum of two such errors). Ragged batches
+    (B % 16 != 0), Cout 128 (the policy head's conv), the gathered form (each env's image read from a slot of a
+    latent pool with the action planes' folded [HW][A][Cout] bias table, (acc + act_bias) + bias: the f32
+    dynamics' first conv), and ks = 1 (the reward / value heads' 1x1 ConvBlocks: the centre tap only)."""
     from mzba import _lib as L
     from mzba.agent import split_pack_x6
     H, W, Cin, A, S = 4, 5, 256, 3, 6
     g = torch.Generator(device="cuda").manual_seed(B + Cout)
     dev = torch.device("cuda")
-    w = torch.randn(Cout, 3, 3, Cin, generator=g, device=dev) / (Cin * 9) ** 0.5
+    w = torch.randn(Cout, ks, ks, Cin, generator=g, device=dev) / (Cin * ks * ks) ** 0.5
     b = torch.randn(Cout, generator=g, device=dev) * 0.1
-    wx = split_pack_x6(w.cpu().numpy().reshape(Cout, -1), Cout, 3, Cin).cuda()
+    wx = split_pack_x6(w.cpu().numpy().reshape(Cout, -1), Cout, ks, Cin).cuda()
     relu = 1 if mode != "plain" else 0
     res = tab = act = slot = None
     if mode == "gather":
@@ -759,32 +761,32 @@ def test_conv_x6_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode):
         if mode == "res":
             res = torch.rand(B, H, W, Cout, generator=g, device=dev)
     ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), b.double(),
-                                     padding=1).permute(0, 2, 3, 1)
+                                     padding=ks // 2).permute(0, 2, 3, 1)
     if res is not None:
         ref = ref + res.double()
     if tab is not None:
         ref = ref + tab.double()[:, act.long()].permute(1, 0, 2).reshape(B, H, W, Cout)
     if relu:
         ref = torch.relu(ref)
-    assert L.lib().mzba_conv_x6_ex_supported(H, W, Cin, Cout, 3, int(mode == "gather"))
+    assert L.lib().mzba_conv_x6_ex_supported(H, W, Cin, Cout, ks, int(mode == "gather"))
     out = torch.full((B, H, W, Cout), float("nan"), device=dev)
     try:
         assert L.lib().mzba_conv_x6_set_variant(3) == 0
         L.call("mzba_conv_x6_ex", L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(wx), L.ptr(b), L.ptr(tab),
-               L.ptr(act), A if tab is not None else 0, L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu, L.stream())
+               L.ptr(act), A if tab is not None else 0, L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, ks, relu, L.stream())
     finally:
         L.lib().mzba_conv_x6_set_variant(2)
     # the f32-input MFMA conv (conv_igemm, the f32 path's form before x6) on the same gathered operands
     f32 = torch.empty(B, H, W, Cout, device=dev)
     wd = w.reshape(Cout, -1).contiguous()
     L.call("mzba_conv2d", 0, L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(wd), L.ptr(b), L.ptr(tab), L.ptr(act),
-           A if tab is not None else 0, L.ptr(res), L.ptr(f32), B, H, W, Cin, Cout, 3, relu, L.stream())
+           A if tab is not None else 0, L.ptr(res), L.ptr(f32), B, H, W, Cin, Cout, ks, relu, L.stream())
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
     scale = ref.abs().max().item()
     et, e32 = (out.double() - ref).abs().max().item(), (f32.double() - ref).abs().max().item()
     msg = f"conv_x6t B={B} Cout={Cout} {mode}: max err vs f64 {et / scale:.2e} of the magnitude, f32 MFMA conv {e32 / scale:.2e}"
-    if mode != "gather" and Cout == 256:  # the pre-split halo form on the same contiguous operands
+    if mode != "gather" and Cout == 256 and ks == 3:  # the pre-split halo form on the same contiguous operands
         try:
             assert L.lib().mzba_conv_x6_set_variant(1) == 0
             outp = torch.full_like(out, float("nan"))
@@ -1589,3 +1591,50 @@ def test_fp16_dynamics_step(B, variant):
         e16 = (res["fp16"][i] - res["f32"][i]).abs().max().item()
         eb = (res["bf16"][i] - res["f32"][i]).abs().max().item()
         assert torch.isfinite(res["fp16"][i]).all() and e16 <= max(eb, 1e-2), (nm, e16, eb)
+
+
+def test_f32_heads_bit_identical_to_their_sum_order():
+    """mzba_heads (f32 parity path: the Linear heads + softmax / support decode, networks.py:138-149, 200-223,
+    utils.py:74-81) with several envs per workgroup (round 5: the weights read once per 8 envs, not per env) keeps
+    each env's f32 sum order: thread t accumulates k = t, t + 256, ... in sequence, the wave's xor-shuffle tree,
+    then ((w0 + w1) + (w2 + w3)) + bias. The logits equal a numpy f32 emulation of exactly that order bit for bit
+    (ragged B), two heads per launch (value: support decode; policy: softmax)."""
+    from mzba import _lib as L
+    g = np.random.default_rng(5)
+    B = 37
+    heads = [(5120, 11, 1), (2560, 3, 0)]
+    xs = [g.standard_normal((B, K)).astype(np.float32) for K, _, _ in heads]
+    ws = [(g.standard_normal((O, K)) * 0.02).astype(np.float32) for K, O, _ in heads]
+    bs = [g.standard_normal(O).astype(np.float32) * 0.1 for _, O, _ in heads]
+
+    def emulate(x, w, b):
+        K, O = w.shape
+        out = np.zeros((x.shape[0], O), np.float32)
+        for e in range(x.shape[0]):
+            for o in range(O):
+                part = np.zeros(256, np.float32)
+                for k0 in range(0, K, 256):
+                    part = (part + (x[e, k0:k0 + 256] * w[o, k0:k0 + 256]).astype(np.float32)).astype(np.float32)
+                waves = []
+                for wv in range(4):
+                    v = part[64 * wv:64 * (wv + 1)].copy()
+                    for s in (32, 16, 8, 4, 2, 1):
+                        v = (v + v[np.arange(64) ^ s]).astype(np.float32)
+                    waves.append(v[0])
+                r = np.float32(np.float32(waves[0] + waves[1]) + np.float32(waves[2] + waves[3]))
+                out[e, o] = np.float32(r + b[o])
+        return out
+
+    dx = [torch.as_tensor(x, device="cuda") for x in xs]
+    dw = [torch.as_tensor(w, device="cuda") for w in ws]
+    db = [torch.as_tensor(b, device="cuda") for b in bs]
+    lg = [torch.empty(B, O, device="cuda") for _, O, _ in heads]
+    dec = [torch.empty(B, device="cuda"), torch.empty(B, 3, device="cuda")]
+    L.call("mzba_heads", 0, 2, L.ptr(dx[0]), L.ptr(dw[0]), L.ptr(db[0]), 5120, 11, 1, L.ptr(lg[0]), L.ptr(dec[0]),
+           L.ptr(dx[1]), L.ptr(dw[1]), L.ptr(db[1]), 2560, 3, 0, L.ptr(lg[1]), L.ptr(dec[1]), -5.0, 5.0, B, L.stream())
+    torch.cuda.synchronize()
+    for i in range(2):
+        want = emulate(xs[i], ws[i], bs[i])
+        np.testing.assert_array_equal(lg[i].cpu().numpy().view(np.uint32), want.view(np.uint32))
+    p = torch.softmax(lg[1], 1)
+    torch.testing.assert_close(dec[1], p, rtol=1e-6, atol=1e-7)
