@@ -1608,7 +1608,7 @@ def test_f32_heads_bit_identical_to_their_sum_order():
     bs = [g.standard_normal(O).astype(np.float32) * 0.1 for _, O, _ in heads]
 
     def emulate(x, w, b):
-        K, O = w.shape
+        O, K = w.shape
         out = np.zeros((x.shape[0], O), np.float32)
         for e in range(x.shape[0]):
             for o in range(O):
