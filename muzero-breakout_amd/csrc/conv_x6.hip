@@ -253,27 +253,31 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6_kernel(X6Args a) {
 // to conv_x6_kernel.
 MZ_DEV int pkey(int r) { return ((r << 1) & 6) | (((r >> 2) & 1) * 9); }  // = conv_halo.hip hkey
 
-template <int CIN, int TM>
+// CT: 16-channel column tiles per wave (2: 256 output channels per workgroup; 1: 128, the Cout 128 convs). NBLK:
+// the input channels staged in NBLK blocks of CIN / NBLK (round 5: the 16x20 Cin-256 convs in two 128-channel blocks,
+// so a 160-pixel tile's 1.5x rows fit — one block took 48-pixel tiles there, each streaming all 3.5 MB of weight
+// parts, the L2 weight stream then bounding it); NBLK > 1 sums (block, tap, channel step) in that order.
+template <int CIN, int TM, int CT = 2, int NBLK = 1>
 __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
-  constexpr int PB = CIN * 2;        // bytes per plane row (bf16)
+  constexpr int CB = CIN / NBLK;     // channels per staged block
+  constexpr int PB = CB * 2;         // bytes per plane row (bf16)
   constexpr int RB = 3 * PB;         // bytes per staged row: hi | mid | lo
-  constexpr int NC8 = CIN / 8;       // 8-channel chunks per row
-  constexpr int NCS = CIN / 32;      // 32-channel k steps per tap
-  constexpr int CT = 2;              // column tiles per wave (32 channels)
+  constexpr int NC8 = CB / 8;        // 8-channel chunks per row
+  constexpr int NCS = CB / 32;       // 32-channel k steps per tap and block
   constexpr int MT = TM / 16;        // pixel tiles per wave: all of the workgroup's
-  static_assert(NCS % 2 == 0 && TM % 16 == 0 && MT <= 8, "ring slot = step parity; whole pixel tiles");
-  constexpr int nsteps = 9 * NCS;
+  static_assert(NCS % 2 == 0 && TM % 16 == 0 && MT <= 10, "ring slot = step parity; whole pixel tiles");
+  constexpr int nsteps = NBLK * 9 * NCS;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, n = lane & 15;
-  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * x6::TN;
+  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * (128 * CT);
   const int HW = a.H * a.W;
   const int HR = TM + 2 * a.HALO;
 
   for (int i = tid; i < RB / 16; i += x6::NT) *reinterpret_cast<uint4*>(lds + a.ZOFF + i * 16) = make_uint4(0, 0, 0, 0);
 
-  const int prow0 = n + a.HALO;
+  int prow0 = n + a.HALO;
   uint32_t okw[(MT + 3) / 4] = {};
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
@@ -289,8 +293,11 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
   const uint4* wbase = reinterpret_cast<const uint4*>(a.wx) + (size_t)(n0 / 16 + wave * CT) * KS * 64;
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wbase), 0, 0x7fffffff, 0x00020000);
   const int pstride = (int)(a.part * 2);
-  auto wload = [&](int ct, int part, int s) {
-    s = s < nsteps ? s : nsteps - 1;
+  // loop step j = (block, tap, channel step) -> pack k step tap * CIN / 32 + block * NCS + c
+  auto wload = [&](int ct, int part, int j) {
+    j = j < nsteps ? j : nsteps - 1;
+    const int blk = j / (9 * NCS), r = j - blk * 9 * NCS, t = r / NCS, c = r - t * NCS;
+    const int s = t * (CIN / 32) + blk * NCS + c;
     return __builtin_bit_cast(bf16x8,
                               __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + (ct * KS + s) * 1024, 0));
   };
@@ -308,35 +315,36 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) acc[mi][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // staging: item g = (row, 8-channel chunk); 8 f32 loaded, split, written as one chunk per plane. Loads of a
-  // batch of 8 items are all issued before its first split.
+  // staging of block blk: item g = (row, 8-channel chunk); 8 f32 loaded, split, written as one chunk per plane.
+  // Loads of a batch of 8 items are all issued before its first split.
   const int items = HR * NC8;
-  for (int g0 = 0; g0 < items; g0 += 8 * x6::NT) {
-    uint4 v[8][2];
+  auto stage = [&](int blk) {
+    for (int g0 = 0; g0 < items; g0 += 8 * x6::NT) {
+      uint4 v[8][2];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int g = min(g0 + u * x6::NT + tid, items - 1), r = g / NC8, s8 = g - r * NC8;
-      int m = m0 - a.HALO + r;
-      m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);
-      const float* src = a.in + (size_t)m * CIN + s8 * 8;
-      v[u][0] = *reinterpret_cast<const uint4*>(src);
-      v[u][1] = *reinterpret_cast<const uint4*>(src + 4);
-    }
+      for (int u = 0; u < 8; ++u) {
+        const int g = min(g0 + u * x6::NT + tid, items - 1), r = g / NC8, s8 = g - r * NC8;
+        int m = m0 - a.HALO + r;
+        m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);
+        const float* src = a.in + (size_t)m * CIN + blk * CB + s8 * 8;
+        v[u][0] = *reinterpret_cast<const uint4*>(src);
+        v[u][1] = *reinterpret_cast<const uint4*>(src + 4);
+      }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int g = g0 + u * x6::NT + tid;
-      if (g < items) {
-        const int r = g / NC8, s8 = g - r * NC8;
-        bf16x8 h, mm, l;
-        split8(v[u][0], v[u][1], h, mm, l);
-        uint8_t* row = lds + r * RB + ((s8 ^ pkey(r)) << 4);
-        *reinterpret_cast<bf16x8*>(row) = h;
-        *reinterpret_cast<bf16x8*>(row + PB) = mm;
-        *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+      for (int u = 0; u < 8; ++u) {
+        const int g = g0 + u * x6::NT + tid;
+        if (g < items) {
+          const int r = g / NC8, s8 = g - r * NC8;
+          bf16x8 h, mm, l;
+          split8(v[u][0], v[u][1], h, mm, l);
+          uint8_t* row = lds + r * RB + ((s8 ^ pkey(r)) << 4);
+          *reinterpret_cast<bf16x8*>(row) = h;
+          *reinterpret_cast<bf16x8*>(row + PB) = mm;
+          *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+        }
       }
     }
-  }
-  __syncthreads();
+  };
 
   // fragment of pixel tile mi, channel step c at tap t: chunk 4c + q of the three planes of its row (the zero row
   // for a tap leaving the image; its bank slots collide with at most a few lanes', measured neutral for conv_x6)
@@ -350,41 +358,52 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
     for (int pt = 0; pt < 3; ++pt) f[pt] = *reinterpret_cast<const bf16x8*>(lds + base + pt * PB);
   };
   constexpr int NF = MT * NCS;
-  bf16x8 fr[2][3];  // rolling: fragment i + 1 read during fragment i's MFMAs
-  frag(0, 0, 0, fr[0]);
   int j = 0;
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
+  for (int blk = 0; blk < NBLK; ++blk) {
+    if (blk > 0) __syncthreads();  // every wave is done with the previous block's rows
+    if (NBLK > 1) {  // opaque per block: the fragment addresses CSE'd across the unrolled blocks spill (conv_halo.hip)
+      asm volatile("" : "+v"(prow0));
 #pragma unroll
-    for (int c = 0; c < NCS; ++c) {
-      const int sl = c & 1;
-      const int sn = j + 2;
+      for (int i = 0; i < (MT + 3) / 4; ++i) asm volatile("" : "+v"(okw[i]));
+    }
+    stage(blk);
+    __syncthreads();
+    bf16x8 fr[2][3];  // rolling: fragment i + 1 read during fragment i's MFMAs
+    frag(0, 0, 0, fr[0]);
 #pragma unroll
-      for (int mi = 0; mi < MT; ++mi) {
-        const int idx = c * MT + mi, nx = idx + 1;
-        // the flat fragment index parity picks the buffer: NF may be odd, so count across taps
-        const int cur = (t * NF + idx) & 1, nxt = cur ^ 1;
-        if (nx < NF)
-          frag(t, nx / MT, nx % MT, fr[nxt]);
-        else if (t < 8)
-          frag(t + 1, 0, 0, fr[nxt]);
-        const bf16x8* xs[6] = {&fr[cur][0], &fr[cur][1], &fr[cur][2], &fr[cur][0], &fr[cur][1], &fr[cur][0]};
-        constexpr int wp[6] = {2, 1, 0, 1, 0, 0};  // per accumulator the small terms first, as conv_x6_kernel
+    for (int t = 0; t < 9; ++t) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
+      for (int c = 0; c < NCS; ++c) {
+        const int sl = c & 1;
+        const int sn = j + 2;
 #pragma unroll
-          for (int ct = 0; ct < CT; ++ct)
-            acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][wp[k]][ct], *xs[k], acc[mi][ct], 0, 0, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-        __builtin_amdgcn_sched_group_barrier(0x008, 6 * CT, 0);
+        for (int mi = 0; mi < MT; ++mi) {
+          const int idx = c * MT + mi, nx = idx + 1;
+          // the flat fragment index parity picks the buffer: NF may be odd, so count across taps
+          const int cur = (t * NF + idx) & 1, nxt = cur ^ 1;
+          if (nx < NF)
+            frag(t, nx / MT, nx % MT, fr[nxt]);
+          else if (t < 8)
+            frag(t + 1, 0, 0, fr[nxt]);
+          const bf16x8* xs[6] = {&fr[cur][0], &fr[cur][1], &fr[cur][2], &fr[cur][0], &fr[cur][1], &fr[cur][0]};
+          constexpr int wp[6] = {2, 1, 0, 1, 0, 0};  // per accumulator the small terms first, as conv_x6_kernel
+#pragma unroll
+          for (int k = 0; k < 6; ++k)
+#pragma unroll
+            for (int ct = 0; ct < CT; ++ct)
+              acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][wp[k]][ct], *xs[k], acc[mi][ct], 0, 0, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 6 * CT, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct) bq[sl][pt][ct] = wload(ct, pt, sn);
         __builtin_amdgcn_sched_barrier(0);
+        ++j;
       }
-#pragma unroll
-      for (int pt = 0; pt < 3; ++pt)
-#pragma unroll
-        for (int ct = 0; ct < CT; ++ct) bq[sl][pt][ct] = wload(ct, pt, sn);
-      __builtin_amdgcn_sched_barrier(0);
-      ++j;
     }
   }
 
@@ -717,20 +736,35 @@ int x6p_ncu() {
   return ncu;
 }
 
-// pre-split geometry for (W, Cin, M pixels): among the tiles whose 1.5x rows fit the LDS, the one that loads the
-// busiest CU least (ceil(tiles / CUs) x TM; the larger tile on a tie); 0 if none fits
-int x6p_geometry(int W, int Cin, long long M, X6Args& g) {
-  if (Cin != 128 && Cin != 256) return 0;
-  int best = 0;
-  long long best_load = 0;
-  for (int tm : {128, 112, 96, 80, 64, 48}) {
-    const int halo = W + 1, hr = tm + 2 * halo, rb = 3 * Cin * 2;
-    if ((long long)(hr + 1) * rb > x6::LDS_MAX) continue;
-    const long long load = ((M + tm - 1) / tm + x6p_ncu() - 1) / x6p_ncu() * tm;
-    if (!best || load < best_load) best = tm, best_load = load;
-  }
-  if (!best) return 0;
-  g.HALO = W + 1, g.NI = 0, g.ZOFF = (best + 2 * (W + 1)) * 3 * Cin * 2;
+// pre-split geometry for (W, Cin, Cout, M pixels): a tile TM, the staged channel blocks NBLK and the 16-channel column
+// tiles per wave CT (Cout = 128 CT per workgroup). Among the candidates whose 1.5x rows fit the LDS, the one whose
+// busiest CU finishes first: rounds x max(its MFMA time, its weight stream: every tile streams all three weight parts
+// of its 128 CT channels from L2 at ~67 GB/s per CU, profiles/l2_stream.json), x 1.05 for a second staging. One
+// block and CT 2 everywhere up to round 4; at W >= 16 (the 16x20 representation convs: 2 (W + 1) halo rows per tile)
+// also TM 160 in two 128-channel blocks (Cin 256) or one (Cin 128), and Cout 128 (CT 1). 0 if nothing fits.
+struct X6PGeo {
+  int tm = 0, nblk = 1, ct = 2;
+};
+X6PGeo x6p_geometry(int W, int Cin, int Cout, long long M, X6Args& g) {
+  X6PGeo best{};
+  if ((Cin != 128 && Cin != 256) || (Cout % 256 != 0 && !(Cout == 128 && Cin == 128 && W >= 16))) return best;
+  double best_cost = 0;
+  const int ct = Cout % 256 == 0 ? 2 : 1;
+  const long long ncu = x6p_ncu();
+  auto consider = [&](int tm, int nblk) {
+    const int halo = W + 1, hr = tm + 2 * halo, rb = 3 * (Cin / nblk) * 2;
+    if ((long long)(hr + 1) * rb > x6::LDS_MAX) return;
+    const long long rounds = ((M + tm - 1) / tm * (Cout / (128 * ct)) + ncu - 1) / ncu;
+    const double mfma_ns = tm * 9.0 * Cin * 128 * ct * 2 * 6 / 9.77e3;  // 2.5 PF / 256 CUs, ns
+    const double wgt_ns = 3.0 * 128 * ct * 9 * Cin * 2 / 66.7;
+    const double cost = rounds * (mfma_ns > wgt_ns ? mfma_ns : wgt_ns) * (nblk > 1 ? 1.05 : 1.0);
+    if (!best.tm || cost < best_cost) best.tm = tm, best.nblk = nblk, best.ct = ct, best_cost = cost;
+  };
+  if (ct == 2)
+    for (int tm : {128, 112, 96, 80, 64, 48}) consider(tm, 1);
+  if (W >= 16) consider(160, Cin == 256 ? 2 : 1);
+  if (!best.tm) return best;
+  g.HALO = W + 1, g.NI = 0, g.ZOFF = (best.tm + 2 * (W + 1)) * 3 * (Cin / best.nblk) * 2;
   return best;
 }
 
@@ -759,6 +793,8 @@ int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks) {
   X6Args g{};
   if ((ks == 3 || ks == 1) && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128))
     return 1;  // conv_x6t (the 4x5 latent; 3x3 and 1x1)
+  if (ks == 3 && H >= 2 && Cout == 128 && Cin == 128 && W >= 16)
+    return x6p_geometry(W, Cin, Cout, (long long)H * W, g).tm > 0 ? 1 : 0;  // the pre-split form's CT 1 instance
   return ks == 3 && H >= 2 && W >= 2 && Cout % 256 == 0 && x6_geometry(W, Cin, g) > 0 ? 1 : 0;
 }
 
@@ -782,7 +818,7 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
   if (tiled && ks == 3 && !ga && Cout % 256 == 0 && g_x6_variant < 3) {
     // the pixel tiles where they load the busiest CU less (pixel-taps issued per CU) than conv_x6p's tiles
     X6Args ap{};
-    const int tmp = g_x6_variant >= 1 ? x6p_geometry(W, Cin, M, ap) : 0;
+    const int tmp = g_x6_variant >= 1 ? x6p_geometry(W, Cin, Cout, M, ap).tm : 0;
     const long long ncu = x6p_ncu(), t16 = (B + x6t::E - 1) / x6t::E;
     const long long load_t = (2 * t16 + ncu - 1) / ncu * x6t::E * kPairs.n / 2;  // two 128-channel halves
     const long long load_p = tmp ? ((M + tmp - 1) / tmp + ncu - 1) / ncu * tmp * 9 : load_t + 1;
@@ -821,22 +857,29 @@ namespace {
 // the halo-staged forms (conv_x6p_kernel, else conv_x6_kernel) on contiguous images, Cout % 256 == 0
 int x6_halo_launch(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
                    int Cin, int Cout, int relu, hipStream_t stream) {
-  X6Args g0{};
-  MZ_CHECK_ARG(Cout % 256 == 0 && H >= 2 && W >= 2 && x6_geometry(W, Cin, g0) > 0, -2);
   const long long M = (long long)B * H * W;
   MZ_CHECK_ARG(M + 256 < (1LL << 31), -3);  // pixel indices in int (global offsets are size_t)
   X6Args a{(const float*)in, (const bf16_t*)wx, bias, (const float*)res, (float*)out, (int)M, H, W, Cin, Cout, relu};
   a.part = (long long)Cout * 9 * Cin;
   X6Args ap = a;
-  const int tmp = g_x6_variant >= 1 ? x6p_geometry(W, Cin, M, ap) : 0;
-  if (tmp == 128 || tmp == 112 || tmp == 96 || tmp == 80 || tmp == 64 || tmp == 48) {
-    const int ldsp = ap.ZOFF + 3 * Cin * 2;
-    const dim3 gridp((unsigned)((M + tmp - 1) / tmp), (unsigned)(Cout / x6::TN));
+  // the pre-split form (the Cout 128 instance has no per-read-split twin: taken whatever the A/B variant)
+  const X6PGeo geo = (g_x6_variant >= 1 || Cout == 128) ? x6p_geometry(W, Cin, Cout, M, ap) : X6PGeo{};
+  const int tmp = geo.tm;
+  if (tmp) {
+    const int ldsp = ap.ZOFF + 3 * (Cin / geo.nblk) * 2;
+    const dim3 gridp((unsigned)((M + tmp - 1) / tmp), (unsigned)(Cout / (128 * geo.ct)));
     auto launchp = [&](auto kern) {
       mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
       hipLaunchKernelGGL(kern, gridp, dim3(x6::NT), ldsp, stream, ap);
     };
-    if (Cin == 256) {
+    if (tmp == 160) {  // the 16x20 instances
+      if (Cin == 256)
+        launchp(conv_x6p_kernel<256, 160, 2, 2>);
+      else if (geo.ct == 2)
+        launchp(conv_x6p_kernel<128, 160, 2, 1>);
+      else
+        launchp(conv_x6p_kernel<128, 160, 1, 1>);
+    } else if (Cin == 256) {
       switch (tmp) {
         case 128: launchp(conv_x6p_kernel<256, 128>); break;
         case 112: launchp(conv_x6p_kernel<256, 112>); break;
@@ -858,6 +901,8 @@ int x6_halo_launch(const void* in, const void* wx, const float* bias, const void
     MZ_LAUNCH_CHECK();
     return 0;
   }
+  X6Args g0{};
+  MZ_CHECK_ARG(Cout % 256 == 0 && H >= 2 && W >= 2 && x6_geometry(W, Cin, g0) > 0, -2);
   const int tm = x6_geometry(W, Cin, a);
   const int lds = a.ZOFF + 16 * Cin * 4;
   const dim3 grid((unsigned)((M + tm - 1) / tm), (unsigned)(Cout / x6::TN));

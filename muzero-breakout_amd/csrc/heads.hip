@@ -40,6 +40,9 @@ __global__ __launch_bounds__(256) void heads_kernel(HeadArgs a, int B) {
     for (int e = 0; e < EPB; ++e)
 #pragma unroll
       for (int o = 0; o < MAXO; ++o) acc[e][o] = 0.f;
+    // four k iterations' loads in flight (a rolled loop waited one memory round trip per iteration); per env and
+    // output the adds stay in k order
+#pragma unroll 4
     for (int k = tid; k < K; k += 256) {
       float xv[EPB];
 #pragma unroll

@@ -680,17 +680,21 @@ def test_conv_halo_gather_action_bias_vs_torch_fp32(B, S, A):
     assert not L.lib().mzba_conv_halo_ex_supported(4, 5, Cin, Cout, 3, 1)
 
 
-@pytest.mark.parametrize("B,H,W,Cin,relu,with_res", [(1000, 4, 5, 256, 1, True), (37, 4, 5, 256, 0, False),
-                                                     (7, 16, 20, 128, 1, True), (3, 21, 21, 256, 1, True)])
-def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, relu, with_res):
+@pytest.mark.parametrize("B,H,W,Cin,Cout,relu,with_res,same_order",
+                         [(1000, 4, 5, 256, 256, 1, True, True), (37, 4, 5, 256, 256, 0, False, True),
+                          (7, 16, 20, 128, 256, 1, True, True), (3, 21, 21, 256, 256, 1, True, True),
+                          (512, 16, 20, 256, 256, 1, True, False), (512, 16, 20, 128, 128, 1, True, True)])
+def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, Cout, relu, with_res, same_order):
     """mzba_conv_x6 (the f32 parity path's latent convs as six split-bf16 MFMA products each) against an f64
     conv of the same f32 operands: at least as close as the f32-input MFMA conv of the f32 path (mzba_conv2d
     dtype 0) — within 2x its error + 1e-7 of the magnitude — and within 2e-6 of the magnitude absolutely
     (ragged tiles, tiles crossing envs, every tap that leaves the image); the pre-split form (default) and the
-    per-read-split kernel bit-identical."""
+    per-read-split kernel bit-identical where both sum (tap, channel step) in order (same_order); round 5's 16x20
+    instances: Cin 256 staged in two 128-channel blocks (160-pixel tiles; sums (block, tap, step): within 4e-6 of
+    the per-read-split kernel), Cout 128 (the representation's 128-channel blocks; no per-read-split twin, the A/B
+    variant 0 runs the same instance)."""
     from mzba import _lib as L
     from mzba.agent import split_pack_x6
-    Cout = 256
     assert L.lib().mzba_conv_x6_supported(H, W, Cin, Cout, 3)
     g = torch.Generator(device="cuda").manual_seed(B + Cin + W)
     dev = torch.device("cuda")
@@ -720,8 +724,11 @@ def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, relu, with_res):
            B, H, W, Cin, Cout, 3, relu, L.stream())
     torch.cuda.synchronize()
     assert torch.isfinite(out).all()
-    assert torch.equal(out, out2)
     scale = ref.abs().max().item()
+    if same_order:
+        assert torch.equal(out, out2)
+    else:
+        assert (out - out2).abs().max().item() <= 4e-6 * scale
     e6, e32 = (out.double() - ref).abs().max().item(), (f32.double() - ref).abs().max().item()
     print(f"conv_x6 {B}x{H}x{W} {Cin}: max err vs f64 {e6 / scale:.2e} of the magnitude, f32 MFMA conv {e32 / scale:.2e}")
     assert e6 <= 2 * e32 + 1e-7 * scale and e6 <= 2e-6 * scale, (e6 / scale, e32 / scale)
