@@ -360,6 +360,8 @@ int mzba_scale_state(int dtype, const void* h, void* out, void* pool, long long 
 int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const float* b0, int K0, int O0, int dec0,
                float* logits0, float* out0, const void* x1, const float* w1, const float* b1, int K1, int O1,
                int dec1, float* logits1, float* out1, float smin, float smax, int B, hipStream_t stream);
+/* f32 heads: 1 (default) the f32-MFMA form (16 envs per workgroup; K % 16 == 0), 0 the per-thread FMA form (A/B). */
+int mzba_heads_set_variant(int v);
 
 /* ScalarTransforms.inverted_softmax_expectation (utils.py:74-81) on rows x n f32 logits. */
 int mzba_support_decode(const float* logits, float* out, int rows, int n, float smin, float smax, hipStream_t stream);

@@ -156,6 +156,70 @@ __global__ __launch_bounds__(512) void heads_mfma_kernel(HeadArgsB a) {
   }
 }
 
+// f32 path (round 5): the heads as an f32 MFMA GEMM (v_mfma_f32_16x16x4_f32, the f32 convs' arithmetic: f32
+// products accumulated in f32), 16 envs x 16 (padded) outputs per workgroup, 8 waves splitting K. A lane loads
+// 4 consecutive k (16 B) of its env row and of its output's weight row; MFMA i of a 16-k step sums k = 16 s + 4 q + i
+// over the four lane quarters q. The one-env-per-workgroup FMA form (heads_kernel) spent its time in 128 xor-shuffle
+// reduction chains per launch (123 us at B = 4096 vs ~20 us of HBM reads).
+__global__ __launch_bounds__(512) void heads_mfma_f32_kernel(HeadArgs a, int B) {
+  __shared__ float part[8][16][17];
+  __shared__ float lg[2][16][MAXO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int e0 = blockIdx.x * 16;
+  const int el = lane & 15, q = lane >> 4;
+  for (int hd = 0; hd < a.nheads; ++hd) {
+    const int K = a.K[hd], O = a.O[hd];
+    const int env = min(e0 + el, B - 1);
+    const float* xr = (const float*)a.x[hd] + (size_t)env * K;
+    const float* wr = a.w[hd] + (size_t)min(el, O - 1) * K;
+    const bool wok = el < O;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int ns = K / 16;
+    for (int s = wave; s < ns; s += 8) {
+      const int k = s * 16 + q * 4;
+      const float4 xv = *reinterpret_cast<const float4*>(xr + k);
+      float4 wv = *reinterpret_cast<const float4*>(wr + k);
+      if (!wok) wv = make_float4(0.f, 0.f, 0.f, 0.f);
+      // D[row = env][col = output]: A = activations (row el), B = weights (col el)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, wv.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, wv.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.z, wv.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.w, wv.w, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) part[wave][4 * q + i][el] = acc[i];
+    __syncthreads();
+    if (tid < 256) {
+      const int e = tid >> 4, o = tid & 15;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v = v + part[w][e][o];
+      if (o < O) lg[hd][e][o] = v + a.bias[hd][o];
+    }
+    __syncthreads();
+  }
+  if (tid < 16 * a.nheads) {
+    const int hd = tid >> 4, e = tid & 15, b = e0 + e;
+    if (b < B) {
+      const int O = a.O[hd];
+      float l[MAXO];
+      for (int o = 0; o < O; ++o) {
+        l[o] = lg[hd][e][o];
+        if (a.logits[hd]) a.logits[hd][(size_t)b * O + o] = l[o];
+      }
+      if (a.decode[hd] == 0) {
+        float m = l[0];
+        for (int o = 1; o < O; ++o) m = fmaxf(m, l[o]);
+        float ex[MAXO], sm = 0.f;
+        for (int o = 0; o < O; ++o) { ex[o] = expf(l[o] - m); sm = sm + ex[o]; }
+        for (int o = 0; o < O; ++o) a.dec[hd][(size_t)b * O + o] = ex[o] / sm;
+      } else {
+        a.dec[hd][b] = decode_support(l, O, a.smin, a.smax);
+      }
+    }
+  }
+}
+
 // ScalarTransforms.inverted_softmax_expectation over rows of n logits (utils.py:74-81)
 __global__ void support_decode_kernel(const float* __restrict__ logits, float* __restrict__ out, int rows, int n,
                                       float smin, float smax) {
@@ -168,7 +232,15 @@ __global__ void support_decode_kernel(const float* __restrict__ logits, float* _
 
 }  // namespace
 
+static int g_heads_mfma = 1;  // f32 heads: 1 the MFMA form (default), 0 the FMA form (heads_kernel; A/B, tests)
+
 extern "C" {
+
+int mzba_heads_set_variant(int v) {
+  if (v != 0 && v != 1) return -1;
+  g_heads_mfma = v;
+  return 0;
+}
 
 int mzba_support_decode(const float* logits, float* out, int rows, int n, float smin, float smax,
                         hipStream_t stream) {
@@ -206,6 +278,8 @@ int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const flo
   const dim3 grid((unsigned)((B + EPB - 1) / EPB));
   if (dtype)
     hipLaunchKernelGGL((heads_kernel<bf16_t, EPB>), grid, dim3(256), 0, stream, a, B);
+  else if (g_heads_mfma && K0 % 16 == 0 && (nheads == 1 || K1 % 16 == 0))
+    hipLaunchKernelGGL(heads_mfma_f32_kernel, dim3((B + 15) / 16), dim3(512), 0, stream, a, B);
   else
     hipLaunchKernelGGL((heads_kernel<float, EPB>), grid, dim3(256), 0, stream, a, B);
   MZ_LAUNCH_CHECK();

@@ -68,6 +68,7 @@ SIGNATURES = {
     "mzba_scale_state": [I, P, P, P, LL, P, I, LL, I, I, P],
     "mzba_heads": [I, I, P, P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, F, I, P],
     "mzba_support_decode": [P, P, I, I, F, F, P],
+    "mzba_heads_set_variant": [I],
     "mzba_heads_bf16": [I, P, P, P, I, I, I, P, P, P, P, P, I, I, I, P, P, F, F, I, P],
     "mzba_mcts_node_bytes": [],
     "mzba_mcts_root": [P, P, P, P, P, P, P, P, P, I, I, I, I, U64, P, P, P, P, P, F, F, P, F, P],

@@ -1602,10 +1602,12 @@ def test_fp16_dynamics_step(B, variant):
 
 def test_f32_heads_bit_identical_to_their_sum_order():
     """mzba_heads (f32 parity path: the Linear heads + softmax / support decode, networks.py:138-149, 200-223,
-    utils.py:74-81) with several envs per workgroup (round 5: the weights read once per 8 envs, not per env) keeps
-    each env's f32 sum order: thread t accumulates k = t, t + 256, ... in sequence, the wave's xor-shuffle tree,
-    then ((w0 + w1) + (w2 + w3)) + bias. The logits equal a numpy f32 emulation of exactly that order bit for bit
-    (ragged B), two heads per launch (value: support decode; policy: softmax)."""
+    utils.py:74-81). The FMA form (variant 0) with several envs per workgroup (round 5: the weights read once per 8
+    envs, not per env) keeps each env's f32 sum order: thread t accumulates k = t, t + 256, ... in sequence, the
+    wave's xor-shuffle tree, then ((w0 + w1) + (w2 + w3)) + bias — the logits equal a numpy f32 emulation of exactly
+    that order bit for bit (ragged B), two heads per launch (value: support decode; policy: softmax). The f32-MFMA
+    form (default since round 5: 16 envs per workgroup, f32 products accumulated in f32) is as close to an f64
+    evaluation as that FMA form (within 2x its error + 1e-7 of the magnitude)."""
     from mzba import _lib as L
     g = np.random.default_rng(5)
     B = 37
@@ -1637,11 +1639,26 @@ def test_f32_heads_bit_identical_to_their_sum_order():
     db = [torch.as_tensor(b, device="cuda") for b in bs]
     lg = [torch.empty(B, O, device="cuda") for _, O, _ in heads]
     dec = [torch.empty(B, device="cuda"), torch.empty(B, 3, device="cuda")]
-    L.call("mzba_heads", 0, 2, L.ptr(dx[0]), L.ptr(dw[0]), L.ptr(db[0]), 5120, 11, 1, L.ptr(lg[0]), L.ptr(dec[0]),
-           L.ptr(dx[1]), L.ptr(dw[1]), L.ptr(db[1]), 2560, 3, 0, L.ptr(lg[1]), L.ptr(dec[1]), -5.0, 5.0, B, L.stream())
-    torch.cuda.synchronize()
+    def run():
+        L.call("mzba_heads", 0, 2, L.ptr(dx[0]), L.ptr(dw[0]), L.ptr(db[0]), 5120, 11, 1, L.ptr(lg[0]), L.ptr(dec[0]),
+               L.ptr(dx[1]), L.ptr(dw[1]), L.ptr(db[1]), 2560, 3, 0, L.ptr(lg[1]), L.ptr(dec[1]), -5.0, 5.0, B,
+               L.stream())
+        torch.cuda.synchronize()
+        return [t.clone() for t in lg], [t.clone() for t in dec]
+
+    try:
+        assert L.lib().mzba_heads_set_variant(0) == 0
+        lg_fma, dec_fma = run()
+    finally:
+        L.lib().mzba_heads_set_variant(1)
+    lg_mfma, dec_mfma = run()
     for i in range(2):
         want = emulate(xs[i], ws[i], bs[i])
-        np.testing.assert_array_equal(lg[i].cpu().numpy().view(np.uint32), want.view(np.uint32))
-    p = torch.softmax(lg[1], 1)
-    torch.testing.assert_close(dec[1], p, rtol=1e-6, atol=1e-7)
+        np.testing.assert_array_equal(lg_fma[i].cpu().numpy().view(np.uint32), want.view(np.uint32))
+        exact = xs[i].astype(np.float64) @ ws[i].astype(np.float64).T + bs[i]
+        scale = np.abs(exact).max()
+        e_fma = np.abs(want - exact).max()
+        e_mfma = np.abs(lg_mfma[i].cpu().numpy() - exact).max()
+        assert e_mfma <= 2 * e_fma + 1e-7 * scale, (i, e_mfma / scale, e_fma / scale)
+    for dd, ll in ((dec_fma, lg_fma), (dec_mfma, lg_mfma)):
+        torch.testing.assert_close(dd[1], torch.softmax(ll[1], 1), rtol=1e-6, atol=1e-7)
