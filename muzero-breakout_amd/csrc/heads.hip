@@ -173,7 +173,8 @@ __global__ __launch_bounds__(512) void heads_mfma_f32_kernel(HeadArgs a, int B) 
     const float* xr = (const float*)a.x[hd] + (size_t)env * K;
     const float* wr = a.w[hd] + (size_t)min(el, O - 1) * K;
     const bool wok = el < O;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    // four accumulators (one per 4-k component): each sums a quarter of the wave's products, then pairwise
+    f32x4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
     const int ns = K / 16;
     for (int s = wave; s < ns; s += 8) {
       const int k = s * 16 + q * 4;
@@ -181,19 +182,19 @@ __global__ __launch_bounds__(512) void heads_mfma_f32_kernel(HeadArgs a, int B) 
       float4 wv = *reinterpret_cast<const float4*>(wr + k);
       if (!wok) wv = make_float4(0.f, 0.f, 0.f, 0.f);
       // D[row = env][col = output]: A = activations (row el), B = weights (col el)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, wv.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, wv.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.z, wv.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.w, wv.w, acc, 0, 0, 0);
+      acc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, wv.x, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, wv.y, acc[1], 0, 0, 0);
+      acc[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.z, wv.z, acc[2], 0, 0, 0);
+      acc[3] = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.w, wv.w, acc[3], 0, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) part[wave][4 * q + i][el] = acc[i];
+    for (int i = 0; i < 4; ++i) part[wave][4 * q + i][el] = (acc[0][i] + acc[1][i]) + (acc[2][i] + acc[3][i]);
     __syncthreads();
     if (tid < 256) {
       const int e = tid >> 4, o = tid & 15;
       float v = 0.f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) v = v + part[w][e][o];
+      for (int w = 0; w < 8; w += 2) v = v + (part[w][e][o] + part[w + 1][e][o]);
       if (o < O) lg[hd][e][o] = v + a.bias[hd][o];
     }
     __syncthreads();
