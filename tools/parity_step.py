@@ -1,7 +1,7 @@
 """One acting step of the f32 parity path (bench.py's parity_path replay) on its own, for a kernel trace:
 `rocprofv3 --kernel-trace --stats -- python3 tools/parity_step.py [B] [S] [X6] [HEADS] [REPS]`. Builds the f32 agent
-(x6 latent convs) and an ActingLoop of B envs (default 4096) x S sims (default 50), runs eager acting steps from the
-same state (the first warms scratch and code objects) and prints one JSON line per timed step. X6: the
+(x6 latent convs) and an ActingLoop of B envs (default 4096) x S sims (default 50), runs consecutive eager acting
+steps (the first warms scratch and code objects) and prints one JSON line per timed step. X6: the
 mzba_conv_x6_set_variant to run (2 default: pixel-tiled at the 4x5 latent; 1: the round-4 pre-split form), HEADS:
 mzba_heads_set_variant (1 default: f32 MFMA; 0: the FMA form); REPS timed steps (default 1). A same-box A/B
 alternates processes with different X6 / HEADS."""
