@@ -76,7 +76,9 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
   // AB: the tile's pixels span at most two envs (TM <= H W): their action indices read once
   int tb0 = 0, tb1 = 0, av0 = 0, av1 = 0;
   if (AB) {
-    tb0 = __builtin_amdgcn_readfirstlane(mb / HW);
+    // a wave wholly past the last pixel (the grid's partial last tile) takes the last env: its clamped pixels
+    // (mc = M - 1) then sit in env tb0 and act[] is read in bounds (mb / HW = B read act[B] and indexed with it)
+    tb0 = __builtin_amdgcn_readfirstlane(min(mb / HW, a.M / HW - 1));
     tb1 = (tb0 + 1) * HW;
     av0 = a.act[tb0];
     av1 = a.act[min(tb0 + 1, a.M / HW - 1)];

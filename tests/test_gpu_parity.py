@@ -680,6 +680,32 @@ def test_conv_halo_gather_action_bias_vs_torch_fp32(B, S, A):
     assert not L.lib().mzba_conv_halo_ex_supported(4, 5, Cin, Cout, 3, 1)
 
 
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(150, 21, 21, 256, 256), (5, 84, 84, 256, 256), (37, 21, 21, 256, 128),
+                                            (6, 84, 84, 128, 128)])
+def test_conv_halo_in_place_residual(B, H, W, Cin, Cout):
+    """The halo conv written in place over its residual (out aliases res, as a residual block may run it) equals the
+    out-of-place result bit for bit: every lane reads its own (pixel, channel) residual elements before it writes
+    them. The grid's partial last tile has waves wholly past the last pixel at B = 150 (their action-bias env index
+    is clamped to the last env, conv_halo.hip halo_epilogue)."""
+    from mzba import _lib as L
+    from mzba.agent import pack_lat16
+    g = torch.Generator(device="cuda").manual_seed(B + W + Cout)
+    dev = torch.device("cuda")
+    x = torch.randn(B, H, W, Cin, generator=g, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Cout, 3, 3, Cin, generator=g, device=dev) / (Cin * 9) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(Cout, generator=g, device=dev)
+    res = torch.randn(B, H, W, Cout, generator=g, device=dev).to(torch.bfloat16)
+    wh = torch.tensor(pack_lat16(w.float().cpu().numpy().reshape(Cout, -1), Cout, 3, Cin)).to(torch.bfloat16).cuda()
+    out = torch.full((B, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
+    L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, 1, L.stream())
+    inplace = res.clone()
+    L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(inplace), L.ptr(inplace), B, H, W, Cin, Cout, 1,
+           L.stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(out.float()).all()
+    assert torch.equal(out.view(torch.int16), inplace.view(torch.int16))
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,relu,with_res,same_order",
                          [(1000, 4, 5, 256, 256, 1, True, True), (37, 4, 5, 256, 256, 0, False, True),
                           (7, 16, 20, 128, 256, 1, True, True), (3, 21, 21, 256, 256, 1, True, True),

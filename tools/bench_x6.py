@@ -2,8 +2,8 @@
 acting loop's shapes: x6 at the 4x5 latent (B = 4096, the parity path's towers) and 8x10 (the representation
 tail), halo at config 3's 21x21 latent (B = 4096). HIP events around 20 launches after 3 warm-up launches,
 alternated twice. Prints one JSON line per (kernel, shape, variant). The variant setters
-(mzba_conv_x6_set_variant: 1 the pre-split x6 form, 0 the per-read-split kernel; mzba_conv_halo_set_wm: the halo
-conv's wave split, round-4 A/B builds only) may be missing from a build; the default then runs once per variant
+(mzba_conv_x6_set_variant: 3 the pixel-tiled form, 1 the pre-split x6 form; mzba_conv_halo_set_epilogue: the halo
+conv's epilogue in the rejected A/B build of profiles/r05/halo_epi, 0 serial / 1 pipelined) may be missing from a build; the default then runs once per variant
 slot (variant None).
   python tools/bench_x6.py"""
 import json
@@ -66,14 +66,16 @@ def main():
     b = torch.randn(C, generator=g, device=dev)
     out = torch.empty(B, H, W, C, dtype=torch.bfloat16, device=dev)
     fl = 2.0 * B * H * W * C * 9 * C
-    for rep in range(2):
-        for v in (1, 2, 3):
-            v = set_variant("mzba_conv_halo_set_wm", v)
-            ms = timeit(lambda: L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(x), L.ptr(out), B, H, W, C, C, 1,
-                                       L.stream()), n=10)
-            print(json.dumps({"lib": tag, "kernel": "conv_halo", "shape": [B, H, W, C], "variant": v, "rep": rep, "ms": ms,
-                              "tflops": fl / ms / 1e9, "frac": fl / ms / 1e9 / 2500}), flush=True)
-    set_variant("mzba_conv_halo_set_wm", 1)
+    for rep in range(3):
+        for v in (0, 1):  # mzba_conv_halo_set_epilogue (an A/B build: profiles/r05/halo_epi); None when absent
+            v = set_variant("mzba_conv_halo_set_epilogue", v)
+            for res in (x, None):
+                ms = timeit(lambda: L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W,
+                                           C, C, 1, L.stream()), n=10)
+                print(json.dumps({"lib": tag, "kernel": "conv_halo", "shape": [B, H, W, C], "epilogue": v,
+                                  "residual": res is not None, "rep": rep, "ms": ms, "tflops": fl / ms / 1e9,
+                                  "frac": fl / ms / 1e9 / 2500}), flush=True)
+    set_variant("mzba_conv_halo_set_epilogue", 1)
 
 
 if __name__ == "__main__":

@@ -1,5 +1,5 @@
 """Phase breakdown of conv_lat from in-kernel s_memtime stamps (diagnostic build only).
-Stamps: 0 entry, 1 after staging barrier, 3 wave0 after main loop (7 = wave 4), 4 after the
+`python tools/stamp_conv.py [variants|ablate|learner]`. Stamps: 0 entry, 1 after staging barrier, 3 wave0 after main loop (7 = wave 4), 4 after the
 post-loop barrier, 5 end. Shares are what count (the stamps' fences perturb timing)."""
 import ctypes
 import json
@@ -19,6 +19,7 @@ def load(tag):
     D.mzba_conv_lat.argtypes = [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P]
     D.mzba_lat_stamps_read.argtypes = [P, I]
     D.mzba_conv_lat_set_variant.argtypes = [I]
+    D.mzba_conv_lat_bn_chunks.argtypes = [I, I, I, I, I, I, P, P]
     return D
 
 
@@ -28,13 +29,19 @@ def run(D, B, H, W, Cin, Cout, ks, res=True):
     w = (torch.randn(Cout * ks * ks * Cin + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
     b = torch.zeros(Cout, device="cuda")
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for _ in range(20):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for it in range(40):
+        if it == 20:
+            e0.record()
         rc = D.mzba_conv_lat(x.data_ptr(), H * W * Cin, None, 0, w.data_ptr(), b.data_ptr(), None, None, 0,
                              x.data_ptr() if res else None, out.data_ptr(), B, H, W, Cin, Cout, ks, 1, st)
         assert rc == 0
+    e1.record()
     torch.cuda.synchronize()
-    E = 160 // (H * W)
-    nblk = ((B + E - 1) // E) * ((Cout + 127) // 128)
+    us = e0.elapsed_time(e1) * 1e3 / 20
+    nch, rpc = ctypes.c_int(), ctypes.c_int()
+    assert D.mzba_conv_lat_bn_chunks(B, H, W, Cin, Cout, ks, ctypes.byref(nch), ctypes.byref(rpc)) == 0
+    nblk = nch.value * ((Cout + 127) // 128)
     buf = (ctypes.c_ulonglong * (8 * nblk))()
     D.mzba_lat_stamps_read(buf, nblk)
     a = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, 8).astype(np.float64)
@@ -43,13 +50,21 @@ def run(D, B, H, W, Cin, Cout, ks, res=True):
     ph = {"stage": np.median(a[:, 1] - a[:, 0]), "loop_w0": np.median(a[:, 3] - a[:, 1]),
           "loop_w4": np.median(a[:, 7] - a[:, 1]), "wait_barrier": np.median(a[:, 4] - a[:, 3]),
           "epilogue": np.median(a[:, 5] - a[:, 4]), "total_block": np.median(a[:, 5] - a[:, 0]),
-          "launch_spread(start max-min)": float(rel[:, 0].max()), "end_max": float(rel[:, 5].max())}
+          "launch_spread(start max-min)": float(rel[:, 0].max()), "end_max": float(rel[:, 5].max()),
+          "us_per_launch": us, "workgroups": nblk}
     return {k: float(v) for k, v in ph.items()}
 
 
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "variants"
-    if which == "ablate":
+    if which == "learner":  # the learner's B = 512 latent conv: 3-row (variant 0) and 5-row (2) tiles
+        for tag, name in (("", "full"), ("_a1", "hot 8KB weights"), ("_a2", "no LDS A reads"), ("_a3", "no MFMA")):
+            D = load(tag)
+            for v in (0, 2):
+                assert D.mzba_conv_lat_set_variant(v) == 0
+                for s in [(512, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 3)]:
+                    print(json.dumps({"variant": name, "lat_variant": v, "shape": s, "cycles": run(D, *s)}), flush=True)
+    elif which == "ablate":
         for tag, name in (("", "full"), ("_a1", "hot 8KB weights"), ("_a2", "no LDS A reads"), ("_a3", "no MFMA")):
             D = load(tag)
             for s in [(1024, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 1)]:
