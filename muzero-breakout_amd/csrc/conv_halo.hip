@@ -37,6 +37,9 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
+#ifndef HALO_RING
+#define HALO_RING 2  // weight ring depth in k steps (an A/B build may deepen it)
+#endif
 namespace hl {
 constexpr int TM = 256;            // output pixels per workgroup
 constexpr int TN = 256;            // output channels per workgroup
@@ -189,12 +192,11 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   auto wload = [&](int ct, int s) {
     return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, (ct * KS + s) * 1024, 0));
   };
-  bf16x8 bq[2][CT];
+  bf16x8 bq[HALO_RING][CT];
 #pragma unroll
-  for (int ct = 0; ct < CT; ++ct) {
-    bq[0][ct] = wload(ct, kstep(0));
-    bq[1][ct] = wload(ct, kstep(1));
-  }
+  for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+    for (int i = 0; i < HALO_RING; ++i) bq[i][ct] = wload(ct, kstep(i));
 
   f32x4 acc[MT][CT];
 #pragma unroll
@@ -250,8 +252,8 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
     for (int t = 0; t < 9; ++t) {
 #pragma unroll
       for (int c = 0; c < NCS; ++c) {
-        const int sl = c & 1;  // = j & 1: the steps per tap (NCS) are even
-        const int sn = kstep(j + 2);
+        const int sl = HALO_RING == 2 ? (c & 1) : j % HALO_RING;  // j & 1: the steps per tap (NCS) are even
+        const int sn = kstep(j + HALO_RING);
 #pragma unroll
         for (int mi = 0; mi < MT; ++mi) {
           const int idx = c * MT + mi, nx = idx + PF;

@@ -41,7 +41,7 @@ def main():
     dev = torch.device("cuda")
     g = torch.Generator(device="cuda").manual_seed(0)
     C = 256
-    for (B, H, W) in ((4096, 4, 5), (4096, 8, 10)):
+    for (B, H, W) in (() if os.environ.get("HALO_ONLY") else ((4096, 4, 5), (4096, 8, 10))):
         x = torch.rand(B, H, W, C, generator=g, device=dev)
         wx = torch.randn(3 * C * 9 * C, generator=g, device=dev).to(torch.bfloat16)
         b = torch.randn(C, generator=g, device=dev)
