@@ -37,6 +37,9 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
+#ifndef HALO_EPI16
+#define HALO_EPI16 1  // 16-B epilogue accesses through v_permlane16_swap (0: the round-4 8-B form, an A/B build)
+#endif
 #ifndef HALO_RING
 #define HALO_RING 2  // weight ring depth in k steps (an A/B build may deepen it)
 #endif
@@ -90,6 +93,59 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
   const float lo = a.relu ? 0.f : -__builtin_inff();  // ReLU as max(v, 0); max(v, -inf) = v
+#if HALO_EPI16
+  // 16-B form: the k-quarter rows q = 2j and 2j + 1 of a wave hold the two 8-B halves of chunk j (channels 8j..8j + 7
+  // of a 16-channel column tile) of the same pixel. For a column-tile pair (ct, ct + 1) one v_permlane16_swap per
+  // dword of (acc + bias) hands the odd row's ct half to the even row and the even row's ct + 1 half to the odd
+  // row: an even-row lane then owns tile ct's chunk j, an odd-row lane tile ct + 1's, and its residual load, the
+  // ReLU / bf16 pack and the store are one 16-B access each (half the epilogue's memory instructions). The f32
+  // expression of every element is unchanged, so the outputs are bit-identical to the 8-B form.
+  static_assert(CT % 2 == 0, "column-tile pairs");
+  const int cj = 8 * (q >> 1), codd = q & 1;
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi) {
+    const int m = mb + mi * 16 + n;
+    const int mc = m < a.M ? m : a.M - 1;
+    float4 ab[CT];
+    if (AB) {
+      const bool hi = mc >= tb1;
+      const int p = mc - (hi ? tb1 : tb1 - HW), av = hi ? av1 : av0;
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct)
+        ab[ct] = *reinterpret_cast<const float4*>(a.act_bias + ((size_t)p * a.A + av) * a.Cout + nb + ct * 16 + 4 * q);
+    }
+    uint4 rv[CT / 2];
+    if (RES) {
+#pragma unroll
+      for (int cp = 0; cp < CT / 2; ++cp)
+        rv[cp] = *reinterpret_cast<const uint4*>(a.res + (size_t)mc * a.Cout + nb + (2 * cp + codd) * 16 + cj);
+    }
+#pragma unroll
+    for (int cp = 0; cp < CT / 2; ++cp) {
+      float w[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c0 = 2 * cp, c1 = 2 * cp + 1;
+        const float v0 = AB ? (acc[mi][c0][i] + (&ab[c0].x)[i]) + (&bb[c0].x)[i] : acc[mi][c0][i] + (&bb[c0].x)[i];
+        const float v1 = AB ? (acc[mi][c1][i] + (&ab[c1].x)[i]) + (&bb[c1].x)[i] : acc[mi][c1][i] + (&bb[c1].x)[i];
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v0), __float_as_uint(v1), false, false);
+        w[i] = __uint_as_float(r[0]);
+        w[4 + i] = __uint_as_float(r[1]);
+      }
+      if (RES) {
+        const uint32_t rw[4] = {rv[cp].x, rv[cp].y, rv[cp].z, rv[cp].w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w[i] = w[i] + bf16_to_f32((bf16_t)(rw[i >> 1] >> (16 * (i & 1))));
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) w[i] = fmaxf(w[i], lo);
+      const uint4 o = make_uint4(pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3]), pack_bf16x2(w[4], w[5]),
+                                 pack_bf16x2(w[6], w[7]));
+      if (m < a.M) *reinterpret_cast<uint4*>(a.out + (size_t)m * a.Cout + nb + (2 * cp + codd) * 16 + cj) = o;
+    }
+  }
+  return;
+#endif
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
     const int m = mb + mi * 16 + n;

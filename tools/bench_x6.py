@@ -72,9 +72,12 @@ def main():
             for res in (x, None):
                 ms = timeit(lambda: L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W,
                                            C, C, 1, L.stream()), n=10)
+                # output checksum (int16 bit patterns, position-weighted): equal across builds = bit-identical
+                h = out.view(torch.int16).flatten().to(torch.int64)
+                ck = int((h * (torch.arange(h.numel(), device=dev) % 65521 + 1)).sum().item())
                 print(json.dumps({"lib": tag, "kernel": "conv_halo", "shape": [B, H, W, C], "epilogue": v,
                                   "residual": res is not None, "rep": rep, "ms": ms, "tflops": fl / ms / 1e9,
-                                  "frac": fl / ms / 1e9 / 2500}), flush=True)
+                                  "frac": fl / ms / 1e9 / 2500, "checksum": ck}), flush=True)
     set_variant("mzba_conv_halo_set_epilogue", 1)
 
 
