@@ -123,6 +123,15 @@ def run_env(args, world, rank, local):
         tj = json.load(open(tpath))
         if (tj.get("envs"), tj.get("H"), tj.get("W")) == (B, H, W) and tj.get("write_bytes") is not None:
             traffic = tj["write_bytes"] + (tj.get("fetch_bytes") or 0)
+    # the env kernel's own duration (rocprofv3 kernel trace of this geometry, profiles/env_kernel_time.json): the
+    # event-timed figure above includes whatever separates consecutive graph-replayed launches
+    ktimed = None
+    kpath = os.path.join(ROOT, "profiles", "env_kernel_time.json")
+    if os.path.exists(kpath):
+        for e in json.load(open(kpath)):
+            if (e["envs"], e["H"], e["W"], e["hist"]) == (B, H, W, args.hist):
+                a_k = B * env_bytes(H, W) / (e["avg_ns"] * 1e-9) / 1e9
+                ktimed = {"avg_kernel_ms": e["avg_ns"] * 1e-6, "achieved": a_k, "frac": a_k / 8000.0, "source": e["source"]}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle.env import BreakoutEnvOracle, convert_to_grayscale
@@ -152,7 +161,8 @@ def run_env(args, world, rank, local):
                        "envs_per_gpu": B},
             "roofline": {"bound": "hbm", "kernel": "env_step_compact_kernel (step + render + history push)",
                          "achieved": achieved, "peak": 8000.0, "unit": "GB/s", "frac": achieved / 8000.0,
-                         "traffic": traffic, "bytes_per_env_step": env_bytes(H, W), "avg_launch_ms": kms},
+                         "traffic": traffic, "bytes_per_env_step": env_bytes(H, W), "avg_launch_ms": kms,
+                         "kernel_timed": ktimed},
             "cpu_baseline": cpu,
         }
         check_fracs(line)
