@@ -1,0 +1,70 @@
+"""bench.py's host-side contract pieces, on the CPU: the fraction guard, the config naming, the L2 weight-stream
+arithmetic and the committed measurement records the bench line quotes (every fraction in them a fraction of a
+true peak, every record keyed the way bench.py looks it up)."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "muzero-breakout_amd"))
+import bench  # noqa: E402
+
+
+def test_check_fracs_fails_on_any_fraction_above_one():
+    ok = {"roofline": {"frac": 0.96, "executed_frac": 0.68, "l2_weight_stream": {"frac": 0.59},
+                       "kernel_timed": {"frac": 0.41}}, "parity_path": {"roofline": {"frac": 0.93}}}
+    bench.check_fracs(ok)
+    for bad in ({"roofline": {"frac": 1.0001}}, {"parity_path": {"roofline": {"frac": 1.59}}},
+                {"roofline": {"l2_weight_stream": {"frac": 1.058}}}, {"roofline": {"executed_frac": 1.2}}):
+        with pytest.raises(SystemExit):
+            bench.check_fracs(bad)
+    bench.check_fracs({"roofline": {"fraction_note": 3.0, "frac": None}})  # only numeric *frac keys are checked
+
+
+def test_cfg_name_maps_the_baseline_configs():
+    assert bench.cfg_name(4096, 50).startswith("north_star")
+    assert bench.cfg_name(1024, 50) == "config 2"
+    assert bench.cfg_name(4096, 200, "fp16") == "config 5"
+    assert bench.cfg_name(4096, 200, "bf16").startswith("config 5 geometry")
+    assert bench.cfg_name(512, 50) == "custom"
+
+
+def test_l2_weight_stream_arithmetic():
+    r = bench.l2_weight_stream(0.0147)  # a 14.7 us tower conv
+    assert r["bytes_per_cu_per_conv"] == 256 * 9 * 256 * 2
+    assert abs(r["achieved_per_cu_GBps"] - 1179648 / 14.7e-6 / 1e9) < 1e-6
+    assert abs(r["peak_per_cu_GBps"] - bench.L2_PEAK_TBPS * 1e3 / 256) < 1e-9
+    assert abs(r["frac"] - r["achieved_per_cu_GBps"] / r["peak_per_cu_GBps"]) < 1e-12
+    assert bench.l2_weight_stream(None) is None
+
+
+def test_env_bytes_and_committed_env_kernel_times():
+    assert bench.env_bytes(84, 84) == 7104 and bench.env_bytes(16, 20) == 368
+    recs = json.load(open(os.path.join(ROOT, "profiles", "env_kernel_time.json")))
+    assert {(r["H"], r["W"], r["hist"]) for r in recs} >= {(84, 84, 4), (16, 20, 32)}
+    for r in recs:
+        assert r["kernel"].startswith("env_step_compact_kernel") and r["calls"] > 0
+        assert 0 < r["min_ns"] <= r["avg_ns"]
+        gbps = r["envs"] * bench.env_bytes(r["H"], r["W"]) / (r["avg_ns"] * 1e-9) / 1e9
+        assert gbps / 8000.0 <= 1.0
+        assert os.path.exists(os.path.join(ROOT, r["source"]))
+
+
+def test_committed_tower_records_are_keyed_as_bench_reads_them():
+    traffic = json.load(open(os.path.join(ROOT, "profiles", "tower_hbm_traffic.json")))["records"]
+    for rec in traffic:
+        assert isinstance(rec["envs"], int) and rec["kernel_name"] in bench.EXECUTED_FRACTION
+        assert rec["bytes_per_launch"] >= rec["algorithmic_bytes"] > 0
+    counters = json.load(open(os.path.join(ROOT, "profiles", "tower_sq_counters.json")))["records"]
+    keys = [(r.get("envs"), r.get("kernel_name"), r.get("sims", 50), r.get("dyn_dtype")) for r in counters]
+    assert len(keys) == len(set(keys))  # one record per (batch, instance, sims, dynamics precision)
+    for r in counters:
+        for k, v in r.items():
+            if (k == "frac" or k.endswith("_frac") or k.endswith("_busy")) and isinstance(v, float):
+                assert 0.0 <= v <= 1.0, (k, v)
+    headline = [r for r in counters if (r.get("envs"), r.get("kernel_name")) == (4096, "towerp_kernel<0>")
+                and r.get("sims", 50) == 50]
+    assert headline, "the north_star line's counters"

@@ -5,6 +5,7 @@ geometry, so the bench line reports the HBM fraction from the kernel's own durat
 import csv
 import json
 import os
+import re
 import sys
 
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
@@ -18,7 +19,8 @@ def main():
             rows = [r for r in csv.DictReader(f) if "env_step_compact_kernel" in r["Name"]]
         assert len(rows) == 1, rows
         r = rows[0]
-        out.append({"envs": 4096, "H": int(H), "W": int(W), "hist": int(hist), "kernel": r["Name"].split("(")[0].replace("void ", ""),
+        kname = re.search(r"env_step_compact_kernel<\d+>", r["Name"]).group(0)
+        out.append({"envs": 4096, "H": int(H), "W": int(W), "hist": int(hist), "kernel": kname,
                     "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
                     "source": os.path.relpath(path, ROOT)})
     with open(os.path.join(ROOT, "profiles", "env_kernel_time.json"), "w") as f:
