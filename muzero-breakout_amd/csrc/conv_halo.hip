@@ -144,8 +144,7 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
       if (m < a.M) *reinterpret_cast<uint4*>(a.out + (size_t)m * a.Cout + nb + (2 * cp + codd) * 16 + cj) = o;
     }
   }
-  return;
-#endif
+#else
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
     const int m = mb + mi * 16 + n;
@@ -184,6 +183,7 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
       for (int ct = 0; ct < CT; ++ct) *reinterpret_cast<uint2*>(a.out + (size_t)m * a.Cout + nb + ct * 16 + 4 * q) = o[ct];
     }
   }
+#endif
 }
 
 // WM = 2 pixel halves x 4 quarters of 64 channels. Measured and dropped (profiles/r04/halo_wm/, same box, B = 4096,
