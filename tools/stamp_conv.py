@@ -1,5 +1,5 @@
 """Phase breakdown of conv_lat from in-kernel s_memtime stamps (diagnostic build only).
-`python tools/stamp_conv.py [variants|ablate|learner|mfma|zrows]`. Stamps: 0 entry, 1 after staging barrier, 3 wave0 after main loop (7 = wave 4), 4 after the
+`python tools/stamp_conv.py [variants|ablate|learner|mfma|zrows|libs TAG...]`. Stamps: 0 entry, 1 after staging barrier, 3 wave0 after main loop (7 = wave 4), 4 after the
 post-loop barrier, 5 end. Shares are what count (the stamps' fences perturb timing)."""
 import ctypes
 import json
@@ -57,7 +57,17 @@ def run(D, B, H, W, Cin, Cout, ks, res=True):
 
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "variants"
-    if which == "zrows":  # a 16-row zero block (the A/B build of profiles/r05/lat_zero_block, LAT_ZROWS=16) vs one
+    if which == "libs":  # diagnostic builds named on the command line (base = libmzba_diag.so), alternated
+        tags = ["" if t == "base" else t for t in sys.argv[2:]]
+        for rep in range(2):
+            for tag in tags:
+                D = load(tag)
+                for v in (0, 2):
+                    assert D.mzba_conv_lat_set_variant(v) == 0
+                    for s in [(512, 4, 5, 256, 256, 3), (1024, 4, 5, 256, 256, 3)]:
+                        print(json.dumps({"lib": "libmzba_diag%s.so" % tag, "rep": rep, "lat_variant": v, "shape": s,
+                                          "cycles": run(D, *s)}), flush=True)
+    elif which == "zrows":  # a 16-row zero block (the A/B build of profiles/r05/lat_zero_block, LAT_ZROWS=16) vs one
         # shared zero row (libmzba_diag_z1.so, LAT_ZROWS=1)
         for rep in range(2):
             for tag in ("_z1", ""):
