@@ -341,6 +341,19 @@ def tower_counters(B, kname, sims, dyn):
     return None
 
 
+def conv_counters(B, H, W, kname):
+    """PMC record of the non-fused path's dominant conv kernel (config 3's halo conv) at this batch and latent size
+    (profiles/conv_counters.json, tools/gpu_run.sh step 'pmck' + tools/pmc_conv.py: HBM bytes per launch from the
+    FETCH_SIZE / WRITE_SIZE passes, MFMA busy / clock / LDS conflicts from the SQ passes of the same bench)."""
+    tpath = os.path.join(ROOT, "profiles", "conv_counters.json")
+    if not os.path.exists(tpath):
+        return None
+    for rec in json.load(open(tpath))["records"]:
+        if (rec.get("envs"), rec.get("H"), rec.get("W")) == (B, H, W) and kname in rec.get("kernel_name", ""):
+            return rec
+    return None
+
+
 L2_PEAK_TBPS = 34.5  # MI355X L2 (8 XCDs x 4 MiB) aggregate read rate, MI355X_MICROARCH.md 'L2 (per XCD)'
 
 
@@ -680,6 +693,11 @@ def main():
     # config 5: the fp16 dynamics step is its own instance (towerp_kernel<1>), counted separately
     kname16 = tower_kernel_name(B, fp16=True) if (kname and args.dyn_dtype == "fp16") else None
     sq16 = tower_counters(B, kname16, args.sims, args.dyn_dtype) if kname16 else None
+    if not tower_launch_ms:  # config 3: the per-conv kernel's own PMC record (traffic and SQ figures)
+        crec = conv_counters(B, p.lh, p.lw, big_conv_kernel(args, B, p) + "_kernel")
+        if crec:
+            traffic, sq = crec.get("bytes_per_launch"), crec
+            traffic_rec = {"algorithmic_bytes": crec.get("algorithmic_bytes"), "source": "profiles/conv_counters.json"}
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -713,9 +731,9 @@ def main():
                          "traffic_algorithmic_bytes": traffic_rec and traffic_rec.get("algorithmic_bytes"),
                          # the floor with per-XCD L2s: every one of the 8 XCDs fetches the tower's weights
                          # once (33 MB each), the latents once in all
-                         "traffic_per_xcd_floor_bytes": traffic_rec and (
+                         "traffic_per_xcd_floor_bytes": traffic_rec and tower_launch_ms and (
                              traffic_rec.get("algorithmic_bytes") + 7 * (2 * 14 * 256 * 2304 * 2)),
-                         "traffic_source": traffic_rec and "profiles/tower_hbm_traffic.json",
+                         "traffic_source": traffic_rec and traffic_rec.get("source", "profiles/tower_hbm_traffic.json"),
                          "flop_per_conv": fl, "avg_ms_per_conv": conv_ms, "avg_launch_ms": tower_launch_ms or conv_ms,
                          "launches_timed": len(probe),
                          # what the MFMA pipe actually issues: the algorithmic rate x the kernel's padding-free

@@ -68,3 +68,16 @@ def test_committed_tower_records_are_keyed_as_bench_reads_them():
     headline = [r for r in counters if (r.get("envs"), r.get("kernel_name")) == (4096, "towerp_kernel<0>")
                 and r.get("sims", 50) == 50]
     assert headline, "the north_star line's counters"
+
+
+def test_conv_counter_record_for_config3():
+    """The non-fused path's PMC record (config 3's halo conv at the 21x21 latent): found by bench.conv_counters for
+    the config 3 batch and latent size only; traffic at least the algorithmic bytes, fractions within [0, 1]."""
+    rec = bench.conv_counters(4096, 21, 21, "conv_halo_kernel")
+    assert rec is not None and rec["kernel_name"].startswith("conv_halo_kernel<256, 1, 2, 1, 256, false>")
+    assert rec["bytes_per_launch"] >= rec["algorithmic_bytes"] > 0
+    for k in ("mfma_busy", "wait_inst", "lds_bank_conflict_frac"):
+        assert 0.0 <= rec[k] <= 1.0
+    assert os.path.isdir(os.path.join(ROOT, rec["source"]))
+    assert bench.conv_counters(1024, 21, 21, "conv_halo_kernel") is None
+    assert bench.conv_counters(4096, 4, 5, "conv_halo_kernel") is None

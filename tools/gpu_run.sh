@@ -12,6 +12,8 @@
 #                                                                              -> tower_hbm_traffic.json
 #   sq:NAME:KERNELS[:ARGS]    two SQ counter passes of bench.py ARGS; KERNELS = comma-separated rocprof name
 #                             substrings (e.g. "towerp_kernel<0>,towerp_kernel<1>") -> NAME/sq{1,2}_<k>.json
+#   pmck:NAME:KERNEL:ENVS:H:W:ARGS  FETCH_SIZE / WRITE_SIZE / two SQ passes of one conv kernel over bench.py ARGS
+#                                                                              -> NAME.json, conv_counters.json
 #   rehearse:N:ENVS[:ARGS]    bench.py's N > 1 path: N ranks on cuda:0 over gloo (MZBA_DIST_REHEARSAL=1)
 #                                                                              -> rehearse_nN.json
 #   py:NAME:SECONDS:CMD       any python tool (CMD = script + args)           -> NAME.log
@@ -82,6 +84,23 @@ for step in "$@"; do
           $O/tower_sq_counters.json $sims $dyn
       done
       echo "sq $name done: $kernels" ;;
+    pmck)
+      # pmck:NAME:KERNEL:ENVS:H:W:ARGS — HBM bytes + SQ figures of one conv kernel over bench.py ARGS (four --pmc passes
+      # of their own) -> NAME.json (and merged into $O/conv_counters.json)
+      IFS=: read -r kname envs hh ww args <<< "$rest"
+      mkdir -p $O/$name
+      i=0
+      for ctr in "FETCH_SIZE" "WRITE_SIZE" \
+                 "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                 "SQ_INSTS_MFMA SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"; do
+        sub=(fetch write sq1 sq2); sub=${sub[$i]}; i=$((i + 1))
+        log "rocprofv3 --pmc $ctr --kernel-trace -d $O/$name/$sub -o run -- python3 bench.py $args"
+        timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -d $O/$name/$sub -o run -- python3 bench.py $args \
+          > $O/$name/$sub.log 2>&1
+      done
+      python3 tools/pmc_conv.py $O/$name "$kname" $envs $hh $ww $O/conv_counters.json > $O/$name.json
+      rm -rf $O/$name/fetch $O/$name/write $O/$name/sq1 $O/$name/sq2
+      cat $O/$name.json ;;
     rehearse)
       N=$name
       IFS=: read -r envs args <<< "$rest"
