@@ -264,7 +264,10 @@ def run_learner(args, world, rank, local):
                        "minibatch": B, "parallelism": "replicas" if world > 1 else "single device"},
             "roofline": {"bound": "mfma", "kernel": "whole minibatch (conv fwd / dgrad / wgrad + BN + heads + Adam)",
                          "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak,
-                         "traffic": None, "flop_per_minibatch": fl, "avg_launch_ms": kms},
+                         "traffic": None, "flop_per_minibatch": fl, "avg_launch_ms": kms,
+                         # the minibatch's top kernels by kernel time (rocprof of this workload, with SQ figures of
+                         # the two largest: profiles/learner_kernels.json), for the reader of the 0.2 above
+                         "top_kernels": learner_kernels(B, dt)},
             "loss": float(loss[0]),
             "launch": "eager" if args.no_graph else "hip-graph replay of the whole minibatch",
             "streams": args.learner_streams,
@@ -339,6 +342,16 @@ def tower_counters(B, kname, sims, dyn):
         if (rec.get("envs"), rec.get("kernel_name"), rec.get("sims", 50), rec.get("dyn_dtype")) == (B, kname, sims, dyn):
             return rec
     return None
+
+
+def learner_kernels(B, dt):
+    """The committed kernel breakdown of the learner minibatch (profiles/learner_kernels.json) when it was measured at
+    this minibatch size and dtype, else None."""
+    tpath = os.path.join(ROOT, "profiles", "learner_kernels.json")
+    if not os.path.exists(tpath):
+        return None
+    rec = json.load(open(tpath))
+    return rec if (rec.get("minibatch"), rec.get("dtype")) == (B, dt) else None
 
 
 def conv_counters(B, H, W, kname):

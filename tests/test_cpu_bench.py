@@ -81,3 +81,12 @@ def test_conv_counter_record_for_config3():
     assert os.path.isdir(os.path.join(ROOT, rec["source"]))
     assert bench.conv_counters(1024, 21, 21, "conv_halo_kernel") is None
     assert bench.conv_counters(4096, 4, 5, "conv_halo_kernel") is None
+
+
+def test_learner_kernel_breakdown_record():
+    rec = bench.learner_kernels(512, "bf16")
+    assert rec is not None and rec["kernels"][0]["kernel"].startswith("conv_lat_kernel")
+    shares = [k["share_of_kernel_time"] for k in rec["kernels"]]
+    assert shares == sorted(shares, reverse=True) and sum(shares) <= 1.0
+    assert bench.learner_kernels(512, "f32") is None and bench.learner_kernels(256, "bf16") is None
+    bench.check_fracs({"roofline": {"top_kernels": rec}})
