@@ -85,7 +85,8 @@ template <int NT, int MR = MAXROWS>
 __device__ __forceinline__ void lat_res_prefetch(const LatArgs& a, uint4 (&rv)[EPT_MAX], int rows, int env0, int HW,
                                                  int tid) {
   constexpr int EPT = (MR * 16 + NT - 1) / NT;
-  const int ncols = min(128, a.Cout - blockIdx.y * 128);
+  // int arithmetic (min(int, unsigned) resolved to the double overload: a v_min_f64 round trip per call)
+  const int ncols = min(128, a.Cout - (int)blockIdx.y * 128);
   const int ncb = ncols / 8;
   const int nchunks = rows * ncb;
   if (a.res) {
@@ -103,7 +104,7 @@ template <int NT, int MR = MAXROWS>
 __device__ __forceinline__ void lat_epilogue(const LatArgs& a, float* ot, const uint4 (&rv)[EPT_MAX], int rows,
                                              int env0, int HW, int tid) {
   constexpr int EPT = (MR * 16 + NT - 1) / NT;
-  const int ncols = min(128, a.Cout - blockIdx.y * 128);
+  const int ncols = min(128, a.Cout - (int)blockIdx.y * 128);
   const int ncb = ncols / 8;
   const int nchunks = rows * ncb;
   // smode 2: this thread's chunk column is fixed (ncb = 16 divides NT): register partial sums
