@@ -174,9 +174,20 @@ __device__ __forceinline__ void lat_epilogue(const LatArgs& a, float* ot, const 
     constexpr int TPC = NT / 128;  // (a wave reads 64 consecutive columns of one row: conflict-free)
     const int col = tid % 128, q = tid / 128;
     float* red = ot + MR * 128;    // [TPC][128] after the tile (LDS_C covers MR rows; see caller)
+    // every row's value read before the first add (one LDS round trip, not one per row of a rolled loop);
+    // rows past `rows` add an exact 0, so the sums are the rolled loop's, bit for bit
+    constexpr int RPT = MR / TPC;
     float s = 0.f;
-    if (col < ncols)
-      for (int r = q; r < rows; r += TPC) s += ot[r * 128 + col];
+    if (col < ncols) {
+      float vv[RPT];
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const int r = q + k * TPC;
+        vv[k] = r < rows ? ot[r * 128 + col] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) s += vv[k];
+    }
     red[q * 128 + col] = s;
     __syncthreads();
     float tot = 0.f;
@@ -184,11 +195,19 @@ __device__ __forceinline__ void lat_epilogue(const LatArgs& a, float* ot, const 
     for (int k = 0; k < TPC; ++k) tot += red[k * 128 + col];
     const float mean = tot / rows;
     float m2 = 0.f;
-    if (col < ncols)
-      for (int r = q; r < rows; r += TPC) {
-        const float d = ot[r * 128 + col] - mean;
+    if (col < ncols) {
+      float vv[RPT];
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const int r = q + k * TPC;
+        vv[k] = r < rows ? ot[r * 128 + col] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const float d = q + k * TPC < rows ? vv[k] - mean : 0.f;
         m2 += d * d;
       }
+    }
     __syncthreads();
     red[q * 128 + col] = m2;
     __syncthreads();
