@@ -147,6 +147,10 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
  * 0: the per-read-split kernel only (A/B). The pre-split and per-read-split forms are bit-identical (same sums in
  * the same order); the pixel-tiled form sums the same products in another order (channel block, tap). */
 int mzba_conv_x6_set_variant(int v);
+/* Workgroup width of the pixel-tiled x6 conv (process-wide): 0 (default) 4 waves / 64 output channels where the
+ * 8-wave grid (16 envs x 128 channels per workgroup) would leave CUs idle (config 2's 1 024 envs), else 8; 8 or 4
+ * force it. Per 16-channel tile the arithmetic is the same, so the outputs are identical. -1 otherwise. */
+int mzba_conv_x6_set_waves(int nw);
 int mzba_conv_halo(const void* in, const void* wh, const float* bias, const void* res, void* out, int B, int H, int W,
                    int Cin, int Cout, int relu, hipStream_t stream);
 

@@ -549,9 +549,12 @@ struct X6TArgs {
 
 MZ_DEV int tkey(int e) { return (e >> 2) & 2; }  // chunk swizzle of row 16 p + e (64-B plane rows)
 
-template <bool GA, int KSZ = 3>
-__global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
+// NW waves of 16 output channels each: 8 (128 channels per workgroup, the default) or 4 (64 channels: twice the
+// workgroups where the 8-wave grid leaves CUs idle, config 2's 1 024 envs; per wave the same arithmetic)
+template <bool GA, int KSZ = 3, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   using namespace x6t;
+  constexpr int NT = 64 * NW;
   constexpr const X6TGroups& G = KSZ == 3 ? kGroups : kGroups1;
   constexpr int SPB = KSZ == 3 ? 3 : 1;     // ring steps per channel block (the dy rows)
   constexpr int KST = KSZ * KSZ * NCS;      // pack k steps per column tile
@@ -560,26 +563,26 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4, n = lane & 15;
   const int e0 = blockIdx.x * E;
-  const int nb = blockIdx.y * 128 + wave * 16;  // the wave's first output channel
+  const int nb = blockIdx.y * (16 * NW) + wave * 16;  // the wave's first output channel
 
   // LDS-DMA of block cb's f32 rows: 1-KiB piece i = rows 8 i .. 8 i + 7 = pixel i >> 1, envs 8 (i & 1) + 0..7; the
-  // waves take pieces wave + 8 k, so a lane's env (8 (wave & 1) + lane / 8) is fixed: its offset is read once
+  // waves take pieces wave + NW k (NW even), so a lane's env (8 (wave & 1) + lane / 8) is fixed: its offset is read once
   const int se = min(e0 + 8 * (wave & 1) + (lane >> 3), a.B - 1);
   long long eoff = (long long)se * a.env_stride;
   if (GA && a.slot) eoff += (long long)a.slot[se] * a.slot_stride;
   const float* src0 = a.in + eoff + (lane & 7) * 4;
   auto stage = [&](int cb) {
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const int i = wave + 8 * k;
+    for (int k = 0; k < 40 / NW; ++k) {
+      const int i = wave + NW * k;
       __builtin_amdgcn_global_load_lds(src0 + (size_t)(i >> 1) * CIN + cb * 32, lds + RAW + i * 1024, 16, 0, 0);
     }
   };
   // split of the raw block into the three planes: item g = (row, 8-channel chunk)
   auto split = [&]() {
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int g = tid + u * x6::NT;
+    for (int u = 0; u < (ROWS * 4 + NT - 1) / NT; ++u) {
+      const int g = tid + u * NT;
       if (g < ROWS * 4) {
         const int r = g >> 2, k8 = g & 3;
         const uint4 u0 = *reinterpret_cast<const uint4*>(lds + RAW + r * 128 + k8 * 32);
@@ -725,6 +728,8 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6t_kernel(X6TArgs a) {
 // A/B: 0 conv_x6_kernel only, 1 + the pre-split form where it fits, 2 (default) + the pixel-tiled form where it
 // loads the busiest CU less than the pre-split one, 3 the pixel-tiled form wherever it applies
 static int g_x6_variant = 2;
+// conv_x6t workgroup width: 0 auto (4 waves where the 8-wave grid leaves CUs idle), 8 or 4 forced
+static int g_x6t_waves = 0;
 
 int x6p_ncu() {
   static int ncu = 0;
@@ -820,22 +825,33 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
     X6Args ap{};
     const int tmp = g_x6_variant >= 1 ? x6p_geometry(W, Cin, Cout, M, ap).tm : 0;
     const long long ncu = x6p_ncu(), t16 = (B + x6t::E - 1) / x6t::E;
-    const long long load_t = (2 * t16 + ncu - 1) / ncu * x6t::E * kPairs.n / 2;  // two 128-channel halves
+    const int nwt = g_x6t_waves ? g_x6t_waves : (t16 * 2 < ncu ? 4 : 8);  // as the launch below picks
+    const long long load_t = ((256 / (16 * nwt)) * t16 + ncu - 1) / ncu * x6t::E * kPairs.n * nwt / 16;
     const long long load_p = tmp ? ((M + tmp - 1) / tmp + ncu - 1) / ncu * tmp * 9 : load_t + 1;
     tiled = g_x6_variant == 2 && load_t < load_p;
   }
   if (tiled) {
     X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx, bias, act_bias, act, A,
               (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin};
-    const dim3 grid((unsigned)((B + x6t::E - 1) / x6t::E), (unsigned)(Cout / 128));
-    auto launch = [&](auto kern) {
+    // 4-wave (64-channel) workgroups where the 8-wave grid leaves CUs idle (mzba_conv_x6_set_waves: auto / 8 / 4)
+    const long long t16 = (B + x6t::E - 1) / x6t::E;
+    const int nw = g_x6t_waves ? g_x6t_waves : (t16 * (Cout / 128) < x6p_ncu() ? 4 : 8);
+    const dim3 grid((unsigned)t16, (unsigned)(Cout / (16 * nw)));
+    auto launch = [&](auto kern, int nthreads) {
       mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
-      hipLaunchKernelGGL(kern, grid, dim3(x6::NT), x6t::LDS, stream, t);
+      hipLaunchKernelGGL(kern, grid, dim3(nthreads), x6t::LDS, stream, t);
     };
-    if (ks == 1)
-      launch(conv_x6t_kernel<false, 1>);  // the reward / value heads' 1x1 ConvBlocks (never gathered)
-    else
-      ga ? launch(conv_x6t_kernel<true, 3>) : launch(conv_x6t_kernel<false, 3>);
+    if (nw == 4) {
+      if (ks == 1)
+        launch(conv_x6t_kernel<false, 1, 4>, 256);
+      else
+        ga ? launch(conv_x6t_kernel<true, 3, 4>, 256) : launch(conv_x6t_kernel<false, 3, 4>, 256);
+    } else {
+      if (ks == 1)
+        launch(conv_x6t_kernel<false, 1>, 512);  // the reward / value heads' 1x1 ConvBlocks (never gathered)
+      else
+        ga ? launch(conv_x6t_kernel<true, 3>, 512) : launch(conv_x6t_kernel<false, 3>, 512);
+    }
     MZ_LAUNCH_CHECK();
     return 0;
   }
@@ -924,6 +940,12 @@ extern "C" {
 int mzba_conv_x6_set_variant(int v) {
   if (v < 0 || v > 3) return -1;
   g_x6_variant = v;
+  return 0;
+}
+
+int mzba_conv_x6_set_waves(int nw) {
+  if (nw != 0 && nw != 4 && nw != 8) return -1;
+  g_x6t_waves = nw;
   return 0;
 }
 

@@ -714,7 +714,7 @@ def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, Cout, relu, with_res,
     """mzba_conv_x6 (the f32 parity path's latent convs as six split-bf16 MFMA products each) against an f64
     conv of the same f32 operands: at least as close as the f32-input MFMA conv of the f32 path (mzba_conv2d
     dtype 0) — within 2x its error + 1e-7 of the magnitude — and within 2e-6 of the magnitude absolutely
-    (ragged tiles, tiles crossing envs, every tap that leaves the image); the pre-split form (default) and the
+    (ragged tiles, tiles crossing envs, every tap that leaves the image); the pre-split form (variant 1) and the
     per-read-split kernel bit-identical where both sum (tap, channel step) in order (same_order); round 5's 16x20
     instances: Cin 256 staged in two 128-channel blocks (160-pixel tiles; sums (block, tap, step): within 4e-6 of
     the per-read-split kernel), Cout 128 (the representation's 128-channel blocks; no per-read-split twin, the A/B
@@ -736,7 +736,12 @@ def test_conv_x6_is_as_close_to_exact_as_f32(B, H, W, Cin, Cout, relu, with_res,
         ref = torch.relu(ref)
     wx = split_pack_x6(w.cpu().numpy().reshape(Cout, -1), Cout, 3, Cin).cuda()
     out = torch.full((B, H, W, Cout), float("nan"), device=dev)
-    L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu, L.stream())
+    try:  # the pre-split form (variant 1; the default may pick the pixel-tiled form at 4x5, tested on its own below)
+        assert L.lib().mzba_conv_x6_set_variant(1) == 0
+        L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu,
+               L.stream())
+    finally:
+        L.lib().mzba_conv_x6_set_variant(2)
     # the per-read-split kernel (the fallback where the pre-split form's rows do not fit): the same sums in the same order
     out2 = torch.full((B, H, W, Cout), float("nan"), device=dev)
     try:
@@ -833,6 +838,22 @@ def test_conv_x6_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks):
         assert ep <= 4e-6 * scale, msg  # each within ~2e-6 of f64: apart by up to the sum
     print(msg)
     assert et <= 2 * e32 + 1e-7 * scale and et <= 2e-6 * scale, msg
+    # the 4-wave (64-channel) and 8-wave (128-channel) workgroups: per 16-channel tile the same arithmetic, so the
+    # same bits (the auto choice takes 4 waves where the 8-wave grid leaves CUs idle, e.g. config 2's 1 024 envs)
+    outs = []
+    try:
+        for nw in (8, 4):
+            assert L.lib().mzba_conv_x6_set_waves(nw) == 0 and L.lib().mzba_conv_x6_set_variant(3) == 0
+            o = torch.full_like(out, float("nan"))
+            L.call("mzba_conv_x6_ex", L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(wx), L.ptr(b), L.ptr(tab),
+                   L.ptr(act), A if tab is not None else 0, L.ptr(res), L.ptr(o), B, H, W, Cin, Cout, ks, relu, L.stream())
+            outs.append(o)
+    finally:
+        L.lib().mzba_conv_x6_set_waves(0)
+        L.lib().mzba_conv_x6_set_variant(2)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], out)
+    assert L.lib().mzba_conv_x6_set_waves(6) == -1
 
 
 # ------------------------------------------------------------------------------ MCTS
