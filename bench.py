@@ -356,7 +356,7 @@ def learner_kernels(B, dt):
 
 def conv_counters(B, H, W, kname):
     """PMC record of the non-fused path's dominant conv kernel (config 3's halo conv) at this batch and latent size
-    (profiles/conv_counters.json, tools/gpu_run.sh step 'pmck' + tools/pmc_conv.py: HBM bytes per launch from the
+    (profiles/conv_counters.json, tools/gpu_run.sh step 'pmck' + tools/pmc_conv_summary.py: HBM bytes per launch from the
     FETCH_SIZE / WRITE_SIZE passes, MFMA busy / clock / LDS conflicts from the SQ passes of the same bench)."""
     tpath = os.path.join(ROOT, "profiles", "conv_counters.json")
     if not os.path.exists(tpath):

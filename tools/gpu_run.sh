@@ -98,7 +98,7 @@ for step in "$@"; do
         timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -d $O/$name/$sub -o run -- python3 bench.py $args \
           > $O/$name/$sub.log 2>&1
       done
-      python3 tools/pmc_conv.py $O/$name "$kname" $envs $hh $ww $O/conv_counters.json > $O/$name.json
+      python3 tools/pmc_conv_summary.py $O/$name "$kname" $envs $hh $ww $O/conv_counters.json > $O/$name.json
       rm -rf $O/$name/fetch $O/$name/write $O/$name/sq1 $O/$name/sq2
       cat $O/$name.json ;;
     rehearse)

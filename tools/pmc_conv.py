@@ -1,48 +1,38 @@
-"""PMC summary of one conv kernel of a bench run (config 3's `conv_halo_kernel`): HBM bytes per launch from the
-FETCH_SIZE / WRITE_SIZE passes (FETCH_SIZE x2: the gfx950 half-count of 16-B coalesced reads; both in KB) and the SQ
-figures of the two SQ passes (tools/pmc_sq.py), beside the launch's algorithmic bytes, merged into a records file
-that bench.py reads for the non-fused acting path (profiles/conv_counters.json).
-  pmc_conv.py DIR KERNEL_NAME ENVS H W OUT_JSON
-DIR holds the rocprofv3 outputs fetch/, write/, sq1/, sq2/ (tools/gpu_run.sh step 'pmck')."""
-import json
+"""Single-shape driver for PMC passes on the dominant kernel at the bench's B: run under
+`rocprofv3 --pmc FETCH_SIZE --kernel-trace` (and WRITE_SIZE in a separate pass).
+  pmc_conv.py B            conv_lat 3x3 256->256 (one latent residual conv)
+  pmc_conv.py B tower N    tower_kernel, N residual blocks (the bench's dyn/pred tower)"""
 import os
 import sys
 
-import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "muzero-breakout_amd"))
+import torch  # noqa: E402
+from mzba import _lib as L  # noqa: E402
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from rocpd_report import counter_values  # noqa: E402
-from pmc_sq import summarize  # noqa: E402
-
-
-def algorithmic_bytes(B, H, W, C=256):
-    """One 3x3 C -> C conv of the latent residual blocks: input + output image (+ the residual image on the second
-    conv of every block: half the launches) + the bf16 weights."""
-    img = B * H * W * C * 2
-    return 2 * img + 0.5 * img + 9 * C * C * 2
-
-
-if __name__ == "__main__":
-    d, kname, B, H, W, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), sys.argv[6]
-    f = counter_values(os.path.join(d, "fetch"), "FETCH_SIZE", kname)
-    w = counter_values(os.path.join(d, "write"), "WRITE_SIZE", kname)
-    s1 = summarize(os.path.join(d, "sq1"), kname)
-    s2 = summarize(os.path.join(d, "sq2"), kname)
-    fetch = float(np.mean(f)) * 1024 * 2 if f else None
-    write = float(np.mean(w)) * 1024 if w else None
-    rec = {"kernel_name": kname, "envs": B, "H": H, "W": W, "fetch_bytes": fetch, "write_bytes": write,
-           "bytes_per_launch": fetch + write if f and w else None, "algorithmic_bytes": algorithmic_bytes(B, H, W),
-           "n_samples": [len(f), len(w)], "mfma_busy": s1.get("mfma_busy"), "clock_ghz": s1.get("clock_ghz"),
-           "wait_inst": s1.get("wait_inst"), "duration_ns": s1.get("duration_ns"),
-           "lds_bank_conflict_frac": (s2["SQ_LDS_BANK_CONFLICT"] / s2["SQ_LDS_IDX_ACTIVE"])
-           if s2.get("SQ_LDS_IDX_ACTIVE") else None,
-           "source": d,
-           "method": "rocprofv3 --pmc passes of their own (FETCH_SIZE; WRITE_SIZE; two SQ groups), --kernel-trace, over "
-                     "the eager acting bench (--no-graph --no-cpu); traffic = mean per launch, SQ = medians"}
-    db = {"records": []}
-    if os.path.exists(out):
-        db = json.load(open(out))
-    db["records"] = [r for r in db["records"] if (r.get("envs"), r.get("H"), r.get("W"), r.get("kernel_name"))
-                     != (B, H, W, kname)] + [rec]
-    json.dump(db, open(out, "w"), indent=1)
-    print(json.dumps(rec))
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+H, W, C = 4, 5, 256
+if len(sys.argv) > 2 and sys.argv[2] == "tower":
+    nb = int(sys.argv[3]) if len(sys.argv) > 3 else 14
+    x = torch.randn(B * H * W * C, device="cuda").to(torch.bfloat16)
+    out = torch.empty_like(x)
+    wf = (torch.randn(2 * nb * C * 9 * C + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
+    b = torch.zeros(2 * nb * C, device="cuda")
+    nws = L.lib().mzba_tower_ws_bytes(B)
+    ws = torch.zeros(max(nws, 16), dtype=torch.uint8, device="cuda")
+    for _ in range(20):
+        L.call("mzba_tower", L.ptr(x), H * W * C, None, 0, L.ptr(out), L.ptr(wf), L.ptr(b), nb, B, L.ptr(ws), nws,
+               L.stream())
+    torch.cuda.synchronize()
+    print("done tower", B, nb)
+    sys.exit(0)
+x = torch.randn(B * H * W * C, device="cuda").to(torch.bfloat16)
+res = torch.randn(B * H * W * C, device="cuda").to(torch.bfloat16)
+out = torch.empty(B * H * W * C, device="cuda", dtype=torch.bfloat16)
+w = (torch.randn(C * 9 * C + 8 * 64 * 8, device="cuda") * 0.02).to(torch.bfloat16)
+b = torch.zeros(C, device="cuda")
+for _ in range(20):
+    L.call("mzba_conv_lat", L.ptr(x), H * W * C, None, 0, L.ptr(w), L.ptr(b), None, None, 0, L.ptr(res), L.ptr(out),
+           B, H, W, C, C, 3, 1, L.stream())
+torch.cuda.synchronize()
+print("done", B)
