@@ -480,6 +480,10 @@ int mzba_conv_wpack(int dtype, const float* w, void* wt, int Cout, int taps, int
  * (N x Cc; flip: N <= Cin, Cc = Cout), + pad zero elements. */
 int mzba_conv_pack_bf16(const float* w, void* out, int Cout, int taps, int Cin, int N, int Cc, int flip, int layout,
                         long long pad, hipStream_t stream);
+/* njobs mzba_conv_pack_bf16 calls in ceil(njobs / 32) launches (the learner's per-minibatch packs, round 5):
+ * w[j], out[j] (16-B aligned), prm[8 j .. 8 j + 7] = {Cout, taps, Cin, N, Cc, flip, layout, pad} (pad % 8 == 0);
+ * host arrays; the same outputs as the separate calls. */
+int mzba_conv_pack_bf16_multi(const float* const* w, void* const* out, const int* prm, int njobs, hipStream_t stream);
 /* Conv2d weight / bias gradient: dw [Cout][ks*ks][Cin] += sum_m dy[m][co] * x_tap[m][ci],
  * db [Cout] += sum_m dy[m][co] (db may be NULL). x NHWC [B][H][W][Cin], dy [B][H][W][Cout]. */
 long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks);

@@ -53,6 +53,7 @@ MZ_DEV float4 f4add(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.
 // part[chunk][c] = (chunk mean, chunk M2) over rows [chunk*rpc, min(M, (chunk+1)*rpc)).
 // 256 threads = (channel quads of a 64-channel group = 16) x 16 row lanes.
 constexpr int BN_RPC = 64;
+constexpr int BN_FK = 8;  // chunks per lane the BN finalisers load ahead (nchunk <= 512 in one round trip)
 template <typename T>
 __global__ __launch_bounds__(256) void bn_stats_partial_kernel(const T* __restrict__ x, int M, int C, int rpc,
                                                                float2* __restrict__ part) {
@@ -108,7 +109,17 @@ __global__ __launch_bounds__(64) void bn_stats_final_kernel(const float2* __rest
                                                             float* __restrict__ run_mean, float* __restrict__ run_var) {
   const int c = blockIdx.x, lane = threadIdx.x;
   double n = 0, mean = 0, m2 = 0;
-  for (int k = lane; k < nchunk; k += 64) {
+  // the lane's chunks l, l + 64, ... (up to BN_FK of them) are all loaded before the first fold: a rolled
+  // load-then-fold loop waited one memory round trip per chunk. The folds keep their order (the same sums)
+  float2 pv[BN_FK];
+#pragma unroll
+  for (int i = 0; i < BN_FK; ++i) pv[i] = lane + 64 * i < nchunk ? part[(size_t)(lane + 64 * i) * C + c] : float2{};
+#pragma unroll
+  for (int i = 0; i < BN_FK; ++i) {
+    const int k = lane + 64 * i;
+    if (k < nchunk) chan_combine(n, mean, m2, (double)min(rpc, M - k * rpc), (double)pv[i].x, (double)pv[i].y);
+  }
+  for (int k = lane + 64 * BN_FK; k < nchunk; k += 64) {
     const float2 p = part[(size_t)k * C + c];
     chan_combine(n, mean, m2, (double)min(rpc, M - k * rpc), (double)p.x, (double)p.y);
   }
@@ -202,7 +213,16 @@ __global__ __launch_bounds__(64) void bn_bwd_final_kernel(const float2* __restri
                                                           float* __restrict__ dbeta, float* __restrict__ coef) {
   const int c = blockIdx.x, lane = threadIdx.x;
   double sg = 0, dot = 0;
-  for (int k = lane; k < nchunk; k += 64) {
+  float2 pv[BN_FK];  // loaded before the first add, as bn_stats_final_kernel (the same sums)
+#pragma unroll
+  for (int i = 0; i < BN_FK; ++i) pv[i] = lane + 64 * i < nchunk ? part[(size_t)(lane + 64 * i) * C + c] : float2{};
+#pragma unroll
+  for (int i = 0; i < BN_FK; ++i)
+    if (lane + 64 * i < nchunk) {
+      sg += pv[i].x;
+      dot += pv[i].y;
+    }
+  for (int k = lane + 64 * BN_FK; k < nchunk; k += 64) {
     const float2 p = part[(size_t)k * C + c];
     sg += p.x;
     dot += p.y;
@@ -296,6 +316,54 @@ __global__ void conv_pack_kernel(const float* __restrict__ w, bf16_t* __restrict
     }
     const float v = flip ? w[((size_t)c * taps + (taps - 1 - tap)) * Cin + n] : w[((size_t)n * taps + tap) * Cin + c];
     out[i] = f32_to_bf16(v);
+  }
+}
+
+// Many packs in one launch (the learner's per-minibatch packs of every conv: one launch per PK_MAX of them instead of
+// one each): blockIdx.y = job, a thread per 8 consecutive output elements (8 consecutive c of one (n, tap): Cc % 32
+// == 0 and pad % 8 == 0), the same element values as conv_pack_kernel, one 16-B store.
+struct PackJob {
+  const float* w;
+  bf16_t* out;
+  int Cout, taps, Cin, N, Cc, flip, layout, pad;
+};
+constexpr int PK_MAX = 32;
+struct PackJobs {
+  PackJob j[PK_MAX];
+};
+__global__ __launch_bounds__(256) void conv_pack_multi_kernel(PackJobs js) {
+  const PackJob& jb = js.j[blockIdx.y];
+  const int taps = jb.taps, Cc = jb.Cc, Cin = jb.Cin;
+  const int n_el = jb.N * taps * Cc, ng = (n_el + jb.pad) / 8;
+  for (int g8 = blockIdx.x * blockDim.x + threadIdx.x; g8 < ng; g8 += gridDim.x * blockDim.x) {
+    const int i = 8 * g8;
+    uint4 o = make_uint4(0, 0, 0, 0);
+    if (i < n_el) {
+      int n, tap, c, q = i / 8;
+      if (jb.layout == 1) {
+        const int r = q % 32; q /= 32;
+        const int h = q % 2; q /= 2;
+        const int cc = q % (Cc / 32); q /= Cc / 32;
+        tap = q % taps; q /= taps;
+        const int kh = q % 2, ct = q / 2;
+        n = 32 * ct + r;
+        c = kh * (Cc / 2) + 16 * cc + 8 * h;
+      } else {
+        const int r = q % 16; q /= 16;
+        const int g = q % 4; q /= 4;
+        const int nk = taps * Cc / 32, s_ = q % nk, ct = q / nk;
+        n = 16 * ct + r;
+        const int k = 32 * s_ + 8 * g, qq = k / Cc;
+        c = k - qq * Cc;
+        tap = (qq % 3) * 3 + qq / 3;
+      }
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = jb.flip ? jb.w[((size_t)(c + j) * taps + (taps - 1 - tap)) * Cin + n] : jb.w[((size_t)n * taps + tap) * Cin + c + j];
+      o = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    }
+    *reinterpret_cast<uint4*>(jb.out + i) = o;
   }
 }
 
@@ -801,14 +869,23 @@ static bool wgrad_img_plan(int B, int Bseg, int H, int W, int Cin, int Cout, WgP
 // the weight and bias partials of one split weight-gradient launch, summed in one launch: acc[i] += sum_s
 // part[s][i] for i < n, bacc[j] += sum_s bpart[s][j] for j < nb, each element in split order (round 4: one launch
 // instead of one per buffer, the same sums)
+constexpr int SP_FK = 16;
 __global__ void sum_partials2_kernel(const float* __restrict__ part, const float* __restrict__ bpart, int nsplit,
                                      size_t n, size_t nb, float* __restrict__ acc, float* __restrict__ bacc) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + nb; i += (size_t)gridDim.x * blockDim.x) {
     const bool w = i < n;
     const float* p = w ? part + i : bpart + (i - n);
     const size_t st = w ? n : nb;
-    float s = p[0];
-    for (int k = 1; k < nsplit; ++k) s += p[(size_t)k * st];
+    // the first SP_FK partials loaded before the first add (a rolled loop waited one round trip per split); the
+    // adds keep split order
+    float v[SP_FK];
+#pragma unroll
+    for (int k = 0; k < SP_FK; ++k) v[k] = k < nsplit ? p[(size_t)k * st] : 0.f;
+    float s = v[0];
+#pragma unroll
+    for (int k = 1; k < SP_FK; ++k)
+      if (k < nsplit) s += v[k];
+    for (int k = SP_FK; k < nsplit; ++k) s += p[(size_t)k * st];
     (w ? acc[i] : bacc[i - n]) += s;
   }
 }
@@ -1285,6 +1362,31 @@ int mzba_conv_pack_bf16(const float* w, void* out, int Cout, int taps, int Cin, 
   hipLaunchKernelGGL(conv_pack_kernel, dim3(grid_for(n)), dim3(256), 0, stream, w, (bf16_t*)out, Cout, taps, Cin, N, Cc,
                      flip, layout, (size_t)pad);
   MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+// njobs packs, each the arguments of one mzba_conv_pack_bf16 call: w[j], out[j] (16-B aligned) and
+// prm[8 j ..] = {Cout, taps, Cin, N, Cc, flip, layout, pad}; the same outputs as the njobs separate calls, in
+// launches of PK_MAX jobs
+int mzba_conv_pack_bf16_multi(const float* const* w, void* const* out, const int* prm, int njobs, hipStream_t stream) {
+  MZ_CHECK_ARG(w && out && prm && njobs > 0, -1);
+  for (int j0 = 0; j0 < njobs; j0 += PK_MAX) {
+    PackJobs js{};
+    const int nj = njobs - j0 < PK_MAX ? njobs - j0 : PK_MAX;
+    for (int k = 0; k < nj; ++k) {
+      const int* p = prm + 8 * (j0 + k);
+      const int Cout = p[0], taps = p[1], Cin = p[2], N = p[3], Cc = p[4], flip = p[5], layout = p[6], pad = p[7];
+      MZ_CHECK_ARG(w[j0 + k] && out[j0 + k] && ((uintptr_t)out[j0 + k] & 15) == 0 && Cout > 0 && Cin > 0 && N > 0 &&
+                       Cc > 0 && pad >= 0 && pad % 8 == 0 && (layout == 1 || layout == 2), -1);
+      MZ_CHECK_ARG(layout != 1 || (N % 32 == 0 && Cc % 32 == 0), -2);
+      MZ_CHECK_ARG(layout != 2 || (taps == 9 && N % 16 == 0 && Cc % 32 == 0), -3);
+      MZ_CHECK_ARG(flip ? (N <= Cin && Cc == Cout) : (N == Cout && Cc <= Cin), -4);
+      MZ_CHECK_ARG((long long)N * taps * Cc + pad < (1LL << 31), -5);
+      js.j[k] = PackJob{w[j0 + k], (bf16_t*)out[j0 + k], Cout, taps, Cin, N, Cc, flip, layout, pad};
+    }
+    hipLaunchKernelGGL(conv_pack_multi_kernel, dim3(64, nj), dim3(256), 0, stream, js);
+    MZ_LAUNCH_CHECK();
+  }
   return 0;
 }
 

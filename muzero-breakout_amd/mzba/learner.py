@@ -360,6 +360,7 @@ class Learner:
         band layouts), and flipped-transposed packs for the input-gradient convs."""
         s = L.stream()
         pad = LAT_PAD_ELEMS
+        jobs = []  # the conv_lat / band packs: one mzba_conv_pack_bf16_multi call (32 per launch)
         for c in self.convs:
             taps = c.ks * c.ks
             first = c is self.rep[0][1]  # the input planes need no gradient
@@ -379,15 +380,19 @@ class Learner:
                 if c.fkind == "gen":
                     L.call("mzba_conv_wpack", 1, L.ptr(c.w), L.ptr(c.wf), c.cout, taps, c.cin_p, c.cin_p, 0, s)
                 else:
-                    L.call("mzba_conv_pack_bf16", L.ptr(c.w), L.ptr(c.wf), c.cout, taps, c.cin_p, c.cout, c.cin_p, 0,
-                           1 if c.fkind == "lat" else 2, pad, s)
+                    jobs.append((c.w, c.wf, (c.cout, taps, c.cin_p, c.cout, c.cin_p, 0, 1 if c.fkind == "lat" else 2, pad)))
             if first:
                 continue
             if c.dkind == "gen":
                 L.call("mzba_conv_wpack", self.dt, L.ptr(c.w), L.ptr(c.wt), c.cout, taps, c.cin_p, cin_used, 1, s)
             else:
-                L.call("mzba_conv_pack_bf16", L.ptr(c.w), L.ptr(c.wt), c.cout, taps, c.cin_p, cin_used, c.cout, 1,
-                       1 if c.dkind == "lat" else 2, pad, s)
+                jobs.append((c.w, c.wt, (c.cout, taps, c.cin_p, cin_used, c.cout, 1, 1 if c.dkind == "lat" else 2, pad)))
+        if jobs:
+            n = len(jobs)
+            w = (ctypes.c_void_p * n)(*[j[0].data_ptr() for j in jobs])
+            o = (ctypes.c_void_p * n)(*[j[1].data_ptr() for j in jobs])
+            prm = (ctypes.c_int * (8 * n))(*[v for j in jobs for v in j[2]])
+            L.call("mzba_conv_pack_bf16_multi", ctypes.addressof(w), ctypes.addressof(o), ctypes.addressof(prm), n, s)
 
     def _run_conv(self, kind, x, cin, w, bias, res, out, B, H, W, cout, ks):
         s = L.stream()
