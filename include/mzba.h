@@ -119,6 +119,9 @@ int mzba_conv_halo_ex_supported(int H, int W, int Cin, int Cout, int ks, int gat
 int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wh,
                       const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,
                       int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream);
+/* Waves per workgroup of the Cin 256 one-block halo instances: 0 default (8), 4, 8; -1 otherwise. Outputs are
+ * identical for every choice (each accumulator takes its taps in the same order). */
+int mzba_conv_halo_set_waves(int nw);
 /* f32-faithful 3x3 conv on bf16 MFMAs (the f32 parity path's latent towers, networks.py:19-35): f32 NHWC in /
  * out, out = act(conv3x3(in) + bias (+ res)); every f32 operand split into three bf16 parts and each product
  * taken as the six terms down to 2^-18 (csrc/conv_x6.hip), as close to exact as an f32 conv. wx = the three

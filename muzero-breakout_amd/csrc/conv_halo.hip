@@ -190,12 +190,13 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
 // 21x21): WM = 1 (8 slices of 32 channels over all 256 pixels: no weight fragment loaded twice per workgroup,
 // half the per-CU L2 weight stream, twice the B reads) 1.76-1.85 ms vs 1.75-1.83; B fragments read 16 MFMAs
 // ahead instead of 8: 1.82-1.83 ms. Neither the weight stream nor the LDS read latency bounds this kernel.
-template <int CB, int NBLK, int WM = 2, int PFM = 1, int TN = hl::TN, bool GA = false>
-__global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
+template <int CB, int NBLK, int WM = 2, int PFM = 1, int TN = hl::TN, bool GA = false, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 1) void conv_halo_kernel(HaloArgs a) {
   constexpr int RB = CB * 2;        // bytes per staged row
   constexpr int NC = CB / 8;        // 16-B chunks per row
   constexpr int NCS = CB / 32;      // 32-channel k steps per tap and block
-  constexpr int WN = 8 / WM, CT = TN / 16 / WN, MT = 16 / WM;  // channel slices, column tiles / pixel tiles per wave
+  constexpr int WN = NW / WM, CT = TN / 16 / WN, MT = 16 / WM;  // channel slices, column tiles / pixel tiles per wave
+  constexpr int NT = 64 * NW;
   constexpr int PF = PFM * 8 / CT;  // fragment reads ahead: 8 PFM MFMAs
   static_assert(NCS % 2 == 0, "ring slot = channel step parity");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
   constexpr int nsteps = NBLK * 9 * NCS;  // NBLK = Cin / CB
 
   // the zero block: 16 rows (never overwritten by staging)
-  for (int i = tid; i < RB; i += hl::NT) *reinterpret_cast<uint4*>(lds + a.ZOFF + i * 16) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < RB; i += NT) *reinterpret_cast<uint4*>(lds + a.ZOFF + i * 16) = make_uint4(0, 0, 0, 0);
 
   // per pixel tile mi of the wave: the lane's pixel is staged row prow0 + 16 mi at tap (0, 0); byte mi of
   // okw[mi / 4] says which taps stay in the image (bit 0: y > 0, 1: y < H - 1, 2: x > 0, 3: x < W - 1,
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(hl::NT, 1) void conv_halo_kernel(HaloArgs a) {
     }
     // stage rows [m0 - HALO, m0 - HALO + HR) x channels [blk CB, (blk + 1) CB): block i of 1 KiB holds
     // chunks 64 i .. 64 i + 63 (row g / NC, physical chunk g % NC = logical chunk ^ hkey(row))
-    for (int i = wave; i < a.NI; i += 8) {
+    for (int i = wave; i < a.NI; i += NW) {
       const int g = i * 64 + lane, r = g / NC, s = g - r * NC;
       int m = m0 - a.HALO + r;
       m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);  // rows outside [0, M) are only read by masked taps
@@ -364,7 +365,17 @@ int halo_geometry(int W, int Cin, HaloArgs& g) {
 
 }  // namespace
 
+static int g_halo_waves = 0;
+
 extern "C" {
+
+// waves per workgroup of the Cin 256 one-block instances (config 3's 21x21 convs): 0 default (8: two per SIMD, each
+// 128 pixels x 64 channels), 4 (one per SIMD, 128 pixels x 128 channels: half the LDS fragment reads per MFMA), 8
+int mzba_conv_halo_set_waves(int nw) {
+  if (nw != 0 && nw != 4 && nw != 8) return -1;
+  g_halo_waves = nw;
+  return 0;
+}
 
 int mzba_conv_halo_supported(int H, int W, int Cin, int Cout, int ks) {
   HaloArgs g{};
@@ -400,19 +411,22 @@ int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot,
   const int tn = Cout % 256 == 0 ? 256 : 128;
   const dim3 grid((unsigned)((M + hl::TM - 1) / hl::TM), (unsigned)(Cout / tn));
   typedef void (*Kern)(HaloArgs);
-  static const Kern kerns[6] = {conv_halo_kernel<256, 1, 2, 1, 256, true>, conv_halo_kernel<256, 1, 4, 1, 128>,
+  static const Kern kerns[8] = {conv_halo_kernel<256, 1, 2, 1, 256, true>, conv_halo_kernel<256, 1, 4, 1, 128>,
                                 conv_halo_kernel<256, 1>, conv_halo_kernel<128, 1>, conv_halo_kernel<128, 2>,
-                                conv_halo_kernel<128, 1, 4, 1, 128>};
+                                conv_halo_kernel<128, 1, 4, 1, 128>, conv_halo_kernel<256, 1, 2, 1, 256, true, 4>,
+                                conv_halo_kernel<256, 1, 2, 1, 256, false, 4>};
   static const bool attrs = [] {  // every instance: the 160 KiB of dynamic LDS
     for (Kern k : kerns)
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, hl::LDS_MAX);
     return true;
   }();
   (void)attrs;
-  const Kern kern = ga ? kerns[0]
+  const bool w4 = g_halo_waves == 4;  // the Cin 256 one-block instances: 4 waves of 128 pixels x 128 channels
+  const Kern kern = ga ? kerns[w4 ? 6 : 0]
                        : tn == 128 ? (Cin == 256 ? kerns[1] : kerns[5])
-                                   : (a.CB == 256 ? kerns[2] : (Cin == 128 ? kerns[3] : kerns[4]));
-  hipLaunchKernelGGL(kern, grid, dim3(hl::NT), lds, stream, a);
+                                   : (a.CB == 256 ? kerns[w4 ? 7 : 2] : (Cin == 128 ? kerns[3] : kerns[4]));
+  const int nt = w4 && tn == 256 && a.CB == 256 ? 256 : hl::NT;
+  hipLaunchKernelGGL(kern, grid, dim3(nt), lds, stream, a);
   MZ_LAUNCH_CHECK();
   return 0;
 }

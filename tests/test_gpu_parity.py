@@ -706,6 +706,46 @@ def test_conv_halo_in_place_residual(B, H, W, Cin, Cout):
     assert torch.equal(out.view(torch.int16), inplace.view(torch.int16))
 
 
+@pytest.mark.parametrize("B,ga", [(150, False), (37, True)])
+def test_conv_halo_four_waves_equal_eight(B, ga):
+    """mzba_conv_halo_set_waves(4) (one wave per SIMD, 128 pixels x 128 channels each: the round-5 A/B form of the
+    Cin 256 one-block instances) gives the 8-wave outputs bit for bit, plain with a residual and gathered with an
+    action-bias table (each accumulator takes its taps in the same order); other wave counts are refused."""
+    from mzba import _lib as L
+    from mzba.agent import pack_lat16
+    H = W = 21
+    C, A, S = 256, 3, 2
+    HW = H * W
+    g = torch.Generator(device="cuda").manual_seed(B + 7)
+    dev = torch.device("cuda")
+    pool = torch.randn(B, S + 1, H, W, C, generator=g, device=dev).to(torch.bfloat16)
+    slot = torch.randint(0, S + 1, (B,), generator=g, device=dev, dtype=torch.int32)
+    act = torch.randint(0, A, (B,), generator=g, device=dev, dtype=torch.int32)
+    w = (torch.randn(C, 3, 3, C, generator=g, device=dev) / (C * 9) ** 0.5).to(torch.bfloat16)
+    b = torch.randn(C, generator=g, device=dev)
+    tab = torch.randn(HW, A, C, generator=g, device=dev)
+    res = torch.randn(B, H, W, C, generator=g, device=dev).to(torch.bfloat16)
+    wh = torch.tensor(pack_lat16(w.float().cpu().numpy().reshape(C, -1), C, 3, C)).to(torch.bfloat16).cuda()
+    x = pool[:, 0].contiguous()
+    outs = []
+    try:
+        for nw in (8, 4):
+            assert L.lib().mzba_conv_halo_set_waves(nw) == 0
+            o = torch.full((B, H, W, C), float("nan"), dtype=torch.bfloat16, device=dev)
+            if ga:
+                L.call("mzba_conv_halo_ex", L.ptr(pool), (S + 1) * HW * C, L.ptr(slot), HW * C, L.ptr(wh), L.ptr(b),
+                       L.ptr(tab), L.ptr(act), A, None, L.ptr(o), B, H, W, C, C, 1, L.stream())
+            else:
+                L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(o), B, H, W, C, C, 1, L.stream())
+            outs.append(o)
+    finally:
+        L.lib().mzba_conv_halo_set_waves(0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+    assert L.lib().mzba_conv_halo_set_waves(6) == -1
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,relu,with_res,same_order",
                          [(1000, 4, 5, 256, 256, 1, True, True), (37, 4, 5, 256, 256, 0, False, True),
                           (7, 16, 20, 128, 256, 1, True, True), (3, 21, 21, 256, 256, 1, True, True),
