@@ -108,6 +108,10 @@ __global__ __launch_bounds__(64) void bn_stats_final_kernel(const float2* __rest
                                                             const float* __restrict__ beta, float* __restrict__ stats,
                                                             float* __restrict__ run_mean, float* __restrict__ run_var) {
   const int c = blockIdx.x, lane = threadIdx.x;
+  // the per-channel operands of the tail, loaded with the partials (after the butterfly each was one more
+  // memory round trip on the chain)
+  const float g_c = gamma[c], b_c = beta[c];
+  const float rm_c = run_mean ? run_mean[c] : 0.f, rv_c = run_mean ? run_var[c] : 0.f;
   double n = 0, mean = 0, m2 = 0;
   // the lane's chunks l, l + 64, ... (up to BN_FK of them) are all loaded before the first fold: a rolled
   // load-then-fold loop waited one memory round trip per chunk. The folds keep their order (the same sums)
@@ -130,16 +134,16 @@ __global__ __launch_bounds__(64) void bn_stats_final_kernel(const float2* __rest
   if (lane) return;
   const float var = (float)(m2 / M);
   const float invstd = (float)(1.0 / sqrt((double)var + (double)eps));
-  const float alpha = invstd * gamma[c];
+  const float alpha = invstd * g_c;
   const float fm = (float)mean;
   stats[c] = fm;                 // mean
   stats[C + c] = invstd;         // invstd
   stats[2 * C + c] = alpha;      // gamma * invstd
-  stats[3 * C + c] = beta[c] - fm * alpha;
+  stats[3 * C + c] = b_c - fm * alpha;
   if (run_mean) {
-    run_mean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)run_mean[c]);
+    run_mean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rm_c);
     const double unbiased = M > 1 ? m2 / (double)(M - 1) : m2;
-    run_var[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)run_var[c]);
+    run_var[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)rv_c);
   }
 }
 
@@ -212,6 +216,8 @@ __global__ __launch_bounds__(64) void bn_bwd_final_kernel(const float2* __restri
                                                           const float* __restrict__ stats, float* __restrict__ dgamma,
                                                           float* __restrict__ dbeta, float* __restrict__ coef) {
   const int c = blockIdx.x, lane = threadIdx.x;
+  // the tail's per-channel operands, loaded with the partials (as bn_stats_final_kernel)
+  const float invstd = stats[C + c], alpha = stats[2 * C + c], dg_c = dgamma[c], db_c = dbeta[c];
   double sg = 0, dot = 0;
   float2 pv[BN_FK];  // loaded before the first add, as bn_stats_final_kernel (the same sums)
 #pragma unroll
@@ -232,12 +238,11 @@ __global__ __launch_bounds__(64) void bn_bwd_final_kernel(const float2* __restri
     dot += __shfl_xor(dot, o);
   }
   if (lane) return;
-  const float invstd = stats[C + c];
-  dgamma[c] += (float)dot * invstd;
-  dbeta[c] += (float)sg;
+  dgamma[c] = dg_c + (float)dot * invstd;
+  dbeta[c] = db_c + (float)sg;
   coef[c] = (float)(sg / M);
   coef[C + c] = (float)dot * invstd * invstd / (float)M;
-  coef[2 * C + c] = stats[2 * C + c];
+  coef[2 * C + c] = alpha;
 }
 
 template <typename T>
@@ -878,6 +883,8 @@ __global__ void sum_partials2_kernel(const float* __restrict__ part, const float
     const size_t st = w ? n : nb;
     // the first SP_FK partials loaded before the first add (a rolled loop waited one round trip per split); the
     // adds keep split order
+    float* dst = w ? acc + i : bacc + (i - n);
+    const float a0 = *dst;  // loaded with the partials (read after the sum it was one more round trip)
     float v[SP_FK];
 #pragma unroll
     for (int k = 0; k < SP_FK; ++k) v[k] = k < nsplit ? p[(size_t)k * st] : 0.f;
@@ -886,7 +893,7 @@ __global__ void sum_partials2_kernel(const float* __restrict__ part, const float
     for (int k = 1; k < SP_FK; ++k)
       if (k < nsplit) s += v[k];
     for (int k = SP_FK; k < nsplit; ++k) s += p[(size_t)k * st];
-    (w ? acc[i] : bacc[i - n]) += s;
+    *dst = a0 + s;
   }
 }
 
