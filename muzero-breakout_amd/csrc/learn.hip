@@ -912,6 +912,23 @@ __global__ void avgpool2_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx
   }
 }
 
+// the same element values, 4 channels per thread (C % 4 == 0) with 32-bit index arithmetic (n < 2^31): the
+// per-element 64-bit divisions above held the kernel at a fifth of the HBM rate
+template <typename T>
+__global__ void avgpool2_bwd4_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int H, int W, int C) {
+  const int C4 = C / 4, Ho = H / 2, Wo = W / 2;
+  const unsigned n4 = (unsigned)B * H * W * C4;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const unsigned c4 = i % C4;
+    unsigned q = i / C4;
+    const unsigned xx = q % W;
+    q /= W;
+    const unsigned yy = q % H, b = q / H;
+    const float4 v = Vec4<T>::load(dy + ((size_t)(b * Ho + yy / 2) * Wo + xx / 2) * C + 4 * c4);
+    Vec4<T>::store(dx + (size_t)i * 4, make_float4(v.x / 4.0f, v.y / 4.0f, v.z / 4.0f, v.w / 4.0f));
+  }
+}
+
 template <typename T>
 __global__ void axpy_kernel(T* __restrict__ y, const T* __restrict__ x, size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -1181,6 +1198,31 @@ __global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__
     m[i] = mv;
     v[i] = vv;
     p[i] = pv + (neg_step * mv) / (sqrtf(vv) / bc2s + eps);
+  }
+}
+
+// adam_dev_kernel's update, 4 parameters per thread (n % 4 == 0, 16-B aligned arrays: one 16-B access per array
+// instead of four 4-B ones)
+__global__ void adam_dev4_kernel(float4* __restrict__ p, const float4* __restrict__ grad, float4* __restrict__ m,
+                                 float4* __restrict__ v, size_t n4, const float* __restrict__ sc) {
+  const float neg_step = sc[0], one_m_b1 = sc[1], b2 = sc[2], one_m_b2 = sc[3], bc2s = sc[4], eps = sc[5], wd = sc[6];
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const float4 p4 = p[i], g4 = grad[i], m4 = m[i], v4 = v[i];
+    float po[4], mo[4], vo[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float pv = (&p4.x)[k];
+      const float g = (&g4.x)[k] + wd * pv;
+      const float mk = (&m4.x)[k];
+      const float mv = mk + one_m_b1 * (g - mk);
+      const float vv = (&v4.x)[k] * b2 + (one_m_b2 * g) * g;
+      mo[k] = mv;
+      vo[k] = vv;
+      po[k] = pv + (neg_step * mv) / (sqrtf(vv) / bc2s + eps);
+    }
+    m[i] = make_float4(mo[0], mo[1], mo[2], mo[3]);
+    v[i] = make_float4(vo[0], vo[1], vo[2], vo[3]);
+    p[i] = make_float4(po[0], po[1], po[2], po[3]);
   }
 }
 
@@ -1504,8 +1546,12 @@ int mzba_avgpool2_backward(int dtype, const void* dy, void* dx, int B, int H, in
   MZ_CHECK_ARG(dy && dx && B > 0 && H % 2 == 0 && W % 2 == 0, -1);
   return dispatch(dtype, [&](auto t) {
     using T = decltype(t);
-    hipLaunchKernelGGL(avgpool2_bwd_kernel<T>, dim3(grid_for((size_t)B * H * W * C)), dim3(256), 0, stream,
-                       (const T*)dy, (T*)dx, B, H, W, C);
+    if (C % 4 == 0 && (long long)B * H * W * C < (1LL << 31))
+      hipLaunchKernelGGL(avgpool2_bwd4_kernel<T>, dim3(grid_for((size_t)B * H * W * C / 4)), dim3(256), 0, stream,
+                         (const T*)dy, (T*)dx, B, H, W, C);
+    else
+      hipLaunchKernelGGL(avgpool2_bwd_kernel<T>, dim3(grid_for((size_t)B * H * W * C)), dim3(256), 0, stream,
+                         (const T*)dy, (T*)dx, B, H, W, C);
     MZ_LAUNCH_CHECK();
     return 0;
   });
@@ -1611,8 +1657,13 @@ int mzba_adam_dev(float* p, const float* grad, float* m, float* v, long long n, 
                   hipStream_t stream) {
   MZ_CHECK_ARG(p && grad && m && v && scalars && n >= 0, -1);
   if (n == 0) return 0;
-  hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, stream, p, grad, m, v, (size_t)n,
-                     scalars);
+  const bool a16 = (((uintptr_t)p | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+  if (n % 4 == 0 && a16)
+    hipLaunchKernelGGL(adam_dev4_kernel, dim3(grid_for((size_t)n / 4)), dim3(256), 0, stream, (float4*)p,
+                       (const float4*)grad, (float4*)m, (float4*)v, (size_t)n / 4, scalars);
+  else
+    hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, stream, p, grad, m, v, (size_t)n,
+                       scalars);
   MZ_LAUNCH_CHECK();
   return 0;
 }
