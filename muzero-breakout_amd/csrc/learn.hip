@@ -1201,11 +1201,15 @@ __global__ void adam_dev_kernel(float* __restrict__ p, const float* __restrict__
   }
 }
 
-// adam_dev_kernel's update, 4 parameters per thread (n % 4 == 0, 16-B aligned arrays: one 16-B access per array
-// instead of four 4-B ones)
-__global__ void adam_dev4_kernel(float4* __restrict__ p, const float4* __restrict__ grad, float4* __restrict__ m,
-                                 float4* __restrict__ v, size_t n4, const float* __restrict__ sc) {
-  const float neg_step = sc[0], one_m_b1 = sc[1], b2 = sc[2], one_m_b2 = sc[3], bc2s = sc[4], eps = sc[5], wd = sc[6];
+// adam_kernel's / adam_dev_kernel's update, 4 parameters per thread (n % 4 == 0, 16-B aligned arrays: one 16-B access
+// per array instead of four 4-B ones); DEV: the scalars from device memory (sc), else from the arguments
+template <bool DEV>
+__global__ void adam4_kernel(float4* __restrict__ p, const float4* __restrict__ grad, float4* __restrict__ m,
+                             float4* __restrict__ v, size_t n4, const float* __restrict__ sc, float a_neg_step,
+                             float a_one_m_b1, float a_b2, float a_one_m_b2, float a_bc2s, float a_eps, float a_wd) {
+  const float neg_step = DEV ? sc[0] : a_neg_step, one_m_b1 = DEV ? sc[1] : a_one_m_b1, b2 = DEV ? sc[2] : a_b2;
+  const float one_m_b2 = DEV ? sc[3] : a_one_m_b2, bc2s = DEV ? sc[4] : a_bc2s, eps = DEV ? sc[5] : a_eps;
+  const float wd = DEV ? sc[6] : a_wd;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     const float4 p4 = p[i], g4 = grad[i], m4 = m[i], v4 = v[i];
     float po[4], mo[4], vo[4];
@@ -1647,8 +1651,14 @@ int mzba_adam(float* p, const float* grad, float* m, float* v, long long n, floa
               float one_m_b2, float bc2_sqrt, float eps, float weight_decay, hipStream_t stream) {
   MZ_CHECK_ARG(p && grad && m && v && n >= 0, -1);
   if (n == 0) return 0;
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, stream, p, grad, m, v, (size_t)n, neg_step,
-                     one_m_b1, b2, one_m_b2, bc2_sqrt, eps, weight_decay);
+  const bool a16 = (((uintptr_t)p | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
+  if (n % 4 == 0 && a16)
+    hipLaunchKernelGGL(adam4_kernel<false>, dim3(grid_for((size_t)n / 4)), dim3(256), 0, stream, (float4*)p,
+                       (const float4*)grad, (float4*)m, (float4*)v, (size_t)n / 4, nullptr, neg_step, one_m_b1, b2,
+                       one_m_b2, bc2_sqrt, eps, weight_decay);
+  else
+    hipLaunchKernelGGL(adam_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, stream, p, grad, m, v, (size_t)n, neg_step,
+                       one_m_b1, b2, one_m_b2, bc2_sqrt, eps, weight_decay);
   MZ_LAUNCH_CHECK();
   return 0;
 }
@@ -1659,8 +1669,9 @@ int mzba_adam_dev(float* p, const float* grad, float* m, float* v, long long n, 
   if (n == 0) return 0;
   const bool a16 = (((uintptr_t)p | (uintptr_t)grad | (uintptr_t)m | (uintptr_t)v) & 15) == 0;
   if (n % 4 == 0 && a16)
-    hipLaunchKernelGGL(adam_dev4_kernel, dim3(grid_for((size_t)n / 4)), dim3(256), 0, stream, (float4*)p,
-                       (const float4*)grad, (float4*)m, (float4*)v, (size_t)n / 4, scalars);
+    hipLaunchKernelGGL(adam4_kernel<true>, dim3(grid_for((size_t)n / 4)), dim3(256), 0, stream, (float4*)p,
+                       (const float4*)grad, (float4*)m, (float4*)v, (size_t)n / 4, scalars, 0.f, 0.f, 0.f, 0.f, 0.f,
+                       0.f, 0.f);
   else
     hipLaunchKernelGGL(adam_dev_kernel, dim3(grid_for((size_t)n)), dim3(256), 0, stream, p, grad, m, v, (size_t)n,
                        scalars);
