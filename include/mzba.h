@@ -529,6 +529,13 @@ int mzba_learner_loss(const float* logit_r, const float* logit_v, const float* l
                       const float* targets, const float* counts, const int32_t* slots, int B, int K, int ns, int na,
                       float smin, float smax, float* dlogit_r, float* dlogit_v, float* dlogit_p, float* loss,
                       hipStream_t stream);
+/* The same outputs, bit for bit, over many workgroups (a thread per (window, step) row, then one reduction
+ * workgroup folding the rows in mzba_learner_loss's order): ws >= mzba_learner_loss_ws_bytes(B, K) bytes. */
+long long mzba_learner_loss_ws_bytes(int B, int K);
+int mzba_learner_loss_ws(const float* logit_r, const float* logit_v, const float* logit_p, const float* rewards,
+                         const float* targets, const float* counts, const int32_t* slots, int B, int K, int ns, int na,
+                         float smin, float smax, float* dlogit_r, float* dlogit_v, float* dlogit_p, float* loss,
+                         void* ws, long long ws_bytes, hipStream_t stream);
 /* Adam with L2 weight decay, torch single-tensor order: g = grad + wd*p; m += (1-b1)(g - m);
  * v = v*b2 + (1-b2)*g*g; p += (-step_size*m) / (sqrt(v)/bc2_sqrt + eps). Host computes
  * neg_step = -lr/(1-b1^t), bc2_sqrt = sqrt(1-b2^t) in double (python float semantics). */

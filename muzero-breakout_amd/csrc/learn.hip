@@ -1169,6 +1169,70 @@ __global__ __launch_bounds__(LOSS_T) void loss_kernel(const float* __restrict__ 
   }
 }
 
+// loss_kernel over many workgroups (round 5: the one-workgroup form took 159 us of the minibatch's critical path):
+// a thread per row r computes its three KL terms (gradients written as loss_kernel) and stores them to
+// ws[j][r]; loss_reduce_kernel then folds them exactly as loss_kernel's threads did — thread t adds rows t,
+// t + LOSS_T, ... in order into its double accumulators, then the same tree — so the loss is bit-identical
+__global__ __launch_bounds__(256) void loss_rows_kernel(const float* __restrict__ lr, const float* __restrict__ lv,
+                                                        const float* __restrict__ lp, const float* __restrict__ rewards,
+                                                        const float* __restrict__ targets,
+                                                        const float* __restrict__ counts, const int32_t* slots, int B,
+                                                        int K, int ns, int na, float smin, float smax,
+                                                        float* __restrict__ dlr, float* __restrict__ dlv,
+                                                        float* __restrict__ dlp, double* __restrict__ ws) {
+  const float scale = (1.f / (float)K) / (float)(B * K);
+  const int r = blockIdx.x * blockDim.x + threadIdx.x, BK = B * K;
+  if (r >= BK) return;
+  const int b = r / K, k = r - b * K;
+  const size_t src = slots ? (size_t)slots[b] : (size_t)b;
+  float t[16], z[16], dz[16];
+  const size_t o1 = ((size_t)k * B + b) * ns, o3 = ((size_t)k * B + b) * na;
+  two_hot(rewards[src * K + k], smin, smax, ns, t);
+  for (int i = 0; i < ns; ++i) z[i] = lr[o1 + i];
+  ws[r] = kl_row(z, t, ns, scale, dz);
+  for (int i = 0; i < ns; ++i) dlr[o1 + i] = dz[i];
+  two_hot(targets[src * K + k], smin, smax, ns, t);
+  for (int i = 0; i < ns; ++i) z[i] = lv[o1 + i];
+  ws[BK + r] = kl_row(z, t, ns, scale, dz);
+  for (int i = 0; i < ns; ++i) dlv[o1 + i] = dz[i];
+  float cs = 0.f;
+  for (int i = 0; i < na; ++i) cs += counts[(src * K + k) * na + i];
+  for (int i = 0; i < na; ++i) { t[i] = counts[(src * K + k) * na + i] / cs; z[i] = lp[o3 + i]; }
+  ws[2 * BK + r] = kl_row(z, t, na, scale, dz);
+  for (int i = 0; i < na; ++i) dlp[o3 + i] = dz[i];
+}
+
+__global__ __launch_bounds__(LOSS_T) void loss_reduce_kernel(const double* __restrict__ ws, int B, int K,
+                                                             float* __restrict__ loss) {
+  __shared__ double red[3][LOSS_T];
+  const int BK = B * K;
+  for (int j = 0; j < 3; ++j) {
+    double acc = 0.0;
+    int r = threadIdx.x;
+    for (; r + 3 * LOSS_T < BK; r += 4 * LOSS_T) {  // four rows' loads ahead of their adds, added in row order
+      const double v0 = ws[j * BK + r], v1 = ws[j * BK + r + LOSS_T], v2 = ws[j * BK + r + 2 * LOSS_T],
+                   v3 = ws[j * BK + r + 3 * LOSS_T];
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; r < BK; r += LOSS_T) acc += ws[j * BK + r];
+    red[j][threadIdx.x] = acc;
+  }
+  __syncthreads();
+  for (int s = LOSS_T / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s)
+      for (int j = 0; j < 3; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float rl = (float)(red[0][0] / (B * K)), vl = (float)(red[1][0] / (B * K)), pl = (float)(red[2][0] / (B * K));
+    loss[0] = (1.f / (float)K) * ((rl + vl) + pl);
+    loss[1] = rl; loss[2] = vl; loss[3] = pl;
+  }
+}
+
 // ------------------------------------------------------------------ Adam (networks.py:268)
 // g = grad + wd*p; m += (1-b1)(g - m); v = v*b2 + (1-b2)*g*g; p += (-step_size*m) / (sqrt(v)/bc2s + eps)
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ grad, float* __restrict__ m,
@@ -1643,6 +1707,24 @@ int mzba_learner_loss(const float* logit_r, const float* logit_v, const float* l
                -1);
   hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(LOSS_T), 0, stream, logit_r, logit_v, logit_p, rewards, targets, counts,
                      slots, B, K, ns, na, smin, smax, dlogit_r, dlogit_v, dlogit_p, loss);
+  MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+long long mzba_learner_loss_ws_bytes(int B, int K) { return 3LL * B * K * (long long)sizeof(double); }
+
+int mzba_learner_loss_ws(const float* logit_r, const float* logit_v, const float* logit_p, const float* rewards,
+                         const float* targets, const float* counts, const int32_t* slots, int B, int K, int ns, int na,
+                         float smin, float smax, float* dlogit_r, float* dlogit_v, float* dlogit_p, float* loss,
+                         void* ws, long long ws_bytes, hipStream_t stream) {
+  MZ_CHECK_ARG(logit_r && logit_v && logit_p && rewards && targets && counts && dlogit_r && dlogit_v && dlogit_p &&
+                   loss && ws && B > 0 && K > 0 && ns >= 2 && ns <= 16 && na > 0 && na <= 16,
+               -1);
+  MZ_CHECK_ARG(mzba_learner_loss_ws_bytes(B, K) <= ws_bytes && (long long)B * K < (1LL << 28), -2);
+  const int BK = B * K;
+  hipLaunchKernelGGL(loss_rows_kernel, dim3((BK + 255) / 256), dim3(256), 0, stream, logit_r, logit_v, logit_p, rewards,
+                     targets, counts, slots, B, K, ns, na, smin, smax, dlogit_r, dlogit_v, dlogit_p, (double*)ws);
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(LOSS_T), 0, stream, (const double*)ws, B, K, loss);
   MZ_LAUNCH_CHECK();
   return 0;
 }

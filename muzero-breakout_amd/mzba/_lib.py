@@ -106,6 +106,8 @@ SIGNATURES = {
     "mzba_linear_ws_bytes": [I, I, I],
     "mzba_linear_backward": [I, P, P, P, P, I, P, P, I, I, I, P, LL, P],
     "mzba_learner_loss": [P, P, P, P, P, P, P, I, I, I, I, F, F, P, P, P, P, P],
+    "mzba_learner_loss_ws_bytes": [I, I],
+    "mzba_learner_loss_ws": [P, P, P, P, P, P, P, I, I, I, I, F, F, P, P, P, P, P, LL, P],
     "mzba_adam": [P, P, P, P, LL, F, F, F, F, F, F, F, P],
     "mzba_adam_dev": [P, P, P, P, LL, P, P],
     "mzba_learner_input": [I, P, P, P, P, P, I, I, I, I, P],
@@ -135,7 +137,7 @@ class TowerExt(ctypes.Structure):
 
 # entry points that return something other than a status code
 RESTYPES = {"mzba_tower_ws_bytes": LL, "mzba_tower_plan": I, "mzba_conv_lat_get_variant": I, "mzba_conv_wgrad_ws_bytes": LL,
-            "mzba_linear_ws_bytes": LL}
+            "mzba_linear_ws_bytes": LL, "mzba_learner_loss_ws_bytes": LL}
 
 
 def lib():

@@ -782,9 +782,10 @@ class Learner:
         # ---- loss_fn
         dlr, dlv, dlp = torch.empty_like(lr_all), torch.empty_like(lv_all), torch.empty_like(lp_all)
         loss = torch.empty(4, device=self.device)
-        L.call("mzba_learner_loss", L.ptr(lr_all), L.ptr(lv_all), L.ptr(lp_all), L.ptr(g["rewards"]),
+        lws = self._scratch("loss", L.lib().mzba_learner_loss_ws_bytes(B, K))
+        L.call("mzba_learner_loss_ws", L.ptr(lr_all), L.ptr(lv_all), L.ptr(lp_all), L.ptr(g["rewards"]),
                L.ptr(g["targets"]), L.ptr(g["counts"]), L.ptr(slots), B, K, self.ns, self.na, self.smin, self.smax,
-               L.ptr(dlr), L.ptr(dlv), L.ptr(dlp), L.ptr(loss), s)
+               L.ptr(dlr), L.ptr(dlv), L.ptr(dlp), L.ptr(loss), L.ptr(lws), lws.numel(), s)
         self.last_logits = (lr_all, lv_all, lp_all)
         # ---- backward
         # prediction k: heads -> res blocks -> d h_k (prediction part); independent of the dynamics
