@@ -605,3 +605,41 @@ def test_learner_fused_bn_statistics_track_separate_passes():
             cs = torch.nn.functional.cosine_similarity(a, b, dim=0).item()
             print(f"seed {seed}: {k} fused~sep cosine {cs:.5f}")
             assert cs >= 0.95, (seed, k, cs)
+
+
+@pytest.mark.parametrize("B,K,ns,na,with_slots", [(512, 5, 11, 3, True), (37, 3, 16, 4, False), (1, 1, 2, 1, True)])
+def test_loss_ws_equals_one_workgroup_loss(B, K, ns, na, with_slots):
+    """mzba_learner_loss_ws (a thread per (window, step) row, then one workgroup folding the rows in the one-workgroup
+    kernel's order) gives mzba_learner_loss's loss and logit gradients bit for bit, at the learner's shape and at
+    ragged row counts (B K not a multiple of 256, one row)."""
+    from mzba import _lib as L
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(B * 7 + K)
+    cap = B + 5
+    lr = torch.randn(K, B, ns, generator=g, device=dev) * 3
+    lv = torch.randn(K, B, ns, generator=g, device=dev) * 3
+    lp = torch.randn(K, B, na, generator=g, device=dev)
+    rewards = torch.randint(-1, 2, (cap, K), generator=g, device=dev).float()
+    targets = torch.randn(cap, K, generator=g, device=dev) * 4
+    counts = torch.randint(0, 51, (cap, K, na), generator=g, device=dev).float() + 1
+    slots = torch.randperm(cap, generator=g, device=dev)[:B].to(torch.int32) if with_slots else None
+    outs = []
+    for use_ws in (False, True):
+        d = [torch.full_like(t, float("nan")) for t in (lr, lv, lp)]
+        loss = torch.full((4,), float("nan"), device=dev)
+        args = [L.ptr(lr), L.ptr(lv), L.ptr(lp), L.ptr(rewards), L.ptr(targets), L.ptr(counts), L.ptr(slots), B, K, ns, na,
+                -5.0, 5.0, L.ptr(d[0]), L.ptr(d[1]), L.ptr(d[2]), L.ptr(loss)]
+        if use_ws:
+            ws = torch.empty(int(L.lib().mzba_learner_loss_ws_bytes(B, K)), dtype=torch.uint8, device=dev)
+            L.call("mzba_learner_loss_ws", *args, L.ptr(ws), ws.numel(), L.stream())
+        else:
+            L.call("mzba_learner_loss", *args, L.stream())
+        outs.append([loss] + d)
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0][0]).all()
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    ws = torch.empty(8, dtype=torch.uint8, device=dev)
+    assert L.lib().mzba_learner_loss_ws(L.ptr(lr), L.ptr(lv), L.ptr(lp), L.ptr(rewards), L.ptr(targets), L.ptr(counts),
+                                        None, B, K, ns, na, ctypes.c_float(-5.0), ctypes.c_float(5.0), L.ptr(lr),
+                                        L.ptr(lv), L.ptr(lp), L.ptr(lr), L.ptr(ws), 8, L.stream()) == -2
