@@ -9,7 +9,8 @@ representation -> 50 x (select, dynamics, prediction, backup) -> sampling -> env
 (RCCL gather to rank 0 for N>1) into rank 0's pinned host buffer (the replay-buffer sink).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...)
+       N>1 either under python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ... (WORLD_SIZE must
+       equal N), or plain `python bench.py --gpus N`, which starts that torchrun as a child process itself.
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -50,7 +51,7 @@ def parse():
     ap.add_argument("--learner-streams", type=int, default=2, choices=[1, 2],
                     help="learner: 2 = prediction nets on a side stream beside the dynamics chain")
     ap.add_argument("--tower-variant", type=int, default=0, help="tower kernel (mzba_tower_set_variant; 0 = by batch)")
-    ap.add_argument("--workload", default="acting", choices=["acting", "env", "learner"],
+    ap.add_argument("--workload", default="acting", choices=["acting", "env", "learner", "selfcheck"],
                     help="acting: the whole acting loop (headline); env: env step + render + frame stack only "
                          "(configs 1/3, HBM roofline)")
     ap.add_argument("--height", type=int, default=None, help="env workload frame height (default 84)")
@@ -153,7 +154,7 @@ def run_env(args, world, rank, local):
     if rank == 0:
         line = {
             "metric": "env-steps/sec, env step + render + frame stack only (SURVEY configs 1/3)",
-            "value": world * B * args.steps / dt, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "value": world * B * args.steps / dt, "unit": "env-steps/s", "n_gpus": world, **dist_info(), "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: seeded resets, uniform random actions",
@@ -256,7 +257,7 @@ def run_learner(args, world, rank, local):
         line = {
             "metric": "learner windows/sec (RLSystem._training_stage minibatch: K=5 rollout, train-mode BN, "
                       "backward, Adam)",
-            "value": world * B * args.steps / dtt, "unit": "windows/s", "n_gpus": world, "steps": args.steps,
+            "value": world * B * args.steps / dtt, "unit": "windows/s", "n_gpus": world, **dist_info(), "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": dtt / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": dt,
             "data": "synthetic replay ring (4096 windows), seeded random-init reference-architecture nets",
@@ -543,11 +544,59 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
     return out
 
 
+def launcher_argv(n, argv, port):
+    """The child command `bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment) starts: one rank per GPU
+    under torch.distributed.run on this node, rendezvous on 127.0.0.1, the same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def world_from_env(gpus, env):
+    """(world, rank, local) from the torchrun environment; refuses a world size that differs from --gpus, so a
+    line can never report N GPUs while running another number of ranks."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" in env and world != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={world}: the launcher and the flag disagree")
+    return world, int(env.get("RANK", "0")), int(env.get("LOCAL_RANK", "0"))
+
+
+def dist_info():
+    """What the collectives actually ran on: the ranks the process group holds and its backend ("nccl" is RCCL on
+    ROCm; "gloo" only in the one-GPU rehearsal, MZBA_DIST_REHEARSAL=1)."""
+    if dist.is_available() and dist.is_initialized():
+        return {"ranks_seen": dist.get_world_size(), "backend": str(dist.get_backend()),
+                "rehearsal": os.environ.get("MZBA_DIST_REHEARSAL") == "1"}
+    return {"ranks_seen": 1, "backend": None, "rehearsal": False}
+
+
+def self_launch(n):
+    """`python bench.py --gpus N` without a torchrun environment: start the N ranks as a child process (before any
+    GPU call in this process — no exec), let rank 0's JSON line through, exit with the child's return code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launcher_argv(n, sys.argv[1:], port), env=env)
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus))
+    world, rank, local = world_from_env(args.gpus, os.environ)
+    if args.workload == "selfcheck":  # the launcher and process group alone (gloo, no GPU call): CPU tests
+        if world > 1:
+            dist.init_process_group("gloo")
+        if rank == 0:
+            print(json.dumps({"workload": "selfcheck", "n_gpus": world, **dist_info()}))
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if world > 1:
         # production: one rank per GPU over RCCL. Rehearsal on a one-GPU box (MZBA_DIST_REHEARSAL=1):
         # every rank on cuda:0, gloo collectives — the same code path minus RCCL itself
@@ -717,6 +766,7 @@ def main():
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
+            **dist_info(),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,

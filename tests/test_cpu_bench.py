@@ -90,3 +90,34 @@ def test_learner_kernel_breakdown_record():
     assert shares == sorted(shares, reverse=True) and sum(shares) <= 1.0
     assert bench.learner_kernels(512, "f32") is None and bench.learner_kernels(256, "bf16") is None
     bench.check_fracs({"roofline": {"top_kernels": rec}})
+
+
+def test_self_launcher_argv_runs_n_ranks_of_this_bench():
+    argv = bench.launcher_argv(8, ["--gpus", "8", "--steps", "5"], 29511)
+    assert argv[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in argv and "--nnodes=1" in argv and "--master-addr=127.0.0.1" in argv
+    assert "--master-port=29511" in argv
+    i = argv.index(os.path.abspath(bench.__file__))
+    assert argv[i + 1:] == ["--gpus", "8", "--steps", "5"]
+
+
+def test_world_size_mismatch_is_refused():
+    assert bench.world_from_env(1, {}) == (1, 0, 0)
+    assert bench.world_from_env(4, {"WORLD_SIZE": "4", "RANK": "2", "LOCAL_RANK": "2"}) == (4, 2, 2)
+    for gpus, ws in ((8, "4"), (1, "2"), (2, "1")):
+        with pytest.raises(SystemExit):
+            bench.world_from_env(gpus, {"WORLD_SIZE": ws, "RANK": "0", "LOCAL_RANK": "0"})
+
+
+def test_self_launched_ranks_report_ranks_seen(tmp_path):
+    """`bench.py --gpus 2` with no torchrun environment starts two ranks itself; a gloo rehearsal of the launcher
+    path (the bench's --workload selfcheck: process group only, no GPU) prints ranks_seen 2 from rank 0 only."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MZBA_DIST_REHEARSAL"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "selfcheck"],
+                       capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2 and lines[0]["backend"] == "gloo"
