@@ -670,12 +670,13 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
 
   for (int b = 0; b < NCS; b += 2) {
     block(b, std::integral_constant<int, 0>());  // SPB b even
-    // block b + 1's raw rows: wait for this wave's LDS-DMA (older than every ring load of block b: all but the
-    // youngest 2 steps of ring loads, 2 x 9 or 2 x 3, may be waited on), then every wave's, then split
+    // block b + 1's raw rows: wait for this wave's LDS-DMA, then every wave's, then split. The DMA is older than
+    // every ring load block b issued after it: 3 reloads of 9 (3x3; waiting down to the youngest 18 is enough) or
+    // one reload of 3 (1x1: the youngest 3 only — 6 would leave the last DMA pieces in flight)
     if (KSZ == 3)
       asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
     else
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     __syncthreads();
     split();
     __syncthreads();
@@ -685,7 +686,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
       if (KSZ == 3)
         asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
       else
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
       __syncthreads();
       split();
       __syncthreads();
@@ -806,6 +807,7 @@ int mzba_conv_x6_supported(int H, int W, int Cin, int Cout, int ks) {
 // gather = 1: a slot-gathered / strided input and / or an action-bias table (conv_x6t's GA instance: the 4x5
 // latent, Cin 256, Cout 256 / 128)
 int mzba_conv_x6_ex_supported(int H, int W, int Cin, int Cout, int ks, int gather) {
+  if (ks == 1 && gather) return 0;  // the 1x1 instance reads contiguous images only (no slot, no action bias)
   if ((ks == 3 || ks == 1) && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128)) return 1;
   return gather ? 0 : mzba_conv_x6_supported(H, W, Cin, Cout, ks);
 }

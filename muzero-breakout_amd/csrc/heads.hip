@@ -267,6 +267,8 @@ int mzba_heads_bf16(int nheads, const void* x0, const void* w0, const float* b0,
 }
 
 
+static inline bool a16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 // x*: [B][K] activations (dtype 0 f32 / 1 bf16); w*: [O][K] f32; decode 0 softmax, 1 support
 int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const float* b0, int K0, int O0, int dec0,
                float* logits0, float* out0, const void* x1, const float* w1, const float* b1, int K1, int O1,
@@ -279,7 +281,8 @@ int mzba_heads(int dtype, int nheads, const void* x0, const float* w0, const flo
   const dim3 grid((unsigned)((B + EPB - 1) / EPB));
   if (dtype)
     hipLaunchKernelGGL((heads_kernel<bf16_t, EPB>), grid, dim3(256), 0, stream, a, B);
-  else if (g_heads_mfma && K0 % 16 == 0 && (nheads == 1 || K1 % 16 == 0))
+  else if (g_heads_mfma && K0 % 16 == 0 && (nheads == 1 || K1 % 16 == 0) && a16(x0) && a16(w0) &&
+           (nheads == 1 || (a16(x1) && a16(w1))))  // its float4 loads: 16-B aligned bases (else the scalar form)
     hipLaunchKernelGGL(heads_mfma_f32_kernel, dim3((B + 15) / 16), dim3(512), 0, stream, a, B);
   else
     hipLaunchKernelGGL((heads_kernel<float, EPB>), grid, dim3(256), 0, stream, a, B);

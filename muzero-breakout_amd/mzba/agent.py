@@ -576,16 +576,32 @@ class LearnerOptimizer:
     f32 master weights, gradients and moments (mzba_adam: torch's single-tensor order). The state_dict is
     torch.optim.Adam's (params in MuZeroAgent.parameters() order), so the reference's checkpoints round-trip."""
 
+    FIXED = {"betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 1e-4}  # what mzba_adam computes with
+
     def __init__(self, agent):
         self.agent = agent
         self._pending = None  # an optimizer state loaded before the first train_mode()
+        self._groups = None
 
     @property
     def param_groups(self):
+        """One persistent group, as torch.optim.Adam's: writing g["lr"] (a scheduler, a manual decay) takes effect
+        at the next step(); the other hyperparameters are the kernel's constants and a change to them raises there."""
         ln = self.agent._learner
-        lr = ln.lr if ln is not None else float(self.agent.cfg["learning_rate"])
-        return [{"params": list(self.agent.parameters()), "lr": lr, "betas": (0.9, 0.999), "eps": 1e-8,
-                 "weight_decay": 1e-4}]
+        if self._groups is None:
+            lr = ln.lr if ln is not None else float(self.agent.cfg["learning_rate"])
+            self._groups = [{"params": list(self.agent.parameters()), "lr": lr, **self.FIXED}]
+        return self._groups
+
+    def _sync_groups(self, ln):
+        if self._groups is None:
+            return
+        g = self._groups[0]
+        for k, v in self.FIXED.items():
+            cur = tuple(g[k]) if isinstance(v, tuple) else g[k]
+            if cur != v:
+                raise NotImplementedError(f"param_groups[0][{k!r}] = {g[k]!r}: the device Adam runs with {v!r} only")
+        ln.lr = float(g["lr"])
 
     def zero_grad(self, set_to_none=True):
         ln = self.agent._learner
@@ -597,6 +613,7 @@ class LearnerOptimizer:
         ln = self.agent._learner
         if ln is None:
             raise RuntimeError("optimizer.step() before train_mode(): no gradients")
+        self._sync_groups(ln)
         ln.adam_step()
         ln.begin_calls()
         self.agent._host_stale = True
@@ -617,6 +634,8 @@ class LearnerOptimizer:
             ln.load_optimizer_state_dict(d)
         else:
             self._pending = d
+        if self._groups is not None:  # the loaded lr replaces the group's
+            self._groups[0]["lr"] = float(d["param_groups"][0]["lr"])
 
 
 class MuZeroAgent:

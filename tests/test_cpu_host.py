@@ -231,3 +231,31 @@ def test_conv_halo_support_matrix_and_bad_arguments_without_gpu():
     assert L.mzba_conv_halo_supported(8, 184, 128, 128, 3) == 0
     assert L.mzba_conv_halo_supported(8, 183, 256, 256, 3) == 1
     assert L.mzba_conv_halo_supported(8, 184, 256, 256, 3) == 0
+
+
+def test_learner_optimizer_param_groups_persist_and_lr_writes_reach_the_learner():
+    """`for g in opt.param_groups: g["lr"] = x` must act like torch.optim.Adam's — one persistent group
+    whose lr the next step() uses; the kernel's fixed hyperparameters refuse a change instead of ignoring it."""
+    from mzba.agent import LearnerOptimizer
+
+    class Ln:
+        lr = 1e-3
+
+    class Ag:
+        _learner = Ln()
+        cfg = {"learning_rate": 1e-3}
+
+        def parameters(self):
+            return iter([np.zeros(1)])
+
+    opt = LearnerOptimizer(Ag())
+    assert opt.param_groups is opt.param_groups
+    for g in opt.param_groups:
+        g["lr"] = 2.5e-4
+    opt._sync_groups(Ag._learner)
+    assert Ag._learner.lr == 2.5e-4
+    opt.param_groups[0]["betas"] = [0.9, 0.999]  # a list equal to the constant is fine
+    opt._sync_groups(Ag._learner)
+    opt.param_groups[0]["weight_decay"] = 0.0
+    with pytest.raises(NotImplementedError):
+        opt._sync_groups(Ag._learner)
