@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--width", type=int, default=None, help="env workload frame width (default 84)")
     ap.add_argument("--hist", type=int, default=4, help="env workload frame-stack length")
     ap.add_argument("--minibatch", type=int, default=512, help="learner workload minibatch (config.yaml:7)")
+    ap.add_argument("--parity-envs", type=int, default=512,
+                    help="config 3 geometry: envs of the f32 parity-path replay (the first ones of the batch)")
     ap.add_argument("--no-halo", action="store_true",
                     help="A/B: large-image 3x3 convs on conv_big_bf16_kernel instead of the halo-tiled conv_halo_kernel")
     ap.add_argument("--pow-threads", type=int, default=1,
@@ -450,8 +452,8 @@ def conv_flops(B, hw, C):
 PEAK_F32_TFLOPS = 157.3  # MI355X dense f32 MFMA (MI355X_MICROARCH.md chip table)
 
 
-def want_parity(args, rank, world, custom_geom):
-    return rank == 0 and world == 1 and not args.no_parity and not custom_geom and args.dtype != "f32"
+def want_parity(args, rank, world):
+    return rank == 0 and world == 1 and not args.no_parity and args.dtype != "f32"
 
 
 LOOP_STATE = ("paddle", "bx", "by", "dx", "dy", "done", "bricks", "cur_frame", "cur_src", "hist_frames", "hist_actions",
@@ -468,27 +470,36 @@ def snapshot_loop(loop):
     return snap
 
 
-def restore_loop(loop, snap):
+def restore_loop(loop, snap, B=None):
+    """Restore a snapshot into `loop`; with B (the snapshot's batch) larger than the loop's, its first envs only (every
+    env tensor is env-major, so a prefix of B_loop / B of it is the first envs' state)."""
     for k in LOOP_STATE:
         if k in snap:
-            getattr(loop.env, k).copy_(snap[k])
+            dst, src = getattr(loop.env, k), snap[k]
+            if B is not None and src.shape[0] != dst.shape[0]:
+                src = src.reshape(B, -1)[: loop.B].reshape(dst.shape)
+            dst.copy_(src)
     loop.ctx.copy_(snap["ctx"])
     loop.search_id, loop.step_index, loop.t = snap["ids"]
 
 
-def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
+def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W, nsub=None):
     """The first timed step replayed on the f32 parity path (networks within 1e-5 of the reference,
     bit-exact trees): the same env state, search id and keyed randomness as the benchmarked step. The parity
     path's latent convs run as f32-faithful split-bf16 products (conv_x6: six bf16 MFMAs per f32 product,
     each conv as close to exact as an f32 one); the same step is also replayed with those convs on the
     f32-input MFMA (conv_igemm, the parity path of rounds 1-3). Returns the fraction of all B envs whose visit
     counts equal the benchmarked step's, the agreement of the two parity paths, and their throughputs (second
-    replays, HIP events) against the dense f32 MFMA peak."""
+    replays, HIP events) against the dense f32 MFMA peak.
+    nsub < B (config 3's 84x84 geometry, whose f32 node pool at 4096 envs would not fit beside the benchmarked
+    loop's): the first nsub envs only, restored from the snapshot's env-major prefix; the same global env ids, so the
+    same keyed noise and tie-breaks; conv_x6 only (no f32-MFMA A/B)."""
     from mzba.agent import MuZeroAgent
     from mzba.acting import ActingLoop
+    nsub = nsub or B
     ag32 = MuZeroAgent(mcfg, dtype="f32", device=loop.agent.device)
     ag32.load_state_dict(sd)
-    l32 = ActingLoop(cfg, ag32, B, seed=args.seed, env_offset=loop.env_offset, height=H, width=W,
+    l32 = ActingLoop(cfg, ag32, nsub, seed=args.seed, env_offset=loop.env_offset, height=H, width=W,
                      n_envs_total=loop.n_envs_total, pow_threads=loop.pow_threads)
     l32.temperature = loop.temperature
     l32.search.noise_weight = loop.search.noise_weight
@@ -496,12 +507,12 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
     fl = step_flops(ag32.packed, H, W, args.sims)
     p32 = ag32.packed
     runs = {}
-    for x6 in (True, False):
+    for x6 in ((True, False) if nsub == B else (True,)):
         for rn in (l32.ws.runner, l32.rep_runner):
             rn.use_x6 = x6
         counts, ms = [], []
         for _ in range(2):  # the first replay also warms the path (scratch, code objects)
-            restore_loop(l32, snap)
+            restore_loop(l32, snap, B)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             l32.act(eager=True)
@@ -511,16 +522,24 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
             counts.append(l32.rec["counts"][t0].cpu().numpy())
         runs[x6] = (counts, ms, l32.rec["values"][t0].cpu().numpy())
     counts, ms, v32 = runs[True]
-    c16 = loop.rec["counts"][t0].cpu().numpy()
+    c16 = loop.rec["counts"][t0].cpu().numpy()[:nsub]
     same = (counts[-1] == c16).all(1)
     l1 = np.abs(counts[-1].astype(np.int64) - c16.astype(np.int64)).sum(1)
-    v16 = loop.rec["values"][t0].cpu().numpy()
-    eps = B / (ms[-1] * 1e-3)
-    cf, msf, vf = runs[False]
-    same_f = (cf[-1] == counts[-1]).all(1)
-    eps_f = B / (msf[-1] * 1e-3)
-    rl = parity_roofline(p32, H, W, args.sims, ms[-1], B)
-    out = {"match": float(same.mean()),
+    v16 = loop.rec["values"][t0].cpu().numpy()[:nsub]
+    eps = nsub / (ms[-1] * 1e-3)
+    rl = parity_roofline(p32, H, W, args.sims, ms[-1], nsub)
+    vs_mfma = None
+    if False in runs:
+        cf, msf, vf = runs[False]
+        same_f = (cf[-1] == counts[-1]).all(1)
+        eps_f = nsub / (msf[-1] * 1e-3)
+        vs_mfma = {"value": eps_f, "ms_per_step": msf[-1], "speedup": eps / eps_f,
+                   "frac": eps_f * fl / 1e12 / PEAK_F32_TFLOPS,
+                   "visit_count_match": float(same_f.mean()),
+                   "value_max_abs_diff": float(np.abs(vf - v32).max()),
+                   "deterministic": bool((cf[0] == cf[1]).all())}
+    out = {"match": float(same.mean()), "envs": nsub,
+           "root_value_max_abs_diff": float(np.abs(v16 - v32).max()),
            # beside the exact-match fraction: how far the count rows are apart, and whether the most visited
            # action (what temperature sampling mostly picks at low T) agrees
            "l1_mean": float(l1.mean()), "l1_max": int(l1.max()),
@@ -531,11 +550,8 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W):
                     "peak": rl["peak"], "frac": rl["frac"], "roofline": rl,
                     "deterministic": bool((counts[0] == counts[1]).all()),
                     "value_max_abs_diff_where_counts_agree": float(np.abs(v16 - v32)[same].max()) if same.any() else None,
-                    "vs_f32_mfma_path": {"value": eps_f, "ms_per_step": msf[-1], "speedup": eps / eps_f,
-                                         "frac": eps_f * fl / 1e12 / PEAK_F32_TFLOPS,
-                                         "visit_count_match": float(same_f.mean()),
-                                         "value_max_abs_diff": float(np.abs(vf - v32).max()),
-                                         "deterministic": bool((cf[0] == cf[1]).all())},
+                    "envs": nsub,
+                    "vs_f32_mfma_path": vs_mfma,
                     "what": "one acting step of the same envs on the f32 parity path (separate launches per layer, "
                             "the latent 3x3 convs on conv_x6), eager, HIP events around the step; vs_f32_mfma_path: "
                             "the same with those convs on the f32-input MFMA"}}
@@ -711,7 +727,7 @@ def main():
                               f"bench's own state, 1 acting step ({cpu_s:.1f} s)"}
 
     # the state before the first timed step: the f32 parity path replays that step afterwards
-    snap = snapshot_loop(loop) if want_parity(args, rank, world, custom_geom) else None
+    snap = snapshot_loop(loop) if want_parity(args, rank, world) else None
     t_snap = loop.t
 
     # ---- timed region ---------------------------------------------------------------------
@@ -744,7 +760,8 @@ def main():
     tower_launch_ms = (float(np.mean([ms for ms, n in probe if n > 1])) if any(n > 1 for _, n in probe) else None)
     parity = None
     if snap is not None:  # after the timed region: nothing here is timed in `value`
-        parity = f32_parity_path(cfg, mcfg, sd, loop, snap, t_snap, args, B, H, W)
+        parity = f32_parity_path(cfg, mcfg, sd, loop, snap, t_snap, args, B, H, W,
+                                 nsub=min(B, args.parity_envs) if custom_geom else None)
     p = agent.packed
     fl = conv_flops(B, p.lh * p.lw, p.c1)
     achieved = fl / (conv_ms * 1e-3) / 1e12 if conv_ms else None
@@ -826,8 +843,10 @@ def main():
             "visit_count_l1_full": parity and {"mean": parity["l1_mean"], "max": parity["l1_max"], "sims": args.sims},
             "top_action_agreement_full": parity and parity["top_action_agreement"],
             "visit_count_match_full_sample": parity and (
-                f"all {B} envs of the first timed step: {args.dtype} HIP path vs the f32 HIP parity path from the "
+                (f"all {B} envs" if parity["envs"] == B else f"the first {parity['envs']} of the {B} envs") +
+                f" of the first timed step: {args.dtype} HIP path vs the f32 HIP parity path from the "
                 "same env state, search id and keyed noise / tie-breaks"),
+            "root_value_max_abs_diff_full": parity and parity["root_value_max_abs_diff"],
             "parity_path": parity and parity["path"],
             "launch": "eager" if args.no_graph else "hip-graph replay (probe step eager)",
             "whole_step_mfma_frac": (B * world * step_flops(agent.packed, H, W, args.sims) * args.steps / dt / 1e12)

@@ -70,6 +70,91 @@ def test_config3_env_84x84_at_4096_envs_matches_oracle():
     np.testing.assert_array_equal(got, want)
 
 
+def _config3_cfg():
+    """Config 3's acting geometry with the full-width nets (config.yaml): 84x84 frames, a 4-frame stack (8 input
+    planes) and the 21x21 latent the two avg-pools leave (parallel_breakout.py:76-77 with H / W overridden)."""
+    cfg = default_config()
+    cfg["num_simulations"] = 50
+    cfg["model"]["state_history_length"] = 4
+    cfg["model"]["latent_resolution"] = [21, 21]
+    return cfg
+
+
+def test_config3_full_width_f32_nets_84x84_match_oracle():
+    """The f32 parity path's full-width nets at config 3's geometry (B = 2) against the oracle's torch-CPU
+    evaluation of the reference networks (networks.py:38-241: the same conv2d / batch_norm / avg_pool2d ops)
+    within 1e-5: representation (+ min-max scale), prediction logits, dynamics state and reward logits."""
+    from mzba.agent import MuZeroAgent
+    from oracle.nets_torch import TorchNets
+    cfg = _config3_cfg()
+    mcfg = cfg["model"]
+    sd = init_state_dict(mcfg, 23)
+    ag = MuZeroAgent(mcfg, dtype="f32")
+    ag.load_state_dict(sd)
+    rng = np.random.default_rng(4)
+    x = (rng.integers(0, 4, (2, 8, 84, 84)) * 0.3).astype(np.float32)
+    o = TorchNets(sd, mcfg)
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        h_ref = o.representation(torch.from_numpy(x))
+        p_ref, v_ref = o.prediction(h_ref)
+        planes = N.encode_action_planes(np.array([0, 2]), mcfg["latent_resolution"])
+        h1_ref, r_ref = o.dynamics(h_ref, torch.from_numpy(planes))
+    tol = dict(rtol=1e-5, atol=1e-5)  # north_star: within 1e-5 for network logits/values
+    h = ag.create_hidden_state_root(torch.from_numpy(x).cuda())
+    assert tuple(h.shape) == (2, 256, 21, 21)
+    np.testing.assert_allclose(h.cpu().numpy(), h_ref.numpy(), **tol)
+    hd = h_ref.cuda()
+    pl, vl = ag.evaluate_state(hd)
+    np.testing.assert_allclose(pl.cpu().numpy(), p_ref.numpy(), **tol)
+    np.testing.assert_allclose(vl.cpu().numpy(), v_ref.numpy(), **tol)
+    h1, rl = ag.hidden_state_transition(hd, torch.from_numpy(planes).cuda())
+    np.testing.assert_allclose(h1.cpu().numpy(), h1_ref.numpy(), **tol)
+    np.testing.assert_allclose(rl.cpu().numpy(), r_ref.numpy(), **tol)
+
+
+def test_config3_full_width_bf16_acting_step_vs_f32_path():
+    """Config 3's benchmarked acting path under -m gpu: one acting step of 256 envs x 50 sims at 84x84 / 4-frame /
+    latent 21x21 with the full-width bf16 nets — every 3x3 conv with Cin >= 128 on the halo-tiled kernel
+    (conv_halo_kernel, incl. the dynamics' first conv off the latent pool with its action-bias table) — against
+    the same step on the f32 parity path (same env state, same keyed noise and tie-breaks).
+    Bound, as config 5's: bf16 rounding in the towers moves PUCT decisions that are close, so the counts are
+    compared by distance: every row sums to S, mean L1 <= 0.03 S, max <= 0.1 S, the most-visited action equal in
+    >= 85 % of envs, root values within 0.02."""
+    from mzba import _lib as L
+    from mzba.agent import MuZeroAgent
+    from mzba.acting import ActingLoop
+    cfg = _config3_cfg()
+    S, B = cfg["num_simulations"], 256
+    sd = init_state_dict(cfg["model"], 3)
+    assert L.lib().mzba_conv_halo_ex_supported(21, 21, 256, 256, 3, 1)
+    out = {}
+    for dt in ("bf16", "f32"):
+        ag = MuZeroAgent(cfg["model"], dtype=dt)
+        ag.load_state_dict(sd)
+        if dt == "bf16":  # the halo packing is there: the benchmarked kernel runs
+            assert all(c.get("wh") is not None for blk in ag.packed.dyn + ag.packed.pred for c in blk)
+            assert ag.packed.dyn0.get("wh") is not None
+        loop = ActingLoop(cfg, ag, B, seed=9, height=84, width=84)
+        assert loop.ws.runner.use_halo
+        loop.reset(0)
+        loop.act(eager=True)
+        loop.act(eager=True)  # the second step: a 2-frame history and a non-zero action in the stack
+        out[dt] = {k: v[1].cpu().numpy() for k, v in loop.rec.items() if v is not None}
+        del loop, ag
+        torch.cuda.empty_cache()
+    c16, c32 = out["bf16"]["counts"], out["f32"]["counts"]
+    assert (c16.sum(1) == S).all() and (c32.sum(1) == S).all()
+    l1 = np.abs(c16.astype(np.int64) - c32).sum(1)
+    top = (c16.argmax(1) == c32.argmax(1)).mean()
+    dv = np.abs(out["bf16"]["values"] - out["f32"]["values"])
+    print(f"config 3 bf16 vs f32 path at {B} x {S}, 84x84: exact {(l1 == 0).mean():.4f}, L1 mean {l1.mean():.2f} "
+          f"max {l1.max()}, top action {top:.4f}, |dv| max {dv.max():.2e}")
+    assert l1.mean() <= 0.03 * S and l1.max() <= 0.1 * S, (l1.mean(), l1.max())
+    assert top >= 0.85, top
+    assert dv.max() <= 0.02, dv.max()
+
+
 # ------------------------------------------------------------------------------ config 4
 def test_config4_bf16_fused_shards_equal_global_loop():
     """Config 4's partitioning on the benchmarked kernels: the bf16 fused path (tree step in the

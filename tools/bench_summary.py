@@ -11,8 +11,11 @@ if __name__ == "__main__":
         out.append(f"match_full {d['visit_count_match_full']}")
     pp = d.get("parity_path")
     if pp:
-        out.append(f"parity {pp['value']:.1f} (frac {pp['frac']:.3f}, f32mfma {pp['vs_f32_mfma_path']['value']:.1f}, "
-                   f"x6==f32mfma {pp['vs_f32_mfma_path']['visit_count_match']})")
+        vm = pp.get("vs_f32_mfma_path")
+        out.append(f"parity {pp['value']:.1f} on {pp.get('envs')} envs (frac {pp['frac']:.3f}" +
+                   (f", f32mfma {vm['value']:.1f}, x6==f32mfma {vm['visit_count_match']})" if vm else ")"))
+    if d.get("ranks_seen") is not None:
+        out.append(f"ranks_seen {d['ranks_seen']} ({d.get('backend')})")
     if d.get("cpu_baseline"):
         out.append(f"cpu {d['cpu_baseline']['value']:.2f}")
     print(" | ".join(out))

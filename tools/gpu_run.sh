@@ -16,6 +16,8 @@
 #                                                                              -> NAME.json, conv_counters.json
 #   rehearse:N:ENVS[:ARGS]    bench.py's N > 1 path: N ranks on cuda:0 over gloo (MZBA_DIST_REHEARSAL=1)
 #                                                                              -> rehearse_nN.json
+#   selflaunch:N:ENVS[:ARGS]  plain `bench.py --gpus N` (it starts its N ranks itself), ranks on cuda:0 over gloo
+#                                                                              -> selflaunch_nN.json
 #   py:NAME:SECONDS:CMD       any python tool (CMD = script + args)           -> NAME.log
 set -euo pipefail
 TAG=$1
@@ -109,6 +111,14 @@ for step in "$@"; do
         --master-addr 127.0.0.1 --master-port $((29500 + N)) bench.py --gpus $N --envs $envs ${args:-} \
         > $O/rehearse_n$N.json 2> $O/rehearse_n$N.err || { tail -30 $O/rehearse_n$N.err; exit 1; }
       python3 tools/bench_summary.py $O/rehearse_n$N.json ;;
+    selflaunch)
+      # plain `bench.py --gpus N` (no torchrun around it): bench.py starts its own N ranks (all on cuda:0, gloo)
+      N=$name
+      IFS=: read -r envs args <<< "$rest"
+      log "MZBA_DIST_REHEARSAL=1 python bench.py --gpus $N --envs $envs ${args:-} > $O/selflaunch_n$N.json"
+      MZBA_DIST_REHEARSAL=1 timeout -k 10 600 python bench.py --gpus $N --envs $envs ${args:-} \
+        > $O/selflaunch_n$N.json 2> $O/selflaunch_n$N.err || { tail -30 $O/selflaunch_n$N.err; exit 1; }
+      python3 tools/bench_summary.py $O/selflaunch_n$N.json ;;
     py)
       IFS=: read -r secs cmd <<< "$rest"
       log "python $cmd > $O/$name.log"
