@@ -413,10 +413,11 @@ def tower_kernel_name(B, fp16=False):
         L.lib().mzba_tower_plan(B), f"tower_kernel<{e}>")
 
 
-def x6_flops(p, H, W, S):
-    """Per env-step FLOPs of the f32 parity path's convs that run as split-bf16 x6 products (conv_x6: the
-    layers PackedNets gave x6 weights, 'wx' — the representation's Cout-256 3x3 convs, the latent towers'
-    residual convs) and of the rest (f32-input MFMA convs and heads), at this geometry."""
+def x6_flops(p, H, W, S, x3=False):
+    """Per env-step FLOPs of the f32 parity path's convs by the form they run in: split-fp16 x3 products (x3: the 4x5
+    latent's convs PackedNets gave 'wx3' — the towers, the dynamics' first conv, the heads' convs), split-bf16 x6
+    products (conv_x6: the layers with 'wx' and no x3 form in use — the representation's Cout-256 3x3 convs; all the
+    latent ones too without x3) and the rest (f32-input MFMA convs and heads), at this geometry: (x3, x6, rest)."""
     conv = lambda c, hw: 2.0 * hw * c["cout"] * c["ks"] ** 2 * c["cin"]  # noqa: E731
     x6, hh, ww = 0.0, H, W
     for kind, layer in p.rep:
@@ -427,21 +428,34 @@ def x6_flops(p, H, W, S):
             if c.get("wx") is not None:
                 x6 += conv(c, hh * ww)
     hw = p.lh * p.lw
-    tower = lambda blocks: sum(conv(c, hw) for blk in blocks for c in blk if c.get("wx") is not None)  # noqa: E731
-    x6 += tower(p.pred) + S * (tower(p.dyn) + tower(p.pred))
-    return x6, step_flops(p, H, W, S) - x6
+    lat = {"x3": 0.0, "x6": 0.0}
+
+    def add(c, n):
+        if x3 and c.get("wx3") is not None:
+            lat["x3"] += n * conv(c, hw)
+        elif c.get("wx") is not None:
+            lat["x6"] += n * conv(c, hw)
+    for c in [c for blk in p.pred for c in blk] + [p.pol_conv, p.val_conv]:
+        add(c, 1 + S)
+    for c in [c for blk in p.dyn for c in blk] + [p.dyn0, p.rew_conv]:
+        add(c, S)
+    x6 += lat["x6"]
+    return lat["x3"], x6, step_flops(p, H, W, S) - x6 - lat["x3"]
 
 
 X6_PEAK_TFLOPS = 2500.0 / 6  # six bf16 MFMAs per f32-faithful product
+X3_PEAK_TFLOPS = 2500.0 / 3  # three fp16 MFMAs per split-fp16 product (fp16 dense MFMA = the bf16 rate)
 
 
-def parity_roofline(p, H, W, S, ms_per_step, B):
-    """Roofline of the f32 parity path's step: its x6 convs against the dense bf16 peak / 6, the rest against
-    the dense f32 MFMA peak; frac = the time both would take at their peaks / the measured time."""
-    fx6, frest = x6_flops(p, H, W, S)
-    ideal_ms = B * (fx6 / (X6_PEAK_TFLOPS * 1e12) + frest / (PEAK_F32_TFLOPS * 1e12)) * 1e3
-    return {"flop_x6_per_env_step": fx6, "flop_f32_per_env_step": frest, "peak_x6": X6_PEAK_TFLOPS,
-            "peak_f32": PEAK_F32_TFLOPS, "peak": B * (fx6 + frest) / (ideal_ms * 1e-3) / 1e12,
+def parity_roofline(p, H, W, S, ms_per_step, B, x3=False):
+    """Roofline of the f32 parity path's step: its x3 convs against the dense fp16 peak / 3, its x6 convs against the
+    dense bf16 peak / 6, the rest against the dense f32 MFMA peak; frac = the time all would take at their peaks / the
+    measured time."""
+    fx3, fx6, frest = x6_flops(p, H, W, S, x3)
+    ideal_ms = B * (fx3 / (X3_PEAK_TFLOPS * 1e12) + fx6 / (X6_PEAK_TFLOPS * 1e12) + frest / (PEAK_F32_TFLOPS * 1e12)) * 1e3
+    return {"flop_x3_per_env_step": fx3, "flop_x6_per_env_step": fx6, "flop_f32_per_env_step": frest,
+            "peak_x3": X3_PEAK_TFLOPS, "peak_x6": X6_PEAK_TFLOPS,
+            "peak_f32": PEAK_F32_TFLOPS, "peak": B * (fx3 + fx6 + frest) / (ideal_ms * 1e-3) / 1e12,
             "ideal_ms_per_step": ideal_ms, "frac": ideal_ms / ms_per_step}
 
 
@@ -486,14 +500,15 @@ def restore_loop(loop, snap, B=None):
 def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W, nsub=None):
     """The first timed step replayed on the f32 parity path (networks within 1e-5 of the reference,
     bit-exact trees): the same env state, search id and keyed randomness as the benchmarked step. The parity
-    path's latent convs run as f32-faithful split-bf16 products (conv_x6: six bf16 MFMAs per f32 product,
-    each conv as close to exact as an f32 one); the same step is also replayed with those convs on the
-    f32-input MFMA (conv_igemm, the parity path of rounds 1-3). Returns the fraction of all B envs whose visit
-    counts equal the benchmarked step's, the agreement of the two parity paths, and their throughputs (second
-    replays, HIP events) against the dense f32 MFMA peak.
+    path's 4x5-latent convs run as split-fp16 x3 products (round 6: three fp16 MFMAs per f32 product, about 22
+    bits per operand), the representation's as split-bf16 x6 products; the same step is also replayed with the
+    latent convs on x6 (round 5's parity path) and on the f32-input MFMA (conv_igemm, rounds 1-3) — the visit
+    counts of all three must agree. Returns the fraction of the envs whose visit counts equal the benchmarked
+    step's, the agreement of the parity forms, and their throughputs (second replays, HIP events) against their
+    rooflines.
     nsub < B (config 3's 84x84 geometry, whose f32 node pool at 4096 envs would not fit beside the benchmarked
     loop's): the first nsub envs only, restored from the snapshot's env-major prefix; the same global env ids, so the
-    same keyed noise and tie-breaks; conv_x6 only (no f32-MFMA A/B)."""
+    same keyed noise and tie-breaks; the default form only (no A/B)."""
     from mzba.agent import MuZeroAgent
     from mzba.acting import ActingLoop
     nsub = nsub or B
@@ -506,10 +521,14 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W, nsub=None):
     l32.reset(0)
     fl = step_flops(ag32.packed, H, W, args.sims)
     p32 = ag32.packed
+    has_x3 = p32.dyn0.get("wx3") is not None
+    forms = [("x3", True, True)] if has_x3 else []
+    forms += [("x6", True, False), ("f32mfma", False, False)] if nsub == B or not has_x3 else []
+    forms = forms if nsub == B else forms[:1]
     runs = {}
-    for x6 in ((True, False) if nsub == B else (True,)):
+    for name, x6, x3 in forms:
         for rn in (l32.ws.runner, l32.rep_runner):
-            rn.use_x6 = x6
+            rn.use_x6, rn.use_x3 = x6, x3
         counts, ms = [], []
         for _ in range(2):  # the first replay also warms the path (scratch, code objects)
             restore_loop(l32, snap, B)
@@ -520,41 +539,50 @@ def f32_parity_path(cfg, mcfg, sd, loop, snap, t0, args, B, H, W, nsub=None):
             torch.cuda.synchronize()
             ms.append(e0.elapsed_time(e1))
             counts.append(l32.rec["counts"][t0].cpu().numpy())
-        runs[x6] = (counts, ms, l32.rec["values"][t0].cpu().numpy())
-    counts, ms, v32 = runs[True]
+        runs[name] = (counts, ms, l32.rec["values"][t0].cpu().numpy())
+    main = forms[0][0]
+    counts, ms, v32 = runs[main]
     c16 = loop.rec["counts"][t0].cpu().numpy()[:nsub]
     same = (counts[-1] == c16).all(1)
     l1 = np.abs(counts[-1].astype(np.int64) - c16.astype(np.int64)).sum(1)
     v16 = loop.rec["values"][t0].cpu().numpy()[:nsub]
     eps = nsub / (ms[-1] * 1e-3)
-    rl = parity_roofline(p32, H, W, args.sims, ms[-1], nsub)
-    vs_mfma = None
-    if False in runs:
-        cf, msf, vf = runs[False]
-        same_f = (cf[-1] == counts[-1]).all(1)
+    rl = parity_roofline(p32, H, W, args.sims, ms[-1], nsub, x3=main == "x3")
+
+    def other(name):
+        if name not in runs or name == main:
+            return None
+        cf, msf, vf = runs[name]
         eps_f = nsub / (msf[-1] * 1e-3)
-        vs_mfma = {"value": eps_f, "ms_per_step": msf[-1], "speedup": eps / eps_f,
-                   "frac": eps_f * fl / 1e12 / PEAK_F32_TFLOPS,
-                   "visit_count_match": float(same_f.mean()),
-                   "value_max_abs_diff": float(np.abs(vf - v32).max()),
-                   "deterministic": bool((cf[0] == cf[1]).all())}
+        r = {"value": eps_f, "ms_per_step": msf[-1], "speedup": eps / eps_f,
+             "visit_count_match": float((cf[-1] == counts[-1]).all(1).mean()),
+             "value_max_abs_diff": float(np.abs(vf - v32).max()),
+             "deterministic": bool((cf[0] == cf[1]).all())}
+        r["frac"] = (eps_f * fl / 1e12 / PEAK_F32_TFLOPS if name == "f32mfma" else
+                     parity_roofline(p32, H, W, args.sims, msf[-1], nsub)["frac"])
+        return r
     out = {"match": float(same.mean()), "envs": nsub,
            "root_value_max_abs_diff": float(np.abs(v16 - v32).max()),
            # beside the exact-match fraction: how far the count rows are apart, and whether the most visited
            # action (what temperature sampling mostly picks at low T) agrees
            "l1_mean": float(l1.mean()), "l1_max": int(l1.max()),
            "top_action_agreement": float((counts[-1].argmax(1) == c16.argmax(1)).mean()),
-           "path": {"dtype": "f32 (latent convs as split-bf16 x6 products)", "value": eps, "unit": "env-steps/s",
+           "path": {"dtype": ("f32 (4x5 latent convs as split-fp16 x3 products, representation convs as split-bf16 x6)"
+                              if main == "x3" else "f32 (latent convs as split-bf16 x6 products)"),
+                    "value": eps, "unit": "env-steps/s",
                     "ms_per_step": ms[-1], "achieved_tflops": eps * fl / 1e12,
-                    # the x6 convs against 2500 / 6 TF, the rest against 157.3 TF; `peak` = the blended ceiling
+                    # the x3 convs against 2500 / 3 TF, x6 against 2500 / 6 TF, the rest against 157.3 TF;
+                    # `peak` = the blended ceiling
                     "peak": rl["peak"], "frac": rl["frac"], "roofline": rl,
                     "deterministic": bool((counts[0] == counts[1]).all()),
                     "value_max_abs_diff_where_counts_agree": float(np.abs(v16 - v32)[same].max()) if same.any() else None,
-                    "envs": nsub,
-                    "vs_f32_mfma_path": vs_mfma,
-                    "what": "one acting step of the same envs on the f32 parity path (separate launches per layer, "
-                            "the latent 3x3 convs on conv_x6), eager, HIP events around the step; vs_f32_mfma_path: "
-                            "the same with those convs on the f32-input MFMA"}}
+                    "envs": nsub, "form": main,
+                    "vs_x6_path": other("x6"),
+                    "vs_f32_mfma_path": other("f32mfma"),
+                    "what": "one acting step of the same envs on the f32 parity path (separate launches per layer), "
+                            "eager, HIP events around the step; vs_x6_path / vs_f32_mfma_path: the same with the "
+                            "latent convs on the split-bf16 x6 form / the f32-input MFMA (visit_count_match: against "
+                            "this path's counts)"}}
     del l32, ag32
     torch.cuda.empty_cache()
     return out

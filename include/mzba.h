@@ -143,6 +143,18 @@ int mzba_conv_x6_ex_supported(int H, int W, int Cin, int Cout, int ks, int gathe
 int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx,
                     const float* bias, const float* act_bias, const int32_t* act, int A, const void* res, void* out,
                     int B, int H, int W, int Cin, int Cout, int ks, int relu, hipStream_t stream);
+/* Split-fp16 x3 form of the pixel-tiled conv (round 6; networks.py:19-35, 103-241, the reference's f32 convs):
+ * every f32 operand as two fp16 parts (x = xh + xl, xh = fp16(x), xl = fp16(x - xh)) and a product as the three
+ * terms xh wl + xl wh + xh wh on fp16 MFMAs with f32 accumulation — about 22 significant bits per operand, half the
+ * MFMAs of the x6 form. wx3 = the two fp16 parts of w 2^k (k per output channel: max |w 2^k| in [2^14, 2^15)), each in
+ * pack_lat16's packing, back to back; wscale[Cout] = 2^-k. Activations must stay below 65520 in magnitude (else the
+ * output turns NaN). Same shapes, gather and action-bias contract as mzba_conv_x6_ex at the 4x5 latent
+ * (mzba_conv_x3_supported). */
+int mzba_conv_x3_supported(int H, int W, int Cin, int Cout, int ks, int gather);
+int mzba_conv_x3_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx3,
+                    const float* wscale, const float* bias, const float* act_bias, const int32_t* act, int A,
+                    const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
+                    hipStream_t stream);
 /* 2 (default): the pixel-tiled form at the 4x5 latent where its 16-env workgroups load the busiest CU less than the
  * pre-split tiles (the gathered / Cout 128 convs always), else the pre-split form where its staged rows fit (the f32
  * activations split once into bf16 hi / mid / lo planes while staging, 1.5x the f32 row; 8 waves x 32 channels),

@@ -18,6 +18,7 @@
 // operand, read as f32 from LDS and split in registers per fragment (each split feeds 4 column tiles x 6
 // MFMAs). Epilogue in f32: + bias (+ residual), ReLU.
 #include "common.h"
+#include "elt.h"
 #include <type_traits>
 #include <utility>
 
@@ -56,6 +57,20 @@ MZ_DEV void split8(const uint4& u0, const uint4& u1, bf16x8& h, bf16x8& m, bf16x
     h[i] = hb;
     m[i] = mb;
     l[i] = (__bf16)r2;
+  }
+}
+
+// fp16 split of 8 f32 for the x3 form: hi = fp16(x), lo = fp16(x - hi) (x - hi is exact in f32; |lo| <= 2^-11 |x|,
+// lo's own rounding <= 2^-22 |x| while lo is normal, i.e. |x| >= 2^-3; below, absolute 2^-25). |x| < 65520 or
+// hi = inf and the output turns NaN (loud, never silently wrong)
+MZ_DEV void split8h(const uint4& u0, const uint4& u1, f16x8& h, f16x8& l) {
+  const float x[8] = {__uint_as_float(u0.x), __uint_as_float(u0.y), __uint_as_float(u0.z), __uint_as_float(u0.w),
+                      __uint_as_float(u1.x), __uint_as_float(u1.y), __uint_as_float(u1.z), __uint_as_float(u1.w)};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const _Float16 hb = (_Float16)x[i];
+    h[i] = hb;
+    l[i] = (_Float16)(x[i] - (float)hb);
   }
 }
 
@@ -454,9 +469,10 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
 namespace x6t {
 constexpr int E = 16, HW = 20, H = 4, W = 5, CIN = 256, NCS = 8;
 constexpr int ROWS = HW * E;          // 320 staged rows (pixel, env)
-constexpr int PB = ROWS * 64;         // bytes per bf16 plane of a 32-channel block
-constexpr int RAW = 3 * PB;           // f32 rows of the next block: 320 x 128 B
-constexpr int LDS = RAW + ROWS * 128;  // 100 KiB
+constexpr int PB = ROWS * 64;         // bytes per 16-bit plane of a 32-channel block
+// NP planes (3: the bf16 x6 form, 2: the fp16 x3 form), then the f32 rows of the next block: 320 x 128 B
+constexpr int raw(int np) { return np * PB; }
+constexpr int lds(int np) { return raw(np) + ROWS * 128; }  // 100 / 80 KiB
 }  // namespace x6t
 
 // the (tap, output pixel) pairs of a 3x3 conv on the 4x5 latent whose source pixel is in the image: 130 of 180
@@ -545,15 +561,38 @@ struct X6TArgs {
   float* out;             // [B][20][Cout]
   int B, Cout, relu;
   long long part;         // elements per weight part
+  const float* wscale;    // x3 form: per output channel, 2^-k of the host's weight scaling (exact); x6: unused
 };
 
 MZ_DEV int tkey(int e) { return (e >> 2) & 2; }  // chunk swizzle of row 16 p + e (64-B plane rows)
 
 // NW waves of 16 output channels each: 8 (128 channels per workgroup, the default) or 4 (64 channels: twice the
 // workgroups where the 8-wave grid leaves CUs idle, config 2's 1 024 envs; per wave the same arithmetic)
-template <bool GA, int KSZ = 3, int NW = 8>
+// s_waitcnt vmcnt(N) for the ring depths below
+template <int N>
+MZ_DEV void x6t_wait_vm() {
+  static_assert(N == 18 || N == 12 || N == 3 || N == 2, "ring wait depth");
+  if constexpr (N == 18)
+    asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+  else if constexpr (N == 12)
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 3)
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+}
+
+// NP = 3: the bf16 x6 form above. NP = 2 (round 6): split-fp16 x3 — x = xh + xl (fp16 hi / lo, split8h), the weights
+// likewise from w 2^k (k per output channel, so every weight's lo part stays normal: agent.py split_pack_x3), and a
+// product as the three terms xh wl + xl wh + xh wh (xl wl, below 2^-22 of the product, dropped) on
+// v_mfma_f32_16x16x32_f16, f32 accumulate; the accumulator times 2^-k in the epilogue (exact). About 22 significant
+// bits per operand at half the MFMAs of x6 (tests/test_gpu_parity.py: the nets at 1e-5 of the reference)
+template <bool GA, int KSZ = 3, int NW = 8, int NP = 3>
 __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   using namespace x6t;
+  static_assert(NP == 3 || NP == 2, "x6 (bf16) or x3 (fp16)");
+  using V8 = std::conditional_t<NP == 3, bf16x8, f16x8>;
+  constexpr int RAW = raw(NP);
   constexpr int NT = 64 * NW;
   constexpr const X6TGroups& G = KSZ == 3 ? kGroups : kGroups1;
   constexpr int SPB = KSZ == 3 ? 3 : 1;     // ring steps per channel block (the dy rows)
@@ -587,12 +626,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
         const int r = g >> 2, k8 = g & 3;
         const uint4 u0 = *reinterpret_cast<const uint4*>(lds + RAW + r * 128 + k8 * 32);
         const uint4 u1 = *reinterpret_cast<const uint4*>(lds + RAW + r * 128 + k8 * 32 + 16);
-        bf16x8 h, m, l;
-        split8(u0, u1, h, m, l);
         uint8_t* row = lds + r * 64 + ((k8 ^ tkey(r & 15)) << 4);
-        *reinterpret_cast<bf16x8*>(row) = h;
-        *reinterpret_cast<bf16x8*>(row + PB) = m;
-        *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+        if constexpr (NP == 3) {
+          bf16x8 h, m, l;
+          split8(u0, u1, h, m, l);
+          *reinterpret_cast<bf16x8*>(row) = h;
+          *reinterpret_cast<bf16x8*>(row + PB) = m;
+          *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+        } else {
+          f16x8 h, l;
+          split8h(u0, u1, h, l);
+          *reinterpret_cast<f16x8*>(row) = h;
+          *reinterpret_cast<f16x8*>(row + PB) = l;
+        }
       }
     }
   };
@@ -605,16 +651,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   auto wload = [&](int ti, int part, int j) {
     j = j < SPB * NCS ? j : SPB * NCS - 1;
     const int s = KSZ == 3 ? (3 * (j % 3) + ti) * 8 + j / 3 : j;
-    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + s * 1024, 0));
+    return __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + s * 1024, 0));
   };
   constexpr int T0 = KSZ == 3 ? 0 : 1, T1 = KSZ == 3 ? 3 : 2;  // the dx taps the ring holds
-  bf16x8 bq[2][3][3];  // [step parity][dx tap][part]
+  // ring loads a reload issues; after the LDS-DMA of the next block a 3x3 block issues three reloads, a 1x1 block one,
+  // so waiting down to the youngest two (3x3) or one (1x1) reloads has the DMA complete
+  constexpr int RL = (T1 - T0) * NP, VM = KSZ == 3 ? 2 * RL : RL;
+  V8 bq[2][3][NP];  // [step parity][dx tap][part]
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
     for (int ti = T0; ti < T1; ++ti)
 #pragma unroll
-      for (int pt = 0; pt < 3; ++pt) bq[cc][ti][pt] = wload(ti, pt, cc);
+      for (int pt = 0; pt < NP; ++pt) bq[cc][ti][pt] = wload(ti, pt, cc);
 
   f32x4 acc[HW];
 #pragma unroll
@@ -632,37 +681,45 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
 
   // the lane's B fragment of source pixel ps: row 16 ps + n, chunk q of each plane
   const int lrow = n * 64 + ((q ^ tkey(n)) << 4);
-  auto frag = [&](int ps, bf16x8 (&f)[3]) {
+  auto frag = [&](int ps, V8 (&f)[NP]) {
 #pragma unroll
-    for (int pt = 0; pt < 3; ++pt) f[pt] = *reinterpret_cast<const bf16x8*>(lds + pt * PB + ps * 1024 + lrow);
+    for (int pt = 0; pt < NP; ++pt) f[pt] = *reinterpret_cast<const V8*>(lds + pt * PB + ps * 1024 + lrow);
   };
 
   // one 32-channel block: the (dy, source pixel) groups (x6t::kGroups), the next group's fragment read during the
   // current group's MFMAs; after a dy row's last group its ring slot is reloaded (step j + 2)
   auto block = [&](int b, auto par) {
     constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (SPB b)
-    bf16x8 fr[2][3];
+    V8 fr[2][NP];
     frag(G.src[0], fr[0]);
     x6t_static_for<G.n>([&](auto I) {
       constexpr int i = decltype(I)::value;
       constexpr int d = G.dy[i], sl = (P0 + d) & 1, cur = i & 1, cnt = G.cnt[i];
       if (i + 1 < G.n) frag(G.src[i + 1], fr[cur ^ 1]);
-      const bf16x8* xs[6] = {&fr[cur][0], &fr[cur][1], &fr[cur][2], &fr[cur][0], &fr[cur][1], &fr[cur][0]};
-      constexpr int wp[6] = {2, 1, 0, 1, 0, 0};  // per accumulator the small terms first (conv_x6p's order)
+      // per accumulator the small terms first (conv_x6p's order): x6 (w, x) parts (2,0) (1,1) (0,2) (1,0) (0,1)
+      // (0,0); x3 (1,0) (0,1) (0,0)
+      constexpr int NTM = NP == 3 ? 6 : 3;
+      constexpr int wp6[6] = {2, 1, 0, 1, 0, 0}, xp6[6] = {0, 1, 2, 0, 1, 0};
+      constexpr int wp3[3] = {1, 0, 0}, xp3[3] = {0, 1, 0};
 #pragma unroll
-      for (int k = 0; k < 6; ++k)
+      for (int k = 0; k < NTM; ++k)
 #pragma unroll
-        for (int o = 0; o < cnt; ++o)
-          acc[G.out[i][o]] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][G.dx[i][o]][wp[k]], *xs[k],
-                                                                     acc[G.out[i][o]], 0, 0, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 6 * cnt, 0);
+        for (int o = 0; o < cnt; ++o) {
+          if constexpr (NP == 3)
+            acc[G.out[i][o]] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][G.dx[i][o]][wp6[k]], fr[cur][xp6[k]],
+                                                                       acc[G.out[i][o]], 0, 0, 0);
+          else
+            acc[G.out[i][o]] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[sl][G.dx[i][o]][wp3[k]], fr[cur][xp3[k]],
+                                                                      acc[G.out[i][o]], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NTM * cnt, 0);
       __builtin_amdgcn_sched_barrier(0);
       if (G.last[i]) {
 #pragma unroll
         for (int ti = T0; ti < T1; ++ti)
 #pragma unroll
-          for (int pt = 0; pt < 3; ++pt) bq[sl][ti][pt] = wload(ti, pt, SPB * b + d + 2);
+          for (int pt = 0; pt < NP; ++pt) bq[sl][ti][pt] = wload(ti, pt, SPB * b + d + 2);
         __builtin_amdgcn_sched_barrier(0);
       }
     });
@@ -671,22 +728,15 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   for (int b = 0; b < NCS; b += 2) {
     block(b, std::integral_constant<int, 0>());  // SPB b even
     // block b + 1's raw rows: wait for this wave's LDS-DMA, then every wave's, then split. The DMA is older than
-    // every ring load block b issued after it: 3 reloads of 9 (3x3; waiting down to the youngest 18 is enough) or
-    // one reload of 3 (1x1: the youngest 3 only — 6 would leave the last DMA pieces in flight)
-    if (KSZ == 3)
-      asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    // every ring load block b issued after it (VM above: a 1x1 block's one reload only — ADVICE r5)
+    x6t_wait_vm<VM>();
     __syncthreads();
     split();
     __syncthreads();
     if (b + 2 < NCS) stage(b + 2);
     block(b + 1, std::integral_constant<int, 1>());  // SPB (b + 1) odd (SPB = 3 or 1)
     if (b + 2 < NCS) {
-      if (KSZ == 3)
-        asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      x6t_wait_vm<VM>();
       __syncthreads();
       split();
       __syncthreads();
@@ -700,6 +750,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   const float lo = a.relu ? 0.f : -__builtin_inff();
   const int ch = nb + 4 * q;
   const float4 bb = *reinterpret_cast<const float4*>(a.bias + ch);
+  if constexpr (NP == 2) {  // undo the weights' 2^k (exact)
+    const float4 sc = *reinterpret_cast<const float4*>(a.wscale + ch);
+#pragma unroll
+    for (int p = 0; p < HW; ++p) acc[p] *= f32x4{sc.x, sc.y, sc.z, sc.w};
+  }
   const int act = GA && a.act_bias ? a.act[env] : 0;
   const size_t ob = (size_t)env * HW * a.Cout;
   float4 rv[HW];
@@ -791,6 +846,30 @@ int x6_geometry(int W, int Cin, X6Args& g) {
 int x6_halo_launch(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
                    int Cin, int Cout, int relu, hipStream_t stream);
 
+// conv_x6t_kernel's grid for t.B envs: 4-wave (64-channel) workgroups where the 8-wave grid leaves CUs idle
+// (mzba_conv_x6_set_waves: auto / 8 / 4)
+template <int NP>
+void x6t_launch(const X6TArgs& t, int ks, bool ga, hipStream_t stream) {
+  const long long t16 = (t.B + x6t::E - 1) / x6t::E;
+  const int nw = g_x6t_waves ? g_x6t_waves : (t16 * (t.Cout / 128) < x6p_ncu() ? 4 : 8);
+  const dim3 grid((unsigned)t16, (unsigned)(t.Cout / (16 * nw)));
+  auto launch = [&](auto kern, int nthreads) {
+    mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
+    hipLaunchKernelGGL(kern, grid, dim3(nthreads), x6t::lds(NP), stream, t);
+  };
+  if (nw == 4) {
+    if (ks == 1)
+      launch(conv_x6t_kernel<false, 1, 4, NP>, 256);
+    else
+      ga ? launch(conv_x6t_kernel<true, 3, 4, NP>, 256) : launch(conv_x6t_kernel<false, 3, 4, NP>, 256);
+  } else {
+    if (ks == 1)
+      launch(conv_x6t_kernel<false, 1, 8, NP>, 512);  // the reward / value heads' 1x1 ConvBlocks (never gathered)
+    else
+      ga ? launch(conv_x6t_kernel<true, 3, 8, NP>, 512) : launch(conv_x6t_kernel<false, 3, 8, NP>, 512);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -834,30 +913,36 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
   }
   if (tiled) {
     X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx, bias, act_bias, act, A,
-              (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin};
-    // 4-wave (64-channel) workgroups where the 8-wave grid leaves CUs idle (mzba_conv_x6_set_waves: auto / 8 / 4)
-    const long long t16 = (B + x6t::E - 1) / x6t::E;
-    const int nw = g_x6t_waves ? g_x6t_waves : (t16 * (Cout / 128) < x6p_ncu() ? 4 : 8);
-    const dim3 grid((unsigned)t16, (unsigned)(Cout / (16 * nw)));
-    auto launch = [&](auto kern, int nthreads) {
-      mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
-      hipLaunchKernelGGL(kern, grid, dim3(nthreads), x6t::LDS, stream, t);
-    };
-    if (nw == 4) {
-      if (ks == 1)
-        launch(conv_x6t_kernel<false, 1, 4>, 256);
-      else
-        ga ? launch(conv_x6t_kernel<true, 3, 4>, 256) : launch(conv_x6t_kernel<false, 3, 4>, 256);
-    } else {
-      if (ks == 1)
-        launch(conv_x6t_kernel<false, 1>, 512);  // the reward / value heads' 1x1 ConvBlocks (never gathered)
-      else
-        ga ? launch(conv_x6t_kernel<true, 3>, 512) : launch(conv_x6t_kernel<false, 3>, 512);
-    }
+              (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin, nullptr};
+    x6t_launch<3>(t, ks, ga, stream);
     MZ_LAUNCH_CHECK();
     return 0;
   }
   return x6_halo_launch(in, wx, bias, res, out, B, H, W, Cin, Cout, relu, stream);
+}
+
+// the split-fp16 x3 form of the pixel-tiled conv (conv_x6t_kernel<.., NP = 2>): the 4x5 latent, Cin 256, Cout 256 /
+// 128, 3x3 (gathered / action-biased like conv_x6_ex) or 1x1 (contiguous). wx3 = the two fp16 parts of w 2^k in the
+// pack_lat16 packing back to back (agent.py split_pack_x3), wscale[Cout] = 2^-k.
+int mzba_conv_x3_supported(int H, int W, int Cin, int Cout, int ks, int gather) {
+  if (ks == 1 && gather) return 0;
+  return (ks == 3 || ks == 1) && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128) ? 1 : 0;
+}
+
+int mzba_conv_x3_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx3,
+                    const float* wscale, const float* bias, const float* act_bias, const int32_t* act, int A,
+                    const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
+                    hipStream_t stream) {
+  MZ_CHECK_ARG(in && wx3 && wscale && bias && out && B > 0, -1);
+  MZ_CHECK_ARG(!act_bias || (act && A > 0 && !res), -1);
+  const bool ga = slot || act_bias || env_stride != (long long)H * W * Cin;
+  MZ_CHECK_ARG(mzba_conv_x3_supported(H, W, Cin, Cout, ks, ga ? 1 : 0), -2);
+  MZ_CHECK_ARG((long long)B * H * W + 256 < (1LL << 31), -3);
+  X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx3, bias, act_bias, act, A,
+            (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin, wscale};
+  x6t_launch<2>(t, ks, ga, stream);
+  MZ_LAUNCH_CHECK();
+  return 0;
 }
 
 // out = act(conv3x3(in) + bias (+ res)) in f32 on contiguous NHWC images of B envs, every product as the

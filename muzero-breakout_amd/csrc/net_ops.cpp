@@ -51,7 +51,7 @@ void check_dev(const at::Tensor& t, const char* name) {
 int64_t round64(int64_t c) { return (c + 63) / 64 * 64; }
 
 struct Conv {  // one conv (+ folded BN); PackedNets._conv
-  at::Tensor w, b, wf, wt, act_bias, wh, wx;
+  at::Tensor w, b, wf, wt, act_bias, wh, wx, wx3, wsc;  // wx3 / wsc: the split-fp16 x3 form's parts and 2^-k
   int64_t cin = 0, cout = 0, ks = 0, A = 0;
 };
 struct Lin {  // Linear head in NHWC flatten order; PackedNets._linear
@@ -94,6 +94,12 @@ struct NetPack : torch::CustomClassHolder {
     if (wh.has_value()) c.wh = *wh;
     if (wx.has_value()) c.wx = *wx;
     convs[name] = c;
+  }
+  // the f32 parity path's split-fp16 x3 weights of an added conv (round 6: mzba_conv_x3_ex)
+  void add_conv_x3(const std::string& name, const at::Tensor& wx3, const at::Tensor& wsc) {
+    auto it = convs.find(name);
+    TORCH_CHECK(it != convs.end(), "mz.NetPack: add_conv_x3 before add_conv of '", name, "'");
+    it->second.wx3 = wx3, it->second.wsc = wsc;
   }
   void add_linear(const std::string& name, const at::Tensor& w, const at::Tensor& b, const c10::optional<at::Tensor>& wb,
                   int64_t K, int64_t O) {
@@ -158,7 +164,7 @@ struct NetRunner : torch::CustomClassHolder {
   NetPack* p;
   int64_t B, H, W, lhw, HW, plan = 0;
   bool use_lat = true, use_tower = true, use_fused = true, use_band = true, use_rep_tail = true, use_band_res = true,
-       use_rep_blocks = true, use_rep_trunk = true, use_halo = true, use_x6 = true;
+       use_rep_blocks = true, use_rep_trunk = true, use_halo = true, use_x6 = true, use_x3 = true;
   at::Tensor r_a, r_t, r_b, x, tt, rc, pc, vc;  // scratch, allocated on first use
   // live probe: HIP events around every tower launch / latent residual conv (eager launches only)
   bool probe_on = false;
@@ -170,6 +176,7 @@ struct NetRunner : torch::CustomClassHolder {
     lhw = p->lh * p->lw;
     HW = H * W;
     if (p->tower_ok()) plan = mzba_tower_plan((int)B);  // the kernel this runner launches, fixed here
+    use_x3 = p->i("use_x3", 1) != 0;  // the pack's default for new runners (NetPack.set_int("use_x3", 0 / 1))
   }
   ~NetRunner() override { clear_probe(); }
   c10::intrusive_ptr<NetPack> pin() const {
@@ -227,6 +234,15 @@ struct NetRunner : torch::CustomClassHolder {
     env_stride = env_stride < 0 ? H_ * W_ * l.cin : env_stride;
     const bool ab = l.act_bias.defined();
     const int gather = (slot || ab || env_stride != H_ * W_ * l.cin) ? 1 : 0;
+    // the f32 parity path's latent convs at the 4x5 latent: split-fp16 x3 products (round 6) where the pack has them
+    if (l.wx3.defined() && use_x6 && use_x3 && p->dtype == 0 && !(ab && res) &&
+        mzba_conv_x3_supported((int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks, gather)) {
+      check_rc(mzba_conv_x3_ex(in, env_stride, slot, slot_stride, vp(l.wx3), vp<float>(l.wsc), vp<float>(l.b),
+                               ab ? vp<float>(l.act_bias) : nullptr, ab ? act : nullptr, (int)l.A, res, out, (int)B,
+                               (int)H_, (int)W_, (int)l.cin, (int)l.cout, (int)l.ks, relu, s),
+               "mzba_conv_x3_ex");
+      return;
+    }
     // the f32 parity path's 3x3 convs: f32-faithful split-bf16 products (conv_x6; at the 4x5 latent the pixel-tiled
     // form, which also takes the dynamics' first conv off the latent pool + its action-bias table)
     if (l.wx.defined() && use_x6 && p->dtype == 0 && !(ab && res) &&
@@ -719,6 +735,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              else if (k == "use_rep_trunk") r->use_rep_trunk = v;
              else if (k == "use_halo") r->use_halo = v;
              else if (k == "use_x6") r->use_x6 = v;
+             else if (k == "use_x3") r->use_x3 = v;
              else TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
            })
       .def("get_flag",
@@ -733,6 +750,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
              if (k == "use_rep_trunk") return r->use_rep_trunk;
              if (k == "use_halo") return r->use_halo;
              if (k == "use_x6") return r->use_x6;
+             if (k == "use_x3") return r->use_x3;
              TORCH_CHECK(false, "mz.NetRunner: unknown flag ", k);
              return false;
            })
@@ -752,6 +770,7 @@ TORCH_LIBRARY_FRAGMENT(mz, m) {
       .def(torch::init<>())
       .def("set_meta", &NetPack::set_meta)
       .def("add_conv", &NetPack::add_conv)
+      .def("add_conv_x3", &NetPack::add_conv_x3)
       .def("add_linear", &NetPack::add_linear)
       .def("add_rep", &NetPack::add_rep)
       .def("set_tensor", &NetPack::set_tensor)

@@ -41,6 +41,8 @@ SIGNATURES = {
     "mzba_conv_x6": [P, P, P, P, P, I, I, I, I, I, I, P],
     "mzba_conv_x6_ex_supported": [I, I, I, I, I, I],
     "mzba_conv_x6_ex": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
+    "mzba_conv_x3_supported": [I, I, I, I, I, I],
+    "mzba_conv_x3_ex": [P, LL, P, LL, P, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
     "mzba_conv_x6_set_variant": [I],
     "mzba_conv_x6_set_waves": [I],
     "mzba_conv_lat_supported": [I, I, I, I, I],

@@ -58,6 +58,22 @@ def split_pack_x6(wp, cout, ks, cin):
                       for part in (hi, mid, lo)])
 
 
+def split_pack_x3(wp, cout, ks, cin):
+    """mzba_conv_x3_ex's weights (round 6): the f32 weights [Cout][tap][Cin], each output channel c scaled by 2^k_c
+    (max |w_c 2^k_c| in [2^14, 2^15], so every part below stays a normal fp16 down to 2^-25 of the row's largest
+    weight; the scaling is exact), split into two fp16 parts hi = fp16(w 2^k), lo = fp16(w 2^k - hi) (round to
+    nearest even), each in the pack_lat16 packing, back to back; and 2^-k_c per channel (f32) for the epilogue."""
+    w = np.asarray(wp, dtype=np.float64).astype(np.float32).reshape(cout, -1)
+    m = np.abs(w).max(1)
+    k = np.where(m > 0, np.floor(np.log2(2.0 ** 15 / np.where(m > 0, m, 1.0))), 0.0).clip(-100, 100)
+    ws = (w.astype(np.float64) * 2.0 ** k[:, None]).astype(np.float32)  # exact: a power of two
+    hi = ws.astype(np.float16)
+    lo = (ws - hi.astype(np.float32)).astype(np.float16)
+    assert np.isfinite(hi).all() and np.isfinite(lo).all()
+    parts = torch.cat([torch.from_numpy(np.ascontiguousarray(pack_lat16(x, cout, ks, cin))) for x in (hi, lo)])
+    return parts, torch.tensor(2.0 ** -k, dtype=torch.float32)
+
+
 def pack_tower_conv(w):
     """3x3 conv weight (OIHW, BN folded) -> the fused tower's packing: pack_lat16 with the taps
     ordered (dx, dy) (tower.hip walks column shifts outermost)."""
@@ -144,6 +160,8 @@ class PackedNets:
         def conv(name, c):
             n.add_conv(name, c["w"], c["b"], c.get("wf"), c.get("wt"), c.get("act_bias"), c["cin"], c["cout"], c["ks"],
                        c.get("A", 0), c.get("wh"), c.get("wx"))
+            if c.get("wx3") is not None:
+                n.add_conv_x3(name, c["wx3"], c["wsc"])
 
         for i, (kind, layer) in enumerate(self.rep):
             if kind == "conv":
@@ -374,6 +392,11 @@ class PackedNets:
             # the f32 parity path's 3x3 convs as split-bf16 x6 products (round 5: the 4x5 latent's dynamics first
             # conv with its slot gather + action-bias table, and the policy head's 256 -> 128 conv, too)
             layer["wx"] = split_pack_x6(wp, cout, k, cin_p).to(self.device)
+        if (hw is not None and self.dtype == "f32"
+                and L.lib().mzba_conv_x3_supported(hw[0], hw[1], cin_p, cout, k, int(act_w is not None))):
+            # round 6: the 4x5 latent's convs also as split-fp16 x3 products (half the MFMAs of x6)
+            wx3, wsc = split_pack_x3(wp, cout, k, cin_p)
+            layer["wx3"], layer["wsc"] = wx3.to(self.device), wsc.to(self.device)
         if band and self.dtype == "bf16" and k == 3 and L.lib().mzba_conv_band_supported(16, 20, cin, cout, 3):
             # representation convs at full resolution: the band kernel's packing (tower order)
             layer["wt"] = torch.tensor(np.concatenate([pack_tower_conv(w), np.zeros(LAT_PAD_ELEMS)]),
@@ -422,7 +445,7 @@ class NetRunner:
     stream — representation_ / dynamics_ / prediction_ / prediction_tree_ (`torch.ops.mz`)."""
 
     FLAGS = ("use_lat", "use_tower", "use_fused", "use_band", "use_rep_tail", "use_band_res", "use_rep_blocks",
-             "use_rep_trunk", "use_halo", "use_x6")
+             "use_rep_trunk", "use_halo", "use_x6", "use_x3")
 
     def __init__(self, packed, B, H, W):
         self.p = packed

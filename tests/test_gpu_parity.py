@@ -206,11 +206,12 @@ def test_rep_input_builder(L, steps, single_write):
 
 
 # ------------------------------------------------------------------------------ nets
-@pytest.mark.parametrize("tag,x6", [("small", 2), ("full", 2), ("full", 3)])
-def test_nets_f32_match_reference(tag, x6):
+@pytest.mark.parametrize("tag,x6,x3", [("small", 2, 0), ("full", 2, 0), ("full", 3, 0), ("full", 2, 1)])
+def test_nets_f32_match_reference(tag, x6, x3):
     """The f32 parity path's nets on the reference's own outputs (nets_*.npz) within 1e-5. x6 = 3: every 4x5 latent
     3x3 conv on the pixel-tiled x6 form (the form the 4096-env parity path runs: the towers, the dynamics' first
-    conv with its gather + action bias, the policy head's conv); 2: the form chosen by batch (pre-split here)."""
+    conv with its gather + action bias, the policy head's conv); 2: the form chosen by batch (pre-split here).
+    x3 = 1 (round 6): the 4x5 latent's convs on the split-fp16 x3 form instead (mzba_conv_x3_ex), the same 1e-5."""
     from mzba import _lib as L
     from mzba.agent import MuZeroAgent
     d = np.load(os.path.join(GOLDEN, f"nets_{tag}.npz"))
@@ -218,6 +219,7 @@ def test_nets_f32_match_reference(tag, x6):
     mcfg = cfg["model"] if tag == "full" else small_model_cfg(cfg)
     ag = MuZeroAgent(mcfg, dtype="f32")
     ag.load_state_dict(init_state_dict(mcfg, int(d["weight_seed"])))
+    ag.packed.native.set_int("use_x3", x3)  # before the first op creates this batch's runner
     tol = dict(rtol=1e-5, atol=1e-5)  # north_star: within 1e-5 for network logits/values
     try:
         assert L.lib().mzba_conv_x6_set_variant(x6) == 0
@@ -233,9 +235,10 @@ def test_nets_f32_match_reference(tag, x6):
     finally:
         L.lib().mzba_conv_x6_set_variant(2)
     if tag == "full":  # the 4x5 latent's 3x3 convs all carry x6 weights (round 5: dyn0 and the policy conv too)
-        p = ag.packed
+        p = ag.packed    # and x3 weights (round 6)
         assert p.dyn0.get("wx") is not None and p.pol_conv.get("wx") is not None
-        assert all(c.get("wx") is not None for blk in p.dyn + p.pred for c in blk)
+        assert all(c.get("wx") is not None and c.get("wx3") is not None for blk in p.dyn + p.pred for c in blk)
+        assert p.dyn0.get("wx3") is not None and p.pol_conv.get("wx3") is not None
 
 
 def test_nets_bf16_close():
@@ -894,6 +897,92 @@ def test_conv_x6_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks):
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], out)
     assert L.lib().mzba_conv_x6_set_waves(6) == -1
+
+
+@pytest.mark.parametrize("B,Cout,mode,ks,wspread", [(4100, 256, "res", 3, 0), (37, 256, "plain", 3, 0),
+                                                    (4096, 128, "plain", 3, 0), (1000, 256, "gather", 3, 0),
+                                                    (21, 128, "gather", 3, 0), (4096, 256, "plain", 1, 0),
+                                                    (45, 128, "plain", 1, 0), (512, 256, "res", 3, 8),
+                                                    (64, 128, "gather", 3, 8)])
+def test_conv_x3_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks, wspread):
+    """Round 6: the split-fp16 x3 form of the pixel-tiled conv (mzba_conv_x3_ex: x = fp16 hi + fp16 lo, three fp16 MFMA
+    products per f32 product, weights scaled by 2^k per output channel) against an f64 conv of the same f32 operands,
+    on conv_x6t's cases (ragged batches, Cout 128, the gathered + action-biased form, 1x1): within 2x the f32-input MFMA
+    conv's error + 2e-7 and within 3e-6 of the magnitude, and within 5e-6 of the x6 form. wspread: output channels
+    whose weights differ in magnitude by up to 2^wspread (BN-folded weights of trained nets), each kept to 22 bits by
+    its own 2^k. 8- and 4-wave workgroups bit-identical."""
+    from mzba import _lib as L
+    from mzba.agent import split_pack_x6, split_pack_x3
+    H, W, Cin, A, S = 4, 5, 256, 3, 6
+    g = torch.Generator(device="cuda").manual_seed(B + Cout + 7)
+    dev = torch.device("cuda")
+    w = torch.randn(Cout, ks, ks, Cin, generator=g, device=dev) / (Cin * ks * ks) ** 0.5
+    if wspread:
+        w = w * torch.exp2(torch.rand(Cout, 1, 1, 1, generator=g, device=dev) * wspread - wspread / 2)
+    b = torch.randn(Cout, generator=g, device=dev) * 0.1
+    wn = w.cpu().numpy().reshape(Cout, -1)
+    wx = split_pack_x6(wn, Cout, ks, Cin).cuda()
+    wx3, wsc = split_pack_x3(wn, Cout, ks, Cin)
+    wx3, wsc = wx3.cuda(), wsc.cuda()
+    relu = 1 if mode != "plain" else 0
+    res = tab = act = slot = None
+    if mode == "gather":
+        pool = torch.rand(B, S + 1, H, W, Cin, generator=g, device=dev)
+        slot = torch.randint(0, S + 1, (B,), generator=g, device=dev, dtype=torch.int32)
+        act = torch.randint(0, A, (B,), generator=g, device=dev, dtype=torch.int32)
+        tab = torch.randn(H * W, A, Cout, generator=g, device=dev) * 0.1
+        x = pool[torch.arange(B, device=dev), slot.long()].contiguous()
+        src, env_stride, slot_stride = pool, (S + 1) * H * W * Cin, H * W * Cin
+    else:
+        x = torch.rand(B, H, W, Cin, generator=g, device=dev)
+        src, env_stride, slot_stride = x, H * W * Cin, 0
+        if mode == "res":
+            res = torch.rand(B, H, W, Cout, generator=g, device=dev)
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), b.double(),
+                                     padding=ks // 2).permute(0, 2, 3, 1)
+    if res is not None:
+        ref = ref + res.double()
+    if tab is not None:
+        ref = ref + tab.double()[:, act.long()].permute(1, 0, 2).reshape(B, H, W, Cout)
+    if relu:
+        ref = torch.relu(ref)
+    assert L.lib().mzba_conv_x3_supported(H, W, Cin, Cout, ks, int(mode == "gather"))
+    assert not L.lib().mzba_conv_x3_supported(H, W, Cin, Cout, 1, 1) and not L.lib().mzba_conv_x3_supported(8, 10, Cin, Cout, 3, 0)
+
+    def run(fn, wts, extra=()):
+        o = torch.full((B, H, W, Cout), float("nan"), device=dev)
+        L.call(fn, L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(wts), *extra, L.ptr(b), L.ptr(tab), L.ptr(act),
+               A if tab is not None else 0, L.ptr(res), L.ptr(o), B, H, W, Cin, Cout, ks, relu, L.stream())
+        return o
+    out = run("mzba_conv_x3_ex", wx3, (L.ptr(wsc),))
+    try:
+        assert L.lib().mzba_conv_x6_set_variant(3) == 0
+        out6 = run("mzba_conv_x6_ex", wx)
+    finally:
+        L.lib().mzba_conv_x6_set_variant(2)
+    f32 = torch.empty(B, H, W, Cout, device=dev)
+    wd = w.reshape(Cout, -1).contiguous()
+    L.call("mzba_conv2d", 0, L.ptr(src), env_stride, L.ptr(slot), slot_stride, L.ptr(wd), L.ptr(b), L.ptr(tab), L.ptr(act),
+           A if tab is not None else 0, L.ptr(res), L.ptr(f32), B, H, W, Cin, Cout, ks, relu, L.stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    scale = ref.abs().max().item()
+    e3, e6, e32 = [(o.double() - ref).abs().max().item() for o in (out, out6, f32)]
+    d36 = (out - out6).abs().max().item()
+    msg = (f"conv_x3t B={B} Cout={Cout} {mode} ks={ks} spread={wspread}: max err vs f64 {e3 / scale:.2e} of the "
+           f"magnitude (x6 {e6 / scale:.2e}, f32 MFMA conv {e32 / scale:.2e}), vs x6 {d36 / scale:.2e}")
+    print(msg)
+    assert e3 <= 2 * e32 + 2e-7 * scale and e3 <= 3e-6 * scale, msg
+    assert d36 <= 5e-6 * scale, msg
+    outs = []
+    try:
+        for nw in (8, 4):
+            assert L.lib().mzba_conv_x6_set_waves(nw) == 0
+            outs.append(run("mzba_conv_x3_ex", wx3, (L.ptr(wsc),)))
+    finally:
+        L.lib().mzba_conv_x6_set_waves(0)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], out)
 
 
 # ------------------------------------------------------------------------------ MCTS

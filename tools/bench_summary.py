@@ -11,9 +11,11 @@ if __name__ == "__main__":
         out.append(f"match_full {d['visit_count_match_full']}")
     pp = d.get("parity_path")
     if pp:
-        vm = pp.get("vs_f32_mfma_path")
-        out.append(f"parity {pp['value']:.1f} on {pp.get('envs')} envs (frac {pp['frac']:.3f}" +
-                   (f", f32mfma {vm['value']:.1f}, x6==f32mfma {vm['visit_count_match']})" if vm else ")"))
+        out.append(f"parity[{pp.get('form', 'x6')}] {pp['value']:.1f} on {pp.get('envs')} envs (frac {pp['frac']:.3f}")
+        for k in ("vs_x6_path", "vs_f32_mfma_path"):
+            vm = pp.get(k)
+            if vm:
+                out.append(f"{k[3:]} {vm['value']:.1f} match {vm['visit_count_match']}")
     if d.get("ranks_seen") is not None:
         out.append(f"ranks_seen {d['ranks_seen']} ({d.get('backend')})")
     if d.get("cpu_baseline"):
