@@ -155,6 +155,10 @@ int mzba_conv_x3_ex(const void* in, long long env_stride, const int32_t* slot, l
                     const float* wscale, const float* bias, const float* act_bias, const int32_t* act, int A,
                     const void* res, void* out, int B, int H, int W, int Cin, int Cout, int ks, int relu,
                     hipStream_t stream);
+/* The x3 form's block pipeline (process-wide): 1 (default) each wave splits its own LDS-DMA rows of the next
+ * 32-channel block into a second plane set during the current block's k loop (one barrier per block); 0 the
+ * round-5 structure, a split phase between two barriers per block (A/B). Bit-identical. -1 on a bad value. */
+int mzba_conv_x3_set_pipe(int on);
 /* 2 (default): the pixel-tiled form at the 4x5 latent where its 16-env workgroups load the busiest CU less than the
  * pre-split tiles (the gathered / Cout 128 convs always), else the pre-split form where its staged rows fit (the f32
  * activations split once into bf16 hi / mid / lo planes while staging, 1.5x the f32 row; 8 waves x 32 channels),

@@ -471,8 +471,9 @@ constexpr int E = 16, HW = 20, H = 4, W = 5, CIN = 256, NCS = 8;
 constexpr int ROWS = HW * E;          // 320 staged rows (pixel, env)
 constexpr int PB = ROWS * 64;         // bytes per 16-bit plane of a 32-channel block
 // NP planes (3: the bf16 x6 form, 2: the fp16 x3 form), then the f32 rows of the next block: 320 x 128 B
-constexpr int raw(int np) { return np * PB; }
-constexpr int lds(int np) { return raw(np) + ROWS * 128; }  // 100 / 80 KiB
+// pipe (round 6): two plane sets, the next block's split into the idle one during the current block's k loop
+constexpr int raw(int np, bool pipe = false) { return np * PB * (pipe ? 2 : 1); }
+constexpr int lds(int np, bool pipe = false) { return raw(np, pipe) + ROWS * 128; }  // 100 / 80 KiB; piped 160 / 120
 }  // namespace x6t
 
 // the (tap, output pixel) pairs of a 3x3 conv on the 4x5 latent whose source pixel is in the image: 130 of 180
@@ -504,6 +505,7 @@ struct X6TGroups {
   int n = 0;
   int dy[60] = {}, src[60] = {}, cnt[60] = {}, out[60][3] = {}, dx[60][3] = {};
   bool last[60] = {};  // the dy row's last group
+  int last_first = 0;  // the first dy row's last group (the block's first ring reload)
 };
 // ks = 3: the 3x3 conv's groups; ks = 1: the centre tap only (a 1x1 conv: 20 groups of one pixel each)
 constexpr X6TGroups make_x6t_groups(int ks) {
@@ -529,6 +531,11 @@ constexpr X6TGroups make_x6t_groups(int ks) {
     r.last[r.n - 1] = true;
   }
   r.n = pairs == (ks == 3 ? 130 : 20) ? r.n : -1;
+  for (int i = 0; i < 60; ++i)
+    if (r.last[i]) {
+      r.last_first = i;
+      break;
+    }
   return r;
 }
 constexpr X6TGroups kGroups = make_x6t_groups(3);
@@ -568,11 +575,22 @@ MZ_DEV int tkey(int e) { return (e >> 2) & 2; }  // chunk swizzle of row 16 p + 
 
 // NW waves of 16 output channels each: 8 (128 channels per workgroup, the default) or 4 (64 channels: twice the
 // workgroups where the 8-wave grid leaves CUs idle, config 2's 1 024 envs; per wave the same arithmetic)
+#ifndef X3_ABLATE
+#define X3_ABLATE 0  // diagnostic builds only (numerically wrong): 1 no per-block staging / split, 2 no ring reloads
+#endif
+#ifndef X3_PFD
+#define X3_PFD 2  // the x3 form's fragment prefetch distance in (dy, source pixel) groups (A/B: -DX3_PFD=1)
+#endif
+
 // s_waitcnt vmcnt(N) for the ring depths below
 template <int N>
 MZ_DEV void x6t_wait_vm() {
-  static_assert(N == 18 || N == 12 || N == 3 || N == 2, "ring wait depth");
-  if constexpr (N == 18)
+  static_assert(N == 27 || N == 18 || N == 12 || N == 3 || N == 2 || N == 0, "ring wait depth");
+  if constexpr (N == 27)
+    asm volatile("s_waitcnt vmcnt(27)" ::: "memory");
+  else if constexpr (N == 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 18)
     asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
   else if constexpr (N == 12)
     asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
@@ -587,12 +605,18 @@ MZ_DEV void x6t_wait_vm() {
 // product as the three terms xh wl + xl wh + xh wh (xl wl, below 2^-22 of the product, dropped) on
 // v_mfma_f32_16x16x32_f16, f32 accumulate; the accumulator times 2^-k in the epilogue (exact). About 22 significant
 // bits per operand at half the MFMAs of x6 (tests/test_gpu_parity.py: the nets at 1e-5 of the reference)
-template <bool GA, int KSZ = 3, int NW = 8, int NP = 3>
+//
+// PIPE (round 6): no split phase between the blocks. Each wave splits only the raw rows its own LDS-DMA pieces
+// brought in (so its own vmcnt is the only wait: no barrier between the DMA and the split), into the idle one of
+// two plane sets, in a few sub-steps between the first (dy, source pixel) groups of the block before, then re-issues
+// its DMA pieces for the block after into the same rows; one barrier per block publishes the new planes. Same
+// products in the same order: bit-identical to PIPE = false.
+template <bool GA, int KSZ = 3, int NW = 8, int NP = 3, bool PIPE = false>
 __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   using namespace x6t;
   static_assert(NP == 3 || NP == 2, "x6 (bf16) or x3 (fp16)");
   using V8 = std::conditional_t<NP == 3, bf16x8, f16x8>;
-  constexpr int RAW = raw(NP);
+  constexpr int RAW = raw(NP, PIPE);
   constexpr int NT = 64 * NW;
   constexpr const X6TGroups& G = KSZ == 3 ? kGroups : kGroups1;
   constexpr int SPB = KSZ == 3 ? 3 : 1;     // ring steps per channel block (the dy rows)
@@ -616,6 +640,30 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
       const int i = wave + NW * k;
       __builtin_amdgcn_global_load_lds(src0 + (size_t)(i >> 1) * CIN + cb * 32, lds + RAW + i * 1024, 16, 0, 0);
     }
+  };
+  // one (row, 8-channel chunk) of the raw block into the planes at pdst
+  auto split_item = [&](int r, int k8, int pdst) {
+    const uint4 u0 = *reinterpret_cast<const uint4*>(lds + RAW + r * 128 + k8 * 32);
+    const uint4 u1 = *reinterpret_cast<const uint4*>(lds + RAW + r * 128 + k8 * 32 + 16);
+    uint8_t* row = lds + pdst + r * 64 + ((k8 ^ tkey(r & 15)) << 4);
+    if constexpr (NP == 3) {
+      bf16x8 h, m, l;
+      split8(u0, u1, h, m, l);
+      *reinterpret_cast<bf16x8*>(row) = h;
+      *reinterpret_cast<bf16x8*>(row + PB) = m;
+      *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+    } else {
+      f16x8 h, l;
+      split8h(u0, u1, h, l);
+      *reinterpret_cast<f16x8*>(row) = h;
+      *reinterpret_cast<f16x8*>(row + PB) = l;
+    }
+  };
+  // PIPE: sub-step u of this wave's own rows (its DMA pieces wave + NW k, 8 rows x 4 chunks each): item lane + 64 u
+  constexpr int PPW = 40 / NW, NSUB = (PPW + 1) / 2;
+  auto split_own = [&](int u, int pdst) {
+    const int idx = lane + 64 * u, k = idx >> 5;
+    if (k < PPW) split_item(8 * (wave + NW * k) + ((idx & 31) >> 2), idx & 3, pdst);
   };
   // split of the raw block into the three planes: item g = (row, 8-channel chunk)
   auto split = [&]() {
@@ -674,28 +722,42 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
 
   stage(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  split();
+  if constexpr (PIPE) {  // own rows only: no barrier before the split
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u) split_own(u, 0);
+  } else {
+    __syncthreads();
+    split();
+  }
   __syncthreads();
   stage(1);
 
-  // the lane's B fragment of source pixel ps: row 16 ps + n, chunk q of each plane
+  // the lane's B fragment of source pixel ps: row 16 ps + n, chunk q of each plane (PIPE: plane set ps0)
   const int lrow = n * 64 + ((q ^ tkey(n)) << 4);
-  auto frag = [&](int ps, V8 (&f)[NP]) {
+  auto frag = [&](int ps, V8 (&f)[NP], int pset) {
 #pragma unroll
-    for (int pt = 0; pt < NP; ++pt) f[pt] = *reinterpret_cast<const V8*>(lds + pt * PB + ps * 1024 + lrow);
+    for (int pt = 0; pt < NP; ++pt) f[pt] = *reinterpret_cast<const V8*>(lds + pset + pt * PB + ps * 1024 + lrow);
   };
 
   // one 32-channel block: the (dy, source pixel) groups (x6t::kGroups), the next group's fragment read during the
-  // current group's MFMAs; after a dy row's last group its ring slot is reloaded (step j + 2)
-  auto block = [&](int b, auto par) {
-    constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (SPB b)
-    V8 fr[2][NP];
-    frag(G.src[0], fr[0]);
+  // current group's MFMAs; after a dy row's last group its ring slot is reloaded (step j + 2).
+  // PIPE: groups 1, 3, .. (NSUB sub-steps) split block b + 1's own rows into the other plane set, after waiting for
+  // the DMA the block before issued (FIRST: the prologue's, nothing younger; else the block before's SPB ring reloads
+  // are younger), and group 2 NSUB re-issues the DMA for block b + 2
+  auto block = [&](int b, auto par, auto first) __attribute__((always_inline)) {
+    constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (SPB b) = plane set
+    constexpr bool FIRST = decltype(first)::value;
+    constexpr int PSET = PIPE ? P0 * NP * PB : 0, PNEXT = PIPE ? (P0 ^ 1) * NP * PB : 0;
+    const bool has_next = b + 1 < NCS, has_next2 = b + 2 < NCS;
+    // fragment reads PFD groups ahead: an x3 group is 6-9 MFMAs (96-144 cycles), too short to cover an LDS read
+    constexpr int PFD = NP == 2 ? X3_PFD : 1;
+    V8 fr[PFD + 1][NP];
+#pragma unroll
+    for (int j = 0; j < PFD; ++j) frag(G.src[j], fr[j], PSET);
     x6t_static_for<G.n>([&](auto I) {
       constexpr int i = decltype(I)::value;
-      constexpr int d = G.dy[i], sl = (P0 + d) & 1, cur = i & 1, cnt = G.cnt[i];
-      if (i + 1 < G.n) frag(G.src[i + 1], fr[cur ^ 1]);
+      constexpr int d = G.dy[i], sl = (P0 + d) & 1, cur = i % (PFD + 1), cnt = G.cnt[i];
+      if (i + PFD < G.n) frag(G.src[i + PFD], fr[(i + PFD) % (PFD + 1)], PSET);
       // per accumulator the small terms first (conv_x6p's order): x6 (w, x) parts (2,0) (1,1) (0,2) (1,0) (0,1)
       // (0,0); x3 (1,0) (0,1) (0,0)
       constexpr int NTM = NP == 3 ? 6 : 3;
@@ -715,18 +777,41 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
       __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, NTM * cnt, 0);
       __builtin_amdgcn_sched_barrier(0);
-      if (G.last[i]) {
+      if (G.last[i] && !(PIPE && (X3_ABLATE & 2))) {
 #pragma unroll
         for (int ti = T0; ti < T1; ++ti)
 #pragma unroll
           for (int pt = 0; pt < NP; ++pt) bq[sl][ti][pt] = wload(ti, pt, SPB * b + d + 2);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr (PIPE && !(X3_ABLATE & 1)) {
+        static_assert(!PIPE || (2 * NSUB < G.last_first && G.n > 2 * NSUB), "sub-steps before the first reload");
+        if constexpr (i % 2 == 1 && i / 2 < NSUB) {
+          if (has_next) {
+            if constexpr (i == 1) x6t_wait_vm<FIRST ? 0 : SPB * RL>();
+            split_own(i / 2, PNEXT);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (i == 2 * NSUB) {
+          if (has_next2) stage(b + 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
     });
   };
 
+  if constexpr (PIPE) {
+    // all NCS blocks unrolled: straight-line code, so the compiler's vmcnt waits for the ring count exactly (a
+    // loop back edge merged the ring's and the DMA's pending loads into vmcnt(0) waits at every block start)
+    x6t_static_for<NCS>([&](auto B) {
+      constexpr int b = decltype(B)::value;
+      block(b, std::integral_constant<int, b & 1>(), std::integral_constant<bool, b == 0>());
+      __syncthreads();
+    });
+  } else
   for (int b = 0; b < NCS; b += 2) {
-    block(b, std::integral_constant<int, 0>());  // SPB b even
+    block(b, std::integral_constant<int, 0>(), std::false_type());  // SPB b even
     // block b + 1's raw rows: wait for this wave's LDS-DMA, then every wave's, then split. The DMA is older than
     // every ring load block b issued after it (VM above: a 1x1 block's one reload only — ADVICE r5)
     x6t_wait_vm<VM>();
@@ -734,7 +819,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
     split();
     __syncthreads();
     if (b + 2 < NCS) stage(b + 2);
-    block(b + 1, std::integral_constant<int, 1>());  // SPB (b + 1) odd (SPB = 3 or 1)
+    block(b + 1, std::integral_constant<int, 1>(), std::false_type());  // SPB (b + 1) odd (SPB = 3 or 1)
     if (b + 2 < NCS) {
       x6t_wait_vm<VM>();
       __syncthreads();
@@ -848,27 +933,29 @@ int x6_halo_launch(const void* in, const void* wx, const float* bias, const void
 
 // conv_x6t_kernel's grid for t.B envs: 4-wave (64-channel) workgroups where the 8-wave grid leaves CUs idle
 // (mzba_conv_x6_set_waves: auto / 8 / 4)
-template <int NP>
+template <int NP, bool PIPE>
 void x6t_launch(const X6TArgs& t, int ks, bool ga, hipStream_t stream) {
   const long long t16 = (t.B + x6t::E - 1) / x6t::E;
   const int nw = g_x6t_waves ? g_x6t_waves : (t16 * (t.Cout / 128) < x6p_ncu() ? 4 : 8);
   const dim3 grid((unsigned)t16, (unsigned)(t.Cout / (16 * nw)));
   auto launch = [&](auto kern, int nthreads) {
     mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
-    hipLaunchKernelGGL(kern, grid, dim3(nthreads), x6t::lds(NP), stream, t);
+    hipLaunchKernelGGL(kern, grid, dim3(nthreads), x6t::lds(NP, PIPE), stream, t);
   };
   if (nw == 4) {
     if (ks == 1)
-      launch(conv_x6t_kernel<false, 1, 4, NP>, 256);
+      launch(conv_x6t_kernel<false, 1, 4, NP, PIPE>, 256);
     else
-      ga ? launch(conv_x6t_kernel<true, 3, 4, NP>, 256) : launch(conv_x6t_kernel<false, 3, 4, NP>, 256);
+      ga ? launch(conv_x6t_kernel<true, 3, 4, NP, PIPE>, 256) : launch(conv_x6t_kernel<false, 3, 4, NP, PIPE>, 256);
   } else {
     if (ks == 1)
-      launch(conv_x6t_kernel<false, 1, 8, NP>, 512);  // the reward / value heads' 1x1 ConvBlocks (never gathered)
+      launch(conv_x6t_kernel<false, 1, 8, NP, PIPE>, 512);  // the reward / value heads' 1x1 ConvBlocks (never gathered)
     else
-      ga ? launch(conv_x6t_kernel<true, 3, 8, NP>, 512) : launch(conv_x6t_kernel<false, 3, 8, NP>, 512);
+      ga ? launch(conv_x6t_kernel<true, 3, 8, NP, PIPE>, 512) : launch(conv_x6t_kernel<false, 3, 8, NP, PIPE>, 512);
   }
 }
+// x3 form: 1 (default) the pipelined split (PIPE), 0 the split phase between blocks (A/B; bit-identical)
+static int g_x3_pipe = 1;
 
 }  // namespace
 
@@ -914,7 +1001,7 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
   if (tiled) {
     X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx, bias, act_bias, act, A,
               (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin, nullptr};
-    x6t_launch<3>(t, ks, ga, stream);
+    x6t_launch<3, false>(t, ks, ga, stream);
     MZ_LAUNCH_CHECK();
     return 0;
   }
@@ -940,7 +1027,7 @@ int mzba_conv_x3_ex(const void* in, long long env_stride, const int32_t* slot, l
   MZ_CHECK_ARG((long long)B * H * W + 256 < (1LL << 31), -3);
   X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx3, bias, act_bias, act, A,
             (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin, wscale};
-  x6t_launch<2>(t, ks, ga, stream);
+  g_x3_pipe ? x6t_launch<2, true>(t, ks, ga, stream) : x6t_launch<2, false>(t, ks, ga, stream);
   MZ_LAUNCH_CHECK();
   return 0;
 }
@@ -1027,6 +1114,12 @@ extern "C" {
 int mzba_conv_x6_set_variant(int v) {
   if (v < 0 || v > 3) return -1;
   g_x6_variant = v;
+  return 0;
+}
+
+int mzba_conv_x3_set_pipe(int on) {
+  if (on != 0 && on != 1) return -1;
+  g_x3_pipe = on;
   return 0;
 }
 

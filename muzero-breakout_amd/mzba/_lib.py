@@ -43,6 +43,7 @@ SIGNATURES = {
     "mzba_conv_x6_ex": [P, LL, P, LL, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
     "mzba_conv_x3_supported": [I, I, I, I, I, I],
     "mzba_conv_x3_ex": [P, LL, P, LL, P, P, P, P, P, I, P, P, I, I, I, I, I, I, I, P],
+    "mzba_conv_x3_set_pipe": [I],
     "mzba_conv_x6_set_variant": [I],
     "mzba_conv_x6_set_waves": [I],
     "mzba_conv_lat_supported": [I, I, I, I, I],

@@ -975,14 +975,16 @@ def test_conv_x3_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks, wspr
     assert e3 <= 2 * e32 + 2e-7 * scale and e3 <= 3e-6 * scale, msg
     assert d36 <= 5e-6 * scale, msg
     outs = []
-    try:
-        for nw in (8, 4):
-            assert L.lib().mzba_conv_x6_set_waves(nw) == 0
+    try:  # 8 / 4 waves, and the pipelined split (default) against the split phase: the same sums, the same bits
+        for nw, pipe in ((8, 1), (4, 1), (8, 0), (4, 0)):
+            assert L.lib().mzba_conv_x6_set_waves(nw) == 0 and L.lib().mzba_conv_x3_set_pipe(pipe) == 0
             outs.append(run("mzba_conv_x3_ex", wx3, (L.ptr(wsc),)))
     finally:
         L.lib().mzba_conv_x6_set_waves(0)
+        L.lib().mzba_conv_x3_set_pipe(1)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], out)
+    assert all(torch.equal(o, out) for o in outs)
+    assert L.lib().mzba_conv_x3_set_pipe(2) == -1
 
 
 # ------------------------------------------------------------------------------ MCTS
