@@ -26,6 +26,7 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
 
 namespace x6 {
 constexpr int TN = 256;            // output channels per workgroup
@@ -578,6 +579,9 @@ MZ_DEV int tkey(int e) { return (e >> 2) & 2; }  // chunk swizzle of row 16 p + 
 #ifndef X3_ABLATE
 #define X3_ABLATE 0  // diagnostic builds only (numerically wrong): 1 no per-block staging / split, 2 no ring reloads
 #endif
+#ifndef X3_ASM_RING
+#define X3_ASM_RING 0  // A/B build (-DX3_ASM_RING=1): the pipelined x3 form's ring loads, DMA and raw reads as inline asm with explicit waits (+0.6 %)
+#endif
 #ifndef X3_PFD
 #define X3_PFD 2  // the x3 form's fragment prefetch distance in (dy, source pixel) groups (A/B: -DX3_PFD=1)
 #endif
@@ -634,11 +638,20 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   long long eoff = (long long)se * a.env_stride;
   if (GA && a.slot) eoff += (long long)a.slot[se] * a.slot_stride;
   const float* src0 = a.in + eoff + (lane & 7) * 4;
+  // PIPE (asm ring): the DMA as inline asm too, so every vmcnt wait of the k loop is this kernel's own (a compiler-
+  // tracked DMA made the compiler drain vmcnt — the ring loads just issued included — before each raw-row read)
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)lds;
   auto stage = [&](int cb) {
 #pragma unroll
     for (int k = 0; k < 40 / NW; ++k) {
       const int i = wave + NW * k;
-      __builtin_amdgcn_global_load_lds(src0 + (size_t)(i >> 1) * CIN + cb * 32, lds + RAW + i * 1024, 16, 0, 0);
+      if constexpr (PIPE && X3_ASM_RING) {
+        const float* g = src0 + (size_t)(i >> 1) * CIN + cb * 32;
+        const uint32_t m0v = __builtin_amdgcn_readfirstlane(lds0 + RAW + i * 1024);
+        asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0v) : "memory", "m0");
+      } else {
+        __builtin_amdgcn_global_load_lds(src0 + (size_t)(i >> 1) * CIN + cb * 32, lds + RAW + i * 1024, 16, 0, 0);
+      }
     }
   };
   // one (row, 8-channel chunk) of the raw block into the planes at pdst
@@ -664,6 +677,43 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   auto split_own = [&](int u, int pdst) {
     const int idx = lane + 64 * u, k = idx >> 5;
     if (k < PPW) split_item(8 * (wave + NW * k) + ((idx & 31) >> 2), idx & 3, pdst);
+  };
+  // the same in two halves (the reads one group ahead of the conversion); lanes past the wave's last piece redo the
+  // last one (the same values to the same addresses), so no lane branches
+  auto own_row = [&](int u, int& r, int& k8) {
+    const int idx = lane + 64 * u, k = min(idx >> 5, PPW - 1);
+    r = 8 * (wave + NW * k) + ((idx & 31) >> 2), k8 = idx & 3;
+  };
+  auto raw_read = [&](int u, u32x4 (&v)[2]) {
+    int r, k8;
+    own_row(u, r, k8);
+    if constexpr (PIPE && X3_ASM_RING) {  // untracked like the DMA (the compiler would drain vmcnt before it)
+      const uint32_t ad = lds0 + RAW + r * 128 + k8 * 32;
+      u32x4 a0, a1;
+      asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16" : "=&v"(a0), "=&v"(a1) : "v"(ad) : "memory");
+      v[0] = a0, v[1] = a1;
+    } else {
+      v[0] = *reinterpret_cast<const u32x4*>(lds + RAW + r * 128 + k8 * 32);
+      v[1] = *reinterpret_cast<const u32x4*>(lds + RAW + r * 128 + k8 * 32 + 16);
+    }
+  };
+  auto raw_split_write = [&](int u, const u32x4 (&vv)[2], int pdst) {
+    int r, k8;
+    own_row(u, r, k8);
+    const uint4 v[2] = {__builtin_bit_cast(uint4, vv[0]), __builtin_bit_cast(uint4, vv[1])};
+    uint8_t* row = lds + pdst + r * 64 + ((k8 ^ tkey(r & 15)) << 4);
+    if constexpr (NP == 3) {
+      bf16x8 h, m, l;
+      split8(v[0], v[1], h, m, l);
+      *reinterpret_cast<bf16x8*>(row) = h;
+      *reinterpret_cast<bf16x8*>(row + PB) = m;
+      *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+    } else {
+      f16x8 h, l;
+      split8h(v[0], v[1], h, l);
+      *reinterpret_cast<f16x8*>(row) = h;
+      *reinterpret_cast<f16x8*>(row + PB) = l;
+    }
   };
   // split of the raw block into the three planes: item g = (row, 8-channel chunk)
   auto split = [&]() {
@@ -699,13 +749,36 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   auto wload = [&](int ti, int part, int j) {
     j = j < SPB * NCS ? j : SPB * NCS - 1;
     const int s = KSZ == 3 ? (3 * (j % 3) + ti) * 8 + j / 3 : j;
-    return __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + s * 1024, 0));
+    if constexpr (PIPE && X3_ASM_RING) {
+      // PIPE: the ring's loads are invisible to the compiler's wait insertion (inline asm) and waited for explicitly
+      // (ring_wait): the LDS-DMA pending beside them made it wait vmcnt(0) at a row start, right after a reload
+      V8 r;
+      asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(r) : "v"(lane * 16), "s"(wrs),
+                   "s"(part * pstride + s * 1024));
+      return r;
+    } else {
+      return __builtin_bit_cast(V8, __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + s * 1024, 0));
+    }
   };
   constexpr int T0 = KSZ == 3 ? 0 : 1, T1 = KSZ == 3 ? 3 : 2;  // the dx taps the ring holds
   // ring loads a reload issues; after the LDS-DMA of the next block a 3x3 block issues three reloads, a 1x1 block one,
   // so waiting down to the youngest two (3x3) or one (1x1) reloads has the DMA complete
   constexpr int RL = (T1 - T0) * NP, VM = KSZ == 3 ? 2 * RL : RL;
   V8 bq[2][3][NP];  // [step parity][dx tap][part]
+  // PIPE (asm ring): wait until ring slot slw's loads have landed, given N vector-memory ops issued after them; the
+  // slot's registers pass through each wait, so no MFMA reading them can be scheduled above it
+  auto ring_wait = [&](auto nc, auto slc) __attribute__((always_inline)) {
+    constexpr int N = decltype(nc)::value, SLW = decltype(slc)::value;
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+#pragma unroll
+    for (int ti = T0; ti < T1; ++ti)
+#pragma unroll
+      for (int pt = 0; pt < NP; ++pt) {
+        V8 t = bq[SLW][ti][pt];
+        asm volatile("s_waitcnt vmcnt(%1)" : "+v"(t) : "n"(N));
+        bq[SLW][ti][pt] = t;
+      }
+  };
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
@@ -744,19 +817,59 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
   // PIPE: groups 1, 3, .. (NSUB sub-steps) split block b + 1's own rows into the other plane set, after waiting for
   // the DMA the block before issued (FIRST: the prologue's, nothing younger; else the block before's SPB ring reloads
   // are younger), and group 2 NSUB re-issues the DMA for block b + 2
-  auto block = [&](int b, auto par, auto first) __attribute__((always_inline)) {
+  auto block = [&](int b, auto par, auto first, auto bconst) __attribute__((always_inline)) {
     constexpr int P0 = decltype(par)::value;  // ring slot parity of the block's first step (SPB b) = plane set
     constexpr bool FIRST = decltype(first)::value;
     constexpr int PSET = PIPE ? P0 * NP * PB : 0, PNEXT = PIPE ? (P0 ^ 1) * NP * PB : 0;
     const bool has_next = b + 1 < NCS, has_next2 = b + 2 < NCS;
+
     // fragment reads PFD groups ahead: an x3 group is 6-9 MFMAs (96-144 cycles), too short to cover an LDS read
     constexpr int PFD = NP == 2 ? X3_PFD : 1;
     V8 fr[PFD + 1][NP];
 #pragma unroll
     for (int j = 0; j < PFD; ++j) frag(G.src[j], fr[j], PSET);
+    u32x4 rv[2];  // PIPE: the raw f32 chunk of the split item in flight
     x6t_static_for<G.n>([&](auto I) {
       constexpr int i = decltype(I)::value;
       constexpr int d = G.dy[i], sl = (P0 + d) & 1, cur = i % (PFD + 1), cnt = G.cnt[i];
+      // PIPE: block b + 1's own rows split in NSUB items, item u's raw reads in group 2u + 1 and its conversion +
+      // plane writes in group 2u + 2 (interleaved with that group's MFMAs); block b + 2's DMA in group 2 NSUB + 1
+      constexpr bool SPLIT = PIPE && !(X3_ABLATE & 1);
+      constexpr bool RD = SPLIT && i % 2 == 1 && i / 2 < NSUB;
+      constexpr bool CV = SPLIT && i >= 2 && i % 2 == 0 && i / 2 - 1 < NSUB;
+      static_assert(!SPLIT || (2 * NSUB + 1 < G.last_first && G.n > 2 * NSUB + 1), "split before the first reload");
+      if constexpr (PIPE && X3_ASM_RING) {  // a row's first group: its ring slot complete (counts: DESIGN §3.6)
+        constexpr int BC = decltype(bconst)::value;
+        constexpr int DMA = BC + 2 < NCS ? PPW : 0;  // this block's DMA for block b + 2 (issued in group 2 NSUB + 1)
+        using SL = std::integral_constant<int, sl>;
+        if constexpr (KSZ == 3 && i == 0) ring_wait(std::integral_constant<int, RL>(), SL());
+        if constexpr (KSZ == 3 && i == G.last_first + 1) ring_wait(std::integral_constant<int, RL + DMA>(), SL());
+        // (the last block issues no reloads past the last step: nothing younger than its row-0 reload, and in a
+        // 1x1 conv nothing younger than the block before's)
+        if constexpr (KSZ == 3 && i > G.last_first + 1 && G.last[i - 1])
+          ring_wait(std::integral_constant<int, BC + 1 < NCS ? RL : 0>(), SL());
+        if constexpr (KSZ == 1 && i == 0)
+          ring_wait(std::integral_constant<int, BC + 1 < NCS ? RL + PPW : 0>(), SL());
+      }
+      if constexpr (RD) {
+        if (has_next) {
+          if constexpr (i == 1) x6t_wait_vm<FIRST ? 0 : SPB * RL>();
+          raw_read(i / 2, rv);
+        }
+      }
+      if constexpr (CV && !(PIPE && X3_ASM_RING)) {
+        if (has_next) raw_split_write(i / 2 - 1, rv, PNEXT);
+      }
+      if constexpr (CV && PIPE && X3_ASM_RING) {
+        if (has_next) {
+          if constexpr (PIPE && X3_ASM_RING) {  // the raw reads (asm, group i - 1) landed: 2 LDS reads are younger
+            u32x4 r0 = rv[0], r1 = rv[1];
+            asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(r0), "+v"(r1));
+            rv[0] = r0, rv[1] = r1;
+          }
+          raw_split_write(i / 2 - 1, rv, PNEXT);
+        }
+      }
       if (i + PFD < G.n) frag(G.src[i + PFD], fr[(i + PFD) % (PFD + 1)], PSET);
       // per accumulator the small terms first (conv_x6p's order): x6 (w, x) parts (2,0) (1,1) (0,2) (1,0) (0,1)
       // (0,0); x3 (1,0) (0,1) (0,0)
@@ -774,29 +887,30 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
             acc[G.out[i][o]] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[sl][G.dx[i][o]][wp3[k]], fr[cur][xp3[k]],
                                                                       acc[G.out[i][o]], 0, 0, 0);
         }
-      __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, NTM * cnt, 0);
+      if constexpr (CV) {  // one MFMA, then up to 6 VALU of the split, ..., then the plane writes
+        __builtin_amdgcn_sched_group_barrier(0x100, NP + (RD ? 2 : 0), 0);
+        x6t_static_for<NTM * cnt>([&](auto) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+        });
+        __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x100, NP + (RD ? 2 : 0), 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NTM * cnt, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
-      if (G.last[i] && !(PIPE && (X3_ABLATE & 2))) {
+      // (PIPE asm ring: no reload past the last step — an untracked load whose value is dead would land in a
+      // register the compiler has meanwhile given to something else)
+      if (G.last[i] && !(PIPE && (X3_ABLATE & 2)) && !(PIPE && X3_ASM_RING && SPB * b + d + 2 >= SPB * NCS)) {
 #pragma unroll
         for (int ti = T0; ti < T1; ++ti)
 #pragma unroll
           for (int pt = 0; pt < NP; ++pt) bq[sl][ti][pt] = wload(ti, pt, SPB * b + d + 2);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (PIPE && !(X3_ABLATE & 1)) {
-        static_assert(!PIPE || (2 * NSUB < G.last_first && G.n > 2 * NSUB), "sub-steps before the first reload");
-        if constexpr (i % 2 == 1 && i / 2 < NSUB) {
-          if (has_next) {
-            if constexpr (i == 1) x6t_wait_vm<FIRST ? 0 : SPB * RL>();
-            split_own(i / 2, PNEXT);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (i == 2 * NSUB) {
-          if (has_next2) stage(b + 2);
-          __builtin_amdgcn_sched_barrier(0);
-        }
+      if constexpr (SPLIT && i == 2 * NSUB + 1) {
+        if (has_next2) stage(b + 2);
+        __builtin_amdgcn_sched_barrier(0);
       }
     });
   };
@@ -806,12 +920,18 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
     // loop back edge merged the ring's and the DMA's pending loads into vmcnt(0) waits at every block start)
     x6t_static_for<NCS>([&](auto B) {
       constexpr int b = decltype(B)::value;
-      block(b, std::integral_constant<int, b & 1>(), std::integral_constant<bool, b == 0>());
-      __syncthreads();
+      block(b, std::integral_constant<int, b & 1>(), std::integral_constant<bool, b == 0>(),
+            std::integral_constant<int, b>());
+      // publish the new planes: this wave's plane writes done, then the barrier alone (a __syncthreads() fence
+      // drained vmcnt too — the ring loads and the DMA just issued — at every block end)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
     });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing untracked in flight into the epilogue
   } else
   for (int b = 0; b < NCS; b += 2) {
-    block(b, std::integral_constant<int, 0>(), std::false_type());  // SPB b even
+    block(b, std::integral_constant<int, 0>(), std::false_type(), std::integral_constant<int, 0>());  // SPB b even
     // block b + 1's raw rows: wait for this wave's LDS-DMA, then every wave's, then split. The DMA is older than
     // every ring load block b issued after it (VM above: a 1x1 block's one reload only — ADVICE r5)
     x6t_wait_vm<VM>();
@@ -819,7 +939,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
     split();
     __syncthreads();
     if (b + 2 < NCS) stage(b + 2);
-    block(b + 1, std::integral_constant<int, 1>(), std::false_type());  // SPB (b + 1) odd (SPB = 3 or 1)
+    block(b + 1, std::integral_constant<int, 1>(), std::false_type(), std::integral_constant<int, 0>());  // SPB odd
     if (b + 2 < NCS) {
       x6t_wait_vm<VM>();
       __syncthreads();
