@@ -370,6 +370,21 @@ def conv_counters(B, H, W, kname):
     return None
 
 
+def fp16_clock_note():
+    """Config 5's fp16 dynamics net holds a lower clock than bf16 with the same instruction stream: register-only
+    16x16x32 MFMA streams with random operands (profiles/mfma_clock_dtype.json, tools/mfma_clock_dtype.hip) run
+    fp16 at ~0.94 of bf16's clock and ~0.96 of its rate — the fp16 multipliers' power, not this code."""
+    tpath = os.path.join(ROOT, "profiles", "mfma_clock_dtype.json")
+    if not os.path.exists(tpath):
+        return None
+    r = json.load(open(tpath))
+    return {"bf16_core_ghz": r["bf16"]["core_ghz_median"], "fp16_core_ghz": r["fp16"]["core_ghz_median"],
+            "fp16_over_bf16_clock": r["fp16_over_bf16_clock"], "fp16_over_bf16_rate": r["fp16_over_bf16_rate"],
+            "cause": "fp16 MFMA streams hold a lower clock than bf16 under the power limit (register-only probe, "
+                     "random operands): the fp16 step cannot match the bf16 one with the same instruction stream",
+            "source": "profiles/mfma_clock_dtype.json"}
+
+
 L2_PEAK_TBPS = 34.5  # MI355X L2 (8 XCDs x 4 MiB) aggregate read rate, MI355X_MICROARCH.md 'L2 (per XCD)'
 
 
@@ -859,7 +874,9 @@ def main():
                              "kernel_name", "mfma_busy", "clock_ghz", "wait_inst", "duration_ns",
                              "lds_bank_conflict_frac", "source")},
                          # below 16 x CUs envs a CU holds too few envs to hide its weight stream: the bound there
-                         "l2_weight_stream": l2_weight_stream(conv_ms) if tower_launch_ms else None},
+                         "l2_weight_stream": l2_weight_stream(conv_ms) if tower_launch_ms else None,
+                         # config 5: why the fp16 dynamics step runs slower than bf16 (a property of the fp16 MFMA)
+                         "fp16_clock": fp16_clock_note() if args.dyn_dtype == "fp16" else None},
             "cpu_baseline": cpu_info,
             "visit_count_match": match,
             "visit_count_match_sample": (f"{min(args.cpu_envs, B)} envs, bf16 HIP path vs the f32 CPU port (same keyed "

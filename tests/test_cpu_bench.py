@@ -121,3 +121,10 @@ def test_self_launched_ranks_report_ranks_seen(tmp_path):
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1
     assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2 and lines[0]["backend"] == "gloo"
+
+
+def test_fp16_clock_record():
+    """Config 5's fp16 note: the committed probe record has both element types and the ratios bench.py quotes."""
+    r = bench.fp16_clock_note()
+    assert r is not None and 0 < r["fp16_over_bf16_clock"] <= 1.0 and 0 < r["fp16_over_bf16_rate"] <= 1.0
+    assert os.path.exists(os.path.join(ROOT, "profiles", "r06", "r6l", "mfma_clock_dtype.jsonl"))
