@@ -616,7 +616,9 @@ MZ_DEV void x6t_wait_vm() {
 // its DMA pieces for the block after into the same rows; one barrier per block publishes the new planes. Same
 // products in the same order: bit-identical to PIPE = false.
 template <bool GA, int KSZ = 3, int NW = 8, int NP = 3, bool PIPE = false>
-__global__ __launch_bounds__(64 * NW, 1) void conv_x6t_kernel(X6TArgs a) {
+// (the 4-wave x3 form without PIPE: 80 KiB of LDS and at most 256 registers a lane, so two workgroups share a CU and
+// one's split phase and barriers overlap the other's k loop — mzba_conv_x3_set_pipe(2))
+__global__ __launch_bounds__(64 * NW, (NW == 4 && NP == 2 && !PIPE) ? 2 : 1) void conv_x6t_kernel(X6TArgs a) {
   using namespace x6t;
   static_assert(NP == 3 || NP == 2, "x6 (bf16) or x3 (fp16)");
   using V8 = std::conditional_t<NP == 3, bf16x8, f16x8>;
@@ -1054,9 +1056,9 @@ int x6_halo_launch(const void* in, const void* wx, const float* bias, const void
 // conv_x6t_kernel's grid for t.B envs: 4-wave (64-channel) workgroups where the 8-wave grid leaves CUs idle
 // (mzba_conv_x6_set_waves: auto / 8 / 4)
 template <int NP, bool PIPE>
-void x6t_launch(const X6TArgs& t, int ks, bool ga, hipStream_t stream) {
+void x6t_launch(const X6TArgs& t, int ks, bool ga, hipStream_t stream, int force_nw = 0) {
   const long long t16 = (t.B + x6t::E - 1) / x6t::E;
-  const int nw = g_x6t_waves ? g_x6t_waves : (t16 * (t.Cout / 128) < x6p_ncu() ? 4 : 8);
+  const int nw = force_nw ? force_nw : g_x6t_waves ? g_x6t_waves : (t16 * (t.Cout / 128) < x6p_ncu() ? 4 : 8);
   const dim3 grid((unsigned)t16, (unsigned)(t.Cout / (16 * nw)));
   auto launch = [&](auto kern, int nthreads) {
     mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
@@ -1147,7 +1149,10 @@ int mzba_conv_x3_ex(const void* in, long long env_stride, const int32_t* slot, l
   MZ_CHECK_ARG((long long)B * H * W + 256 < (1LL << 31), -3);
   X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx3, bias, act_bias, act, A,
             (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin, wscale};
-  g_x3_pipe ? x6t_launch<2, true>(t, ks, ga, stream) : x6t_launch<2, false>(t, ks, ga, stream);
+  if (g_x3_pipe == 2)
+    x6t_launch<2, false>(t, ks, ga, stream, 4);  // two 4-wave workgroups per CU
+  else
+    g_x3_pipe ? x6t_launch<2, true>(t, ks, ga, stream) : x6t_launch<2, false>(t, ks, ga, stream);
   MZ_LAUNCH_CHECK();
   return 0;
 }
@@ -1238,7 +1243,7 @@ int mzba_conv_x6_set_variant(int v) {
 }
 
 int mzba_conv_x3_set_pipe(int on) {
-  if (on != 0 && on != 1) return -1;
+  if (on < 0 || on > 2) return -1;
   g_x3_pipe = on;
   return 0;
 }

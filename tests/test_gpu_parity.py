@@ -976,7 +976,7 @@ def test_conv_x3_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks, wspr
     assert d36 <= 5e-6 * scale, msg
     outs = []
     try:  # 8 / 4 waves, and the pipelined split (default) against the split phase: the same sums, the same bits
-        for nw, pipe in ((8, 1), (4, 1), (8, 0), (4, 0)):
+        for nw, pipe in ((8, 1), (4, 1), (8, 0), (4, 0), (0, 2)):
             assert L.lib().mzba_conv_x6_set_waves(nw) == 0 and L.lib().mzba_conv_x3_set_pipe(pipe) == 0
             outs.append(run("mzba_conv_x3_ex", wx3, (L.ptr(wsc),)))
     finally:
@@ -984,7 +984,7 @@ def test_conv_x3_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks, wspr
         L.lib().mzba_conv_x3_set_pipe(1)
     torch.cuda.synchronize()
     assert all(torch.equal(o, out) for o in outs)
-    assert L.lib().mzba_conv_x3_set_pipe(2) == -1
+    assert L.lib().mzba_conv_x3_set_pipe(3) == -1
 
 
 # ------------------------------------------------------------------------------ MCTS

@@ -43,9 +43,9 @@ def main():
     fl = 2.0 * B * H * W * C * 9 * C
     L.call("mzba_conv_x6_set_variant", 3)
     for rep in range(2):
-        for form in ("x3", "x3nopipe", "x6"):
+        for form in ("x3", "x3nopipe", "x3dual", "x6"):
             if form.startswith("x3") and hasattr(L.lib(), "mzba_conv_x3_set_pipe"):
-                L.call("mzba_conv_x3_set_pipe", int(form == "x3"))
+                L.call("mzba_conv_x3_set_pipe", {"x3": 1, "x3nopipe": 0, "x3dual": 2}[form])
             for res in (None, x):
                 if form.startswith("x3"):
                     fn = lambda: L.call("mzba_conv_x3_ex", L.ptr(x), H * W * C, None, 0, L.ptr(wx3), L.ptr(wsc), L.ptr(b),  # noqa
