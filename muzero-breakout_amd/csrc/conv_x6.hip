@@ -36,13 +36,14 @@ constexpr int LDS_MAX = 160 * 1024;
 
 struct X6Args {
   const float* in;     // [M][Cin] f32
-  const bf16_t* wx;    // [3 parts][Cout / 16][9 Cin / 32][64][8]
+  const bf16_t* wx;    // [3 parts][Cout / 16][9 Cin / 32][64][8] (x3: [2 fp16 parts]...)
   const float* bias;   // [Cout]
   const float* res;    // optional [M][Cout] f32
   float* out;          // [M][Cout] f32
   int M, H, W, Cin, Cout, relu;
   int HALO, NI, ZOFF;  // halo rows each side, LDS-DMA 1-KiB blocks of the staging, byte offset of the zero block
   long long part;      // elements per weight part
+  const float* wscale = nullptr;  // x3 (conv_x6p_kernel NP = 2): per output channel 2^-k of the weights' scaling
 };
 
 // bf16 split of 8 f32 (two 16-B halves): hi, mid, lo with x == hi + mid + lo up to the lo part's rounding
@@ -273,11 +274,15 @@ MZ_DEV int pkey(int r) { return ((r << 1) & 6) | (((r >> 2) & 1) * 9); }  // = c
 // the input channels staged in NBLK blocks of CIN / NBLK (round 5: the 16x20 Cin-256 convs in two 128-channel blocks,
 // so a 160-pixel tile's 1.5x rows fit — one block took 48-pixel tiles there, each streaming all 3.5 MB of weight
 // parts, the L2 weight stream then bounding it); NBLK > 1 sums (block, tap, channel step) in that order.
-template <int CIN, int TM, int CT = 2, int NBLK = 1>
+// NP = 2 (round 6): the split-fp16 x3 form of conv_x6t (§3.6 of DESIGN.md) on these tiles — two fp16 planes per row,
+// three fp16 MFMAs per product, weights scaled by 2^k per output channel (undone in the epilogue): the f32 path's
+// 16x20 / 8x10 representation convs.
+template <int CIN, int TM, int CT = 2, int NBLK = 1, int NP = 3>
 __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
+  using V8 = std::conditional_t<NP == 3, bf16x8, f16x8>;
   constexpr int CB = CIN / NBLK;     // channels per staged block
-  constexpr int PB = CB * 2;         // bytes per plane row (bf16)
-  constexpr int RB = 3 * PB;         // bytes per staged row: hi | mid | lo
+  constexpr int PB = CB * 2;         // bytes per plane row (bf16 / fp16)
+  constexpr int RB = NP * PB;        // bytes per staged row: hi | mid | lo (x3: hi | lo)
   constexpr int NC8 = CB / 8;        // 8-channel chunks per row
   constexpr int NCS = CB / 32;       // 32-channel k steps per tap and block
   constexpr int MT = TM / 16;        // pixel tiles per wave: all of the workgroup's
@@ -314,14 +319,14 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
     j = j < nsteps ? j : nsteps - 1;
     const int blk = j / (9 * NCS), r = j - blk * 9 * NCS, t = r / NCS, c = r - t * NCS;
     const int s = t * (CIN / 32) + blk * NCS + c;
-    return __builtin_bit_cast(bf16x8,
+    return __builtin_bit_cast(V8,
                               __builtin_amdgcn_raw_buffer_load_b128(wrs, lane * 16, part * pstride + (ct * KS + s) * 1024, 0));
   };
-  bf16x8 bq[2][3][CT];
+  V8 bq[2][NP][CT];
 #pragma unroll
   for (int cc = 0; cc < 2; ++cc)
 #pragma unroll
-    for (int pt = 0; pt < 3; ++pt)
+    for (int pt = 0; pt < NP; ++pt)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) bq[cc][pt][ct] = wload(ct, pt, cc);
 
@@ -351,12 +356,19 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
         const int g = g0 + u * x6::NT + tid;
         if (g < items) {
           const int r = g / NC8, s8 = g - r * NC8;
-          bf16x8 h, mm, l;
-          split8(v[u][0], v[u][1], h, mm, l);
           uint8_t* row = lds + r * RB + ((s8 ^ pkey(r)) << 4);
-          *reinterpret_cast<bf16x8*>(row) = h;
-          *reinterpret_cast<bf16x8*>(row + PB) = mm;
-          *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+          if constexpr (NP == 3) {
+            bf16x8 h, mm, l;
+            split8(v[u][0], v[u][1], h, mm, l);
+            *reinterpret_cast<bf16x8*>(row) = h;
+            *reinterpret_cast<bf16x8*>(row + PB) = mm;
+            *reinterpret_cast<bf16x8*>(row + 2 * PB) = l;
+          } else {
+            f16x8 h, l;
+            split8h(v[u][0], v[u][1], h, l);
+            *reinterpret_cast<f16x8*>(row) = h;
+            *reinterpret_cast<f16x8*>(row + PB) = l;
+          }
         }
       }
     }
@@ -364,14 +376,14 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
 
   // fragment of pixel tile mi, channel step c at tap t: chunk 4c + q of the three planes of its row (the zero row
   // for a tap leaving the image; its bank slots collide with at most a few lanes', measured neutral for conv_x6)
-  auto frag = [&](int t, int c, int mi, bf16x8 (&f)[3]) {
+  auto frag = [&](int t, int c, int mi, V8 (&f)[NP]) {
     const int dy = t / 3 - 1, dx = t % 3 - 1;
     const uint32_t need = 16u | (dy < 0 ? 1u : 0u) | (dy > 0 ? 2u : 0u) | (dx < 0 ? 4u : 0u) | (dx > 0 ? 8u : 0u);
     const bool ok = ((okw[mi >> 2] >> (8 * (mi & 3))) & need) == need;
     const int r = prow0 + 16 * mi + dy * a.W + dx;
     const int base = ok ? r * RB + (((4 * c + q) ^ pkey(r)) << 4) : a.ZOFF;
 #pragma unroll
-    for (int pt = 0; pt < 3; ++pt) f[pt] = *reinterpret_cast<const bf16x8*>(lds + base + pt * PB);
+    for (int pt = 0; pt < NP; ++pt) f[pt] = *reinterpret_cast<const V8*>(lds + base + pt * PB);
   };
   constexpr int NF = MT * NCS;
   int j = 0;
@@ -385,7 +397,7 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
     }
     stage(blk);
     __syncthreads();
-    bf16x8 fr[2][3];  // rolling: fragment i + 1 read during fragment i's MFMAs
+    V8 fr[2][NP];  // rolling: fragment i + 1 read during fragment i's MFMAs
     frag(0, 0, 0, fr[0]);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
@@ -402,19 +414,26 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
             frag(t, nx / MT, nx % MT, fr[nxt]);
           else if (t < 8)
             frag(t + 1, 0, 0, fr[nxt]);
-          const bf16x8* xs[6] = {&fr[cur][0], &fr[cur][1], &fr[cur][2], &fr[cur][0], &fr[cur][1], &fr[cur][0]};
-          constexpr int wp[6] = {2, 1, 0, 1, 0, 0};  // per accumulator the small terms first, as conv_x6_kernel
+          // per accumulator the small terms first, as conv_x6_kernel: x6 (w, x) parts (2,0) (1,1) (0,2) (1,0) (0,1)
+          // (0,0); x3 (1,0) (0,1) (0,0)
+          constexpr int NTM = NP == 3 ? 6 : 3;
+          constexpr int wp6[6] = {2, 1, 0, 1, 0, 0}, xp6[6] = {0, 1, 2, 0, 1, 0};
+          constexpr int wp3[3] = {1, 0, 0}, xp3[3] = {0, 1, 0};
 #pragma unroll
-          for (int k = 0; k < 6; ++k)
+          for (int k = 0; k < NTM; ++k)
 #pragma unroll
-            for (int ct = 0; ct < CT; ++ct)
-              acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][wp[k]][ct], *xs[k], acc[mi][ct], 0, 0, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 6 * CT, 0);
+            for (int ct = 0; ct < CT; ++ct) {
+              if constexpr (NP == 3)
+                acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bq[sl][wp6[k]][ct], fr[cur][xp6[k]], acc[mi][ct], 0, 0, 0);
+              else
+                acc[mi][ct] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bq[sl][wp3[k]][ct], fr[cur][xp3[k]], acc[mi][ct], 0, 0, 0);
+            }
+          __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, NTM * CT, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
 #pragma unroll
-        for (int pt = 0; pt < 3; ++pt)
+        for (int pt = 0; pt < NP; ++pt)
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct) bq[sl][pt][ct] = wload(ct, pt, sn);
         __builtin_amdgcn_sched_barrier(0);
@@ -428,6 +447,14 @@ __global__ __launch_bounds__(x6::NT, 1) void conv_x6p_kernel(X6Args a) {
   float4 bb[CT];
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct) bb[ct] = *reinterpret_cast<const float4*>(a.bias + nb + ct * 16 + 4 * q);
+  if constexpr (NP == 2) {  // undo the weights' 2^k (exact)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const float4 sc = *reinterpret_cast<const float4*>(a.wscale + nb + ct * 16 + 4 * q);
+#pragma unroll
+      for (int mi = 0; mi < MT; ++mi) acc[mi][ct] *= f32x4{sc.x, sc.y, sc.z, sc.w};
+    }
+  }
   const float lo = a.relu ? 0.f : -__builtin_inff();
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
@@ -1052,6 +1079,8 @@ int x6_geometry(int W, int Cin, X6Args& g) {
 
 int x6_halo_launch(const void* in, const void* wx, const float* bias, const void* res, void* out, int B, int H, int W,
                    int Cin, int Cout, int relu, hipStream_t stream);
+int x3_halo_launch(const void* in, const void* wx3, const float* wscale, const float* bias, const void* res, void* out,
+                   int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream, bool dry = false);
 
 // conv_x6t_kernel's grid for t.B envs: 4-wave (64-channel) workgroups where the 8-wave grid leaves CUs idle
 // (mzba_conv_x6_set_waves: auto / 8 / 4)
@@ -1135,7 +1164,13 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
 // pack_lat16 packing back to back (agent.py split_pack_x3), wscale[Cout] = 2^-k.
 int mzba_conv_x3_supported(int H, int W, int Cin, int Cout, int ks, int gather) {
   if (ks == 1 && gather) return 0;
-  return (ks == 3 || ks == 1) && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128) ? 1 : 0;
+  if ((ks == 3 || ks == 1) && H == x6t::H && W == x6t::W && Cin == x6t::CIN && (Cout == 256 || Cout == 128)) return 1;
+  // the pre-split tiles (conv_x6p_kernel<.., NP = 2>): contiguous 3x3 convs where an x3 instance exists (the 16x20 and
+  // 8x10 representation convs)
+  return ks == 3 && !gather && H >= 2 && W >= 2 &&
+                 x3_halo_launch(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 1, H, W, Cin, Cout, 1, nullptr, true) == 0
+             ? 1
+             : 0;
 }
 
 int mzba_conv_x3_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx3,
@@ -1147,6 +1182,11 @@ int mzba_conv_x3_ex(const void* in, long long env_stride, const int32_t* slot, l
   const bool ga = slot || act_bias || env_stride != (long long)H * W * Cin;
   MZ_CHECK_ARG(mzba_conv_x3_supported(H, W, Cin, Cout, ks, ga ? 1 : 0), -2);
   MZ_CHECK_ARG((long long)B * H * W + 256 < (1LL << 31), -3);
+  if (!(H == x6t::H && W == x6t::W)) {
+    const int rc = x3_halo_launch(in, wx3, wscale, bias, res, out, B, H, W, Cin, Cout, relu, stream);
+    if (rc == 0) MZ_LAUNCH_CHECK();
+    return rc;
+  }
   X6TArgs t{(const float*)in, env_stride, slot, slot_stride, (const bf16_t*)wx3, bias, act_bias, act, A,
             (const float*)res, (float*)out, B, Cout, relu, (long long)Cout * ks * ks * Cin, wscale};
   if (g_x3_pipe == 2)
@@ -1230,6 +1270,57 @@ int x6_halo_launch(const void* in, const void* wx, const float* bias, const void
   else
     tm == 96 ? launch(conv_x6_kernel<128, 96>) : launch(conv_x6_kernel<128, 64>);
   MZ_LAUNCH_CHECK();
+  return 0;
+}
+
+// the x3 form on the pre-split tiles, with a batch-independent choice: W >= 16 (the 16x20 representation convs) 160-pixel
+// tiles (Cin 256 in two 128-channel blocks; Cin 128 at Cout 256 or 128); otherwise Cin 256, Cout % 256 == 0 on
+// x6p_geometry's tile (two fp16 planes per row instead of three bf16: the x6 tile always fits). -2 elsewhere (dry: the
+// check only)
+int x3_halo_launch(const void* in, const void* wx3, const float* wscale, const float* bias, const void* res, void* out,
+                   int B, int H, int W, int Cin, int Cout, int relu, hipStream_t stream, bool dry) {
+  const long long M = (long long)B * H * W;
+  MZ_CHECK_ARG(M + 256 < (1LL << 31), -3);
+  X6Args ap{(const float*)in, (const bf16_t*)wx3, bias, (const float*)res, (float*)out, (int)M, H, W, Cin, Cout, relu};
+  ap.part = (long long)Cout * 9 * Cin;
+  ap.wscale = wscale;
+  X6PGeo geo{};
+  if (W >= 16) {
+    const bool ok = (Cin == 256 && Cout % 256 == 0) || (Cin == 128 && (Cout % 256 == 0 || Cout == 128));
+    geo.tm = 160, geo.nblk = Cin == 256 ? 2 : 1, geo.ct = Cout % 256 == 0 ? 2 : 1;
+    if (!ok || (160 + 2 * (W + 1) + 1) * 2 * (Cin / geo.nblk) * 2 > x6::LDS_MAX) return -2;
+    ap.HALO = W + 1, ap.NI = 0;
+  } else {
+    if (Cin != 256 || Cout % 256 != 0) return -2;
+    geo = x6p_geometry(W, Cin, Cout, M, ap);
+    if (!geo.tm || geo.ct != 2 || geo.nblk != 1) return -2;
+  }
+  if (dry) return 0;
+  const int tm = geo.tm;
+  ap.ZOFF = (tm + 2 * (W + 1)) * 2 * (Cin / geo.nblk) * 2;  // HR rows of hi | lo
+  const int ldsp = ap.ZOFF + 2 * (Cin / geo.nblk) * 2;
+  const dim3 gridp((unsigned)((M + tm - 1) / tm), (unsigned)(Cout / (128 * geo.ct)));
+  auto launchp = [&](auto kern) {
+    mz_set_lds_max_once(reinterpret_cast<const void*>(kern), x6::LDS_MAX);
+    hipLaunchKernelGGL(kern, gridp, dim3(x6::NT), ldsp, stream, ap);
+  };
+  if (tm == 160) {
+    if (Cin == 256)
+      launchp(conv_x6p_kernel<256, 160, 2, 2, 2>);
+    else if (geo.ct == 2)
+      launchp(conv_x6p_kernel<128, 160, 2, 1, 2>);
+    else
+      launchp(conv_x6p_kernel<128, 160, 1, 1, 2>);
+  } else {
+    switch (tm) {
+      case 128: launchp(conv_x6p_kernel<256, 128, 2, 1, 2>); break;
+      case 112: launchp(conv_x6p_kernel<256, 112, 2, 1, 2>); break;
+      case 96: launchp(conv_x6p_kernel<256, 96, 2, 1, 2>); break;
+      case 80: launchp(conv_x6p_kernel<256, 80, 2, 1, 2>); break;
+      case 64: launchp(conv_x6p_kernel<256, 64, 2, 1, 2>); break;
+      default: launchp(conv_x6p_kernel<256, 48, 2, 1, 2>); break;
+    }
+  }
   return 0;
 }
 }  // namespace

@@ -947,7 +947,7 @@ def test_conv_x3_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks, wspr
     if relu:
         ref = torch.relu(ref)
     assert L.lib().mzba_conv_x3_supported(H, W, Cin, Cout, ks, int(mode == "gather"))
-    assert not L.lib().mzba_conv_x3_supported(H, W, Cin, Cout, 1, 1) and not L.lib().mzba_conv_x3_supported(8, 10, Cin, Cout, 3, 0)
+    assert not L.lib().mzba_conv_x3_supported(H, W, Cin, Cout, 1, 1) and not L.lib().mzba_conv_x3_supported(8, 10, 128, 256, 3, 0)
 
     def run(fn, wts, extra=()):
         o = torch.full((B, H, W, Cout), float("nan"), device=dev)
@@ -985,6 +985,55 @@ def test_conv_x3_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks, wspr
     torch.cuda.synchronize()
     assert all(torch.equal(o, out) for o in outs)
     assert L.lib().mzba_conv_x3_set_pipe(3) == -1
+
+
+@pytest.mark.parametrize("B,H,W,Cin,Cout,relu,with_res", [(7, 16, 20, 128, 256, 1, True), (512, 16, 20, 256, 256, 1, True),
+                                                      (300, 16, 20, 128, 128, 1, False), (37, 8, 10, 256, 256, 0, False),
+                                                      (1000, 8, 10, 256, 256, 1, True)])
+def test_conv_x3_presplit_tiles_as_close_to_exact_as_f32(B, H, W, Cin, Cout, relu, with_res):
+    """Round 6: the x3 form on the pre-split halo tiles (conv_x6p_kernel<.., NP = 2>, the f32 path's 16x20 and 8x10
+    representation convs through mzba_conv_x3_ex) against an f64 conv of the same f32 operands: within 2x the
+    f32-input MFMA conv's error + 2e-7 and within 3e-6 of the magnitude, within 5e-6 of the x6 form; ragged tiles,
+    tiles crossing envs, every tap that leaves the image, weights differing by 2^6 between output channels."""
+    from mzba import _lib as L
+    from mzba.agent import split_pack_x6, split_pack_x3
+    assert L.lib().mzba_conv_x3_supported(H, W, Cin, Cout, 3, 0) and not L.lib().mzba_conv_x3_supported(H, W, Cin, Cout, 3, 1)
+    g = torch.Generator(device="cuda").manual_seed(B + Cin + W + 3)
+    dev = torch.device("cuda")
+    x = torch.rand(B, H, W, Cin, generator=g, device=dev)
+    w = torch.randn(Cout, 3, 3, Cin, generator=g, device=dev) / (Cin * 9) ** 0.5
+    w = w * torch.exp2(torch.rand(Cout, 1, 1, 1, generator=g, device=dev) * 6 - 3)
+    b = torch.randn(Cout, generator=g, device=dev) * 0.1
+    res = torch.rand(B, H, W, Cout, generator=g, device=dev) if with_res else None
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), b.double(),
+                                     padding=1).permute(0, 2, 3, 1)
+    if with_res:
+        ref = ref + res.double()
+    if relu:
+        ref = torch.relu(ref)
+    wn = w.cpu().numpy().reshape(Cout, -1)
+    wx3, wsc = split_pack_x3(wn, Cout, 3, Cin)
+    wx3, wsc = wx3.cuda(), wsc.cuda()
+    wx = split_pack_x6(wn, Cout, 3, Cin).cuda()
+    out = torch.full((B, H, W, Cout), float("nan"), device=dev)
+    L.call("mzba_conv_x3_ex", L.ptr(x), H * W * Cin, None, 0, L.ptr(wx3), L.ptr(wsc), L.ptr(b), None, None, 0, L.ptr(res),
+           L.ptr(out), B, H, W, Cin, Cout, 3, relu, L.stream())
+    out6 = torch.full_like(out, float("nan"))
+    L.call("mzba_conv_x6", L.ptr(x), L.ptr(wx), L.ptr(b), L.ptr(res), L.ptr(out6), B, H, W, Cin, Cout, relu, L.stream())
+    f32 = torch.empty(B, H, W, Cout, device=dev)
+    wd = w.reshape(Cout, -1).contiguous()
+    L.call("mzba_conv2d", 0, L.ptr(x), H * W * Cin, None, 0, L.ptr(wd), L.ptr(b), None, None, 0, L.ptr(res), L.ptr(f32),
+           B, H, W, Cin, Cout, 3, relu, L.stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    scale = ref.abs().max().item()
+    e3, e6, e32 = [(o.double() - ref).abs().max().item() for o in (out, out6, f32)]
+    d36 = (out - out6).abs().max().item()
+    msg = (f"conv_x3 pre-split {B}x{H}x{W} {Cin}->{Cout}: max err vs f64 {e3 / scale:.2e} of the magnitude (x6 "
+           f"{e6 / scale:.2e}, f32 MFMA conv {e32 / scale:.2e}), vs x6 {d36 / scale:.2e}")
+    print(msg)
+    assert e3 <= 2 * e32 + 2e-7 * scale and e3 <= 3e-6 * scale, msg
+    assert d36 <= 5e-6 * scale, msg
 
 
 # ------------------------------------------------------------------------------ MCTS
