@@ -429,21 +429,23 @@ def tower_kernel_name(B, fp16=False):
 
 
 def x6_flops(p, H, W, S, x3=False):
-    """Per env-step FLOPs of the f32 parity path's convs by the form they run in: split-fp16 x3 products (x3: the 4x5
-    latent's convs PackedNets gave 'wx3' — the towers, the dynamics' first conv, the heads' convs), split-bf16 x6
-    products (conv_x6: the layers with 'wx' and no x3 form in use — the representation's Cout-256 3x3 convs; all the
-    latent ones too without x3) and the rest (f32-input MFMA convs and heads), at this geometry: (x3, x6, rest)."""
+    """Per env-step FLOPs of the f32 parity path's convs by the form they run in: split-fp16 x3 products (x3: the convs
+    PackedNets gave 'wx3' — the 4x5 latent's towers, dynamics' first conv and heads' convs, and the representation's
+    16x20 / 8x10 3x3 convs on the pre-split tiles), split-bf16 x6 products (conv_x6: the layers with 'wx' and no x3
+    form in use) and the rest (f32-input MFMA convs and heads), at this geometry: (x3, x6, rest)."""
     conv = lambda c, hw: 2.0 * hw * c["cout"] * c["ks"] ** 2 * c["cin"]  # noqa: E731
+    lat = {"x3": 0.0, "x6": 0.0}
     x6, hh, ww = 0.0, H, W
     for kind, layer in p.rep:
         if kind == "pool":
             hh, ww = hh // 2, ww // 2
             continue
         for c in ([layer] if kind == "conv" else list(layer)):
-            if c.get("wx") is not None:
+            if x3 and c.get("wx3") is not None:  # round 6: the representation's convs on the x3 pre-split tiles
+                lat["x3"] += conv(c, hh * ww)
+            elif c.get("wx") is not None:
                 x6 += conv(c, hh * ww)
     hw = p.lh * p.lw
-    lat = {"x3": 0.0, "x6": 0.0}
 
     def add(c, n):
         if x3 and c.get("wx3") is not None:
