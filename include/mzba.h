@@ -148,8 +148,9 @@ int mzba_conv_x6_ex(const void* in, long long env_stride, const int32_t* slot, l
  * terms xh wl + xl wh + xh wh on fp16 MFMAs with f32 accumulation — about 22 significant bits per operand, half the
  * MFMAs of the x6 form. wx3 = the two fp16 parts of w 2^k (k per output channel: max |w 2^k| in [2^14, 2^15)), each in
  * pack_lat16's packing, back to back; wscale[Cout] = 2^-k. Activations must stay below 65520 in magnitude (else the
- * output turns NaN). Same shapes, gather and action-bias contract as mzba_conv_x6_ex at the 4x5 latent
- * (mzba_conv_x3_supported). */
+ * output turns non-finite). Same shapes, gather and action-bias contract as mzba_conv_x6_ex at the 4x5 latent; and
+ * contiguous 3x3 convs on the pre-split halo tiles (160-pixel tiles at W >= 16 for Cin 256 / 128; Cin 256, Cout % 256
+ * == 0 elsewhere: the 16x20 and 8x10 representation convs) (mzba_conv_x3_supported). */
 int mzba_conv_x3_supported(int H, int W, int Cin, int Cout, int ks, int gather);
 int mzba_conv_x3_ex(const void* in, long long env_stride, const int32_t* slot, long long slot_stride, const void* wx3,
                     const float* wscale, const float* bias, const float* act_bias, const int32_t* act, int A,

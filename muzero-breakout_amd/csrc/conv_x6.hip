@@ -64,7 +64,7 @@ MZ_DEV void split8(const uint4& u0, const uint4& u1, bf16x8& h, bf16x8& m, bf16x
 
 // fp16 split of 8 f32 for the x3 form: hi = fp16(x), lo = fp16(x - hi) (x - hi is exact in f32; |lo| <= 2^-11 |x|,
 // lo's own rounding <= 2^-22 |x| while lo is normal, i.e. |x| >= 2^-3; below, absolute 2^-25). |x| < 65520 or
-// hi = inf and the output turns NaN (loud, never silently wrong)
+// hi = inf and the output turns non-finite (loud, never silently wrong)
 MZ_DEV void split8h(const uint4& u0, const uint4& u1, f16x8& h, f16x8& l) {
   const float x[8] = {__uint_as_float(u0.x), __uint_as_float(u0.y), __uint_as_float(u0.z), __uint_as_float(u0.w),
                       __uint_as_float(u1.x), __uint_as_float(u1.y), __uint_as_float(u1.z), __uint_as_float(u1.w)};

@@ -987,6 +987,51 @@ def test_conv_x3_pixel_tiled_is_as_close_to_exact_as_f32(B, Cout, mode, ks, wspr
     assert L.lib().mzba_conv_x3_set_pipe(3) == -1
 
 
+def test_f32_runner_defaults_to_x3_and_the_switch_reaches_new_runners():
+    """The f32 agent's runners take the x3 convs by default (NetPack int use_x3 = 1) wherever a conv carries x3 weights
+    — the latent towers, dyn0, the heads' convs and the representation's 3x3 convs — and NetPack.set_int('use_x3', 0)
+    before a batch's first op gives that batch's runner the x6 convs."""
+    from mzba.agent import MuZeroAgent, NetRunner
+    cfg = default_config()
+    ag = MuZeroAgent(cfg["model"], dtype="f32")
+    ag.load_state_dict(init_state_dict(cfg["model"], 1))
+    p = ag.packed
+    assert all(c.get("wx3") is not None for blk in p.dyn + p.pred for c in blk)
+    rep_3x3 = [c for kind, layer in p.rep if kind != "pool" for c in ([layer] if kind == "conv" else list(layer))
+               if c["ks"] == 3 and c["cout"] % 128 == 0 and c["cin"] in (128, 256)]
+    assert rep_3x3 and all(c.get("wx3") is not None for c in rep_3x3)
+    assert NetRunner(p, 8, 16, 20).use_x3
+    p.native.set_int("use_x3", 0)
+    assert not NetRunner(p, 9, 16, 20).use_x3
+    p.native.set_int("use_x3", 1)
+
+
+def test_conv_x3_out_of_range_activation_is_loud():
+    """The x3 form's one precondition: activations below 65 520 in magnitude (fp16's range). Past it the
+    hi part is inf and the products turn non-finite (inf / NaN), so a violation shows as non-finite outputs at every
+    position whose receptive field holds the value — never as a finite wrong number — while every other env is
+    unaffected."""
+    from mzba import _lib as L
+    from mzba.agent import split_pack_x3
+    B, H, W, C = 40, 4, 5, 256
+    g = torch.Generator(device="cuda").manual_seed(5)
+    dev = torch.device("cuda")
+    x = torch.rand(B, H, W, C, generator=g, device=dev)
+    x[3, 1, 2, 7] = 7.0e4
+    w = torch.randn(C, 3, 3, C, generator=g, device=dev) / 48.0
+    b = torch.zeros(C, device=dev)
+    wx3, wsc = split_pack_x3(w.cpu().numpy().reshape(C, -1), C, 3, C)
+    wx3, wsc = wx3.cuda(), wsc.cuda()
+    out = torch.zeros(B, H, W, C, device=dev)
+    L.call("mzba_conv_x3_ex", L.ptr(x), H * W * C, None, 0, L.ptr(wx3), L.ptr(wsc), L.ptr(b), None, None, 0, None,
+           L.ptr(out), B, H, W, C, C, 3, 0, L.stream())
+    torch.cuda.synchronize()
+    assert not torch.isfinite(out[3, 0:3, 1:4]).any()  # the 3x3 neighbourhood of pixel (1, 2)
+    mask = torch.ones(B, dtype=torch.bool, device=dev)
+    mask[3] = False
+    assert torch.isfinite(out[mask]).all()
+
+
 @pytest.mark.parametrize("B,H,W,Cin,Cout,relu,with_res", [(7, 16, 20, 128, 256, 1, True), (512, 16, 20, 256, 256, 1, True),
                                                       (300, 16, 20, 128, 128, 1, False), (37, 8, 10, 256, 256, 0, False),
                                                       (1000, 8, 10, 256, 256, 1, True)])
