@@ -871,6 +871,221 @@ static bool wgrad_img_plan(int B, int Bseg, int H, int W, int Cin, int Cout, WgP
   return true;
 }
 
+// bf16 3x3 weight gradient over pixel rows (round 6): the whole-image kernel's tiling (64 co x 64 ci,
+// all 9 taps, 8 waves) without the zero border. The contraction index k runs over the E * HW real
+// pixels of a stage — row e * HW + p of dY and of X, which is how E consecutive envs already lie in
+// HBM — padded to a multiple of 32 with zero dY rows. Tap (dy, dx) of k row r is X row r + dy * W + dx,
+// or the zero row XR where the tap leaves the image: each lane hands its own row address to the
+// transposed read, with the 9-tap validity of its two k rows from a per-workgroup mask table (the same
+// for every stage). Against the bordered kernel: 20 instead of 28 k per 4x5 image (the border columns'
+// MFMAs and staging rows are gone), twice the envs per stage (10 k steps between barriers instead of 7),
+// no per-step divisions, and an XCD-aware workgroup order (the 16 tiles of one env range share an L2).
+struct WgPx {
+  int B, H, W, Cin, Cout, E, KS, XR, stages_per_split, Bseg, tiles, remap;
+  const bf16_t* xs[WG_MAXSEG];
+  const bf16_t* dys[WG_MAXSEG];
+};
+
+__global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __restrict__ part,
+                                                              float* __restrict__ bpart) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds_img[];
+  bf16_t* ldy = lds_img;                                      // [KS][WI_LD]
+  bf16_t* lx = lds_img + (size_t)a.KS * WI_LD;                // [XR + 1][WI_LD], row XR = zeros
+  uint16_t* tmask = reinterpret_cast<uint16_t*>(lx + (size_t)(a.XR + 1) * WI_LD);  // [KS]
+  __shared__ float bred[WI_NT / 8][64];
+  const int H = a.H, W = a.W, HW = H * W, NR = a.E * HW;
+  const int nci = (a.Cin + 63) / 64;
+  // workgroup -> (tile, split). remap: workgroup ids congruent mod 8 run on one XCD; they take
+  // consecutive split-major work items, so the tiles of one env range read its X / dY through one L2
+  int tile = blockIdx.x, split = blockIdx.y;
+  if (a.remap) {
+    const int L = blockIdx.x + blockIdx.y * gridDim.x, per = (gridDim.x * gridDim.y) >> 3;
+    const int Lp = (L & 7) * per + (L >> 3);
+    tile = Lp % a.tiles;
+    split = Lp / a.tiles;
+  }
+  const int cit = tile % nci, cot = tile / nci;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tg = wave >> 2, wr = (wave >> 1) & 1, wc = wave & 1;
+  const int tap0 = 5 * tg, ntap = tg ? 4 : 5;
+  const int ch = tid & 7;
+  const int co_s = cot * 64 + ch * 8, ci_s = cit * 64 + ch * 8;
+  const bool do_bias = bpart && cit == 0;
+  float bacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bacc[j] = 0.f;
+  if (tid < 8) *reinterpret_cast<uint4*>(lx + (size_t)a.XR * WI_LD + tid * 8) = make_uint4(0, 0, 0, 0);
+  for (int r = tid; r < a.KS; r += WI_NT) {  // bit t: tap t of pixel row r stays inside its image
+    uint32_t m = 0u;
+    if (r < NR) {
+      const int p = r % HW, y = p / W, x = p - (p / W) * W;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int sy = y + t / 3 - 1, sx = x + t % 3 - 1;
+        if (sy >= 0 && sy < H && sx >= 0 && sx < W) m |= 1u << t;
+      }
+    }
+    tmask[r] = (uint16_t)m;
+  }
+  f32x4_t acc[5][2][2];
+#pragma unroll
+  for (int t = 0; t < 5; ++t)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int nst_total = a.B / a.E;
+  const int st0 = split * a.stages_per_split, st1 = min(nst_total, st0 + a.stages_per_split);
+  // every chunk of a stage in one register batch (the planner guarantees (KS + XR) * 8 <= WI_PFN * WI_NT):
+  // the next stage's loads are in flight during this stage's MFMAs. Offsets from the stage's env-0 base
+  // are the same for every stage.
+  const int nchunk = (a.KS + a.XR) * 8;
+  int soff[WI_PFN];
+  uint32_t sdy = 0u;
+#pragma unroll
+  for (int u = 0; u < WI_PFN; ++u) {
+    int off = -1;
+    const int i = u * WI_NT + tid;
+    if (i < a.KS * 8) {
+      const int r = i >> 3;
+      if (r < NR && co_s < a.Cout) off = r * a.Cout + co_s;
+      sdy |= 1u << u;
+    } else if (i < nchunk) {
+      const int r = (i >> 3) - a.KS;
+      if (ci_s < a.Cin) off = r * a.Cin + ci_s;
+    }
+    soff[u] = off;
+  }
+  uint4 pf[WI_PFN];
+  auto load_stage = [&](int st) {
+    const int b0 = st * a.E, sg = b0 / a.Bseg, bl = b0 - sg * a.Bseg;
+    const bf16_t* xb = a.xs[sg] + (size_t)bl * HW * a.Cin;
+    const bf16_t* db = a.dys[sg] + (size_t)bl * HW * a.Cout;
+#pragma unroll
+    for (int u = 0; u < WI_PFN; ++u)
+      pf[u] = *reinterpret_cast<const uint4*>(((sdy >> u) & 1u ? db : xb) + (soff[u] >= 0 ? soff[u] : 0));
+#pragma unroll
+    for (int u = 0; u < WI_PFN; ++u)
+      if (soff[u] < 0) pf[u] = make_uint4(0, 0, 0, 0);
+  };
+  auto store_stage = [&]() {
+#pragma unroll
+    for (int u = 0; u < WI_PFN; ++u) {
+      const int i = u * WI_NT + tid;
+      if (i < a.KS * 8) {
+        *reinterpret_cast<uint4*>(ldy + (size_t)(i >> 3) * WI_LD + ch * 8) = pf[u];
+        if (do_bias) {
+          const bf16_t* h = reinterpret_cast<const bf16_t*>(&pf[u]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) bacc[j] += bf16_to_f32(h[j]);
+        }
+      } else if (i < nchunk) {
+        *reinterpret_cast<uint4*>(lx + (size_t)((i >> 3) - a.KS) * WI_LD + ch * 8) = pf[u];
+      }
+    }
+  };
+  if (st0 < st1) load_stage(st0);
+  for (int st = st0; st < st1; ++st) {
+    __syncthreads();  // previous stage fully consumed (first pass: the zero row and mask table written)
+    store_stage();
+    __syncthreads();
+    if (st + 1 < st1) load_stage(st + 1);
+    for (int ks = 0; ks < a.KS / 32; ++ks) {
+      const int r0 = ks * 32 + 4 * g + q, r1 = r0 + 16;
+      const uint32_t m0 = tmask[r0], m1 = tmask[r1];
+      bf16x8_t af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int c = wr * 32 + i * 16 + 4 * pp;
+        af[i] = tr_frag_at(ldy + (size_t)r0 * WI_LD + c, ldy + (size_t)r1 * WI_LD + c);
+      }
+      auto bload = [&](int t, bf16x8_t (&b)[2]) {
+        const int off = (t / 3 - 1) * W + (t % 3 - 1);
+        const int x0 = (m0 >> t) & 1u ? r0 + off : a.XR, x1 = (m1 >> t) & 1u ? r1 + off : a.XR;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = wc * 32 + j * 16 + 4 * pp;
+          b[j] = tr_frag_at(lx + (size_t)x0 * WI_LD + c, lx + (size_t)x1 * WI_LD + c);
+        }
+      };
+      bf16x8_t bcur[2], bnxt[2];
+      bload(tap0, bcur);
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt) {
+        if (tt < ntap) {  // wave-uniform: tap group 1 has 4 taps
+          if (tt + 1 < ntap) bload(tap0 + tt + 1, bnxt);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[tt][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[tt][i][j], 0, 0, 0);
+          if (tt + 1 < ntap) { bcur[0] = bnxt[0]; bcur[1] = bnxt[1]; }
+        }
+      }
+    }
+  }
+  const size_t K = (size_t)9 * a.Cin;
+  float* outp = part + (size_t)split * a.Cout * K;
+  const int fr = lane & 15, fk = lane >> 4;
+#pragma unroll
+  for (int tt = 0; tt < 5; ++tt)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int t = tap0 + tt;
+        const int ci = cit * 64 + wc * 32 + j * 16 + fr;
+        if (tt >= ntap) continue;
+        if (ci >= a.Cin) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = cot * 64 + wr * 32 + i * 16 + 4 * fk + r;
+          if (co < a.Cout) outp[(size_t)co * K + (size_t)t * a.Cin + ci] = acc[tt][i][j][r];
+        }
+      }
+  if (do_bias) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bred[tid >> 3][ch * 8 + j] = bacc[j];
+    __syncthreads();
+    if (tid < 64) {
+      float sum = 0.f;
+      for (int r = 0; r < WI_NT / 8; ++r) sum += bred[r][tid];
+      const int co = cot * 64 + tid;
+      if (co < a.Cout) bpart[(size_t)split * a.Cout + co] = sum;
+    }
+  }
+}
+
+struct WgPxPlan {
+  WgPx a;
+  int nsplit;
+  size_t lds;
+};
+// B = all envs (nseg * Bseg); E (envs per stage) divides Bseg, so a stage never straddles a segment and
+// every stage is full; false when one env's stage does not fit the register batch or the LDS budget
+static bool wgrad_px_plan(int B, int Bseg, int H, int W, int Cin, int Cout, WgPxPlan& p) {
+  const int HW = H * W;
+  if (HW <= 0 || Bseg <= 0 || B % Bseg) return false;
+  auto ksr = [&](int e) { return (e * HW + 31) / 32 * 32; };
+  auto bytes = [&](int e) { return (size_t)(ksr(e) + e * HW + 1) * WI_LD * 2 + (size_t)ksr(e) * 2; };
+  auto fits = [&](int e) { return bytes(e) <= WI_LDS_MAX && (ksr(e) + e * HW) * 8 <= WI_PFN * WI_NT; };
+  if (!fits(1)) return false;
+  int E = 1;
+  while (E < 64 && Bseg % (E * 2) == 0 && fits(E * 2)) E *= 2;
+  const int tiles = ((Cout + 63) / 64) * ((Cin + 63) / 64);
+  const int stages = B / E;
+  int nsplit = (256 + tiles - 1) / tiles;  // one workgroup per CU
+  if (nsplit > stages) nsplit = stages;
+  const int sps = (stages + nsplit - 1) / nsplit;
+  nsplit = (stages + sps - 1) / sps;
+  p.a = WgPx{B, H, W, Cin, Cout, E, ksr(E), E * HW, sps, Bseg, tiles, (tiles * nsplit) % 8 == 0, {}, {}};
+  p.nsplit = nsplit;
+  p.lds = bytes(E);
+  return true;
+}
+
 // the weight and bias partials of one split weight-gradient launch, summed in one launch: acc[i] += sum_s
 // part[s][i] for i < n, bacc[j] += sum_s bpart[s][j] for j < nb, each element in split order (round 4: one launch
 // instead of one per buffer, the same sums)
@@ -1515,6 +1730,14 @@ int mzba_conv_wgrad_set_variant(int v) {
   g_wgrad_img = v;
   return 0;
 }
+// which whole-image kernel: 1 (default) pixel rows (conv_wgrad_px_kernel), 0 zero-bordered images
+// (conv_wgrad_img_kernel, the round-5 form, for A/B)
+static thread_local int g_wgrad_form = 1;
+int mzba_conv_wgrad_set_form(int v) {
+  if (v < 0 || v > 1) return -1;
+  g_wgrad_form = v;
+  return 0;
+}
 
 long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int ks) {
   const long long M = (long long)B * H * W;
@@ -1522,18 +1745,19 @@ long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int k
   long long n = wgrad_splits(M, tiles);
   WgPlan p;
   if (ks == 3 && Cin % 8 == 0 && Cout % 8 == 0 && wgrad_img_plan(B, 1, H, W, Cin, Cout, p) && p.nsplit > n) n = p.nsplit;
+  WgPxPlan px;
+  if (ks == 3 && Cin % 8 == 0 && Cout % 8 == 0 && wgrad_px_plan(B, 1, H, W, Cin, Cout, px) && px.nsplit > n) n = px.nsplit;
   return n * ((long long)Cout * ks * ks * Cin + Cout) * 4;
 }
 
-// the whole-image kernel over nseg segments of B envs (false: shape not supported by it)
-static bool wgrad_img_eligible(int dtype, int nseg, int B, int H, int W, int Cin, int Cout, int ks, WgPlan& ip) {
+// a whole-image kernel for nseg segments of B envs (its plan may still refuse the shape)
+static bool wgrad_img_eligible(int dtype, int nseg, int B, int H, int W, int Cin, int Cout, int ks) {
   // it wins where an image has many pixels per tap re-read (8x10: 138 vs 277 us, 16x20: 153 vs
   // 283 us at B = 512) and, at 4x5, once the K unrolled uses of a conv reduce in one launch
   // (per-tap kernel: 80 us per use; 5 x 512 at 256 -> 256: 188 vs 401 us, and 362 vs 464 us for
   // the dynamics ConvBlock's 264 input channels; tools/bench_wgrad_segs.py)
   if (dtype != 1 || ks != 3 || !g_wgrad_img || Cin % 8 || Cout % 8) return false;
-  if (H * W < 64 && !(g_wgrad_img == 2 || nseg * B >= 2048)) return false;
-  return wgrad_img_plan(nseg * B, B, H, W, Cin, Cout, ip);
+  return H * W >= 64 || g_wgrad_img == 2 || nseg * B >= 2048;
 }
 
 static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, int nseg, int B, int H, int W, int Cin,
@@ -1544,8 +1768,33 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
   MZ_CHECK_ARG(dtype == 0 || dtype == 1, -9);
   for (int i = 0; i < nseg; ++i) MZ_CHECK_ARG(xs[i] && dys[i], -1);
   MZ_CHECK_ARG(mzba_conv_wgrad_ws_bytes(nseg * B, H, W, Cin, Cout, ks) <= ws_bytes, -2);
+  WgPxPlan pxp;
+  if (g_wgrad_form == 1 && wgrad_img_eligible(dtype, nseg, B, H, W, Cin, Cout, ks) &&
+      wgrad_px_plan(nseg * B, B, H, W, Cin, Cout, pxp)) {
+    static bool attr = false;
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_px_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)WI_LDS_MAX);
+      if (e != hipSuccess) return (int)e;
+      attr = true;
+    }
+    for (int i = 0; i < nseg; ++i) {
+      pxp.a.xs[i] = (const bf16_t*)xs[i];
+      pxp.a.dys[i] = (const bf16_t*)dys[i];
+    }
+    const size_t nwi = (size_t)Cout * 9 * Cin;
+    float* ipart = (float*)ws;
+    float* ibpart = db ? ipart + (size_t)pxp.nsplit * nwi : nullptr;
+    hipLaunchKernelGGL(conv_wgrad_px_kernel, dim3(pxp.a.tiles, pxp.nsplit), dim3(WI_NT), pxp.lds, stream, pxp.a,
+                       ipart, ibpart);
+    const size_t nbi = db ? (size_t)Cout : 0;
+    hipLaunchKernelGGL(sum_partials2_kernel, dim3(grid_for(nwi + nbi)), dim3(256), 0, stream, (const float*)ipart,
+                       (const float*)ibpart, pxp.nsplit, nwi, nbi, dw, db);
+    MZ_LAUNCH_CHECK();
+    return 0;
+  }
   WgPlan ip;
-  if (wgrad_img_eligible(dtype, nseg, B, H, W, Cin, Cout, ks, ip)) {
+  if (wgrad_img_eligible(dtype, nseg, B, H, W, Cin, Cout, ks) && wgrad_img_plan(nseg * B, B, H, W, Cin, Cout, ip)) {
     static bool attr = false;  // the 16x20 images need more than the default 64 KB of dynamic LDS
     if (!attr) {
       hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_img_kernel<false>),

@@ -99,6 +99,7 @@ SIGNATURES = {
     "mzba_conv_pack_bf16_multi": [P, P, P, I, P],
     "mzba_conv_halo_set_waves": [I],
     "mzba_conv_wgrad_set_variant": [I],
+    "mzba_conv_wgrad_set_form": [I],
     "mzba_conv_wgrad": [I, P, P, I, I, I, I, I, I, P, P, P, LL, P],
     "mzba_conv_wgrad_segs": [I, P, P, I, I, I, I, I, I, I, P, P, P, LL, P],
     "mzba_avgpool2_backward": [I, P, P, I, I, I, I, P],

@@ -338,14 +338,19 @@ def test_learner_bf16_conv_packs(case, flip):
 @pytest.mark.parametrize("case", [("bf16", 1, 5, 512, 4, 5, 256, 256), ("bf16", 1, 5, 512, 4, 5, 264, 256),
                                   ("bf16", 2, 3, 7, 4, 5, 64, 64),
                                   ("bf16", 1, 3, 7, 4, 5, 64, 64), ("f32", 1, 2, 6, 4, 5, 40, 24),
-                                  ("bf16", 2, 8, 16, 8, 10, 128, 128)])
-def test_conv_wgrad_segs_matches_torch(case):
+                                  ("bf16", 2, 8, 16, 8, 10, 128, 128), ("bf16", 2, 3, 24, 3, 7, 64, 72),
+                                  ("bf16", 2, 2, 4, 16, 20, 128, 256)])
+@pytest.mark.parametrize("form", [1, 0])
+def test_conv_wgrad_segs_matches_torch(case, form):
     """mzba_conv_wgrad_segs (the learner's deferred latent weight gradient: K (x, dY) pairs in
     one contraction) against the torch fp32 weight gradient of the concatenated segments.
     variant 1 = automatic (5 x 512 envs at 4x5 -> whole-image kernel, small batches -> one
-    per-tap launch pair per segment), 2 = whole-image kernel forced."""
+    per-tap launch pair per segment), 2 = whole-image kernel forced. form 1 = the pixel-row
+    whole-image kernel (default), 0 = the zero-bordered one (the 3x7 case: HW = 21, odd rows per
+    stage; the bordered form refuses it and the per-tap kernel runs)."""
     from mzba import _lib as L
     dt, var, nseg, B, H, W, Cin, Cout = case
+    L.call("mzba_conv_wgrad_set_form", form)
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(nseg * 1000 + B)
     tdt = torch.float32 if dt == "f32" else torch.bfloat16
@@ -364,6 +369,7 @@ def test_conv_wgrad_segs_matches_torch(case):
                L.ptr(db), L.ptr(ws), nb, L.stream())
     finally:
         L.call("mzba_conv_wgrad_set_variant", 1)
+        L.call("mzba_conv_wgrad_set_form", 1)
     x = torch.cat(xs).float().permute(0, 3, 1, 2)
     dy = torch.cat(dys).float().permute(0, 3, 1, 2)
     ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dy, padding=1)

@@ -3,7 +3,8 @@ two builds in alternating processes: bench.py's learner setup (synthetic device 
 K = 5), 2 eager minibatches whose gradients and parameters are hashed (sha256 of their bytes: two builds that
 must be bit-identical are checked on the same seeded input), then the minibatch as one HIP graph, median of
 HIP-event times over 10 replays.
-usage (GPU box): MZBA_LIB=muzero-breakout_amd/mzba/libmzba_base.so python tools/ab_lib_learner.py [bf16|f32]"""
+usage (GPU box): MZBA_LIB=muzero-breakout_amd/mzba/libmzba_base.so python tools/ab_lib_learner.py [bf16|f32]
+MZBA_WGRAD_FORM=0|1 picks the whole-image weight-gradient form of the one build (mzba_conv_wgrad_set_form)."""
 import hashlib
 import json
 import os
@@ -39,6 +40,10 @@ def main():
         "targets": torch.randn(cap, K, device=dev, generator=g) * 2,
         "counts": torch.randint(0, 51, (cap, K, 3), device=dev, generator=g).float() + 1,
     }
+    form = os.environ.get("MZBA_WGRAD_FORM")
+    if form is not None:
+        from mzba import _lib as L
+        L.call("mzba_conv_wgrad_set_form", int(form))
     ln = Learner(mcfg, init_state_dict(mcfg, 0), K=K, dtype=dt, device=dev)
     slots = [torch.randperm(cap, device=dev, generator=g)[:B].to(torch.int32) for _ in range(12)]
     for i in range(2):
@@ -58,7 +63,7 @@ def main():
         ev[i][1].record()
     torch.cuda.synchronize()
     ms = float(np.median([a.elapsed_time(c) for a, c in ev]))
-    print(json.dumps({"lib": os.path.basename(os.environ.get("MZBA_LIB", "libmzba.so")), "dtype": dt,
+    print(json.dumps({"lib": os.path.basename(os.environ.get("MZBA_LIB", "libmzba.so")), "dtype": dt, "wgrad_form": form,
                       "minibatch_ms": ms, "sha": h.hexdigest()[:16]}))
 
 

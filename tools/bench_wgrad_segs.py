@@ -1,6 +1,8 @@
 """Learner latent weight gradient: K = 5 unrolled uses of one 3x3 256->256 conv at 4x5, B = 512
 per use. Immediate (5 x mzba_conv_wgrad, per-tap kernel) vs deferred (one mzba_conv_wgrad_segs,
-whole-image kernel). HIP-event median; FLOP = 2 M Cout Cin 9 over all segments."""
+whole-image kernel: form 1 = pixel rows, the default since round 6; form 0 = zero-bordered images). Also the
+representation's 16x20 / 8x10 shapes as single segments. HIP-event median; FLOP = 2 M Cout Cin 9 over all
+segments."""
 import ctypes
 import json
 import os
@@ -12,7 +14,8 @@ import torch  # noqa: E402
 from mzba import _lib as L  # noqa: E402
 
 dev = torch.device("cuda")
-for (nseg, B, H, W, Cin, Cout) in [(5, 512, 4, 5, 256, 256), (5, 512, 4, 5, 264, 256), (5, 512, 4, 5, 256, 128)]:
+for (nseg, B, H, W, Cin, Cout) in [(5, 512, 4, 5, 256, 256), (5, 512, 4, 5, 264, 256), (5, 512, 4, 5, 256, 128),
+                                   (1, 512, 8, 10, 256, 256), (1, 512, 16, 20, 128, 128), (1, 512, 16, 20, 256, 256)]:
     xs = [torch.randn(B, H, W, Cin, device=dev).to(torch.bfloat16) for _ in range(nseg)]
     dys = [torch.randn(B, H, W, Cout, device=dev).to(torch.bfloat16) for _ in range(nseg)]
     dw = torch.zeros(Cout, 9, Cin, device=dev)
@@ -22,8 +25,9 @@ for (nseg, B, H, W, Cin, Cout) in [(5, 512, 4, 5, 256, 256), (5, 512, 4, 5, 264,
     xp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in xs])
     dp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in dys])
     fl = 2.0 * nseg * B * H * W * Cout * Cin * 9
-    for mode in ("immediate", "segs_auto", "segs_img"):
-        L.call("mzba_conv_wgrad_set_variant", 2 if mode == "segs_img" else 1)
+    for mode in ("immediate", "segs_img_form0", "segs_img_form1"):
+        L.call("mzba_conv_wgrad_set_variant", 2 if mode.startswith("segs_img") else 1)
+        L.call("mzba_conv_wgrad_set_form", 0 if mode == "segs_img_form0" else 1)
         ts = []
         for it in range(10):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -44,3 +48,4 @@ for (nseg, B, H, W, Cin, Cout) in [(5, 512, 4, 5, 256, 256), (5, 512, 4, 5, 264,
         print(json.dumps({"shape": [nseg, B, H, W, Cin, Cout], "mode": mode, "us": round(us, 1),
                           "tflops": round(fl / us / 1e6, 1)}), flush=True)
 L.call("mzba_conv_wgrad_set_variant", 1)
+L.call("mzba_conv_wgrad_set_form", 1)

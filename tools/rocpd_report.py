@@ -1,6 +1,8 @@
 """Read rocprofv3's rocpd SQLite output (run_results.db) without the rocpd CLI.
   rocpd_report.py stats DB OUT.csv         per-kernel stats (calls, total/avg/min/max ns, %)
   rocpd_report.py counter DB NAME KERNEL   print per-dispatch values of counter NAME for kernels matching KERNEL
+  rocpd_report.py timeline DB OUT.csv      every kernel in start order: name, start/end (ns from the first), stream/queue
+                                           columns as the db names them
   rocpd_report.py gaps DB OUT.json         per acting step (kernels between two ctx_advance_kernel launches): span,
                                            busy time (sum of kernel durations), idle gaps between consecutive kernels"""
 import csv
@@ -59,7 +61,27 @@ def step_gaps(db):
     return out
 
 
+def timeline(db, out):
+    c = sqlite3.connect(find_db(db))
+    cur = c.execute("select * from kernels limit 1")
+    cols = [d[0] for d in cur.description]
+    ks = "start" if "start" in cols else [x for x in cols if "start" in x][0]
+    ke = "end" if "end" in cols else [x for x in cols if x.endswith("end")][0]
+    extra = [x for x in cols if any(t in x.lower() for t in ("stream", "queue"))]
+    rows = c.execute(f"select name, {ks}, {ke}{''.join(', ' + x for x in extra)} from kernels order by {ks}").fetchall()
+    t0 = rows[0][1] if rows else 0
+    with open(out, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["name", "start_ns", "end_ns"] + extra)
+        for r in rows:
+            w.writerow([r[0], r[1] - t0, r[2] - t0] + list(r[3:]))
+    print(f"{len(rows)} kernels, columns {cols}")
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "timeline":
+        timeline(sys.argv[2], sys.argv[3])
+        sys.exit(0)
     if sys.argv[1] == "gaps":
         import json
         res = step_gaps(sys.argv[2])
