@@ -206,6 +206,19 @@ int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const vo
                      int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
                      const float* mean, const float* pstats, const void* pres, int prelu, void* pout,
                      const float* pcoef, hipStream_t stream);
+/* mzba_conv_lat_bn plus the consuming BatchNorm's finaliser in the same launch: the last workgroup of each
+ * 128-channel column block (told by its add to ctr[column block]) folds every workgroup's partials (sc1 stores and
+ * loads: MI355X_MICROARCH.md's hand-off table, row 1). mode 1 = mzba_bn_stats_final (fstats out [4][Cout], running
+ * statistics updated when run_mean != NULL); mode 2 = mzba_bn_backward_coef (fstats in, dgamma / dbeta +=, coef out
+ * [3][Cout]). The chunk statistics fold in another order than those kernels' (f32 last-place differences). ctr:
+ * Cout / 128 words, zero at entry, zero again at exit, one launch in flight per word. Replaces, in the learner, the
+ * BN finaliser launch after each fused conv (train_torch.py:487-528's BatchNorm2d in train mode). */
+int mzba_conv_lat_bn_fin(const void* in, const void* wf, const float* bias, const void* res, void* out, int B, int H,
+                         int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
+                         const float* mean, const float* pstats, const void* pres, int prelu, void* pout,
+                         const float* pcoef, unsigned* ctr, float eps, float momentum, const float* gamma,
+                         const float* beta, float* fstats, float* run_mean, float* run_var, float* dgamma, float* dbeta,
+                         float* coef, hipStream_t stream);
 
 /* Fused residual tower: nblocks ResidualBlock(256) on the 4x5 latent in ONE launch (networks.py:19-35,
  * 124-131, 190-197); a workgroup keeps 4 (or, for B >= 8 x CUs, 8) envs' activations in LDS for the

@@ -75,7 +75,125 @@ struct LatArgs {
   // mean_g) alpha of the BN output gradient g = in and BN input x = pres (mean / alpha = pstats rows
   // 0 / 2, mean_g / k = pcoef rows 0 / 1: mzba_bn_backward_coef), also stored to pout
   const float* pcoef;
+  // learner: the consuming BatchNorm's finaliser in this launch (ctr != null, smode 1 / 2; lat_bn_finish): the last
+  // workgroup of each column block folds every workgroup's partials. smode 1: fstats = out [4][Cout] (mean, invstd,
+  // alpha, beta'), running statistics updated in place (optional); smode 2: fstats = in (invstd row 1, alpha row 2),
+  // dgamma / dbeta += in place, coef = out [3][Cout] (mean_g, k, alpha) — bn_stats_final_kernel /
+  // bn_bwd_final_kernel (learn.hip) without their launches
+  unsigned* ctr;  // [Cout / 128] zero at entry; the last workgroup of a column block resets its word
+  float eps, momentum;
+  const float* gamma;
+  const float* beta;
+  float* fstats;
+  float* run_mean;
+  float* run_var;
+  float* dgamma;
+  float* dbeta;
+  float* coef;
 };
+
+// The consuming BatchNorm's finaliser at the end of the producing launch. Every workgroup has stored its partials
+// with sc1 stores (lat_epilogue); after every wave's stores have completed (vmcnt(0), then a workgroup barrier) one
+// lane adds to its column block's counter, and the workgroup whose add returns gridDim.x - 1 loads all the
+// partials with sc1 loads — the hand-off of MI355X_MICROARCH.md's table, row 1 (one workgroup per CU: conv_lat's
+// 8-wave instances hold > 80 KiB of LDS; hipMalloc memory) — and folds them, 4 threads per channel (chunks
+// q, q + 4, ...) combined in q order: forward mean = sum n_k mean_k / M, M2 = sum (M2_k + n_k (mean_k - mean)^2)
+// in double (the division-free fold of the chunk statistics), backward sum g and sum g (x - mean) in double; then
+// the tails of bn_stats_final_kernel / bn_bwd_final_kernel, expression for expression. The fold order differs
+// from those kernels' (Chan pairs + butterfly), so statistics can differ from theirs in the last f32 place.
+template <int NT>
+__device__ __forceinline__ void lat_bn_finish(const LatArgs& a, float* ws, int tid) {
+  static_assert(NT == 512, "4 threads per channel of a 128-channel column block");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
+  __syncthreads();
+  volatile int* flag = reinterpret_cast<volatile int*>(ws);
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(a.ctr + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == gridDim.x - 1;
+    if (last) __hip_atomic_store(a.ctr + blockIdx.y, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  const int col = tid & 127, q = tid >> 7;
+  const int n = blockIdx.y * 128 + col;
+  const int nchunk = gridDim.x, rpc = a.E * a.H * a.W, M = a.B * a.H * a.W;
+  unsigned long long* P = reinterpret_cast<unsigned long long*>(a.part) + n;  // float2 [chunk][Cout]
+  auto ld = [&](int k) {
+    const unsigned long long u = __hip_atomic_load(P + (size_t)k * a.Cout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float2(__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)));
+  };
+  auto nk = [&](int k) { return (double)min(rpc, M - k * rpc); };
+  constexpr int CK = 16;  // chunks per thread held in registers (nchunk <= 64: all of them)
+  float2 pv[CK];
+#pragma unroll
+  for (int i = 0; i < CK; ++i) pv[i] = q + 4 * i < nchunk ? ld(q + 4 * i) : make_float2(0.f, 0.f);
+  double* rd = reinterpret_cast<double*>(ws) + 8;  // [4][128] after the flag
+  auto fold4 = [&](double v) {  // (v_0 + v_1) + v_2 + v_3 over q, every thread gets it
+    __syncthreads();
+    rd[q * 128 + col] = v;
+    __syncthreads();
+    return ((rd[col] + rd[128 + col]) + rd[256 + col]) + rd[384 + col];
+  };
+  if (a.smode == 1) {
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < CK; ++i)
+      if (q + 4 * i < nchunk) s += nk(q + 4 * i) * (double)pv[i].x;
+    for (int k = q + 4 * CK; k < nchunk; k += 4) s += nk(k) * (double)ld(k).x;
+    const double mean = fold4(s) / M;
+    double m2 = 0;
+#pragma unroll
+    for (int i = 0; i < CK; ++i)
+      if (q + 4 * i < nchunk) {
+        const double d = (double)pv[i].x - mean;
+        m2 += (double)pv[i].y + nk(q + 4 * i) * d * d;
+      }
+    for (int k = q + 4 * CK; k < nchunk; k += 4) {
+      const float2 v = ld(k);
+      const double d = (double)v.x - mean;
+      m2 += (double)v.y + nk(k) * d * d;
+    }
+    m2 = fold4(m2);
+    if (q) return;
+    const int C = a.Cout;
+    const float var = (float)(m2 / M);
+    const float invstd = (float)(1.0 / sqrt((double)var + (double)a.eps));
+    const float alpha = invstd * a.gamma[n];
+    const float fm = (float)mean;
+    a.fstats[n] = fm;
+    a.fstats[C + n] = invstd;
+    a.fstats[2 * C + n] = alpha;
+    a.fstats[3 * C + n] = a.beta[n] - fm * alpha;
+    if (a.run_mean) {
+      a.run_mean[n] = (float)((double)a.momentum * mean + (1.0 - (double)a.momentum) * (double)a.run_mean[n]);
+      const double unbiased = M > 1 ? m2 / (double)(M - 1) : m2;
+      a.run_var[n] = (float)((double)a.momentum * unbiased + (1.0 - (double)a.momentum) * (double)a.run_var[n]);
+    }
+    return;
+  }
+  double sg = 0, dot = 0;
+#pragma unroll
+  for (int i = 0; i < CK; ++i) {
+    sg += (double)pv[i].x;  // chunks past nchunk hold exact zeros
+    dot += (double)pv[i].y;
+  }
+  for (int k = q + 4 * CK; k < nchunk; k += 4) {
+    const float2 v = ld(k);
+    sg += (double)v.x;
+    dot += (double)v.y;
+  }
+  sg = fold4(sg);
+  dot = fold4(dot);
+  if (q) return;
+  const int C = a.Cout;
+  const float invstd = a.fstats[C + n], alpha = a.fstats[2 * C + n];
+  a.dgamma[n] = a.dgamma[n] + (float)dot * invstd;
+  a.dbeta[n] = a.dbeta[n] + (float)sg;
+  a.coef[n] = (float)(sg / M);
+  a.coef[C + n] = (float)dot * invstd * invstd / (float)M;
+  a.coef[2 * C + n] = alpha;
+}
 
 // epilogue: (1) issue the residual loads (16 B per lane) so they land while the f32 tile is
 // reduced through LDS; (2) finish 16-B output chunks: + residual, ReLU, bf16, 16-B stores.
@@ -215,9 +333,17 @@ __device__ __forceinline__ void lat_epilogue(const LatArgs& a, float* ot, const 
       float t2 = 0.f;
 #pragma unroll
       for (int k = 0; k < TPC; ++k) t2 += red[k * 128 + col];
-      pf[2 * col] = mean;
-      pf[2 * col + 1] = t2;
+      if (a.ctr)  // one 8-B sc1 store (lat_bn_finish's hand-off)
+        __hip_atomic_store(reinterpret_cast<unsigned long long*>(pf + 2 * col),
+                           (unsigned long long)__float_as_uint(mean) | ((unsigned long long)__float_as_uint(t2) << 32),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else {
+        pf[2 * col] = mean;
+        pf[2 * col + 1] = t2;
+      }
     }
+    if constexpr (NT == 512)
+      if (a.ctr) lat_bn_finish<NT>(a, ot, tid);
     return;
   }
   // smode 2: the NT / ncb threads of a chunk column reduce through the tile, in thread order
@@ -233,8 +359,16 @@ __device__ __forceinline__ void lat_epilogue(const LatArgs& a, float* ot, const 
     const float* src = tid < 128 ? rg : rd;
     float t = 0.f;
     for (int k = 0; k < G; ++k) t += src[k * 128 + col];
-    if (col < ncols) pf[2 * col + (tid >> 7)] = t;
+    if (col < ncols) {
+      if (a.ctr)  // sc1 store (lat_bn_finish's hand-off)
+        __hip_atomic_store(reinterpret_cast<unsigned*>(pf + 2 * col + (tid >> 7)), __float_as_uint(t), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        pf[2 * col + (tid >> 7)] = t;
+    }
   }
+  if constexpr (NT == 512)
+    if (a.ctr) lat_bn_finish<NT>(a, ot, tid);
 }
 
 // accumulator init for the first channel group: bias (+ per-(pixel, action) bias) of this
@@ -252,8 +386,10 @@ __device__ __forceinline__ float lat_acc_init(const LatArgs& a, float bias_n, in
 
 // RT: 32-row tiles per workgroup (5: E*HW <= 160; 3: E*HW <= 96, twice the workgroups for the
 // learner's B = 512 latent convs, whose 5-tile grid fills only half the CUs)
-template <int KS, int CIN, int WAVES, int DMAX, int RT = R>
-__global__ __launch_bounds__(64 * WAVES, WAVES / 4) void conv_lat_kernel(LatArgs a) {
+// OCC: workgroups per CU the register budget allows (2: <= 128 VGPRs at 8 waves, the 3-row instance with a 4-deep
+// ring whose ~56 KiB of LDS lets two workgroups share a CU, one's staging / epilogue beside the other's k loop)
+template <int KS, int CIN, int WAVES, int DMAX, int RT = R, int OCC = 1>
+__global__ __launch_bounds__(64 * WAVES, OCC * WAVES / 4) void conv_lat_kernel(LatArgs a) {
   constexpr int MAXROWS = 32 * RT;
   constexpr int KSPLIT = WAVES / 4;      // channel groups per tap (1: 4 waves, 2: 8 waves)
   constexpr int NC = CIN / 16;           // k steps per tap
@@ -693,9 +829,11 @@ static int lat_ncu() {
 // 0: 8 waves (2 per SIMD: 4 column tiles x 2 channel halves), the default (3-row-tile workgroups
 //    where the 5-tile grid would leave CUs idle);
 // 1: 4 waves with 2 column tiles each (conv_lat2_kernel, experiment). Same weight packing;
-// 2: the default kernel with 5-row-tile workgroups only (A/B reference).
+// 2: the default kernel with 5-row-tile workgroups only (A/B reference);
+// 3: 3-row-tile workgroups wherever they apply, the two-workgroups-per-CU instance (OCC 2: <= 128 VGPRs, ring depth
+//    4, ~56 KiB LDS); the fused BN finaliser (ctr) keeps the one-per-CU instances (its hand-off's condition).
 int mzba_conv_lat_set_variant(int v) {
-  if (v < 0 || v > 2) return -1;
+  if (v < 0 || v > 3) return -1;
   g_lat_variant = v;
   return 0;
 }
@@ -725,6 +863,7 @@ static void lat_geometry(int B, int H, int W, int Cin, int Cout, int& E, bool& r
   const int E3 = (32 * 3) / HW;
   rt3 = g_lat_variant == 0 && E3 >= 1 && (long long)((B + E - 1) / E) * ny < lat_ncu() &&
         (B + E3 - 1) / E3 > (B + E - 1) / E && Cin >= 128;
+  if (g_lat_variant == 3 && E3 >= 1 && Cin >= 128) rt3 = true;
   if (rt3) E = E3;
 }
 
@@ -736,8 +875,13 @@ static int lat_launch(LatArgs& a, hipStream_t stream) {
   const int v = g_lat_variant;
 #define MZ_LAT(KS_, CIN_, W_, D_) \
   if (ks == KS_ && Cin == CIN_) { hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, W_, D_>), grid, dim3(64 * W_), 0, stream, a); }
-#define MZ_LAT3(KS_, CIN_) \
-  if (ks == KS_ && Cin == CIN_) { hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, 8, 8, 3>), grid, dim3(512), 0, stream, a); }
+#define MZ_LAT3(KS_, CIN_)                                                                                      \
+  if (ks == KS_ && Cin == CIN_) {                                                                               \
+    if (v == 3 && !a.ctr)                                                                                       \
+      hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, 8, 4, 3, 2>), grid, dim3(512), 0, stream, a);              \
+    else                                                                                                        \
+      hipLaunchKernelGGL((conv_lat_kernel<KS_, CIN_, 8, 8, 3>), grid, dim3(512), 0, stream, a);                 \
+  }
   if (v == 1) {
     if (a.smode) return -4;  // the fused statistics ride on the 8-wave kernel only
     if (ks == 3 && Cin == 256) hipLaunchKernelGGL((conv_lat2_kernel<3, 256>), grid, dim3(256), 0, stream, a);
@@ -788,6 +932,31 @@ int mzba_conv_lat_bn(const void* in, const void* wf, const float* bias, const vo
             (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, 0, 0,
             mode, (float2*)part, (const bf16_t*)y, (const bf16_t*)x, mean,
             pstats, (const bf16_t*)pres, prelu, (bf16_t*)pout, pcoef};
+  return lat_launch(a, stream);
+}
+
+// mzba_conv_lat_bn plus the consuming BatchNorm's finaliser in the same launch (lat_bn_finish): mode 1 writes that
+// BN's stats [4][Cout] and updates its running statistics (run_mean / run_var optional) as mzba_bn_stats_final does;
+// mode 2 reads its stats and adds to dgamma / dbeta and writes coef [3][Cout] as mzba_bn_backward_coef does. ctr:
+// Cout / 128 unsigned words, zero at entry and zero again at exit (the launch's last workgroups reset them), never
+// shared by two launches in flight. The 8-wave kernels only (variant 0 / 2).
+int mzba_conv_lat_bn_fin(const void* in, const void* wf, const float* bias, const void* res, void* out, int B, int H,
+                         int W, int Cin, int Cout, int ks, int mode, float* part, const void* y, const void* x,
+                         const float* mean, const float* pstats, const void* pres, int prelu, void* pout,
+                         const float* pcoef, unsigned* ctr, float eps, float momentum, const float* gamma,
+                         const float* beta, float* fstats, float* run_mean, float* run_var, float* dgamma, float* dbeta,
+                         float* coef, hipStream_t stream) {
+  MZ_CHECK_ARG(B > 0 && in && wf && bias && out && mzba_conv_lat_supported(H, W, Cin, Cout, ks), -1);
+  MZ_CHECK_ARG(Cout % 128 == 0 && part && (mode == 1 || (mode == 2 && y && x && mean)), -3);
+  MZ_CHECK_ARG(!pstats || pout, -3);
+  MZ_CHECK_ARG(!pcoef || (pstats && pres), -3);
+  MZ_CHECK_ARG(ctr && fstats && g_lat_variant != 1, -3);
+  MZ_CHECK_ARG(mode == 1 ? (gamma && beta && (!run_mean || run_var)) : (dgamma && dbeta && coef), -3);
+  LatArgs a{(const bf16_t*)in, (long long)H * W * Cin, nullptr, 0, (const bf16_t*)wf, bias, nullptr, nullptr, 0,
+            (const bf16_t*)res, (bf16_t*)out, B, H, W, Cin, Cout, ks, 0, 0,
+            mode, (float2*)part, (const bf16_t*)y, (const bf16_t*)x, mean,
+            pstats, (const bf16_t*)pres, prelu, (bf16_t*)pout, pcoef,
+            ctr, eps, momentum, gamma, beta, fstats, run_mean, run_var, dgamma, dbeta, coef};
   return lat_launch(a, stream);
 }
 

@@ -91,6 +91,8 @@ SIGNATURES = {
     "mzba_bn_backward_final": [I, P, P, P, P, I, I, I, P, P, P, P, LL, P],
     "mzba_conv_lat_bn_chunks": [I, I, I, I, I, I, P, P],
     "mzba_conv_lat_bn": [P, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P, I, P, P, P],
+    "mzba_conv_lat_bn_fin": [P, P, P, P, P, I, I, I, I, I, I, I, P, P, P, P, P, P, I, P, P, P, F, F, P, P, P, P, P, P,
+                             P, P, P],
     "mzba_bn_backward_coef": [P, I, I, I, P, P, P, P, P],
     "mzba_bn_backward_apply": [I, P, P, P, P, P, I, I, P],
     "mzba_conv_wpack": [I, P, P, I, I, I, I, I, P],

@@ -22,6 +22,7 @@ bf16) with f32 statistics, gradients, Adam state and master weights.
 """
 import contextlib
 import ctypes
+import os
 from collections import OrderedDict
 
 import numpy as np
@@ -34,6 +35,7 @@ from .weights import init_state_dict, rep_layout, state_dict_spec
 LAT_PAD_ELEMS = 8 * 64 * 8  # conv_lat / band weight-ring overrun (agent.LAT_PAD_ELEMS)
 
 BN_EPS, BN_MOMENTUM = 1e-5, 0.1
+CTR_WORDS = 8192  # BN finaliser counter words per minibatch (about 2 x 632 used at the reference architecture)
 BETAS, ADAM_EPS, WEIGHT_DECAY = (0.9, 0.999), 1e-8, 1e-4
 
 
@@ -96,7 +98,7 @@ class Learner:
     """
 
     def __init__(self, mcfg, state_dict=None, K=5, dtype="f32", lr=None, seed=0, device="cuda", defer_wgrad=True,
-                 fuse_bn=True, streams=2, lat_rows=None):
+                 fuse_bn=True, streams=2, lat_rows=None, fuse_fin=None):
         L.require_gpu()
         # streams=2: the prediction net of every unrolled step runs on a side stream, concurrently
         # with the dynamics chain (forward: prediction(h_k) beside dynamics(h_k); backward: all
@@ -108,17 +110,35 @@ class Learner:
         self._side_stream = None
         # conv_lat workgroup rows for the bf16 latent convs: "auto" lets conv_lat take 3-row tiles where
         # a lone B = 512 conv's 5-row grid would leave CUs idle; with two streams the other chain fills
-        # them and forced 5-row tiles (less weight streaming per row) win — 31.6 vs 32.5 ms (two
-        # streams), 42.2 vs 37.9 ms (one stream). The choice is a per-host-thread conv_lat setting
-        # (thread_local in csrc/conv_lat.hip) bracketed around each minibatch.
-        if lat_rows not in (None, "auto", 5):
-            raise ValueError('lat_rows must be None, "auto" or 5')
-        self.lat_rows = lat_rows if lat_rows is not None else (5 if streams == 2 else "auto")
+        # them and forced 5-row tiles (less weight streaming per row) beat "auto" — 31.6 vs 32.5 ms (two
+        # streams), 42.2 vs 37.9 ms (one stream). Round 6: 3-row tiles on the two-workgroups-per-CU
+        # instance (lat_rows=3) beat both with two streams — 25.9-26.0 vs 27.2-27.3 ms (5-row) and 27.1-27.2
+        # (auto), profiles/r06/lat_occ2/ — so it is the two-stream default. The choice is a per-host-thread
+        # conv_lat setting (thread_local in csrc/conv_lat.hip) bracketed around each minibatch.
+        # lat_rows=3: 3-row tiles on the two-workgroups-per-CU instance (<= 128 VGPRs, ~56 KiB LDS: one workgroup's
+        # staging and epilogue beside another's k loop; conv_lat variant 3). MZBA_LAT_ROWS overrides the default.
+        if lat_rows is None and os.environ.get("MZBA_LAT_ROWS"):
+            v = os.environ["MZBA_LAT_ROWS"]
+            lat_rows = v if v == "auto" else int(v)
+        if lat_rows not in (None, "auto", 5, 3):
+            raise ValueError('lat_rows must be None, "auto", 5 or 3')
+        self.lat_rows = lat_rows if lat_rows is not None else (3 if streams == 2 else "auto")
         self._tag = ""
         self.defer_wgrad = defer_wgrad
         # bf16: BN batch statistics computed in the epilogue of the conv_lat launch that produces the
         # BN's input (forward) / output gradient (backward) — mzba_conv_lat_bn
         self.fuse_bn = fuse_bn
+        # fuse_fin (bf16 with fuse_bn): each fused conv also runs its consumer BN's finaliser (mzba_conv_lat_bn_fin:
+        # the last workgroup of a column block folds the partials; no bn_stats_final / bn_backward_coef launch).
+        # Counter words (zero between launches; every launch takes fresh ones, so the two streams never share one)
+        # come from a pool the minibatch walks in launch order. Off by default: 586 fewer launches per minibatch
+        # and no faster (27.38-27.53 vs 27.29-27.37 ms graph-replayed, same process, profiles/r06/bn_fin/) — the
+        # finalisers ran beside the other stream's convs, and the folding workgroup's tail lands on the conv.
+        # MZBA_BN_FIN=1 turns it on (A/B).
+        if fuse_fin is None:
+            fuse_fin = os.environ.get("MZBA_BN_FIN", "0") != "0"
+        self.fuse_fin = bool(fuse_fin)
+        self._ctr, self._ctr_i = None, 0
         self._gpart = {}
         self._lazy = {}  # BN outputs whose apply rides on the consuming conv_lat (id(y) -> (y, t, stats, res, relu))
         self._lazyb = {}  # BN input gradients likewise (id(dt) -> (dt, g, t, stats, coef))
@@ -408,16 +428,41 @@ class Learner:
     def _fusable(self, kind, cout):
         return self.fuse_bn and self.dt == 1 and kind == "lat" and cout % 128 == 0
 
-    def _lat_bn(self, x, w, bias, res, out, B, H, W, cin, cout, ks, mode, y=None, t=None, stats=None, pro=None):
+    def _ctr_take(self, n):
+        """n zeroed counter words for one mzba_conv_lat_bn_fin launch (fresh per launch within a minibatch)."""
+        if self._ctr is None:
+            self._ctr = torch.zeros(CTR_WORDS, dtype=torch.int32, device=self.device)
+        if self._ctr_i + n > CTR_WORDS:
+            raise RuntimeError("Learner: BN finaliser counter pool exhausted")
+        w = self._ctr[self._ctr_i:self._ctr_i + n]
+        self._ctr_i += n
+        return w
+
+    def _lat_bn(self, x, w, bias, res, out, B, H, W, cin, cout, ks, mode, y=None, t=None, stats=None, pro=None,
+                fin=None):
         """mzba_conv_lat_bn: the conv plus its consumer BN's per-workgroup partial statistics;
-        pro = (stats, res, relu, y) of the producing BN applied while staging (x is then its input t)."""
+        pro = (stats, res, relu, y) of the producing BN applied while staging (x is then its input t).
+        fin: the consumer BN's finaliser in the same launch (mzba_conv_lat_bn_fin) — mode 1: (stats out,
+        gamma, beta, running mean, running var); mode 2: (dgamma, dbeta, coef out) with stats = that BN's."""
         nc, rpc = ctypes.c_int(), ctypes.c_int()
         L.call("mzba_conv_lat_bn_chunks", B, H, W, cin, cout, ks, ctypes.byref(nc), ctypes.byref(rpc))
         part = torch.empty(nc.value * cout * 2, dtype=torch.float32, device=self.device)
         ps, pr, prelu, po, pc = pro if pro is not None else (None, None, 0, None, None)
-        L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(w), L.ptr(bias), L.ptr(res), L.ptr(out), B, H, W, cin, cout, ks, mode,
-               L.ptr(part), L.ptr(y), L.ptr(t), L.ptr(stats), L.ptr(ps), L.ptr(pr), int(prelu), L.ptr(po), L.ptr(pc),
-               L.stream())
+        if fin is None:
+            L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(w), L.ptr(bias), L.ptr(res), L.ptr(out), B, H, W, cin, cout, ks,
+                   mode, L.ptr(part), L.ptr(y), L.ptr(t), L.ptr(stats), L.ptr(ps), L.ptr(pr), int(prelu), L.ptr(po),
+                   L.ptr(pc), L.stream())
+            return part, nc.value, rpc.value
+        ctr = self._ctr_take(cout // 128)
+        if mode == 1:
+            fst, gamma, beta, rm, rv = fin
+            fargs = (L.ptr(gamma), L.ptr(beta), L.ptr(fst), L.ptr(rm), L.ptr(rv), None, None, None)
+        else:
+            dg, db, coef = fin
+            fargs = (None, None, L.ptr(stats), None, None, L.ptr(dg), L.ptr(db), L.ptr(coef))
+        L.call("mzba_conv_lat_bn_fin", L.ptr(x), L.ptr(w), L.ptr(bias), L.ptr(res), L.ptr(out), B, H, W, cin, cout, ks,
+               mode, L.ptr(part), L.ptr(y), L.ptr(t), L.ptr(stats), L.ptr(ps), L.ptr(pr), int(prelu), L.ptr(po),
+               L.ptr(pc), L.ptr(ctr), BN_EPS, BN_MOMENTUM, *fargs, L.stream())
         return part, nc.value, rpc.value
 
     def _materialize(self, y):
@@ -444,12 +489,17 @@ class Learner:
         Returns (output, fused partials or None)."""
         t = self._act(B * H * W, c.cout)
         if bn and self._fusable(c.fkind, c.cout):
+            fin = fst = None
+            if self.fuse_fin:  # the BN's finaliser rides on this launch: (partials, stats) -> _bn
+                fst = torch.empty(4, c.cout, dtype=torch.float32, device=self.device)
+                rm, rv = self.run[c.bn_key]
+                fin = (fst, c.gamma, c.beta, rm, rv)
             e = self._lazy.pop(id(x), None)
             if e is not None and e[0] is x:  # x = [relu](t' * alpha + beta' [+ res]) computed in the staging
                 _, tp, st, res, relu = e
                 return t, self._lat_bn(tp, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1,
-                                       pro=(st, res, relu, x, None))
-            return t, self._lat_bn(x, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1)
+                                       pro=(st, res, relu, x, None), fin=fin) + (fst,)
+            return t, self._lat_bn(x, c.wf, c.b, None, t, B, H, W, c.cin_p, c.cout, c.ks, 1, fin=fin) + (fst,)
         self._materialize(x)
         self._run_conv(c.fkind, x, c.cin_p, c.w if self.dt == 0 else c.wf, c.b, None, t, B, H, W, c.cout, c.ks)
         return t, None
@@ -459,9 +509,12 @@ class Learner:
         stats = torch.empty(4, c.cout, dtype=torch.float32, device=self.device)
         rm, rv = self.run[c.bn_key]
         if fpart is not None:  # statistics from the producing conv; the apply is deferred to the consumer
-            part, nc, rpc = fpart
-            L.call("mzba_bn_stats_final", L.ptr(part), nc, rpc, M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma),
-                   L.ptr(c.beta), L.ptr(stats), L.ptr(rm), L.ptr(rv), L.stream())
+            part, nc, rpc, fst = fpart
+            if fst is not None:  # finalised in the producing launch (mzba_conv_lat_bn_fin)
+                stats = fst
+            else:
+                L.call("mzba_bn_stats_final", L.ptr(part), nc, rpc, M, c.cout, BN_EPS, BN_MOMENTUM, L.ptr(c.gamma),
+                       L.ptr(c.beta), L.ptr(stats), L.ptr(rm), L.ptr(rv), L.stream())
             self.nbt[c.bn_key] += 1
             y = self._act(M, c.cout)
             self._lazy[id(y)] = (y, t, stats, res, relu)
@@ -482,9 +535,11 @@ class Learner:
         e = self._gpart.pop(id(dy), None)
         if e is not None and e[0] is dy and e[1] is y and self.dt == 1:
             # dy came masked with partials from its producing conv; the apply rides on the consumer
-            coef = torch.empty(3 * c.cout, dtype=torch.float32, device=self.device)
-            L.call("mzba_bn_backward_coef", L.ptr(e[2]), e[3], M, c.cout, L.ptr(stats), L.ptr(c.dgamma),
-                   L.ptr(c.dbeta), L.ptr(coef), L.stream())
+            coef = e[4]  # finalised in the producing launch (mzba_conv_lat_bn_fin), else here
+            if coef is None:
+                coef = torch.empty(3 * c.cout, dtype=torch.float32, device=self.device)
+                L.call("mzba_bn_backward_coef", L.ptr(e[2]), e[3], M, c.cout, L.ptr(stats), L.ptr(c.dgamma),
+                       L.ptr(c.dbeta), L.ptr(coef), L.stream())
             self._lazyb[id(dt)] = (dt, dy, t, stats, coef)
             return dt
         if e is not None and e[0] is dy and e[1] is y:  # dy came masked, partials from its producing conv
@@ -545,10 +600,14 @@ class Learner:
             src = dy
         if (bn is not None or pro is not None) and self._fusable(c.dkind, cu):
             if bn is not None:
-                _, y, t, st = bn
+                bc, y, t, st = bn
+                fin = coef = None
+                if self.fuse_fin:  # the BN's backward finaliser rides on this launch
+                    coef = torch.empty(3 * cu, dtype=torch.float32, device=self.device)
+                    fin = (bc.dgamma, bc.dbeta, coef)
                 part, nc, _ = self._lat_bn(src, c.wt, self._zero, acc, out, B, H, W, c.cout, cu, c.ks, 2, y, t, st,
-                                           pro=pro)
-                self._gpart[id(out)] = (out, y, part, nc)
+                                           pro=pro, fin=fin)
+                self._gpart[id(out)] = (out, y, part, nc, coef)
             else:
                 self._lat_bn(src, c.wt, self._zero, acc, out, B, H, W, c.cout, cu, c.ks, 0, pro=pro)
             return out
@@ -692,11 +751,12 @@ class Learner:
         self._graph, self._g_ring, self._g_loss = g, ring, loss
 
     def _minibatch(self, ring, slots):
-        """One minibatch with conv_lat set to this learner's tile rows (variant 2 = 5-row tiles only,
-        0 = auto), restored afterwards; a captured graph keeps the shapes it recorded."""
+        """One minibatch with conv_lat set to this learner's tile rows (variant 2 = 5-row tiles only, 3 = 3-row
+        tiles on the two-workgroups-per-CU instance, 0 = auto), restored afterwards; a captured graph keeps the
+        shapes it recorded."""
         prev = L.lib().mzba_conv_lat_get_variant()
-        want = 2 if self.lat_rows == 5 else 0
-        if prev not in (0, 2) or prev == want:
+        want = {5: 2, 3: 3}.get(self.lat_rows, 0)
+        if prev not in (0, 2, 3) or prev == want:
             return self._minibatch_body(ring, slots)
         L.call("mzba_conv_lat_set_variant", want)
         try:
@@ -718,6 +778,7 @@ class Learner:
         self._gpart = {}
         self._lazy = {}
         self._lazyb = {}
+        self._ctr_i = 0
         self._prepare_packs()
         # ---- forward (_k_step_rollout)
         cin_p = self.rep[0][1].cin_p

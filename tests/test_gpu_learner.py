@@ -450,7 +450,7 @@ def test_learner_side_stream_matches_one_stream(dt, ch):
     ring = _random_ring(64, mcfg["state_history_length"], 5, 13)
     gen = torch.Generator().manual_seed(7)
     slots = [torch.randperm(64, generator=gen)[:32].to(torch.int32) for _ in range(4)]
-    a = Learner(mcfg, init_state_dict(mcfg, 6), K=5, dtype=dt, streams=1, lat_rows=5)  # same conv tiles as b, c
+    a = Learner(mcfg, init_state_dict(mcfg, 6), K=5, dtype=dt, streams=1, lat_rows=3)  # same conv tiles as b, c
     b = Learner(mcfg, init_state_dict(mcfg, 6), K=5, dtype=dt, streams=2)
     c = Learner(mcfg, init_state_dict(mcfg, 6), K=5, dtype=dt, streams=2)
     la = [a.train_minibatch(ring, s).cpu().clone() for s in slots]
@@ -468,7 +468,7 @@ def test_learner_side_stream_matches_one_stream(dt, ch):
     assert torch.equal(a.M1, c.M1) and torch.equal(a.M2, c.M2)
 
 
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 3])
 @pytest.mark.parametrize("B,H,W,Cin,Cout,ks", [(512, 4, 5, 256, 256, 3), (37, 4, 5, 256, 128, 3),
                                                 (19, 4, 5, 128, 256, 1), (64, 8, 10, 256, 256, 3)])
 def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks, variant):
@@ -483,6 +483,62 @@ def test_conv_lat_bn_matches_separate_passes(B, H, W, Cin, Cout, ks, variant):
         _conv_lat_bn_case(B, H, W, Cin, Cout, ks)
     finally:
         L.call("mzba_conv_lat_set_variant", 0)
+
+
+@pytest.mark.parametrize("B,Cin,Cout,ks", [(512, 256, 256, 3), (37, 256, 128, 3), (19, 128, 256, 1), (1, 256, 256, 3)])
+def test_conv_lat_two_per_cu_instance_is_bit_identical(B, Cin, Cout, ks):
+    """conv_lat variant 3 (3-row tiles on the two-workgroups-per-CU instance: ring depth 4, <= 128 VGPRs) gives the
+    3-row one-per-CU instance's outputs bit for bit (the same per-element arithmetic), every BN mode included:
+    plain, statistics (mode 1) with the producing BN applied in the staging, and masked gradient (mode 2)."""
+    from mzba import _lib as L
+    from mzba.agent import pack_lat
+    dev = torch.device("cuda")
+    H, W = 4, 5
+    g = torch.Generator().manual_seed(11 * B + Cout)
+    x = torch.randn(B * H * W, Cin, generator=g).to(torch.bfloat16).to(dev)
+    w = torch.randn(Cout, Cin, ks, ks, generator=g) / (Cin * ks * ks) ** 0.5
+    wf = torch.from_numpy(pack_lat(w.permute(0, 2, 3, 1).reshape(Cout, -1).numpy(), Cout, ks, Cin)).to(
+        torch.bfloat16).to(dev)
+    bias = torch.randn(Cout, generator=g).to(dev) * 0.1
+    res = torch.randn(B * H * W, Cout, generator=g).to(torch.bfloat16).to(dev)
+    st = torch.randn(4, Cin, generator=g).to(dev)
+    pres = torch.randn(B * H * W, Cin, generator=g).to(torch.bfloat16).to(dev)
+    by = torch.relu(torch.randn(B * H * W, Cout, generator=g)).to(torch.bfloat16).to(dev)
+    bx = torch.randn(B * H * W, Cout, generator=g).to(torch.bfloat16).to(dev)
+    smean = torch.randn(Cout, generator=g).to(dev)
+
+    def run(variant):
+        L.call("mzba_conv_lat_set_variant", variant)
+        try:
+            outs = []
+            o = torch.empty(B * H * W, Cout, dtype=torch.bfloat16, device=dev)
+            L.call("mzba_conv_lat", L.ptr(x), H * W * Cin, None, 0, L.ptr(wf), L.ptr(bias), None, None, 0, L.ptr(res),
+                   L.ptr(o), B, H, W, Cin, Cout, ks, 1, L.stream())
+            outs.append(o)
+            if Cout % 128 == 0:
+                nc, rpc = ctypes.c_int(), ctypes.c_int()
+                L.call("mzba_conv_lat_bn_chunks", B, H, W, Cin, Cout, ks, ctypes.byref(nc), ctypes.byref(rpc))
+                for mode in (1, 2):
+                    part = torch.zeros(nc.value * Cout * 2, device=dev)
+                    o = res.clone()
+                    po = torch.empty_like(x)
+                    L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), L.ptr(o) if mode == 2 else None,
+                           L.ptr(o), B, H, W, Cin, Cout, ks, mode, L.ptr(part), L.ptr(by) if mode == 2 else None,
+                           L.ptr(bx) if mode == 2 else None, L.ptr(smean) if mode == 2 else None, L.ptr(st),
+                           L.ptr(pres), 1, L.ptr(po), None, L.stream())
+                    outs += [o, part, po]
+            torch.cuda.synchronize()
+            return outs
+        finally:
+            L.call("mzba_conv_lat_set_variant", 0)
+    L.call("mzba_conv_lat_set_variant", 3)
+    nc3 = ctypes.c_int(); rpc3 = ctypes.c_int()
+    L.call("mzba_conv_lat_bn_chunks", B, H, W, Cin, Cout, ks, ctypes.byref(nc3), ctypes.byref(rpc3))
+    L.call("mzba_conv_lat_set_variant", 0)
+    assert rpc3.value == (96 // (H * W)) * H * W  # variant 3 always takes the 3-row tiles
+    a, b = run(0), run(3)  # these shapes: variant 0 takes 3-row tiles too (B = 1: one 20-row chunk either way)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
 
 
 def _conv_lat_bn_case(B, H, W, Cin, Cout, ks):
@@ -561,6 +617,115 @@ def _conv_lat_bn_case(B, H, W, Cin, Cout, ks):
     torch.testing.assert_close(dg1, dg2, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db1, db2, rtol=1e-4, atol=1e-3)
     assert (dx1.float() - dx2.float()).abs().max().item() <= 1e-2 * dx2.float().abs().max().item()
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("B,H,W,Cin,Cout,ks", [(512, 4, 5, 256, 256, 3), (37, 4, 5, 256, 128, 3),
+                                                (19, 4, 5, 128, 256, 1), (64, 8, 10, 256, 256, 3), (1, 4, 5, 256, 256, 3)])
+def test_conv_lat_bn_fin_matches_separate_finalisers(B, H, W, Cin, Cout, ks, variant):
+    """mzba_conv_lat_bn_fin (the consuming BN's finaliser folded into the producing launch by its last workgroup per
+    column block, sc1 hand-off) against mzba_conv_lat_bn followed by the separate finaliser launches on the SAME
+    partials: outputs and partials bit for bit; mode 1 stats and running statistics, mode 2 coef / dgamma / dbeta
+    within f32 rounding of the other fold order (rtol 2e-6: both fold in double); the counter words are zero again
+    after every launch, and a second launch on the same words gives the same bits (the reset works). variant 0 at
+    B = 512 = 3-row tiles, 128 chunks per column block (the finaliser's register cache holds 64: the reload path)."""
+    from mzba import _lib as L
+    from mzba.agent import pack_lat
+    L.call("mzba_conv_lat_set_variant", variant)
+    try:
+        dev = torch.device("cuda")
+        g = torch.Generator().manual_seed(3 * B + Cout)
+        x = torch.randn(B * H * W, Cin, generator=g).to(torch.bfloat16).to(dev)
+        w = torch.randn(Cout, Cin, ks, ks, generator=g) / (Cin * ks * ks) ** 0.5
+        wf = torch.from_numpy(pack_lat(w.permute(0, 2, 3, 1).reshape(Cout, -1).numpy(), Cout, ks, Cin)).to(
+            torch.bfloat16).to(dev)
+        bias = torch.randn(Cout, generator=g).to(dev) * 0.1
+        M = B * H * W
+        nc, rpc = ctypes.c_int(), ctypes.c_int()
+        L.call("mzba_conv_lat_bn_chunks", B, H, W, Cin, Cout, ks, ctypes.byref(nc), ctypes.byref(rpc))
+        ctr = torch.zeros(Cout // 128 + 3, dtype=torch.int32, device=dev)
+        gamma, beta = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+        # mode 1
+        pa, pb = torch.empty(nc.value * Cout * 2, device=dev), torch.empty(nc.value * Cout * 2, device=dev)
+        ta, tb = (torch.empty(M, Cout, dtype=torch.bfloat16, device=dev) for _ in range(2))
+        L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), None, L.ptr(ta), B, H, W, Cin, Cout, ks, 1,
+               L.ptr(pa), None, None, None, None, None, 0, None, None, L.stream())
+        sa = torch.empty(4, Cout, device=dev)
+        rma, rva = torch.randn(Cout, device=dev), torch.rand(Cout, device=dev) + 0.5
+        rmb, rvb = rma.clone(), rva.clone()
+        L.call("mzba_bn_stats_final", L.ptr(pa), nc.value, rpc.value, M, Cout, 1e-5, 0.1, L.ptr(gamma), L.ptr(beta),
+               L.ptr(sa), L.ptr(rma), L.ptr(rva), L.stream())
+        sbs = []
+        for rep in range(2):
+            sb = torch.empty(4, Cout, device=dev)
+            L.call("mzba_conv_lat_bn_fin", L.ptr(x), L.ptr(wf), L.ptr(bias), None, L.ptr(tb), B, H, W, Cin, Cout, ks,
+                   1, L.ptr(pb), None, None, None, None, None, 0, None, None, L.ptr(ctr), 1e-5, 0.1, L.ptr(gamma),
+                   L.ptr(beta), L.ptr(sb), L.ptr(rmb) if rep == 0 else None, L.ptr(rvb) if rep == 0 else None, None,
+                   None, None, L.stream())
+            torch.cuda.synchronize()
+            assert int(ctr.abs().sum()) == 0
+            sbs.append(sb)
+        assert torch.equal(ta, tb) and torch.equal(pa, pb)
+        assert torch.equal(sbs[0], sbs[1])
+        torch.testing.assert_close(sbs[0], sa, rtol=2e-6, atol=1e-7)
+        torch.testing.assert_close(rmb, rma, rtol=2e-6, atol=1e-7)
+        torch.testing.assert_close(rvb, rva, rtol=2e-6, atol=1e-7)
+        # mode 2: the conv output is a BN output gradient (BN input bx, output by, stats sa)
+        by = torch.relu(torch.randn(M, Cout, generator=g)).to(torch.bfloat16).to(dev)
+        bx = torch.randn(M, Cout, generator=g).to(torch.bfloat16).to(dev)
+        acc = torch.randn(M, Cout, generator=g).to(torch.bfloat16).to(dev)
+        ga, gb = acc.clone(), acc.clone()
+        L.call("mzba_conv_lat_bn", L.ptr(x), L.ptr(wf), L.ptr(bias), L.ptr(ga), L.ptr(ga), B, H, W, Cin, Cout, ks, 2,
+               L.ptr(pa), L.ptr(by), L.ptr(bx), L.ptr(sa), None, None, 0, None, None, L.stream())
+        dga, dba = torch.randn(Cout, device=dev), torch.randn(Cout, device=dev)
+        dgb, dbb = dga.clone(), dba.clone()
+        ca, cb = torch.empty(3 * Cout, device=dev), torch.empty(3 * Cout, device=dev)
+        L.call("mzba_bn_backward_coef", L.ptr(pa), nc.value, M, Cout, L.ptr(sa), L.ptr(dga), L.ptr(dba), L.ptr(ca),
+               L.stream())
+        L.call("mzba_conv_lat_bn_fin", L.ptr(x), L.ptr(wf), L.ptr(bias), L.ptr(gb), L.ptr(gb), B, H, W, Cin, Cout, ks,
+               2, L.ptr(pb), L.ptr(by), L.ptr(bx), L.ptr(sa), None, None, 0, None, None, L.ptr(ctr), 1e-5, 0.1, None,
+               None, L.ptr(sa), None, None, L.ptr(dgb), L.ptr(dbb), L.ptr(cb), L.stream())
+        torch.cuda.synchronize()
+        assert int(ctr.abs().sum()) == 0
+        assert torch.equal(ga, gb) and torch.equal(pa, pb)
+        torch.testing.assert_close(cb, ca, rtol=2e-6, atol=1e-9)
+        torch.testing.assert_close(dgb, dga, rtol=2e-6, atol=1e-6)
+        torch.testing.assert_close(dbb, dba, rtol=2e-6, atol=1e-6)
+    finally:
+        L.call("mzba_conv_lat_set_variant", 0)
+
+
+def test_learner_bn_fin_tracks_separate_finalisers():
+    """The bf16 learner with every fused BN finaliser in its producing conv_lat launch (fuse_fin, the default) vs the
+    separate finaliser launches: the same algorithm with another double fold order of the chunk statistics, so a
+    statistic can move by an f32 last place and the chaotic bf16 k-step loss with it (the fused-statistics test's
+    bound: losses within 2e-3 relative over two minibatches); the counter pool is zero after each minibatch, eager and
+    graph-replayed, and the replay equals the eager minibatch bit for bit."""
+    from mzba.config import learner_model_cfg
+    from mzba.learner import Learner
+    from mzba.weights import init_state_dict
+    mcfg = learner_model_cfg()
+    mcfg["latent_channels"] = [128, 128]  # conv_lat widths (the fused path needs Cout % 128 == 0)
+    ring = _random_ring(96, mcfg["state_history_length"], 5, 77)
+    losses = {}
+    for fin in (False, True):
+        ln = Learner(mcfg, init_state_dict(mcfg, 9), K=5, dtype="bf16", fuse_fin=fin)
+        out = [ln.train_minibatch(ring, ring.slots()).cpu() for _ in range(2)]
+        if fin:
+            assert ln._ctr is not None and int(ln._ctr.abs().sum()) == 0 and ln._ctr_i > 0
+            e = Learner(mcfg, init_state_dict(mcfg, 9), K=5, dtype="bf16", fuse_fin=True)
+            r = Learner(mcfg, init_state_dict(mcfg, 9), K=5, dtype="bf16", fuse_fin=True)
+            sl = ring.slots()
+            le = [e.train_minibatch(ring, sl).cpu() for _ in range(3)]
+            r.train_minibatch(ring, sl)
+            r.capture(ring, sl.numel())
+            lr = [r.train_minibatch(ring, sl).cpu() for _ in range(2)]
+            torch.cuda.synchronize()
+            assert torch.equal(le[1], lr[0]) and torch.equal(le[2], lr[1])
+            assert int(r._ctr.abs().sum()) == 0
+        losses[fin] = out
+    for a, b in zip(losses[True], losses[False]):
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=1e-5)
 
 
 def test_learner_fused_bn_statistics_track_separate_passes():
