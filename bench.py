@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--minibatch", type=int, default=512, help="learner workload minibatch (config.yaml:7)")
     ap.add_argument("--parity-envs", type=int, default=512,
                     help="config 3 geometry: envs of the f32 parity-path replay (the first ones of the batch)")
+    ap.add_argument("--halo-form", type=int, default=None, choices=[0, 1, 2],
+                    help="conv_halo pixels per workgroup (mzba_conv_halo_set_form; default: the library's)")
     ap.add_argument("--no-halo", action="store_true",
                     help="A/B: large-image 3x3 convs on conv_big_bf16_kernel instead of the halo-tiled conv_halo_kernel")
     ap.add_argument("--pow-threads", type=int, default=1,
@@ -681,6 +683,8 @@ def main():
 
     if args.tower_variant:
         L.call("mzba_tower_set_variant", args.tower_variant)
+    if args.halo_form is not None:
+        L.call("mzba_conv_halo_set_form", args.halo_form)
     cfg = default_config()
     cfg["num_simulations"] = args.sims
     mcfg = cfg["model"]

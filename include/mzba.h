@@ -122,6 +122,13 @@ int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot,
 /* Waves per workgroup of the Cin 256 one-block halo instances: 0 default (8), 4, 8; -1 otherwise. Outputs are
  * identical for every choice (each accumulator takes its taps in the same order). */
 int mzba_conv_halo_set_waves(int nw);
+/* Pixels per workgroup of the Cin 256 / Cout 256 halo instances. 256-pixel form: all 256 channels staged at once
+ * where the halo fits (W <= 23), else two 128-channel blocks, one workgroup per CU; 128-pixel form: two staged
+ * 128-channel blocks within 80 KiB and <= 128 VGPRs, two workgroups per CU. 0 (default): the 128-pixel form where
+ * the 256-pixel form stages two blocks anyway (W > 23; the same k order, the same bits); 1: the 128-pixel form
+ * wherever it fits (at W <= 23 each output's taps sum block by block: bf16-rounding-level differences); 2: never;
+ * -1 otherwise. */
+int mzba_conv_halo_set_form(int f);
 /* f32-faithful 3x3 conv on bf16 MFMAs (the f32 parity path's latent towers, networks.py:19-35): f32 NHWC in /
  * out, out = act(conv3x3(in) + bias (+ res)); every f32 operand split into three bf16 parts and each product
  * taken as the six terms down to 2^-18 (csrc/conv_x6.hip), as close to exact as an f32 conv. wx = the three

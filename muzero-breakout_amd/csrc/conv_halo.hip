@@ -190,21 +190,25 @@ MZ_DEV void halo_epilogue(const HaloArgs& a, const f32x4 (&acc)[MT][CT], int mb,
 // 21x21): WM = 1 (8 slices of 32 channels over all 256 pixels: no weight fragment loaded twice per workgroup,
 // half the per-CU L2 weight stream, twice the B reads) 1.76-1.85 ms vs 1.75-1.83; B fragments read 16 MFMAs
 // ahead instead of 8: 1.82-1.83 ms. Neither the weight stream nor the LDS read latency bounds this kernel.
-template <int CB, int NBLK, int WM = 2, int PFM = 1, int TN = hl::TN, bool GA = false, int NW = 8>
-__global__ __launch_bounds__(64 * NW, 1) void conv_halo_kernel(HaloArgs a) {
+// TMW: output pixels per workgroup; OCC: workgroups per CU the register budget allows (2: the 128-pixel instance,
+// <= 128 VGPRs at 8 waves, two 128-channel staged blocks of ~44 KiB, so two workgroups share a CU and one's staging
+// and epilogue run beside the other's k loop); PFX > 0 sets the fragment read-ahead directly.
+template <int CB, int NBLK, int WM = 2, int PFM = 1, int TN = hl::TN, bool GA = false, int NW = 8, int TMW = hl::TM,
+          int OCC = 1, int PFX = 0>
+__global__ __launch_bounds__(64 * NW, OCC == 1 ? 1 : OCC * NW / 4) void conv_halo_kernel(HaloArgs a) {
   constexpr int RB = CB * 2;        // bytes per staged row
   constexpr int NC = CB / 8;        // 16-B chunks per row
   constexpr int NCS = CB / 32;      // 32-channel k steps per tap and block
-  constexpr int WN = NW / WM, CT = TN / 16 / WN, MT = 16 / WM;  // channel slices, column tiles / pixel tiles per wave
+  constexpr int WN = NW / WM, CT = TN / 16 / WN, MT = TMW / 16 / WM;  // channel slices, column / pixel tiles per wave
   constexpr int NT = 64 * NW;
-  constexpr int PF = PFM * 8 / CT;  // fragment reads ahead: 8 PFM MFMAs
+  constexpr int PF = PFX > 0 ? PFX : PFM * 8 / CT;  // fragment reads ahead: 8 PFM MFMAs
   static_assert(NCS % 2 == 0, "ring slot = channel step parity");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;  // pixel part (TM / WM), channel slice (16 CT)
   const int q = lane >> 4, n = lane & 15;
-  const int m0 = blockIdx.x * hl::TM, n0 = blockIdx.y * TN;
+  const int m0 = blockIdx.x * TMW, n0 = blockIdx.y * TN;
   const int HW = a.H * a.W;
   // GA: element offset of staged row m = eoff[m >= sb1] + m Cin (the range's two envs, b env_stride + slot[b]
   // slot_stride - b H W Cin)
@@ -225,11 +229,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_halo_kernel(HaloArgs a) {
   // per pixel tile mi of the wave: the lane's pixel is staged row prow0 + 16 mi at tap (0, 0); byte mi of
   // okw[mi / 4] says which taps stay in the image (bit 0: y > 0, 1: y < H - 1, 2: x > 0, 3: x < W - 1,
   // 4: the pixel exists — rows past M read only the zero block)
-  int prow0 = wm * (hl::TM / WM) + n + a.HALO;
+  int prow0 = wm * (TMW / WM) + n + a.HALO;
   uint32_t okw[MT / 4] = {};
 #pragma unroll
   for (int mi = 0; mi < MT; ++mi) {
-    const int m = m0 + wm * (hl::TM / WM) + mi * 16 + n;
+    const int m = m0 + wm * (TMW / WM) + mi * 16 + n;
     if (m < a.M) {
       const int p = m % HW, y = p / a.W, x = p - y * a.W;
       const uint32_t b = 16u | (y > 0 ? 1u : 0u) | (y < a.H - 1 ? 2u : 0u) | (x > 0 ? 4u : 0u) | (x < a.W - 1 ? 8u : 0u);
@@ -341,19 +345,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_halo_kernel(HaloArgs a) {
 
   // epilogue: acc[mi][ct] = D[channel n0 + 16 CT wn + 16 ct + 4q + i][pixel m0 + TM / WM wm + 16 mi + n]
   if (GA && a.act_bias)
-    halo_epilogue<false, GA>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
+    halo_epilogue<false, GA>(a, acc, m0 + wm * (TMW / WM), n0 + wn * 16 * CT, q, n);
   else if (a.res)
-    halo_epilogue<true, false>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
+    halo_epilogue<true, false>(a, acc, m0 + wm * (TMW / WM), n0 + wn * 16 * CT, q, n);
   else
-    halo_epilogue<false, false>(a, acc, m0 + wm * (hl::TM / WM), n0 + wn * 16 * CT, q, n);
+    halo_epilogue<false, false>(a, acc, m0 + wm * (TMW / WM), n0 + wn * 16 * CT, q, n);
 }
 
 // staging geometry for a (W, Cin) pair: the whole Cin staged at once where it fits (one block), else Cin 256 in two
 // 128-channel blocks (the blocks unrolled: a rolled loop would carry the accumulators across its back edge, which
 // the compiler renames and copies); 0 if the halo does not fit the LDS
-int halo_geometry(int W, int Cin, HaloArgs& g) {
-  for (int cb = Cin; cb >= 128; cb /= 2) {
-    const int halo = W + 1, hr = hl::TM + 2 * halo, rb = cb * 2;
+int halo_geometry(int W, int Cin, HaloArgs& g, int tm = hl::TM, int cb_max = 256) {
+  for (int cb = Cin < cb_max ? Cin : cb_max; cb >= 128; cb /= 2) {
+    const int halo = W + 1, hr = tm + 2 * halo, rb = cb * 2;
     const int ni = (hr * rb + 1023) / 1024;
     const int zoff = (ni * 1024 + 16 * rb - 1) / (16 * rb) * (16 * rb);  // the 16-row zero block, 16-row aligned
     if ((Cin != 128 && Cin != 256) || zoff + 16 * rb > hl::LDS_MAX) continue;
@@ -366,6 +370,7 @@ int halo_geometry(int W, int Cin, HaloArgs& g) {
 }  // namespace
 
 static int g_halo_waves = 0;
+static int g_halo_form = 0;
 
 extern "C" {
 
@@ -374,6 +379,20 @@ extern "C" {
 int mzba_conv_halo_set_waves(int nw) {
   if (nw != 0 && nw != 4 && nw != 8) return -1;
   g_halo_waves = nw;
+  return 0;
+}
+
+// pixels per workgroup of the Cin 256 / Cout 256 instances. The 256-pixel form stages all 256 input channels at once
+// (one workgroup per CU) where its halo fits the LDS (W <= 23), else two 128-channel blocks; the 128-pixel form (8
+// waves of 128 pixels x 32 channels, two staged 128-channel blocks of <= 80 KiB, <= 128 VGPRs: two workgroups per CU,
+// one's staging / epilogue beside the other's k loop) takes each output's taps in the two-block order.
+// 0 (default): the 128-pixel form where the 256-pixel form would stage two blocks anyway (W > 23: config 3's 42x42
+// and 84x84 256-channel convs) — the same k order, so the same bits; 1: the 128-pixel form wherever it fits (the
+// 21x21 convs too: block order, bf16-rounding-level differences; measured slower there, profiles/r06/halo_form/);
+// 2: never (the round-5 kernels, A/B reference).
+int mzba_conv_halo_set_form(int f) {
+  if (f < 0 || f > 2) return -1;
+  g_halo_form = f;
   return 0;
 }
 
@@ -407,10 +426,31 @@ int mzba_conv_halo_ex(const void* in, long long env_stride, const int32_t* slot,
   MZ_CHECK_ARG(M + 2 * hl::TM < (1LL << 31), -3);  // pixel indices in int (global offsets are size_t)
   HaloArgs a{(const bf16_t*)in, (const bf16_t*)wh, bias, (const bf16_t*)res, (bf16_t*)out, (int)M, H, W, Cin, Cout, relu};
   a.slot = slot, a.env_stride = env_stride, a.slot_stride = slot_stride, a.act_bias = act_bias, a.act = act, a.A = A;
-  const int lds = halo_geometry(W, Cin, a);
   const int tn = Cout % 256 == 0 ? 256 : 128;
-  const dim3 grid((unsigned)((M + hl::TM - 1) / hl::TM), (unsigned)(Cout / tn));
   typedef void (*Kern)(HaloArgs);
+  HaloArgs g0{};
+  const bool two_blocks = halo_geometry(W, Cin, g0) > 0 && g0.CB < Cin;  // the 256-pixel form's staging
+  if (Cin == 256 && tn == 256 && (g_halo_form == 1 || (g_halo_form == 0 && two_blocks && !ga))) {  // 128-pixel form
+    HaloArgs g{};
+    const int lds1 = halo_geometry(W, Cin, g, 128, 128);
+    if (lds1 > 0 && lds1 <= 80 * 1024 && g.CB == 128 && (!ga || g.HR <= H * W)) {
+      a.HALO = g.HALO, a.HR = g.HR, a.CB = g.CB, a.NI = g.NI, a.ZOFF = g.ZOFF;
+      static const Kern k1[2] = {conv_halo_kernel<128, 2, 1, 1, 256, false, 8, 128, 2, 2>,
+                                 conv_halo_kernel<128, 2, 1, 1, 256, true, 8, 128, 2, 2>};
+      static const bool attrs1 = [] {
+        for (Kern k : k1)
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        return true;
+      }();
+      (void)attrs1;
+      const dim3 grid1((unsigned)((M + 127) / 128), (unsigned)(Cout / 256));
+      hipLaunchKernelGGL(k1[ga ? 1 : 0], grid1, dim3(hl::NT), lds1, stream, a);
+      MZ_LAUNCH_CHECK();
+      return 0;
+    }
+  }
+  const int lds = halo_geometry(W, Cin, a);
+  const dim3 grid((unsigned)((M + hl::TM - 1) / hl::TM), (unsigned)(Cout / tn));
   static const Kern kerns[8] = {conv_halo_kernel<256, 1, 2, 1, 256, true>, conv_halo_kernel<256, 1, 4, 1, 128>,
                                 conv_halo_kernel<256, 1>, conv_halo_kernel<128, 1>, conv_halo_kernel<128, 2>,
                                 conv_halo_kernel<128, 1, 4, 1, 128>, conv_halo_kernel<256, 1, 2, 1, 256, true, 4>,

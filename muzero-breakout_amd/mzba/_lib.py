@@ -100,6 +100,7 @@ SIGNATURES = {
     "mzba_conv_pack_bf16": [P, P, I, I, I, I, I, I, I, LL, P],
     "mzba_conv_pack_bf16_multi": [P, P, P, I, P],
     "mzba_conv_halo_set_waves": [I],
+    "mzba_conv_halo_set_form": [I],
     "mzba_conv_wgrad_set_variant": [I],
     "mzba_conv_wgrad_set_form": [I],
     "mzba_conv_wgrad": [I, P, P, I, I, I, I, I, I, P, P, P, LL, P],

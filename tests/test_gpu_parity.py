@@ -601,11 +601,15 @@ def test_conv_big_kernel_vs_torch_fp32(B, H, W, Cin, Cout, ks, relu):
                                                           (3, 21, 21, 256, 512, 1, True), (37, 21, 21, 256, 128, 1, False),
                                                           (20, 21, 21, 256, 128, 0, True), (5, 84, 84, 256, 256, 1, True),
                                                           (9, 42, 42, 256, 256, 0, False), (6, 84, 84, 128, 128, 1, True)])
-def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res):
+@pytest.mark.parametrize("form", [0, 1, 2])
+def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res, form):
     """The halo-tiled 3x3 conv (mzba_conv_halo: config 3's 21x21 latent convs and 84x84 128 -> 256 conv; 256
     output pixels + W + 1 halo rows staged once per workgroup, every tap read from LDS, taps leaving the image
     redirected to a zero row) vs a torch fp32 conv of the same bf16 operands (+ bias, residual, ReLU), ragged
-    pixel counts (the last tile partial), tiles crossing env boundaries; and close to conv_big_bf16_kernel."""
+    pixel counts (the last tile partial), tiles crossing env boundaries; and close to conv_big_bf16_kernel.
+    form (mzba_conv_halo_set_form): 0 the default (the 128-pixel two-workgroups-per-CU instance at W > 23, Cin =
+    Cout = 256), 1 that instance wherever it fits, 2 the round-5 kernels; at W > 23 forms 0 / 1 equal form 2 bit for
+    bit (the same two-block k order)."""
     from mzba import _lib as L
     from mzba.agent import pack_lat16
     assert L.lib().mzba_conv_halo_supported(H, W, Cin, Cout, 3)
@@ -621,13 +625,28 @@ def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res):
         ref = torch.relu(ref)
     wh = torch.tensor(pack_lat16(w.float().cpu().numpy().reshape(Cout, -1), Cout, 3, Cin)).to(torch.bfloat16).cuda()
     out = torch.full((B, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
-    L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu, L.stream())
+    assert L.lib().mzba_conv_halo_set_form(form) == 0
+    try:
+        L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, relu,
+               L.stream())
+    finally:
+        L.lib().mzba_conv_halo_set_form(0)
     big = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=dev)
     L.call("mzba_conv2d", 1, L.ptr(x), H * W * Cin, None, 0, L.ptr(w), L.ptr(b), None, None, 0, L.ptr(res), L.ptr(big),
            B, H, W, Cin, Cout, 3, relu, L.stream())
     torch.cuda.synchronize()
     got = out.float()
     assert torch.isfinite(got).all()
+    if W > 23 and Cin == Cout == 256 and form != 2:  # the 128-pixel form where the default takes it: round-5 bits
+        o2 = torch.empty_like(out)
+        assert L.lib().mzba_conv_halo_set_form(2) == 0
+        try:
+            L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(o2), B, H, W, Cin, Cout, relu,
+                   L.stream())
+        finally:
+            L.lib().mzba_conv_halo_set_form(0)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int16), o2.view(torch.int16))
     scale = ref.abs().max().item()
     err = (got - ref).abs().max().item()
     print(f"conv_halo {B}x{H}x{W} {Cin}->{Cout}: max err {err / scale:.2e} of the magnitude, vs conv_big "
@@ -637,7 +656,8 @@ def test_conv_halo_kernel_vs_torch_fp32(B, H, W, Cin, Cout, relu, with_res):
 
 
 @pytest.mark.parametrize("B,S,A", [(37, 5, 3), (150, 1, 3), (9, 50, 4)])
-def test_conv_halo_gather_action_bias_vs_torch_fp32(B, S, A):
+@pytest.mark.parametrize("form", [0, 1])
+def test_conv_halo_gather_action_bias_vs_torch_fp32(B, S, A, form):
     """mzba_conv_halo_ex as config 3's dynamics first conv (networks.py:117-122, 160): every env's input
     gathered from its slot of a latent pool ((S + 1) latents per env), the action planes folded into a
     [HW][A][Cout] bias table (agent.py _conv act_w), ReLU — vs a torch fp32 conv of the gathered bf16 operands
@@ -662,8 +682,12 @@ def test_conv_halo_gather_action_bias_vs_torch_fp32(B, S, A):
     ref = torch.relu(ref)
     wh = torch.tensor(pack_lat16(w.float().cpu().numpy().reshape(Cout, -1), Cout, 3, Cin)).to(torch.bfloat16).cuda()
     out = torch.full((B, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
-    L.call("mzba_conv_halo_ex", L.ptr(pool), (S + 1) * HW * Cin, L.ptr(slot), HW * Cin, L.ptr(wh), L.ptr(b), L.ptr(tab),
-           L.ptr(act), A, None, L.ptr(out), B, H, W, Cin, Cout, 1, L.stream())
+    assert L.lib().mzba_conv_halo_set_form(form) == 0
+    try:
+        L.call("mzba_conv_halo_ex", L.ptr(pool), (S + 1) * HW * Cin, L.ptr(slot), HW * Cin, L.ptr(wh), L.ptr(b),
+               L.ptr(tab), L.ptr(act), A, None, L.ptr(out), B, H, W, Cin, Cout, 1, L.stream())
+    finally:
+        L.lib().mzba_conv_halo_set_form(0)
     ig = torch.empty(B, H, W, Cout, dtype=torch.bfloat16, device=dev)
     L.call("mzba_conv2d", 1, L.ptr(pool), (S + 1) * HW * Cin, L.ptr(slot), HW * Cin, L.ptr(w), L.ptr(b), L.ptr(tab),
            L.ptr(act), A, None, L.ptr(ig), B, H, W, Cin, Cout, 3, 1, L.stream())
@@ -685,7 +709,8 @@ def test_conv_halo_gather_action_bias_vs_torch_fp32(B, S, A):
 
 @pytest.mark.parametrize("B,H,W,Cin,Cout", [(150, 21, 21, 256, 256), (5, 84, 84, 256, 256), (37, 21, 21, 256, 128),
                                             (6, 84, 84, 128, 128)])
-def test_conv_halo_in_place_residual(B, H, W, Cin, Cout):
+@pytest.mark.parametrize("form", [0, 1])
+def test_conv_halo_in_place_residual(B, H, W, Cin, Cout, form):
     """The halo conv written in place over its residual (out aliases res, as a residual block may run it) equals the
     out-of-place result bit for bit: every lane reads its own (pixel, channel) residual elements before it writes
     them. The grid's partial last tile has waves wholly past the last pixel at B = 150 (their action-bias env index
@@ -700,10 +725,15 @@ def test_conv_halo_in_place_residual(B, H, W, Cin, Cout):
     res = torch.randn(B, H, W, Cout, generator=g, device=dev).to(torch.bfloat16)
     wh = torch.tensor(pack_lat16(w.float().cpu().numpy().reshape(Cout, -1), Cout, 3, Cin)).to(torch.bfloat16).cuda()
     out = torch.full((B, H, W, Cout), float("nan"), dtype=torch.bfloat16, device=dev)
-    L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, 1, L.stream())
-    inplace = res.clone()
-    L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(inplace), L.ptr(inplace), B, H, W, Cin, Cout, 1,
-           L.stream())
+    assert L.lib().mzba_conv_halo_set_form(form) == 0
+    try:
+        L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W, Cin, Cout, 1,
+               L.stream())
+        inplace = res.clone()
+        L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(inplace), L.ptr(inplace), B, H, W, Cin, Cout, 1,
+               L.stream())
+    finally:
+        L.lib().mzba_conv_halo_set_form(0)
     torch.cuda.synchronize()
     assert torch.isfinite(out.float()).all()
     assert torch.equal(out.view(torch.int16), inplace.view(torch.int16))

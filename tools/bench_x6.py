@@ -2,8 +2,8 @@
 acting loop's shapes: x6 at the 4x5 latent (B = 4096, the parity path's towers) and 8x10 (the representation
 tail), halo at config 3's 21x21 latent (B = 4096). HIP events around 20 launches after 3 warm-up launches,
 alternated twice. Prints one JSON line per (kernel, shape, variant). The variant setters
-(mzba_conv_x6_set_variant: 3 the pixel-tiled form, 1 the pre-split x6 form; mzba_conv_halo_set_waves: 8 or 4 waves
-per halo workgroup) may be missing from a build; the default then runs once per variant
+(mzba_conv_x6_set_variant: 3 the pixel-tiled form, 1 the pre-split x6 form; mzba_conv_halo_set_form: 0 the 256-pixel
+one-per-CU form, 1 the 128-pixel two-per-CU form; config 3's 21x21 shape, where the default is the 256-pixel form) may be missing from a build; the default then runs once per variant
 slot (variant None).
   python tools/bench_x6.py"""
 import json
@@ -67,15 +67,15 @@ def main():
     out = torch.empty(B, H, W, C, dtype=torch.bfloat16, device=dev)
     fl = 2.0 * B * H * W * C * 9 * C
     for rep in range(3):
-        for v in (8, 4):  # mzba_conv_halo_set_waves (round 5: 8 two per SIMD, 4 one per SIMD); None when absent
-            v = set_variant("mzba_conv_halo_set_waves", v)
+        for v in (2, 1):  # mzba_conv_halo_set_form (round 6: 2 = 256 pixels one per CU, 1 = 128 pixels two per CU)
+            v = set_variant("mzba_conv_halo_set_form", v)
             for res in (x, None):
                 ms = timeit(lambda: L.call("mzba_conv_halo", L.ptr(x), L.ptr(wh), L.ptr(b), L.ptr(res), L.ptr(out), B, H, W,
                                            C, C, 1, L.stream()), n=10)
                 # output checksum (int16 bit patterns, position-weighted): equal across builds = bit-identical
                 h = out.view(torch.int16).flatten().to(torch.int64)
                 ck = int((h * (torch.arange(h.numel(), device=dev) % 65521 + 1)).sum().item())
-                print(json.dumps({"lib": tag, "kernel": "conv_halo", "shape": [B, H, W, C], "waves": v,
+                print(json.dumps({"lib": tag, "kernel": "conv_halo", "shape": [B, H, W, C], "form": v,
                                   "residual": res is not None, "rep": rep, "ms": ms, "tflops": fl / ms / 1e9,
                                   "frac": fl / ms / 1e9 / 2500, "checksum": ck}), flush=True)
     set_variant("mzba_conv_halo_set_waves", 0)
