@@ -886,8 +886,15 @@ struct WgPx {
   const bf16_t* dys[WG_MAXSEG];
 };
 
+// WF (the waves' share of the 64 x 64 x 9 tile): 0 = 32 co x 32 ci x 5 / 4 taps per wave (2 A + 10 B fragment
+// reads per 20 MFMAs); 1 = 64 co x 32 ci x 3 / 2 taps per wave (taps {0,1,2}, {3,4}, {5,6}, {7,8}; 4 A + 6 / 4 B
+// reads per 24 / 16 MFMAs: 29 % fewer LDS fragment reads per stage). A SIMD holds waves w and w + 4, so each
+// SIMD runs one 3-tap and one 2-tap wave (40 MFMAs per k step, as WF 0) or two 2-tap waves. Every output
+// element is the same chain of the same MFMAs over the same fragments in both forms: the same bits.
+template <int WF>
 __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __restrict__ part,
                                                               float* __restrict__ bpart) {
+  constexpr int NT = WF ? 3 : 5, NI = WF ? 4 : 2;  // taps and 16-row co fragments per wave
   extern __shared__ __attribute__((aligned(16))) bf16_t lds_img[];
   bf16_t* ldy = lds_img;                                      // [KS][WI_LD]
   bf16_t* lx = lds_img + (size_t)a.KS * WI_LD;                // [XR + 1][WI_LD], row XR = zeros
@@ -906,8 +913,9 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
   }
   const int cit = tile % nci, cot = tile / nci;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tg = wave >> 2, wr = (wave >> 1) & 1, wc = wave & 1;
-  const int tap0 = 5 * tg, ntap = tg ? 4 : 5;
+  const int wc = wave & 1;
+  const int tg = WF ? wave >> 1 : wave >> 2, wr = WF ? 0 : (wave >> 1) & 1;
+  const int tap0 = WF ? (tg ? 2 * tg + 1 : 0) : 5 * tg, ntap = WF ? (tg ? 2 : 3) : (tg ? 4 : 5);
   const int ch = tid & 7;
   const int co_s = cot * 64 + ch * 8, ci_s = cit * 64 + ch * 8;
   const bool do_bias = bpart && cit == 0;
@@ -927,11 +935,11 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
     }
     tmask[r] = (uint16_t)m;
   }
-  f32x4_t acc[5][2][2];
+  f32x4_t acc[NT][NI][2];
 #pragma unroll
-  for (int t = 0; t < 5; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[t][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
@@ -941,33 +949,42 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
   // the next stage's loads are in flight during this stage's MFMAs. Offsets from the stage's env-0 base
   // are the same for every stage.
   const int nchunk = (a.KS + a.XR) * 8;
-  int soff[WI_PFN];
-  uint32_t sdy = 0u;
-#pragma unroll
-  for (int u = 0; u < WI_PFN; ++u) {
+  // chunk u of a stage: offset from the stage's env-0 base, -1 for a zero chunk (WF 1 recomputes it per stage
+  // instead of holding WI_PFN offsets in registers beside its larger accumulator set)
+  auto chunk_off = [&](int u) {
     int off = -1;
     const int i = u * WI_NT + tid;
     if (i < a.KS * 8) {
       const int r = i >> 3;
       if (r < NR && co_s < a.Cout) off = r * a.Cout + co_s;
-      sdy |= 1u << u;
     } else if (i < nchunk) {
       const int r = (i >> 3) - a.KS;
       if (ci_s < a.Cin) off = r * a.Cin + ci_s;
     }
-    soff[u] = off;
+    return off;
+  };
+  int soff[WF ? 1 : WI_PFN];
+  if constexpr (!WF) {
+#pragma unroll
+    for (int u = 0; u < WI_PFN; ++u) soff[u] = chunk_off(u);
   }
   uint4 pf[WI_PFN];
   auto load_stage = [&](int st) {
     const int b0 = st * a.E, sg = b0 / a.Bseg, bl = b0 - sg * a.Bseg;
     const bf16_t* xb = a.xs[sg] + (size_t)bl * HW * a.Cin;
     const bf16_t* db = a.dys[sg] + (size_t)bl * HW * a.Cout;
+    int offs[WI_PFN];
+#pragma unroll
+    for (int u = 0; u < WI_PFN; ++u) {
+      if constexpr (WF) offs[u] = chunk_off(u);
+      else offs[u] = soff[u];
+    }
 #pragma unroll
     for (int u = 0; u < WI_PFN; ++u)
-      pf[u] = *reinterpret_cast<const uint4*>(((sdy >> u) & 1u ? db : xb) + (soff[u] >= 0 ? soff[u] : 0));
+      pf[u] = *reinterpret_cast<const uint4*>((u * WI_NT + tid < a.KS * 8 ? db : xb) + (offs[u] >= 0 ? offs[u] : 0));
 #pragma unroll
     for (int u = 0; u < WI_PFN; ++u)
-      if (soff[u] < 0) pf[u] = make_uint4(0, 0, 0, 0);
+      if (offs[u] < 0) pf[u] = make_uint4(0, 0, 0, 0);
   };
   auto store_stage = [&]() {
 #pragma unroll
@@ -994,9 +1011,9 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
     for (int ks = 0; ks < a.KS / 32; ++ks) {
       const int r0 = ks * 32 + 4 * g + q, r1 = r0 + 16;
       const uint32_t m0 = tmask[r0], m1 = tmask[r1];
-      bf16x8_t af[2];
+      bf16x8_t af[NI];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < NI; ++i) {
         const int c = wr * 32 + i * 16 + 4 * pp;
         af[i] = tr_frag_at(ldy + (size_t)r0 * WI_LD + c, ldy + (size_t)r1 * WI_LD + c);
       }
@@ -1012,11 +1029,11 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
       bf16x8_t bcur[2], bnxt[2];
       bload(tap0, bcur);
 #pragma unroll
-      for (int tt = 0; tt < 5; ++tt) {
-        if (tt < ntap) {  // wave-uniform: tap group 1 has 4 taps
+      for (int tt = 0; tt < NT; ++tt) {
+        if (tt < ntap) {  // wave-uniform: the last tap group(s) have one tap fewer
           if (tt + 1 < ntap) bload(tap0 + tt + 1, bnxt);
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < NI; ++i)
 #pragma unroll
             for (int j = 0; j < 2; ++j)
               acc[tt][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[tt][i][j], 0, 0, 0);
@@ -1029,9 +1046,9 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
   float* outp = part + (size_t)split * a.Cout * K;
   const int fr = lane & 15, fk = lane >> 4;
 #pragma unroll
-  for (int tt = 0; tt < 5; ++tt)
+  for (int tt = 0; tt < NT; ++tt)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int t = tap0 + tt;
@@ -1730,11 +1747,12 @@ int mzba_conv_wgrad_set_variant(int v) {
   g_wgrad_img = v;
   return 0;
 }
-// which whole-image kernel: 1 (default) pixel rows (conv_wgrad_px_kernel), 0 zero-bordered images
-// (conv_wgrad_img_kernel, the round-5 form, for A/B)
-static thread_local int g_wgrad_form = 1;
+// which whole-image kernel: 2 (default) pixel rows with 64-co wave tiles (conv_wgrad_px_kernel<1>), 1 pixel
+// rows with 32-co wave tiles (conv_wgrad_px_kernel<0>, the same bits, 3-6 % slower per launch), 0 zero-bordered
+// images (conv_wgrad_img_kernel, the round-5 form); 1 and 0 for A/B
+static thread_local int g_wgrad_form = 2;
 int mzba_conv_wgrad_set_form(int v) {
-  if (v < 0 || v > 1) return -1;
+  if (v < 0 || v > 2) return -1;
   g_wgrad_form = v;
   return 0;
 }
@@ -1769,12 +1787,15 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
   for (int i = 0; i < nseg; ++i) MZ_CHECK_ARG(xs[i] && dys[i], -1);
   MZ_CHECK_ARG(mzba_conv_wgrad_ws_bytes(nseg * B, H, W, Cin, Cout, ks) <= ws_bytes, -2);
   WgPxPlan pxp;
-  if (g_wgrad_form == 1 && wgrad_img_eligible(dtype, nseg, B, H, W, Cin, Cout, ks) &&
+  if (g_wgrad_form >= 1 && wgrad_img_eligible(dtype, nseg, B, H, W, Cin, Cout, ks) &&
       wgrad_px_plan(nseg * B, B, H, W, Cin, Cout, pxp)) {
     static bool attr = false;
     if (!attr) {
-      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_px_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)WI_LDS_MAX);
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_px_kernel<0>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)WI_LDS_MAX);
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_px_kernel<1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)WI_LDS_MAX);
       if (e != hipSuccess) return (int)e;
       attr = true;
     }
@@ -1785,8 +1806,12 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
     const size_t nwi = (size_t)Cout * 9 * Cin;
     float* ipart = (float*)ws;
     float* ibpart = db ? ipart + (size_t)pxp.nsplit * nwi : nullptr;
-    hipLaunchKernelGGL(conv_wgrad_px_kernel, dim3(pxp.a.tiles, pxp.nsplit), dim3(WI_NT), pxp.lds, stream, pxp.a,
-                       ipart, ibpart);
+    if (g_wgrad_form == 2)
+      hipLaunchKernelGGL(conv_wgrad_px_kernel<1>, dim3(pxp.a.tiles, pxp.nsplit), dim3(WI_NT), pxp.lds, stream, pxp.a,
+                         ipart, ibpart);
+    else
+      hipLaunchKernelGGL(conv_wgrad_px_kernel<0>, dim3(pxp.a.tiles, pxp.nsplit), dim3(WI_NT), pxp.lds, stream, pxp.a,
+                         ipart, ibpart);
     const size_t nbi = db ? (size_t)Cout : 0;
     hipLaunchKernelGGL(sum_partials2_kernel, dim3(grid_for(nwi + nbi)), dim3(256), 0, stream, (const float*)ipart,
                        (const float*)ibpart, pxp.nsplit, nwi, nbi, dw, db);

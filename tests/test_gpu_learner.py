@@ -340,13 +340,14 @@ def test_learner_bf16_conv_packs(case, flip):
                                   ("bf16", 1, 3, 7, 4, 5, 64, 64), ("f32", 1, 2, 6, 4, 5, 40, 24),
                                   ("bf16", 2, 8, 16, 8, 10, 128, 128), ("bf16", 2, 3, 24, 3, 7, 64, 72),
                                   ("bf16", 2, 2, 4, 16, 20, 128, 256)])
-@pytest.mark.parametrize("form", [1, 0])
+@pytest.mark.parametrize("form", [2, 1, 0])
 def test_conv_wgrad_segs_matches_torch(case, form):
     """mzba_conv_wgrad_segs (the learner's deferred latent weight gradient: K (x, dY) pairs in
     one contraction) against the torch fp32 weight gradient of the concatenated segments.
     variant 1 = automatic (5 x 512 envs at 4x5 -> whole-image kernel, small batches -> one
     per-tap launch pair per segment), 2 = whole-image kernel forced. form 1 = the pixel-row
-    whole-image kernel (default), 0 = the zero-bordered one (the 3x7 case: HW = 21, odd rows per
+    whole-image kernel with 32-co wave tiles, 2 = the same with 64-co wave tiles (default), 0 = the
+    zero-bordered one (the 3x7 case: HW = 21, odd rows per
     stage; the bordered form refuses it and the per-tap kernel runs)."""
     from mzba import _lib as L
     dt, var, nseg, B, H, W, Cin, Cout = case
@@ -369,7 +370,7 @@ def test_conv_wgrad_segs_matches_torch(case, form):
                L.ptr(db), L.ptr(ws), nb, L.stream())
     finally:
         L.call("mzba_conv_wgrad_set_variant", 1)
-        L.call("mzba_conv_wgrad_set_form", 1)
+        L.call("mzba_conv_wgrad_set_form", 2)
     x = torch.cat(xs).float().permute(0, 3, 1, 2)
     dy = torch.cat(dys).float().permute(0, 3, 1, 2)
     ref = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dy, padding=1)
@@ -378,6 +379,42 @@ def test_conv_wgrad_segs_matches_torch(case, form):
     tol = 1e-4 if dt == "f32" else 2e-3
     assert (dw - ref).abs().max().item() <= tol * ref.abs().max().item()
     assert (db - refb).abs().max().item() <= tol * refb.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("case", [(5, 512, 4, 5, 256, 256), (5, 512, 4, 5, 264, 256), (5, 512, 4, 5, 256, 128),
+                                  (1, 512, 8, 10, 256, 256), (1, 512, 16, 20, 128, 128), (2, 24, 3, 7, 64, 72)])
+def test_conv_wgrad_px_wave_tile_forms_bit_identical(case):
+    """The pixel-row weight gradient's two wave decompositions (form 1: 32 co x 32 ci x 5 / 4 taps per wave;
+    form 2: 64 co x 32 ci x 3 / 2 taps per wave) give the same bits: every output element is the same chain of
+    the same MFMAs over the same fragments (the learner's shapes, the representation's, a ragged one)."""
+    from mzba import _lib as L
+    nseg, B, H, W, Cin, Cout = case
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(7 * nseg + B)
+    xs = [torch.randn(B, H, W, Cin, generator=g, device=dev).to(torch.bfloat16) for _ in range(nseg)]
+    dys = [torch.randn(B, H, W, Cout, generator=g, device=dev).to(torch.bfloat16) for _ in range(nseg)]
+    dw0 = torch.randn(Cout, 9, Cin, generator=g, device=dev)
+    db0 = torch.randn(Cout, generator=g, device=dev)
+    nb = L.lib().mzba_conv_wgrad_ws_bytes(nseg * B, H, W, Cin, Cout, 3)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    xp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in xs])
+    dp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in dys])
+    outs = []
+    L.call("mzba_conv_wgrad_set_variant", 2)
+    try:
+        for form in (1, 2):
+            L.call("mzba_conv_wgrad_set_form", form)
+            dw, db = dw0.clone(), db0.clone()
+            L.call("mzba_conv_wgrad_segs", 1, xp, dp, nseg, B, H, W, Cin, Cout, 3, L.ptr(dw), L.ptr(db), L.ptr(ws),
+                   nb, L.stream())
+            torch.cuda.synchronize()
+            outs.append((dw, db))
+    finally:
+        L.call("mzba_conv_wgrad_set_variant", 1)
+        L.call("mzba_conv_wgrad_set_form", 2)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    assert not torch.equal(outs[0][0], dw0)
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])

@@ -4,7 +4,7 @@ K = 5), 2 eager minibatches whose gradients and parameters are hashed (sha256 of
 must be bit-identical are checked on the same seeded input), then the minibatch as one HIP graph, median of
 HIP-event times over 10 replays.
 usage (GPU box): MZBA_LIB=muzero-breakout_amd/mzba/libmzba_base.so python tools/ab_lib_learner.py [bf16|f32]
-MZBA_WGRAD_FORM=0|1 picks the whole-image weight-gradient form of the one build (mzba_conv_wgrad_set_form)."""
+MZBA_WGRAD_FORM=0|1|2 picks the whole-image weight-gradient form of the one build (mzba_conv_wgrad_set_form)."""
 import hashlib
 import json
 import os

@@ -1,0 +1,5 @@
+set -e
+D=gpurun_out/wgrad_wf; mkdir -p $D
+timeout -k 10 300 python -u -m pytest tests/test_gpu_learner.py -x -q -k "wgrad" --timeout 120 --timeout-method thread > $D/pytest_wgrad.log 2>&1
+for f in 1 2 1 2; do MZBA_WGRAD_FORM=$f timeout -k 10 200 python tools/ab_lib_learner.py bf16 >> $D/ab.jsonl; done
+timeout -k 10 200 python tools/bench_wgrad_segs.py > $D/segs.jsonl

@@ -1,6 +1,7 @@
 """Learner latent weight gradient: K = 5 unrolled uses of one 3x3 256->256 conv at 4x5, B = 512
 per use. Immediate (5 x mzba_conv_wgrad, per-tap kernel) vs deferred (one mzba_conv_wgrad_segs,
-whole-image kernel: form 1 = pixel rows, the default since round 6; form 0 = zero-bordered images). Also the
+whole-image kernel: form 1 = pixel rows (round 6); form 2 = pixel rows with 64-co wave tiles, the default;
+form 0 = zero-bordered images). Also the
 representation's 16x20 / 8x10 shapes as single segments. HIP-event median; FLOP = 2 M Cout Cin 9 over all
 segments."""
 import ctypes
@@ -25,9 +26,10 @@ for (nseg, B, H, W, Cin, Cout) in [(5, 512, 4, 5, 256, 256), (5, 512, 4, 5, 264,
     xp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in xs])
     dp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in dys])
     fl = 2.0 * nseg * B * H * W * Cout * Cin * 9
-    for mode in ("immediate", "segs_img_form0", "segs_img_form1"):
+    for mode in ("immediate", "segs_img_form0", "segs_img_form1", "segs_img_form2", "segs_img_form1b",
+                 "segs_img_form2b"):
         L.call("mzba_conv_wgrad_set_variant", 2 if mode.startswith("segs_img") else 1)
-        L.call("mzba_conv_wgrad_set_form", 0 if mode == "segs_img_form0" else 1)
+        L.call("mzba_conv_wgrad_set_form", int(mode[13]) if mode.startswith("segs_img") else 1)
         ts = []
         for it in range(10):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -48,4 +50,4 @@ for (nseg, B, H, W, Cin, Cout) in [(5, 512, 4, 5, 256, 256), (5, 512, 4, 5, 264,
         print(json.dumps({"shape": [nseg, B, H, W, Cin, Cout], "mode": mode, "us": round(us, 1),
                           "tflops": round(fl / us / 1e6, 1)}), flush=True)
 L.call("mzba_conv_wgrad_set_variant", 1)
-L.call("mzba_conv_wgrad_set_form", 1)
+L.call("mzba_conv_wgrad_set_form", 2)
