@@ -886,7 +886,8 @@ struct WgPx {
   const bf16_t* dys[WG_MAXSEG];
 };
 
-// WF (the waves' share of the 64 x 64 x 9 tile): 0 = 32 co x 32 ci x 5 / 4 taps per wave (2 A + 10 B fragment
+// WF (the waves' share of the 64 x 64 x 9 tile; 2 = WF 1 with its k steps software-pipelined): 0 = 32 co x
+// 32 ci x 5 / 4 taps per wave (2 A + 10 B fragment
 // reads per 20 MFMAs); 1 = 64 co x 32 ci x 3 / 2 taps per wave (taps {0,1,2}, {3,4}, {5,6}, {7,8}; 4 A + 6 / 4 B
 // reads per 24 / 16 MFMAs: 29 % fewer LDS fragment reads per stage). A SIMD holds waves w and w + 4, so each
 // SIMD runs one 3-tap and one 2-tap wave (40 MFMAs per k step, as WF 0) or two 2-tap waves. Every output
@@ -1008,36 +1009,96 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
     store_stage();
     __syncthreads();
     if (st + 1 < st1) load_stage(st + 1);
-    for (int ks = 0; ks < a.KS / 32; ++ks) {
-      const int r0 = ks * 32 + 4 * g + q, r1 = r0 + 16;
-      const uint32_t m0 = tmask[r0], m1 = tmask[r1];
-      bf16x8_t af[NI];
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-        const int c = wr * 32 + i * 16 + 4 * pp;
-        af[i] = tr_frag_at(ldy + (size_t)r0 * WI_LD + c, ldy + (size_t)r1 * WI_LD + c);
-      }
-      auto bload = [&](int t, bf16x8_t (&b)[2]) {
+    if constexpr (WF == 2) {
+      // the k steps software-pipelined: the last tap's MFMAs of step ks interleave the A fragments and the
+      // first tap's B fragments of step ks + 1 (each register refilled right after the last MFMA reading it),
+      // so a step no longer opens on a full LDS round trip. The same MFMAs in the same order per element.
+      const int nks = a.KS / 32;
+      int r0 = 4 * g + q, r1 = r0 + 16;
+      uint32_t m0 = tmask[r0], m1 = tmask[r1];
+      auto afrag = [&](int i, int s0, int s1) {
+        const int c = i * 16 + 4 * pp;
+        return tr_frag_at(ldy + (size_t)s0 * WI_LD + c, ldy + (size_t)s1 * WI_LD + c);
+      };
+      auto bload = [&](int t, int s0, int s1, uint32_t k0, uint32_t k1, bf16x8_t (&b)[2]) {
         const int off = (t / 3 - 1) * W + (t % 3 - 1);
-        const int x0 = (m0 >> t) & 1u ? r0 + off : a.XR, x1 = (m1 >> t) & 1u ? r1 + off : a.XR;
+        const int x0 = (k0 >> t) & 1u ? s0 + off : a.XR, x1 = (k1 >> t) & 1u ? s1 + off : a.XR;
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const int c = wc * 32 + j * 16 + 4 * pp;
           b[j] = tr_frag_at(lx + (size_t)x0 * WI_LD + c, lx + (size_t)x1 * WI_LD + c);
         }
       };
-      bf16x8_t bcur[2], bnxt[2];
-      bload(tap0, bcur);
+      bf16x8_t af[NI], bcur[2], bnxt[2];
 #pragma unroll
-      for (int tt = 0; tt < NT; ++tt) {
-        if (tt < ntap) {  // wave-uniform: the last tap group(s) have one tap fewer
-          if (tt + 1 < ntap) bload(tap0 + tt + 1, bnxt);
+      for (int i = 0; i < NI; ++i) af[i] = afrag(i, r0, r1);
+      bload(tap0, r0, r1, m0, m1, bcur);
+      for (int ks = 0; ks < nks; ++ks) {
+        // the last step re-reads its own rows (valid addresses, results unused): no branches in the loop
+        const int step = ks + 1 < nks ? 32 : 0;
+        const int n0 = r0 + step, n1 = r1 + step;
+        const uint32_t nm0 = tmask[n0], nm1 = tmask[n1];
 #pragma unroll
-          for (int i = 0; i < NI; ++i)
+        for (int tt = 0; tt < NT; ++tt) {
+          if (tt < ntap) {  // wave-uniform
+            if (tt + 1 < ntap) {
+              bload(tap0 + tt + 1, r0, r1, m0, m1, bnxt);
 #pragma unroll
-            for (int j = 0; j < 2; ++j)
-              acc[tt][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[tt][i][j], 0, 0, 0);
-          if (tt + 1 < ntap) { bcur[0] = bnxt[0]; bcur[1] = bnxt[1]; }
+              for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                  acc[tt][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[tt][i][j], 0, 0, 0);
+              bcur[0] = bnxt[0];
+              bcur[1] = bnxt[1];
+            } else {
+#pragma unroll
+              for (int i = 0; i < NI; ++i) {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                  acc[tt][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[tt][i][j], 0, 0, 0);
+                af[i] = afrag(i, n0, n1);
+              }
+              bload(tap0, n0, n1, nm0, nm1, bcur);
+            }
+          }
+        }
+        r0 = n0;
+        r1 = n1;
+        m0 = nm0;
+        m1 = nm1;
+      }
+    } else {
+      for (int ks = 0; ks < a.KS / 32; ++ks) {
+        const int r0 = ks * 32 + 4 * g + q, r1 = r0 + 16;
+        const uint32_t m0 = tmask[r0], m1 = tmask[r1];
+        bf16x8_t af[NI];
+  #pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int c = wr * 32 + i * 16 + 4 * pp;
+          af[i] = tr_frag_at(ldy + (size_t)r0 * WI_LD + c, ldy + (size_t)r1 * WI_LD + c);
+        }
+        auto bload = [&](int t, bf16x8_t (&b)[2]) {
+          const int off = (t / 3 - 1) * W + (t % 3 - 1);
+          const int x0 = (m0 >> t) & 1u ? r0 + off : a.XR, x1 = (m1 >> t) & 1u ? r1 + off : a.XR;
+  #pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int c = wc * 32 + j * 16 + 4 * pp;
+            b[j] = tr_frag_at(lx + (size_t)x0 * WI_LD + c, lx + (size_t)x1 * WI_LD + c);
+          }
+        };
+        bf16x8_t bcur[2], bnxt[2];
+        bload(tap0, bcur);
+  #pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+          if (tt < ntap) {  // wave-uniform: the last tap group(s) have one tap fewer
+            if (tt + 1 < ntap) bload(tap0 + tt + 1, bnxt);
+  #pragma unroll
+            for (int i = 0; i < NI; ++i)
+  #pragma unroll
+              for (int j = 0; j < 2; ++j)
+                acc[tt][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bcur[j], acc[tt][i][j], 0, 0, 0);
+            if (tt + 1 < ntap) { bcur[0] = bnxt[0]; bcur[1] = bnxt[1]; }
+          }
         }
       }
     }
@@ -1749,10 +1810,11 @@ int mzba_conv_wgrad_set_variant(int v) {
 }
 // which whole-image kernel: 2 (default) pixel rows with 64-co wave tiles (conv_wgrad_px_kernel<1>), 1 pixel
 // rows with 32-co wave tiles (conv_wgrad_px_kernel<0>, the same bits, 3-6 % slower per launch), 0 zero-bordered
-// images (conv_wgrad_img_kernel, the round-5 form); 1 and 0 for A/B
+// images (conv_wgrad_img_kernel, the round-5 form); 1 and 0 for A/B; 3 = form 2 with the k steps
+// software-pipelined (conv_wgrad_px_kernel<2>, the same bits)
 static thread_local int g_wgrad_form = 2;
 int mzba_conv_wgrad_set_form(int v) {
-  if (v < 0 || v > 2) return -1;
+  if (v < 0 || v > 3) return -1;
   g_wgrad_form = v;
   return 0;
 }
@@ -1796,6 +1858,9 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
       if (e == hipSuccess)
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_px_kernel<1>),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)WI_LDS_MAX);
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_wgrad_px_kernel<2>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)WI_LDS_MAX);
       if (e != hipSuccess) return (int)e;
       attr = true;
     }
@@ -1806,7 +1871,10 @@ static int wgrad_core(int dtype, const void* const* xs, const void* const* dys, 
     const size_t nwi = (size_t)Cout * 9 * Cin;
     float* ipart = (float*)ws;
     float* ibpart = db ? ipart + (size_t)pxp.nsplit * nwi : nullptr;
-    if (g_wgrad_form == 2)
+    if (g_wgrad_form == 3)
+      hipLaunchKernelGGL(conv_wgrad_px_kernel<2>, dim3(pxp.a.tiles, pxp.nsplit), dim3(WI_NT), pxp.lds, stream, pxp.a,
+                         ipart, ibpart);
+    else if (g_wgrad_form == 2)
       hipLaunchKernelGGL(conv_wgrad_px_kernel<1>, dim3(pxp.a.tiles, pxp.nsplit), dim3(WI_NT), pxp.lds, stream, pxp.a,
                          ipart, ibpart);
     else

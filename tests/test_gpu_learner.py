@@ -340,7 +340,7 @@ def test_learner_bf16_conv_packs(case, flip):
                                   ("bf16", 1, 3, 7, 4, 5, 64, 64), ("f32", 1, 2, 6, 4, 5, 40, 24),
                                   ("bf16", 2, 8, 16, 8, 10, 128, 128), ("bf16", 2, 3, 24, 3, 7, 64, 72),
                                   ("bf16", 2, 2, 4, 16, 20, 128, 256)])
-@pytest.mark.parametrize("form", [2, 1, 0])
+@pytest.mark.parametrize("form", [2, 3, 1, 0])
 def test_conv_wgrad_segs_matches_torch(case, form):
     """mzba_conv_wgrad_segs (the learner's deferred latent weight gradient: K (x, dY) pairs in
     one contraction) against the torch fp32 weight gradient of the concatenated segments.
@@ -385,7 +385,8 @@ def test_conv_wgrad_segs_matches_torch(case, form):
                                   (1, 512, 8, 10, 256, 256), (1, 512, 16, 20, 128, 128), (2, 24, 3, 7, 64, 72)])
 def test_conv_wgrad_px_wave_tile_forms_bit_identical(case):
     """The pixel-row weight gradient's two wave decompositions (form 1: 32 co x 32 ci x 5 / 4 taps per wave;
-    form 2: 64 co x 32 ci x 3 / 2 taps per wave) give the same bits: every output element is the same chain of
+    form 2: 64 co x 32 ci x 3 / 2 taps per wave; form 3: form 2 with its k steps software-pipelined) give the
+    same bits: every output element is the same chain of
     the same MFMAs over the same fragments (the learner's shapes, the representation's, a ragged one)."""
     from mzba import _lib as L
     nseg, B, H, W, Cin, Cout = case
@@ -402,7 +403,7 @@ def test_conv_wgrad_px_wave_tile_forms_bit_identical(case):
     outs = []
     L.call("mzba_conv_wgrad_set_variant", 2)
     try:
-        for form in (1, 2):
+        for form in (1, 2, 3):
             L.call("mzba_conv_wgrad_set_form", form)
             dw, db = dw0.clone(), db0.clone()
             L.call("mzba_conv_wgrad_segs", 1, xp, dp, nseg, B, H, W, Cin, Cout, 3, L.ptr(dw), L.ptr(db), L.ptr(ws),
@@ -412,8 +413,9 @@ def test_conv_wgrad_px_wave_tile_forms_bit_identical(case):
     finally:
         L.call("mzba_conv_wgrad_set_variant", 1)
         L.call("mzba_conv_wgrad_set_form", 2)
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1], outs[1][1])
+    for dw, db in outs[1:]:
+        assert torch.equal(outs[0][0], dw)
+        assert torch.equal(outs[0][1], db)
     assert not torch.equal(outs[0][0], dw0)
 
 

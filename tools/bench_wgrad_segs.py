@@ -26,8 +26,8 @@ for (nseg, B, H, W, Cin, Cout) in [(5, 512, 4, 5, 256, 256), (5, 512, 4, 5, 264,
     xp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in xs])
     dp = (ctypes.c_void_p * nseg)(*[t.data_ptr() for t in dys])
     fl = 2.0 * nseg * B * H * W * Cout * Cin * 9
-    for mode in ("immediate", "segs_img_form0", "segs_img_form1", "segs_img_form2", "segs_img_form1b",
-                 "segs_img_form2b"):
+    for mode in ("immediate", "segs_img_form0", "segs_img_form1", "segs_img_form2", "segs_img_form3",
+                 "segs_img_form2b", "segs_img_form3b"):
         L.call("mzba_conv_wgrad_set_variant", 2 if mode.startswith("segs_img") else 1)
         L.call("mzba_conv_wgrad_set_form", int(mode[13]) if mode.startswith("segs_img") else 1)
         ts = []
