@@ -532,8 +532,9 @@ long long mzba_conv_wgrad_ws_bytes(int B, int H, int W, int Cin, int Cout, int k
 int mzba_conv_wgrad_set_variant(int v);
 /* the whole-image kernel's form (per host thread): 2 (default) pixel rows with 64-co wave tiles — k over the
  * real pixels of a stage, out-of-image taps read a zero row (round 6); 1 the same with 32-co wave tiles
- * (bit-identical to 2, more LDS fragment reads); 0 zero-bordered images (round 5, A/B; the same sums in a
- * different f32 order); -1 for another value. */
+ * (bit-identical to 2, more LDS fragment reads); 3 form 2 with software-pipelined k steps (bit-identical,
+ * measured slower, A/B); 0 zero-bordered images (round 5, A/B; the same sums in a different f32 order); -1 for
+ * another value. */
 int mzba_conv_wgrad_set_form(int v);
 int mzba_conv_wgrad(int dtype, const void* x, const void* dy, int B, int H, int W, int Cin, int Cout, int ks,
                     float* dw, float* db, void* ws, long long ws_bytes, hipStream_t stream);
