@@ -1008,7 +1008,10 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
     __syncthreads();  // previous stage fully consumed (first pass: the zero row and mask table written)
     store_stage();
     __syncthreads();
-    if (st + 1 < st1) load_stage(st + 1);
+#ifndef MZBA_WGRAD_ABLATE
+#define MZBA_WGRAD_ABLATE 0  // diagnostic builds only (numerically wrong): 1 no next-stage loads, 3 no B-tap reloads
+#endif
+    if (MZBA_WGRAD_ABLATE != 1 && st + 1 < st1) load_stage(st + 1);
     if constexpr (WF == 2) {
       // the k steps software-pipelined: the last tap's MFMAs of step ks interleave the A fragments and the
       // first tap's B fragments of step ks + 1 (each register refilled right after the last MFMA reading it),
@@ -1091,7 +1094,10 @@ __global__ __launch_bounds__(WI_NT) void conv_wgrad_px_kernel(WgPx a, float* __r
   #pragma unroll
         for (int tt = 0; tt < NT; ++tt) {
           if (tt < ntap) {  // wave-uniform: the last tap group(s) have one tap fewer
-            if (tt + 1 < ntap) bload(tap0 + tt + 1, bnxt);
+            if (tt + 1 < ntap) {
+            if (MZBA_WGRAD_ABLATE == 3) { bnxt[0] = bcur[0]; bnxt[1] = bcur[1]; }
+            else bload(tap0 + tt + 1, bnxt);
+          }
   #pragma unroll
             for (int i = 0; i < NI; ++i)
   #pragma unroll
